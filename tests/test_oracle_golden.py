@@ -1,0 +1,133 @@
+"""Pin the CPU oracle before trusting it.
+
+1. Against the reference outputs the survey recorded (tests/golden/reference_survey.json,
+   SURVEY.md sec. 8(c)): converged vectors must agree bit for bit.
+2. Against known answers held by the reference's own files: ExampleObjectives.hpp builds
+   ExpCurve / Cubic data from exact parameters (10.2, 0.4, 0.1) and (0.3, 1.1, -4.3, 7.3);
+   Rosenbrock's minimum is (1, ..., 1); PowerObject(3)'s gradient at 3 is 27
+   (testGradientEvaluation, Examples.cpp:512-540).
+3. Structural properties the reference states in code: the zero-padded Allreduce makes the
+   sharded FD bitwise equal to the serial one (PNOL_Objective.cpp:147-148, 279-288) for any
+   rank count; BFGS_MPI depends on the rank count through Npool (BFGS_with_linesearch_MPI.cpp:235)
+   and reports f = 0 when the pool search ends in its first phase (A10 defect).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_survey.json")))
+
+
+def test_bfgs_rosenbrock2_bitwise(oracle):
+    for key in ("bfgs_rosenbrock2_m12_1", "bfgs_rosenbrock2_3_3"):
+        g = GOLD[key]
+        o = oracle.rosenbrock(2)
+        X, res, _ = oracle.bfgs_findmin(o, g["x0"], g["params"])
+        assert X.tolist() == g["X"], key
+        assert res.fopt == g["f"]
+        assert o.evals == g["evals"]
+
+
+def test_testBFGS_rosenbrock5(oracle):
+    g = GOLD["testBFGS_rosenbrock5"]
+    o = oracle.rosenbrock(5)
+    X, res, _ = oracle.bfgs_findmin(o, g["x0"], g["params"])
+    assert res.fopt == g["f"]
+    assert abs(X[0] - g["x0_approx"]) < 1e-3
+
+
+@pytest.mark.parametrize("key,factory", [("testLMExp", "expcurve"), ("testLMCubicLinearCoef", "cubic")])
+def test_lm_examples_bitwise(oracle, key, factory):
+    g = GOLD[key]
+    o = getattr(oracle, factory)()
+    X, res, F0, FOpt, _ = oracle.lm_findmin(o, g["x0"], g["params"])
+    assert X.tolist() == g["X"]
+
+
+def test_lm_known_answers(oracle):
+    X, *_ = oracle.lm_findmin(oracle.expcurve(), [0.1] * 3, (0.001, 10, 1e-6, 100, 1e-6, 1))
+    np.testing.assert_allclose(X, [10.2, 0.4, 0.1], rtol=1e-9)
+    X, *_ = oracle.lm_findmin(oracle.cubic(), [0.1] * 4, (0.001, 10, 1e-6, 10, 1e-5, 1))
+    np.testing.assert_allclose(X, [0.3, 1.1, -4.3, 7.3], rtol=1e-12)
+
+
+def test_fd_gradient_power3_known_answer(oracle):
+    # testGradientEvaluation, Examples.cpp:512-540: PowerObject(3), X = 3, dX = 1e-6
+    o = oracle.power(5, 3)
+    g = oracle.fd_gradient(o, [3.0] * 5, [1e-6] * 5)
+    np.testing.assert_allclose(g, 27.0, rtol=1e-5)
+    assert o.evals == 6
+
+
+@pytest.mark.parametrize("nprocs", [1, 2, 3, 4, 8])
+def test_sharded_fd_bitwise_equal_serial(oracle, nprocs):
+    x = np.linspace(-0.5, 0.7, 7)
+    o = oracle.rosenbrock(7)
+    g1 = oracle.fd_gradient(o, x, [1e-6] * 7)
+    gP = oracle.fd_gradient_sharded(o, x, [1e-6] * 7, nprocs)
+    assert np.array_equal(g1, gP)
+    oc = oracle.cubic()
+    J1 = oracle.fd_jacobian(oc, [0.1] * 4, [1e-6] * 4)
+    JP = oracle.fd_jacobian_sharded(oc, [0.1] * 4, [1e-6] * 4, nprocs)
+    assert np.array_equal(J1, JP)
+
+
+def test_recur_gradient_matches_full(oracle):
+    # testGradientApproxMultMPIRecur, Examples.cpp:593-663: freezing x3 leaves the other entries
+    n = 8
+    X = np.arange(n) * 0.1
+    o = oracle.rosenbrock(n)
+    g = oracle.fd_gradient(o, X, [1e-6] * n)
+    cx = np.zeros(n); ci = np.zeros(n, dtype=np.uint8)
+    g0 = oracle.fd_gradient_recur(o, X, [1e-6] * n, cx, ci)
+    assert np.array_equal(g, g0)
+    cx[3] = X[3]; ci[3] = 1
+    xr = np.delete(X, 3)
+    gr = oracle.fd_gradient_recur(o, xr, [1e-6] * (n - 1), cx, ci)
+    assert np.array_equal(gr, np.delete(g, 3))
+
+
+def test_rank2_update_equals_reference_form(oracle):
+    rng = np.random.default_rng(7)
+    for n in (8, 64):
+        D = np.eye(n) + 0.1 * rng.standard_normal((n, n))
+        y = rng.standard_normal(n); s = rng.standard_normal(n)
+        ref = oracle.update_hessian_inv(D, y, s)
+        r2 = oracle.update_hessian_inv_rank2(D, y, s)
+        np.testing.assert_allclose(r2, ref, rtol=0, atol=1e-11 * np.abs(ref).max())
+
+
+def test_bfgs_mpi_depends_on_pool_and_a10_defect(oracle):
+    P = (1e-4, 0.1, 4, 1, 1000, 1e-7, 1e-3, 200, 1e-5, 1e-5, 0, 1)  # testBFGS_MPI, Examples.cpp:163-189
+    outs = {}
+    for nprocs in (2, 4, 8):
+        X, res = oracle.bfgs_mpi_findmin(oracle.rosenbrock(10), [10.0] * 10, P, nprocs)
+        outs[nprocs] = (X, res.fopt)
+    assert outs[8][1] == 0.0          # survey probe: "reports f=0 at np=8"
+    assert not np.array_equal(outs[2][0], outs[4][0])
+
+
+def test_compute_alpha_bnd_edge_cases(oracle):
+    # BFGS_with_bnd_linsearch_MPI.cpp:665-708
+    x = np.array([0.0, 0.5, 1.0]); lb = np.zeros(3); ub = np.ones(3)
+    assert oracle.compute_alpha_bnd(x, lb, ub, np.array([1.0, 1.0, -1.0])) == 0.5
+    # a coordinate on its UPPER bound with p = 0: (ub-x)/0 is NaN, (lb-x)/0 is -inf, alpha = 0
+    assert oracle.compute_alpha_bnd(x, lb, ub, np.array([1.0, 1.0, 0.0])) == 0.0
+    # ... on its lower bound with p = 0: (ub-x)/0 = +inf, so that coordinate never binds
+    assert oracle.compute_alpha_bnd(x, lb, ub, np.array([0.0, 1.0, -1.0])) == 0.5
+
+
+def test_bfgs_bnd_examples(oracle):
+    # testBFGSBnd, Examples.cpp:49-83 (box [-5,5]^5 is inactive: same local minimum as testBFGS)
+    Pb = (1e-4, 0.8, 1e-6, 1, 1e-10, 2, 50, 1e-5, 1e-6, 1e-3, 200, 1e-5, 1e-5, 0, 1)
+    X, res = oracle.bfgs_bnd_findmin(oracle.rosenbrock(5), [2.0] * 5, [-5.0] * 5, [5.0] * 5, Pb)
+    assert abs(res.fopt - 3.9308394) < 1e-5
+    # active lower bound on x0 (testBFGSBndMPISW geometry): converges to the interior optimum
+    X, res = oracle.bfgs_bnd_findmin(oracle.rosenbrock(3), [-1.0, 2.0, 2.0], [-1.0] * 3, [5.0] * 3, Pb)
+    np.testing.assert_allclose(X, 1.0, atol=1e-3)
+    # optimum outside the box: the bound must hold at the solution
+    X, res = oracle.bfgs_bnd_findmin(oracle.rosenbrock(3), [0.0, 0.0, 0.0], [-2.0] * 3, [0.5] * 3, Pb)
+    assert np.all(X <= 0.5 + 1e-12) and np.all(X >= -2.0)
+    assert X[0] > 0.49
