@@ -1,0 +1,255 @@
+"""bench.py -- MI355X PNOL hot path: LM iterations/s at m=16384, n=2048 (+ BFGS H.g GB/s).
+
+A "step" is one LevenbergMarquardt loop trip of the C++ drop-in (LevMarq at N=1, LevMarqMPI
+at N>1, one process per GPU, FD columns sharded with an RCCL allgather): the batched
+finite-difference Jacobian of the synthetic dense residual r(x) = A x - y (SURVEY 8(d)
+cfg 3/4, splitmix64 seed 0x5EED2018, data generated in HBM), J^T J on fp64 MFMA with the
+Marquardt diagonal, -J^T F, the damped Cholesky solve, F(x + sigma) and the accept/reject
+test.  Every trip does the full work (no Jacobian reuse across rejected steps).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  Per-kernel durations come from HIP events recorded on the
+solver's own stream during the timed steps (pnol_ctx_timer); `cpu_baseline` times the
+oracle (oracle/, the CPU restatement of the reference) on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+M_RES, N_PAR = 16384, 2048          # BASELINE.json metric: LM at m=16384, n=2048
+HG_N = 8192                         # north-star H.g size (>= 60% of HBM roofline target)
+HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6             # fp64 matrix == fp64 vector peak on MI355X
+
+
+def _args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-hg", action="store_true")
+    ap.add_argument("--m", type=int, default=M_RES)
+    ap.add_argument("--n", type=int, default=N_PAR)
+    return ap.parse_args()
+
+
+def _timer(L, ctx_h, name):
+    ms, cnt = C.c_double(), C.c_int()
+    L.check(L.lib().pnol_ctx_timer(ctx_h, name.encode(), C.byref(ms), C.byref(cnt)), "pnol_ctx_timer")
+    return ms.value, cnt.value
+
+
+def bench_hg(ctx, n, reps=20):
+    """Standalone p = -D g at n (8 n^2 + 16 n bytes per launch) and the fused BFGS pass
+    (16 n^2 bytes with write-back), timed with HIP events on the context stream."""
+    import torch
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    g = torch.randn(n, dtype=torch.float64, device="cuda")
+    D = torch.randn(n, n, dtype=torch.float64, device="cuda")
+    flush = torch.empty(512 * 1024 * 1024 // 8, dtype=torch.float64, device="cuda")   # > 256 MiB MALL
+    L.check(L.lib().pnol_ctx_enable_timers(ctx.h, 1), "timers")
+    L.check(L.lib().pnol_ctx_reset_timers(ctx.h), "reset")
+    for _ in range(3):
+        ctx.hg(D, g)
+    ctx.synchronize()
+    L.check(L.lib().pnol_ctx_reset_timers(ctx.h), "reset")
+    for _ in range(reps):
+        flush.fill_(1.0)      # cold Infinity Cache before every launch
+        ctx.hg(D, g)
+    ctx.synchronize()
+    ms, cnt = _timer(L, ctx.h, "hg")
+    t_hg = ms / cnt * 1e-3
+    hg_bytes = 8.0 * n * n + 16.0 * n
+    # fused pass with write-back and a pending correction (the fast-mode BFGS iteration)
+    y = torch.randn(n, dtype=torch.float64, device="cuda")
+    s, a, b = (torch.randn(n, dtype=torch.float64, device="cuda") * 1e-3 for _ in range(3))
+    ctx.bfgs_pass(D, y, g, (s, a, b), True)
+    ctx.synchronize()
+    L.check(L.lib().pnol_ctx_reset_timers(ctx.h), "reset")
+    for _ in range(reps):
+        flush.fill_(1.0)
+        ctx.bfgs_pass(D, y, g, (s, a, b), True)
+    ctx.synchronize()
+    ms2, cnt2 = _timer(L, ctx.h, "bfgs_pass")
+    t_pass = ms2 / cnt2 * 1e-3
+    del D, flush
+    torch.cuda.empty_cache()
+    return {
+        "n": n, "hg_us": t_hg * 1e6, "hg_GBps": hg_bytes / t_hg / 1e9,
+        "hg_frac_of_hbm": hg_bytes / t_hg / 1e9 / HBM_PEAK_GBS,
+        "fused_pass_us": t_pass * 1e6, "fused_pass_GBps": 16.0 * n * n / t_pass / 1e9,
+        "fused_pass_frac_of_hbm": 16.0 * n * n / t_pass / 1e9 / HBM_PEAK_GBS,
+        "cold_cache": True,
+    }
+
+
+def cpu_baseline(m, n, budget_s=20.0):
+    """Oracle (CPU restatement of the reference, 1 thread) on a bounded sample of one LM loop
+    trip at (m, n): FD residual evaluations (the n+1 columns), rows of J^T J (the reference's
+    matrixMultiply), the reference LU once; extrapolated to one full trip."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.build()
+    A, xs, y = O.linres_data(m, n)
+    o = O.Obj(O.LINRES, n, m, A, y)
+    x = np.zeros(n)
+    t0 = time.perf_counter(); k_eval = 0
+    while k_eval < 4 or (time.perf_counter() - t0 < budget_s * 0.3 and k_eval < 64):
+        O.obj_eval_multi(o, x); k_eval += 1
+    t_eval = (time.perf_counter() - t0) / k_eval
+    J = np.ascontiguousarray(A)                    # any m x n data: cost is data-independent
+    JT = np.ascontiguousarray(J.T)
+    t0 = time.perf_counter(); k_rows = 0
+    while k_rows < 2 or (time.perf_counter() - t0 < budget_s * 0.3 and k_rows < 64):
+        O.matmul(JT[k_rows:k_rows + 1], J); k_rows += 1
+    t_row = (time.perf_counter() - t0) / k_rows
+    nl = min(n, 1024)
+    Al = JT[:nl, :nl] @ JT[:nl, :nl].T + np.eye(nl)
+    t0 = time.perf_counter(); O.lusolve(Al, np.ones(nl)); t_lu = (time.perf_counter() - t0) * (n / nl) ** 3
+    t_iter = t_eval * (n + 2) + t_row * n + t_lu
+    return {
+        "value": 1.0 / t_iter, "unit": "LM iters/sec", "cores": 1, "kind": "port",
+        "sample": (f"oracle (C restatement, gcc -O2, 1 thread) at m={m}, n={n}: {k_eval} residual evals "
+                   f"({t_eval*1e3:.1f} ms each, x{n + 2} per trip), {k_rows} rows of J^T J "
+                   f"({t_row*1e3:.1f} ms each, x{n}), LU at n={nl} scaled by (n/{nl})^3 "
+                   f"({t_lu:.1f} s); extrapolated {t_iter:.1f} s per LM trip"),
+        "seconds_per_trip": t_iter,
+    }
+
+
+def main():
+    args = _args()
+    import torch
+    import torch.distributed as dist
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective
+    from parallelnonlinearoptimizationlibrary_amd.dist import env_rank_world, init_rccl
+
+    rank, world, local = env_rank_world()
+    torch.cuda.set_device(local)
+    os.environ["PNOL_DEVICE"] = str(local)
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+
+    m, n = args.m, args.n
+    ctx = Context(local)
+    # the C++ drop-in classes run on the process default context: bind its timers
+    dctx = C.c_void_p()
+    L.check(L.lib().pnol_default_ctx(C.byref(dctx)), "pnol_default_ctx")
+    if world > 1:
+        class _Ctx:  # RCCL communicator on the solver's context
+            h = dctx
+        init_rccl(_Ctx, rank, world)
+
+    obj = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)   # A, y generated in HBM
+    x0 = np.zeros(n)
+    which = 1 if world > 1 else 0
+
+    def run(iters):
+        X = x0.copy()
+        p = np.array([0.001, 10.0, 1e-7, float(iters), 0.0, -1.0])  # xMinDiff 0: every trip runs
+        F0, FO = np.zeros(m), np.zeros(m)
+        res = L.Result()
+        dp = C.POINTER(C.c_double)
+        L.check(L.lib().pnol_run_levmarq(which, obj.h, 0, p.ctypes.data_as(dp), X.ctypes.data_as(dp), n,
+                                         F0.ctypes.data_as(dp), FO.ctypes.data_as(dp), m, C.byref(res)),
+                "pnol_run_levmarq")
+        return X
+
+    run(args.warmup)
+    torch.cuda.synchronize()
+    L.check(L.lib().pnol_ctx_enable_timers(dctx, 1), "timers")
+    L.check(L.lib().pnol_ctx_reset_timers(dctx), "timers")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    X = run(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    timers = {k: _timer(L, dctx, k) for k in ("fd_jacobian", "linres_eval", "syrk", "syrk_reduce", "jtr", "solve",
+                                              "allgather")}
+    L.check(L.lib().pnol_ctx_enable_timers(dctx, 0), "timers")
+    err = float(np.max(np.abs(X - obj.xstar)) / np.max(np.abs(obj.xstar)))
+
+    hg = None
+    if rank == 0 and not args.no_hg:
+        hg = bench_hg(ctx, HG_N)
+        hg4096 = bench_hg(ctx, 4096)
+    if rank == 0:
+        per = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timers.items()}
+        syrk_ms = per["syrk"]
+        jtj_flop = float(m) * n * (n + 1)                   # unique entries of the symmetric result
+        my_cols = -(-n // world)
+        fd_flop = 2.0 * m * n * my_cols                      # this rank's batched FD GEMM
+        roofline = {
+            "kernel": "k_syrk_tile (J^T J, fp64 MFMA v_mfma_f64_16x16x4_f64)",
+            "bound": "mfma", "achieved": jtj_flop / (syrk_ms * 1e-3) / 1e12 if syrk_ms else None,
+            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "traffic": None,
+        }
+        roofline["frac"] = roofline["achieved"] / FP64_PEAK_TFLOPS if roofline["achieved"] else None
+        fd_ms = per["fd_jacobian"]
+        rooflines = {
+            "fd_jacobian": {"kernel": "k_linres_fd (batched FD GEMM, fp64 VALU fma)", "bound": "valu_fp64",
+                            "ms": fd_ms, "achieved": fd_flop / (fd_ms * 1e-3) / 1e12 if fd_ms else None,
+                            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s"},
+            "jtj": dict(roofline, ms=syrk_ms),
+        }
+        if hg:
+            rooflines["hg"] = {"kernel": "k_gemv_neg<4> (p = -D g)", "bound": "hbm", "achieved": hg["hg_GBps"],
+                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hg["hg_frac_of_hbm"],
+                               "traffic": None, "n": HG_N}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(m, n)
+        ms_per_step = elapsed / args.steps * 1e3
+        line = {
+            "metric": f"LM iters/sec at m={m},n={n}",
+            "value": args.steps / elapsed,
+            "unit": "iters/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (splitmix64 seed 0x5EED2018, r(x)=Ax-y generated in HBM)",
+            "config": {"workload": f"LevenbergMarquardt{'MPI' if world > 1 else ''} m={m} n={n}, "
+                                   f"FD columns {'sharded over ' + str(world) + ' GPUs + RCCL allgather' if world > 1 else 'on 1 GPU'}",
+                       "m": m, "n": n, "parallelism": f"fd-columns x{world}" if world > 1 else "single"},
+            "roofline": roofline,
+            "rooflines": rooflines,
+            "kernel_ms_per_step": per,
+            "converged_rel_err_vs_xstar": err,
+            "bfgs_hg": hg, "bfgs_hg_n4096": hg4096 if hg else None,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

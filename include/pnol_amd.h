@@ -1,0 +1,170 @@
+/*
+ * pnol_amd.h -- C ABI of the MI355X-native PNOL hot path (libpnol_amd.so).
+ *
+ * Plain pointers, sizes and int status codes; no exceptions and no torch/HIP types cross
+ * this boundary.  Functions suffixed _d take DEVICE pointers (allocated with pnol_malloc or
+ * any hipMalloc'd / torch CUDA buffer on the context's device) and enqueue on the context's
+ * stream; call pnol_ctx_synchronize before reading results on the host.  Functions without
+ * the suffix take HOST pointers and return after the result is on the host.
+ *
+ * Each entry point names the reference code it replaces (paths relative to
+ * briandaniel/ParallelNonlinearOptimizationLibrary/Source).  The C++ drop-in classes in
+ * include/ headers (BFGS, BFGS_MPI, BFGS_Bnd, LevMarq, LevMarqMPI) are built on these.
+ */
+#ifndef PNOL_AMD_H_
+#define PNOL_AMD_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PNOL_AMD_VERSION 100 /* 1.0.0 */
+
+enum pnol_status {
+    PNOL_OK = 0,
+    PNOL_ERR_ARG = 1,        /* bad argument (null pointer, n <= 0, ld < n, misaligned) */
+    PNOL_ERR_HIP = 2,        /* a HIP runtime call failed */
+    PNOL_ERR_NOMEM = 3,
+    PNOL_ERR_NODEVICE = 4,   /* no MI355X (gfx950) visible: the product path has no CPU fallback */
+    PNOL_ERR_SINGULAR = 5,   /* zero pivot in the damped solve */
+    PNOL_ERR_COMM = 6,       /* collective failed / communicator not initialised */
+    PNOL_ERR_UNSUPPORTED = 7
+};
+
+typedef struct pnol_ctx pnol_ctx;   /* one GPU: device, stream, workspace, communicator */
+typedef struct pnol_dobj pnol_dobj; /* device-resident objective (batched FD evaluation) */
+
+const char* pnol_status_string(int status);
+int pnol_version(void);
+int pnol_device_count(int* count);              /* gfx950 devices visible to this process */
+
+/* ---- context ---------------------------------------------------------------------- */
+int pnol_ctx_create(int device, pnol_ctx** out);
+int pnol_ctx_destroy(pnol_ctx* ctx);
+int pnol_ctx_synchronize(pnol_ctx* ctx);
+int pnol_ctx_get_stream(pnol_ctx* ctx, void** hip_stream);  /* hipStream_t, for interop timing */
+int pnol_ctx_set_stream(pnol_ctx* ctx, void* hip_stream);   /* run on a caller-owned stream (NULL: own) */
+int pnol_ctx_device(pnol_ctx* ctx, int* device);
+/* process default context used by the C++ drop-in classes (device = LOCAL_RANK or 0) */
+int pnol_default_ctx(pnol_ctx** out);
+
+/* Per-kernel HIP-event timers on the context's stream (off by default).  Names: "fd_jacobian",
+ * "fd_gradient", "linres_eval", "syrk", "syrk_reduce", "jtr", "solve", "hg", "bfgs_pass",
+ * "allgather".  total_ms sums the recorded launches since the last reset. */
+int pnol_ctx_enable_timers(pnol_ctx* ctx, int on);
+int pnol_ctx_reset_timers(pnol_ctx* ctx);
+int pnol_ctx_timer(pnol_ctx* ctx, const char* name, double* total_ms, int* count);
+
+int pnol_malloc(pnol_ctx* ctx, size_t bytes, void** dptr);
+int pnol_free(pnol_ctx* ctx, void* dptr);
+int pnol_memcpy_h2d(pnol_ctx* ctx, void* dst, const void* src, size_t bytes);  /* synchronous */
+int pnol_memcpy_d2h(pnol_ctx* ctx, void* dst, const void* src, size_t bytes);  /* synchronous */
+
+/* ---- BFGS dense inverse Hessian ------------------------------------------------------ */
+/* p = -D g.  Replaces matrixVectorMultiply(D, dFdX, p) + negate, BFGS_with_linesearch.cpp:78-79
+ * (also BFGS_with_linesearch_MPI.cpp:81-82, BFGS_bnd_linesearch.cpp:142-143).
+ * D is n x n row-major with leading dimension ldd (doubles, even, 16-byte aligned base).
+ * n <= PNOL_SEQ_MAX uses reference summation order (bitwise equal to the CPU path). */
+#define PNOL_SEQ_MAX 64
+int pnol_hg_d(pnol_ctx* ctx, const double* D, int ldd, const double* g, double* p, int n);
+/* y = -A x for a rows x cols row-major A (the same streaming kernel; also rhs = -J^T F). */
+int pnol_gemv_neg_d(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y);
+
+/* D <- (I - rho s y^T) D (I - rho y s^T) + rho s s^T, rho = 1/(y.s), in the reference's
+ * O(n^3) operation order (updateHessianInv, BFGS_with_linesearch.cpp:389-432).  Bitwise
+ * equal to the CPU path; intended for n <= a few hundred. */
+int pnol_bfgs_update_exact_d(pnol_ctx* ctx, double* D, int ldd, const double* y, const double* s, int n);
+
+/* One streaming pass over D (16 n^2 bytes when write-back is on, 8 n^2 otherwise):
+ *   Dc = D + s_p a_p^T + b_p s_p^T   (pending rank-2 correction; s_p == NULL: none)
+ *   if (write_back) D = Dc
+ *   u = Dc y, w = Dc^T y, v = Dc g     (any of y/g may be NULL to skip; outputs n doubles)
+ * The O(n^2) form of updateHessianInv plus the next H.g: see DESIGN.md "fused BFGS pass". */
+int pnol_bfgs_pass_d(pnol_ctx* ctx, double* D, int ldd, int n,
+                     const double* s_p, const double* a_p, const double* b_p, int write_back,
+                     const double* y, const double* g, double* u, double* w, double* v);
+/* D = I (BFGS_with_linesearch.cpp:46-56), or diag(scale) when scale != NULL (BFGS_bnd_linesearch.cpp:65-83) */
+int pnol_set_identity_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale);
+
+/* ---- Levenberg-Marquardt -------------------------------------------------------------- */
+/* A = JT JT^T (= J^T J) with A_ii = (1 + lambda) * (J^T J)_ii  (Marquardt scaling).
+ * Replaces matrixTranspose + matrixMultiply(JT, J, JTJ) + the diag loop,
+ * LevenbergMarquardt.cpp:59-73.  JT is n x m row-major (ld ldjt): column j of J is row j.
+ * fp64 MFMA (v_mfma_f64_16x16x4_f64) SYRK on the lower triangle, mirrored; n <= PNOL_SEQ_MAX
+ * and m <= 4096 use the reference summation order.  jtj_diag (nullable) receives (J^T J)_ii. */
+int pnol_jtj_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda,
+               double* A, int lda, double* jtj_diag);
+/* rhs = -(J^T F), LevenbergMarquardt.cpp:78-80 */
+int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
+/* sigma = A^{-1} rhs, replacing luSolve(A, rhs, sigma), LevenbergMarquardt.cpp:83.
+ * method 0 = auto (n <= PNOL_SEQ_MAX: reference LU; else blocked Cholesky, LU on a non-positive
+ * pivot), 1 = Cholesky, 2 = LU with partial pivoting (reference operation order).
+ * A is consumed (overwritten by its factor).  info (host, nullable) gets the method used
+ * (1 or 2) or -1 on a singular matrix. */
+int pnol_solve_d(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n,
+                 int method, int* info);
+
+/* ---- device objectives and the batched finite-difference engine ---------------------- */
+enum pnol_dobj_kind {
+    PNOL_OBJ_ROSENBROCK = 0,  /* RosenbrockObject, ExampleObjectives.hpp:79-111 */
+    PNOL_OBJ_POWER = 1,       /* PowerObject, :206-234 (power argument) */
+    PNOL_OBJ_QUADRATIC = 4,   /* synthetic convex quadratic, p0 = d[n], p1 = b[n] (SURVEY 8(d) cfg 2/5) */
+    PNOL_OBJ_EXPCURVE = 10,   /* ExpCurveObjective, :113-154; p0 = xData[m], p1 = yData[m] */
+    PNOL_OBJ_CUBIC = 11,      /* CubicObjective, :160-201; p0 = xData[m], p1 = yData[m] */
+    PNOL_OBJ_LINRES = 12      /* r = A x - y, p0 = A[m*n] row-major, p1 = y[m] (SURVEY 8(d) cfg 3/4) */
+};
+/* host_p0/host_p1 are copied to the device (NULL + len 0 when unused). */
+int pnol_dobj_create(pnol_ctx* ctx, int kind, int n, int m, const double* host_p0, size_t len0,
+                     const double* host_p1, size_t len1, double power, pnol_dobj** out);
+/* Generate the synthetic data on the device from the splitmix64 stream (seed);
+ * kind PNOL_OBJ_QUADRATIC (bscale scales b) or PNOL_OBJ_LINRES (xstar_out, host, nullable). */
+int pnol_dobj_create_synthetic(pnol_ctx* ctx, int kind, int n, int m, unsigned long long seed,
+                               double bscale, double* xstar_out, pnol_dobj** out);
+int pnol_dobj_destroy(pnol_dobj* obj);
+int pnol_dobj_info(pnol_dobj* obj, int* kind, int* n, int* m);
+/* f = objEval(x) (scalar kinds, out[0]) or F = objEval(x) (residual kinds, out[0..m)) */
+int pnol_dobj_eval_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, double* out);
+/* Forward differences, Objective::gradientApproximation (PNOL_Objective.cpp:12-34):
+ * f0 = f(x); g_i = (f(x + h_i e_i) - f0) / h_i for i in [i0, i0 + cnt).  g gets cnt values. */
+int pnol_fd_gradient_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, int i0, int cnt,
+                       double* f0, double* g);
+/* MultiObjective::gradientApproximation (PNOL_Objective.cpp:165-197) for columns [j0, j0+cnt):
+ * F0 = F(x) (computed here when compute_f0, else read), JT row (j - j0) = (F(x + h_j e_j) - F0)/h_j. */
+int pnol_fd_jacobian_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, int j0, int cnt,
+                       double* F0, int compute_f0, double* JT, int ldjt);
+
+/* ---- communicator (replaces MPI_COMM_WORLD on the FD / pool paths) ------------------- */
+/* RCCL over xGMI: one process per GPU.  Exchange the 128-byte id out of band (rank 0 creates). */
+int pnol_comm_unique_id(char id[128]);
+int pnol_comm_init_rccl(pnol_ctx* ctx, int nranks, int rank, const char id[128]);
+/* Host backend (tests / host objectives): the caller supplies the allgather. */
+typedef int (*pnol_host_allgather_fn)(const void* send, void* recv, size_t bytes_per_rank, void* user);
+int pnol_comm_init_host(int nranks, int rank, pnol_host_allgather_fn fn, void* user);
+int pnol_comm_finalize(void);
+int pnol_comm_size(int* nranks, int* rank);
+/* recv[r * count + i] = send_r[i]  (device buffers on the RCCL backend) */
+int pnol_comm_allgather_d(pnol_ctx* ctx, const double* send, double* recv, size_t count);
+/* contiguous column block owned by `rank` of `nranks` over `ncols` columns (also the host split) */
+void pnol_block_range(int ncols, int nranks, int rank, int* begin, int* count);
+
+/* ---- whole-solver drivers: the C++ drop-in classes run on built-in objectives --------- */
+/* params arrays follow the classes' setParams order (see the headers in include/). */
+typedef struct { int iters; long evals; double f0; double fopt; } pnol_result;
+/* which: 0 = BFGS (12 params), 1 = BFGS_MPI (12 params), 2 = BFGS_Bnd (15 params) */
+int pnol_run_bfgs(int which, pnol_dobj* obj, int host_eval, const double* params, int nparams,
+                  double* X, int n, const double* Xlb, const double* Xub, pnol_result* res);
+/* which: 0 = LevMarq, 1 = LevMarqMPI (6 params). F0/FOpt host arrays of m. */
+int pnol_run_levmarq(int which, pnol_dobj* obj, int host_eval, const double* params, double* X, int n,
+                     double* F0, double* FOpt, int m, pnol_result* res);
+/* Host-objective FD through the C++ MultiObjective with a C callback objective
+ * (gradientApproximation / gradientApproximationMPI on the active communicator). */
+typedef void (*pnol_host_multi_fn)(const double* x, int n, double* F, int m, void* user);
+int pnol_host_fd_jacobian(pnol_host_multi_fn fn, void* user, const double* x, const double* h, int n, int m,
+                          int sharded, double* J_rowmajor);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PNOL_AMD_H_ */

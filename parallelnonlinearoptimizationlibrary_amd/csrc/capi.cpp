@@ -1,0 +1,195 @@
+// capi.cpp -- extern "C" kernel-level entry points of libpnol_amd.so (see include/pnol_amd.h).
+// Argument checking happens here and in the launchers; every function returns a status.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "pnol_internal.hpp"
+
+using namespace pnol;
+
+namespace {
+
+int set_device(pnol_ctx* ctx) {
+    if (!ctx) return PNOL_ERR_ARG;
+    PNOL_HIP(hipSetDevice(ctx->device));
+    return PNOL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pnol_hg_d(pnol_ctx* ctx, const double* D, int ldd, const double* g, double* p, int n) {
+    PNOL_CHECK(set_device(ctx));
+    ScopedTimer tm(ctx, "hg");
+    if (n <= PNOL_SEQ_MAX) return launch_gemv_neg_seq(ctx, D, ldd, n, n, g, p);
+    return launch_gemv_neg(ctx, D, ldd, n, n, g, p);
+}
+
+int pnol_gemv_neg_d(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y) {
+    PNOL_CHECK(set_device(ctx));
+    return launch_gemv_neg(ctx, A, lda, rows, cols, x, y);
+}
+
+int pnol_bfgs_update_exact_d(pnol_ctx* ctx, double* D, int ldd, const double* y, const double* s, int n) {
+    PNOL_CHECK(set_device(ctx));
+    return launch_bfgs_update_exact(ctx, D, ldd, y, s, n);
+}
+
+int pnol_bfgs_pass_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p, const double* a_p,
+                     const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
+                     double* v) {
+    PNOL_CHECK(set_device(ctx));
+    ScopedTimer tm(ctx, "bfgs_pass");
+    return launch_bfgs_pass(ctx, D, ldd, n, s_p, a_p, b_p, write_back, y, g, u, w, v);
+}
+
+int pnol_set_identity_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale) {
+    PNOL_CHECK(set_device(ctx));
+    return launch_set_identity(ctx, D, ldd, n, scale);
+}
+
+int pnol_jtj_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
+               double* jtj_diag) {
+    PNOL_CHECK(set_device(ctx));
+    return launch_jtj(ctx, JT, ldjt, m, n, lambda, A, lda, jtj_diag);
+}
+
+int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs) {
+    PNOL_CHECK(set_device(ctx));
+    if (!JT || !F || !rhs || m <= 0 || n <= 0 || ldjt < m) return PNOL_ERR_ARG;
+    ScopedTimer tm(ctx, "jtr");
+    return launch_jtr(ctx, JT, ldjt, m, n, F, rhs);
+}
+
+int pnol_solve_d(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n, int method, int* info) {
+    PNOL_CHECK(set_device(ctx));
+    if (method < 0 || method > 2) return PNOL_ERR_ARG;
+    ScopedTimer tm(ctx, "solve");
+    return launch_solve(ctx, A, lda, rhs, sigma, n, method, info);
+}
+
+int pnol_dobj_create(pnol_ctx* ctx, int kind, int n, int m, const double* host_p0, size_t len0,
+                     const double* host_p1, size_t len1, double power, pnol_dobj** out) {
+    PNOL_CHECK(set_device(ctx));
+    if (!out || n <= 0) return PNOL_ERR_ARG;
+    *out = nullptr;
+    switch (kind) {
+        case PNOL_OBJ_ROSENBROCK: case PNOL_OBJ_POWER: break;
+        case PNOL_OBJ_QUADRATIC:
+            if (!host_p0 || !host_p1 || len0 < (size_t)n || len1 < (size_t)n) return PNOL_ERR_ARG;
+            break;
+        case PNOL_OBJ_EXPCURVE: case PNOL_OBJ_CUBIC:
+            if (m <= 0 || !host_p0 || !host_p1 || len0 < (size_t)m || len1 < (size_t)m) return PNOL_ERR_ARG;
+            if ((kind == PNOL_OBJ_EXPCURVE && n != 3) || (kind == PNOL_OBJ_CUBIC && n != 4)) return PNOL_ERR_ARG;
+            break;
+        case PNOL_OBJ_LINRES:
+            if (m <= 0 || !host_p0 || !host_p1 || len0 < (size_t)m * n || len1 < (size_t)m) return PNOL_ERR_ARG;
+            break;
+        default:
+            return PNOL_ERR_UNSUPPORTED;
+    }
+    auto* o = new pnol_dobj();
+    o->kind = kind; o->n = n; o->m = m; o->power = power; o->ctx = ctx;
+    o->len0 = len0; o->len1 = len1;
+    auto upload = [&](const double* src, size_t len, double** dst) -> int {
+        if (!src || !len) return PNOL_OK;
+        if (hipMalloc(dst, sizeof(double) * len) != hipSuccess) return PNOL_ERR_NOMEM;
+        PNOL_HIP(hipMemcpy(*dst, src, sizeof(double) * len, hipMemcpyHostToDevice));
+        return PNOL_OK;
+    };
+    int st = upload(host_p0, len0, &o->p0);
+    if (st == PNOL_OK) st = upload(host_p1, len1, &o->p1);
+    if (st == PNOL_OK && kind == PNOL_OBJ_CUBIC) {
+        // CubicObjective evaluates pow(xData[k],3) every call (ExampleObjectives.hpp:175); it only
+        // depends on the data, so tabulate it once with the host libm the reference uses.
+        std::vector<double> p3(m);
+        for (int k = 0; k < m; ++k) p3[k] = std::pow(host_p0[k], 3.0);
+        st = upload(p3.data(), (size_t)m, &o->p2);
+    }
+    if (st != PNOL_OK) {
+        pnol_dobj_destroy(o);
+        return st;
+    }
+    *out = o;
+    return PNOL_OK;
+}
+
+int pnol_dobj_create_synthetic(pnol_ctx* ctx, int kind, int n, int m, unsigned long long seed, double bscale,
+                               double* xstar_out, pnol_dobj** out) {
+    PNOL_CHECK(set_device(ctx));
+    if (!out || n <= 0) return PNOL_ERR_ARG;
+    *out = nullptr;
+    auto* o = new pnol_dobj();
+    o->kind = kind; o->n = n; o->m = m; o->ctx = ctx;
+    int st = PNOL_OK;
+    if (kind == PNOL_OBJ_QUADRATIC) {
+        if (hipMalloc(&o->p0, sizeof(double) * n) != hipSuccess || hipMalloc(&o->p1, sizeof(double) * n) != hipSuccess)
+            st = PNOL_ERR_NOMEM;
+        o->len0 = o->len1 = (size_t)n;
+        if (st == PNOL_OK) st = launch_synthetic_quadratic(ctx, seed, n, bscale, o->p0, o->p1);
+    } else if (kind == PNOL_OBJ_LINRES) {
+        if (m <= 0) st = PNOL_ERR_ARG;
+        double* xs = nullptr;
+        if (st == PNOL_OK &&
+            (hipMalloc(&o->p0, sizeof(double) * (size_t)m * n) != hipSuccess ||
+             hipMalloc(&o->p1, sizeof(double) * (size_t)m) != hipSuccess || hipMalloc(&xs, sizeof(double) * n) != hipSuccess))
+            st = PNOL_ERR_NOMEM;
+        o->len0 = (size_t)m * n; o->len1 = (size_t)m;
+        if (st == PNOL_OK) st = launch_synthetic_linres(ctx, seed, m, n, o->p0, xs, o->p1);
+        if (st == PNOL_OK && xstar_out) {
+            if (hipMemcpyAsync(xstar_out, xs, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+                st = PNOL_ERR_HIP;
+        }
+        if (hipStreamSynchronize(ctx->stream) != hipSuccess) st = PNOL_ERR_HIP;
+        if (xs) (void)hipFree(xs);
+    } else {
+        st = PNOL_ERR_UNSUPPORTED;
+    }
+    if (st == PNOL_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) st = PNOL_ERR_HIP;
+    if (st != PNOL_OK) {
+        pnol_dobj_destroy(o);
+        return st;
+    }
+    *out = o;
+    return PNOL_OK;
+}
+
+int pnol_dobj_destroy(pnol_dobj* o) {
+    if (!o) return PNOL_ERR_ARG;
+    if (o->ctx) (void)hipSetDevice(o->ctx->device);
+    if (o->p0) (void)hipFree(o->p0);
+    if (o->p1) (void)hipFree(o->p1);
+    if (o->p2) (void)hipFree(o->p2);
+    delete o;
+    return PNOL_OK;
+}
+
+int pnol_dobj_info(pnol_dobj* o, int* kind, int* n, int* m) {
+    if (!o) return PNOL_ERR_ARG;
+    if (kind) *kind = o->kind;
+    if (n) *n = o->n;
+    if (m) *m = o->m;
+    return PNOL_OK;
+}
+
+int pnol_dobj_eval_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, double* out) {
+    PNOL_CHECK(set_device(ctx));
+    return launch_dobj_eval(ctx, obj, x, out);
+}
+
+int pnol_fd_gradient_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, int i0, int cnt,
+                       double* f0, double* g) {
+    PNOL_CHECK(set_device(ctx));
+    ScopedTimer tm(ctx, "fd_gradient");
+    return launch_fd_gradient(ctx, obj, x, h, i0, cnt, f0, g);
+}
+
+int pnol_fd_jacobian_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, int j0, int cnt, double* F0,
+                       int compute_f0, double* JT, int ldjt) {
+    PNOL_CHECK(set_device(ctx));
+    return launch_fd_jacobian(ctx, obj, x, h, j0, cnt, F0, compute_f0, JT, ldjt);
+}
+
+}  // extern "C"

@@ -1,0 +1,325 @@
+// bfgs_bnd.cpp -- bounded BFGS with active-set recursion (drop-in for
+// Source/BFGS_bnd_linesearch.cpp) plus the box helpers (Box_boundary_functions.cpp:11-40,
+// BFGS_with_bnd_linsearch_MPI.cpp:665-708).
+#include <cmath>
+#include <cstdio>
+#include <iostream>
+
+#include "../pnol_comm.hpp"
+#include "BFGS_bnd_linesearch.hpp"
+#include "dense_hessian.hpp"
+
+using namespace pnol;
+
+namespace {
+double sign_of(double x) { return x > 0 ? 1.0 : (x < 0 ? -1.0 : 0.0); }
+void print_vec(const std::vector<double>& v) {
+    for (double x : v) std::printf("%.17g ", x);
+    std::printf("\n");
+}
+}  // namespace
+
+void checkBoxBounds(std::vector<double>& X, std::vector<double>& Xlb, std::vector<double>& Xub) {
+    for (size_t i = 0; i < X.size(); ++i) {
+        if (X[i] - Xlb[i] < -std::fabs(Xlb[i]) / 1000 || X[i] - Xub[i] > std::fabs(Xub[i]) / 1000) {
+            if (comm_rank() == 0)
+                std::cout << std::endl << "!!!!----------------- WARNING -----------------!!!!" << std::endl
+                          << "X[" << i << "] = " << X[i] << " is outside of bounds Xlb[i] = " << Xlb[i]
+                          << ", Xub[i] = " << Xub[i] << std::endl;
+            X[i] = (Xlb[i] + Xub[i]) / 2.0;
+            if (comm_rank() == 0)
+                std::cout << " Replaced X[" << i << "] with " << X[i] << std::endl
+                          << "!!!!----------------- END WARNING -----------------!!!!" << std::endl << std::endl;
+        }
+    }
+}
+
+double computeAlphaBnd(std::vector<double>& X, std::vector<double>& Xlb, std::vector<double>& Xub,
+                       std::vector<double>& p) {
+    double bnd = 0;
+    for (size_t i = 0; i < X.size(); ++i) {
+        const double a1 = (Xub[i] - X[i]) / p[i];
+        const double a2 = (Xlb[i] - X[i]) / p[i];
+        double ai;
+        if (a1 > 0) ai = a1;
+        else if (a2 > 0) ai = a2;
+        else ai = 0;
+        if (i == 0) bnd = ai;
+        if (bnd > ai) bnd = ai;
+    }
+    return bnd;
+}
+
+double cubicInterpMinSimple(double aa, double ab, double pa, double pb, double da, double db) {
+    const double d1 = da + db - 3 * (pa - pb) / (aa - ab);
+    const double d2 = sign_of(ab - aa) * std::sqrt(d1 * d1 - da * db);
+    double an = ab - (ab - aa) * (db + d2 - d1) / (db - da + 2 * d2);
+    if (an < aa || an > ab || an != an) an = (aa + ab) / 2;
+    return an;
+}
+
+double BFGS_Bnd::lineSearchObj(double alpha, vector<double>& X, vector<double>& p, vector<double>& cX,
+                               vector<bool>& cI) {
+    std::vector<double> Xa(X.size());
+    for (size_t i = 0; i < X.size(); ++i) Xa[i] = X[i] + alpha * p[i];
+    return objPtr->objEvalRecur(Xa, cX, cI);
+}
+
+double BFGS_Bnd::lineSearchFDDerivative(double alpha, double phialpha, vector<double>& X, vector<double>& p,
+                                        vector<double>& cX, vector<bool>& cI) {
+    std::vector<double> Xa(X.size());
+    for (size_t i = 0; i < X.size(); ++i) Xa[i] = X[i] + (alpha + dalpha) * p[i];
+    const double Fa = objPtr->objEvalRecur(Xa, cX, cI);
+    return (Fa - phialpha) / dalpha;
+}
+
+void BFGS_Bnd::lineSearchZoomBnd(double aa, double ab, double pa, double pb, double da, double db, double phi0,
+                                 double dphi0, vector<double>& X, vector<double>& p, vector<double>& cX,
+                                 vector<bool>& cI, int& iter_ls, double& aOpt, double& pOpt, double& dOpt) {
+    // BFGS_bnd_linesearch.cpp:358-457
+    bool success = false;
+    while (iter_ls < maxIterLineSearch && (ab - aa > alphaTol)) {
+        const double ac = cubicInterpMinSimple(aa, ab, pa, pb, da, db);
+        const double pc = lineSearchObj(ac, X, p, cX, cI);
+        const double dc = lineSearchFDDerivative(ac, pc, X, p, cX, cI);
+        double pmin = pa;
+        if (pb < pa) pmin = pb;
+        if (pc > phi0 + c1 * ac * dphi0 || pc >= pmin) {
+            if (pa < pb) { ab = ac; pb = pc; db = dc; }
+            else { aa = ac; pa = pc; da = dc; }
+        } else {
+            if (std::fabs(dc) <= std::fabs(c2 * dphi0)) {
+                aOpt = ac; pOpt = pc; dOpt = dc; success = true;
+                break;
+            }
+            if (dc < 0) { aa = ac; pa = pc; da = dc; }
+            else { ab = ac; pb = pc; db = dc; }
+        }
+        iter_ls++;
+    }
+    if (!success) {
+        if (pa < pb) { aOpt = aa; pOpt = pa; dOpt = da; }
+        else { aOpt = ab; pOpt = pb; dOpt = db; }
+    }
+}
+
+void BFGS_Bnd::cubicInterpolationLineSearchBnd(vector<double>& X, vector<double>& Xlb, vector<double>& Xub,
+                                               double FX, vector<double>& dFdX, vector<double>& p, vector<double>& cX,
+                                               vector<bool>& cI, double& aOpt, double& Fopt) {
+    // BFGS_bnd_linesearch.cpp:203-353
+    bool success = false, atBound = false;
+    double dOpt = 0, phii = 0;
+    aOpt = 0;
+    Fopt = FX;
+    const double phi0 = FX, dphi0 = seq_dot(dFdX, p);
+    double aim1 = 0, pim1 = phi0, dim1 = dphi0;
+    const double amax = computeAlphaBnd(X, Xlb, Xub, p);
+    double ai = alphaGuess;
+    if (ai > amax) ai = amax;
+    int iter_ls = 0;
+    while (iter_ls < maxIterLineSearch) {
+        phii = lineSearchObj(ai, X, p, cX, cI);
+        const double di = lineSearchFDDerivative(ai, phii, X, p, cX, cI);
+        if ((phii > phi0 + c1 * ai * dphi0) || (phii >= pim1 && iter_ls > 1)) {
+            lineSearchZoomBnd(aim1, ai, pim1, phii, dim1, di, phi0, dphi0, X, p, cX, cI, iter_ls, aOpt, Fopt, dOpt);
+            success = true;
+            break;
+        }
+        if (std::fabs(di) <= std::fabs(c2 * dphi0)) { aOpt = ai; Fopt = phii; success = true; break; }
+        if (di >= 0) {
+            lineSearchZoomBnd(aim1, ai, pim1, phii, dim1, di, phi0, dphi0, X, p, cX, cI, iter_ls, aOpt, Fopt, dOpt);
+            success = true;
+            break;
+        }
+        if (ai == amax) { aOpt = ai; Fopt = phii; atBound = true; success = true; break; }
+        aim1 = ai; pim1 = phii; dim1 = di;
+        ai = 2 * ai;
+        if (ai > amax) ai = amax;
+        iter_ls++;
+    }
+    if (!success) {
+        if (pim1 < phii) { aOpt = aim1; Fopt = pim1; }
+        else if (phi0 < phii) { aOpt = 0; Fopt = phi0; }
+        else { aOpt = ai; Fopt = phii; }
+    }
+    if (verbose > 0 && comm_rank() == ROOT_ID) {
+        if (!atBound)
+            std::cout << "  Line search completed with alpha = " << aOpt << " and F = " << Fopt << " after " << iter_ls
+                      << " iterations. Note: alphaMax = " << amax << std::endl << std::endl;
+        else
+            std::cout << "  ! Line search terminated at boundary with alpha = " << aOpt << " and F = " << Fopt
+                      << " after " << iter_ls << " iterations. Note: alphaMax = " << amax << std::endl << std::endl;
+    }
+}
+
+void BFGS_Bnd::boundaryAssessment(double& F, vector<double>& X, vector<double>& p, vector<double>& dFdX,
+                                  DenseInverseHessian& D, vector<double>& Xlb, vector<double>& Xub, vector<double>& dX,
+                                  vector<double>& cX, vector<bool>& cI, bool& optimFlag, int& recurFlag) {
+    // BFGS_bnd_linesearch.cpp:503-728
+    const int ncur = (int)X.size();
+    const int Ndim = (int)cX.size();
+    std::vector<bool> cIcur(ncur, false);
+    std::vector<int> frozen;
+    bool bndFlag = false;
+    int icur = 0;
+    for (int i = 0; i < Ndim; ++i) {
+        if (cI[i]) continue;
+        if ((std::fabs(X[icur] - Xlb[icur]) < bndTol) && ((p[icur] < 0) || (dFdX[icur] > 0))) {
+            bndFlag = true; cI[i] = true; cX[i] = X[icur]; cIcur[icur] = true; frozen.push_back(i);
+        } else if ((std::fabs(X[icur] - Xub[icur]) < bndTol) && ((p[icur] > 0) || (dFdX[icur] < 0))) {
+            bndFlag = true; cI[i] = true; cX[i] = X[icur]; cIcur[icur] = true; frozen.push_back(i);
+        }
+        icur++;
+    }
+    int Nconst = 0;
+    for (int i = 0; i < Ndim; ++i) Nconst += cI[i];
+    if (bndFlag && verbose && comm_rank() == ROOT_ID) {
+        std::cout << std::endl << "Optimizer reached box boundary; steepest descent points outside the box at "
+                  << frozen.size() << " coordinate(s); recursing on the remaining ones." << std::endl;
+    }
+    const int nr = Ndim - Nconst;
+    if (bndFlag && nr > 0) {
+        double FR = F;
+        std::vector<double> XR, gR, lbR, ubR, dXR;
+        for (icur = 0; icur < ncur; ++icur)
+            if (!cIcur[icur]) {
+                XR.push_back(X[icur]); gR.push_back(dFdX[icur]); lbR.push_back(Xlb[icur]);
+                ubR.push_back(Xub[icur]); dXR.push_back(dX[icur]);
+            }
+        DenseInverseHessian DR(require_ctx(), nr, updateMode);
+        std::vector<double> scaleR;
+        if (!initialScalingVec.empty()) {
+            for (int i = 0; i < Ndim; ++i) if (!cI[i]) scaleR.push_back(initialScalingVec[i]);
+            DR.setIdentity(&scaleR);
+        } else {
+            DR.setIdentity();
+        }
+        recurFlag = true;
+        mainBFGSLoop(FR, XR, gR, DR, lbR, ubR, dXR, cX, cI, optimFlag, recurFlag);
+        int ir = 0;
+        for (icur = 0; icur < ncur; ++icur)
+            if (!cIcur[icur]) {
+                F = FR; X[icur] = XR[ir]; dFdX[icur] = gR[ir]; Xlb[icur] = lbR[ir]; Xub[icur] = ubR[ir];
+                dX[icur] = dXR[ir];
+                ir++;
+            }
+        for (int k : frozen) cI[k] = false;
+        if (!initialScalingVec.empty()) {
+            std::vector<double> scale;
+            for (int i = 0; i < Ndim; ++i) if (!cI[i]) scale.push_back(initialScalingVec[i]);
+            scale.resize(ncur, 1.0);
+            D.setIdentity(&scale);
+        } else {
+            D.setIdentity();
+        }
+        objPtr->gradientApproximationRecur(X, dX, dFdX, cX, cI);
+        bool cont = false;
+        for (icur = 0; icur < ncur; ++icur)
+            if (cIcur[icur]) {
+                if ((std::fabs(X[icur] - Xlb[icur]) < bndTol) && (dFdX[icur] < 0)) cont = true;
+                else if ((std::fabs(X[icur] - Xub[icur]) < bndTol) && (dFdX[icur] > 0)) cont = true;
+            }
+        Nconst = 0;
+        for (int i = 0; i < Ndim; ++i) Nconst += cI[i];
+        if (Nconst == 0) recurFlag = false;
+        optimFlag = cont;
+        if (verbose > 0 && comm_rank() == ROOT_ID)
+            std::cout << (cont ? "     Optimization continuing after recursive boundary optimization."
+                               : "     Optimization exiting after recursive boundary optimization.")
+                      << std::endl;
+    } else if (nr == 0) {
+        optimFlag = false;
+        if (verbose > 0 && comm_rank() == ROOT_ID) std::cout << "      NO VARIABLES LEFT TO OPTIMIZE!!!! " << std::endl;
+    }
+}
+
+void BFGS_Bnd::mainBFGSLoop(double& F, vector<double>& X, vector<double>& dFdX, DenseInverseHessian& D,
+                            vector<double>& Xlb, vector<double>& Xub, vector<double>& dX, vector<double>& cX,
+                            vector<bool>& cI, bool& optimFlag, int& recurFlag) {
+    // BFGS_bnd_linesearch.cpp:116-201
+    const int n = (int)X.size();
+    std::vector<double> gprev = dFdX, p(n), s(n), y(n), Xprev(n);
+    int iter = 0;
+    double xdiff = xMinDiff * 2, gnorm = 2 * minGrad2Norm;
+    while (optimFlag && iter < maxIter && xdiff > xMinDiff && gnorm > minGrad2Norm && totalIter < maxIter) {
+        if (verbose > 0 && comm_rank() == ROOT_ID)
+            std::cout << std::endl << "Iter = " << iter << " of bounded BFGS search starting with previous F = " << F
+                      << "." << std::endl;
+        D.direction(dFdX, p);
+        double alpha = 0, Fopt = 0;
+        cubicInterpolationLineSearchBnd(X, Xlb, Xub, F, dFdX, p, cX, cI, alpha, Fopt);
+        for (int i = 0; i < n; ++i) { Xprev[i] = X[i]; X[i] = X[i] + alpha * p[i]; }
+        F = Fopt;
+        gprev = dFdX;
+        objPtr->gradientApproximationRecur(X, dX, dFdX, cX, cI);
+        for (int i = 0; i < n; ++i) { s[i] = alpha * p[i]; y[i] = dFdX[i] - gprev[i]; }
+        D.update(y, s, nullptr, nullptr);
+        boundaryAssessment(F, X, p, dFdX, D, Xlb, Xub, dX, cX, cI, optimFlag, recurFlag);
+        xdiff = 0;
+        for (int i = 0; i < n; ++i) xdiff += std::fabs(X[i] - Xprev[i]);
+        gnorm = std::sqrt(seq_dot(dFdX, dFdX));
+        if (verbose > 1 && comm_rank() == ROOT_ID) {
+            std::cout << "  Step completed with F = " << F << " and mean abs xdiff is " << xdiff
+                      << " and the grad2norm = " << gnorm << std::endl << "  X = ";
+            print_vec(X);
+        }
+        iter = iter + 1;
+        totalIter = totalIter + 1;
+    }
+}
+
+void BFGS_Bnd::findMinBnd(vector<double>& X, vector<double>& Xlb, vector<double>& Xub, double& f0, double& fOpt) {
+    // BFGS_bnd_linesearch.cpp:15-113
+    totalIter = 0;
+    if (verbose >= 0 && comm_rank() == ROOT_ID) {
+        std::cout << std::endl << "  Starting bounded BFGS with line search. " << std::endl << "  X0 = ";
+        print_vec(X);
+    }
+    const int n = (int)X.size();
+    checkBoxBounds(X, Xlb, Xub);
+    std::vector<double> cX(n, 0.0), X0 = X;
+    std::vector<bool> cI(n, false);
+    std::vector<double> dX(n, dXGrad);
+    if (!dXGradVec.empty())
+        for (int i = 0; i < n; ++i) dX[i] = dXGradVec[i];
+    std::vector<double> dFdX(n, 0.0);
+    pnol_ctx* ctx = require_ctx();
+    DenseInverseHessian D(ctx, n, updateMode);
+    if (initHessFD) {
+        std::vector<double> dXH(n, dXHess);
+        std::vector<std::vector<double>> B;
+        objPtr->hessianApproximation(X, dXH, B);
+        const int ld = even_ld(n);
+        std::vector<double> hB((size_t)n * ld, 0.0), e(n, 0.0), c(n);
+        for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) hB[(size_t)i * ld + j] = B[i][j];
+        DevVec dA(ctx, hB.size()), de(ctx, n), dc(ctx, n);
+        std::vector<std::vector<double>> Dinv(n, std::vector<double>(n));
+        for (int j = 0; j < n; ++j) {
+            dA.upload(hB); e[j] = 1.0; de.upload(e);
+            int info = 0;
+            check(pnol_solve_d(ctx, dA.get(), ld, de.get(), dc.get(), n, 2, &info), "solve(initHessFD)");
+            dc.download(c);
+            for (int i = 0; i < n; ++i) Dinv[i][j] = c[i];
+            e[j] = 0.0;
+        }
+        D.setMatrix(Dinv);
+    } else if (!initialScalingVec.empty()) {
+        D.setIdentity(&initialScalingVec);
+    } else {
+        D.setIdentity();
+    }
+    objPtr->gradientApproximationRecur(X, dX, dFdX, cX, cI);
+    double F = objPtr->objEvalRecur(X, cX, cI);
+    f0 = F;
+    bool optimFlag = true;
+    int recurFlag = 0;
+    mainBFGSLoop(F, X, dFdX, D, Xlb, Xub, dX, cX, cI, optimFlag, recurFlag);
+    fOpt = F;
+    if (verbose >= 0 && comm_rank() == ROOT_ID) {
+        std::cout << std::endl << "  Completed bounded BFGS." << std::endl << "  X0 = ";
+        print_vec(X0);
+        std::cout << "  Xopt = ";
+        print_vec(X);
+        std::cout << "  f0 = " << f0 << ", fOpt = " << fOpt << std::endl << std::endl;
+    }
+}

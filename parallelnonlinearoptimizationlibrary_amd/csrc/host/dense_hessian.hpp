@@ -1,0 +1,49 @@
+// dense_hessian.hpp -- the BFGS inverse Hessian D as a device-resident matrix.
+//
+// Two execution modes (chosen per solve):
+//  exact  updateHessianInv and p = -D g in the reference's operation order
+//         (BFGS_with_linesearch.cpp:78-79, 389-432): bitwise equal to the CPU path.
+//  fast   the rank-2 form, applied lazily: D is stored together with a pending correction
+//         (s, a, b) meaning D + s a^T + b s^T.  update() runs ONE streaming pass that folds
+//         the pending correction into D (write-back), and returns u = D y, w = D^T y and
+//         v = D g_next, from which the next correction and the next direction follow with
+//         O(n) vector algebra: 16 n^2 bytes of HBM traffic per BFGS iteration.
+#pragma once
+
+#include <vector>
+
+#include "device_util.hpp"
+
+namespace pnol {
+
+class DenseInverseHessian {
+  public:
+    // mode: 0 auto (exact for n <= PNOL_SEQ_MAX), 1 exact, 2 fast
+    DenseInverseHessian(pnol_ctx* ctx, int n, int mode);
+    int n() const { return n_; }
+    bool exact() const { return exact_; }
+
+    void setIdentity(const std::vector<double>* diagScale = nullptr);
+    void setMatrix(const std::vector<std::vector<double>>& D);
+    void getMatrix(std::vector<std::vector<double>>& D);
+
+    // p = -D g
+    void direction(const std::vector<double>& g, std::vector<double>& p);
+    // D <- (I - rho s y^T) D (I - rho y s^T) + rho s s^T; with gnext, pnext = -D_new gnext
+    void update(const std::vector<double>& y, const std::vector<double>& s, const std::vector<double>* gnext,
+                std::vector<double>* pnext);
+
+  private:
+    void materialize();   // fold a pending correction into D
+
+    pnol_ctx* ctx_;
+    int n_, ld_;
+    bool exact_;
+    DevVec D_;
+    DevVec y_, s_, g_, u_, w_, v_;     // staging vectors
+    DevVec ps_, pa_, pb_;              // pending correction (fast mode)
+    bool pending_ = false;
+    std::vector<double> hs_, ha_, hb_; // host copies of the pending correction
+};
+
+}  // namespace pnol

@@ -1,0 +1,80 @@
+// device_util.hpp -- small RAII helpers the C++ drop-in classes use on top of the C ABI.
+#pragma once
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../pnol_comm.hpp"
+#include "pnol_amd.h"
+
+namespace pnol {
+
+// The drop-in classes have no error return (as in the reference); a failed device call is
+// fatal for the solve and surfaces as an exception naming the call.
+inline void check(int status, const char* what) {
+    if (status != PNOL_OK)
+        throw std::runtime_error(std::string("pnol_amd: ") + what + ": " + pnol_status_string(status));
+}
+
+inline pnol_ctx* require_ctx() {
+    pnol_ctx* c = default_ctx_or_null();
+    if (!c) throw std::runtime_error("pnol_amd: no gfx950 (MI355X) device visible; the HIP path has no CPU fallback");
+    return c;
+}
+
+// device array of doubles
+class DevVec {
+  public:
+    DevVec() = default;
+    DevVec(pnol_ctx* ctx, size_t count) { reset(ctx, count); }
+    ~DevVec() { release(); }
+    DevVec(const DevVec&) = delete;
+    DevVec& operator=(const DevVec&) = delete;
+    DevVec(DevVec&& o) noexcept : ctx_(o.ctx_), p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
+    DevVec& operator=(DevVec&& o) noexcept {
+        if (this != &o) { release(); ctx_ = o.ctx_; p_ = o.p_; n_ = o.n_; o.p_ = nullptr; o.n_ = 0; }
+        return *this;
+    }
+
+    void reset(pnol_ctx* ctx, size_t count) {
+        release();
+        ctx_ = ctx;
+        n_ = count;
+        void* p = nullptr;
+        check(pnol_malloc(ctx, sizeof(double) * (count ? count : 1), &p), "pnol_malloc");
+        p_ = static_cast<double*>(p);
+    }
+    void release() {
+        if (p_ && ctx_) pnol_free(ctx_, p_);
+        p_ = nullptr;
+        n_ = 0;
+    }
+    double* get() const { return p_; }
+    size_t size() const { return n_; }
+    void upload(const double* src, size_t count, size_t offset = 0) {
+        check(pnol_memcpy_h2d(ctx_, p_ + offset, src, sizeof(double) * count), "h2d");
+    }
+    void upload(const std::vector<double>& v) { upload(v.data(), v.size()); }
+    void download(double* dst, size_t count, size_t offset = 0) const {
+        check(pnol_memcpy_d2h(ctx_, dst, p_ + offset, sizeof(double) * count), "d2h");
+    }
+    void download(std::vector<double>& v) const { download(v.data(), v.size()); }
+
+  private:
+    pnol_ctx* ctx_ = nullptr;
+    double* p_ = nullptr;
+    size_t n_ = 0;
+};
+
+inline int even_ld(int n) { return (n + 1) & ~1; }
+
+// reference utility restatements used by the host-side control logic (sequential order,
+// identical to the CPU oracle's)
+inline double seq_dot(const std::vector<double>& a, const std::vector<double>& b) {
+    double s = 0.0;
+    for (size_t i = 0; i < a.size(); ++i) s = s + a[i] * b[i];
+    return s;
+}
+
+}  // namespace pnol

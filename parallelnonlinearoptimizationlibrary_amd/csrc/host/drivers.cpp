@@ -1,0 +1,232 @@
+// drivers.cpp -- C ABI entry points that run the C++ drop-in classes end to end on a
+// built-in device objective (used by the parity tests and bench.py through ctypes), plus a
+// callback-objective FD entry point for the host path of the FD engine.
+#include <cmath>
+#include <cstdio>
+#include <exception>
+#include <vector>
+
+#include "BFGS_bnd_linesearch.hpp"
+#include "BFGS_with_linesearch.hpp"
+#include "BFGS_with_linesearch_MPI.hpp"
+#include "LevenbergMarquardt.hpp"
+#include "LevenbergMarquardtMPI.hpp"
+#include "device_util.hpp"
+#include "../pnol_internal.hpp"
+
+using namespace pnol;
+
+namespace {
+
+std::vector<double> download_param(pnol_dobj* d, const double* p, size_t len) {
+    std::vector<double> h(len);
+    if (len && p) check(pnol_memcpy_d2h(d->ctx, h.data(), p, sizeof(double) * len), "d2h(params)");
+    return h;
+}
+
+// scalar objective around a pnol_dobj: FD batches on the device; single points evaluated with
+// the objective's host formula (identical arithmetic to the device batch)
+class DriverScalar : public Objective {
+  public:
+    DriverScalar(pnol_dobj* d, bool host_only) : d_(d), host_only_(host_only) {
+        p0_ = download_param(d, d->p0, d->len0);
+        p1_ = download_param(d, d->p1, d->len1);
+    }
+    double objEval(vector<double>& X) override {
+        evals++;
+        const size_t n = X.size();
+        double f = 0.0;
+        switch (d_->kind) {
+            case PNOL_OBJ_ROSENBROCK:
+                for (size_t k = 0; k + 1 < n; ++k) {
+                    const double t = X[k + 1] - X[k] * X[k], u = 1.0 - X[k];
+                    f = f + (100.0 * (t * t) + u * u);
+                }
+                return f;
+            case PNOL_OBJ_POWER:
+                for (size_t k = 0; k < n; ++k) f = f + (d_->power == 2.0 ? X[k] * X[k] : std::pow(X[k], d_->power));
+                return f;
+            case PNOL_OBJ_QUADRATIC:
+                for (size_t i = 0; i < n; ++i) {
+                    double t = (0.5 * p0_[i] * X[i]) * X[i] - p1_[i] * X[i];
+                    if (i + 1 < n) t = t + (0.25 * X[i]) * X[i + 1];
+                    f = f + t;
+                }
+                return f;
+            default:
+                throw std::runtime_error("DriverScalar: not a scalar objective");
+        }
+    }
+    pnol_dobj* deviceObjective(int n) override { return (host_only_ || n != d_->n) ? nullptr : d_; }
+    void countEvals(long k) override { evals += k; }
+    long evals = 0;
+
+  private:
+    pnol_dobj* d_;
+    bool host_only_;
+    std::vector<double> p0_, p1_;
+};
+
+class DriverMulti : public MultiObjective {
+  public:
+    DriverMulti(pnol_dobj* d, bool host_only) : d_(d), host_only_(host_only) {
+        if (host_only) {
+            p0_ = download_param(d, d->p0, d->len0);
+            p1_ = download_param(d, d->p1, d->len1);
+        }
+        x_.reset(d->ctx, d->n);
+        F_.reset(d->ctx, d->m);
+    }
+    void objEval(vector<double>& X, vector<double>& F) override {
+        evals++;
+        if (!host_only_) {
+            x_.upload(X);
+            check(pnol_dobj_eval_d(d_->ctx, d_, x_.get(), F_.get()), "dobj_eval");
+            F_.download(F);
+            return;
+        }
+        const int m = d_->m, n = d_->n;
+        switch (d_->kind) {
+            case PNOL_OBJ_EXPCURVE:
+                for (int k = 0; k < m; ++k) F[k] = p1_[k] - (X[0] * std::exp(X[1] * p0_[k]) + X[2]);
+                return;
+            case PNOL_OBJ_CUBIC:
+                for (int k = 0; k < m; ++k) {
+                    const double x = p0_[k];
+                    F[k] = p1_[k] - (X[0] * std::pow(x, 3.0) + X[1] * (x * x) + X[2] * x + X[3]);
+                }
+                return;
+            case PNOL_OBJ_LINRES:
+                for (int i = 0; i < m; ++i) {
+                    double acc = 0.0;
+                    for (int k = 0; k < n; ++k) acc = std::fma(p0_[(size_t)i * n + k], X[k], acc);
+                    F[i] = acc - p1_[i];
+                }
+                return;
+            default:
+                throw std::runtime_error("DriverMulti: not a residual objective");
+        }
+    }
+    pnol_dobj* deviceObjective() override { return host_only_ ? nullptr : d_; }
+    void countEvals(long k) override { evals += k; }
+    long evals = 0;
+
+  private:
+    pnol_dobj* d_;
+    bool host_only_;
+    std::vector<double> p0_, p1_;
+    DevVec x_, F_;
+};
+
+class CallbackMulti : public MultiObjective {
+  public:
+    CallbackMulti(pnol_host_multi_fn fn, void* user, int m) : fn_(fn), user_(user), m_(m) {}
+    void objEval(vector<double>& X, vector<double>& F) override { fn_(X.data(), (int)X.size(), F.data(), m_, user_); }
+
+  private:
+    pnol_host_multi_fn fn_;
+    void* user_;
+    int m_;
+};
+
+template <class F>
+int guarded(F&& body) {
+    try {
+        body();
+        return PNOL_OK;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "[pnol_amd] %s\n", e.what());
+        return PNOL_ERR_HIP;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int pnol_run_bfgs(int which, pnol_dobj* obj, int host_eval, const double* p, int np, double* X, int n,
+                  const double* Xlb, const double* Xub, pnol_result* res) {
+    if (!obj || !p || !X || n <= 0 || !res) return PNOL_ERR_ARG;
+    return guarded([&] {
+        DriverScalar o(obj, host_eval != 0);
+        std::vector<double> x(X, X + n);
+        double f0 = 0, fopt = 0;
+        if (which == 0) {
+            if (np < 12) throw std::runtime_error("BFGS needs 12 params");
+            BFGS b;
+            b.setParams(p[0], p[1], p[2], p[3], (int)p[4], p[5], p[6], p[7], p[8], p[9], p[10] != 0, p[11] != 0);
+            if (np > 12) b.setUpdateMode((int)p[12]);
+            b.setObjPtr(o);
+            b.findMin(x, f0, fopt);
+        } else if (which == 1) {
+            if (np < 12) throw std::runtime_error("BFGS_MPI needs 12 params");
+            BFGS_MPI b;
+            b.setParams(p[0], p[1], p[2], p[3], (int)p[4], p[5], p[6], p[7], p[8], p[9], p[10] != 0, p[11] != 0);
+            if (np > 12) b.setPoolSize((int)p[12]);
+            if (np > 13) b.setFixZeroPool(p[13] != 0);
+            if (np > 14) b.setUpdateMode((int)p[14]);
+            b.setObjPtr(o);
+            b.findMin(x, f0, fopt);
+        } else if (which == 2) {
+            if (np < 15 || !Xlb || !Xub) throw std::runtime_error("BFGS_Bnd needs 15 params and bounds");
+            BFGS_Bnd b;
+            b.setParams(p[0], p[1], p[2], p[3], p[4], p[5], (int)p[6], p[7], p[8], p[9], p[10], p[11], p[12],
+                        p[13] != 0, (int)p[14]);
+            if (np > 15) b.setUpdateMode((int)p[15]);
+            b.setObjPtr(o);
+            std::vector<double> lb(Xlb, Xlb + n), ub(Xub, Xub + n);
+            b.findMinBnd(x, lb, ub, f0, fopt);
+        } else {
+            throw std::runtime_error("unknown BFGS variant");
+        }
+        for (int i = 0; i < n; ++i) X[i] = x[i];
+        res->iters = 0;
+        res->evals = o.evals;
+        res->f0 = f0;
+        res->fopt = fopt;
+    });
+}
+
+int pnol_run_levmarq(int which, pnol_dobj* obj, int host_eval, const double* p, double* X, int n, double* F0,
+                     double* FOpt, int m, pnol_result* res) {
+    if (!obj || !p || !X || !F0 || !FOpt || n <= 0 || m <= 0 || !res) return PNOL_ERR_ARG;
+    return guarded([&] {
+        DriverMulti o(obj, host_eval != 0);
+        std::vector<double> x(X, X + n), f0(m, 0.0), fopt(m, 0.0);
+        if (which == 0) {
+            LevMarq lm;
+            lm.setParams(p[0], p[1], p[2], p[3], p[4], (int)p[5]);
+            lm.setObjPtr(o);
+            lm.findMin(x, f0, fopt);
+        } else {
+            LevMarqMPI lm;
+            lm.setParams(p[0], p[1], p[2], p[3], p[4], (int)p[5]);
+            lm.setObjPtr(o);
+            lm.findMin(x, f0, fopt);
+        }
+        for (int i = 0; i < n; ++i) X[i] = x[i];
+        for (int i = 0; i < m; ++i) { F0[i] = f0[i]; FOpt[i] = fopt[i]; }
+        res->iters = 0;
+        res->evals = o.evals;
+        double c0 = 0, c1 = 0;
+        for (int i = 0; i < m; ++i) { c0 = c0 + f0[i] * f0[i]; c1 = c1 + fopt[i] * fopt[i]; }
+        res->f0 = c0;
+        res->fopt = c1;
+    });
+}
+
+int pnol_host_fd_jacobian(pnol_host_multi_fn fn, void* user, const double* x, const double* h, int n, int m,
+                          int sharded, double* J) {
+    if (!fn || !x || !h || !J || n <= 0 || m <= 0) return PNOL_ERR_ARG;
+    return guarded([&] {
+        CallbackMulti o(fn, user, m);
+        std::vector<double> X(x, x + n), dX(h, h + n);
+        std::vector<std::vector<double>> Jv(m, std::vector<double>(n));
+        if (sharded) o.gradientApproximationMPI(X, dX, Jv);
+        else o.gradientApproximation(X, dX, Jv);
+        for (int i = 0; i < m; ++i)
+            for (int j = 0; j < n; ++j) J[(size_t)i * n + j] = Jv[i][j];
+    });
+}
+
+}  // extern "C"

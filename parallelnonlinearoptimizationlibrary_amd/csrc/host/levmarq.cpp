@@ -1,0 +1,177 @@
+// levmarq.cpp -- LevMarq and LevMarqMPI (drop-in for Source/LevenbergMarquardt.cpp and
+// Source/LevenbergMarquardtMPI.cpp).  Both share one device-resident loop; the MPI form
+// shards the FD Jacobian columns over the communicator and allgathers J^T.
+#include <cmath>
+#include <cstdio>
+#include <iostream>
+#include <utility>
+
+#include "../pnol_comm.hpp"
+#include "LevenbergMarquardt.hpp"
+#include "LevenbergMarquardtMPI.hpp"
+#include "device_util.hpp"
+
+using namespace pnol;
+
+namespace {
+
+struct LMParams {
+    double lambda0, lambdaFactor, dXGrad, xMinDiff;
+    int maxIter, verbose;
+};
+
+double norm2(const std::vector<double>& v) { return std::sqrt(seq_dot(v, v)); }
+
+void print_vec(const std::vector<double>& v) {
+    for (double x : v) std::printf("%.17g ", x);
+    std::printf("\n");
+}
+
+// Device state of one LM solve.  JT holds J column-major (one FD column per row, ld = ldjt)
+// with room for P * ceil(n/P) rows so a rank's block and the allgather share one buffer.
+class LMDevice {
+  public:
+    LMDevice(pnol_ctx* ctx, int n, int m, int nranks)
+        : ctx_(ctx), n_(n), m_(m), ldjt_(even_ld(m)), lda_(even_ld(n)), per_((n + nranks - 1) / nranks) {
+        JT_.reset(ctx, (size_t)nranks * per_ * ldjt_);
+        A_.reset(ctx, (size_t)n * lda_);
+        rhs_.reset(ctx, n); sigma_.reset(ctx, n); x_.reset(ctx, n); h_.reset(ctx, n);
+        F_.reset(ctx, m); Fprev_.reset(ctx, m); F0_.reset(ctx, m);
+    }
+
+    // residuals at X into host F and device F_
+    void evalResiduals(MultiObjective* obj, std::vector<double>& X, std::vector<double>& F) {
+        if (pnol_dobj* d = obj->deviceObjective()) {
+            x_.upload(X);
+            check(pnol_dobj_eval_d(ctx_, d, x_.get(), F_.get()), "objective eval");
+            F_.download(F);
+            obj->countEvals(1);
+        } else {
+            obj->objEval(X, F);
+            F_.upload(F);
+        }
+    }
+
+    // J^T at X (LevenbergMarquardt.cpp:55 / LevenbergMarquardtMPI.cpp:60)
+    void jacobian(MultiObjective* obj, std::vector<double>& X, std::vector<double>& dX, bool sharded) {
+        const int P = sharded ? comm_size() : 1, r = sharded ? comm_rank() : 0;
+        int b = 0, cnt = 0;
+        block_range(n_, P, r, &b, &cnt);
+        if (pnol_dobj* d = obj->deviceObjective()) {
+            x_.upload(X);
+            h_.upload(dX);
+            check(pnol_fd_jacobian_d(ctx_, d, x_.get(), h_.get(), b, cnt, F0_.get(), 1, JT_.get() + (size_t)b * ldjt_,
+                                     ldjt_),
+                  "fd_jacobian");
+            obj->countEvals(cnt + 1);
+        } else {
+            // host objective: the reference's column loop for this rank's block, one upload
+            std::vector<double> F0(m_), FdX(m_), XdX(n_), blk((size_t)per_ * ldjt_, 0.0);
+            obj->objEval(X, F0);
+            for (int q = 0; q < cnt; ++q) {
+                const int j = b + q;
+                XdX = X;
+                XdX[j] = XdX[j] + dX[j];
+                obj->objEval(XdX, FdX);
+                for (int i = 0; i < m_; ++i) blk[(size_t)q * ldjt_ + i] = (FdX[i] - F0[i]) / dX[j];
+            }
+            if (cnt > 0) JT_.upload(blk.data(), (size_t)cnt * ldjt_, (size_t)b * ldjt_);
+        }
+        if (P > 1)
+            check(comm_allgather_device(ctx_, JT_.get() + (size_t)r * per_ * ldjt_, JT_.get(), (size_t)per_ * ldjt_),
+                  "allgather(J)");
+    }
+
+    // sigma = (J^T J + lambda diag(J^T J))^{-1} (-J^T F)   (LevenbergMarquardt.cpp:59-83)
+    void step(double lambda, std::vector<double>& sigma) {
+        check(pnol_jtj_d(ctx_, JT_.get(), ldjt_, m_, n_, lambda, A_.get(), lda_, nullptr), "jtj");
+        check(pnol_jtr_d(ctx_, JT_.get(), ldjt_, m_, n_, F_.get(), rhs_.get()), "jtr");
+        int info = 0;
+        check(pnol_solve_d(ctx_, A_.get(), lda_, rhs_.get(), sigma_.get(), n_, 0, &info), "solve");
+        sigma_.download(sigma);
+    }
+
+    void saveF() { std::swap(F_, Fprev_); }      // Fprev <- F (the next eval overwrites F_)
+    void restoreF() { std::swap(F_, Fprev_); }
+
+  private:
+    pnol_ctx* ctx_;
+    int n_, m_, ldjt_, lda_, per_;
+    DevVec JT_, A_, rhs_, sigma_, x_, h_, F_, Fprev_, F0_;
+};
+
+void lm_solve(MultiObjective* obj, const LMParams& P, bool sharded, std::vector<double>& X, std::vector<double>& F0,
+              std::vector<double>& FOpt) {
+    const int n = (int)X.size();
+    const int m = (int)F0.size();
+    const int rank = sharded ? comm_rank() : 0;
+    const bool loud = rank == ROOT_ID;
+    pnol_ctx* ctx = require_ctx();
+    LMDevice dev(ctx, n, m, sharded ? comm_size() : 1);
+
+    double lambda = P.lambda0;
+    std::vector<double> dX(n, P.dXGrad), F(m), Fprev(m), sigma(n), Xprev(n);
+    dev.evalResiduals(obj, X, F0);
+    F = F0;
+    Fprev = F;
+    Xprev = X;
+    double nrm = norm2(F);
+    double chiSq = nrm * nrm;   // pow(vector2Norm(F), 2)
+    int iter = 0;
+    double xdiff2Norm = P.xMinDiff * 2;
+    while (iter < P.maxIter) {
+        dev.jacobian(obj, X, dX, sharded);
+        dev.step(lambda, sigma);
+        Xprev = X;
+        Fprev = F;
+        dev.saveF();
+        for (int i = 0; i < n; ++i) X[i] = X[i] + sigma[i];
+        dev.evalResiduals(obj, X, F);
+        const double chiSqPrev = chiSq;
+        nrm = norm2(F);
+        chiSq = nrm * nrm;
+        if (chiSq >= chiSqPrev || chiSq != chiSq) {
+            const bool talk = sharded ? (P.verbose >= 1 && loud) : (P.verbose > 1);
+            if (talk)
+                std::cout << "Step " << iter << " failed with chiSq = " << chiSq << ", chiSqPrev = " << chiSqPrev
+                          << ",  increasing lambda: " << lambda << " --> " << lambda * P.lambdaFactor << std::endl;
+            chiSq = chiSqPrev;
+            X = Xprev;
+            F = Fprev;
+            dev.restoreF();
+            lambda = lambda * P.lambdaFactor;
+        } else {
+            lambda = lambda / P.lambdaFactor;
+            xdiff2Norm = norm2(sigma);
+            if (xdiff2Norm < P.xMinDiff) break;
+        }
+        const bool talk = sharded ? (P.verbose >= 1 && loud) : (P.verbose > 0);
+        if (talk && iter % 10 == 0) {
+            std::cout << "At iter = " << iter << " the xdiff 2Norm = " << xdiff2Norm << ", chi^2 = " << chiSq
+                      << ", and params: ";
+            print_vec(X);
+        }
+        iter++;
+    }
+    FOpt = F;
+    if (P.verbose >= 0 && loud) {
+        std::cout << std::endl << "-----------------------------------------------------------------------------------" << std::endl;
+        std::cout << "Completed Levenberg Marquardt." << std::endl;
+        std::cout << "At iter = " << iter << " the xdiff 2Norm = " << xdiff2Norm << ", chi^2 = " << chiSq
+                  << ", and  optimal params: " << std::endl;
+        print_vec(X);
+        std::cout << "-----------------------------------------------------------------------------------" << std::endl << std::endl;
+    }
+}
+
+}  // namespace
+
+void LevMarq::findMin(vector<double>& X, vector<double>& F0, vector<double>& FOpt) {
+    LMParams P{lambda0, lambdaFactor, dXGrad, xMinDiff, maxIter, verbose};
+    lm_solve(mObjPtr, P, false, X, F0, FOpt);
+}
+
+void LevMarqMPI::findMin(vector<double>& X, vector<double>& F0, vector<double>& FOpt) {
+    LMParams P{lambda0, lambdaFactor, dXGrad, xMinDiff, maxIter, verbose};
+    lm_solve(mObjPtr, P, true, X, F0, FOpt);
+}

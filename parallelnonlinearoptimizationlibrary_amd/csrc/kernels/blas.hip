@@ -1,0 +1,399 @@
+// blas.hip -- HBM-streaming fp64 kernels of the BFGS inverse-Hessian path (gfx950).
+//
+//   k_gemv_neg        p = -D g  (BFGS_with_linesearch.cpp:78-79) and rhs = -J^T F
+//                     (LevenbergMarquardt.cpp:78-80): row-major streaming GEMV, 16-B loads,
+//                     R rows per wave, one wave reduction per row.  8 bytes/element.
+//   k_gemv_neg_seq    the same in the reference's summation order (one thread per row,
+//                     sequential from 0.0, no contraction) for n <= PNOL_SEQ_MAX.
+//   k_bfgs_exact_*    updateHessianInv (BFGS_with_linesearch.cpp:389-432) in its O(n^3)
+//                     operation order, bitwise equal to the CPU path, small n only.
+//   k_bfgs_pass       one read(+write) sweep of D: applies a pending rank-2 correction,
+//                     optionally writes D back, and accumulates D y, D^T y, D g with
+//                     deterministic partial sums.  16 bytes/element with write-back.
+//
+// All device code is compiled with -ffp-contract=off: every fma here is explicit.
+#include "../pnol_internal.hpp"
+
+namespace pnol {
+namespace {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, kWave);
+    return v;
+}
+
+// ------------------------------------------------------------------------------------
+// streaming GEMV: y = -A x, A rows x cols, row-major, lda even, A and x 16-byte aligned.
+// ------------------------------------------------------------------------------------
+template <int R>
+__global__ __launch_bounds__(256) void k_gemv_neg(const double* __restrict__ A, long lda, int rows, int cols,
+                                                  const double* __restrict__ x, double* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const long row0 = ((long)blockIdx.x * 4 + wave) * R;
+    if (row0 >= rows) return;
+
+    const double2* __restrict__ xv = reinterpret_cast<const double2*>(x);
+    const double2* arow[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        long rr = row0 + r < rows ? row0 + r : rows - 1;   // clamp: loads stay in bounds
+        arow[r] = reinterpret_cast<const double2*>(A + rr * lda);
+    }
+    double acc0[R], acc1[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) { acc0[r] = 0.0; acc1[r] = 0.0; }
+
+    const int pairs = cols >> 1;
+    constexpr int U = 4;                       // 4 x 1 KiB in flight per row per wave
+    int base = 0;
+    for (; base + U * kWave <= pairs; base += U * kWave) {
+        double2 xr[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) xr[u] = xv[base + u * kWave + lane];
+        double2 ar[R][U];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u) ar[r][u] = arow[r][base + u * kWave + lane];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                acc0[r] = fma(ar[r][u].x, xr[u].x, acc0[r]);
+                acc1[r] = fma(ar[r][u].y, xr[u].y, acc1[r]);
+            }
+    }
+    for (int c = base + lane; c < pairs; c += kWave) {
+        double2 xr = xv[c];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            double2 a = arow[r][c];
+            acc0[r] = fma(a.x, xr.x, acc0[r]);
+            acc1[r] = fma(a.y, xr.y, acc1[r]);
+        }
+    }
+    if ((cols & 1) && lane == 0) {             // odd trailing column
+        const double xl = x[cols - 1];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            long rr = row0 + r < rows ? row0 + r : rows - 1;
+            acc0[r] = fma(A[rr * lda + cols - 1], xl, acc0[r]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        double s = wave_sum(acc0[r] + acc1[r]);
+        if (lane == 0 && row0 + r < rows) y[row0 + r] = -s;
+    }
+}
+
+// reference order: s = 0; s = s + A_ij x_j, j ascending; y = -s  (matrixVectorMultiply + negate)
+__global__ void k_gemv_neg_seq(const double* __restrict__ A, long lda, int rows, int cols,
+                               const double* __restrict__ x, double* __restrict__ y) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows) return;
+    const double* a = A + (long)i * lda;
+    double s = 0.0;
+    for (int j = 0; j < cols; ++j) s = s + a[j] * x[j];
+    y[i] = -s;
+}
+
+// ------------------------------------------------------------------------------------
+// updateHessianInv in the reference's order (M1 D, then (M1 D) M2 + M3)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ double seq_dot(const double* a, const double* b, int n) {
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s = s + a[i] * b[i];
+    return s;
+}
+
+// T = M1 D with M1_il = [i==l] - rho s_i y_l
+__global__ void k_bfgs_exact_1(const double* __restrict__ D, long ldd, const double* __restrict__ y,
+                               const double* __restrict__ s, int n, double* __restrict__ T) {
+    __shared__ double rho_sh;
+    if (threadIdx.x == 0 && threadIdx.y == 0) rho_sh = 1 / seq_dot(y, s, n);
+    __syncthreads();
+    const double rho = rho_sh;
+    int i = blockIdx.y * blockDim.y + threadIdx.y;
+    int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || j >= n) return;
+    double acc = 0.0;
+    for (int l = 0; l < n; ++l) {
+        double m1 = (i == l ? 1.0 : 0.0) - rho * s[i] * y[l];
+        acc = acc + m1 * D[(long)l * ldd + j];
+    }
+    T[(long)i * n + j] = acc;
+}
+
+// D = T M2 + M3 with M2_lj = [l==j] - rho y_l s_j, M3_ij = rho s_i s_j
+__global__ void k_bfgs_exact_2(const double* __restrict__ T, double* __restrict__ D, long ldd,
+                               const double* __restrict__ y, const double* __restrict__ s, int n) {
+    __shared__ double rho_sh;
+    if (threadIdx.x == 0 && threadIdx.y == 0) rho_sh = 1 / seq_dot(y, s, n);
+    __syncthreads();
+    const double rho = rho_sh;
+    int i = blockIdx.y * blockDim.y + threadIdx.y;
+    int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || j >= n) return;
+    double acc = 0.0;
+    for (int l = 0; l < n; ++l) {
+        double m2 = (l == j ? 1.0 : 0.0) - rho * y[l] * s[j];
+        acc = acc + T[(long)i * n + l] * m2;
+    }
+    D[(long)i * ldd + j] = acc + rho * s[i] * s[j];
+}
+
+// ------------------------------------------------------------------------------------
+// fused BFGS pass
+// Tile: 256 rows x 512 columns per 256-thread workgroup; wave w owns 128 columns (2 per
+// lane) and walks the 256 rows in groups of 8.  Row partial sums (u = Dc y, v = Dc g) are
+// reduced across the wave with a 16-value butterfly (reduce-scatter) and written per
+// 128-column strip; column partials (w = Dc^T y) stay in registers and are written per
+// 256-row tile.  k_bfgs_pass_finish sums the partials in a fixed order: deterministic.
+// ------------------------------------------------------------------------------------
+constexpr int kPassRows = 256;
+constexpr int kPassCols = 512;
+constexpr int kGroup = 8;
+
+// reduce-scatter 16 values across the wave; the lanes with (lane & 3) == 0 end up with the
+// full 64-lane sum of value index ((lane>>5)&1)*8 + ((lane>>4)&1)*4 + ((lane>>3)&1)*2 + ((lane>>2)&1)
+__device__ __forceinline__ double butterfly16(double (&v)[16], int lane) {
+    {
+        const bool hi = (lane >> 5) & 1;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            double send = hi ? v[k] : v[k + 8];
+            double keep = hi ? v[k + 8] : v[k];
+            v[k] = keep + __shfl_xor(send, 32, kWave);
+        }
+    }
+    {
+        const bool hi = (lane >> 4) & 1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            double send = hi ? v[k] : v[k + 4];
+            double keep = hi ? v[k + 4] : v[k];
+            v[k] = keep + __shfl_xor(send, 16, kWave);
+        }
+    }
+    {
+        const bool hi = (lane >> 3) & 1;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            double send = hi ? v[k] : v[k + 2];
+            double keep = hi ? v[k + 2] : v[k];
+            v[k] = keep + __shfl_xor(send, 8, kWave);
+        }
+    }
+    {
+        const bool hi = (lane >> 2) & 1;
+        double send = hi ? v[0] : v[1];
+        double keep = hi ? v[1] : v[0];
+        v[0] = keep + __shfl_xor(send, 4, kWave);
+    }
+    double r = v[0];
+    r += __shfl_xor(r, 2, kWave);
+    r += __shfl_xor(r, 1, kWave);
+    return r;
+}
+
+template <bool PEND, bool WB>
+__global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ D, long ldd, int n,
+                                                   const double* __restrict__ sp, const double* __restrict__ ap,
+                                                   const double* __restrict__ bp, const double* __restrict__ y,
+                                                   const double* __restrict__ g, double* __restrict__ part_u,
+                                                   double* __restrict__ part_v, double* __restrict__ part_w) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int ncolt = (n + kPassCols - 1) / kPassCols;
+    const int rt = blockIdx.x / ncolt;            // row tile
+    const int ct = blockIdx.x % ncolt;            // column tile
+    const int strip = ct * 4 + wave;              // 128-column strip index
+    const int col = strip * 128 + 2 * lane;       // this lane's first column
+    const bool c0ok = col < n, c1ok = col + 1 < n;
+    const int colc = c0ok ? col : 0;              // clamped load column (pair start, even)
+
+    // per-lane column vectors
+    double yc0 = c0ok ? y[col] : 0.0, yc1 = c1ok ? y[col + 1] : 0.0;
+    double gc0 = c0ok ? g[col] : 0.0, gc1 = c1ok ? g[col + 1] : 0.0;
+    double ac0 = 0, ac1 = 0, sc0 = 0, sc1 = 0;
+    if (PEND) {
+        ac0 = c0ok ? ap[col] : 0.0; ac1 = c1ok ? ap[col + 1] : 0.0;
+        sc0 = c0ok ? sp[col] : 0.0; sc1 = c1ok ? sp[col + 1] : 0.0;
+    }
+    double w0 = 0.0, w1 = 0.0;
+
+    const int r_begin = rt * kPassRows;
+    const int r_end = min(n, r_begin + kPassRows);
+    for (int r0 = r_begin; r0 < r_end; r0 += kGroup) {
+        double2 d[kGroup];
+        double yr[kGroup], sr[kGroup], br[kGroup];
+#pragma unroll
+        for (int q = 0; q < kGroup; ++q) {
+            const int row = min(r0 + q, n - 1);
+            d[q] = *reinterpret_cast<const double2*>(D + (long)row * ldd + colc);
+            yr[q] = (r0 + q < n) ? y[row] : 0.0;
+            if (PEND) { sr[q] = sp[row]; br[q] = bp[row]; }
+        }
+        double vals[16];
+#pragma unroll
+        for (int q = 0; q < kGroup; ++q) {
+            double e0 = d[q].x, e1 = d[q].y;
+            if (PEND) {
+                e0 = fma(br[q], sc0, fma(sr[q], ac0, e0));
+                e1 = fma(br[q], sc1, fma(sr[q], ac1, e1));
+                if (!c0ok) e0 = d[q].x;
+                if (!c1ok) e1 = d[q].y;
+            }
+            if (WB && r0 + q < n && c0ok) {
+                *reinterpret_cast<double2*>(D + (long)(r0 + q) * ldd + col) = make_double2(e0, e1);
+            }
+            const double m0 = c0ok ? e0 : 0.0, m1 = c1ok ? e1 : 0.0;
+            vals[q] = fma(m1, yc1, m0 * yc0);
+            vals[8 + q] = fma(m1, gc1, m0 * gc0);
+            w0 = fma(m0, yr[q], w0);
+            w1 = fma(m1, yr[q], w1);
+        }
+        const double red = butterfly16(vals, lane);
+        if ((lane & 3) == 0) {
+            const int idx = ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
+            const int row = r0 + (idx & 7);
+            if (row < n) {
+                if (idx < 8) part_u[(long)strip * n + row] = red;
+                else part_v[(long)strip * n + row] = red;
+            }
+        }
+    }
+    if (c0ok) part_w[(long)rt * n + col] = w0;
+    if (c1ok) part_w[(long)rt * n + col + 1] = w1;
+}
+
+__global__ void k_bfgs_pass_finish(int n, int nstrips, int nrowt, const double* __restrict__ part_u,
+                                   const double* __restrict__ part_v, const double* __restrict__ part_w,
+                                   double* __restrict__ u, double* __restrict__ v, double* __restrict__ w) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double su = 0.0, sv = 0.0, sw = 0.0;
+    for (int s = 0; s < nstrips; ++s) {
+        su += part_u[(long)s * n + i];
+        sv += part_v[(long)s * n + i];
+    }
+    for (int t = 0; t < nrowt; ++t) sw += part_w[(long)t * n + i];
+    if (u) u[i] = su;
+    if (v) v[i] = sv;
+    if (w) w[i] = sw;
+}
+
+__global__ void k_set_identity(double* __restrict__ D, long ldd, int n, const double* __restrict__ scale) {
+    long total = (long)n * ldd;
+    for (long k = (long)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += (long)gridDim.x * blockDim.x) {
+        long i = k / ldd, j = k % ldd;
+        double v = 0.0;
+        if (i == j) v = scale ? scale[i] : 1.0;
+        D[k] = v;
+    }
+}
+
+__global__ void k_fill(double* __restrict__ p, size_t count, double value) {
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < count; k += (size_t)gridDim.x * blockDim.x)
+        p[k] = value;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int launch_gemv_neg(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y) {
+    if (!A || !x || !y || rows <= 0 || cols <= 0 || lda < cols) return PNOL_ERR_ARG;
+    if ((lda & 1) || !aligned16(A) || !aligned16(x)) return PNOL_ERR_ARG;
+    // rows per wave: enough waves to cover the chip (>= ~2 per SIMD) with long streams each
+    if (rows >= 8192) {
+        int blocks = (rows + 15) / 16;
+        hipLaunchKernelGGL((k_gemv_neg<4>), dim3(blocks), dim3(256), 0, ctx->stream, A, (long)lda, rows, cols, x, y);
+    } else if (rows >= 4096) {
+        int blocks = (rows + 7) / 8;
+        hipLaunchKernelGGL((k_gemv_neg<2>), dim3(blocks), dim3(256), 0, ctx->stream, A, (long)lda, rows, cols, x, y);
+    } else {
+        int blocks = (rows + 3) / 4;
+        hipLaunchKernelGGL((k_gemv_neg<1>), dim3(blocks), dim3(256), 0, ctx->stream, A, (long)lda, rows, cols, x, y);
+    }
+    return launch_check();
+}
+
+int launch_gemv_neg_seq(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y) {
+    if (!A || !x || !y || rows <= 0 || cols <= 0 || lda < cols) return PNOL_ERR_ARG;
+    int blocks = (rows + 63) / 64;
+    hipLaunchKernelGGL(k_gemv_neg_seq, dim3(blocks), dim3(64), 0, ctx->stream, A, (long)lda, rows, cols, x, y);
+    return launch_check();
+}
+
+int launch_bfgs_update_exact(pnol_ctx* ctx, double* D, int ldd, const double* y, const double* s, int n) {
+    if (!D || !y || !s || n <= 0 || ldd < n) return PNOL_ERR_ARG;
+    void* T = nullptr;
+    PNOL_CHECK(ws_get(ctx, "bfgs_exact_T", sizeof(double) * (size_t)n * n, &T));
+    dim3 blk(16, 16), grd((n + 15) / 16, (n + 15) / 16);
+    hipLaunchKernelGGL(k_bfgs_exact_1, grd, blk, 0, ctx->stream, D, (long)ldd, y, s, n, (double*)T);
+    PNOL_CHECK(launch_check());
+    hipLaunchKernelGGL(k_bfgs_exact_2, grd, blk, 0, ctx->stream, (const double*)T, D, (long)ldd, y, s, n);
+    return launch_check();
+}
+
+int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p, const double* a_p,
+                     const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
+                     double* v) {
+    if (!D || n <= 0 || ldd < n || (ldd & 1) || !aligned16(D)) return PNOL_ERR_ARG;
+    const bool pend = s_p != nullptr;
+    if (pend && (!a_p || !b_p)) return PNOL_ERR_ARG;
+    const int ncolt = (n + kPassCols - 1) / kPassCols;
+    const int nrowt = (n + kPassRows - 1) / kPassRows;
+    const int nstrips = ncolt * 4;
+    void *pu = nullptr, *pv = nullptr, *pw = nullptr, *zeros = nullptr;
+    PNOL_CHECK(ws_get(ctx, "pass_part_u", sizeof(double) * (size_t)nstrips * n, &pu));
+    PNOL_CHECK(ws_get(ctx, "pass_part_v", sizeof(double) * (size_t)nstrips * n, &pv));
+    PNOL_CHECK(ws_get(ctx, "pass_part_w", sizeof(double) * (size_t)nrowt * n, &pw));
+    if (!y || !g) {
+        PNOL_CHECK(ws_get(ctx, "pass_zeros", sizeof(double) * (size_t)n, &zeros));
+        PNOL_CHECK(launch_fill(ctx, (double*)zeros, (size_t)n, 0.0));
+        if (!y) y = (const double*)zeros;
+        if (!g) g = (const double*)zeros;
+    }
+    dim3 grd(nrowt * ncolt), blk(256);
+    auto* P0 = (double*)pu; auto* P1 = (double*)pv; auto* P2 = (double*)pw;
+    if (pend && write_back)
+        hipLaunchKernelGGL((k_bfgs_pass<true, true>), grd, blk, 0, ctx->stream, D, (long)ldd, n, s_p, a_p, b_p, y, g, P0, P1, P2);
+    else if (pend)
+        hipLaunchKernelGGL((k_bfgs_pass<true, false>), grd, blk, 0, ctx->stream, D, (long)ldd, n, s_p, a_p, b_p, y, g, P0, P1, P2);
+    else if (write_back)
+        hipLaunchKernelGGL((k_bfgs_pass<false, true>), grd, blk, 0, ctx->stream, D, (long)ldd, n, s_p, a_p, b_p, y, g, P0, P1, P2);
+    else
+        hipLaunchKernelGGL((k_bfgs_pass<false, false>), grd, blk, 0, ctx->stream, D, (long)ldd, n, s_p, a_p, b_p, y, g, P0, P1, P2);
+    PNOL_CHECK(launch_check());
+    hipLaunchKernelGGL(k_bfgs_pass_finish, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, n, nstrips, nrowt,
+                       (const double*)P0, (const double*)P1, (const double*)P2, u, v, w);
+    return launch_check();
+}
+
+int launch_set_identity(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale) {
+    if (!D || n <= 0 || ldd < n) return PNOL_ERR_ARG;
+    long total = (long)n * ldd;
+    int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_set_identity, dim3(blocks), dim3(256), 0, ctx->stream, D, (long)ldd, n, scale);
+    return launch_check();
+}
+
+int launch_fill(pnol_ctx* ctx, double* p, size_t count, double value) {
+    if (!p) return PNOL_ERR_ARG;
+    if (count == 0) return PNOL_OK;
+    int blocks = (int)std::min<size_t>((count + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(256), 0, ctx->stream, p, count, value);
+    return launch_check();
+}
+
+}  // namespace pnol

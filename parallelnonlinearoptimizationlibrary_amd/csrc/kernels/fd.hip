@@ -1,0 +1,393 @@
+// fd.hip -- device objectives and the batched forward-difference engine (gfx950).
+//
+// Replaces the N+1 sequential objEval calls of Objective::gradientApproximation
+// (PNOL_Objective.cpp:12-34) and MultiObjective::gradientApproximation (:165-197), and their
+// round-robin MPI forms (:88-159, :202-299): every perturbed point x + h_j e_j of a column
+// block [j0, j0+cnt) is evaluated in one launch.  Each point's objective value is computed
+// in the objective's own sequential operation order (one thread or one register tile per
+// point), so the device FD values equal the host objEval's bit for bit wherever the
+// objective uses no transcendental (Rosenbrock, quadratic, cubic with pow(x,3) tabulated on
+// the host, the fma-chain linear residual).  The perturbed coordinate is formed exactly as
+// the reference forms XdX[j] = X[j] + dX[j].
+//
+//   k_scalar_fd_values   scalar objectives: one thread per point, x staged through LDS
+//   k_multi_fd           ExpCurve / Cubic (tiny n): one thread per (point, residual)
+//   k_linres_eval        r = A x - y: one thread per residual row, A tiles staged in LDS
+//   k_linres_fd          all points of a block at once: a register-tiled fp64 VALU GEMM
+//                        R = A [x + h_j e_j]_j, epilogue J = ((R - y) - F0) / h  (no MFMA:
+//                        this is the objective, evaluated like user code would be)
+#include "../pnol_internal.hpp"
+
+namespace pnol {
+namespace {
+
+__device__ __forceinline__ double u01(unsigned long long seed, unsigned long long idx) {
+    unsigned long long z = seed + (idx + 1ULL) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z = z ^ (z >> 31);
+    return (double)(z >> 11) * 0x1.0p-53;
+}
+
+// ---- scalar objectives ------------------------------------------------------------------
+constexpr int kChunk = 1024;
+
+// Point p in [0, cnt] (p == cnt: the base point); vals[p] = f(x_p).
+template <int KIND>
+__global__ __launch_bounds__(256) void k_scalar_fd_values(const double* __restrict__ x, const double* __restrict__ h,
+                                                          int n, int i0, int cnt, const double* __restrict__ p0,
+                                                          const double* __restrict__ p1, double power,
+                                                          double* __restrict__ vals) {
+    __shared__ double xs[kChunk + 1];
+    __shared__ double ds[KIND == PNOL_OBJ_QUADRATIC ? kChunk : 1];
+    __shared__ double bs[KIND == PNOL_OBJ_QUADRATIC ? kChunk : 1];
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = p <= cnt;
+    const int j = (active && p < cnt) ? i0 + p : -1;          // perturbed coordinate, -1 = base
+    const double xj = (j >= 0) ? x[j] + h[j] : 0.0;            // XdX[j] = X[j] + dX[j]
+    double f = 0.0;
+    for (int c0 = 0; c0 < n; c0 += kChunk) {
+        const int len = min(kChunk, n - c0);
+        __syncthreads();
+        for (int e = threadIdx.x; e <= len && c0 + e < n; e += blockDim.x) xs[e] = x[c0 + e];
+        if (KIND == PNOL_OBJ_QUADRATIC)
+            for (int e = threadIdx.x; e < len; e += blockDim.x) { ds[e] = p0[c0 + e]; bs[e] = p1[c0 + e]; }
+        __syncthreads();
+        if (!active) continue;
+        if (KIND == PNOL_OBJ_ROSENBROCK) {
+            // value += 100 (x_{k+1} - x_k^2)^2 + (1 - x_k)^2, k < n-1  (ExampleObjectives.hpp:93-96)
+            const int kmax = min(len, n - 1 - c0);
+            for (int e = 0; e < kmax; ++e) {
+                const int k = c0 + e;
+                double xk = (k == j) ? xj : xs[e];
+                double xk1 = (k + 1 == j) ? xj : xs[e + 1];
+                double t = xk1 - xk * xk;
+                double u = 1.0 - xk;
+                f = f + (100.0 * (t * t) + u * u);
+            }
+        } else if (KIND == PNOL_OBJ_QUADRATIC) {
+            for (int e = 0; e < len; ++e) {
+                const int k = c0 + e;
+                double xk = (k == j) ? xj : xs[e];
+                double t = (0.5 * ds[e] * xk) * xk - bs[e] * xk;
+                if (k + 1 < n) {
+                    double xk1 = (k + 1 == j) ? xj : xs[e + 1];
+                    t = t + (0.25 * xk) * xk1;
+                }
+                f = f + t;
+            }
+        } else {  // PNOL_OBJ_POWER (ExampleObjectives.hpp:219-222)
+            for (int e = 0; e < len; ++e) {
+                const int k = c0 + e;
+                double xk = (k == j) ? xj : xs[e];
+                f = f + (power == 2.0 ? xk * xk : pow(xk, power));
+            }
+        }
+    }
+    if (active) vals[p] = f;
+}
+
+__global__ void k_scalar_fd_finish(const double* __restrict__ vals, const double* __restrict__ h, int i0, int cnt,
+                                   double* __restrict__ f0, double* __restrict__ g) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const double F = vals[cnt];
+    if (p == 0 && f0) *f0 = F;
+    if (p < cnt) g[p] = (vals[p] - F) / h[i0 + p];
+}
+
+// ---- small residual objectives (ExpCurve, Cubic) ---------------------------------------
+template <int KIND>
+__device__ __forceinline__ double multi_residual(const double* X, int k, const double* xd, const double* yd,
+                                                 const double* p3) {
+    if (KIND == PNOL_OBJ_EXPCURVE) {
+        double func = X[0] * exp(X[1] * xd[k]) + X[2];        // ExampleObjectives.hpp:128
+        return yd[k] - func;
+    } else {
+        double xv = xd[k];                                      // :175, pow(x,3) tabulated
+        double func = X[0] * p3[k] + X[1] * (xv * xv) + X[2] * xv + X[3];
+        return yd[k] - func;
+    }
+}
+
+template <int KIND>
+__global__ void k_multi_eval(const double* __restrict__ x, int n, int m, const double* __restrict__ xd,
+                             const double* __restrict__ yd, const double* __restrict__ p3, double* __restrict__ F) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    double X[4] = {0, 0, 0, 0};
+    for (int q = 0; q < n && q < 4; ++q) X[q] = x[q];
+    F[k] = multi_residual<KIND>(X, k, xd, yd, p3);
+}
+
+template <int KIND>
+__global__ void k_multi_fd(const double* __restrict__ x, const double* __restrict__ h, int n, int m, int j0, int cnt,
+                           const double* __restrict__ xd, const double* __restrict__ yd, const double* __restrict__ p3,
+                           const double* __restrict__ F0, double* __restrict__ JT, long ldjt) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int p = blockIdx.y;
+    if (k >= m || p >= cnt) return;
+    const int j = j0 + p;
+    double X[4] = {0, 0, 0, 0};
+    for (int q = 0; q < n && q < 4; ++q) X[q] = x[q];
+    X[j] = x[j] + h[j];
+    const double Fj = multi_residual<KIND>(X, k, xd, yd, p3);
+    JT[(long)p * ldjt + k] = (Fj - F0[k]) / h[j];
+}
+
+// ---- linear residual r = A x - y --------------------------------------------------------
+// one thread per row, fma chain over k ascending (the objective's definition); 64 rows per
+// workgroup, A staged 64 columns at a time (coalesced), LDS rows padded to 65 doubles.
+__global__ __launch_bounds__(64) void k_linres_eval(const double* __restrict__ A, const double* __restrict__ x,
+                                                    const double* __restrict__ y, int m, int n,
+                                                    double* __restrict__ F) {
+    __shared__ double As[64][65];
+    __shared__ double xs[64];
+    const int t = threadIdx.x;
+    const int r0 = blockIdx.x * 64;
+    double acc = 0.0;
+    for (int k0 = 0; k0 < n; k0 += 64) {
+        const int len = min(64, n - k0);
+        __syncthreads();
+        for (int r = 0; r < 64; ++r) {
+            const int row = r0 + r;
+            As[r][t] = (row < m && t < len) ? A[(long)row * n + k0 + t] : 0.0;
+        }
+        xs[t] = t < len ? x[k0 + t] : 0.0;
+        __syncthreads();
+        for (int e = 0; e < len; ++e) acc = fma(As[t][e], xs[e], acc);
+    }
+    const int row = r0 + t;
+    if (row < m) F[row] = y ? acc - y[row] : acc;
+}
+
+// Batched FD GEMM.  Workgroup tile 128 residual rows x 64 points, K staged 16 at a time;
+// thread (ty, tx) = (t >> 4, t & 15) owns rows ty*8..+8 and points tx*4..+4 (32 fp64
+// accumulators), every accumulator a sequential fma chain over k = 0..n-1.
+constexpr int kBM = 128, kBN = 64, kBK = 16;
+
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    const int xcd = orig % kNumXcd, q = nwg / kNumXcd, r = nwg % kNumXcd;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / kNumXcd;
+}
+
+template <bool EVEN>
+__global__ __launch_bounds__(256) void k_linres_fd(const double* __restrict__ A, const double* __restrict__ y,
+                                                   const double* __restrict__ x, const double* __restrict__ h, int m,
+                                                   int n, int j0, int cnt, const double* __restrict__ F0,
+                                                   double* __restrict__ JT, long ldjt) {
+    __shared__ __attribute__((aligned(16))) double As[kBK][kBM];
+    __shared__ __attribute__((aligned(16))) double Bs[kBK][kBN];
+    const int nmt = (m + kBM - 1) / kBM, nnt = (cnt + kBN - 1) / kBN;
+    const int v = xcd_remap(blockIdx.x, nmt * nnt);
+    const int mt = v / nnt, nt = v % nnt;
+    const int m0 = mt * kBM, pbase = nt * kBN;       // pbase: point index relative to j0
+    const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
+
+    double acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+
+    // A stage: thread loads row (t >> 1), k-offset (t & 1) * 8, 8 doubles
+    const int lrow = t >> 1, lk = (t & 1) * 8;
+    const long arow = (long)min(m0 + lrow, m - 1) * n;
+    const bool rowok = m0 + lrow < m;
+    double areg[8];
+    auto load_a = [&](int k0) {
+        if (EVEN && rowok && k0 + kBK <= n) {
+            const double2* p = reinterpret_cast<const double2*>(A + arow + k0 + lk);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { double2 w = p[q]; areg[2 * q] = w.x; areg[2 * q + 1] = w.y; }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int k = k0 + lk + q;
+                areg[q] = (rowok && k < n) ? A[arow + k] : 0.0;
+            }
+        }
+    };
+    const int nk = (n + kBK - 1) / kBK;
+    load_a(0);
+    for (int kc = 0; kc < nk; ++kc) {
+        const int k0 = kc * kBK;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) As[lk + q][lrow] = areg[q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = t + 256 * q;
+            const int k = e / kBN, jj = e % kBN;
+            const int kk = k0 + k;
+            const int p = pbase + jj;
+            const int jcol = j0 + p;
+            double val = kk < n ? x[kk] : 0.0;
+            if (p < cnt && kk == jcol) val = x[kk] + h[jcol];
+            Bs[k][jj] = val;
+        }
+        __syncthreads();
+        if (kc + 1 < nk) load_a(k0 + kBK);
+#pragma unroll
+        for (int k = 0; k < kBK; ++k) {
+            double a[8], b[4];
+            const double2* ap = reinterpret_cast<const double2*>(&As[k][ty * 8]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { double2 w = ap[q]; a[2 * q] = w.x; a[2 * q + 1] = w.y; }
+            const double2* bp = reinterpret_cast<const double2*>(&Bs[k][tx * 4]);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) { double2 w = bp[q]; b[2 * q] = w.x; b[2 * q + 1] = w.y; }
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = fma(a[i], b[j], acc[i][j]);
+        }
+    }
+    // epilogue: F = acc - y; J = (F - F0) / h
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int p = pbase + tx * 4 + j;
+        if (p >= cnt) continue;
+        const double hj = h[j0 + p];
+        double* out = JT + (long)p * ldjt;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int row = m0 + ty * 8 + i;
+            if (row < m) {
+                const double F = acc[i][j] - y[row];
+                out[row] = (F - F0[row]) / hj;
+            }
+        }
+    }
+}
+
+// ---- synthetic data, splitmix64 counter stream ---------------------------
+__global__ void k_synth_quadratic(unsigned long long seed, int n, double bscale, double* d, double* b) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        d[i] = 1.0 + 3.0 * u01(seed, (unsigned long long)i);
+        b[i] = (2.0 * u01(seed, (unsigned long long)(n + i)) - 1.0) * bscale;
+    }
+}
+
+__global__ void k_synth_linres(unsigned long long seed, int m, int n, double scale, double* A, double* xstar) {
+    const long mn = (long)m * n;
+    for (long k = (long)blockIdx.x * blockDim.x + threadIdx.x; k < mn + n; k += (long)gridDim.x * blockDim.x) {
+        if (k < mn) A[k] = (2.0 * u01(seed, (unsigned long long)k) - 1.0) * scale;
+        else xstar[k - mn] = 2.0 * u01(seed, (unsigned long long)k) - 1.0;
+    }
+}
+
+}  // namespace
+
+// ---- launchers ------------------------------------------------------------------------------
+static bool is_scalar_kind(int k) { return k == PNOL_OBJ_ROSENBROCK || k == PNOL_OBJ_POWER || k == PNOL_OBJ_QUADRATIC; }
+
+int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out) {
+    if (!o || !x || !out) return PNOL_ERR_ARG;
+    switch (o->kind) {
+        case PNOL_OBJ_ROSENBROCK:
+        case PNOL_OBJ_POWER:
+        case PNOL_OBJ_QUADRATIC: {
+            // evaluate the base point only: cnt = 0 -> vals[0] = f(x)
+            if (o->kind == PNOL_OBJ_ROSENBROCK)
+                hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_ROSENBROCK>), dim3(1), dim3(64), 0, ctx->stream, x, x, o->n, 0, 0,
+                                   o->p0, o->p1, o->power, out);
+            else if (o->kind == PNOL_OBJ_POWER)
+                hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_POWER>), dim3(1), dim3(64), 0, ctx->stream, x, x, o->n, 0, 0,
+                                   o->p0, o->p1, o->power, out);
+            else
+                hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_QUADRATIC>), dim3(1), dim3(64), 0, ctx->stream, x, x, o->n, 0, 0,
+                                   o->p0, o->p1, o->power, out);
+            return launch_check();
+        }
+        case PNOL_OBJ_EXPCURVE:
+            hipLaunchKernelGGL((k_multi_eval<PNOL_OBJ_EXPCURVE>), dim3((o->m + 255) / 256), dim3(256), 0, ctx->stream, x, o->n,
+                               o->m, o->p0, o->p1, o->p2, out);
+            return launch_check();
+        case PNOL_OBJ_CUBIC:
+            hipLaunchKernelGGL((k_multi_eval<PNOL_OBJ_CUBIC>), dim3((o->m + 255) / 256), dim3(256), 0, ctx->stream, x, o->n,
+                               o->m, o->p0, o->p1, o->p2, out);
+            return launch_check();
+        case PNOL_OBJ_LINRES: {
+            ScopedTimer tm(ctx, "linres_eval");
+            hipLaunchKernelGGL(k_linres_eval, dim3((o->m + 63) / 64), dim3(64), 0, ctx->stream, o->p0, x, o->p1, o->m,
+                               o->n, out);
+            return launch_check();
+        }
+        default:
+            return PNOL_ERR_UNSUPPORTED;
+    }
+}
+
+int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt, double* f0,
+                       double* g) {
+    if (!o || !x || !h || !is_scalar_kind(o->kind)) return PNOL_ERR_ARG;
+    if (i0 < 0 || cnt < 0 || i0 + cnt > o->n) return PNOL_ERR_ARG;
+    void* vals = nullptr;
+    PNOL_CHECK(ws_get(ctx, "fd_vals", sizeof(double) * (size_t)(cnt + 1), &vals));
+    const int blocks = (cnt + 1 + 255) / 256;
+    double* V = (double*)vals;
+    if (o->kind == PNOL_OBJ_ROSENBROCK)
+        hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_ROSENBROCK>), dim3(blocks), dim3(256), 0, ctx->stream, x, h, o->n, i0,
+                           cnt, o->p0, o->p1, o->power, V);
+    else if (o->kind == PNOL_OBJ_POWER)
+        hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_POWER>), dim3(blocks), dim3(256), 0, ctx->stream, x, h, o->n, i0, cnt,
+                           o->p0, o->p1, o->power, V);
+    else
+        hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_QUADRATIC>), dim3(blocks), dim3(256), 0, ctx->stream, x, h, o->n, i0,
+                           cnt, o->p0, o->p1, o->power, V);
+    PNOL_CHECK(launch_check());
+    hipLaunchKernelGGL(k_scalar_fd_finish, dim3((cnt + 255) / 256 + 1), dim3(256), 0, ctx->stream, (const double*)V, h, i0,
+                       cnt, f0, g);
+    return launch_check();
+}
+
+int launch_fd_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int j0, int cnt, double* F0,
+                       int compute_f0, double* JT, int ldjt) {
+    if (!o || !x || !h || !F0 || is_scalar_kind(o->kind)) return PNOL_ERR_ARG;
+    if (j0 < 0 || cnt < 0 || j0 + cnt > o->n || ldjt < o->m) return PNOL_ERR_ARG;
+    if (compute_f0) PNOL_CHECK(launch_dobj_eval(ctx, o, x, F0));
+    if (cnt == 0) return PNOL_OK;
+    if (!JT) return PNOL_ERR_ARG;
+    switch (o->kind) {
+        case PNOL_OBJ_EXPCURVE:
+            hipLaunchKernelGGL((k_multi_fd<PNOL_OBJ_EXPCURVE>), dim3((o->m + 255) / 256, cnt), dim3(256), 0, ctx->stream, x, h,
+                               o->n, o->m, j0, cnt, o->p0, o->p1, o->p2, (const double*)F0, JT, (long)ldjt);
+            return launch_check();
+        case PNOL_OBJ_CUBIC:
+            hipLaunchKernelGGL((k_multi_fd<PNOL_OBJ_CUBIC>), dim3((o->m + 255) / 256, cnt), dim3(256), 0, ctx->stream, x, h,
+                               o->n, o->m, j0, cnt, o->p0, o->p1, o->p2, (const double*)F0, JT, (long)ldjt);
+            return launch_check();
+        case PNOL_OBJ_LINRES: {
+            const int nmt = (o->m + kBM - 1) / kBM, nnt = (cnt + kBN - 1) / kBN;
+            const bool even = (o->n % 2) == 0;
+            ScopedTimer tm(ctx, "fd_jacobian");
+            if (even)
+                hipLaunchKernelGGL((k_linres_fd<true>), dim3(nmt * nnt), dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
+                                   o->n, j0, cnt, (const double*)F0, JT, (long)ldjt);
+            else
+                hipLaunchKernelGGL((k_linres_fd<false>), dim3(nmt * nnt), dim3(256), 0, ctx->stream, o->p0, o->p1, x, h,
+                                   o->m, o->n, j0, cnt, (const double*)F0, JT, (long)ldjt);
+            return launch_check();
+        }
+        default:
+            return PNOL_ERR_UNSUPPORTED;
+    }
+}
+
+int launch_synthetic_quadratic(pnol_ctx* ctx, unsigned long long seed, int n, double bscale, double* d, double* b) {
+    hipLaunchKernelGGL(k_synth_quadratic, dim3(std::min(1024, (n + 255) / 256)), dim3(256), 0, ctx->stream, seed, n, bscale,
+                       d, b);
+    return launch_check();
+}
+
+int launch_synthetic_linres(pnol_ctx* ctx, unsigned long long seed, int m, int n, double* A, double* xstar, double* y) {
+    const double scale = 1.0 / std::sqrt((double)n);
+    hipLaunchKernelGGL(k_synth_linres, dim3(4096), dim3(256), 0, ctx->stream, seed, m, n, scale, A, xstar);
+    PNOL_CHECK(launch_check());
+    // y = A x* with the residual's own fma chain (no y offset)
+    hipLaunchKernelGGL(k_linres_eval, dim3((m + 63) / 64), dim3(64), 0, ctx->stream, (const double*)A,
+                       (const double*)xstar, (const double*)nullptr, m, n, y);
+    return launch_check();
+}
+
+}  // namespace pnol

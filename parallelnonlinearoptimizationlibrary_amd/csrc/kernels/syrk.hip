@@ -1,0 +1,262 @@
+// syrk.hip -- J^T J on fp64 MFMA (v_mfma_f64_16x16x4_f64), gfx950.
+//
+// Replaces matrixTranspose(J, JT) + matrixMultiply(JT, J, JTJ) + the Marquardt diagonal
+// loop, LevenbergMarquardt.cpp:59-73.  J lives on the device as JT (n x m row-major: one
+// finite-difference column per row), so J^T J = JT JT^T is a SYRK whose two operands are
+// both read along contiguous rows of JT.
+//
+//   k_syrk_tile     one 128 x 128 lower-triangle output tile (ti >= tj) per 256-thread
+//                   workgroup, K split over `split_k` workgroups.  4 waves as 2 x 2, each
+//                   64 x 64 = 4 x 4 MFMA tiles (16 fp64 accumulator quads = 128 VGPRs).
+//                   K staged 16 columns at a time through double-buffered LDS (rows padded
+//                   to 18 doubles: 16-B aligned rows, conflict-free fragment reads).
+//   k_syrk_reduce   sums the split-K partial tiles in a fixed order (deterministic), applies
+//                   A_ii = (1 + lambda) * JTJ_ii, writes the lower triangle and its mirror.
+//   k_jtj_seq       n <= PNOL_SEQ_MAX: the reference's summation order, bitwise.
+// The same tile kernel in "direct" mode (C = beta C + alpha X X^T on the lower tiles) is the
+// trailing update of the blocked Cholesky in solve.hip.
+#include "../pnol_internal.hpp"
+
+namespace pnol {
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int kTile = 128;
+constexpr int kTK = 16;
+constexpr int kPad = 18;   // LDS row stride in doubles
+
+__device__ __forceinline__ void tile_of(int t, int& ti, int& tj) {
+    int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while ((r + 1) * (r + 2) / 2 <= t) ++r;
+    while (r * (r + 1) / 2 > t) --r;
+    ti = r;
+    tj = t - r * (r + 1) / 2;
+}
+
+// Stage loader: 128 rows x 16 doubles of X starting at (row0, k0) into registers.
+// Thread t owns row t>>1, columns (t&1)*8 .. +8.  Rows >= nr and columns >= kend read as 0.
+struct StageRegs { double2 v[4]; };
+
+__device__ __forceinline__ void load_stage(StageRegs& s, const double* __restrict__ X, long ldx, int nr, int row0,
+                                           int k0, int kend, bool full) {
+    const int t = threadIdx.x;
+    const int row = row0 + (t >> 1);
+    const int kc = k0 + (t & 1) * 8;
+    if (row < nr && full) {
+        const double2* p = reinterpret_cast<const double2*>(X + (long)row * ldx + kc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s.v[q] = p[q];
+    } else {
+        const double* p = X + (long)min(row, nr - 1) * ldx;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            int c0 = kc + 2 * q;
+            double a = (row < nr && c0 < kend) ? p[c0] : 0.0;
+            double b = (row < nr && c0 + 1 < kend) ? p[c0 + 1] : 0.0;
+            s.v[q] = make_double2(a, b);
+        }
+    }
+}
+
+__device__ __forceinline__ void store_stage(const StageRegs& s, double* __restrict__ lds) {
+    const int t = threadIdx.x;
+    double* dst = lds + (t >> 1) * kPad + (t & 1) * 8;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *reinterpret_cast<double2*>(dst + 2 * q) = s.v[q];
+}
+
+// MODE 0: write split-K partial tile to part; MODE 1: C = beta*C + alpha*acc (lower tiles)
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
+                                                      int split_k, int kchunk, double* __restrict__ part,
+                                                      double* __restrict__ C, long ldc, double alpha,
+                                                      double beta) {
+    __shared__ __attribute__((aligned(16))) double lds[2][2][kTile * kPad];   // [buf][P/Q]
+
+    const int blk = blockIdx.x;
+    const int t = blk / split_k;
+    const int sidx = blk % split_k;
+    int ti, tj;
+    tile_of(t, ti, tj);
+    const bool diag = ti == tj;
+    const int prow0 = ti * kTile, qrow0 = tj * kTile;
+    const int kbeg = sidx * kchunk;
+    const int kend = min(K, kbeg + kchunk);
+    const int nstages = kend > kbeg ? (kend - kbeg + kTK - 1) / kTK : 0;
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const bool ldx_even = (ldx & 1) == 0;
+
+    d4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+
+    StageRegs ps, qs;
+    if (nstages > 0) {
+        bool full = ldx_even && (kbeg + kTK <= kend);
+        load_stage(ps, X, ldx, nr, prow0, kbeg, kend, full);
+        if (!diag) load_stage(qs, X, ldx, nr, qrow0, kbeg, kend, full);
+    }
+    const int frow = lane & 15;
+    const int fk = lane >> 4;
+    for (int st = 0; st < nstages; ++st) {
+        const int buf = st & 1;
+        double* P = lds[buf][0];
+        double* Q = diag ? lds[buf][0] : lds[buf][1];
+        store_stage(ps, P);
+        if (!diag) store_stage(qs, Q);
+        __syncthreads();
+        if (st + 1 < nstages) {
+            const int k0 = kbeg + (st + 1) * kTK;
+            bool full = ldx_even && (k0 + kTK <= kend);
+            load_stage(ps, X, ldx, nr, prow0, k0, kend, full);
+            if (!diag) load_stage(qs, X, ldx, nr, qrow0, k0, kend, full);
+        }
+#pragma unroll
+        for (int kk = 0; kk < kTK / 4; ++kk) {
+            double a[4], b[4];
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) a[mi] = P[(wr * 64 + mi * 16 + frow) * kPad + kk * 4 + fk];
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) b[ni] = Q[(wc * 64 + ni * 16 + frow) * kPad + kk * 4 + fk];
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+        }
+    }
+
+    // f64 MFMA C/D layout: lane l, register r -> row (l >> 4) + 4 r, column l & 15
+    const int ocol = lane & 15;
+    const int orow = lane >> 4;
+    if (MODE == 0) {
+        double* out = part + (long)blk * kTile * kTile;
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    int row = wr * 64 + mi * 16 + orow + 4 * r;
+                    int col = wc * 64 + ni * 16 + ocol;
+                    out[row * kTile + col] = acc[mi][ni][r];
+                }
+    } else {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    int i = prow0 + wr * 64 + mi * 16 + orow + 4 * r;
+                    int j = qrow0 + wc * 64 + ni * 16 + ocol;
+                    if (i < nr && j < nr && j <= i) {
+                        double* c = C + (long)i * ldc + j;
+                        *c = beta * (*c) + alpha * acc[mi][ni][r];
+                    }
+                }
+    }
+}
+
+__global__ void k_syrk_reduce(const double* __restrict__ part, int ntiles, int split_k, int n, double lambda,
+                              double* __restrict__ A, long lda, double* __restrict__ diag_out) {
+    const int t = blockIdx.y;
+    int ti, tj;
+    tile_of(t, ti, tj);
+    const double scale = 1 + lambda;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < kTile * kTile; e += gridDim.x * blockDim.x) {
+        const int r = e / kTile, c = e % kTile;
+        const int i = ti * kTile + r, j = tj * kTile + c;
+        if (i >= n || j >= n || j > i) continue;
+        const double* p = part + ((long)t * split_k) * kTile * kTile + e;
+        double v = 0.0;
+        for (int s = 0; s < split_k; ++s) v += p[(long)s * kTile * kTile];
+        if (i == j) {
+            if (diag_out) diag_out[i] = v;
+            A[(long)i * lda + i] = scale * v;
+        } else {
+            A[(long)i * lda + j] = v;
+            A[(long)j * lda + i] = v;
+        }
+    }
+}
+
+// reference order: JTJ_ij = sum_k JT_ik * JT_jk (k ascending, from 0.0); A_ii = (1+lambda) JTJ_ii
+__global__ void k_jtj_seq(const double* __restrict__ JT, long ldjt, int m, int n, double lambda,
+                          double* __restrict__ A, long lda, double* __restrict__ diag_out) {
+    int i = blockIdx.y * blockDim.y + threadIdx.y;
+    int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || j >= n) return;
+    const double* a = JT + (long)i * ldjt;
+    const double* b = JT + (long)j * ldjt;
+    double s = 0.0;
+    for (int k = 0; k < m; ++k) s = s + a[k] * b[k];
+    if (i == j) {
+        if (diag_out) diag_out[i] = s;
+        A[(long)i * lda + j] = (1 + lambda) * s;
+    } else {
+        A[(long)i * lda + j] = s;
+    }
+}
+
+}  // namespace
+
+static int choose_split_k(int ntiles, int K) {
+    // aim for ~2 resident workgroups on each of the 256 CUs, K slices of >= 256 columns
+    int s = (512 + ntiles - 1) / ntiles;
+    int kmax = (K + 255) / 256;
+    if (s > kmax) s = kmax;
+    if (s < 1) s = 1;
+    return s;
+}
+
+int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
+               double* jtj_diag) {
+    if (!JT || !A || m <= 0 || n <= 0 || ldjt < m || lda < n) return PNOL_ERR_ARG;
+    if (n <= PNOL_SEQ_MAX && m <= 4096) {
+        dim3 blk(16, 16), grd((n + 15) / 16, (n + 15) / 16);
+        hipLaunchKernelGGL(k_jtj_seq, grd, blk, 0, ctx->stream, JT, (long)ldjt, m, n, lambda, A, (long)lda, jtj_diag);
+        return launch_check();
+    }
+    const int nt = (n + kTile - 1) / kTile;
+    const int ntiles = nt * (nt + 1) / 2;
+    const int split_k = choose_split_k(ntiles, m);
+    int kchunk = (m + split_k - 1) / split_k;
+    kchunk = (kchunk + kTK - 1) / kTK * kTK;
+    void* part = nullptr;
+    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * split_k * kTile * kTile, &part));
+    {
+        ScopedTimer tm(ctx, "syrk");
+        hipLaunchKernelGGL((k_syrk_tile<0>), dim3(ntiles * split_k), dim3(256), 0, ctx->stream, JT, (long)ldjt, n, m,
+                           split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0);
+    }
+    PNOL_CHECK(launch_check());
+    ScopedTimer tm(ctx, "syrk_reduce");
+    hipLaunchKernelGGL(k_syrk_reduce, dim3(8, ntiles), dim3(256), 0, ctx->stream, (const double*)part, ntiles,
+                       split_k, n, lambda, A, (long)lda, jtj_diag);
+    return launch_check();
+}
+
+int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, double alpha, double* C, int ldc,
+                      int split_k) {
+    (void)split_k;
+    if (!X || !C || nr <= 0 || K <= 0) return PNOL_ERR_ARG;
+    const int nt = (nr + kTile - 1) / kTile;
+    const int ntiles = nt * (nt + 1) / 2;
+    hipLaunchKernelGGL((k_syrk_tile<1>), dim3(ntiles), dim3(256), 0, ctx->stream, X, (long)ldx, nr, K, 1, K,
+                       (double*)nullptr, C, (long)ldc, alpha, 1.0);
+    return launch_check();
+}
+
+int launch_jtr(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs) {
+    if (n <= PNOL_SEQ_MAX && m <= 4096) return launch_gemv_neg_seq(ctx, JT, ldjt, n, m, F, rhs);
+    return launch_gemv_neg(ctx, JT, ldjt, n, m, F, rhs);
+}
+
+}  // namespace pnol

@@ -1,0 +1,133 @@
+// pnol_internal.hpp -- runtime internals shared by the HIP kernels, the C ABI and the
+// C++ drop-in classes.  Not installed; the public surface is include/pnol_amd.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "pnol_amd.h"
+
+namespace pnol {
+
+// Scratch buffers keyed by purpose; grown on demand, never shrunk, freed with the context.
+// Allocation happens outside any capturable region (first use of a size), so repeated
+// solver iterations allocate nothing.
+struct Workspace {
+    std::map<std::string, std::pair<void*, size_t>> bufs;
+};
+
+}  // namespace pnol
+
+namespace pnol {
+// start/stop event pairs per kernel name, resolved lazily (pnol_ctx_timer)
+struct Timers {
+    bool on = false;
+    std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> pending;
+    std::map<std::string, std::pair<double, int>> done;
+};
+}  // namespace pnol
+
+struct pnol_ctx {
+    int device = 0;
+    pnol::Timers timers;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;   // active stream (own or caller-provided)
+    int num_cu = 0;
+    pnol::Workspace ws;
+    double* pinned = nullptr;       // small host staging buffer (scalars back from the device)
+    size_t pinned_bytes = 0;
+};
+
+struct pnol_dobj {
+    int kind = 0;
+    int n = 0;
+    int m = 0;
+    double power = 2.0;
+    double* p0 = nullptr;     // device data (see pnol_dobj_kind)
+    double* p1 = nullptr;
+    double* p2 = nullptr;     // derived device data (e.g. pow(xData,3) for the cubic)
+    size_t len0 = 0, len1 = 0;
+    pnol_ctx* ctx = nullptr;
+};
+
+namespace pnol {
+
+#define PNOL_HIP(expr)                                                                       \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) {                                                              \
+            std::fprintf(stderr, "[pnol_amd] HIP error %s at %s:%d: %s\n", hipGetErrorName(e_), \
+                         __FILE__, __LINE__, #expr);                                          \
+            return PNOL_ERR_HIP;                                                             \
+        }                                                                                    \
+    } while (0)
+
+#define PNOL_CHECK(expr)             \
+    do {                             \
+        int s_ = (expr);             \
+        if (s_ != PNOL_OK) return s_; \
+    } while (0)
+
+// Returns a device scratch buffer of at least `bytes` for `key` (grows, keeps contents undefined).
+int ws_get(pnol_ctx* ctx, const char* key, size_t bytes, void** out);
+
+// Scoped timer: records a start event now and a stop event at scope exit (when enabled).
+class ScopedTimer {
+  public:
+    ScopedTimer(pnol_ctx* ctx, const char* name);
+    ~ScopedTimer();
+  private:
+    pnol_ctx* ctx_;
+    const char* name_;
+    hipEvent_t a_ = nullptr, b_ = nullptr;
+};
+
+// Launch-error check after a kernel launch.
+inline int launch_check() {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "[pnol_amd] kernel launch failed: %s\n", hipGetErrorString(e));
+        return PNOL_ERR_HIP;
+    }
+    return PNOL_OK;
+}
+
+// ---- kernel launchers (defined in kernels/*.hip) ------------------------------------
+int launch_gemv_neg(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y);
+int launch_gemv_neg_seq(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y);
+int launch_bfgs_update_exact(pnol_ctx* ctx, double* D, int ldd, const double* y, const double* s, int n);
+int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p, const double* a_p,
+                     const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
+                     double* v);
+int launch_set_identity(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale);
+
+int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
+               double* jtj_diag);
+int launch_jtr(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
+// C(lower tiles of rows [r0, r0+nr)) = beta*C + alpha * X X^T  over K columns (MFMA)
+int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, double alpha, double* C,
+                      int ldc, int split_k);
+
+int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n, int method,
+                 int* info);
+
+int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
+int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt,
+                       double* f0, double* g);
+int launch_fd_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int j0, int cnt,
+                       double* F0, int compute_f0, double* JT, int ldjt);
+int launch_synthetic_quadratic(pnol_ctx* ctx, unsigned long long seed, int n, double bscale, double* d, double* b);
+int launch_synthetic_linres(pnol_ctx* ctx, unsigned long long seed, int m, int n, double* A, double* xstar,
+                            double* y);
+int launch_fill(pnol_ctx* ctx, double* p, size_t count, double value);
+
+// number of XCDs (8 on MI355X): used only for blockIdx -> tile remaps (speed, never correctness)
+constexpr int kNumXcd = 8;
+
+}  // namespace pnol

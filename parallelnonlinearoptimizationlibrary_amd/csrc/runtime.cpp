@@ -1,0 +1,366 @@
+// runtime.cpp -- contexts, device memory, workspace and the communicator behind the C ABI.
+//
+// The communicator replaces MPI_COMM_WORLD on the paths the reference distributes
+// (PNOL_Objective.cpp:101-103, 147-148, 226-228, 279-288; BFGS_with_linesearch_MPI.cpp:167-210):
+// RCCL (one process per GPU, xGMI) or a caller-supplied host allgather (tests / host objectives).
+#include <rccl/rccl.h>
+
+#include <cstdlib>
+#include <cstring>
+
+#include "pnol_comm.hpp"
+#include "pnol_internal.hpp"
+
+namespace pnol {
+
+int ws_get(pnol_ctx* ctx, const char* key, size_t bytes, void** out) {
+    if (!ctx || !out) return PNOL_ERR_ARG;
+    auto& slot = ctx->ws.bufs[key];
+    if (slot.second < bytes) {
+        if (slot.first) {
+            PNOL_HIP(hipStreamSynchronize(ctx->stream));
+            PNOL_HIP(hipFree(slot.first));
+            slot.first = nullptr;
+            slot.second = 0;
+        }
+        size_t sz = bytes < 256 ? 256 : bytes;
+        if (hipMalloc(&slot.first, sz) != hipSuccess) {
+            slot.first = nullptr;
+            return PNOL_ERR_NOMEM;
+        }
+        slot.second = sz;
+    }
+    *out = slot.first;
+    return PNOL_OK;
+}
+
+static bool is_gfx950(int dev) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// communicator
+// ---------------------------------------------------------------------------------------
+struct CommState {
+    int kind = 0;   // 0 none (single process), 1 rccl, 2 host callback
+    int nranks = 1, rank = 0;
+    ncclComm_t nccl = nullptr;
+    pnol_ctx* ctx = nullptr;
+    pnol_host_allgather_fn fn = nullptr;
+    void* user = nullptr;
+};
+static CommState g_comm;
+
+int comm_size() { return g_comm.nranks; }
+int comm_rank() { return g_comm.rank; }
+
+void block_range(int ncols, int nranks, int rank, int* begin, int* count) {
+    // ceil-sized contiguous blocks: the padded allgather buffer is then the row-major JT itself
+    int per = (ncols + nranks - 1) / nranks;
+    int b = rank * per;
+    if (b > ncols) b = ncols;
+    int e = b + per;
+    if (e > ncols) e = ncols;
+    *begin = b;
+    *count = e - b;
+}
+
+int comm_allgather_host(pnol_ctx* ctx, const double* send, double* recv, size_t count) {
+    if (g_comm.kind == 0) {
+        std::memcpy(recv, send, sizeof(double) * count);
+        return PNOL_OK;
+    }
+    if (g_comm.kind == 2) return g_comm.fn(send, recv, sizeof(double) * count, g_comm.user) == 0 ? PNOL_OK : PNOL_ERR_COMM;
+    // RCCL: stage through device scratch
+    if (!ctx) ctx = g_comm.ctx;
+    void *ds = nullptr, *dr = nullptr;
+    PNOL_CHECK(ws_get(ctx, "comm_send", sizeof(double) * count, &ds));
+    PNOL_CHECK(ws_get(ctx, "comm_recv", sizeof(double) * count * g_comm.nranks, &dr));
+    PNOL_HIP(hipMemcpyAsync(ds, send, sizeof(double) * count, hipMemcpyHostToDevice, ctx->stream));
+    PNOL_CHECK(comm_allgather_device(ctx, (const double*)ds, (double*)dr, count));
+    PNOL_HIP(hipMemcpyAsync(recv, dr, sizeof(double) * count * g_comm.nranks, hipMemcpyDeviceToHost, ctx->stream));
+    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    return PNOL_OK;
+}
+
+int comm_allgather_device(pnol_ctx* ctx, const double* send, double* recv, size_t count) {
+    if (g_comm.kind == 0) {
+        if (send != recv)
+            PNOL_HIP(hipMemcpyAsync(recv, send, sizeof(double) * count, hipMemcpyDeviceToDevice, ctx->stream));
+        return PNOL_OK;
+    }
+    if (g_comm.kind == 1) {
+        ScopedTimer tm(ctx, "allgather");
+        if (ncclAllGather(send, recv, count, ncclDouble, g_comm.nccl, ctx->stream) != ncclSuccess) return PNOL_ERR_COMM;
+        return PNOL_OK;
+    }
+    // host backend with device buffers: bounce through host memory
+    std::vector<double> hs(count), hr(count * (size_t)g_comm.nranks);
+    PNOL_HIP(hipMemcpyAsync(hs.data(), send, sizeof(double) * count, hipMemcpyDeviceToHost, ctx->stream));
+    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    if (g_comm.fn(hs.data(), hr.data(), sizeof(double) * count, g_comm.user) != 0) return PNOL_ERR_COMM;
+    PNOL_HIP(hipMemcpyAsync(recv, hr.data(), sizeof(double) * hr.size(), hipMemcpyHostToDevice, ctx->stream));
+    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    return PNOL_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// kernel timers
+// ---------------------------------------------------------------------------------------
+ScopedTimer::ScopedTimer(pnol_ctx* ctx, const char* name) : ctx_(ctx), name_(name) {
+    if (!ctx_ || !ctx_->timers.on) return;
+    if (hipEventCreate(&a_) != hipSuccess || hipEventCreate(&b_) != hipSuccess) { a_ = b_ = nullptr; return; }
+    (void)hipEventRecord(a_, ctx_->stream);
+}
+
+ScopedTimer::~ScopedTimer() {
+    if (!a_) return;
+    (void)hipEventRecord(b_, ctx_->stream);
+    ctx_->timers.pending[name_].push_back({a_, b_});
+}
+
+static void resolve_timers(pnol_ctx* ctx) {
+    for (auto& kv : ctx->timers.pending) {
+        auto& acc = ctx->timers.done[kv.first];
+        for (auto& ev : kv.second) {
+            float ms = 0.f;
+            (void)hipEventSynchronize(ev.second);
+            if (hipEventElapsedTime(&ms, ev.first, ev.second) == hipSuccess) {
+                acc.first += ms;
+                acc.second += 1;
+            }
+            (void)hipEventDestroy(ev.first);
+            (void)hipEventDestroy(ev.second);
+        }
+        kv.second.clear();
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// default context for the C++ drop-in classes
+// ---------------------------------------------------------------------------------------
+static pnol_ctx* g_default = nullptr;
+static std::mutex g_default_mu;
+
+pnol_ctx* default_ctx_or_null() {
+    std::lock_guard<std::mutex> lk(g_default_mu);
+    if (g_default) return g_default;
+    int count = 0;
+    if (pnol_device_count(&count) != PNOL_OK || count == 0) return nullptr;
+    int dev = 0;
+    if (const char* e = std::getenv("PNOL_DEVICE")) dev = std::atoi(e);
+    else if (const char* l = std::getenv("LOCAL_RANK")) dev = std::atoi(l) % count;
+    pnol_ctx* c = nullptr;
+    if (pnol_ctx_create(dev, &c) != PNOL_OK) return nullptr;
+    g_default = c;
+    return g_default;
+}
+
+}  // namespace pnol
+
+using namespace pnol;
+
+extern "C" {
+
+const char* pnol_status_string(int s) {
+    switch (s) {
+        case PNOL_OK: return "ok";
+        case PNOL_ERR_ARG: return "invalid argument";
+        case PNOL_ERR_HIP: return "HIP runtime error";
+        case PNOL_ERR_NOMEM: return "out of device memory";
+        case PNOL_ERR_NODEVICE: return "no gfx950 (MI355X) device visible";
+        case PNOL_ERR_SINGULAR: return "singular system";
+        case PNOL_ERR_COMM: return "communicator error";
+        case PNOL_ERR_UNSUPPORTED: return "unsupported";
+        default: return "unknown status";
+    }
+}
+
+int pnol_version(void) { return PNOL_AMD_VERSION; }
+
+int pnol_device_count(int* count) {
+    if (!count) return PNOL_ERR_ARG;
+    *count = 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return PNOL_OK;
+    int c = 0;
+    for (int d = 0; d < n; ++d)
+        if (is_gfx950(d)) ++c;
+    *count = c;
+    return PNOL_OK;
+}
+
+int pnol_ctx_create(int device, pnol_ctx** out) {
+    if (!out) return PNOL_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n || !is_gfx950(device))
+        return PNOL_ERR_NODEVICE;
+    PNOL_HIP(hipSetDevice(device));
+    auto* c = new pnol_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return PNOL_ERR_HIP;
+    }
+    c->stream = c->own_stream;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cu = prop.multiProcessorCount;
+    *out = c;
+    return PNOL_OK;
+}
+
+int pnol_ctx_destroy(pnol_ctx* ctx) {
+    if (!ctx) return PNOL_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->ws.bufs)
+        if (kv.second.first) (void)hipFree(kv.second.first);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    if (ctx == g_default) g_default = nullptr;
+    delete ctx;
+    return PNOL_OK;
+}
+
+int pnol_ctx_synchronize(pnol_ctx* ctx) {
+    if (!ctx) return PNOL_ERR_ARG;
+    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    return PNOL_OK;
+}
+
+int pnol_ctx_get_stream(pnol_ctx* ctx, void** s) {
+    if (!ctx || !s) return PNOL_ERR_ARG;
+    *s = (void*)ctx->stream;
+    return PNOL_OK;
+}
+
+int pnol_ctx_set_stream(pnol_ctx* ctx, void* s) {
+    if (!ctx) return PNOL_ERR_ARG;
+    ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+    return PNOL_OK;
+}
+
+int pnol_ctx_device(pnol_ctx* ctx, int* device) {
+    if (!ctx || !device) return PNOL_ERR_ARG;
+    *device = ctx->device;
+    return PNOL_OK;
+}
+
+int pnol_default_ctx(pnol_ctx** out) {
+    if (!out) return PNOL_ERR_ARG;
+    *out = default_ctx_or_null();
+    return *out ? PNOL_OK : PNOL_ERR_NODEVICE;
+}
+
+int pnol_ctx_enable_timers(pnol_ctx* ctx, int on) {
+    if (!ctx) return PNOL_ERR_ARG;
+    ctx->timers.on = on != 0;
+    return PNOL_OK;
+}
+
+int pnol_ctx_reset_timers(pnol_ctx* ctx) {
+    if (!ctx) return PNOL_ERR_ARG;
+    resolve_timers(ctx);
+    ctx->timers.done.clear();
+    return PNOL_OK;
+}
+
+int pnol_ctx_timer(pnol_ctx* ctx, const char* name, double* total_ms, int* count) {
+    if (!ctx || !name) return PNOL_ERR_ARG;
+    resolve_timers(ctx);
+    auto it = ctx->timers.done.find(name);
+    if (total_ms) *total_ms = it == ctx->timers.done.end() ? 0.0 : it->second.first;
+    if (count) *count = it == ctx->timers.done.end() ? 0 : it->second.second;
+    return PNOL_OK;
+}
+
+int pnol_malloc(pnol_ctx* ctx, size_t bytes, void** dptr) {
+    if (!ctx || !dptr) return PNOL_ERR_ARG;
+    PNOL_HIP(hipSetDevice(ctx->device));
+    if (hipMalloc(dptr, bytes ? bytes : 16) != hipSuccess) return PNOL_ERR_NOMEM;
+    return PNOL_OK;
+}
+
+int pnol_free(pnol_ctx* ctx, void* dptr) {
+    if (!ctx) return PNOL_ERR_ARG;
+    if (dptr) PNOL_HIP(hipFree(dptr));
+    return PNOL_OK;
+}
+
+int pnol_memcpy_h2d(pnol_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!ctx || (!dst && bytes) || (!src && bytes)) return PNOL_ERR_ARG;
+    if (!bytes) return PNOL_OK;
+    PNOL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    return PNOL_OK;
+}
+
+int pnol_memcpy_d2h(pnol_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!ctx || (!dst && bytes) || (!src && bytes)) return PNOL_ERR_ARG;
+    if (!bytes) return PNOL_OK;
+    PNOL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    return PNOL_OK;
+}
+
+int pnol_comm_unique_id(char id[128]) {
+    if (!id) return PNOL_ERR_ARG;
+    static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return PNOL_ERR_COMM;
+    std::memcpy(id, &u, 128);
+    return PNOL_OK;
+}
+
+int pnol_comm_init_rccl(pnol_ctx* ctx, int nranks, int rank, const char id[128]) {
+    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return PNOL_ERR_ARG;
+    pnol_comm_finalize();
+    PNOL_HIP(hipSetDevice(ctx->device));
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    ncclComm_t c;
+    if (ncclCommInitRank(&c, nranks, u, rank) != ncclSuccess) return PNOL_ERR_COMM;
+    g_comm.kind = 1;
+    g_comm.nranks = nranks;
+    g_comm.rank = rank;
+    g_comm.nccl = c;
+    g_comm.ctx = ctx;
+    return PNOL_OK;
+}
+
+int pnol_comm_init_host(int nranks, int rank, pnol_host_allgather_fn fn, void* user) {
+    if (!fn || nranks < 1 || rank < 0 || rank >= nranks) return PNOL_ERR_ARG;
+    pnol_comm_finalize();
+    g_comm.kind = 2;
+    g_comm.nranks = nranks;
+    g_comm.rank = rank;
+    g_comm.fn = fn;
+    g_comm.user = user;
+    return PNOL_OK;
+}
+
+int pnol_comm_finalize(void) {
+    if (g_comm.kind == 1 && g_comm.nccl) ncclCommDestroy(g_comm.nccl);
+    g_comm = CommState();
+    return PNOL_OK;
+}
+
+int pnol_comm_size(int* nranks, int* rank) {
+    if (!nranks || !rank) return PNOL_ERR_ARG;
+    *nranks = g_comm.nranks;
+    *rank = g_comm.rank;
+    return PNOL_OK;
+}
+
+int pnol_comm_allgather_d(pnol_ctx* ctx, const double* send, double* recv, size_t count) {
+    if (!ctx || !send || !recv) return PNOL_ERR_ARG;
+    return comm_allgather_device(ctx, send, recv, count);
+}
+
+void pnol_block_range(int ncols, int nranks, int rank, int* begin, int* count) {
+    block_range(ncols, nranks, rank, begin, count);
+}
+
+}  // extern "C"

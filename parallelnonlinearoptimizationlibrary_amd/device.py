@@ -1,0 +1,208 @@
+"""Torch-facing wrappers over the C ABI (device buffers are torch float64 CUDA tensors).
+
+PyTorch supplies device memory and the stream (the context runs on torch's current stream,
+so launches are ordered with torch ops); every kernel is the library's own HIP code.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+def _ptr(t) -> C.c_void_p:
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+def _dptr(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class Context:
+    """One GPU (pnol_ctx) bound to torch's current stream on that device."""
+
+    def __init__(self, device: int = 0, use_torch_stream: bool = True):
+        import torch
+        self.torch = torch
+        self.device = device
+        h = C.c_void_p()
+        L.check(L.lib().pnol_ctx_create(device, C.byref(h)), "pnol_ctx_create")
+        self.h = h
+        if use_torch_stream:
+            with torch.cuda.device(device):
+                s = torch.cuda.current_stream().cuda_stream
+            L.check(L.lib().pnol_ctx_set_stream(self.h, C.c_void_p(s)), "pnol_ctx_set_stream")
+
+    def close(self):
+        if self.h:
+            L.lib().pnol_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def synchronize(self):
+        L.check(L.lib().pnol_ctx_synchronize(self.h), "pnol_ctx_synchronize")
+
+    def stream(self) -> int:
+        s = C.c_void_p()
+        L.check(L.lib().pnol_ctx_get_stream(self.h, C.byref(s)), "pnol_ctx_get_stream")
+        return s.value or 0
+
+    # ---- tensors ------------------------------------------------------------------
+    def empty(self, *shape):
+        return self.torch.empty(*shape, dtype=self.torch.float64, device=f"cuda:{self.device}")
+
+    def tensor(self, a):
+        return self.torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64)).to(f"cuda:{self.device}")
+
+    # ---- kernels ------------------------------------------------------------------
+    def hg(self, D, g, p=None):
+        """p = -D g (BFGS_with_linesearch.cpp:78-79)."""
+        n = g.numel()
+        p = self.empty(n) if p is None else p
+        L.check(L.lib().pnol_hg_d(self.h, _ptr(D), D.stride(0), _ptr(g), _ptr(p), n), "pnol_hg_d")
+        return p
+
+    def gemv_neg(self, A, x, y=None):
+        rows, cols = A.shape
+        y = self.empty(rows) if y is None else y
+        L.check(L.lib().pnol_gemv_neg_d(self.h, _ptr(A), A.stride(0), rows, cols, _ptr(x), _ptr(y)), "pnol_gemv_neg_d")
+        return y
+
+    def bfgs_update_exact(self, D, y, s):
+        L.check(L.lib().pnol_bfgs_update_exact_d(self.h, _ptr(D), D.stride(0), _ptr(y), _ptr(s), y.numel()),
+                "pnol_bfgs_update_exact_d")
+        return D
+
+    def bfgs_pass(self, D, y=None, g=None, pending=None, write_back=False):
+        """One streaming pass; returns (u, w, v) = (Dc y, Dc^T y, Dc g)."""
+        n = D.shape[0]
+        u, w, v = self.empty(n), self.empty(n), self.empty(n)
+        sp, ap, bp = pending if pending is not None else (None, None, None)
+        L.check(L.lib().pnol_bfgs_pass_d(self.h, _ptr(D), D.stride(0), n, _ptr(sp), _ptr(ap), _ptr(bp),
+                                         int(write_back), _ptr(y), _ptr(g), _ptr(u), _ptr(w), _ptr(v)),
+                "pnol_bfgs_pass_d")
+        return u, w, v
+
+    def set_identity(self, D, scale=None):
+        L.check(L.lib().pnol_set_identity_d(self.h, _ptr(D), D.stride(0), D.shape[0], _ptr(scale)),
+                "pnol_set_identity_d")
+        return D
+
+    def jtj(self, JT, lam, A=None, want_diag=False):
+        """A = J^T J with A_ii *= (1+lam); JT is n x m (one FD column per row)."""
+        n, m = JT.shape
+        A = self.empty(n, n) if A is None else A
+        diag = self.empty(n) if want_diag else None
+        L.check(L.lib().pnol_jtj_d(self.h, _ptr(JT), JT.stride(0), m, n, C.c_double(lam), _ptr(A), A.stride(0),
+                                   _ptr(diag)), "pnol_jtj_d")
+        return (A, diag) if want_diag else A
+
+    def jtr(self, JT, F, rhs=None):
+        n, m = JT.shape
+        rhs = self.empty(n) if rhs is None else rhs
+        L.check(L.lib().pnol_jtr_d(self.h, _ptr(JT), JT.stride(0), m, n, _ptr(F), _ptr(rhs)), "pnol_jtr_d")
+        return rhs
+
+    def solve(self, A, rhs, method=0):
+        """sigma = A^{-1} rhs; A is overwritten.  Returns (sigma, info)."""
+        n = rhs.numel()
+        sigma = self.empty(n)
+        info = C.c_int(0)
+        L.check(L.lib().pnol_solve_d(self.h, _ptr(A), A.stride(0), _ptr(rhs), _ptr(sigma), n, method,
+                                     C.byref(info)), "pnol_solve_d")
+        return sigma, info.value
+
+
+class DeviceObjective:
+    """A pnol_dobj: a built-in objective whose FD batches run on the device."""
+
+    def __init__(self, ctx: Context, kind: int, n: int, m: int = 0, p0=None, p1=None, power: float = 2.0,
+                 handle=None):
+        self.ctx, self.kind, self.n, self.m = ctx, kind, n, m
+        if handle is not None:
+            self.h = handle
+            return
+        a0 = None if p0 is None else np.ascontiguousarray(p0, dtype=np.float64).ravel()
+        a1 = None if p1 is None else np.ascontiguousarray(p1, dtype=np.float64).ravel()
+        h = C.c_void_p()
+        L.check(L.lib().pnol_dobj_create(ctx.h, kind, n, m, _dptr(a0) if a0 is not None else None,
+                                         0 if a0 is None else a0.size, _dptr(a1) if a1 is not None else None,
+                                         0 if a1 is None else a1.size, C.c_double(power), C.byref(h)),
+                "pnol_dobj_create")
+        self.h = h
+
+    @classmethod
+    def synthetic(cls, ctx: Context, kind: int, n: int, m: int = 0, seed: int = 0x5EED2018, bscale: float = 1.0):
+        h = C.c_void_p()
+        xs = np.zeros(n)
+        L.check(L.lib().pnol_dobj_create_synthetic(ctx.h, kind, n, m, C.c_ulonglong(seed), C.c_double(bscale),
+                                                   _dptr(xs), C.byref(h)), "pnol_dobj_create_synthetic")
+        o = cls(ctx, kind, n, m, handle=h)
+        o.xstar = xs
+        return o
+
+    def close(self):
+        if getattr(self, "h", None):
+            L.lib().pnol_dobj_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def eval(self, x):
+        out = self.ctx.empty(self.m if self.m else 1)
+        L.check(L.lib().pnol_dobj_eval_d(self.ctx.h, self.h, _ptr(x), _ptr(out)), "pnol_dobj_eval_d")
+        return out
+
+    def fd_gradient(self, x, h, i0=0, cnt=None):
+        cnt = self.n - i0 if cnt is None else cnt
+        f0, g = self.ctx.empty(1), self.ctx.empty(max(cnt, 1))
+        L.check(L.lib().pnol_fd_gradient_d(self.ctx.h, self.h, _ptr(x), _ptr(h), i0, cnt, _ptr(f0), _ptr(g)),
+                "pnol_fd_gradient_d")
+        return f0, g[:cnt]
+
+    def fd_jacobian(self, x, h, j0=0, cnt=None, JT=None, F0=None, compute_f0=True):
+        """JT rows = FD columns j0..j0+cnt; returns (F0, JT)."""
+        cnt = self.n - j0 if cnt is None else cnt
+        JT = self.ctx.empty(max(cnt, 1), self.m) if JT is None else JT
+        F0 = self.ctx.empty(self.m) if F0 is None else F0
+        L.check(L.lib().pnol_fd_jacobian_d(self.ctx.h, self.h, _ptr(x), _ptr(h), j0, cnt, _ptr(F0),
+                                           int(compute_f0), _ptr(JT), JT.stride(0)), "pnol_fd_jacobian_d")
+        return F0, JT
+
+
+def run_bfgs(obj: DeviceObjective, x0, params, which=0, host_eval=False, lb=None, ub=None):
+    """Run the C++ drop-in BFGS (0), BFGS_MPI (1) or BFGS_Bnd (2) on a device objective."""
+    X = np.array(x0, dtype=np.float64)
+    p = np.array(params, dtype=np.float64)
+    res = L.Result()
+    lbp = _dptr(np.ascontiguousarray(lb, dtype=np.float64)) if lb is not None else None
+    ubp = _dptr(np.ascontiguousarray(ub, dtype=np.float64)) if ub is not None else None
+    lba = np.ascontiguousarray(lb, dtype=np.float64) if lb is not None else None
+    uba = np.ascontiguousarray(ub, dtype=np.float64) if ub is not None else None
+    L.check(L.lib().pnol_run_bfgs(which, obj.h, int(host_eval), _dptr(p), p.size, _dptr(X), X.size,
+                                  _dptr(lba) if lba is not None else lbp, _dptr(uba) if uba is not None else ubp,
+                                  C.byref(res)), "pnol_run_bfgs")
+    return X, res
+
+
+def run_levmarq(obj: DeviceObjective, x0, params, which=0, host_eval=False):
+    """Run the C++ drop-in LevMarq (0) or LevMarqMPI (1); returns (X, F0, FOpt, result)."""
+    X = np.array(x0, dtype=np.float64)
+    p = np.array(params, dtype=np.float64)
+    F0, FO = np.zeros(obj.m), np.zeros(obj.m)
+    res = L.Result()
+    L.check(L.lib().pnol_run_levmarq(which, obj.h, int(host_eval), _dptr(p), _dptr(X), X.size, _dptr(F0), _dptr(FO),
+                                     obj.m, C.byref(res)), "pnol_run_levmarq")
+    return X, F0, FO, res

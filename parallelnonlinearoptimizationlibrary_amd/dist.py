@@ -1,0 +1,59 @@
+"""RCCL communicator bootstrap for the *_MPI drop-ins: one process per GPU.
+
+torch.distributed (launched by torch.distributed.run) only carries the 128-byte RCCL unique
+id from rank 0 to the others; every data-path collective afterwards is the library's own
+ncclAllGather on its stream.  For CPU tests the host backend takes a Python allgather
+(torch.distributed over gloo) instead.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import _lib as L
+
+
+def env_rank_world():
+    return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), \
+        int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def init_rccl(ctx, rank: int, world: int):
+    """Create the library's RCCL communicator; torch.distributed must be initialised."""
+    import torch
+    import torch.distributed as dist
+    buf = C.create_string_buffer(128)
+    if rank == 0:
+        L.check(L.lib().pnol_comm_unique_id(buf), "pnol_comm_unique_id")
+    t = torch.tensor(list(buf.raw), dtype=torch.uint8)
+    if dist.get_backend() == "nccl":
+        t = t.cuda()
+    dist.broadcast(t, src=0)
+    raw = bytes(t.cpu().tolist())
+    L.check(L.lib().pnol_comm_init_rccl(ctx.h, world, rank, raw), "pnol_comm_init_rccl")
+
+
+class HostComm:
+    """Host-backend communicator: allgather of raw bytes through torch.distributed (gloo)."""
+
+    def __init__(self, rank: int, world: int):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.world = torch, dist, world
+
+        def _allgather(send, recv, nbytes, user):
+            try:
+                src = (C.c_uint8 * nbytes).from_address(send)
+                t = torch.frombuffer(bytearray(src), dtype=torch.uint8)
+                outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
+                dist.all_gather(outs, t)
+                C.memmove(recv, bytes(torch.cat(outs).numpy()), nbytes * world)
+                return 0
+            except Exception:  # pragma: no cover - surfaces as PNOL_ERR_COMM
+                return 1
+
+        self._cb = L.ALLGATHER_FN(_allgather)
+        L.check(L.lib().pnol_comm_init_host(world, rank, self._cb, None), "pnol_comm_init_host")
+
+    def close(self):
+        L.lib().pnol_comm_finalize()

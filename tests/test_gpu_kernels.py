@@ -1,0 +1,292 @@
+"""Kernel-level parity of the HIP path against the CPU oracle (and numpy fp64 where the
+reference order is not the contract).  Run on an MI355X: pytest -m gpu.
+
+Tolerances: 'bitwise' where the kernel follows the reference operation order (n <=
+PNOL_SEQ_MAX paths, FD batches of transcendental-free objectives, the exact BFGS update,
+the reference-order LU); otherwise |err| <= 8 eps * sum|a_i b_i| per reduced entry (a
+reordered fp64 sum), written out per test.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EPS = np.finfo(np.float64).eps
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import Context
+    if L.device_count() < 1:
+        pytest.fail("no gfx950 device visible for a -m gpu run")
+    return Context(0)
+
+
+def _reorder_tol(A, x):
+    return 8 * EPS * (np.abs(A) @ np.abs(x)) + 1e-300
+
+
+def _np(t):
+    return t.cpu().numpy()
+
+
+# ---- H.g ---------------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [1, 2, 5, 64])
+def test_hg_small_bitwise(ctx, oracle, n):
+    rng = np.random.default_rng(n)
+    D = rng.standard_normal((n, n)); g = rng.standard_normal(n)
+    p = _np(ctx.hg(ctx.tensor(D), ctx.tensor(g)))
+    assert np.array_equal(p, -oracle.matvec(D, g))
+
+
+@pytest.mark.parametrize("n", [65, 300, 1023, 4099, 8192])
+def test_hg_large(ctx, n):
+    rng = np.random.default_rng(n)
+    D = rng.standard_normal((n, n)); g = rng.standard_normal(n)
+    p = _np(ctx.hg(ctx.tensor(D), ctx.tensor(g)))
+    assert np.all(np.abs(p + D @ g) <= _reorder_tol(D, g))
+
+
+def test_hg_padded_leading_dimension(ctx):
+    rng = np.random.default_rng(3)
+    n, ld = 301, 320
+    big = rng.standard_normal((n, ld))
+    Dt = ctx.tensor(big)[:, :n]
+    g = rng.standard_normal(n)
+    p = _np(ctx.hg(Dt, ctx.tensor(g)))
+    D = big[:, :n]
+    assert np.all(np.abs(p + D @ g) <= _reorder_tol(D, g))
+
+
+@pytest.mark.parametrize("rows,cols", [(2048, 16384), (7, 1001), (4096, 33), (9000, 256)])
+def test_gemv_neg_rectangular(ctx, rows, cols):
+    rng = np.random.default_rng(rows + cols)
+    A = rng.standard_normal((rows, cols)); x = rng.standard_normal(cols)
+    y = _np(ctx.gemv_neg(ctx.tensor(A), ctx.tensor(x)))
+    assert np.all(np.abs(y + A @ x) <= _reorder_tol(A, x))
+
+
+# ---- BFGS update ---------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [1, 3, 8, 64, 100])
+def test_bfgs_update_exact_bitwise(ctx, oracle, n):
+    rng = np.random.default_rng(10 + n)
+    D = np.eye(n) + 0.1 * rng.standard_normal((n, n))
+    y = rng.standard_normal(n); s = rng.standard_normal(n)
+    Dt = ctx.tensor(D)
+    ctx.bfgs_update_exact(Dt, ctx.tensor(y), ctx.tensor(s))
+    assert np.array_equal(_np(Dt), oracle.update_hessian_inv(D, y, s))
+
+
+@pytest.mark.parametrize("n", [1, 7, 300, 513, 1030])
+@pytest.mark.parametrize("pending,wb", [(False, False), (True, True), (True, False)])
+def test_bfgs_pass(ctx, n, pending, wb):
+    rng = np.random.default_rng(n * 7 + pending + 2 * wb)
+    D = rng.standard_normal((n, n)); y = rng.standard_normal(n); g = rng.standard_normal(n)
+    sp, ap, bp = rng.standard_normal(n), rng.standard_normal(n), rng.standard_normal(n)
+    Dt = ctx.tensor(D)
+    pend = (ctx.tensor(sp), ctx.tensor(ap), ctx.tensor(bp)) if pending else None
+    u, w, v = (_np(t) for t in ctx.bfgs_pass(Dt, ctx.tensor(y), ctx.tensor(g), pend, wb))
+    Dc = D + np.outer(sp, ap) + np.outer(bp, sp) if pending else D
+    assert np.all(np.abs(u - Dc @ y) <= _reorder_tol(Dc, y) + 4 * EPS * np.abs(Dc).max() * np.abs(y).sum())
+    assert np.all(np.abs(v - Dc @ g) <= _reorder_tol(Dc, g) + 4 * EPS * np.abs(Dc).max() * np.abs(g).sum())
+    assert np.all(np.abs(w - Dc.T @ y) <= _reorder_tol(Dc.T, y) + 4 * EPS * np.abs(Dc).max() * np.abs(y).sum())
+    Dafter = _np(Dt)
+    if wb:
+        assert np.allclose(Dafter, Dc, rtol=4 * EPS, atol=4 * EPS * np.abs(Dc).max())
+    else:
+        assert np.array_equal(Dafter, D)
+
+
+def test_fused_update_sequence_matches_reference_form(ctx, oracle):
+    """Three lazy rank-2 updates (the fast mode's algebra) vs the reference O(n^3) form."""
+    rng = np.random.default_rng(5)
+    n = 257
+    Dref = np.eye(n)
+    Dt = ctx.tensor(np.eye(n))
+    pend = None
+    for it in range(3):
+        y = rng.standard_normal(n); s = rng.standard_normal(n) + 0.5 * y
+        u, w, _ = (_np(t) for t in ctx.bfgs_pass(Dt, ctx.tensor(y), None, pend, pend is not None))
+        rho = 1 / np.dot(y, s); beta = np.dot(y, u); c = rho * rho * beta + rho
+        a = c * s - rho * w; b = -rho * u
+        pend = (ctx.tensor(s), ctx.tensor(a), ctx.tensor(b))
+        Dref = oracle.update_hessian_inv(Dref, y, s)
+    ctx.bfgs_pass(Dt, None, None, pend, True)
+    assert np.allclose(_np(Dt), Dref, rtol=1e-11, atol=1e-11 * np.abs(Dref).max())
+
+
+def test_set_identity(ctx):
+    Dt = ctx.tensor(np.full((9, 9), 3.0))
+    ctx.set_identity(Dt)
+    assert np.array_equal(_np(Dt), np.eye(9))
+    scale = np.arange(1.0, 10.0)
+    ctx.set_identity(Dt, ctx.tensor(scale))
+    assert np.array_equal(_np(Dt), np.diag(scale))
+
+
+# ---- LM linear algebra ---------------------------------------------------------------------
+@pytest.mark.parametrize("m,n", [(100, 3), (100, 4), (4096, 64)])
+def test_jtj_small_bitwise(ctx, oracle, m, n):
+    rng = np.random.default_rng(m + n)
+    J = rng.standard_normal((m, n)); F = rng.standard_normal(m); lam = 0.01
+    JTJ, A, rhs, _ = oracle.lm_step(J, F, lam)
+    JT = ctx.tensor(J.T.copy())
+    Ad, diag = ctx.jtj(JT, lam, want_diag=True)
+    assert np.array_equal(_np(Ad), A)
+    assert np.array_equal(_np(diag), np.diag(JTJ))
+    assert np.array_equal(_np(ctx.jtr(JT, ctx.tensor(F))), rhs)
+
+
+@pytest.mark.parametrize("m,n", [(1000, 65), (2000, 130), (3001, 300), (16384, 2048), (513, 1000)])
+def test_jtj_mfma(ctx, m, n):
+    rng = np.random.default_rng(m * 3 + n)
+    J = rng.standard_normal((m, n)) / np.sqrt(n)
+    lam = 1e-3
+    Ad, diag = ctx.jtj(ctx.tensor(J.T.copy()), lam, want_diag=True)
+    A = _np(Ad)
+    ref = J.T @ J
+    tol = 8 * EPS * (np.abs(J).T @ np.abs(J)) * max(1, np.log2(m))
+    off = ~np.eye(n, dtype=bool)
+    assert np.all(np.abs(A - ref)[off] <= tol[off])
+    assert np.all(np.abs(np.diag(A) - (1 + lam) * np.diag(ref)) <= 2 * np.diag(tol))
+    assert np.array_equal(A, A.T)   # mirrored: exactly symmetric, like the reference's JT J
+    assert np.all(np.abs(_np(diag) - np.diag(ref)) <= np.diag(tol))
+
+
+def test_jtj_mfma_layout_asymmetric(ctx):
+    """Integer-valued J: the MFMA result is exact, so any row/col slip in the C/D layout shows."""
+    rng = np.random.default_rng(11)
+    m, n = 256, 160
+    J = rng.integers(-3, 4, size=(m, n)).astype(np.float64)
+    A = _np(ctx.jtj(ctx.tensor(J.T.copy()), 0.0))
+    assert np.array_equal(A, J.T @ J)
+
+
+@pytest.mark.parametrize("n", [100, 1000, 2048])
+def test_cholesky_solve(ctx, n):
+    rng = np.random.default_rng(n)
+    J = rng.standard_normal((2 * n, n))
+    A = J.T @ J + np.eye(n)
+    b = rng.standard_normal(n)
+    sigma, info = ctx.solve(ctx.tensor(A), ctx.tensor(b), method=1)
+    assert info == 1
+    x = np.linalg.solve(A, b)
+    assert np.linalg.norm(_np(sigma) - x) <= 1e-10 * np.linalg.norm(x) * np.linalg.cond(A)
+
+
+@pytest.mark.parametrize("n", [3, 4, 50, 100])
+def test_lu_reference_order_bitwise(ctx, oracle, n):
+    rng = np.random.default_rng(n + 100)
+    A = rng.standard_normal((n, n)); b = rng.standard_normal(n)
+    sigma, info = ctx.solve(ctx.tensor(A), ctx.tensor(b), method=2)
+    assert info == 2
+    assert np.array_equal(_np(sigma), oracle.lusolve(A, b))
+
+
+def test_lu_multi_launch_bitwise(ctx, oracle):
+    n = 300   # > 256: the per-column multi-launch form
+    rng = np.random.default_rng(42)
+    A = rng.standard_normal((n, n)); b = rng.standard_normal(n)
+    sigma, info = ctx.solve(ctx.tensor(A), ctx.tensor(b), method=2)
+    assert np.array_equal(_np(sigma), oracle.lusolve(A, b))
+
+
+def test_cholesky_falls_back_to_lu_on_indefinite(ctx, oracle):
+    rng = np.random.default_rng(9)
+    n = 200
+    A = rng.standard_normal((n, n)); A = A + A.T   # symmetric indefinite
+    b = rng.standard_normal(n)
+    sigma, info = ctx.solve(ctx.tensor(A), ctx.tensor(b), method=0)
+    assert info == 2
+    assert np.array_equal(_np(sigma), oracle.lusolve(A, b))
+
+
+# ---- FD engine -------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [2, 5, 1000, 4097])
+def test_fd_gradient_rosenbrock_bitwise(ctx, oracle, n):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-2, 2, n); h = np.full(n, 1e-7)
+    d = DeviceObjective(ctx, L.OBJ_ROSENBROCK, n)
+    f0, g = d.fd_gradient(ctx.tensor(x), ctx.tensor(h))
+    o = oracle.rosenbrock(n)
+    assert np.array_equal(_np(g), oracle.fd_gradient(o, x, h))
+    assert _np(f0)[0] == oracle.obj_eval(o, x)
+    # a column block of the same gradient (the sharded path)
+    i0, cnt = n // 3, max(1, n // 2)
+    _, gb = d.fd_gradient(ctx.tensor(x), ctx.tensor(h), i0, cnt)
+    assert np.array_equal(_np(gb), oracle.fd_gradient(o, x, h)[i0:i0 + cnt])
+
+
+@pytest.mark.parametrize("n", [3, 4096])
+def test_fd_gradient_quadratic_and_power_bitwise(ctx, oracle, n):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    dd, bb = oracle.quadratic_data(n)
+    x = np.linspace(-1, 1, n); h = np.full(n, 1e-6)
+    q = DeviceObjective(ctx, L.OBJ_QUADRATIC, n, 0, dd, bb)
+    _, g = q.fd_gradient(ctx.tensor(x), ctx.tensor(h))
+    assert np.array_equal(_np(g), oracle.fd_gradient(oracle.Obj(oracle.QUADRATIC, n, 0, dd, bb), x, h))
+    p2 = DeviceObjective(ctx, L.OBJ_POWER, n, power=2.0)
+    _, g2 = p2.fd_gradient(ctx.tensor(x), ctx.tensor(h))
+    assert np.array_equal(_np(g2), oracle.fd_gradient(oracle.power(n, 2), x, h))
+
+
+def test_fd_gradient_power3_known_answer(ctx):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    d = DeviceObjective(ctx, L.OBJ_POWER, 5, power=3.0)   # testGradientEvaluation, Examples.cpp:512-540
+    _, g = d.fd_gradient(ctx.tensor(np.full(5, 3.0)), ctx.tensor(np.full(5, 1e-6)))
+    np.testing.assert_allclose(_np(g), 27.0, rtol=1e-5)
+
+
+def test_fd_jacobian_cubic_bitwise_expcurve_close(ctx, oracle):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    oc = oracle.cubic()
+    c = DeviceObjective(ctx, L.OBJ_CUBIC, 4, 100, oc.p0, oc.p1)
+    x = np.full(4, 0.1); h = np.full(4, 1e-6)
+    F0, JT = c.fd_jacobian(ctx.tensor(x), ctx.tensor(h))
+    assert np.array_equal(_np(JT).T, oracle.fd_jacobian(oc, x, h))
+    assert np.array_equal(_np(F0), oracle.obj_eval_multi(oc, x))
+    oe = oracle.expcurve()
+    e = DeviceObjective(ctx, L.OBJ_EXPCURVE, 3, 100, oe.p0, oe.p1)
+    x = np.full(3, 0.1)
+    _, JT = e.fd_jacobian(ctx.tensor(x), ctx.tensor(h[:3]))
+    ref = oracle.fd_jacobian(oe, x, h[:3])
+    # device exp vs glibc exp differ by <= 1 ulp per term; the FD quotient amplifies by |F|/h
+    assert np.all(np.abs(_np(JT).T - ref) <= 4 * EPS * (1 + np.abs(oracle.obj_eval_multi(oe, x)))[:, None] / 1e-6 * 10)
+
+
+@pytest.mark.parametrize("m,n,j0,cnt", [(300, 70, 0, 70), (300, 70, 13, 29), (1000, 129, 64, 65), (257, 33, 32, 1)])
+def test_fd_jacobian_linres_bitwise(ctx, oracle, m, n, j0, cnt):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    A, xs, y = oracle.linres_data(m, n)
+    d = DeviceObjective(ctx, L.OBJ_LINRES, n, m, A, y)
+    x = np.linspace(-0.5, 0.5, n); h = np.full(n, 1e-7)
+    F0, JT = d.fd_jacobian(ctx.tensor(x), ctx.tensor(h), j0, cnt)
+    o = oracle.Obj(oracle.LINRES, n, m, A, y)
+    ref = oracle.fd_jacobian(o, x, h)
+    assert np.array_equal(_np(JT), ref.T[j0:j0 + cnt])
+    assert np.array_equal(_np(F0), oracle.obj_eval_multi(o, x))
+    assert np.array_equal(_np(d.eval(ctx.tensor(x))), oracle.obj_eval_multi(o, x))
+
+
+def test_synthetic_data_matches_oracle_stream(ctx, oracle):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    m, n = 200, 50
+    d = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+    A, xs, y = oracle.linres_data(m, n)
+    assert np.array_equal(d.xstar, xs)
+    x = np.zeros(n)
+    F = _np(d.eval(ctx.tensor(x)))          # r(0) = -y
+    assert np.array_equal(F, -y)
+    q = DeviceObjective.synthetic(ctx, L.OBJ_QUADRATIC, 64, bscale=4.0)
+    dd, bb = oracle.quadratic_data(64, bscale=4.0)
+    _, g = q.fd_gradient(ctx.tensor(np.zeros(64)), ctx.tensor(np.full(64, 1e-6)))
+    assert np.array_equal(_np(g), oracle.fd_gradient(oracle.Obj(oracle.QUADRATIC, 64, 0, dd, bb), np.zeros(64),
+                                                      np.full(64, 1e-6)))

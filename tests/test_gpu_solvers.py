@@ -1,0 +1,152 @@
+"""Solver-level parity: the C++ drop-in classes (BFGS, BFGS_MPI, BFGS_Bnd, LevMarq, LevMarqMPI)
+running on the GPU against the oracle and the reference outputs recorded in
+tests/golden/reference_survey.json.  North-star tolerance: converged X within 1e-10
+relative; bitwise wherever the device path follows the reference order (small n)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_survey.json")))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import Context
+    if L.device_count() < 1:
+        pytest.fail("no gfx950 device visible for a -m gpu run")
+    return Context(0)
+
+
+def _obj(ctx, kind, n, m=0, p0=None, p1=None, power=2.0):
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    return DeviceObjective(ctx, kind, n, m, p0, p1, power)
+
+
+def rel(a, b):
+    return np.max(np.abs(np.asarray(a) - np.asarray(b))) / max(np.max(np.abs(b)), 1e-300)
+
+
+@pytest.mark.parametrize("key", ["bfgs_rosenbrock2_m12_1", "bfgs_rosenbrock2_3_3"])
+def test_bfgs_rosenbrock2_matches_reference(ctx, key):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_bfgs
+    g = GOLD[key]
+    X, res = run_bfgs(_obj(ctx, L.OBJ_ROSENBROCK, 2), g["x0"], g["params"])
+    assert X.tolist() == g["X"]          # bitwise (reference-order device path at n=2)
+    assert res.fopt == g["f"]
+    assert res.evals == g["evals"]
+    assert rel(X, g["X"]) <= 1e-10
+
+
+def test_testBFGS_rosenbrock5(ctx, oracle):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_bfgs
+    g = GOLD["testBFGS_rosenbrock5"]
+    X, res = run_bfgs(_obj(ctx, L.OBJ_ROSENBROCK, 5), g["x0"], g["params"][:11] + [0])
+    Xo, reso, _ = oracle.bfgs_findmin(oracle.rosenbrock(5), g["x0"], g["params"])
+    assert np.array_equal(X, Xo)
+    assert res.fopt == g["f"]
+
+
+def test_bfgs_host_eval_path_equals_device_path(ctx):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_bfgs
+    g = GOLD["bfgs_rosenbrock2_m12_1"]
+    o = _obj(ctx, L.OBJ_ROSENBROCK, 2)
+    Xd, _ = run_bfgs(o, g["x0"], g["params"])
+    Xh, _ = run_bfgs(o, g["x0"], g["params"], host_eval=True)
+    assert np.array_equal(Xd, Xh)
+
+
+def test_lm_expcurve(ctx, oracle):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_levmarq
+    g = GOLD["testLMExp"]
+    oe = oracle.expcurve()
+    d = _obj(ctx, L.OBJ_EXPCURVE, 3, 100, oe.p0, oe.p1)
+    # host objective (glibc exp, as the reference): bitwise with the reference output
+    Xh, *_ = run_levmarq(d, g["x0"], g["params"], host_eval=True)
+    assert Xh.tolist() == g["X"]
+    # device FD batch (device exp): the north-star tolerance
+    Xd, *_ = run_levmarq(d, g["x0"], g["params"])
+    assert rel(Xd, g["X"]) <= 1e-10
+    # LevMarqMPI, single rank: identical to LevMarq
+    Xm, *_ = run_levmarq(d, g["x0"], g["params"], which=1, host_eval=True)
+    assert Xm.tolist() == g["X"]
+
+
+def test_lm_cubic_bitwise(ctx, oracle):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_levmarq
+    g = GOLD["testLMCubicLinearCoef"]
+    oc = oracle.cubic()
+    d = _obj(ctx, L.OBJ_CUBIC, 4, 100, oc.p0, oc.p1)
+    X, F0, FO, _ = run_levmarq(d, g["x0"], g["params"])
+    assert X.tolist() == g["X"]
+
+
+@pytest.mark.parametrize("m,n", [(600, 100), (3000, 257)])
+def test_lm_linres_large(ctx, oracle, m, n):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_levmarq
+    A, xs, y = oracle.linres_data(m, n)
+    d = _obj(ctx, L.OBJ_LINRES, n, m, A, y)
+    params = (0.001, 10, 1e-7, 6, 0.0, -1)
+    X, F0, FO, _ = run_levmarq(d, np.zeros(n), params)
+    Xo, *_ = oracle.lm_findmin(oracle.Obj(oracle.LINRES, n, m, A, y), np.zeros(n), params)
+    assert rel(X, Xo) <= 1e-10
+    assert rel(X, xs) <= 1e-8
+
+
+def test_bfgs_mpi_pool_matches_oracle(ctx, oracle):
+    """BFGS_MPI with Npool = 8 in one process equals the reference at np = 8, including the
+    zero-pool defect (f = 0)."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_bfgs
+    P = [1e-4, 0.1, 4, 1, 1000, 1e-7, 1e-3, 200, 1e-5, 1e-5, 0, 0]   # testBFGS_MPI (verbose off)
+    for npool in (2, 4, 8):
+        X, res = run_bfgs(_obj(ctx, L.OBJ_ROSENBROCK, 10), [10.0] * 10, P + [npool], which=1)
+        Xo, reso = oracle.bfgs_mpi_findmin(oracle.rosenbrock(10), [10.0] * 10, P, npool)
+        assert np.array_equal(X, Xo), npool
+        assert res.fopt == reso.fopt
+    assert res.fopt == 0.0
+    # with the defect fixed the result is a real function value
+    X, res = run_bfgs(_obj(ctx, L.OBJ_ROSENBROCK, 10), [10.0] * 10, P + [8, 1], which=1)
+    assert res.fopt > 0.0
+
+
+@pytest.mark.parametrize("case", [
+    ("testBFGSBnd", 5, [2.0] * 5, [-5.0] * 5, [5.0] * 5),
+    ("lower-active", 3, [-1.0, 2.0, 2.0], [-1.0] * 3, [5.0] * 3),
+    ("upper-active", 3, [0.0, 0.0, 0.0], [-2.0] * 3, [0.5] * 3),
+])
+def test_bfgs_bnd_matches_oracle(ctx, oracle, case):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_bfgs
+    name, n, x0, lb, ub = case
+    Pb = [1e-4, 0.8, 1e-6, 1, 1e-10, 2, 50, 1e-5, 1e-6, 1e-3, 200, 1e-5, 1e-5, 0, -1]   # Examples.cpp:75
+    X, res = run_bfgs(_obj(ctx, L.OBJ_ROSENBROCK, n), x0, Pb, which=2, lb=lb, ub=ub)
+    Xo, reso = oracle.bfgs_bnd_findmin(oracle.rosenbrock(n), x0, lb, ub, Pb)
+    assert np.array_equal(X, Xo), name
+    assert res.fopt == reso.fopt
+
+
+@pytest.mark.parametrize("n", [200, 1000])
+def test_bfgs_quadratic_fast_mode(ctx, oracle, n):
+    """n > PNOL_SEQ_MAX: fused lazy rank-2 passes; converges to the quadratic's minimiser and
+    stays within the stated trajectory tolerance of the reference-form oracle."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective, run_bfgs
+    dd, bb = oracle.quadratic_data(n)
+    P = [1e-4, 0.9, 1e-6, 1, 1000, 1e-6, 1e-3, 200, 1e-9, 1e-6, 0, 0]
+    X, res = run_bfgs(DeviceObjective(ctx, L.OBJ_QUADRATIC, n, 0, dd, bb), np.zeros(n), P)
+    H = np.diag(dd) + 0.25 * (np.eye(n, k=1) + np.eye(n, k=-1))
+    xstar = np.linalg.solve(H, bb)
+    assert rel(X, xstar) <= 1e-5
+    Xo, reso, _ = oracle.bfgs_findmin(oracle.Obj(oracle.QUADRATIC, n, 0, dd, bb), np.zeros(n), P)
+    assert rel(X, Xo) <= 1e-5

@@ -1,0 +1,24 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, rocprofv3 kernel stats.  Each GPU step has its
+# own time limit; a step that faults, aborts or times out ends the session (no retries).
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEPS="${STEPS:-10}"
+ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }   # 1 = test/assert failures, not a fault
+
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
+ok $rc || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log
+ok $rc || exit $rc
+timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err
+rc=$?; echo "bench rc=$rc"; tail -c 3000 gpurun_out/bench.json
+ok $rc || exit $rc
+if [ "${PROFILE:-1}" = "1" ]; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
+      python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/prof.err
+  rc=$?; echo "rocprof rc=$rc"
+fi
+exit 0
