@@ -26,14 +26,46 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // ------------------------------------------------------------------------------------
-// streaming GEMV: y = -A x, A rows x cols, row-major, lda even, A and x 16-byte aligned.
+// streaming GEMV: y = -A x, A rows x cols, row-major.
+// VEC (lda even, A and x 16-byte aligned): each wave owns R rows and streams them in
+// super-chunks of U x 1 KiB per row with 16-byte loads, register double-buffered (the next
+// super-chunk is in flight while the current one is reduced).  Each wave starts at a
+// different super-chunk (rotation by its global wave index) so the concurrently running
+// waves spread over the HBM channels instead of all hitting the same column offset of rows
+// that are 2^k bytes apart.  One wave reduction per row at the end.
 // ------------------------------------------------------------------------------------
+constexpr int kU = 4;
+
+template <int R>
+__device__ __forceinline__ void gemv_load(double2 (&a)[R][kU], double2 (&xr)[kU], const double2* const (&arow)[R],
+                                          const double2* __restrict__ xv, int base, int lane) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u) xr[u] = xv[base + u * kWave + lane];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int u = 0; u < kU; ++u) a[r][u] = arow[r][base + u * kWave + lane];
+}
+
+template <int R>
+__device__ __forceinline__ void gemv_fma(const double2 (&a)[R][kU], const double2 (&xr)[kU], double (&acc0)[R],
+                                         double (&acc1)[R]) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            acc0[r] = fma(a[r][u].x, xr[u].x, acc0[r]);
+            acc1[r] = fma(a[r][u].y, xr[u].y, acc1[r]);
+        }
+}
+
 template <int R>
 __global__ __launch_bounds__(256) void k_gemv_neg(const double* __restrict__ A, long lda, int rows, int cols,
                                                   const double* __restrict__ x, double* __restrict__ y) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const long row0 = ((long)blockIdx.x * 4 + wave) * R;
+    const int gwave = blockIdx.x * 4 + wave;
+    const long row0 = (long)gwave * R;
     if (row0 >= rows) return;
 
     const double2* __restrict__ xv = reinterpret_cast<const double2*>(x);
@@ -48,26 +80,27 @@ __global__ __launch_bounds__(256) void k_gemv_neg(const double* __restrict__ A, 
     for (int r = 0; r < R; ++r) { acc0[r] = 0.0; acc1[r] = 0.0; }
 
     const int pairs = cols >> 1;
-    constexpr int U = 4;                       // 4 x 1 KiB in flight per row per wave
-    int base = 0;
-    for (; base + U * kWave <= pairs; base += U * kWave) {
-        double2 xr[U];
+    constexpr int SC = kU * kWave;                 // pairs per super-chunk
+    const int nfull = pairs / SC;
+    if (nfull > 0) {
+        int sc = gwave % nfull;                    // rotated start
+        double2 cur[R][kU], curx[kU];
+        gemv_load<R>(cur, curx, arow, xv, sc * SC, lane);
+        for (int t = 1; t < nfull; ++t) {
+            sc = (sc + 1 == nfull) ? 0 : sc + 1;
+            double2 nxt[R][kU], nxtx[kU];
+            gemv_load<R>(nxt, nxtx, arow, xv, sc * SC, lane);
+            gemv_fma<R>(cur, curx, acc0, acc1);
 #pragma unroll
-        for (int u = 0; u < U; ++u) xr[u] = xv[base + u * kWave + lane];
-        double2 ar[R][U];
+            for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int r = 0; r < R; ++r)
+                for (int u = 0; u < kU; ++u) cur[r][u] = nxt[r][u];
 #pragma unroll
-            for (int u = 0; u < U; ++u) ar[r][u] = arow[r][base + u * kWave + lane];
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                acc0[r] = fma(ar[r][u].x, xr[u].x, acc0[r]);
-                acc1[r] = fma(ar[r][u].y, xr[u].y, acc1[r]);
-            }
+            for (int u = 0; u < kU; ++u) curx[u] = nxtx[u];
+        }
+        gemv_fma<R>(cur, curx, acc0, acc1);
     }
-    for (int c = base + lane; c < pairs; c += kWave) {
+    for (int c = nfull * SC + lane; c < pairs; c += kWave) {
         double2 xr = xv[c];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -89,6 +122,23 @@ __global__ __launch_bounds__(256) void k_gemv_neg(const double* __restrict__ A, 
         double s = wave_sum(acc0[r] + acc1[r]);
         if (lane == 0 && row0 + r < rows) y[row0 + r] = -s;
     }
+}
+
+// any lda / alignment: one wave per row, 8-byte loads, 4 in flight per lane
+__global__ __launch_bounds__(256) void k_gemv_neg_scalar(const double* __restrict__ A, long lda, int rows, int cols,
+                                                         const double* __restrict__ x, double* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const double* a = A + row * lda;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    int c = lane;
+    for (; c + 3 * kWave < cols; c += 4 * kWave)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] = fma(a[c + u * kWave], x[c + u * kWave], acc[u]);
+    for (; c < cols; c += kWave) acc[0] = fma(a[c], x[c], acc[0]);
+    const double s = wave_sum((acc[0] + acc[1]) + (acc[2] + acc[3]));
+    if (lane == 0) y[row] = -s;
 }
 
 // reference order: s = 0; s = s + A_ij x_j, j ascending; y = -s  (matrixVectorMultiply + negate)
@@ -201,7 +251,25 @@ __device__ __forceinline__ double butterfly16(double (&v)[16], int lane) {
     return r;
 }
 
-template <bool PEND, bool WB>
+template <bool VEC>
+__device__ __forceinline__ void pass_load(double2 (&d)[kGroup], const double* __restrict__ D, long ldd, int n, int r0,
+                                          int colc) {
+#pragma unroll
+    for (int q = 0; q < kGroup; ++q) {
+        const long row = min(r0 + q, n - 1);
+        if (VEC) {
+            d[q] = *reinterpret_cast<const double2*>(D + row * ldd + colc);
+        } else {
+            d[q].x = colc < n ? D[row * ldd + colc] : 0.0;
+            d[q].y = colc + 1 < n ? D[row * ldd + colc + 1] : 0.0;
+        }
+    }
+}
+
+// Rows of a 256-row tile are visited in groups of 8 starting at a tile-dependent group
+// (rotation: concurrently running tiles read different HBM channels); the next group's
+// 16-byte loads are issued before the current group is reduced (register double buffer).
+template <bool PEND, bool WB, bool VEC>
 __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ D, long ldd, int n,
                                                    const double* __restrict__ sp, const double* __restrict__ ap,
                                                    const double* __restrict__ bp, const double* __restrict__ y,
@@ -215,9 +283,10 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ D, long 
     const int strip = ct * 4 + wave;              // 128-column strip index
     const int col = strip * 128 + 2 * lane;       // this lane's first column
     const bool c0ok = col < n, c1ok = col + 1 < n;
-    const int colc = c0ok ? col : 0;              // clamped load column (pair start, even)
+    // load column: lanes past the last column read column 0 (VEC: the pair (col, col+1) is
+    // inside the row because an even ld >= n+1 when n is odd; scalar loads are guarded)
+    const int colc = c0ok ? col : 0;
 
-    // per-lane column vectors
     double yc0 = c0ok ? y[col] : 0.0, yc1 = c1ok ? y[col + 1] : 0.0;
     double gc0 = c0ok ? g[col] : 0.0, gc1 = c1ok ? g[col + 1] : 0.0;
     double ac0 = 0, ac1 = 0, sc0 = 0, sc1 = 0;
@@ -229,28 +298,41 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ D, long 
 
     const int r_begin = rt * kPassRows;
     const int r_end = min(n, r_begin + kPassRows);
-    for (int r0 = r_begin; r0 < r_end; r0 += kGroup) {
-        double2 d[kGroup];
+    const int ngroups = (r_end - r_begin + kGroup - 1) / kGroup;
+    int grp = rt % ngroups;
+    double2 cur[kGroup];
+    pass_load<VEC>(cur, D, ldd, n, r_begin + grp * kGroup, colc);
+    for (int t = 0; t < ngroups; ++t) {
+        const int r0 = r_begin + grp * kGroup;
+        const int gnext = (grp + 1 == ngroups) ? 0 : grp + 1;
+        double2 nxt[kGroup];
+        if (t + 1 < ngroups) pass_load<VEC>(nxt, D, ldd, n, r_begin + gnext * kGroup, colc);
         double yr[kGroup], sr[kGroup], br[kGroup];
 #pragma unroll
         for (int q = 0; q < kGroup; ++q) {
             const int row = min(r0 + q, n - 1);
-            d[q] = *reinterpret_cast<const double2*>(D + (long)row * ldd + colc);
             yr[q] = (r0 + q < n) ? y[row] : 0.0;
             if (PEND) { sr[q] = sp[row]; br[q] = bp[row]; }
         }
         double vals[16];
 #pragma unroll
         for (int q = 0; q < kGroup; ++q) {
-            double e0 = d[q].x, e1 = d[q].y;
+            double e0 = cur[q].x, e1 = cur[q].y;
+            const double o0 = e0, o1 = e1;
             if (PEND) {
                 e0 = fma(br[q], sc0, fma(sr[q], ac0, e0));
                 e1 = fma(br[q], sc1, fma(sr[q], ac1, e1));
-                if (!c0ok) e0 = d[q].x;
-                if (!c1ok) e1 = d[q].y;
             }
+            if (!c0ok) { e0 = o0; }
+            if (!c1ok) { e1 = o1; }
             if (WB && r0 + q < n && c0ok) {
-                *reinterpret_cast<double2*>(D + (long)(r0 + q) * ldd + col) = make_double2(e0, e1);
+                double* dst = D + (long)(r0 + q) * ldd + col;
+                if (VEC) {
+                    *reinterpret_cast<double2*>(dst) = make_double2(e0, c1ok ? e1 : cur[q].y);
+                } else {
+                    dst[0] = e0;
+                    if (c1ok) dst[1] = e1;
+                }
             }
             const double m0 = c0ok ? e0 : 0.0, m1 = c1ok ? e1 : 0.0;
             vals[q] = fma(m1, yc1, m0 * yc0);
@@ -267,6 +349,9 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ D, long 
                 else part_v[(long)strip * n + row] = red;
             }
         }
+#pragma unroll
+        for (int q = 0; q < kGroup; ++q) cur[q] = nxt[q];
+        grp = gnext;
     }
     if (c0ok) part_w[(long)rt * n + col] = w0;
     if (c1ok) part_w[(long)rt * n + col + 1] = w1;
@@ -312,12 +397,13 @@ static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 int launch_gemv_neg(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y) {
     if (!A || !x || !y || rows <= 0 || cols <= 0 || lda < cols) return PNOL_ERR_ARG;
-    if ((lda & 1) || !aligned16(A) || !aligned16(x)) return PNOL_ERR_ARG;
+    if ((lda & 1) || !aligned16(A) || !aligned16(x)) {
+        hipLaunchKernelGGL(k_gemv_neg_scalar, dim3((rows + 3) / 4), dim3(256), 0, ctx->stream, A, (long)lda, rows, cols,
+                           x, y);
+        return launch_check();
+    }
     // rows per wave: enough waves to cover the chip (>= ~2 per SIMD) with long streams each
     if (rows >= 8192) {
-        int blocks = (rows + 15) / 16;
-        hipLaunchKernelGGL((k_gemv_neg<4>), dim3(blocks), dim3(256), 0, ctx->stream, A, (long)lda, rows, cols, x, y);
-    } else if (rows >= 4096) {
         int blocks = (rows + 7) / 8;
         hipLaunchKernelGGL((k_gemv_neg<2>), dim3(blocks), dim3(256), 0, ctx->stream, A, (long)lda, rows, cols, x, y);
     } else {
@@ -348,7 +434,7 @@ int launch_bfgs_update_exact(pnol_ctx* ctx, double* D, int ldd, const double* y,
 int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p, const double* a_p,
                      const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
                      double* v) {
-    if (!D || n <= 0 || ldd < n || (ldd & 1) || !aligned16(D)) return PNOL_ERR_ARG;
+    if (!D || n <= 0 || ldd < n) return PNOL_ERR_ARG;
     const bool pend = s_p != nullptr;
     if (pend && (!a_p || !b_p)) return PNOL_ERR_ARG;
     const int ncolt = (n + kPassCols - 1) / kPassCols;
@@ -366,14 +452,22 @@ int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p
     }
     dim3 grd(nrowt * ncolt), blk(256);
     auto* P0 = (double*)pu; auto* P1 = (double*)pv; auto* P2 = (double*)pw;
-    if (pend && write_back)
-        hipLaunchKernelGGL((k_bfgs_pass<true, true>), grd, blk, 0, ctx->stream, D, (long)ldd, n, s_p, a_p, b_p, y, g, P0, P1, P2);
-    else if (pend)
-        hipLaunchKernelGGL((k_bfgs_pass<true, false>), grd, blk, 0, ctx->stream, D, (long)ldd, n, s_p, a_p, b_p, y, g, P0, P1, P2);
-    else if (write_back)
-        hipLaunchKernelGGL((k_bfgs_pass<false, true>), grd, blk, 0, ctx->stream, D, (long)ldd, n, s_p, a_p, b_p, y, g, P0, P1, P2);
-    else
-        hipLaunchKernelGGL((k_bfgs_pass<false, false>), grd, blk, 0, ctx->stream, D, (long)ldd, n, s_p, a_p, b_p, y, g, P0, P1, P2);
+    const bool vec = (ldd % 2 == 0) && aligned16(D);
+#define PNOL_PASS(PE, W, V)                                                                                    \
+    hipLaunchKernelGGL((k_bfgs_pass<PE, W, V>), grd, blk, 0, ctx->stream, D, (long)ldd, n, s_p, a_p, b_p, y, g, \
+                       P0, P1, P2)
+    if (vec) {
+        if (pend && write_back) PNOL_PASS(true, true, true);
+        else if (pend) PNOL_PASS(true, false, true);
+        else if (write_back) PNOL_PASS(false, true, true);
+        else PNOL_PASS(false, false, true);
+    } else {
+        if (pend && write_back) PNOL_PASS(true, true, false);
+        else if (pend) PNOL_PASS(true, false, false);
+        else if (write_back) PNOL_PASS(false, true, false);
+        else PNOL_PASS(false, false, false);
+    }
+#undef PNOL_PASS
     PNOL_CHECK(launch_check());
     hipLaunchKernelGGL(k_bfgs_pass_finish, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, n, nstrips, nrowt,
                        (const double*)P0, (const double*)P1, (const double*)P2, u, v, w);

@@ -135,29 +135,59 @@ __global__ void k_multi_fd(const double* __restrict__ x, const double* __restric
 }
 
 // ---- linear residual r = A x - y --------------------------------------------------------
-// one thread per row, fma chain over k ascending (the objective's definition); 64 rows per
-// workgroup, A staged 64 columns at a time (coalesced), LDS rows padded to 65 doubles.
-__global__ __launch_bounds__(64) void k_linres_eval(const double* __restrict__ A, const double* __restrict__ x,
-                                                    const double* __restrict__ y, int m, int n,
-                                                    double* __restrict__ F) {
-    __shared__ double As[64][65];
-    __shared__ double xs[64];
+// One residual per lane of wave 0, an fma chain over k ascending (the objective's definition).
+// 64 rows per 256-thread workgroup: all four waves stream the next 64 x 128 tile of A into
+// registers (coalesced 1 KiB row segments, 16-byte loads) while wave 0 runs the chains of
+// the current tile out of LDS -- the chain is sequential, the bytes are not.
+constexpr int kEvRows = 64, kEvK = 128, kEvPad = kEvK + 1;
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_linres_eval(const double* __restrict__ A, const double* __restrict__ x,
+                                                     const double* __restrict__ y, int m, int n,
+                                                     double* __restrict__ F) {
+    __shared__ double As[kEvRows * kEvPad];
+    __shared__ double xs[kEvK];
     const int t = threadIdx.x;
-    const int r0 = blockIdx.x * 64;
-    double acc = 0.0;
-    for (int k0 = 0; k0 < n; k0 += 64) {
-        const int len = min(64, n - k0);
-        __syncthreads();
-        for (int r = 0; r < 64; ++r) {
-            const int row = r0 + r;
-            As[r][t] = (row < m && t < len) ? A[(long)row * n + k0 + t] : 0.0;
+    const int r0 = blockIdx.x * kEvRows;
+    // thread t stages rows (t >> 6) + 4q, columns 2*(t & 63) .. +1  (q = 0..15)
+    const int lr = t >> 6, lc = 2 * (t & 63);
+    double2 reg[16];
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int row = min(r0 + lr + 4 * q, m - 1);
+            const int c = k0 + lc;
+            const double* p = A + (long)row * n + c;
+            if (VEC && c + 1 < n) {
+                reg[q] = *reinterpret_cast<const double2*>(p);
+            } else {
+                reg[q].x = c < n ? p[0] : 0.0;
+                reg[q].y = c + 1 < n ? p[1] : 0.0;
+            }
         }
-        xs[t] = t < len ? x[k0 + t] : 0.0;
+    };
+    double acc = 0.0;
+    const int nk = (n + kEvK - 1) / kEvK;
+    load(0);
+    for (int kc = 0; kc < nk; ++kc) {
+        const int k0 = kc * kEvK;
         __syncthreads();
-        for (int e = 0; e < len; ++e) acc = fma(As[t][e], xs[e], acc);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            As[(lr + 4 * q) * kEvPad + lc] = reg[q].x;
+            As[(lr + 4 * q) * kEvPad + lc + 1] = reg[q].y;
+        }
+        if (t < kEvK) xs[t] = k0 + t < n ? x[k0 + t] : 0.0;
+        __syncthreads();
+        if (kc + 1 < nk) load(k0 + kEvK);
+        if (t < 64) {
+            const int len = min(kEvK, n - k0);
+            const double* a = As + t * kEvPad;
+            for (int e = 0; e < len; ++e) acc = fma(a[e], xs[e], acc);
+        }
     }
     const int row = r0 + t;
-    if (row < m) F[row] = y ? acc - y[row] : acc;
+    if (t < 64 && row < m) F[row] = y ? acc - y[row] : acc;
 }
 
 // Batched FD GEMM.  Workgroup tile 128 residual rows x 64 points, K staged 16 at a time;
@@ -309,8 +339,12 @@ int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out) 
             return launch_check();
         case PNOL_OBJ_LINRES: {
             ScopedTimer tm(ctx, "linres_eval");
-            hipLaunchKernelGGL(k_linres_eval, dim3((o->m + 63) / 64), dim3(64), 0, ctx->stream, o->p0, x, o->p1, o->m,
-                               o->n, out);
+            if (o->n % 2 == 0)
+                hipLaunchKernelGGL((k_linres_eval<true>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0, ctx->stream,
+                                   o->p0, x, o->p1, o->m, o->n, out);
+            else
+                hipLaunchKernelGGL((k_linres_eval<false>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0,
+                                   ctx->stream, o->p0, x, o->p1, o->m, o->n, out);
             return launch_check();
         }
         default:
@@ -385,8 +419,12 @@ int launch_synthetic_linres(pnol_ctx* ctx, unsigned long long seed, int m, int n
     hipLaunchKernelGGL(k_synth_linres, dim3(4096), dim3(256), 0, ctx->stream, seed, m, n, scale, A, xstar);
     PNOL_CHECK(launch_check());
     // y = A x* with the residual's own fma chain (no y offset)
-    hipLaunchKernelGGL(k_linres_eval, dim3((m + 63) / 64), dim3(64), 0, ctx->stream, (const double*)A,
-                       (const double*)xstar, (const double*)nullptr, m, n, y);
+    if (n % 2 == 0)
+        hipLaunchKernelGGL((k_linres_eval<true>), dim3((m + kEvRows - 1) / kEvRows), dim3(256), 0, ctx->stream,
+                           (const double*)A, (const double*)xstar, (const double*)nullptr, m, n, y);
+    else
+        hipLaunchKernelGGL((k_linres_eval<false>), dim3((m + kEvRows - 1) / kEvRows), dim3(256), 0, ctx->stream,
+                           (const double*)A, (const double*)xstar, (const double*)nullptr, m, n, y);
     return launch_check();
 }
 

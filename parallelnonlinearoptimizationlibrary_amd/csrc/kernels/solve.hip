@@ -17,47 +17,41 @@ namespace {
 constexpr int kNB = 64;
 
 // ---- Cholesky ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_potrf_diag(double* __restrict__ A, long lda, int k0, int nbe,
-                                                    int* __restrict__ info) {
+// Diagonal block, one wave: lane t owns row t; left-looking (Crout) column steps
+//   s_t = a_tj - sum_{k<j} L_tk L_jk ;  L_jj = sqrt(s_j) ;  L_tj = s_t / L_jj  (t > j)
+// with row j read as an LDS broadcast.  A single wave needs no workgroup barrier between
+// steps, only LDS ordering (s_barrier with one wave is free).
+__global__ __launch_bounds__(64) void k_potrf_diag(double* __restrict__ A, long lda, int k0, int nbe,
+                                                   int* __restrict__ info) {
     __shared__ double L[kNB][kNB + 1];
-    __shared__ int bad;
     const int t = threadIdx.x;
-    if (t == 0) bad = 0;
-    for (int e = t; e < nbe * nbe; e += blockDim.x) {
-        int r = e / nbe, c = e % nbe;
-        L[r][c] = (c <= r) ? A[(long)(k0 + r) * lda + k0 + c] : 0.0;
-    }
+    for (int r = 0; r < kNB; ++r)
+        L[r][t] = (r < nbe && t <= r) ? A[(long)(k0 + r) * lda + k0 + t] : 0.0;
     __syncthreads();
     if (*info != 0) return;   // an earlier block already failed
+    bool bad = false;
     for (int j = 0; j < nbe; ++j) {
-        // column j: pivot and scale (threads 0..nbe-1 own rows)
-        const double ajj = L[j][j];
-        if (!(ajj > 0.0)) {
-            if (t == 0) { bad = 1; *info = k0 + j + 1; }
+        double s = (t >= j && t < nbe) ? L[t][j] : 0.0;
+        for (int k = 0; k < j; ++k) s = fma(-L[t][k], L[j][k], s);
+        const double sjj = __shfl(s, j, 64);
+        if (!(sjj > 0.0)) {          // not positive definite (or NaN): uniform exit
+            if (t == 0) *info = k0 + j + 1;
+            bad = true;
             break;
         }
-        const double d = sqrt(ajj);
-        __syncthreads();
-        if (t == 0) L[j][j] = d;
-        for (int r = j + 1 + t; r < nbe; r += blockDim.x) L[r][j] = L[r][j] / d;
-        __syncthreads();
-        // rank-1 update of the trailing lower triangle
-        const int m = nbe - j - 1;
-        for (int e = t; e < m * m; e += blockDim.x) {
-            int r = j + 1 + e / m, c = j + 1 + e % m;
-            if (c <= r) L[r][c] = L[r][c] - L[r][j] * L[c][j];
-        }
+        const double d = sqrt(sjj);
+        if (t == j) L[j][j] = d;
+        else if (t > j && t < nbe) L[t][j] = s / d;
         __syncthreads();
     }
     if (bad) return;
-    for (int e = t; e < nbe * nbe; e += blockDim.x) {
-        int r = e / nbe, c = e % nbe;
-        if (c <= r) A[(long)(k0 + r) * lda + k0 + c] = L[r][c];
-    }
+    for (int r = 0; r < nbe; ++r)
+        if (t <= r) A[(long)(k0 + r) * lda + k0 + t] = L[r][t];
 }
 
-// rows [k0+nbe, n) of the panel: x L11^T = a  ->  x_j = (a_j - sum_{l<j} x_l L_jl) / L_jj,
-// right-looking per row; one thread per row, 64 rows per workgroup, rows and L11 in LDS.
+// Panel below the diagonal block: x L11^T = a for every row, one thread per row with the
+// row in registers (fully unrolled right-looking substitution, L11 read as LDS broadcasts).
+// 64 rows per workgroup, loaded and stored through LDS in coalesced 512-byte row segments.
 __global__ __launch_bounds__(64) void k_trsm_panel(double* __restrict__ A, long lda, int n, int k0, int nbe,
                                                    const int* __restrict__ info) {
     __shared__ double L[kNB][kNB + 1];
@@ -71,11 +65,17 @@ __global__ __launch_bounds__(64) void k_trsm_panel(double* __restrict__ A, long 
         X[r][t] = (row < n && t < nbe) ? A[(long)row * lda + k0 + t] : 0.0;
     }
     __syncthreads();
-    for (int j = 0; j < nbe; ++j) {
-        const double xj = X[t][j] / L[j][j];
-        X[t][j] = xj;
-        for (int l = j + 1; l < nbe; ++l) X[t][l] = fma(-xj, L[l][j], X[t][l]);
+    double x[kNB];
+#pragma unroll
+    for (int j = 0; j < kNB; ++j) x[j] = X[t][j];
+#pragma unroll
+    for (int j = 0; j < kNB; ++j) {
+        x[j] = x[j] / L[j][j];
+#pragma unroll
+        for (int l = j + 1; l < kNB; ++l) x[l] = fma(-x[j], L[l][j], x[l]);
     }
+#pragma unroll
+    for (int j = 0; j < kNB; ++j) X[t][j] = x[j];
     __syncthreads();
     for (int r = 0; r < kNB; ++r) {
         const int row = rbase + r;
@@ -83,10 +83,16 @@ __global__ __launch_bounds__(64) void k_trsm_panel(double* __restrict__ A, long 
     }
 }
 
-// forward then backward substitution with the lower factor; one 1024-thread workgroup.
+// Forward then backward substitution with the lower factor; one 1024-thread workgroup.
+// Per 64-row block: the 64 x 64 diagonal block is staged in LDS and solved by wave 0
+// (lane i owns row i, pivots broadcast by shuffle); the rest of the right-hand side is then
+// updated by all 16 waves with coalesced reads (forward: a wave per row, lanes over the
+// block's columns; backward: a thread per remaining entry, lanes over a row of L).
 __global__ __launch_bounds__(1024) void k_chol_solve(const double* __restrict__ L, long lda, int n,
                                                      const double* __restrict__ rhs, double* __restrict__ x,
                                                      double* __restrict__ work, const int* __restrict__ info) {
+    __shared__ double T[64][65];
+    __shared__ double zb[64];
     if (*info != 0) return;
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6, nwaves = blockDim.x >> 6;
@@ -96,21 +102,27 @@ __global__ __launch_bounds__(1024) void k_chol_solve(const double* __restrict__ 
     // forward: L z = b
     for (int i0 = 0; i0 < n; i0 += 64) {
         const int nb = min(64, n - i0);
+        for (int e = t; e < 64 * 64; e += blockDim.x) {
+            const int r = e >> 6, c = e & 63;
+            T[r][c] = (r < nb && c <= r) ? L[(long)(i0 + r) * lda + i0 + c] : 0.0;
+        }
+        __syncthreads();
         if (wave == 0) {
             double bi = lane < nb ? b[i0 + lane] : 0.0;
             for (int j = 0; j < nb; ++j) {
-                double zj = __shfl(bi, j, 64) / L[(long)(i0 + j) * lda + i0 + j];
+                const double zj = __shfl(bi, j, 64) / T[j][j];
                 if (lane == j) bi = zj;
-                if (lane > j && lane < nb) bi = fma(-L[(long)(i0 + lane) * lda + i0 + j], zj, bi);
+                else if (lane > j) bi = fma(-T[lane][j], zj, bi);
             }
-            if (lane < nb) b[i0 + lane] = bi;
+            if (lane < nb) { b[i0 + lane] = bi; zb[lane] = bi; }
         }
         __syncthreads();
-        for (int i = i0 + nb + t; i < n; i += blockDim.x) {
-            const double* l = L + (long)i * lda + i0;
-            double s = b[i];
-            for (int j = 0; j < nb; ++j) s = fma(-l[j], b[i0 + j], s);
-            b[i] = s;
+        const double zl = lane < nb ? zb[lane] : 0.0;
+        for (int i = i0 + nb + wave; i < n; i += nwaves) {
+            double s = lane < nb ? L[(long)i * lda + i0 + lane] * zl : 0.0;
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+            if (lane == 0) b[i] = b[i] - s;
         }
         __syncthreads();
     }
@@ -118,23 +130,25 @@ __global__ __launch_bounds__(1024) void k_chol_solve(const double* __restrict__ 
     for (int iend = n; iend > 0; iend -= 64) {
         const int i0 = max(0, iend - 64);
         const int nb = iend - i0;
+        for (int e = t; e < 64 * 64; e += blockDim.x) {
+            const int r = e >> 6, c = e & 63;
+            T[r][c] = (r < nb && c <= r) ? L[(long)(i0 + r) * lda + i0 + c] : 0.0;
+        }
+        __syncthreads();
         if (wave == 0) {
             double zi = lane < nb ? b[i0 + lane] : 0.0;
             for (int j = nb - 1; j >= 0; --j) {
-                double xj = __shfl(zi, j, 64) / L[(long)(i0 + j) * lda + i0 + j];
+                const double xj = __shfl(zi, j, 64) / T[j][j];
                 if (lane == j) zi = xj;
-                if (lane < j) zi = fma(-L[(long)(i0 + j) * lda + i0 + lane], xj, zi);
+                else if (lane < j) zi = fma(-T[j][lane], xj, zi);
             }
-            if (lane < nb) b[i0 + lane] = zi;
+            if (lane < nb) { b[i0 + lane] = zi; zb[lane] = zi; }
         }
         __syncthreads();
-        // z_i -= sum_{j in block} L_ji x_j for i < i0 ; wave-per-row-group, lanes over j
-        for (int i = wave; i < i0; i += nwaves) {
+        for (int i = t; i < i0; i += blockDim.x) {
             double s = 0.0;
-            if (lane < nb) s = L[(long)(i0 + lane) * lda + i] * b[i0 + lane];
-#pragma unroll
-            for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
-            if (lane == 0) b[i] = b[i] - s;
+            for (int j = 0; j < nb; ++j) s = fma(L[(long)(i0 + j) * lda + i], zb[j], s);
+            b[i] = b[i] - s;
         }
         __syncthreads();
     }
@@ -302,7 +316,7 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
         hipLaunchKernelGGL(k_set_int, dim3(1), dim3(1), 0, ctx->stream, dinfo, 0);
         for (int k0 = 0; k0 < n; k0 += kNB) {
             const int nbe = std::min(kNB, n - k0);
-            hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(256), 0, ctx->stream, A, (long)lda, k0, nbe, dinfo);
+            hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(64), 0, ctx->stream, A, (long)lda, k0, nbe, dinfo);
             const int below = n - k0 - nbe;
             if (below > 0) {
                 hipLaunchKernelGGL(k_trsm_panel, dim3((below + kNB - 1) / kNB), dim3(kNB), 0, ctx->stream, A, (long)lda, n,

@@ -32,8 +32,13 @@ class Context:
         L.check(L.lib().pnol_ctx_create(device, C.byref(h)), "pnol_ctx_create")
         self.h = h
         if use_torch_stream:
+            # A dedicated torch stream made current: torch ops and this library's launches are
+            # ordered on one real stream (the legacy null stream has handle 0, which the C ABI
+            # reads as "use the context's own stream").
             with torch.cuda.device(device):
-                s = torch.cuda.current_stream().cuda_stream
+                self.tstream = torch.cuda.Stream(device)
+                torch.cuda.set_stream(self.tstream)
+                s = self.tstream.cuda_stream
             L.check(L.lib().pnol_ctx_set_stream(self.h, C.c_void_p(s)), "pnol_ctx_set_stream")
 
     def close(self):
