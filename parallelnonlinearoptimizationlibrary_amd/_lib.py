@@ -102,6 +102,13 @@ def lib() -> C.CDLL:
                 f"{LIB_PATH} is missing: build it with __graft_entry__.build() or "
                 "`make -C parallelnonlinearoptimizationlibrary_amd/csrc` (hipcc, gfx950). "
                 "The HIP path has no CPU fallback.")
+        # torch ships its own libamdhip64.so.7; whichever copy is loaded first owns the SONAME
+        # for the whole process.  Load torch's first so torch and this library share one HIP
+        # runtime (loading /opt/rocm's first leaves torch with "No HIP GPUs are available").
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(L, name)

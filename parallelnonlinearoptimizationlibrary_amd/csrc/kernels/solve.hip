@@ -5,7 +5,8 @@
 //   k_potrf_diag   factor the 64 x 64 diagonal block in LDS (one workgroup)
 //   k_trsm_panel   L21 = A21 L11^{-T}, one row per thread, row held in registers
 //   syrk (MODE 1)  A22 -= L21 L21^T on the lower tiles, fp64 MFMA (syrk.hip)
-//   k_chol_solve   forward / backward substitution, one workgroup, 64-row blocks
+//   k_trsv_fwd/bwd forward / backward substitution: a workgroup per 64-row block, blocks
+//                  chained by agent-scope ready flags
 // A non-positive (or NaN) pivot flips to Gaussian elimination with partial pivoting in the
 // reference's operation order (k_lu_*), which is also the method for n <= PNOL_SEQ_MAX so
 // the small ExampleObjectives problems are bitwise equal to the CPU path.
@@ -17,142 +18,300 @@ namespace {
 constexpr int kNB = 64;
 
 // ---- Cholesky ---------------------------------------------------------------------------
-// Diagonal block, one wave: lane t owns row t; left-looking (Crout) column steps
-//   s_t = a_tj - sum_{k<j} L_tk L_jk ;  L_jj = sqrt(s_j) ;  L_tj = s_t / L_jj  (t > j)
-// with row j read as an LDS broadcast.  A single wave needs no workgroup barrier between
-// steps, only LDS ordering (s_barrier with one wave is free).
-__global__ __launch_bounds__(64) void k_potrf_diag(double* __restrict__ A, long lda, int k0, int nbe,
-                                                   int* __restrict__ info) {
-    __shared__ double L[kNB][kNB + 1];
-    const int t = threadIdx.x;
-    for (int r = 0; r < kNB; ++r)
-        L[r][t] = (r < nbe && t <= r) ? A[(long)(k0 + r) * lda + k0 + t] : 0.0;
-    __syncthreads();
-    if (*info != 0) return;   // an earlier block already failed
-    bool bad = false;
-    for (int j = 0; j < nbe; ++j) {
-        double s = (t >= j && t < nbe) ? L[t][j] : 0.0;
-        for (int k = 0; k < j; ++k) s = fma(-L[t][k], L[j][k], s);
-        const double sjj = __shfl(s, j, 64);
-        if (!(sjj > 0.0)) {          // not positive definite (or NaN): uniform exit
-            if (t == 0) *info = k0 + j + 1;
-            bad = true;
-            break;
-        }
-        const double d = sqrt(sjj);
-        if (t == j) L[j][j] = d;
-        else if (t > j && t < nbe) L[t][j] = s / d;
-        __syncthreads();
+// Diagonal block, one wave: lane t holds row t of the 64 x 64 block in registers (fully
+// unrolled, static indices).  Step j: the pivot comes from lane j, lane t scales its entry of
+// column j, and every lane updates the rest of its row with scalar broadcasts of that column
+// (right-looking, no memory round trips inside the factorisation).  Rows and columns
+// past nbe are padded with the identity, so the unrolled code has no data-dependent shape.
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+
+// One right-looking step of the register Cholesky: column J is scaled by the pivot from lane
+// J and published through LDS; row t is then updated with 16-byte LDS broadcasts of the
+// column (two entries per ds_read_b128), in chunks of 16 columns so that the scheduler does
+// not hoist a whole column of loads on top of the 128 registers holding the row.
+template <int J>
+__device__ __forceinline__ void potrf_step(double (&a)[kNB], double* __restrict__ col, int t, bool& bad) {
+    const double piv = readlane_d(a[J], J);
+    bad |= !(piv > 0.0);
+    const double d = sqrt(piv);
+    // a select, not a branch (a divergent branch here splits the scheduling regions and the
+    // row spills).  Lanes t < J compute junk from their upper-triangle entries; it only ever
+    // reaches upper-triangle entries, which are never written back.
+    const double l = (t == J) ? d : a[J] / d;
+    a[J] = l;
+    col[t] = l;
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the column is in LDS for the wave
+    __builtin_amdgcn_wave_barrier();
+    constexpr int K0 = (J + 1) & ~1;
+#pragma unroll
+    for (int k = K0; k < kNB; k += 2) {
+        const double2 c = *reinterpret_cast<const double2*>(col + k);
+        if (k >= J + 1) a[k] = fma(-l, c.x, a[k]);
+        a[k + 1] = fma(-l, c.y, a[k + 1]);
+        if ((k & 15) == 14) __builtin_amdgcn_sched_barrier(0);
     }
-    if (bad) return;
-    for (int r = 0; r < nbe; ++r)
-        if (t <= r) A[(long)(k0 + r) * lda + k0 + t] = L[r][t];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (J + 1 < kNB) potrf_step<J + 1>(a, col, t, bad);
+}
+
+// Stage rows [r0, r0 + 64) x columns [c0, c0 + 64) of A into S with all 256 threads: 16
+// unconditional loads per thread from clamped addresses are issued back to back (one memory
+// latency instead of one per row), then `pick` decides what each entry becomes.
+template <class Pick>
+__device__ __forceinline__ void stage_block(double (*S)[kNB + 1], const double* __restrict__ A, long lda, int r0,
+                                            int c0, int rlast, int clast, Pick pick) {
+    const int t = threadIdx.x, c = t & 63, rq = t >> 6;
+    double v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int r = rq + 4 * i;
+        v[i] = A[(long)min(r0 + r, rlast) * lda + min(c0 + c, clast)];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int r = rq + 4 * i;
+        S[r][c] = pick(r, c, v[i]);
+    }
+}
+
+// 256 threads: all stage the block, wave 0 factors it in registers.
+__global__ __launch_bounds__(256) void k_potrf_diag(double* __restrict__ A, long lda, int k0, int nbe,
+                                                    int* __restrict__ info) {
+    __shared__ double S[kNB][kNB + 1];
+    __shared__ __attribute__((aligned(16))) double col[kNB];
+    const int t = threadIdx.x;
+    stage_block(S, A, lda, k0, k0, k0 + nbe - 1, k0 + nbe - 1, [nbe](int r, int c, double v) {
+        return (r < nbe && c < nbe) ? (c <= r ? v : 0.0) : (r == c ? 1.0 : 0.0);
+    });
+    __syncthreads();
+    if (t >= 64 || *info != 0) return;   // wave 0 factors; an earlier block may have failed
+    double a[kNB];
+#pragma unroll
+    for (int k = 0; k < kNB; ++k) a[k] = S[t][k];
+    bool bad = false;
+    potrf_step<0>(a, col, t, bad);
+    if (bad) {
+        if (t == 0) *info = k0 + 1;
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < kNB; ++k) S[t][k] = a[k];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 16
+    for (int r = 0; r < kNB; ++r)
+        if (r < nbe && t <= r) A[(long)(k0 + r) * lda + k0 + t] = S[r][t];
 }
 
 // Panel below the diagonal block: x L11^T = a for every row, one thread per row with the
 // row in registers (fully unrolled right-looking substitution, L11 read as LDS broadcasts).
-// 64 rows per workgroup, loaded and stored through LDS in coalesced 512-byte row segments.
-__global__ __launch_bounds__(64) void k_trsm_panel(double* __restrict__ A, long lda, int n, int k0, int nbe,
-                                                   const int* __restrict__ info) {
+// 64 rows per 256-thread workgroup: all waves stage L11 and the rows through LDS (coalesced
+// 512-byte row segments, loads batched), wave 0 solves, all waves store.
+__global__ __launch_bounds__(256) void k_trsm_panel(double* __restrict__ A, long lda, int n, int k0, int nbe,
+                                                    const int* __restrict__ info) {
     __shared__ double L[kNB][kNB + 1];
     __shared__ double X[kNB][kNB + 1];
-    if (*info != 0) return;
     const int t = threadIdx.x;
     const int rbase = k0 + nbe + blockIdx.x * kNB;
-    for (int r = 0; r < kNB; ++r) {
-        L[r][t] = (r < nbe && t < nbe) ? A[(long)(k0 + r) * lda + k0 + t] : (r == t ? 1.0 : 0.0);
-        const int row = rbase + r;
-        X[r][t] = (row < n && t < nbe) ? A[(long)row * lda + k0 + t] : 0.0;
+    stage_block(L, A, lda, k0, k0, k0 + nbe - 1, k0 + nbe - 1, [nbe](int r, int c, double v) {
+        return (r < nbe && c < nbe) ? v : (r == c ? 1.0 : 0.0);
+    });
+    stage_block(X, A, lda, rbase, k0, n - 1, k0 + nbe - 1, [nbe, rbase, n](int r, int c, double v) {
+        return (rbase + r < n && c < nbe) ? v : 0.0;
+    });
+    __syncthreads();
+    if (*info != 0) return;
+    if (t < 64) {
+        double x[kNB];
+#pragma unroll
+        for (int j = 0; j < kNB; ++j) x[j] = X[t][j];
+#pragma unroll
+        for (int j = 0; j < kNB; ++j) {
+            x[j] = x[j] / L[j][j];
+#pragma unroll
+            for (int l = j + 1; l < kNB; ++l) x[l] = fma(-x[j], L[l][j], x[l]);
+        }
+#pragma unroll
+        for (int j = 0; j < kNB; ++j) X[t][j] = x[j];
     }
     __syncthreads();
-    double x[kNB];
+    const int c = t & 63, rq = t >> 6;
 #pragma unroll
-    for (int j = 0; j < kNB; ++j) x[j] = X[t][j];
-#pragma unroll
-    for (int j = 0; j < kNB; ++j) {
-        x[j] = x[j] / L[j][j];
-#pragma unroll
-        for (int l = j + 1; l < kNB; ++l) x[l] = fma(-x[j], L[l][j], x[l]);
-    }
-#pragma unroll
-    for (int j = 0; j < kNB; ++j) X[t][j] = x[j];
-    __syncthreads();
-    for (int r = 0; r < kNB; ++r) {
-        const int row = rbase + r;
-        if (row < n && t < nbe) A[(long)row * lda + k0 + t] = X[r][t];
+    for (int i = 0; i < 16; ++i) {
+        const int r = rq + 4 * i, row = rbase + r;
+        if (row < n && c < nbe) A[(long)row * lda + k0 + c] = X[r][c];
     }
 }
 
-// Forward then backward substitution with the lower factor; one 1024-thread workgroup.
-// Per 64-row block: the 64 x 64 diagonal block is staged in LDS and solved by wave 0
-// (lane i owns row i, pivots broadcast by shuffle); the rest of the right-hand side is then
-// updated by all 16 waves with coalesced reads (forward: a wave per row, lanes over the
-// block's columns; backward: a thread per remaining entry, lanes over a row of L).
-__global__ __launch_bounds__(1024) void k_chol_solve(const double* __restrict__ L, long lda, int n,
-                                                     const double* __restrict__ rhs, double* __restrict__ x,
-                                                     double* __restrict__ work, const int* __restrict__ info) {
-    __shared__ double T[64][65];
-    __shared__ double zb[64];
-    if (*info != 0) return;
-    const int t = threadIdx.x;
-    const int lane = t & 63, wave = t >> 6, nwaves = blockDim.x >> 6;
-    double* b = work;   // n doubles
-    for (int i = t; i < n; i += blockDim.x) b[i] = rhs[i];
-    __syncthreads();
-    // forward: L z = b
-    for (int i0 = 0; i0 < n; i0 += 64) {
-        const int nb = min(64, n - i0);
-        for (int e = t; e < 64 * 64; e += blockDim.x) {
-            const int r = e >> 6, c = e & 63;
-            T[r][c] = (r < nb && c <= r) ? L[(long)(i0 + r) * lda + i0 + c] : 0.0;
-        }
-        __syncthreads();
-        if (wave == 0) {
-            double bi = lane < nb ? b[i0 + lane] : 0.0;
-            for (int j = 0; j < nb; ++j) {
-                const double zj = __shfl(bi, j, 64) / T[j][j];
-                if (lane == j) bi = zj;
-                else if (lane > j) bi = fma(-T[lane][j], zj, bi);
-            }
-            if (lane < nb) { b[i0 + lane] = bi; zb[lane] = bi; }
-        }
-        __syncthreads();
-        const double zl = lane < nb ? zb[lane] : 0.0;
-        for (int i = i0 + nb + wave; i < n; i += nwaves) {
-            double s = lane < nb ? L[(long)i * lda + i0 + lane] * zl : 0.0;
+// Stage a 64 x 64 diagonal block of L into LDS; rows/columns past nb are the identity so the
+// unrolled solves below have a fixed shape (padded entries of the right-hand side are 0).
+// 1024 threads: 4 unconditional loads each from clamped addresses, issued back to back.
+__device__ __forceinline__ void stage_diag(double (*T)[65], const double* __restrict__ L, long lda, int i0, int nb) {
+    const int t = threadIdx.x, c = t & 63, rq = t >> 6;
+    double v[4];
 #pragma unroll
-            for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
-            if (lane == 0) b[i] = b[i] - s;
-        }
-        __syncthreads();
+    for (int i = 0; i < 4; ++i) v[i] = L[(long)(i0 + min(rq + 16 * i, nb - 1)) * lda + i0 + min(c, nb - 1)];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = rq + 16 * i;
+        T[r][c] = (r < nb && c < nb) ? (c <= r ? v[i] : 0.0) : (r == c ? 1.0 : 0.0);
     }
-    // backward: L^T x = z
-    for (int iend = n; iend > 0; iend -= 64) {
-        const int i0 = max(0, iend - 64);
-        const int nb = iend - i0;
-        for (int e = t; e < 64 * 64; e += blockDim.x) {
-            const int r = e >> 6, c = e & 63;
-            T[r][c] = (r < nb && c <= r) ? L[(long)(i0 + r) * lda + i0 + c] : 0.0;
-        }
-        __syncthreads();
-        if (wave == 0) {
-            double zi = lane < nb ? b[i0 + lane] : 0.0;
-            for (int j = nb - 1; j >= 0; --j) {
-                const double xj = __shfl(zi, j, 64) / T[j][j];
-                if (lane == j) zi = xj;
-                else if (lane < j) zi = fma(-T[j][lane], xj, zi);
+}
+
+// L z = b on one diagonal block, lane i owns b_i; z_J = b_J / L_JJ (reciprocal precomputed by
+// each lane for its own row) is broadcast from lane J through scalar registers.
+template <int J>
+__device__ __forceinline__ void trsv_fwd_step(const double (*T)[65], double& bi, double rd, int lane) {
+    const double zj = readlane_d(bi * rd, J);
+    bi = (lane == J) ? zj : fma(-T[lane][J], zj, bi);   // T[lane][J] = 0 above the diagonal
+    if constexpr (J + 1 < 64) trsv_fwd_step<J + 1>(T, bi, rd, lane);
+}
+
+// L^T x = z on one diagonal block, from the last row up.
+template <int J>
+__device__ __forceinline__ void trsv_bwd_step(const double (*T)[65], double& zi, double rd, int lane) {
+    const double xj = readlane_d(zi * rd, J);
+    zi = (lane == J) ? xj : fma(-T[J][lane], xj, zi);   // T[J][lane] = 0 right of the diagonal
+    if constexpr (J > 0) trsv_bwd_step<J - 1>(T, zi, rd, lane);
+}
+
+// ---- Triangular solves: one workgroup per 64-row block, blocks chained by ready flags ----
+// Forward (L z = b): workgroup w owns rows [64 w, 64 w + 64).  For each earlier block c it
+// prefetches L_wc into registers, waits until z_c is published (flag c == epoch), and
+// accumulates L_wc z_c; then it solves its diagonal block (staged in LDS at entry) and
+// publishes z_w.  Workgroups only wait on lower blockIdx, so in-order dispatch guarantees
+// progress even when the grid is not co-resident.  Backward (L^T x = z) runs the blocks in
+// reverse: workgroup b owns block w = nblk - 1 - b and reads the column blocks L_cw, c > w.
+// The memory traffic (one read of the lower triangle per direction) is spread over nblk CUs;
+// the critical path is one flag hop + one diagonal solve per block.
+constexpr int kSpinCap = 1 << 24;   // ~1 s of polling: a broken chain ends the kernel, not the GPU
+constexpr int kInfoChainTimeout = -7;
+
+// 256 threads: stage the lower-triangular diagonal block (identity padding) into T.
+__device__ __forceinline__ void stage_diag_256(double (*T)[kNB + 1], const double* __restrict__ L, long lda,
+                                               int i0, int nb) {
+    stage_block(T, L, lda, i0, i0, i0 + nb - 1, i0 + nb - 1, [nb](int r, int c, double v) {
+        return (r < nb && c < nb) ? (c <= r ? v : 0.0) : (r == c ? 1.0 : 0.0);
+    });
+}
+
+// Wait until *flag == epoch: thread 0 polls with agent-scope acquire loads, the workgroup
+// then synchronises and every thread performs its own acquire fence before reading the data
+// the flag guards.  Returns false (uniformly) if the cap was hit.
+__device__ __forceinline__ bool wait_flag(const int* flag, int epoch, int* info, int* abort_sh) {
+    if (threadIdx.x == 0) {
+        int it = 0;
+        int ok = 1;
+        while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++it > kSpinCap) {
+                ok = 0;
+                atomicExch(info, kInfoChainTimeout);   // the host falls back to LU
+                break;
             }
-            if (lane < nb) { b[i0 + lane] = zi; zb[lane] = zi; }
         }
-        __syncthreads();
-        for (int i = t; i < i0; i += blockDim.x) {
-            double s = 0.0;
-            for (int j = 0; j < nb; ++j) s = fma(L[(long)(i0 + j) * lda + i], zb[j], s);
-            b[i] = b[i] - s;
-        }
-        __syncthreads();
+        *abort_sh = !ok;
     }
-    for (int i = t; i < n; i += blockDim.x) x[i] = b[i];
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return *abort_sh == 0;
+}
+
+__global__ __launch_bounds__(256) void k_trsv_fwd(const double* __restrict__ L, long lda, int n,
+                                                  const double* __restrict__ b, double* z, int* flags, int epoch,
+                                                  int* info) {
+    __shared__ double T[kNB][kNB + 1];
+    __shared__ double part[4][kNB];
+    __shared__ int abort_sh;
+    if (*info != 0) return;
+    const int w = blockIdx.x, t = threadIdx.x;
+    const int i0 = w * kNB, nb = min(kNB, n - i0);
+    stage_diag_256(T, L, lda, i0, nb);
+    // thread (r, q): row r of the block, columns q*16 .. q*16+15 of each earlier block
+    const int r = t >> 2, q = t & 3;
+    const long rowoff = (long)min(i0 + r, n - 1) * lda + q * 16;
+    double acc = 0.0;
+    double Lv[16], Ln[16];
+    if (w > 0) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) Lv[i] = L[rowoff + i];
+    }
+    for (int c = 0; c < w; ++c) {
+        if (c + 1 < w) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) Ln[i] = L[rowoff + (long)(c + 1) * kNB + i];
+        }
+        if (!wait_flag(flags + c, epoch, info, &abort_sh)) return;
+        const double* zc = z + c * kNB + q * 16;   // published, full block (c < w)
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s = fma(Lv[i], zc[i], s);
+        acc += s;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) Lv[i] = Ln[i];
+    }
+    part[q][r] = acc;
+    __syncthreads();
+    if (t < 64) {
+        const double sum = (part[0][t] + part[1][t]) + (part[2][t] + part[3][t]);
+        double bi = t < nb ? b[i0 + t] - sum : 0.0;
+        const double rd = 1.0 / T[t][t];
+        trsv_fwd_step<0>(T, bi, rd, t);
+        z[i0 + t] = t < nb ? bi : 0.0;   // z has nblk * 64 entries: padded rows are 0
+        // release by lane 0: the fence (wait + L2 writeback) is wave-wide and covers the
+        // stores of all 64 lanes above
+        if (t == 0) __hip_atomic_store(flags + w, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_trsv_bwd(const double* __restrict__ L, long lda, int n,
+                                                  const double* __restrict__ z, double* xw,
+                                                  double* __restrict__ x, int* flags, int epoch, int* info) {
+    __shared__ double T[kNB][kNB + 1];
+    __shared__ double part[4][kNB];
+    __shared__ int abort_sh;
+    if (*info != 0) return;
+    const int nblk = gridDim.x, bidx = blockIdx.x, t = threadIdx.x;
+    const int w = nblk - 1 - bidx;
+    const int i0 = w * kNB, nb = min(kNB, n - i0);
+    stage_diag_256(T, L, lda, i0, nb);
+    // thread (j, q): column j of block w, rows q*16 .. q*16+15 of each later block
+    const int j = t & 63, q = t >> 6;
+    const int col = min(i0 + j, n - 1);
+    double acc = 0.0;
+    double Lv[16], Ln[16];
+    auto load_blk = [&](double (&dst)[16], int c) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dst[i] = L[(long)min(c * kNB + q * 16 + i, n - 1) * lda + col];
+    };
+    if (w + 1 < nblk) load_blk(Lv, nblk - 1);
+    for (int c = nblk - 1; c > w; --c) {
+        if (c - 1 > w) load_blk(Ln, c - 1);
+        if (!wait_flag(flags + c, epoch, info, &abort_sh)) return;
+        const double* xc = xw + c * kNB + q * 16;   // padded rows of the last block are 0
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s = fma(Lv[i], xc[i], s);
+        acc += s;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) Lv[i] = Ln[i];
+    }
+    part[q][j] = acc;
+    __syncthreads();
+    if (t < 64) {
+        const double sum = (part[0][t] + part[1][t]) + (part[2][t] + part[3][t]);
+        double zi = t < nb ? z[i0 + t] - sum : 0.0;
+        const double rd = 1.0 / T[t][t];
+        trsv_bwd_step<63>(T, zi, rd, t);
+        xw[i0 + t] = t < nb ? zi : 0.0;
+        if (t < nb) x[i0 + t] = zi;
+        if (t == 0) __hip_atomic_store(flags + w, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // ---- Gaussian elimination with partial pivoting, reference operation order ------------
@@ -298,6 +457,28 @@ static int lu_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs, 
     return launch_check();
 }
 
+// L L^T sigma = rhs with the factor in the lower triangle of A (two flag-chained launches).
+static int chol_trsv(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo) {
+    const int nblk = (n + kNB - 1) / kNB;
+    void *flags_v = nullptr, *zw = nullptr, *xw = nullptr;
+    PNOL_CHECK(ws_get(ctx, "trsv_flags", sizeof(int) * (size_t)(2 * nblk), &flags_v));
+    PNOL_CHECK(ws_get(ctx, "trsv_z", sizeof(double) * (size_t)nblk * kNB, &zw));
+    PNOL_CHECK(ws_get(ctx, "trsv_x", sizeof(double) * (size_t)nblk * kNB, &xw));
+    int* flags = (int*)flags_v;
+    if (flags != ctx->solve_flags || ctx->solve_epoch >= (1 << 30)) {
+        // fresh (or regrown) flag buffer: flags start below every epoch handed out
+        PNOL_HIP(hipMemsetAsync(flags, 0, sizeof(int) * (size_t)(2 * nblk), ctx->stream));
+        ctx->solve_flags = flags;
+        ctx->solve_epoch = 0;
+    }
+    const int epoch = ++ctx->solve_epoch;
+    hipLaunchKernelGGL(k_trsv_fwd, dim3(nblk), dim3(256), 0, ctx->stream, A, (long)lda, n, rhs, (double*)zw, flags,
+                       epoch, dinfo);
+    hipLaunchKernelGGL(k_trsv_bwd, dim3(nblk), dim3(256), 0, ctx->stream, A, (long)lda, n, (const double*)zw,
+                       (double*)xw, sigma, flags + nblk, epoch, dinfo);
+    return launch_check();
+}
+
 int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n, int method,
                  int* info) {
     if (!A || !rhs || !sigma || n <= 0 || lda < n) return PNOL_ERR_ARG;
@@ -316,20 +497,16 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
         hipLaunchKernelGGL(k_set_int, dim3(1), dim3(1), 0, ctx->stream, dinfo, 0);
         for (int k0 = 0; k0 < n; k0 += kNB) {
             const int nbe = std::min(kNB, n - k0);
-            hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(64), 0, ctx->stream, A, (long)lda, k0, nbe, dinfo);
+            hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(256), 0, ctx->stream, A, (long)lda, k0, nbe, dinfo);
             const int below = n - k0 - nbe;
             if (below > 0) {
-                hipLaunchKernelGGL(k_trsm_panel, dim3((below + kNB - 1) / kNB), dim3(kNB), 0, ctx->stream, A, (long)lda, n,
+                hipLaunchKernelGGL(k_trsm_panel, dim3((below + kNB - 1) / kNB), dim3(256), 0, ctx->stream, A, (long)lda, n,
                                    k0, nbe, (const int*)dinfo);
                 PNOL_CHECK(launch_syrk_lower(ctx, A + (long)(k0 + nbe) * lda + k0, lda, below, nbe, -1.0,
                                              A + (long)(k0 + nbe) * lda + k0 + nbe, lda, 1));
             }
         }
-        void* work = nullptr;
-        PNOL_CHECK(ws_get(ctx, "chol_work", sizeof(double) * (size_t)n, &work));
-        hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(1024), 0, ctx->stream, (const double*)A, (long)lda, n, rhs,
-                           sigma, (double*)work, (const int*)dinfo);
-        PNOL_CHECK(launch_check());
+        PNOL_CHECK(chol_trsv(ctx, A, lda, rhs, sigma, n, dinfo));
         int hinfo = 0;
         PNOL_HIP(hipMemcpyAsync(&hinfo, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
         PNOL_HIP(hipStreamSynchronize(ctx->stream));

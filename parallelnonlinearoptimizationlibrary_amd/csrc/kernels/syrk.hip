@@ -5,8 +5,8 @@
 // finite-difference column per row), so J^T J = JT JT^T is a SYRK whose two operands are
 // both read along contiguous rows of JT.
 //
-//   k_syrk_tile     one 128 x 128 lower-triangle output tile (ti >= tj) per 256-thread
-//                   workgroup, K split over `split_k` workgroups.  4 waves as 2 x 2, each
+//   k_syrk_tile     one 128 x 128 (or 64 x 64) lower-triangle output tile (ti >= tj) per
+//                   256-thread workgroup, K split over `split_k` workgroups.  4 waves as 2 x 2, each
 //                   64 x 64 = 4 x 4 MFMA tiles (16 fp64 accumulator quads = 128 VGPRs).
 //                   K staged 16 columns at a time through double-buffered LDS (rows padded
 //                   to 18 doubles: 16-B aligned rows, conflict-free fragment reads).
@@ -34,23 +34,27 @@ __device__ __forceinline__ void tile_of(int t, int& ti, int& tj) {
     tj = t - r * (r + 1) / 2;
 }
 
-// Stage loader: 128 rows x 16 doubles of X starting at (row0, k0) into registers.
-// Thread t owns row t>>1, columns (t&1)*8 .. +8.  Rows >= nr and columns >= kend read as 0.
-struct StageRegs { double2 v[4]; };
+// Stage loader: TILE rows x 16 doubles of X starting at (row0, k0) into registers.
+// 256 threads: TPR = 256 / TILE threads per row, each owning 16 / TPR consecutive columns.
+// Rows >= nr and columns >= kend read as 0.
+template <int TILE>
+struct StageRegs { double2 v[TILE / 32]; };
 
-__device__ __forceinline__ void load_stage(StageRegs& s, const double* __restrict__ X, long ldx, int nr, int row0,
-                                           int k0, int kend, bool full) {
+template <int TILE>
+__device__ __forceinline__ void load_stage(StageRegs<TILE>& s, const double* __restrict__ X, long ldx, int nr,
+                                           int row0, int k0, int kend, bool full) {
+    constexpr int TPR = 256 / TILE, CPT = 16 / TPR, NV = CPT / 2;
     const int t = threadIdx.x;
-    const int row = row0 + (t >> 1);
-    const int kc = k0 + (t & 1) * 8;
+    const int row = row0 + t / TPR;
+    const int kc = k0 + (t % TPR) * CPT;
     if (row < nr && full) {
         const double2* p = reinterpret_cast<const double2*>(X + (long)row * ldx + kc);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s.v[q] = p[q];
+        for (int q = 0; q < NV; ++q) s.v[q] = p[q];
     } else {
         const double* p = X + (long)min(row, nr - 1) * ldx;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < NV; ++q) {
             int c0 = kc + 2 * q;
             double a = (row < nr && c0 < kend) ? p[c0] : 0.0;
             double b = (row < nr && c0 + 1 < kend) ? p[c0 + 1] : 0.0;
@@ -59,20 +63,24 @@ __device__ __forceinline__ void load_stage(StageRegs& s, const double* __restric
     }
 }
 
-__device__ __forceinline__ void store_stage(const StageRegs& s, double* __restrict__ lds) {
+template <int TILE>
+__device__ __forceinline__ void store_stage(const StageRegs<TILE>& s, double* __restrict__ lds) {
+    constexpr int TPR = 256 / TILE, CPT = 16 / TPR, NV = CPT / 2;
     const int t = threadIdx.x;
-    double* dst = lds + (t >> 1) * kPad + (t & 1) * 8;
+    double* dst = lds + (t / TPR) * kPad + (t % TPR) * CPT;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) *reinterpret_cast<double2*>(dst + 2 * q) = s.v[q];
+    for (int q = 0; q < NV; ++q) *reinterpret_cast<double2*>(dst + 2 * q) = s.v[q];
 }
 
-// MODE 0: write split-K partial tile to part; MODE 1: C = beta*C + alpha*acc (lower tiles)
-template <int MODE>
+// MODE 0: write split-K partial tile to part; MODE 1: C = beta*C + alpha*acc (lower tiles).
+// TILE 128: waves 2 x 2 of 64 x 64 (4 x 4 MFMA blocks each); TILE 64: 2 x 2 of 32 x 32.
+template <int MODE, int TILE>
 __global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
                                                       int split_k, int kchunk, double* __restrict__ part,
                                                       double* __restrict__ C, long ldc, double alpha,
                                                       double beta) {
-    __shared__ __attribute__((aligned(16))) double lds[2][2][kTile * kPad];   // [buf][P/Q]
+    constexpr int WT = TILE / 2, NB = WT / 16;
+    __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
 
     const int blk = blockIdx.x;
     const int t = blk / split_k;
@@ -80,7 +88,7 @@ __global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__
     int ti, tj;
     tile_of(t, ti, tj);
     const bool diag = ti == tj;
-    const int prow0 = ti * kTile, qrow0 = tj * kTile;
+    const int prow0 = ti * TILE, qrow0 = tj * TILE;
     const int kbeg = sidx * kchunk;
     const int kend = min(K, kbeg + kchunk);
     const int nstages = kend > kbeg ? (kend - kbeg + kTK - 1) / kTK : 0;
@@ -90,13 +98,13 @@ __global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__
     const int wr = wave >> 1, wc = wave & 1;
     const bool ldx_even = (ldx & 1) == 0;
 
-    d4 acc[4][4];
+    d4 acc[NB][NB];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NB; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+        for (int j = 0; j < NB; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
 
-    StageRegs ps, qs;
+    StageRegs<TILE> ps, qs;
     if (nstages > 0) {
         bool full = ldx_even && (kbeg + kTK <= kend);
         load_stage(ps, X, ldx, nr, prow0, kbeg, kend, full);
@@ -119,15 +127,15 @@ __global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__
         }
 #pragma unroll
         for (int kk = 0; kk < kTK / 4; ++kk) {
-            double a[4], b[4];
+            double a[NB], b[NB];
 #pragma unroll
-            for (int mi = 0; mi < 4; ++mi) a[mi] = P[(wr * 64 + mi * 16 + frow) * kPad + kk * 4 + fk];
+            for (int mi = 0; mi < NB; ++mi) a[mi] = P[(wr * WT + mi * 16 + frow) * kPad + kk * 4 + fk];
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni) b[ni] = Q[(wc * 64 + ni * 16 + frow) * kPad + kk * 4 + fk];
+            for (int ni = 0; ni < NB; ++ni) b[ni] = Q[(wc * WT + ni * 16 + frow) * kPad + kk * 4 + fk];
 #pragma unroll
-            for (int mi = 0; mi < 4; ++mi)
+            for (int mi = 0; mi < NB; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < 4; ++ni)
+                for (int ni = 0; ni < NB; ++ni)
                     acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
         }
     }
@@ -136,26 +144,26 @@ __global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__
     const int ocol = lane & 15;
     const int orow = lane >> 4;
     if (MODE == 0) {
-        double* out = part + (long)blk * kTile * kTile;
+        double* out = part + (long)blk * TILE * TILE;
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
+        for (int mi = 0; mi < NB; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
+            for (int ni = 0; ni < NB; ++ni)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    int row = wr * 64 + mi * 16 + orow + 4 * r;
-                    int col = wc * 64 + ni * 16 + ocol;
-                    out[row * kTile + col] = acc[mi][ni][r];
+                    int row = wr * WT + mi * 16 + orow + 4 * r;
+                    int col = wc * WT + ni * 16 + ocol;
+                    out[row * TILE + col] = acc[mi][ni][r];
                 }
     } else {
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
+        for (int mi = 0; mi < NB; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
+            for (int ni = 0; ni < NB; ++ni)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    int i = prow0 + wr * 64 + mi * 16 + orow + 4 * r;
-                    int j = qrow0 + wc * 64 + ni * 16 + ocol;
+                    int i = prow0 + wr * WT + mi * 16 + orow + 4 * r;
+                    int j = qrow0 + wc * WT + ni * 16 + ocol;
                     if (i < nr && j < nr && j <= i) {
                         double* c = C + (long)i * ldc + j;
                         *c = beta * (*c) + alpha * acc[mi][ni][r];
@@ -233,7 +241,7 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * split_k * kTile * kTile, &part));
     {
         ScopedTimer tm(ctx, "syrk");
-        hipLaunchKernelGGL((k_syrk_tile<0>), dim3(ntiles * split_k), dim3(256), 0, ctx->stream, JT, (long)ldjt, n, m,
+        hipLaunchKernelGGL((k_syrk_tile<0, kTile>), dim3(ntiles * split_k), dim3(256), 0, ctx->stream, JT, (long)ldjt, n, m,
                            split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0);
     }
     PNOL_CHECK(launch_check());
@@ -247,9 +255,12 @@ int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, do
                       int split_k) {
     (void)split_k;
     if (!X || !C || nr <= 0 || K <= 0) return PNOL_ERR_ARG;
-    const int nt = (nr + kTile - 1) / kTile;
+    // 64 x 64 tiles: the Cholesky trailing update has K = 64, so per-workgroup work is small
+    // and the launch is latency-bound; 4x more workgroups than 128 x 128 tiles fill the chip.
+    constexpr int kT = 64;
+    const int nt = (nr + kT - 1) / kT;
     const int ntiles = nt * (nt + 1) / 2;
-    hipLaunchKernelGGL((k_syrk_tile<1>), dim3(ntiles), dim3(256), 0, ctx->stream, X, (long)ldx, nr, K, 1, K,
+    hipLaunchKernelGGL((k_syrk_tile<1, kT>), dim3(ntiles), dim3(256), 0, ctx->stream, X, (long)ldx, nr, K, 1, K,
                        (double*)nullptr, C, (long)ldc, alpha, 1.0);
     return launch_check();
 }

@@ -42,6 +42,8 @@ struct pnol_ctx {
     pnol::Workspace ws;
     double* pinned = nullptr;       // small host staging buffer (scalars back from the device)
     size_t pinned_bytes = 0;
+    int* solve_flags = nullptr;     // per-block ready flags of the triangular solves (workspace)
+    int solve_epoch = 0;            // value the flags of the current solve are set to
 };
 
 struct pnol_dobj {

@@ -163,7 +163,7 @@ def test_jtj_mfma_layout_asymmetric(ctx):
     assert np.array_equal(A, J.T @ J)
 
 
-@pytest.mark.parametrize("n", [100, 1000, 2048])
+@pytest.mark.parametrize("n", [65, 100, 129, 777, 1000, 2048, 3001])
 def test_cholesky_solve(ctx, n):
     rng = np.random.default_rng(n)
     J = rng.standard_normal((2 * n, n))
@@ -173,6 +173,20 @@ def test_cholesky_solve(ctx, n):
     assert info == 1
     x = np.linalg.solve(A, b)
     assert np.linalg.norm(_np(sigma) - x) <= 1e-10 * np.linalg.norm(x) * np.linalg.cond(A)
+
+
+def test_cholesky_repeated_solves_reuse_ready_flags(ctx):
+    """The flag-chained triangular solves tag each call with a new epoch; sizes that grow
+    and shrink (the flag buffer is reallocated) and back-to-back calls must all be exact."""
+    rng = np.random.default_rng(5)
+    for n in (300, 300, 1500, 64 * 70, 200, 1500):
+        J = rng.standard_normal((n + 50, n))
+        A = J.T @ J + n * np.eye(n)
+        b = rng.standard_normal(n)
+        sigma, info = ctx.solve(ctx.tensor(A), ctx.tensor(b), method=1)
+        assert info == 1, n
+        x = np.linalg.solve(A, b)
+        assert np.linalg.norm(_np(sigma) - x) <= 1e-12 * np.linalg.norm(x) * np.linalg.cond(A), n
 
 
 @pytest.mark.parametrize("n", [3, 4, 50, 100])
