@@ -52,6 +52,30 @@ def _timer(L, ctx_h, name):
     return ms.value, cnt.value
 
 
+def pmc_traffic():
+    """Per-launch L2<->fabric bytes of the hot kernels from the newest committed PMC summary
+    (profiles/r*_pmc_traffic.json, made by tools/pmc_traffic.py from separate rocprofv3
+    --pmc FETCH_SIZE / WRITE_SIZE passes of this bench), or {} if none is committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return {}
+    try:
+        return json.load(open(files[-1])).get("kernels", {})
+    except (OSError, ValueError):
+        return {}
+
+
+def fd_flop_executed(m, n, j0, cnt, bn=64, bk=16):
+    """fp64 flops k_linres_fd runs for points [j0, j0+cnt): each 64-point tile continues the
+    base chain from the checkpoint at ks = 16*floor(first column / 16) to k = n-1."""
+    tot = 0
+    for pb in range(0, cnt, bn):
+        ks = ((j0 + pb) // bk) * bk
+        tot += min(bn, cnt - pb) * (n - ks)
+    return 2.0 * m * tot
+
+
 def bench_hg(ctx, n, reps=20):
     """Standalone p = -D g at n (8 n^2 + 16 n bytes per launch) and the fused BFGS pass
     (16 n^2 bytes with write-back), timed with HIP events on the context stream."""
@@ -188,8 +212,8 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    timers = {k: _timer(L, dctx, k) for k in ("fd_jacobian", "linres_eval", "syrk", "syrk_reduce", "jtr", "solve",
-                                              "allgather")}
+    timers = {k: _timer(L, dctx, k) for k in ("fd_jacobian", "fd_ckpt", "linres_eval", "syrk", "syrk_reduce", "jtr",
+                                              "solve", "allgather")}
     L.check(L.lib().pnol_ctx_enable_timers(dctx, 0), "timers")
     err = float(np.max(np.abs(X - obj.xstar)) / np.max(np.abs(obj.xstar)))
 
@@ -202,24 +226,32 @@ def main():
         syrk_ms = per["syrk"]
         jtj_flop = float(m) * n * (n + 1)                   # unique entries of the symmetric result
         my_cols = -(-n // world)
-        fd_flop = 2.0 * m * n * my_cols                      # this rank's batched FD GEMM
+        fd_flop_nominal = 2.0 * m * n * my_cols              # full-length chains for this rank's points
+        fd_flop = fd_flop_executed(m, n, 0, my_cols)          # prefix-shared chains actually run
+        pmc = pmc_traffic()
         roofline = {
             "kernel": "k_syrk_tile (J^T J, fp64 MFMA v_mfma_f64_16x16x4_f64)",
             "bound": "mfma", "achieved": jtj_flop / (syrk_ms * 1e-3) / 1e12 if syrk_ms else None,
-            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "traffic": None,
+            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "traffic": pmc.get("k_syrk_tile<0, 128>", {}).get("traffic_bytes_per_launch"),
         }
         roofline["frac"] = roofline["achieved"] / FP64_PEAK_TFLOPS if roofline["achieved"] else None
         fd_ms = per["fd_jacobian"]
         rooflines = {
-            "fd_jacobian": {"kernel": "k_linres_fd (batched FD GEMM, fp64 VALU fma)", "bound": "valu_fp64",
-                            "ms": fd_ms, "achieved": fd_flop / (fd_ms * 1e-3) / 1e12 if fd_ms else None,
-                            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s"},
+            "fd_jacobian": {"kernel": "k_linres_fd (batched FD GEMM, fp64 VALU fma, prefix-shared chains)",
+                            "bound": "valu_fp64", "ms": fd_ms,
+                            "achieved": fd_flop / (fd_ms * 1e-3) / 1e12 if fd_ms else None,
+                            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "flop_executed": fd_flop,
+                            "flop_nominal_full_chains": fd_flop_nominal,
+                            "ckpt_ms": per["fd_ckpt"]},
             "jtj": dict(roofline, ms=syrk_ms),
         }
         if hg:
-            rooflines["hg"] = {"kernel": "k_gemv_neg<4> (p = -D g)", "bound": "hbm", "achieved": hg["hg_GBps"],
+            rooflines["hg"] = {"kernel": "k_gemv_neg<2> (p = -D g)", "bound": "hbm", "achieved": hg["hg_GBps"],
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hg["hg_frac_of_hbm"],
-                               "traffic": None, "n": HG_N}
+                               "algorithmic_bytes": 8.0 * HG_N * HG_N + 16.0 * HG_N,
+                               "traffic": pmc.get("k_gemv_neg<2>", {}).get("traffic_bytes_per_launch"),
+                               "n": HG_N}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(m, n)

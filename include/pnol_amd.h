@@ -51,8 +51,8 @@ int pnol_ctx_device(pnol_ctx* ctx, int* device);
 int pnol_default_ctx(pnol_ctx** out);
 
 /* Per-kernel HIP-event timers on the context's stream (off by default).  Names: "fd_jacobian",
- * "fd_gradient", "linres_eval", "syrk", "syrk_reduce", "jtr", "solve", "hg", "bfgs_pass",
- * "allgather".  total_ms sums the recorded launches since the last reset. */
+ * "fd_ckpt", "fd_gradient", "linres_eval", "syrk", "syrk_reduce", "jtr", "solve", "hg",
+ * "bfgs_pass", "allgather".  total_ms sums the recorded launches since the last reset. */
 int pnol_ctx_enable_timers(pnol_ctx* ctx, int on);
 int pnol_ctx_reset_timers(pnol_ctx* ctx);
 int pnol_ctx_timer(pnol_ctx* ctx, const char* name, double* total_ms, int* count);

@@ -14,6 +14,8 @@
 // All device code is compiled with -ffp-contract=off: every fma here is explicit.
 #include "../pnol_internal.hpp"
 
+#include <cstdlib>
+
 namespace pnol {
 namespace {
 
@@ -402,14 +404,21 @@ int launch_gemv_neg(pnol_ctx* ctx, const double* A, int lda, int rows, int cols,
                            x, y);
         return launch_check();
     }
-    // rows per wave: enough waves to cover the chip (>= ~2 per SIMD) with long streams each
-    if (rows >= 8192) {
-        int blocks = (rows + 7) / 8;
+    // rows per wave: enough waves to cover the chip (>= ~2 per SIMD) with long streams each;
+    // more rows per wave amortise the x reads (every wave streams all of x from L2).
+    // PNOL_GEMV_ROWS=1|2|4 overrides the choice (tuning sweeps, tools/sweep_hg.py).
+    static const int forced = [] {
+        const char* e = std::getenv("PNOL_GEMV_ROWS");
+        return e ? std::atoi(e) : 0;
+    }();
+    int R = forced == 1 || forced == 2 || forced == 4 ? forced : (rows >= 8192 ? 2 : 1);
+    const int blocks = (rows + 4 * R - 1) / (4 * R);
+    if (R == 4)
+        hipLaunchKernelGGL((k_gemv_neg<4>), dim3(blocks), dim3(256), 0, ctx->stream, A, (long)lda, rows, cols, x, y);
+    else if (R == 2)
         hipLaunchKernelGGL((k_gemv_neg<2>), dim3(blocks), dim3(256), 0, ctx->stream, A, (long)lda, rows, cols, x, y);
-    } else {
-        int blocks = (rows + 3) / 4;
+    else
         hipLaunchKernelGGL((k_gemv_neg<1>), dim3(blocks), dim3(256), 0, ctx->stream, A, (long)lda, rows, cols, x, y);
-    }
     return launch_check();
 }
 

@@ -140,11 +140,14 @@ __global__ void k_multi_fd(const double* __restrict__ x, const double* __restric
 // registers (coalesced 1 KiB row segments, 16-byte loads) while wave 0 runs the chains of
 // the current tile out of LDS -- the chain is sequential, the bytes are not.
 constexpr int kEvRows = 64, kEvK = 128, kEvPad = kEvK + 1;
+constexpr int kCkpt = 16;   // checkpoint stride of the base chain (== the FD kernel's K stage)
 
-template <bool VEC>
+// CKPT: also store the chain value before every 16th column, C[(k / 16) * m + row] for
+// k = 16, 32, ... (the prefix every FD point with a perturbed column >= k shares).
+template <bool VEC, bool CKPT>
 __global__ __launch_bounds__(256) void k_linres_eval(const double* __restrict__ A, const double* __restrict__ x,
                                                      const double* __restrict__ y, int m, int n,
-                                                     double* __restrict__ F) {
+                                                     double* __restrict__ F, double* __restrict__ C) {
     __shared__ double As[kEvRows * kEvPad];
     __shared__ double xs[kEvK];
     const int t = threadIdx.x;
@@ -183,16 +186,30 @@ __global__ __launch_bounds__(256) void k_linres_eval(const double* __restrict__ 
         if (t < 64) {
             const int len = min(kEvK, n - k0);
             const double* a = As + t * kEvPad;
-            for (int e = 0; e < len; ++e) acc = fma(a[e], xs[e], acc);
+            if (CKPT) {
+                const int row = r0 + t;
+                for (int e0 = 0; e0 < len; e0 += kCkpt) {
+                    if (k0 + e0 > 0 && row < m) C[(long)((k0 + e0) / kCkpt) * m + row] = acc;
+                    const int e1 = min(e0 + kCkpt, len);
+                    for (int e = e0; e < e1; ++e) acc = fma(a[e], xs[e], acc);
+                }
+            } else {
+                for (int e = 0; e < len; ++e) acc = fma(a[e], xs[e], acc);
+            }
         }
     }
     const int row = r0 + t;
-    if (t < 64 && row < m) F[row] = y ? acc - y[row] : acc;
+    if (t < 64 && row < m && F) F[row] = y ? acc - y[row] : acc;
 }
 
 // Batched FD GEMM.  Workgroup tile 128 residual rows x 64 points, K staged 16 at a time;
 // thread (ty, tx) = (t >> 4, t & 15) owns rows ty*8..+8 and points tx*4..+4 (32 fp64
 // accumulators), every accumulator a sequential fma chain over k = 0..n-1.
+// Prefix sharing: the chain of point j equals the base chain for every k < j (x is only
+// perturbed at k = j), so a tile whose first point is column jmin starts at
+// ks = 16 * floor(jmin / 16) from the base chain's checkpoint C[ks / 16] and runs k = ks..n-1.
+// Same fma sequence per point, hence bit-identical output; about half the flops of the
+// full-length chains.
 constexpr int kBM = 128, kBN = 64, kBK = 16;
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
@@ -204,7 +221,7 @@ template <bool EVEN>
 __global__ __launch_bounds__(256) void k_linres_fd(const double* __restrict__ A, const double* __restrict__ y,
                                                    const double* __restrict__ x, const double* __restrict__ h, int m,
                                                    int n, int j0, int cnt, const double* __restrict__ F0,
-                                                   double* __restrict__ JT, long ldjt) {
+                                                   const double* __restrict__ C, double* __restrict__ JT, long ldjt) {
     __shared__ __attribute__((aligned(16))) double As[kBK][kBM];
     __shared__ __attribute__((aligned(16))) double Bs[kBK][kBN];
     const int nmt = (m + kBM - 1) / kBM, nnt = (cnt + kBN - 1) / kBN;
@@ -213,11 +230,15 @@ __global__ __launch_bounds__(256) void k_linres_fd(const double* __restrict__ A,
     const int m0 = mt * kBM, pbase = nt * kBN;       // pbase: point index relative to j0
     const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
 
+    const int ks = ((j0 + pbase) / kBK) * kBK;       // kBK == kCkpt
     double acc[8][4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i) {
+        const int row = min(m0 + ty * 8 + i, m - 1);
+        const double c0 = ks > 0 ? C[(long)(ks / kCkpt) * m + row] : 0.0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+        for (int j = 0; j < 4; ++j) acc[i][j] = c0;
+    }
 
     // A stage: thread loads row (t >> 1), k-offset (t & 1) * 8, 8 doubles
     const int lrow = t >> 1, lk = (t & 1) * 8;
@@ -238,8 +259,8 @@ __global__ __launch_bounds__(256) void k_linres_fd(const double* __restrict__ A,
         }
     };
     const int nk = (n + kBK - 1) / kBK;
-    load_a(0);
-    for (int kc = 0; kc < nk; ++kc) {
+    load_a(ks);
+    for (int kc = ks / kBK; kc < nk; ++kc) {
         const int k0 = kc * kBK;
         __syncthreads();
 #pragma unroll
@@ -340,11 +361,11 @@ int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out) 
         case PNOL_OBJ_LINRES: {
             ScopedTimer tm(ctx, "linres_eval");
             if (o->n % 2 == 0)
-                hipLaunchKernelGGL((k_linres_eval<true>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0, ctx->stream,
-                                   o->p0, x, o->p1, o->m, o->n, out);
+                hipLaunchKernelGGL((k_linres_eval<true, false>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0, ctx->stream,
+                                   o->p0, x, o->p1, o->m, o->n, out, (double*)nullptr);
             else
-                hipLaunchKernelGGL((k_linres_eval<false>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0,
-                                   ctx->stream, o->p0, x, o->p1, o->m, o->n, out);
+                hipLaunchKernelGGL((k_linres_eval<false, false>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0,
+                                   ctx->stream, o->p0, x, o->p1, o->m, o->n, out, (double*)nullptr);
             return launch_check();
         }
         default:
@@ -379,6 +400,33 @@ int launch_fd_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
                        int compute_f0, double* JT, int ldjt) {
     if (!o || !x || !h || !F0 || is_scalar_kind(o->kind)) return PNOL_ERR_ARG;
     if (j0 < 0 || cnt < 0 || j0 + cnt > o->n || ldjt < o->m) return PNOL_ERR_ARG;
+    if (o->kind == PNOL_OBJ_LINRES && cnt > 0) {
+        if (!JT) return PNOL_ERR_ARG;
+        // one pass of the base chain: F0 (when asked) and the prefix checkpoints
+        void* C = nullptr;
+        const int ncp = (o->n + kCkpt - 1) / kCkpt;
+        PNOL_CHECK(ws_get(ctx, "linres_ckpt", sizeof(double) * (size_t)o->m * (ncp > 1 ? ncp : 1), &C));
+        double* f0_out = compute_f0 ? F0 : nullptr;
+        {
+            ScopedTimer tm(ctx, "fd_ckpt");
+            if ((o->n % 2) == 0)
+                hipLaunchKernelGGL((k_linres_eval<true, true>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0,
+                                   ctx->stream, o->p0, x, o->p1, o->m, o->n, f0_out, (double*)C);
+            else
+                hipLaunchKernelGGL((k_linres_eval<false, true>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0,
+                                   ctx->stream, o->p0, x, o->p1, o->m, o->n, f0_out, (double*)C);
+        }
+        PNOL_CHECK(launch_check());
+        const int nmt = (o->m + kBM - 1) / kBM, nnt = (cnt + kBN - 1) / kBN;
+        ScopedTimer tm(ctx, "fd_jacobian");
+        if ((o->n % 2) == 0)
+            hipLaunchKernelGGL((k_linres_fd<true>), dim3(nmt * nnt), dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
+                               o->n, j0, cnt, (const double*)F0, (const double*)C, JT, (long)ldjt);
+        else
+            hipLaunchKernelGGL((k_linres_fd<false>), dim3(nmt * nnt), dim3(256), 0, ctx->stream, o->p0, o->p1, x, h,
+                               o->m, o->n, j0, cnt, (const double*)F0, (const double*)C, JT, (long)ldjt);
+        return launch_check();
+    }
     if (compute_f0) PNOL_CHECK(launch_dobj_eval(ctx, o, x, F0));
     if (cnt == 0) return PNOL_OK;
     if (!JT) return PNOL_ERR_ARG;
@@ -391,18 +439,6 @@ int launch_fd_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
             hipLaunchKernelGGL((k_multi_fd<PNOL_OBJ_CUBIC>), dim3((o->m + 255) / 256, cnt), dim3(256), 0, ctx->stream, x, h,
                                o->n, o->m, j0, cnt, o->p0, o->p1, o->p2, (const double*)F0, JT, (long)ldjt);
             return launch_check();
-        case PNOL_OBJ_LINRES: {
-            const int nmt = (o->m + kBM - 1) / kBM, nnt = (cnt + kBN - 1) / kBN;
-            const bool even = (o->n % 2) == 0;
-            ScopedTimer tm(ctx, "fd_jacobian");
-            if (even)
-                hipLaunchKernelGGL((k_linres_fd<true>), dim3(nmt * nnt), dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
-                                   o->n, j0, cnt, (const double*)F0, JT, (long)ldjt);
-            else
-                hipLaunchKernelGGL((k_linres_fd<false>), dim3(nmt * nnt), dim3(256), 0, ctx->stream, o->p0, o->p1, x, h,
-                                   o->m, o->n, j0, cnt, (const double*)F0, JT, (long)ldjt);
-            return launch_check();
-        }
         default:
             return PNOL_ERR_UNSUPPORTED;
     }
@@ -420,11 +456,11 @@ int launch_synthetic_linres(pnol_ctx* ctx, unsigned long long seed, int m, int n
     PNOL_CHECK(launch_check());
     // y = A x* with the residual's own fma chain (no y offset)
     if (n % 2 == 0)
-        hipLaunchKernelGGL((k_linres_eval<true>), dim3((m + kEvRows - 1) / kEvRows), dim3(256), 0, ctx->stream,
-                           (const double*)A, (const double*)xstar, (const double*)nullptr, m, n, y);
+        hipLaunchKernelGGL((k_linres_eval<true, false>), dim3((m + kEvRows - 1) / kEvRows), dim3(256), 0, ctx->stream,
+                           (const double*)A, (const double*)xstar, (const double*)nullptr, m, n, y, (double*)nullptr);
     else
-        hipLaunchKernelGGL((k_linres_eval<false>), dim3((m + kEvRows - 1) / kEvRows), dim3(256), 0, ctx->stream,
-                           (const double*)A, (const double*)xstar, (const double*)nullptr, m, n, y);
+        hipLaunchKernelGGL((k_linres_eval<false, false>), dim3((m + kEvRows - 1) / kEvRows), dim3(256), 0, ctx->stream,
+                           (const double*)A, (const double*)xstar, (const double*)nullptr, m, n, y, (double*)nullptr);
     return launch_check();
 }
 

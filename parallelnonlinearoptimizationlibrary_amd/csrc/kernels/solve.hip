@@ -200,14 +200,16 @@ __device__ __forceinline__ void stage_diag_256(double (*T)[kNB + 1], const doubl
     });
 }
 
-// Wait until *flag == epoch: thread 0 polls with agent-scope acquire loads, the workgroup
-// then synchronises and every thread performs its own acquire fence before reading the data
-// the flag guards.  Returns false (uniformly) if the cap was hit.
+// Wait until *flag == epoch: thread 0 polls with relaxed agent-scope loads (global_load sc1,
+// no cache invalidation per poll), then one acquire fence; the workgroup synchronises and
+// every thread performs its own acquire fence before reading the data the flag guards
+// (MI355X_MICROARCH.md: per-CU L1 and per-XCD L2 are not coherent with other CUs' stores).
+// Returns false (uniformly) if the cap was hit.
 __device__ __forceinline__ bool wait_flag(const int* flag, int epoch, int* info, int* abort_sh) {
     if (threadIdx.x == 0) {
         int it = 0;
         int ok = 1;
-        while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
             __builtin_amdgcn_s_sleep(1);
             if (++it > kSpinCap) {
                 ok = 0;
@@ -215,6 +217,7 @@ __device__ __forceinline__ bool wait_flag(const int* flag, int epoch, int* info,
                 break;
             }
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         *abort_sh = !ok;
     }
     __syncthreads();

@@ -274,8 +274,11 @@ def test_fd_jacobian_cubic_bitwise_expcurve_close(ctx, oracle):
     assert np.all(np.abs(_np(JT).T - ref) <= 4 * EPS * (1 + np.abs(oracle.obj_eval_multi(oe, x)))[:, None] / 1e-6 * 10)
 
 
-@pytest.mark.parametrize("m,n,j0,cnt", [(300, 70, 0, 70), (300, 70, 13, 29), (1000, 129, 64, 65), (257, 33, 32, 1)])
+@pytest.mark.parametrize("m,n,j0,cnt", [(300, 70, 0, 70), (300, 70, 13, 29), (1000, 129, 64, 65), (257, 33, 32, 1),
+                                       (700, 300, 0, 300), (700, 300, 37, 200), (130, 16, 0, 16), (130, 17, 16, 1)])
 def test_fd_jacobian_linres_bitwise(ctx, oracle, m, n, j0, cnt):
+    """Prefix-shared chains (tiles start from the base chain's 16-column checkpoints) are
+    the same fma sequence as full-length evaluation: bitwise equal to the oracle's n+1 evals."""
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
     A, xs, y = oracle.linres_data(m, n)
@@ -287,6 +290,11 @@ def test_fd_jacobian_linres_bitwise(ctx, oracle, m, n, j0, cnt):
     assert np.array_equal(_np(JT), ref.T[j0:j0 + cnt])
     assert np.array_equal(_np(F0), oracle.obj_eval_multi(o, x))
     assert np.array_equal(_np(d.eval(ctx.tensor(x))), oracle.obj_eval_multi(o, x))
+    # caller-provided F0 (compute_f0 = 0, the LM path): same Jacobian, F0 untouched
+    F0b = ctx.tensor(oracle.obj_eval_multi(o, x))
+    _, JT2 = d.fd_jacobian(ctx.tensor(x), ctx.tensor(h), j0, cnt, F0=F0b, compute_f0=False)
+    assert np.array_equal(_np(JT2), ref.T[j0:j0 + cnt])
+    assert np.array_equal(_np(F0b), oracle.obj_eval_multi(o, x))
 
 
 def test_synthetic_data_matches_oracle_stream(ctx, oracle):

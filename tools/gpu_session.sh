@@ -7,6 +7,10 @@ export TMPDIR=/tmp
 STEPS="${STEPS:-10}"
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }   # 1 = test/assert failures, not a fault
 
+if [ "${MB:-0}" = "1" ]; then
+  timeout -k 10 120 ./tools/microbench/fp64_peak > gpurun_out/fp64_peak.json 2>&1
+  rc=$?; echo "microbench rc=$rc"; cat gpurun_out/fp64_peak.json; [ "$rc" -eq 0 ] || exit $rc
+fi
 timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
 ok $rc || exit $rc
@@ -20,5 +24,17 @@ if [ "${PROFILE:-1}" = "1" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
       python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/prof.err
   rc=$?; echo "rocprof rc=$rc"
+fi
+if [ "${SWEEP:-0}" = "1" ]; then
+  timeout -k 10 600 python tools/sweep_hg.py > gpurun_out/sweep_hg.log 2>&1
+  rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep_hg.log; [ "$rc" -eq 0 ] || exit $rc
+fi
+if [ "${PMC:-0}" = "1" ]; then
+  timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o pmc --output-format csv -- \
+      python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_fetch.log 2>&1
+  rc=$?; echo "pmc fetch rc=$rc"; [ "$rc" -eq 0 ] || exit $rc
+  timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o pmc --output-format csv -- \
+      python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_write.log 2>&1
+  rc=$?; echo "pmc write rc=$rc"; [ "$rc" -eq 0 ] || exit $rc
 fi
 exit 0
