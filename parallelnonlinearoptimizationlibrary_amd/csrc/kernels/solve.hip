@@ -1,10 +1,11 @@
 // solve.hip -- the damped LM solve, sigma = A^{-1} rhs (replaces luSolve, LevenbergMarquardt.cpp:83).
 //
 // A = J^T J + lambda diag(J^T J) is symmetric positive definite whenever J has full column
-// rank, so the fast path is a blocked right-looking Cholesky (nb = 64):
-//   k_potrf_diag   factor the 64 x 64 diagonal block in LDS (one workgroup)
-//   k_trsm_panel   L21 = A21 L11^{-T}, one row per thread, row held in registers
-//   syrk (MODE 1)  A22 -= L21 L21^T on the lower tiles, fp64 MFMA (syrk.hip)
+// rank, so the fast path is a tiled Cholesky (64 x 64 tiles) run as ONE persistent launch:
+//   k_chol_dag     POTRF / TRSM / UPDATE tile tasks from an atomic work queue, ordered with
+//                  one step of lookahead, dependencies tracked by per-tile version flags
+// (method 3 runs the same factorisation as per-panel launches: k_potrf_diag, k_trsm_panel
+// and the MODE-1 MFMA SYRK of syrk.hip, kept for comparison), then
 //   k_trsv_fwd/bwd forward / backward substitution: a workgroup per 64-row block, blocks
 //                  chained by agent-scope ready flags
 // A non-positive (or NaN) pivot flips to Gaussian elimination with partial pivoting in the
@@ -12,10 +13,16 @@
 // the small ExampleObjectives problems are bitwise equal to the CPU path.
 #include "../pnol_internal.hpp"
 
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
 namespace pnol {
 namespace {
 
 constexpr int kNB = 64;
+constexpr int kSpinCap = 1 << 24;   // ~1 s of polling: a broken chain ends the kernel, not the GPU
+constexpr int kInfoChainTimeout = -7;
 
 // ---- Cholesky ---------------------------------------------------------------------------
 // Diagonal block, one wave: lane t holds row t of the 64 x 64 block in registers (fully
@@ -79,45 +86,50 @@ __device__ __forceinline__ void stage_block(double (*S)[kNB + 1], const double* 
     }
 }
 
-// 256 threads: all stage the block, wave 0 factors it in registers.
-__global__ __launch_bounds__(256) void k_potrf_diag(double* __restrict__ A, long lda, int k0, int nbe,
-                                                    int* __restrict__ info) {
-    __shared__ double S[kNB][kNB + 1];
-    __shared__ __attribute__((aligned(16))) double col[kNB];
+// Factor the diagonal tile at (k0, k0) in place (256 threads: all stage, wave 0 factors in
+// registers).  Returns false (uniformly) and sets *info on a non-positive pivot.
+__device__ __forceinline__ bool potrf_tile(double* __restrict__ A, long lda, int k0, int nbe, int* info,
+                                           double (*S)[kNB + 1], double* __restrict__ col, int* flag_sh) {
     const int t = threadIdx.x;
     stage_block(S, A, lda, k0, k0, k0 + nbe - 1, k0 + nbe - 1, [nbe](int r, int c, double v) {
         return (r < nbe && c < nbe) ? (c <= r ? v : 0.0) : (r == c ? 1.0 : 0.0);
     });
+    if (t == 0) *flag_sh = 0;
     __syncthreads();
-    if (t >= 64 || *info != 0) return;   // wave 0 factors; an earlier block may have failed
-    double a[kNB];
+    if (t < 64) {
+        double a[kNB];
 #pragma unroll
-    for (int k = 0; k < kNB; ++k) a[k] = S[t][k];
-    bool bad = false;
-    potrf_step<0>(a, col, t, bad);
-    if (bad) {
-        if (t == 0) *info = k0 + 1;
-        return;
+        for (int k = 0; k < kNB; ++k) a[k] = S[t][k];
+        bool bad = false;
+        potrf_step<0>(a, col, t, bad);
+        if (bad) {
+            if (t == 0) {
+                *flag_sh = 1;
+                atomicExch(info, k0 + 1);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kNB; ++k) S[t][k] = a[k];
+        }
     }
+    __syncthreads();
+    if (*flag_sh) return false;
+    const int c = t & 63, rq = t >> 6;
 #pragma unroll
-    for (int k = 0; k < kNB; ++k) S[t][k] = a[k];
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll 16
-    for (int r = 0; r < kNB; ++r)
-        if (r < nbe && t <= r) A[(long)(k0 + r) * lda + k0 + t] = S[r][t];
+    for (int i = 0; i < 16; ++i) {
+        const int r = rq + 4 * i;
+        if (r < nbe && c <= r) A[(long)(k0 + r) * lda + k0 + c] = S[r][c];
+    }
+    return true;
 }
 
-// Panel below the diagonal block: x L11^T = a for every row, one thread per row with the
-// row in registers (fully unrolled right-looking substitution, L11 read as LDS broadcasts).
-// 64 rows per 256-thread workgroup: all waves stage L11 and the rows through LDS (coalesced
-// 512-byte row segments, loads batched), wave 0 solves, all waves store.
-__global__ __launch_bounds__(256) void k_trsm_panel(double* __restrict__ A, long lda, int n, int k0, int nbe,
-                                                    const int* __restrict__ info) {
-    __shared__ double L[kNB][kNB + 1];
-    __shared__ double X[kNB][kNB + 1];
+// One 64-row block of the panel below a factored diagonal tile: x L11^T = a, one thread per
+// row with the row in registers (fully unrolled right-looking substitution, L11 read as LDS
+// broadcasts).  All waves stage L11 and the rows (coalesced 512-byte row segments, loads
+// batched), wave 0 solves, all waves store.
+__device__ __forceinline__ void trsm_tile(double* __restrict__ A, long lda, int n, int k0, int nbe, int rbase,
+                                          double (*L)[kNB + 1], double (*X)[kNB + 1]) {
     const int t = threadIdx.x;
-    const int rbase = k0 + nbe + blockIdx.x * kNB;
     stage_block(L, A, lda, k0, k0, k0 + nbe - 1, k0 + nbe - 1, [nbe](int r, int c, double v) {
         return (r < nbe && c < nbe) ? v : (r == c ? 1.0 : 0.0);
     });
@@ -125,7 +137,6 @@ __global__ __launch_bounds__(256) void k_trsm_panel(double* __restrict__ A, long
         return (rbase + r < n && c < nbe) ? v : 0.0;
     });
     __syncthreads();
-    if (*info != 0) return;
     if (t < 64) {
         double x[kNB];
 #pragma unroll
@@ -148,18 +159,181 @@ __global__ __launch_bounds__(256) void k_trsm_panel(double* __restrict__ A, long
     }
 }
 
-// Stage a 64 x 64 diagonal block of L into LDS; rows/columns past nb are the identity so the
-// unrolled solves below have a fixed shape (padded entries of the right-hand side are 0).
-// 1024 threads: 4 unconditional loads each from clamped addresses, issued back to back.
-__device__ __forceinline__ void stage_diag(double (*T)[65], const double* __restrict__ L, long lda, int i0, int nb) {
-    const int t = threadIdx.x, c = t & 63, rq = t >> 6;
-    double v[4];
+__global__ __launch_bounds__(256) void k_potrf_diag(double* __restrict__ A, long lda, int k0, int nbe,
+                                                    int* __restrict__ info) {
+    __shared__ double S[kNB][kNB + 1];
+    __shared__ __attribute__((aligned(16))) double col[kNB];
+    __shared__ int flag_sh;
+    if (*info != 0) return;   // an earlier block already failed
+    potrf_tile(A, lda, k0, nbe, info, S, col, &flag_sh);
+}
+
+__global__ __launch_bounds__(256) void k_trsm_panel(double* __restrict__ A, long lda, int n, int k0, int nbe,
+                                                    const int* __restrict__ info) {
+    __shared__ double L[kNB][kNB + 1];
+    __shared__ double X[kNB][kNB + 1];
+    if (*info != 0) return;
+    trsm_tile(A, lda, n, k0, nbe, k0 + nbe + blockIdx.x * kNB, L, X);
+}
+
+// ---- Tile-DAG Cholesky: one persistent launch -------------------------------------------
+// The factorisation as a DAG of 64 x 64 tile tasks over the lower triangle (T = ceil(n/64)):
+//   POTRF(k)      factor tile (k,k)                          needs ver(k,k) >= k
+//   TRSM(k,i)     tile (i,k) <- A_ik L_kk^-T, i > k           needs ver(k,k) >= k+1, ver(i,k) >= k
+//   UPDATE(k,i,j) tile (i,j) -= L_ik L_jk^T, k < j <= i       needs ver(i,j) >= k,
+//                                                             ver(i,k) >= k+1, ver(j,k) >= k+1
+// ver(i,j) counts the operations completed on tile (i,j); each task bumps it by one.  Tasks
+// are numbered in a topological order with one step of lookahead (the updates of column k+1
+// and then POTRF(k+1) / TRSM(k+1,.) come before the rest of step k's updates) and handed out
+// by an atomic counter: a workgroup only ever waits on tasks claimed before its own, whose
+// owners are running, so the queue drains without assuming co-residency.  Waits are relaxed
+// sc1 polls + acquire fences; completion is a release fence by every wave, a workgroup
+// barrier and one flag store (MI355X_MICROARCH.md, cross-CU / cross-XCD visibility).
+enum { kTaskPotrf = 0, kTaskTrsm = 1, kTaskUpdate = 2 };
+constexpr int kUpdPad = 18;                 // LDS row stride of the 16-wide K substages
+constexpr int kUpdSub = kNB * kUpdPad;      // doubles per 64 x 16 substage
+
+__device__ __forceinline__ bool wait_ver(const int* v, int target, int* info) {
+    int it = 0;
+    while (__hip_atomic_load(v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((++it & 63) == 0) {
+            if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+            if (it > kSpinCap) {
+                atomicExch(info, kInfoChainTimeout);
+                return false;
+            }
+        }
+    }
+    return true;
+}
+
+// Stage the 64 x 64 tile (r0.., c0..) into four 64 x 16 K-substages (row stride 18 doubles):
+// thread t owns row t >> 2 and the 16 columns of substage t & 3.  Rows >= n read as 0.
+template <bool VEC>
+__device__ __forceinline__ void stage_upd(double* __restrict__ dst, const double* __restrict__ A, long lda, int n,
+                                          int r0, int c0) {
+    const int t = threadIdx.x, row = t >> 2, sub = t & 3;
+    const int gr = r0 + row;
+    const double* src = A + (long)min(gr, n - 1) * lda + c0 + sub * 16;
+    double2 v[8];
+    if (VEC) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = L[(long)(i0 + min(rq + 16 * i, nb - 1)) * lda + i0 + min(c, nb - 1)];
+        for (int q = 0; q < 8; ++q) v[q] = reinterpret_cast<const double2*>(src)[q];
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = rq + 16 * i;
-        T[r][c] = (r < nb && c < nb) ? (c <= r ? v[i] : 0.0) : (r == c ? 1.0 : 0.0);
+        for (int q = 0; q < 8; ++q) v[q] = make_double2(src[2 * q], src[2 * q + 1]);
+    }
+    double* d = dst + sub * kUpdSub + row * kUpdPad;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        reinterpret_cast<double2*>(d)[q] = gr < n ? v[q] : make_double2(0.0, 0.0);
+}
+
+// A_ij -= L_ik L_jk^T on fp64 MFMA: 4 waves as 2 x 2, each 32 x 32 (2 x 2 blocks of
+// v_mfma_f64_16x16x4_f64), C loaded straight into the accumulator layout (lane l, reg r ->
+// row (l >> 4) + 4 r, col l & 15) and the L_ik fragment negated so D = C + (-L_ik) L_jk^T.
+// Tile k is never the last (partial) tile, so K = 64 always; rows/cols >= n are skipped.
+template <bool VEC>
+__device__ __forceinline__ void update_tile(double* __restrict__ A, long lda, int n, int i, int j, int k,
+                                            double* __restrict__ P, double* __restrict__ Q) {
+    typedef double d4 __attribute__((ext_vector_type(4)));
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wr = wave >> 1, wc = wave & 1;
+    stage_upd<VEC>(P, A, lda, n, i * kNB, k * kNB);
+    if (i != j) stage_upd<VEC>(Q, A, lda, n, j * kNB, k * kNB);
+    const double* Qs = (i != j) ? Q : P;
+    const int orow = lane >> 4, ocol = lane & 15;
+    d4 acc[2][2];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gi = i * kNB + wr * 32 + mi * 16 + orow + 4 * r;
+                const int gj = j * kNB + wc * 32 + ni * 16 + ocol;
+                acc[mi][ni][r] = A[(long)min(gi, n - 1) * lda + min(gj, n - 1)];
+            }
+    __syncthreads();
+    const int frow = lane & 15, fk = lane >> 4;
+#pragma unroll
+    for (int sub = 0; sub < 4; ++sub) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            double a[2], b[2];
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi) a[mi] = -P[sub * kUpdSub + (wr * 32 + mi * 16 + frow) * kUpdPad + kk * 4 + fk];
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) b[ni] = Qs[sub * kUpdSub + (wc * 32 + ni * 16 + frow) * kUpdPad + kk * 4 + fk];
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gi = i * kNB + wr * 32 + mi * 16 + orow + 4 * r;
+                const int gj = j * kNB + wc * 32 + ni * 16 + ocol;
+                if (gi < n && gj < n && (i != j || gj <= gi)) A[(long)gi * lda + gj] = acc[mi][ni][r];
+            }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_chol_dag(double* __restrict__ A, long lda, int n, int T,
+                                                  const int4* __restrict__ tasks, int ntasks, int* counter, int* ver,
+                                                  int* info) {
+    __shared__ __attribute__((aligned(16))) double smem[2 * 4 * kUpdSub];   // 73.7 KB, shared by the task kinds
+    __shared__ int task_sh, ok_sh, flag_sh;
+    const int t = threadIdx.x;
+    for (;;) {
+        if (t == 0) task_sh = atomicAdd(counter, 1);
+        __syncthreads();
+        const int g = task_sh;
+        if (g >= ntasks) return;
+        const int4 tk = tasks[g];   // {kind, k, i, j}
+        const int kind = tk.x, k = tk.y, i = tk.z, j = tk.w;
+        if (t == 0) {
+            bool ok;
+            if (kind == kTaskPotrf) {
+                ok = wait_ver(ver + k * T + k, k, info);
+            } else if (kind == kTaskTrsm) {
+                ok = wait_ver(ver + k * T + k, k + 1, info) && wait_ver(ver + i * T + k, k, info);
+            } else {
+                ok = wait_ver(ver + i * T + j, k, info) && wait_ver(ver + i * T + k, k + 1, info) &&
+                     wait_ver(ver + j * T + k, k + 1, info);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            ok_sh = ok;
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (!ok_sh) return;
+        int vi = 0, vj = 0;
+        if (kind == kTaskPotrf) {
+            const int k0 = k * kNB, nbe = min(kNB, n - k0);
+            auto S = reinterpret_cast<double (*)[kNB + 1]>(smem);
+            if (!potrf_tile(A, lda, k0, nbe, info, S, smem + kNB * (kNB + 1), &flag_sh)) return;
+            vi = k; vj = k;
+        } else if (kind == kTaskTrsm) {
+            const int k0 = k * kNB;
+            auto L = reinterpret_cast<double (*)[kNB + 1]>(smem);
+            auto X = reinterpret_cast<double (*)[kNB + 1]>(smem + kNB * (kNB + 1));
+            trsm_tile(A, lda, n, k0, kNB, i * kNB, L, X);
+            vi = i; vj = k;
+        } else {
+            update_tile<VEC>(A, lda, n, i, j, k, smem, smem + 4 * kUpdSub);
+            vi = i; vj = j;
+        }
+        // publish: every wave drains and releases its stores, then one flag store
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        if (t == 0) __hip_atomic_store(ver + vi * T + vj, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -189,8 +363,6 @@ __device__ __forceinline__ void trsv_bwd_step(const double (*T)[65], double& zi,
 // reverse: workgroup b owns block w = nblk - 1 - b and reads the column blocks L_cw, c > w.
 // The memory traffic (one read of the lower triangle per direction) is spread over nblk CUs;
 // the critical path is one flag hop + one diagonal solve per block.
-constexpr int kSpinCap = 1 << 24;   // ~1 s of polling: a broken chain ends the kernel, not the GPU
-constexpr int kInfoChainTimeout = -7;
 
 // 256 threads: stage the lower-triangular diagonal block (identity padding) into T.
 __device__ __forceinline__ void stage_diag_256(double (*T)[kNB + 1], const double* __restrict__ L, long lda,
@@ -460,6 +632,49 @@ static int lu_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs, 
     return launch_check();
 }
 
+// Task list of the tile-DAG Cholesky in its lookahead topological order ({kind, k, i, j}).
+static std::vector<int4> chol_tasks(int T) {
+    std::vector<int4> v;
+    v.push_back(make_int4(kTaskPotrf, 0, 0, 0));
+    for (int i = 1; i < T; ++i) v.push_back(make_int4(kTaskTrsm, 0, i, 0));
+    for (int k = 0; k + 1 < T; ++k) {
+        for (int i = k + 1; i < T; ++i) v.push_back(make_int4(kTaskUpdate, k, i, k + 1));
+        v.push_back(make_int4(kTaskPotrf, k + 1, k + 1, k + 1));
+        for (int i = k + 2; i < T; ++i) v.push_back(make_int4(kTaskTrsm, k + 1, i, 0));
+        for (int j = k + 2; j < T; ++j)
+            for (int i = j; i < T; ++i) v.push_back(make_int4(kTaskUpdate, k, i, j));
+    }
+    return v;
+}
+
+// Factor A (lower triangle) in one persistent launch; *dinfo != 0 afterwards on failure.
+static int chol_factor_dag(pnol_ctx* ctx, double* A, int lda, int n, int* dinfo) {
+    const int T = (n + kNB - 1) / kNB;
+    const long ntasks = (long)T + (long)T * (T - 1) / 2 + (long)(T - 1) * T * (T + 1) / 6;
+    void *tasks_v = nullptr, *ver_v = nullptr;
+    PNOL_CHECK(ws_get(ctx, "chol_tasks", sizeof(int4) * (size_t)ntasks, &tasks_v));
+    if (tasks_v != ctx->chol_tasks || ctx->chol_tasks_T != T) {
+        std::vector<int4> h = chol_tasks(T);
+        if ((long)h.size() != ntasks) return PNOL_ERR_ARG;
+        PNOL_HIP(hipMemcpyAsync(tasks_v, h.data(), sizeof(int4) * h.size(), hipMemcpyHostToDevice, ctx->stream));
+        PNOL_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->chol_tasks = tasks_v;
+        ctx->chol_tasks_T = T;
+    }
+    PNOL_CHECK(ws_get(ctx, "chol_ver", sizeof(int) * (size_t)(T * T + 1), &ver_v));
+    int* ver = (int*)ver_v;
+    PNOL_HIP(hipMemsetAsync(ver, 0, sizeof(int) * (size_t)(T * T + 1), ctx->stream));
+    const int grid = (int)std::min<long>(ntasks, 2L * (ctx->num_cu > 0 ? ctx->num_cu : 256));
+    const bool vec = (lda % 2) == 0 && (reinterpret_cast<uintptr_t>(A) & 15u) == 0;
+    if (vec)
+        hipLaunchKernelGGL((k_chol_dag<true>), dim3(grid), dim3(256), 0, ctx->stream, A, (long)lda, n, T,
+                           (const int4*)tasks_v, (int)ntasks, ver + T * T, ver, dinfo);
+    else
+        hipLaunchKernelGGL((k_chol_dag<false>), dim3(grid), dim3(256), 0, ctx->stream, A, (long)lda, n, T,
+                           (const int4*)tasks_v, (int)ntasks, ver + T * T, ver, dinfo);
+    return launch_check();
+}
+
 // L L^T sigma = rhs with the factor in the lower triangle of A (two flag-chained launches).
 static int chol_trsv(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo) {
     const int nblk = (n + kNB - 1) / kNB;
@@ -490,6 +705,8 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
     int* dinfo = (int*)dinfo_v;
     int used = 0;
     if (method == 0) method = (n <= PNOL_SEQ_MAX) ? 2 : 1;
+    const bool multi_launch = method == 3;   // per-panel launches instead of the tile DAG
+    if (method == 3) method = 1;
     if (method == 1) {
         // keep a copy of A so a failed factorisation can fall back to LU on the original
         void* Acopy = nullptr;
@@ -498,7 +715,8 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
         hipLaunchKernelGGL(k_copy_matrix, dim3((int)std::min<long>((total + 255) / 256, 4096)), dim3(256), 0,
                            ctx->stream, (const double*)A, (long)lda, (double*)Acopy, n);
         hipLaunchKernelGGL(k_set_int, dim3(1), dim3(1), 0, ctx->stream, dinfo, 0);
-        for (int k0 = 0; k0 < n; k0 += kNB) {
+        if (!multi_launch) PNOL_CHECK(chol_factor_dag(ctx, A, lda, n, dinfo));
+        for (int k0 = 0; multi_launch && k0 < n; k0 += kNB) {
             const int nbe = std::min(kNB, n - k0);
             hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(256), 0, ctx->stream, A, (long)lda, k0, nbe, dinfo);
             const int below = n - k0 - nbe;

@@ -44,6 +44,8 @@ struct pnol_ctx {
     size_t pinned_bytes = 0;
     int* solve_flags = nullptr;     // per-block ready flags of the triangular solves (workspace)
     int solve_epoch = 0;            // value the flags of the current solve are set to
+    void* chol_tasks = nullptr;     // uploaded tile-DAG task table (workspace) and its tile count
+    int chol_tasks_T = 0;
 };
 
 struct pnol_dobj {

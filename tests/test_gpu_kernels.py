@@ -163,13 +163,30 @@ def test_jtj_mfma_layout_asymmetric(ctx):
     assert np.array_equal(A, J.T @ J)
 
 
+@pytest.mark.parametrize("method", [1, 3])
 @pytest.mark.parametrize("n", [65, 100, 129, 777, 1000, 2048, 3001])
-def test_cholesky_solve(ctx, n):
+def test_cholesky_solve(ctx, n, method):
+    """method 1: one persistent tile-DAG launch; method 3: per-panel launches."""
     rng = np.random.default_rng(n)
     J = rng.standard_normal((2 * n, n))
     A = J.T @ J + np.eye(n)
     b = rng.standard_normal(n)
-    sigma, info = ctx.solve(ctx.tensor(A), ctx.tensor(b), method=1)
+    sigma, info = ctx.solve(ctx.tensor(A), ctx.tensor(b), method=method)
+    assert info == 1
+    x = np.linalg.solve(A, b)
+    assert np.linalg.norm(_np(sigma) - x) <= 1e-10 * np.linalg.norm(x) * np.linalg.cond(A)
+
+
+def test_cholesky_dag_odd_leading_dimension(ctx):
+    """Odd lda: the tile DAG's scalar staging path (no 16-byte loads)."""
+    rng = np.random.default_rng(77)
+    n = 300
+    J = rng.standard_normal((400, n))
+    A = J.T @ J + np.eye(n)
+    b = rng.standard_normal(n)
+    Ap = ctx.empty(n, n + 1)
+    Ap[:, :n] = ctx.tensor(A)
+    sigma, info = ctx.solve(Ap[:, :n], ctx.tensor(b), method=1)
     assert info == 1
     x = np.linalg.solve(A, b)
     assert np.linalg.norm(_np(sigma) - x) <= 1e-10 * np.linalg.norm(x) * np.linalg.cond(A)
@@ -206,9 +223,9 @@ def test_lu_multi_launch_bitwise(ctx, oracle):
     assert np.array_equal(_np(sigma), oracle.lusolve(A, b))
 
 
-def test_cholesky_falls_back_to_lu_on_indefinite(ctx, oracle):
+@pytest.mark.parametrize("n", [200, 1000])
+def test_cholesky_falls_back_to_lu_on_indefinite(ctx, oracle, n):
     rng = np.random.default_rng(9)
-    n = 200
     A = rng.standard_normal((n, n)); A = A + A.T   # symmetric indefinite
     b = rng.standard_normal(n)
     sigma, info = ctx.solve(ctx.tensor(A), ctx.tensor(b), method=0)
