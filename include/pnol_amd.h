@@ -96,6 +96,12 @@ int pnol_set_identity_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* 
  * and m <= 4096 use the reference summation order.  jtj_diag (nullable) receives (J^T J)_ii. */
 int pnol_jtj_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda,
                double* A, int lda, double* jtj_diag);
+/* LevMarqMPI's J^T J (LevenbergMarquardtMPI.cpp:64-78, replicated on every rank in the
+ * reference): the 128 x 128 tiles are split over the process communicator's ranks, each rank
+ * computes its tile range, one allgather of the packed tiles assembles A on every rank.
+ * Bitwise equal to pnol_jtj_d for any rank count; with one rank it is pnol_jtj_d. */
+int pnol_jtj_mpi_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda,
+                   double* A, int lda, double* jtj_diag);
 /* rhs = -(J^T F), LevenbergMarquardt.cpp:78-80 */
 int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
 /* sigma = A^{-1} rhs, replacing luSolve(A, rhs, sigma), LevenbergMarquardt.cpp:83.

@@ -65,6 +65,7 @@ _SIGS = {
     "pnol_bfgs_pass_d": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
     "pnol_set_identity_d": (_i, [_vp, _vp, _i, _i, _vp]),
     "pnol_jtj_d": (_i, [_vp, _vp, _i, _i, _i, _d, _vp, _i, _vp]),
+    "pnol_jtj_mpi_d": (_i, [_vp, _vp, _i, _i, _i, _d, _vp, _i, _vp]),
     "pnol_jtr_d": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
     "pnol_solve_d": (_i, [_vp, _vp, _i, _vp, _vp, _i, _i, C.POINTER(_i)]),
     "pnol_dobj_create": (_i, [_vp, _i, _i, _i, _dp, _sz, _dp, _sz, _d, C.POINTER(_vp)]),

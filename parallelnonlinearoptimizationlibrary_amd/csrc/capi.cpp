@@ -56,6 +56,12 @@ int pnol_jtj_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     return launch_jtj(ctx, JT, ldjt, m, n, lambda, A, lda, jtj_diag);
 }
 
+int pnol_jtj_mpi_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
+                   double* jtj_diag) {
+    PNOL_CHECK(set_device(ctx));
+    return launch_jtj_sharded(ctx, JT, ldjt, m, n, lambda, A, lda, jtj_diag);
+}
+
 int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs) {
     PNOL_CHECK(set_device(ctx));
     if (!JT || !F || !rhs || m <= 0 || n <= 0 || ldjt < m) return PNOL_ERR_ARG;

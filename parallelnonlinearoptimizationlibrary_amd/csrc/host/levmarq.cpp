@@ -82,9 +82,13 @@ class LMDevice {
                   "allgather(J)");
     }
 
-    // sigma = (J^T J + lambda diag(J^T J))^{-1} (-J^T F)   (LevenbergMarquardt.cpp:59-83)
-    void step(double lambda, std::vector<double>& sigma) {
-        check(pnol_jtj_d(ctx_, JT_.get(), ldjt_, m_, n_, lambda, A_.get(), lda_, nullptr), "jtj");
+    // sigma = (J^T J + lambda diag(J^T J))^{-1} (-J^T F)   (LevenbergMarquardt.cpp:59-83);
+    // LevMarqMPI splits the J^T J tiles over the ranks (bitwise the same A)
+    void step(double lambda, std::vector<double>& sigma, bool sharded) {
+        if (sharded && comm_size() > 1)
+            check(pnol_jtj_mpi_d(ctx_, JT_.get(), ldjt_, m_, n_, lambda, A_.get(), lda_, nullptr), "jtj");
+        else
+            check(pnol_jtj_d(ctx_, JT_.get(), ldjt_, m_, n_, lambda, A_.get(), lda_, nullptr), "jtj");
         check(pnol_jtr_d(ctx_, JT_.get(), ldjt_, m_, n_, F_.get(), rhs_.get()), "jtr");
         int info = 0;
         check(pnol_solve_d(ctx_, A_.get(), lda_, rhs_.get(), sigma_.get(), n_, 0, &info), "solve");
@@ -121,7 +125,7 @@ void lm_solve(MultiObjective* obj, const LMParams& P, bool sharded, std::vector<
     double xdiff2Norm = P.xMinDiff * 2;
     while (iter < P.maxIter) {
         dev.jacobian(obj, X, dX, sharded);
-        dev.step(lambda, sigma);
+        dev.step(lambda, sigma, sharded);
         Xprev = X;
         Fprev = F;
         dev.saveF();

@@ -16,6 +16,9 @@
 // The same tile kernel in "direct" mode (C = beta C + alpha X X^T on the lower tiles) is the
 // trailing update of the blocked Cholesky in solve.hip.
 #include "../pnol_internal.hpp"
+#include "../pnol_comm.hpp"
+
+#include <algorithm>
 
 namespace pnol {
 namespace {
@@ -78,12 +81,12 @@ template <int MODE, int TILE>
 __global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
                                                       int split_k, int kchunk, double* __restrict__ part,
                                                       double* __restrict__ C, long ldc, double alpha,
-                                                      double beta) {
+                                                      double beta, int tile0) {
     constexpr int WT = TILE / 2, NB = WT / 16;
     __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
 
-    const int blk = blockIdx.x;
-    const int t = blk / split_k;
+    const int blk = blockIdx.x;              // partial slot (local to this launch)
+    const int t = tile0 + blk / split_k;     // lower-triangle tile index
     const int sidx = blk % split_k;
     int ti, tj;
     tile_of(t, ti, tj);
@@ -172,6 +175,42 @@ __global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__
     }
 }
 
+// Tile-sharded J^T J (LevMarqMPI): sum one launch's partials per tile in the same fixed
+// order, packed[tl * 128^2 + e] = raw (J^T J) tile values (no Marquardt scaling).
+__global__ void k_syrk_reduce_packed(const double* __restrict__ part, int split_k, double* __restrict__ packed) {
+    const int tl = blockIdx.y;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < kTile * kTile; e += gridDim.x * blockDim.x) {
+        const double* p = part + ((long)tl * split_k) * kTile * kTile + e;
+        double v = 0.0;
+        for (int s = 0; s < split_k; ++s) v += p[(long)s * kTile * kTile];
+        packed[(long)tl * kTile * kTile + e] = v;
+    }
+}
+
+// Unpack the allgathered tile payloads (rank r's slot q holds tile r * tpr + q) into A:
+// lower triangle + mirror, A_ii = (1 + lambda) (J^T J)_ii -- the same writes as k_syrk_reduce.
+__global__ void k_syrk_unpack(const double* __restrict__ packed, int ntiles, int n, double lambda,
+                              double* __restrict__ A, long lda, double* __restrict__ diag_out) {
+    const int t = blockIdx.y;
+    if (t >= ntiles) return;
+    int ti, tj;
+    tile_of(t, ti, tj);
+    const double scale = 1 + lambda;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < kTile * kTile; e += gridDim.x * blockDim.x) {
+        const int r = e / kTile, c = e % kTile;
+        const int i = ti * kTile + r, j = tj * kTile + c;
+        if (i >= n || j >= n || j > i) continue;
+        const double v = packed[(long)t * kTile * kTile + e];
+        if (i == j) {
+            if (diag_out) diag_out[i] = v;
+            A[(long)i * lda + i] = scale * v;
+        } else {
+            A[(long)i * lda + j] = v;
+            A[(long)j * lda + i] = v;
+        }
+    }
+}
+
 __global__ void k_syrk_reduce(const double* __restrict__ part, int ntiles, int split_k, int n, double lambda,
                               double* __restrict__ A, long lda, double* __restrict__ diag_out) {
     const int t = blockIdx.y;
@@ -256,7 +295,7 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     {
         ScopedTimer tm(ctx, "syrk");
         hipLaunchKernelGGL((k_syrk_tile<0, kTile>), dim3(ntiles * split_k), dim3(256), 0, ctx->stream, JT, (long)ldjt, n, m,
-                           split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0);
+                           split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0, 0);
     }
     PNOL_CHECK(launch_check());
     ScopedTimer tm(ctx, "syrk_reduce");
@@ -275,7 +314,47 @@ int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, do
     const int nt = (nr + kT - 1) / kT;
     const int ntiles = nt * (nt + 1) / 2;
     hipLaunchKernelGGL((k_syrk_tile<1, kT>), dim3(ntiles), dim3(256), 0, ctx->stream, X, (long)ldx, nr, K, 1, K,
-                       (double*)nullptr, C, (long)ldc, alpha, 1.0);
+                       (double*)nullptr, C, (long)ldc, alpha, 1.0, 0);
+    return launch_check();
+}
+
+// J^T J with the 128 x 128 tiles split over the communicator's ranks (contiguous ranges of
+// tpr = ceil(ntiles / P) tiles), then one allgather of the packed tiles (P * tpr * 128 KB).
+// The split-K factor comes from the global tile count, so every tile is summed exactly as on
+// one GPU: A is bitwise independent of P.  n <= PNOL_SEQ_MAX keeps the replicated
+// reference-order kernel.
+int launch_jtj_sharded(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
+                       double* jtj_diag) {
+    const int P = comm_size(), rank = comm_rank();
+    if (P <= 1 || (n <= PNOL_SEQ_MAX && m <= 4096)) return launch_jtj(ctx, JT, ldjt, m, n, lambda, A, lda, jtj_diag);
+    if (!JT || !A || m <= 0 || n <= 0 || ldjt < m || lda < n) return PNOL_ERR_ARG;
+    const int nt = (n + kTile - 1) / kTile;
+    const int ntiles = nt * (nt + 1) / 2;
+    const int split_k = choose_split_k(ntiles, m, ctx->num_cu);
+    int kchunk = (m + split_k - 1) / split_k;
+    kchunk = (kchunk + kTK - 1) / kTK * kTK;
+    const int tpr = (ntiles + P - 1) / P;
+    const int t0 = std::min(ntiles, rank * tpr), cnt = std::min(ntiles, t0 + tpr) - t0;
+    const size_t tile_elems = (size_t)kTile * kTile;
+    void *part = nullptr, *packed = nullptr;
+    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)std::max(cnt, 1) * split_k * tile_elems, &part));
+    PNOL_CHECK(ws_get(ctx, "syrk_packed", sizeof(double) * (size_t)P * tpr * tile_elems, &packed));
+    double* mine = (double*)packed + (size_t)rank * tpr * tile_elems;
+    if (cnt > 0) {
+        {
+            ScopedTimer tm(ctx, "syrk");
+            hipLaunchKernelGGL((k_syrk_tile<0, kTile>), dim3(cnt * split_k), dim3(256), 0, ctx->stream, JT, (long)ldjt,
+                               n, m, split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0, t0);
+        }
+        PNOL_CHECK(launch_check());
+        hipLaunchKernelGGL(k_syrk_reduce_packed, dim3(8, cnt), dim3(256), 0, ctx->stream, (const double*)part, split_k,
+                           mine);
+        PNOL_CHECK(launch_check());
+    }
+    PNOL_CHECK(comm_allgather_device(ctx, mine, (double*)packed, (size_t)tpr * tile_elems));
+    ScopedTimer tm(ctx, "syrk_reduce");
+    hipLaunchKernelGGL(k_syrk_unpack, dim3(8, ntiles), dim3(256), 0, ctx->stream, (const double*)packed, ntiles, n,
+                       lambda, A, (long)lda, jtj_diag);
     return launch_check();
 }
 

@@ -113,6 +113,8 @@ int launch_set_identity(pnol_ctx* ctx, double* D, int ldd, int n, const double* 
 
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                double* jtj_diag);
+int launch_jtj_sharded(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
+                       double* jtj_diag);
 int launch_jtr(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
 // C(lower tiles of rows [r0, r0+nr)) = beta*C + alpha * X X^T  over K columns (MFMA)
 int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, double alpha, double* C,

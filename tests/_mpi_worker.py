@@ -1,0 +1,40 @@
+"""Worker for tests/test_gpu_mpi.py: one rank of LevMarqMPI on the (shared) GPU with the
+host communicator backend (torch.distributed gloo allgather).  Writes its results to
+<out>/rank<r>.npz.  Started as a child process by the test (never exec'd in place)."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    out, m, n = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_levmarq
+    from parallelnonlinearoptimizationlibrary_amd.dist import HostComm
+    comm = HostComm(rank, world)
+    ctx = Context(0)
+    obj = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+    X, F0, FO, res = run_levmarq(obj, np.zeros(n), (0.001, 10.0, 1e-7, 5, 0.0, -1), which=1)
+    # the sharded J^T J kernel on its own, on a random JT
+    rng = np.random.default_rng(11)
+    JT = ctx.tensor(rng.standard_normal((n, m)))
+    A = ctx.empty(n, n)
+    diag = ctx.empty(n)
+    L.check(L.lib().pnol_jtj_mpi_d(ctx.h, JT.data_ptr(), m, m, n, 0.25, A.data_ptr(), n, diag.data_ptr()),
+            "pnol_jtj_mpi_d")
+    ctx.synchronize()
+    np.savez(os.path.join(out, f"rank{rank}.npz"), X=X, A=A.cpu().numpy(), diag=diag.cpu().numpy())
+    comm.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,61 @@
+"""LevMarqMPI on the device with more than one rank: two processes share the box's one GPU and
+exchange through the host communicator backend (gloo allgather callback).  The sharded FD
+Jacobian (column blocks + allgather) and the tile-sharded J^T J (pnol_jtj_mpi_d) must give
+results bitwise equal to the single-rank device run -- the reference's MPI results are
+likewise independent of the rank count."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_levmarq_mpi_ranks_bitwise_equal_single(tmp_path, world):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_levmarq
+    m, n = 2000, 300     # 6 J^T J tiles: uneven tile ranges at world = 3 / 4
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", PNOL_DEVICE="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_mpi_worker.py"), str(tmp_path),
+                                       str(m), str(n)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    outs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(o.decode(errors="replace"))
+    assert all(p.returncode == 0 for p in procs), "\n".join(o[-3000:] for o in outs)
+
+    ctx = Context(0)
+    obj = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+    X1, *_ = run_levmarq(obj, np.zeros(n), (0.001, 10.0, 1e-7, 5, 0.0, -1), which=0)
+    rng = np.random.default_rng(11)
+    JT = ctx.tensor(rng.standard_normal((n, m)))
+    A1, d1 = ctx.jtj(JT, 0.25, want_diag=True)
+    A1, d1 = A1.cpu().numpy(), d1.cpu().numpy()
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        assert np.array_equal(z["X"], X1), r
+        assert np.array_equal(z["A"], A1), r
+        assert np.array_equal(z["diag"], d1), r
