@@ -105,9 +105,9 @@ int pnol_jtj_mpi_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, doub
 /* rhs = -(J^T F), LevenbergMarquardt.cpp:78-80 */
 int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
 /* sigma = A^{-1} rhs, replacing luSolve(A, rhs, sigma), LevenbergMarquardt.cpp:83.
- * method 0 = auto (n <= PNOL_SEQ_MAX: reference LU; else tiled Cholesky, LU on a non-positive
- * pivot), 1 = Cholesky (one persistent tile-DAG launch), 2 = LU with partial pivoting
- * (reference operation order), 3 = Cholesky as per-panel launches (comparison path).
+ * method 0 = auto (n <= PNOL_SEQ_MAX: reference LU; else blocked Cholesky, LU on a non-positive
+ * pivot), 1 = Cholesky (per-panel launches), 2 = LU with partial pivoting (reference operation
+ * order), 3 = Cholesky as one persistent tile-DAG launch (experimental).
  * A is consumed (overwritten by its factor).  info (host, nullable) gets the method used
  * (1 or 2) or -1 on a singular matrix. */
 int pnol_solve_d(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n,

@@ -13,10 +13,14 @@
 //   k_scalar_fd_values   scalar objectives: one thread per point, x staged through LDS
 //   k_multi_fd           ExpCurve / Cubic (tiny n): one thread per (point, residual)
 //   k_linres_eval        r = A x - y: one thread per residual row, A tiles staged in LDS
-//   k_linres_fd          all points of a block at once: a register-tiled fp64 VALU GEMM
+//   k_linres_fd2         all points of a block at once: a register-tiled fp64 VALU GEMM
 //                        R = A [x + h_j e_j]_j, epilogue J = ((R - y) - F0) / h  (no MFMA:
-//                        this is the objective, evaluated like user code would be)
+//                        this is the objective, evaluated like user code would be); tiles
+//                        resume from base-chain checkpoints and broadcast x outside the
+//                        perturbation window (k_linres_fd: the full-B-tile form)
 #include "../pnol_internal.hpp"
+
+#include <cstdlib>
 
 namespace pnol {
 namespace {
@@ -311,6 +315,131 @@ __global__ __launch_bounds__(256) void k_linres_fd(const double* __restrict__ A,
     }
 }
 
+// Batched FD GEMM, x-broadcast form.  Thread (ty, tx) = (t >> 4, t & 15) owns RM rows and
+// PN points (RM * PN accumulators); workgroup tile (16 RM) rows x (16 PN) points.  The B
+// operand of this GEMM is x with ONE perturbed entry per point, and with prefix sharing all
+// of a tile's perturbed columns lie in its first few K stages.  Those stages ("window"
+// stages) build the full 16 x BN B tile in LDS; every later stage multiplies by x[k]
+// broadcast to all points, so per k a thread reads RM A values and one x value for RM * PN
+// fmas.  Each accumulator is still the objective's sequential fma chain: bit-identical to
+// k_linres_fd and to the host evaluation.
+template <bool EVEN, int RM, int PN>
+__global__ __launch_bounds__(256) void k_linres_fd2(const double* __restrict__ A, const double* __restrict__ y,
+                                                    const double* __restrict__ x, const double* __restrict__ h, int m,
+                                                    int n, int j0, int cnt, const double* __restrict__ F0,
+                                                    const double* __restrict__ C, double* __restrict__ JT, long ldjt) {
+    constexpr int BM = 16 * RM, BN = 16 * PN;
+    constexpr int TPR = 256 / BM;      // threads staging one A row
+    constexpr int KPT = kBK / TPR;     // consecutive k per staging thread (== RM)
+    __shared__ __attribute__((aligned(16))) double As[kBK][BM];
+    __shared__ __attribute__((aligned(16))) double Bs[kBK][BN];
+    __shared__ __attribute__((aligned(16))) double xs[kBK];
+    const int nmt = (m + BM - 1) / BM, nnt = (cnt + BN - 1) / BN;
+    const int v = xcd_remap(blockIdx.x, nmt * nnt);
+    const int mt = v / nnt, nt = v % nnt;
+    const int m0 = mt * BM, pbase = nt * BN;
+    const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
+    const int jfirst = j0 + pbase, jlast = j0 + min(pbase + BN, cnt) - 1;   // perturbed columns of the tile
+    const int ks = (jfirst / kBK) * kBK;
+
+    double acc[RM][PN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+        const int row = min(m0 + ty * RM + i, m - 1);
+        const double c0 = ks > 0 ? C[(long)(ks / kCkpt) * m + row] : 0.0;
+#pragma unroll
+        for (int j = 0; j < PN; ++j) acc[i][j] = c0;
+    }
+
+    const int lrow = t / TPR, lk = (t % TPR) * KPT;
+    const long arow = (long)min(m0 + lrow, m - 1) * n;
+    const bool rowok = m0 + lrow < m;
+    double areg[KPT];
+    auto load_a = [&](int k0) {
+        if (EVEN && rowok && k0 + kBK <= n) {
+            const double2* p = reinterpret_cast<const double2*>(A + arow + k0 + lk);
+#pragma unroll
+            for (int q = 0; q < KPT / 2; ++q) { double2 w = p[q]; areg[2 * q] = w.x; areg[2 * q + 1] = w.y; }
+        } else {
+#pragma unroll
+            for (int q = 0; q < KPT; ++q) {
+                const int k = k0 + lk + q;
+                areg[q] = (rowok && k < n) ? A[arow + k] : 0.0;
+            }
+        }
+    };
+    const int nk = (n + kBK - 1) / kBK;
+    load_a(ks);
+    for (int kc = ks / kBK; kc < nk; ++kc) {
+        const int k0 = kc * kBK;
+        const bool window = k0 <= jlast && k0 + kBK > jfirst;   // uniform over the workgroup
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < KPT; ++q) As[lk + q][lrow] = areg[q];
+        if (t < kBK) xs[t] = k0 + t < n ? x[k0 + t] : 0.0;
+        if (window) {
+#pragma unroll
+            for (int q = 0; q < PN; ++q) {
+                const int e = t + 256 * q;
+                const int k = e / BN, jj = e % BN;
+                const int kk = k0 + k;
+                const int p = pbase + jj;
+                const int jcol = j0 + p;
+                double val = kk < n ? x[kk] : 0.0;
+                if (p < cnt && kk == jcol) val = x[kk] + h[jcol];
+                Bs[k][jj] = val;
+            }
+        }
+        __syncthreads();
+        if (kc + 1 < nk) load_a(k0 + kBK);
+        if (window) {
+#pragma unroll
+            for (int k = 0; k < kBK; ++k) {
+                double a[RM], b[PN];
+                const double2* ap = reinterpret_cast<const double2*>(&As[k][ty * RM]);
+#pragma unroll
+                for (int q = 0; q < RM / 2; ++q) { double2 w = ap[q]; a[2 * q] = w.x; a[2 * q + 1] = w.y; }
+                const double2* bp = reinterpret_cast<const double2*>(&Bs[k][tx * PN]);
+#pragma unroll
+                for (int q = 0; q < PN / 2; ++q) { double2 w = bp[q]; b[2 * q] = w.x; b[2 * q + 1] = w.y; }
+#pragma unroll
+                for (int i = 0; i < RM; ++i)
+#pragma unroll
+                    for (int j = 0; j < PN; ++j) acc[i][j] = fma(a[i], b[j], acc[i][j]);
+                if (k & 1) __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kBK; ++k) {
+                double a[RM];
+                const double2* ap = reinterpret_cast<const double2*>(&As[k][ty * RM]);
+#pragma unroll
+                for (int q = 0; q < RM / 2; ++q) { double2 w = ap[q]; a[2 * q] = w.x; a[2 * q + 1] = w.y; }
+                const double xk = xs[k];
+#pragma unroll
+                for (int i = 0; i < RM; ++i)
+#pragma unroll
+                    for (int j = 0; j < PN; ++j) acc[i][j] = fma(a[i], xk, acc[i][j]);
+                // bound the loads the scheduler hoists ahead (registers, not latency, limit us)
+                if (k & 1) __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+    // epilogue: F = acc - y; J = (F - F0) / h
+#pragma unroll
+    for (int j = 0; j < PN; ++j) {
+        const int p = pbase + tx * PN + j;
+        if (p >= cnt) continue;
+        const double hj = h[j0 + p];
+        double* out = JT + (long)p * ldjt;
+#pragma unroll
+        for (int i = 0; i < RM; ++i) {
+            const int row = m0 + ty * RM + i;
+            if (row < m) out[row] = ((acc[i][j] - y[row]) - F0[row]) / hj;
+        }
+    }
+}
+
 // ---- synthetic data, splitmix64 counter stream ---------------------------
 __global__ void k_synth_quadratic(unsigned long long seed, int n, double bscale, double* d, double* b) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -417,14 +546,41 @@ int launch_fd_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
                                    ctx->stream, o->p0, x, o->p1, o->m, o->n, f0_out, (double*)C);
         }
         PNOL_CHECK(launch_check());
-        const int nmt = (o->m + kBM - 1) / kBM, nnt = (cnt + kBN - 1) / kBN;
+        // PNOL_FD_KERNEL selects the FD GEMM (tuning): 1 = 128 x 64-point tile with a full B tile
+        // every stage; 2 = x-broadcast 128 x 128 (8 x 8 per thread); 3 (default) = x-broadcast
+        // 64 x 128 (4 x 8 per thread).
+        static const int fdk = [] {
+            const char* e = std::getenv("PNOL_FD_KERNEL");
+            const int v = e ? std::atoi(e) : 3;
+            return (v >= 1 && v <= 3) ? v : 3;
+        }();
+        const bool even = (o->n % 2) == 0;
         ScopedTimer tm(ctx, "fd_jacobian");
-        if ((o->n % 2) == 0)
-            hipLaunchKernelGGL((k_linres_fd<true>), dim3(nmt * nnt), dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
-                               o->n, j0, cnt, (const double*)F0, (const double*)C, JT, (long)ldjt);
-        else
-            hipLaunchKernelGGL((k_linres_fd<false>), dim3(nmt * nnt), dim3(256), 0, ctx->stream, o->p0, o->p1, x, h,
-                               o->m, o->n, j0, cnt, (const double*)F0, (const double*)C, JT, (long)ldjt);
+        const double* F0c = F0;
+        const double* Cc = (const double*)C;
+        auto nwg = [&](int bm, int bn) { return dim3(((o->m + bm - 1) / bm) * ((cnt + bn - 1) / bn)); };
+        if (fdk == 1) {
+            if (even)
+                hipLaunchKernelGGL((k_linres_fd<true>), nwg(kBM, kBN), dim3(256), 0, ctx->stream, o->p0, o->p1, x, h,
+                                   o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
+            else
+                hipLaunchKernelGGL((k_linres_fd<false>), nwg(kBM, kBN), dim3(256), 0, ctx->stream, o->p0, o->p1, x, h,
+                                   o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
+        } else if (fdk == 2) {
+            if (even)
+                hipLaunchKernelGGL((k_linres_fd2<true, 8, 8>), nwg(128, 128), dim3(256), 0, ctx->stream, o->p0, o->p1,
+                                   x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
+            else
+                hipLaunchKernelGGL((k_linres_fd2<false, 8, 8>), nwg(128, 128), dim3(256), 0, ctx->stream, o->p0, o->p1,
+                                   x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
+        } else {
+            if (even)
+                hipLaunchKernelGGL((k_linres_fd2<true, 4, 8>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0, o->p1,
+                                   x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
+            else
+                hipLaunchKernelGGL((k_linres_fd2<false, 4, 8>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0, o->p1,
+                                   x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
+        }
         return launch_check();
     }
     if (compute_f0) PNOL_CHECK(launch_dobj_eval(ctx, o, x, F0));

@@ -1,11 +1,14 @@
 // solve.hip -- the damped LM solve, sigma = A^{-1} rhs (replaces luSolve, LevenbergMarquardt.cpp:83).
 //
 // A = J^T J + lambda diag(J^T J) is symmetric positive definite whenever J has full column
-// rank, so the fast path is a tiled Cholesky (64 x 64 tiles) run as ONE persistent launch:
-//   k_chol_dag     POTRF / TRSM / UPDATE tile tasks from an atomic work queue, ordered with
-//                  one step of lookahead, dependencies tracked by per-tile version flags
-// (method 3 runs the same factorisation as per-panel launches: k_potrf_diag, k_trsm_panel
-// and the MODE-1 MFMA SYRK of syrk.hip, kept for comparison), then
+// rank, so the fast path is a blocked right-looking Cholesky (nb = 64), one panel per step:
+//   k_potrf_diag   factor the 64 x 64 diagonal block (rows in registers, one wave)
+//   k_trsm_panel   L21 = A21 L11^{-T}, one row per thread, row held in registers
+//   syrk (MODE 1)  A22 -= L21 L21^T on 64 x 64 lower tiles, fp64 MFMA (syrk.hip)
+// Method 3 runs the same factorisation as ONE persistent launch (k_chol_dag: POTRF / TRSM /
+// UPDATE tile tasks from an atomic work queue, lookahead order, per-tile version flags);
+// it is parity-tested but slower today (2.5 vs 1.9 ms at n = 2048: its critical path pays a
+// flag hop per task and runs at one wave per SIMD).  Then
 //   k_trsv_fwd/bwd forward / backward substitution: a workgroup per 64-row block, blocks
 //                  chained by agent-scope ready flags
 // A non-positive (or NaN) pivot flips to Gaussian elimination with partial pivoting in the
@@ -287,7 +290,7 @@ __device__ __forceinline__ void update_tile(double* __restrict__ A, long lda, in
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_chol_dag(double* __restrict__ A, long lda, int n, int T,
                                                   const int4* __restrict__ tasks, int ntasks, int* counter, int* ver,
-                                                  int* info) {
+                                                  int* info, int dbg) {
     __shared__ __attribute__((aligned(16))) double smem[2 * 4 * kUpdSub];   // 73.7 KB, shared by the task kinds
     __shared__ int task_sh, ok_sh, flag_sh;
     const int t = threadIdx.x;
@@ -298,7 +301,7 @@ __global__ __launch_bounds__(256) void k_chol_dag(double* __restrict__ A, long l
         if (g >= ntasks) return;
         const int4 tk = tasks[g];   // {kind, k, i, j}
         const int kind = tk.x, k = tk.y, i = tk.z, j = tk.w;
-        if (t == 0) {
+        if (t == 0 && !(dbg & 2)) {
             bool ok;
             if (kind == kTaskPotrf) {
                 ok = wait_ver(ver + k * T + k, k, info);
@@ -311,11 +314,15 @@ __global__ __launch_bounds__(256) void k_chol_dag(double* __restrict__ A, long l
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             ok_sh = ok;
         }
+        if (t == 0 && (dbg & 2)) ok_sh = 1;
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (!ok_sh) return;
         int vi = 0, vj = 0;
-        if (kind == kTaskPotrf) {
+        if (dbg & 1) {
+            vi = kind == kTaskUpdate ? i : (kind == kTaskTrsm ? i : k);
+            vj = kind == kTaskUpdate ? j : k;
+        } else if (kind == kTaskPotrf) {
             const int k0 = k * kNB, nbe = min(kNB, n - k0);
             auto S = reinterpret_cast<double (*)[kNB + 1]>(smem);
             if (!potrf_tile(A, lda, k0, nbe, info, S, smem + kNB * (kNB + 1), &flag_sh)) return;
@@ -333,7 +340,7 @@ __global__ __launch_bounds__(256) void k_chol_dag(double* __restrict__ A, long l
         // publish: every wave drains and releases its stores, then one flag store
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __syncthreads();
-        if (t == 0) __hip_atomic_store(ver + vi * T + vj, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0 && !(dbg & 4)) __hip_atomic_store(ver + vi * T + vj, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -666,12 +673,17 @@ static int chol_factor_dag(pnol_ctx* ctx, double* A, int lda, int n, int* dinfo)
     PNOL_HIP(hipMemsetAsync(ver, 0, sizeof(int) * (size_t)(T * T + 1), ctx->stream));
     const int grid = (int)std::min<long>(ntasks, 2L * (ctx->num_cu > 0 ? ctx->num_cu : 256));
     const bool vec = (lda % 2) == 0 && (reinterpret_cast<uintptr_t>(A) & 15u) == 0;
+    static const int dbg = [] {   // temporary fault-bisection switch
+        const char* e = std::getenv("PNOL_DAG_DEBUG");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (dbg & 8) return PNOL_OK;   // skip the launch entirely
     if (vec)
         hipLaunchKernelGGL((k_chol_dag<true>), dim3(grid), dim3(256), 0, ctx->stream, A, (long)lda, n, T,
-                           (const int4*)tasks_v, (int)ntasks, ver + T * T, ver, dinfo);
+                           (const int4*)tasks_v, (int)ntasks, ver + T * T, ver, dinfo, dbg);
     else
         hipLaunchKernelGGL((k_chol_dag<false>), dim3(grid), dim3(256), 0, ctx->stream, A, (long)lda, n, T,
-                           (const int4*)tasks_v, (int)ntasks, ver + T * T, ver, dinfo);
+                           (const int4*)tasks_v, (int)ntasks, ver + T * T, ver, dinfo, dbg);
     return launch_check();
 }
 
@@ -705,7 +717,7 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
     int* dinfo = (int*)dinfo_v;
     int used = 0;
     if (method == 0) method = (n <= PNOL_SEQ_MAX) ? 2 : 1;
-    const bool multi_launch = method == 3;   // per-panel launches instead of the tile DAG
+    const bool multi_launch = method != 3;   // method 3: the tile-DAG launch (experimental)
     if (method == 3) method = 1;
     if (method == 1) {
         // keep a copy of A so a failed factorisation can fall back to LU on the original

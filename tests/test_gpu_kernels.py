@@ -166,7 +166,7 @@ def test_jtj_mfma_layout_asymmetric(ctx):
 @pytest.mark.parametrize("method", [1, 3])
 @pytest.mark.parametrize("n", [65, 100, 129, 777, 1000, 2048, 3001])
 def test_cholesky_solve(ctx, n, method):
-    """method 1: one persistent tile-DAG launch; method 3: per-panel launches."""
+    """method 1: per-panel launches; method 3: one persistent tile-DAG launch."""
     rng = np.random.default_rng(n)
     J = rng.standard_normal((2 * n, n))
     A = J.T @ J + np.eye(n)
@@ -177,8 +177,9 @@ def test_cholesky_solve(ctx, n, method):
     assert np.linalg.norm(_np(sigma) - x) <= 1e-10 * np.linalg.norm(x) * np.linalg.cond(A)
 
 
-def test_cholesky_dag_odd_leading_dimension(ctx):
-    """Odd lda: the tile DAG's scalar staging path (no 16-byte loads)."""
+@pytest.mark.parametrize("method", [1, 3])
+def test_cholesky_odd_leading_dimension(ctx, method):
+    """Odd lda: scalar staging paths (no 16-byte loads)."""
     rng = np.random.default_rng(77)
     n = 300
     J = rng.standard_normal((400, n))
@@ -186,7 +187,7 @@ def test_cholesky_dag_odd_leading_dimension(ctx):
     b = rng.standard_normal(n)
     Ap = ctx.empty(n, n + 1)
     Ap[:, :n] = ctx.tensor(A)
-    sigma, info = ctx.solve(Ap[:, :n], ctx.tensor(b), method=1)
+    sigma, info = ctx.solve(Ap[:, :n], ctx.tensor(b), method=method)
     assert info == 1
     x = np.linalg.solve(A, b)
     assert np.linalg.norm(_np(sigma) - x) <= 1e-10 * np.linalg.norm(x) * np.linalg.cond(A)
@@ -292,7 +293,8 @@ def test_fd_jacobian_cubic_bitwise_expcurve_close(ctx, oracle):
 
 
 @pytest.mark.parametrize("m,n,j0,cnt", [(300, 70, 0, 70), (300, 70, 13, 29), (1000, 129, 64, 65), (257, 33, 32, 1),
-                                       (700, 300, 0, 300), (700, 300, 37, 200), (130, 16, 0, 16), (130, 17, 16, 1)])
+                                       (700, 300, 0, 300), (700, 300, 37, 200), (130, 16, 0, 16), (130, 17, 16, 1),
+                                       (1500, 1000, 0, 1000), (513, 2048, 100, 700), (257, 400, 250, 150)])
 def test_fd_jacobian_linres_bitwise(ctx, oracle, m, n, j0, cnt):
     """Prefix-shared chains (tiles start from the base chain's 16-column checkpoints) are
     the same fma sequence as full-length evaluation: bitwise equal to the oracle's n+1 evals."""
