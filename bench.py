@@ -247,10 +247,11 @@ def main():
             "jtj": dict(roofline, ms=syrk_ms),
         }
         if hg:
-            rooflines["hg"] = {"kernel": "k_gemv_neg<2> (p = -D g)", "bound": "hbm", "achieved": hg["hg_GBps"],
+            rooflines["hg"] = {"kernel": "k_gemv_neg_wg<2,NT> (p = -D g, non-temporal 16-B loads)", "bound": "hbm",
+                               "achieved": hg["hg_GBps"],
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hg["hg_frac_of_hbm"],
                                "algorithmic_bytes": 8.0 * HG_N * HG_N + 16.0 * HG_N,
-                               "traffic": pmc.get("k_gemv_neg<2>", {}).get("traffic_bytes_per_launch"),
+                               "traffic": pmc.get("k_gemv_neg_wg<2, true>", {}).get("traffic_bytes_per_launch"),
                                "n": HG_N}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:

@@ -126,6 +126,98 @@ __global__ __launch_bounds__(256) void k_gemv_neg(const double* __restrict__ A, 
     }
 }
 
+// Workgroup-cooperative variant: a 256-thread workgroup owns R rows and its 4 waves take
+// interleaved 4 KiB super-chunks of each row (wave w: chunks w, w+4, ...), so the waves of a
+// workgroup stream one contiguous 16 KiB window of a row at a time and the chip keeps ~4x
+// fewer concurrent DRAM streams open than with a wave per row.  NT: non-temporal loads
+// (D is streamed once; keep it out of L2 / MALL).  Partial sums are combined in a fixed
+// order through LDS.
+template <int R, bool NT>
+__global__ __launch_bounds__(256) void k_gemv_neg_wg(const double* __restrict__ A, long lda, int rows, int cols,
+                                                     const double* __restrict__ x, double* __restrict__ y) {
+    __shared__ double part[4][R];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const long row0 = (long)blockIdx.x * R;
+    const double2* __restrict__ xv = reinterpret_cast<const double2*>(x);
+    const double2* arow[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        long rr = row0 + r < rows ? row0 + r : rows - 1;
+        arow[r] = reinterpret_cast<const double2*>(A + rr * lda);
+    }
+    double acc0[R], acc1[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) { acc0[r] = 0.0; acc1[r] = 0.0; }
+    const int pairs = cols >> 1;
+    constexpr int SC = kU * kWave;
+    const int nfull = pairs / SC;
+    auto ld = [&](const double2* p) -> double2 {
+        if (NT) {
+            double2 v;
+            v.x = __builtin_nontemporal_load(&p->x);
+            v.y = __builtin_nontemporal_load(&p->y);
+            return v;
+        }
+        return *p;
+    };
+    int sc = wave;
+    if (sc < nfull) {
+        double2 cur[R][kU], curx[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) curx[u] = xv[sc * SC + u * kWave + lane];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < kU; ++u) cur[r][u] = ld(&arow[r][sc * SC + u * kWave + lane]);
+        for (sc += 4; sc < nfull; sc += 4) {
+            double2 nxt[R][kU], nxtx[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) nxtx[u] = xv[sc * SC + u * kWave + lane];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int u = 0; u < kU; ++u) nxt[r][u] = ld(&arow[r][sc * SC + u * kWave + lane]);
+            gemv_fma<R>(cur, curx, acc0, acc1);
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int u = 0; u < kU; ++u) cur[r][u] = nxt[r][u];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) curx[u] = nxtx[u];
+        }
+        gemv_fma<R>(cur, curx, acc0, acc1);
+    }
+    if (wave == 0) {
+        for (int c = nfull * SC + lane; c < pairs; c += kWave) {
+            double2 xr = xv[c];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                double2 a = arow[r][c];
+                acc0[r] = fma(a.x, xr.x, acc0[r]);
+                acc1[r] = fma(a.y, xr.y, acc1[r]);
+            }
+        }
+        if ((cols & 1) && lane == 0) {
+            const double xl = x[cols - 1];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                long rr = row0 + r < rows ? row0 + r : rows - 1;
+                acc0[r] = fma(A[rr * lda + cols - 1], xl, acc0[r]);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const double s = wave_sum(acc0[r] + acc1[r]);
+        if (lane == 0) part[wave][r] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < R && row0 + threadIdx.x < rows) {
+        const int r = threadIdx.x;
+        y[row0 + r] = -((part[0][r] + part[1][r]) + (part[2][r] + part[3][r]));
+    }
+}
+
 // any lda / alignment: one wave per row, 8-byte loads, 4 in flight per lane
 __global__ __launch_bounds__(256) void k_gemv_neg_scalar(const double* __restrict__ A, long lda, int rows, int cols,
                                                          const double* __restrict__ x, double* __restrict__ y) {
@@ -260,7 +352,11 @@ __device__ __forceinline__ void pass_load(double2 (&d)[kGroup], const double* __
     for (int q = 0; q < kGroup; ++q) {
         const long row = min(r0 + q, n - 1);
         if (VEC) {
-            d[q] = *reinterpret_cast<const double2*>(D + row * ldd + colc);
+            // non-temporal: D is streamed once per pass (MI355X: ~1.6x the HBM rate of
+            // cached loads for this access pattern, tools/sweep_hg.py)
+            const double* p = D + row * ldd + colc;
+            d[q].x = __builtin_nontemporal_load(p);
+            d[q].y = __builtin_nontemporal_load(p + 1);
         } else {
             d[q].x = colc < n ? D[row * ldd + colc] : 0.0;
             d[q].y = colc + 1 < n ? D[row * ldd + colc + 1] : 0.0;
@@ -330,7 +426,8 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ D, long 
             if (WB && r0 + q < n && c0ok) {
                 double* dst = D + (long)(r0 + q) * ldd + col;
                 if (VEC) {
-                    *reinterpret_cast<double2*>(dst) = make_double2(e0, c1ok ? e1 : cur[q].y);
+                    __builtin_nontemporal_store(e0, dst);
+                    __builtin_nontemporal_store(c1ok ? e1 : cur[q].y, dst + 1);
                 } else {
                     dst[0] = e0;
                     if (c1ok) dst[1] = e1;
@@ -359,20 +456,34 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ D, long 
     if (c1ok) part_w[(long)rt * n + col + 1] = w1;
 }
 
-__global__ void k_bfgs_pass_finish(int n, int nstrips, int nrowt, const double* __restrict__ part_u,
-                                   const double* __restrict__ part_v, const double* __restrict__ part_w,
-                                   double* __restrict__ u, double* __restrict__ v, double* __restrict__ w) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// Sum the pass partials in a fixed order.  Workgroup = 64 outputs x 4 quarters: quarter q sums
+// strips s == q (mod 4) (and row tiles t == q (mod 4)) ascending, then the four quarter sums
+// are added (0+1)+(2+3) -- 4x the loads in flight of a thread per output.
+__global__ __launch_bounds__(256) void k_bfgs_pass_finish(int n, int nstrips, int nrowt, const double* __restrict__ part_u,
+                                                          const double* __restrict__ part_v,
+                                                          const double* __restrict__ part_w, double* __restrict__ u,
+                                                          double* __restrict__ v, double* __restrict__ w) {
+    __shared__ double red[3][4][64];
+    const int il = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + il;
+    const int ic = min(i, n - 1);
     double su = 0.0, sv = 0.0, sw = 0.0;
-    for (int s = 0; s < nstrips; ++s) {
-        su += part_u[(long)s * n + i];
-        sv += part_v[(long)s * n + i];
+#pragma unroll 4
+    for (int s = q; s < nstrips; s += 4) {
+        su += part_u[(long)s * n + ic];
+        sv += part_v[(long)s * n + ic];
     }
-    for (int t = 0; t < nrowt; ++t) sw += part_w[(long)t * n + i];
-    if (u) u[i] = su;
-    if (v) v[i] = sv;
-    if (w) w[i] = sw;
+#pragma unroll 4
+    for (int t = q; t < nrowt; t += 4) sw += part_w[(long)t * n + ic];
+    red[0][q][il] = su;
+    red[1][q][il] = sv;
+    red[2][q][il] = sw;
+    __syncthreads();
+    if (q == 0 && i < n) {
+        if (u) u[i] = (red[0][0][il] + red[0][1][il]) + (red[0][2][il] + red[0][3][il]);
+        if (v) v[i] = (red[1][0][il] + red[1][1][il]) + (red[1][2][il] + red[1][3][il]);
+        if (w) w[i] = (red[2][0][il] + red[2][1][il]) + (red[2][2][il] + red[2][3][il]);
+    }
 }
 
 __global__ void k_set_identity(double* __restrict__ D, long ldd, int n, const double* __restrict__ scale) {
@@ -411,6 +522,26 @@ int launch_gemv_neg(pnol_ctx* ctx, const double* A, int lda, int rows, int cols,
         const char* e = std::getenv("PNOL_GEMV_ROWS");
         return e ? std::atoi(e) : 0;
     }();
+    // PNOL_GEMV_MODE (tuning): 0 wave per R rows, 1 workgroup-cooperative rows, 2 (default)
+    // = 1 with non-temporal loads: 6.66 TB/s at n = 8192 vs 4.0 for the best cached variant
+    // (profiles/r01_sweep_hg.log)
+    static const int mode = [] {
+        const char* e = std::getenv("PNOL_GEMV_MODE");
+        return e ? std::atoi(e) : 2;
+    }();
+    if (mode == 1 || mode == 2) {
+        const int Rw = forced == 1 || forced == 2 || forced == 4 ? forced : 2;
+        const int blocks = (rows + Rw - 1) / Rw;
+#define PNOL_GEMV_WG(RR, NTT) \
+    hipLaunchKernelGGL((k_gemv_neg_wg<RR, NTT>), dim3(blocks), dim3(256), 0, ctx->stream, A, (long)lda, rows, cols, x, y)
+        if (mode == 1) {
+            if (Rw == 4) PNOL_GEMV_WG(4, false); else if (Rw == 2) PNOL_GEMV_WG(2, false); else PNOL_GEMV_WG(1, false);
+        } else {
+            if (Rw == 4) PNOL_GEMV_WG(4, true); else if (Rw == 2) PNOL_GEMV_WG(2, true); else PNOL_GEMV_WG(1, true);
+        }
+#undef PNOL_GEMV_WG
+        return launch_check();
+    }
     int R = forced == 1 || forced == 2 || forced == 4 ? forced : (rows >= 8192 ? 2 : 1);
     const int blocks = (rows + 4 * R - 1) / (4 * R);
     if (R == 4)
@@ -478,7 +609,7 @@ int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p
     }
 #undef PNOL_PASS
     PNOL_CHECK(launch_check());
-    hipLaunchKernelGGL(k_bfgs_pass_finish, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, n, nstrips, nrowt,
+    hipLaunchKernelGGL(k_bfgs_pass_finish, dim3((n + 63) / 64), dim3(256), 0, ctx->stream, n, nstrips, nrowt,
                        (const double*)P0, (const double*)P1, (const double*)P2, u, v, w);
     return launch_check();
 }

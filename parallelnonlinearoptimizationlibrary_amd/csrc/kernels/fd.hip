@@ -166,7 +166,9 @@ __global__ __launch_bounds__(256) void k_linres_eval(const double* __restrict__ 
             const int c = k0 + lc;
             const double* p = A + (long)row * n + c;
             if (VEC && c + 1 < n) {
-                reg[q] = *reinterpret_cast<const double2*>(p);
+                // A is streamed once per evaluation: non-temporal 16-byte loads
+                reg[q].x = __builtin_nontemporal_load(p);
+                reg[q].y = __builtin_nontemporal_load(p + 1);
             } else {
                 reg[q].x = c < n ? p[0] : 0.0;
                 reg[q].y = c + 1 < n ? p[1] : 0.0;

@@ -19,13 +19,14 @@ print(json.dumps({n: bench.bench_hg(ctx, n) for n in (8192, 4096)}))
 
 if __name__ == "__main__":
     out = {}
-    for r in ("1", "2", "4"):
-        env = dict(os.environ, PNOL_GEMV_ROWS=r)
+    for mode, r in (("0", "2"), ("0", "1"), ("1", "1"), ("1", "2"), ("1", "4"), ("2", "2"), ("2", "4")):
+        env = dict(os.environ, PNOL_GEMV_ROWS=r, PNOL_GEMV_MODE=mode)
         p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
         if p.returncode != 0:
             print(p.stderr[-2000:])
             sys.exit(p.returncode)
         res = json.loads(p.stdout.strip().splitlines()[-1])
+        r = f"mode{mode}_R{r}"
         out[r] = {n: {k: round(v, 3) if isinstance(v, float) else v for k, v in d.items()
                       if k in ("hg_us", "hg_GBps", "hg_frac_of_hbm", "fused_pass_GBps")} for n, d in res.items()}
         print(r, json.dumps(out[r]), flush=True)
