@@ -105,11 +105,13 @@ int pnol_jtj_mpi_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, doub
 /* rhs = -(J^T F), LevenbergMarquardt.cpp:78-80 */
 int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
 /* sigma = A^{-1} rhs, replacing luSolve(A, rhs, sigma), LevenbergMarquardt.cpp:83.
- * method 0 = auto (n <= PNOL_SEQ_MAX: reference LU; else blocked Cholesky, LU on a non-positive
+ * method 0 = auto (n <= PNOL_SEQ_MAX: reference LU; else method 4, LU on a non-positive
  * pivot), 1 = Cholesky (per-panel launches), 2 = LU with partial pivoting (reference operation
- * order), 3 = Cholesky as one persistent tile-DAG launch (experimental).
- * A is consumed (overwritten by its factor).  info (host, nullable) gets the method used
- * (1 or 2) or -1 on a singular matrix. */
+ * order), 3 = Cholesky as one persistent tile-DAG launch (experimental), 4 = lookahead tile
+ * Cholesky with diagonal-tile inverses, one launch per panel, forward solve folded in.
+ * Methods 1 and 3 consume A (overwritten by its factor); method 4 factors a padded copy and
+ * leaves A intact.  info (host, nullable) gets the method family used (1 = Cholesky, 2 = LU)
+ * or -1 on a singular matrix. */
 int pnol_solve_d(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n,
                  int method, int* info);
 

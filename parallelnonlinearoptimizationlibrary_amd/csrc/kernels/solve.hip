@@ -716,7 +716,19 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
     PNOL_CHECK(ws_get(ctx, "solve_info", sizeof(int) * 4, &dinfo_v));
     int* dinfo = (int*)dinfo_v;
     int used = 0;
-    if (method == 0) method = (n <= PNOL_SEQ_MAX) ? 2 : 1;
+    if (method == 0) method = (n <= PNOL_SEQ_MAX) ? 2 : 4;
+    if (method == 4) {
+        // lookahead tile Cholesky with diagonal inverses (chol.hip); A itself is not modified
+        PNOL_CHECK(launch_chol_solve(ctx, A, lda, rhs, sigma, n, dinfo));
+        int hinfo = 0;
+        PNOL_HIP(hipMemcpyAsync(&hinfo, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        PNOL_HIP(hipStreamSynchronize(ctx->stream));
+        if (hinfo == 0) {
+            if (info) *info = 1;
+            return PNOL_OK;
+        }
+        method = 2;   // non-positive pivot or a timed-out chain: reference-order LU on A
+    }
     const bool multi_launch = method != 3;   // method 3: the tile-DAG launch (experimental)
     if (method == 3) method = 1;
     if (method == 1) {

@@ -46,6 +46,9 @@ struct pnol_ctx {
     int solve_epoch = 0;            // value the flags of the current solve are set to
     void* chol_tasks = nullptr;     // uploaded tile-DAG task table (workspace) and its tile count
     int chol_tasks_T = 0;
+    int* chol4_flags = nullptr;     // method-4 Cholesky: per-row panel flags + backward-solve flags
+    int chol4_cap = 0;              // tile rows the flag buffer holds (2 * cap ints)
+    int chol4_epoch = 0;            // last flag value handed out (monotonic; flags reset on regrow)
 };
 
 struct pnol_dobj {
@@ -120,6 +123,7 @@ int launch_jtr(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const do
 int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, double alpha, double* C,
                       int ldc, int split_k);
 
+int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo);
 int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n, int method,
                  int* info);
 

@@ -163,10 +163,11 @@ def test_jtj_mfma_layout_asymmetric(ctx):
     assert np.array_equal(A, J.T @ J)
 
 
-@pytest.mark.parametrize("method", [1, 3])
+@pytest.mark.parametrize("method", [1, 3, 4])
 @pytest.mark.parametrize("n", [65, 100, 129, 777, 1000, 2048, 3001])
 def test_cholesky_solve(ctx, n, method):
-    """method 1: per-panel launches; method 3: one persistent tile-DAG launch."""
+    """method 1: per-panel launches; method 3: one persistent tile-DAG launch; method 4 (the
+    default): lookahead tile Cholesky with diagonal-tile inverses and the forward solve folded in."""
     rng = np.random.default_rng(n)
     J = rng.standard_normal((2 * n, n))
     A = J.T @ J + np.eye(n)
@@ -177,7 +178,7 @@ def test_cholesky_solve(ctx, n, method):
     assert np.linalg.norm(_np(sigma) - x) <= 1e-10 * np.linalg.norm(x) * np.linalg.cond(A)
 
 
-@pytest.mark.parametrize("method", [1, 3])
+@pytest.mark.parametrize("method", [1, 3, 4])
 def test_cholesky_odd_leading_dimension(ctx, method):
     """Odd lda: scalar staging paths (no 16-byte loads)."""
     rng = np.random.default_rng(77)
@@ -193,15 +194,16 @@ def test_cholesky_odd_leading_dimension(ctx, method):
     assert np.linalg.norm(_np(sigma) - x) <= 1e-10 * np.linalg.norm(x) * np.linalg.cond(A)
 
 
-def test_cholesky_repeated_solves_reuse_ready_flags(ctx):
-    """The flag-chained triangular solves tag each call with a new epoch; sizes that grow
-    and shrink (the flag buffer is reallocated) and back-to-back calls must all be exact."""
+@pytest.mark.parametrize("method", [1, 4])
+def test_cholesky_repeated_solves_reuse_ready_flags(ctx, method):
+    """The flag-chained solves tag each call with a new epoch; sizes that grow and shrink (the
+    flag buffer is reallocated) and back-to-back calls must all be exact."""
     rng = np.random.default_rng(5)
     for n in (300, 300, 1500, 64 * 70, 200, 1500):
         J = rng.standard_normal((n + 50, n))
         A = J.T @ J + n * np.eye(n)
         b = rng.standard_normal(n)
-        sigma, info = ctx.solve(ctx.tensor(A), ctx.tensor(b), method=1)
+        sigma, info = ctx.solve(ctx.tensor(A), ctx.tensor(b), method=method)
         assert info == 1, n
         x = np.linalg.solve(A, b)
         assert np.linalg.norm(_np(sigma) - x) <= 1e-12 * np.linalg.norm(x) * np.linalg.cond(A), n
@@ -222,6 +224,24 @@ def test_lu_multi_launch_bitwise(ctx, oracle):
     A = rng.standard_normal((n, n)); b = rng.standard_normal(n)
     sigma, info = ctx.solve(ctx.tensor(A), ctx.tensor(b), method=2)
     assert np.array_equal(_np(sigma), oracle.lusolve(A, b))
+
+
+def test_cholesky_m4_keeps_A_and_matches_per_panel(ctx):
+    """Method 4 factors a padded copy (A is left intact) and agrees with the per-panel form."""
+    rng = np.random.default_rng(3)
+    n = 1000
+    J = rng.standard_normal((1200, n))
+    A = J.T @ J + 0.5 * np.eye(n)
+    b = rng.standard_normal(n)
+    At = ctx.tensor(A)
+    s4, i4 = ctx.solve(At, ctx.tensor(b), method=4)
+    assert i4 == 1
+    assert np.array_equal(_np(At), A)
+    s1, i1 = ctx.solve(ctx.tensor(A), ctx.tensor(b), method=1)
+    x = np.linalg.solve(A, b)
+    c = np.linalg.cond(A)
+    for s in (s4, s1):
+        assert np.linalg.norm(_np(s) - x) <= 1e-12 * np.linalg.norm(x) * c
 
 
 @pytest.mark.parametrize("n", [200, 1000])
