@@ -7,7 +7,9 @@
 //   diag WG      tile (k+1,k+1): L = A_{k+1,k} W_k^T and A_{k+1,k+1} -= L L^T on fp64 MFMA,
 //                then the 64-step Cholesky of the tile (wave 0, rows in registers) with its
 //                inverse W_{k+1} = L_{k+1,k+1}^{-1} formed one column step behind (wave 1)
-//   panel WGs    L_ik = A_ik W_k^T (TRSM as an MFMA product), published by a per-row flag;
+//   panel WGs    L_ik = A_ik W_k^T (TRSM as an MFMA product) into a separate factor matrix Lm
+//                (the diagonal WG of the same launch still reads A_{k+1,k} from P), published
+//                by a per-row flag;
 //                they also carry the forward substitution: z_k = W_k b_k, b_i -= L_ik z_k
 //   update WGs   A_ij -= L_ik L_jk^T (fp64 MFMA) once rows i and j of the panel are flagged
 // The diagonal workgroup recomputes its own L_{k+1,k} instead of waiting for it, so the critical
@@ -160,42 +162,29 @@ __device__ __forceinline__ bool spin_ge(const int* f, int target, int* info) {
     return true;
 }
 
-// ---- the diagonal tile: Cholesky (wave 0) + inverse (wave 1) ------------------------------
-// Wave 0, lane t = row t of the tile in registers.  Step J: pivot from lane J, r = 1/sqrt(pivot),
-// column J (l_tJ = a_tJ r, diagonal sqrt(pivot), zero above) and r go to LDS, then a rank-1
-// update of the rest of the row from broadcast reads of that column.  Every 4 steps a
-// workgroup-scope release of `cnt` tells wave 1 that columns < cnt are final.
-template <int J>
-__device__ __forceinline__ void potrf_step(double (&a)[NB], double* __restrict__ Lc, double* __restrict__ rinv,
-                                           int* cnt, int t, bool& bad) {
-    const double piv = readlane_d(a[J], J);
-    bad |= !(piv > 0.0);
-    const double r = rsqrt_nr(piv);
-    const double l = (t == J) ? piv * r : (t > J ? a[J] * r : 0.0);
-    a[J] = l;
-    Lc[J * NB + t] = l;
-    rinv[J] = r;   // every lane stores the same value: no divergent branch in the unrolled chain
-    if constexpr ((J & 3) == 3) __hip_atomic_store(cnt, J + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): column J is in LDS for the whole wave
-    __builtin_amdgcn_wave_barrier();
-    constexpr int K0 = (J + 1) & ~1;
-#pragma unroll
-    for (int k = K0; k < NB; k += 2) {
-        const double2 c = *reinterpret_cast<const double2*>(Lc + J * NB + k);
-        if (k >= J + 1) a[k] = fma(-l, c.x, a[k]);
-        a[k + 1] = fma(-l, c.y, a[k + 1]);
-        if ((k & 15) == 14) __builtin_amdgcn_sched_barrier(0);
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (J + 1 < NB) potrf_step<J + 1>(a, Lc, rinv, cnt, t, bad);
-}
+// ---- the diagonal tile: blocked Cholesky + inverse ---------------------------------------
+// The 64 x 64 tile is factored as two 32-wide panels:
+//   P1  wave 0: the 64 x 32 panel [S11; S21] (lane t = row t, 32 entries in registers) gives
+//       L11 and L21 together; wave 1 forms W11 = L11^{-1} one column step behind
+//   P2  S22 -= L21 L21^T (fp64 MFMA, three 16 x 16 quadrants)
+//   P3  wave 0: the 32 x 32 panel S22 -> L22; wave 1: W22 = L22^{-1}; waves 2, 3 meanwhile
+//       form T = L21 W11 (MFMA)
+//   P4  W21 = -W22 T (MFMA)
+// Panel steps are software-pipelined: after column J is formed, lane J+1 alone needs the
+// broadcast l_{J+1,J} to update its diagonal entry, so the next pivot (readlane + rsqrt +
+// two Newton steps) is issued before the rest of the rank-1 update, whose LDS broadcasts
+// and FMAs then overlap that latency chain.  Column J and 1/L_JJ go to LDS (Lc, rinv); every
+// 4 steps an LDS counter tells wave 1 how many columns are final.
+constexpr int kHalf = 32;
+constexpr int kS = kHalf + 1;   // row stride of the LDS copies of the tile halves
 
-// Spin (all lanes, uniform value) until the LDS word *cnt >= target.  The loop is inline asm so
-// that the unrolled register-resident chain around it stays one basic block for the scheduler
-// (a C++ loop here splits it and the 64-entry column spills).  LDS operations of one wave are
-// processed in order, so reads issued after the exit see every LDS write the signalling wave
-// made before its store of *cnt.
+// LDS word store / spin-wait as inline asm: opaque to the scheduler, so the unrolled
+// register-resident chains around them stay one basic block (a C++ loop or an atomic here
+// splits them and the register rows spill).  One wave's LDS operations are processed in order.
+__device__ __forceinline__ void lds_signal(int* cnt, int v) {
+    __attribute__((address_space(3))) int* p = (__attribute__((address_space(3))) int*)cnt;
+    asm volatile("ds_write_b32 %0, %1" ::"v"(p), "v"(v) : "memory");
+}
 __device__ __forceinline__ void wait_lds_ge(const int* cnt, int target) {
     const __attribute__((address_space(3))) int* p = (const __attribute__((address_space(3))) int*)cnt;
     int v;
@@ -213,46 +202,205 @@ __device__ __forceinline__ void wait_lds_ge(const int* cnt, int target) {
         : "vcc", "memory");
 }
 
-// Wave 1, lane c = column c of W = L^{-1}, right-looking forward substitution on e_c:
-// w_J = y_J / L_JJ, then y_r -= L_rJ w_J for r > J (L_rJ read as a broadcast of column J).
-template <int J>
-__device__ __forceinline__ void trinv_step(double (&y)[NB], const double* __restrict__ Lc,
-                                           const double* __restrict__ rinv, const int* cnt) {
-    if constexpr ((J & 3) == 0) wait_lds_ge(cnt, J + 4);
-    const double w = y[J] * rinv[J];
+// One step of a 32-wide panel (wave 0).  On entry piv / r are the pivot of column J and its
+// reciprocal square root; on exit those of column J + 1.  Lc is column-major with stride LDC.
+template <int J, int LDC, bool STAMP = false>
+__device__ __forceinline__ void panel_step(double (&a)[kHalf], double& piv, double& r, double* __restrict__ Lc,
+                                           double* __restrict__ rinv, int* cnt, int cbase, int t, bool& bad,
+                                           long long* st = nullptr) {
+    if constexpr (STAMP && (J & 7) == 0) st[J >> 3] = __builtin_amdgcn_s_memtime();   // microbenchmark only
+    const double l = (t == J) ? piv * r : (t > J ? a[J] * r : 0.0);
+    a[J] = l;
+    double pnext = 0.0;
+    if constexpr (J + 1 < kHalf) {
+        // pivot path of column J + 1 first: it needs only the broadcast of l_{J+1,J}
+        const double l1 = readlane_d(l, J + 1);
+        a[J + 1] = fma(-l, l1, a[J + 1]);
+        pnext = readlane_d(a[J + 1], J + 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    Lc[J * LDC + t] = l;
+    rinv[cbase + J] = r;   // every lane stores the same value: no divergent branch in the chain
+    if constexpr ((J & 3) == 3) lds_signal(cnt, cbase + J + 1);
+    if constexpr (J + 1 < kHalf) {
+        // the whole broadcast of column J is requested at once (one LDS latency), the next
+        // pivot's rsqrt chain runs under it, then the rank-1 update
+        constexpr int K0 = (J + 2) & ~1, NR = (kHalf - K0) / 2;
+        double2 cv[NR > 0 ? NR : 1];
+#pragma unroll
+        for (int q = 0; q < NR; ++q) cv[q] = *reinterpret_cast<const double2*>(Lc + J * LDC + K0 + 2 * q);
+        piv = pnext;
+        bad |= !(piv > 0.0);
+        r = rsqrt_nr(piv);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+            const int k = K0 + 2 * q;
+            if (k >= J + 2) a[k] = fma(-l, cv[q].x, a[k]);
+            a[k + 1] = fma(-l, cv[q].y, a[k + 1]);
+        }
+        asm volatile("" ::: "memory");   // keep the next steps' LDS reads from being hoisted here
+        __builtin_amdgcn_sched_barrier(0);
+        panel_step<J + 1, LDC, STAMP>(a, piv, r, Lc, rinv, cnt, cbase, t, bad, st);
+    }
+}
+
+// One step of the inverse of a 32 x 32 lower factor (wave 1, lane c = column c of W):
+// w_J = y_J / L_JJ, then y_k -= L_kJ w_J for k > J.
+template <int J, int LDC>
+__device__ __forceinline__ void inv_step(double (&y)[kHalf], const double* __restrict__ Lc,
+                                         const double* __restrict__ rinv, const int* cnt, int cbase) {
+    if constexpr ((J & 3) == 0) wait_lds_ge(cnt, cbase + J + 4);
+    const double w = y[J] * rinv[cbase + J];
     y[J] = w;
     constexpr int K0 = (J + 1) & ~1;
 #pragma unroll
-    for (int k = K0; k < NB; k += 2) {
-        const double2 c = *reinterpret_cast<const double2*>(Lc + J * NB + k);
+    for (int k = K0; k < kHalf; k += 2) {
+        const double2 c = *reinterpret_cast<const double2*>(Lc + J * LDC + k);
         if (k >= J + 1) y[k] = fma(-c.x, w, y[k]);
         y[k + 1] = fma(-c.y, w, y[k + 1]);
-        if ((k & 15) == 14) __builtin_amdgcn_sched_barrier(0);
     }
+    asm volatile("" ::: "memory");   // keep the next steps' LDS reads from being hoisted here
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (J + 1 < NB) trinv_step<J + 1>(y, Lc, rinv, cnt);
+    if constexpr (J + 1 < kHalf) inv_step<J + 1, LDC>(y, Lc, rinv, cnt, cbase);
 }
 
-// S: the updated tile, row-major 64 x 65 (lower triangle meaningful).  Lc: 64 x 64 scratch.
-// Writes W_d (row-major, zero above the diagonal) to Wd; sets *info on a bad pivot.
-__device__ __forceinline__ void factor_diag(const double* __restrict__ S, double* __restrict__ Lc,
-                                            double* __restrict__ rinv, int* cnt, double* __restrict__ Wd, int d,
-                                            int* info) {
-    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-    if (wave == 0) {
-        double a[NB];
+// Wave 1's part of a panel: W = L^{-1} of the 32 x 32 factor whose columns appear in Lc, stored
+// row-major into Wl.  Lanes >= 32 (all-zero columns) store into the 32 doubles after Wl
+// instead of branching: a divergent branch after the register chain makes it spill.
+template <int LDC>
+__device__ __forceinline__ void panel_inverse(const double* __restrict__ Lc, const double* __restrict__ rinv,
+                                                         const int* cnt, int cbase, double* __restrict__ Wl, int lane) {
+    double y[kHalf];
 #pragma unroll
-        for (int k = 0; k < NB; ++k) a[k] = S[lane * (NB + 1) + k];
-        bool bad = false;
-        potrf_step<0>(a, Lc, rinv, cnt, lane, bad);
+    for (int k = 0; k < kHalf; ++k) y[k] = (k == lane) ? 1.0 : 0.0;
+    inv_step<0, LDC>(y, Lc, rinv, cnt, cbase);
+#pragma unroll
+    for (int k = 0; k < kHalf; ++k) Wl[lane < kHalf ? k * kHalf + lane : kHalf * kHalf + (lane - kHalf)] = y[k];
+}
+
+// 16 x 16 block of C = sum_k A(i, k) B(j, k) over K (v_mfma_f64_16x16x4_f64), accumulated into acc.
+template <int K, class FA, class FB>
+__device__ __forceinline__ d4 mfma_blk(d4 acc, FA fa, FB fb, int lane) {
+    const int i = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int kk = 0; kk < K; kk += 4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fa(i, kk + kq), fb(i, kk + kq), acc, 0, 0, 0);
+    return acc;
+}
+
+struct DiagLds {
+    double* Sl;    // 64 x 32 left half of the tile, stride kS (dead after P1 starts)
+    double* S22;   // 32 x 32 bottom-right quarter, stride kS
+    double* Lc1;   // P1 columns, column-major, stride 64
+    double* Lc2;   // P3 columns, column-major, stride 64 (lanes >= 32 fill rows 32..63 with zeros)
+    double* W11;   // 32 x 32 row-major, then 32 doubles of discard space
+    double* W22;   // 32 x 32 row-major + 32 discard (in the Sl space)
+    double* Tl;    // 32 x 32 row-major (in the Sl space)
+};
+
+__device__ __forceinline__ DiagLds diag_lds(double* smem) {
+    DiagLds L;
+    L.Sl = smem;
+    L.Tl = smem;
+    L.W22 = smem + 1024;
+    L.S22 = smem + 64 * kS;
+    L.Lc1 = L.S22 + kHalf * kS;
+    L.Lc2 = L.Lc1 + 64 * kHalf;
+    L.W11 = L.Lc2 + 64 * kHalf;
+    return L;
+}
+
+// the tile entry (row, col) of the lower triangle into the split LDS copy (upper-right dropped)
+__device__ __forceinline__ void diag_put(const DiagLds& L, int row, int col, double v) {
+    if (col < kHalf) L.Sl[row * kS + col] = v;
+    else if (row >= kHalf) L.S22[(row - kHalf) * kS + col - kHalf] = v;
+}
+
+// Factor the tile held in L.Sl / L.S22 and write W_d = L_dd^{-1} (64 x 64 row-major) to Wd.
+// STAMP: s_memtime stamps of the phases into st[0..31] (tools/microbench/diag_timing.hip only)
+template <bool STAMP = false>
+__device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict__ rinv, int* cnt,
+                                            double* __restrict__ Wd, int d, int* info, long long* st = nullptr) {
+    const int t = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+    // P1
+    if (wave == 0) {
+        double a[kHalf];
+#pragma unroll
+        for (int k = 0; k < kHalf; ++k) a[k] = L.Sl[lane * kS + k];
+        double piv = readlane_d(a[0], 0);
+        bool bad = !(piv > 0.0);
+        double r = rsqrt_nr(piv);
+        panel_step<0, 64, STAMP>(a, piv, r, L.Lc1, rinv, cnt, 0, lane, bad, st);
+        if constexpr (STAMP) st[4] = __builtin_amdgcn_s_memtime();
         if (bad && lane == 0) atomicCAS(info, 0, d * NB + 1);
     } else if (wave == 1) {
-        double y[NB];
+        panel_inverse<64>(L.Lc1, rinv, cnt, 0, L.W11, lane);
+        if constexpr (STAMP) st[5] = __builtin_amdgcn_s_memtime();
+    }
+    __syncthreads();
+    if constexpr (STAMP) if (wave == 0) st[6] = __builtin_amdgcn_s_memtime();
+    // P2: S22 -= L21 L21^T (quadrants (0,0), (1,0), (1,1) on waves 0, 2, 3)
+    if (wave != 1) {
+        const int qi = wave == 0 ? 0 : 1, qj = wave == 3 ? 1 : 0;
+        d4 acc;
 #pragma unroll
-        for (int k = 0; k < NB; ++k) y[k] = (k == lane) ? 1.0 : 0.0;
-        trinv_step<0>(y, Lc, rinv, cnt);
+        for (int r = 0; r < 4; ++r) acc[r] = L.S22[(qi * 16 + (lane >> 4) + 4 * r) * kS + qj * 16 + (lane & 15)];
+        const double* L21 = L.Lc1 + kHalf;
+        acc = mfma_blk<kHalf>(acc, [&](int i, int k) { return -L21[k * 64 + qi * 16 + i]; },
+                              [&](int j, int k) { return L21[k * 64 + qj * 16 + j]; }, lane);
 #pragma unroll
-        for (int r = 0; r < NB; ++r) Wd[r * NB + lane] = y[r];
+        for (int r = 0; r < 4; ++r) L.S22[(qi * 16 + (lane >> 4) + 4 * r) * kS + qj * 16 + (lane & 15)] = acc[r];
+    }
+    __syncthreads();
+    // P3 (+ T = L21 W11 on waves 2, 3)
+    if (wave == 0) {
+        double a[kHalf];
+#pragma unroll
+        for (int k = 0; k < kHalf; ++k) a[k] = lane < kHalf ? L.S22[lane * kS + k] : 0.0;
+        double piv = readlane_d(a[0], 0);
+        bool bad = !(piv > 0.0);
+        double r = rsqrt_nr(piv);
+        if constexpr (STAMP) st[8] = __builtin_amdgcn_s_memtime();
+        panel_step<0, 64, STAMP>(a, piv, r, L.Lc2, rinv, cnt, kHalf, lane, bad, st + 9);
+        if constexpr (STAMP) st[13] = __builtin_amdgcn_s_memtime();
+        if (bad && lane == 0) atomicCAS(info, 0, d * NB + kHalf + 1);
+    } else if (wave == 1) {
+        panel_inverse<64>(L.Lc2, rinv, cnt, kHalf, L.W22, lane);
+        if constexpr (STAMP) st[14] = __builtin_amdgcn_s_memtime();
+    } else {
+        const int qi = wave - 2;
+        const double* L21 = L.Lc1 + kHalf;
+#pragma unroll
+        for (int qj = 0; qj < 2; ++qj) {
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            acc = mfma_blk<kHalf>(acc, [&](int i, int k) { return L21[k * 64 + qi * 16 + i]; },
+                                  [&](int j, int k) { return L.W11[k * kHalf + qj * 16 + j]; }, lane);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) L.Tl[(qi * 16 + (lane >> 4) + 4 * r) * kHalf + qj * 16 + (lane & 15)] = acc[r];
+        }
+    }
+    __syncthreads();
+    if constexpr (STAMP) if (wave == 0) st[15] = __builtin_amdgcn_s_memtime();
+    // P4: W21 = -W22 T
+    {
+        const int qi = wave >> 1, qj = wave & 1;
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mfma_blk<kHalf>(acc, [&](int i, int k) { return -L.W22[(qi * 16 + i) * kHalf + k]; },
+                              [&](int j, int k) { return L.Tl[k * kHalf + qj * 16 + j]; }, lane);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Wd[(kHalf + qi * 16 + (lane >> 4) + 4 * r) * NB + qj * 16 + (lane & 15)] = acc[r];
+    }
+    if constexpr (STAMP) if (wave == 0) st[16] = __builtin_amdgcn_s_memtime();
+    // W11, W22 and the zero upper-right block: thread t writes columns (t & 31) of rows t >> 5 + 8 q
+    {
+        const int c = t & 31, r0 = t >> 5;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = r0 + 8 * q;
+            Wd[r * NB + c] = L.W11[r * kHalf + c];
+            Wd[r * NB + kHalf + c] = 0.0;
+            Wd[(kHalf + r) * NB + kHalf + c] = L.W22[r * kHalf + c];
+        }
     }
 }
 
@@ -260,8 +408,8 @@ __device__ __forceinline__ void factor_diag(const double* __restrict__ S, double
 // Launch k (-1 <= k <= T-2), R = T-1-k.  blockIdx 0: the diagonal tile k+1; 1..R: panel rows
 // i = k+1 .. T-1; then the update tiles (i, j), k+1 <= j <= i, (i, j) != (k+1, k+1), by columns.
 // Waits only ever target lower blockIdx (the panel workgroups), and every wait is capped.
-__global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, long ldp, int T, int k,
-                                                   double* __restrict__ W, double* __restrict__ bv,
+__global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, double* __restrict__ Lm, long ldp,
+                                                   int T, int k, double* __restrict__ W, double* __restrict__ bv,
                                                    double* __restrict__ zv, int* __restrict__ rowflag, int epoch,
                                                    int* __restrict__ info) {
     __shared__ __attribute__((aligned(16))) double smem[2 * kStage];   // 73.7 KB
@@ -269,7 +417,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, lo
     __shared__ double zsh[NB];
     __shared__ int cnt;
     __shared__ int ok_sh;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wr = wave >> 1, wc = wave & 1;
+    const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), wr = wave >> 1, wc = wave & 1;
     if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
     double* X = smem;
     double* Y = smem + kStage;
@@ -278,29 +426,37 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, lo
 
     if (b == 0) {   // ---------------- diagonal tile d = k + 1
         const int d = k + 1, d0 = d * NB;
-        double* S = Y;   // 64 x 65 rows, overlays the W_k stage once that is consumed
+        const DiagLds L = diag_lds(smem);
         if (t == 0) cnt = 0;
         if (k >= 0) {
             const int k0 = k * NB;
             stage_tile(X, P, ldp, d0, k0);
             stage_tile(Y, W + (long)k * NB * NB, NB, 0, 0);
+            d4 cdd[2][2];
+            acc_load(cdd, P, ldp, d0, d0, wr, wc, lane);   // in flight during the first product
             __syncthreads();
             d4 acc[2][2];
             acc_zero(acc);
             mfma_xyt<false>(acc, X, Y, wr, wc, lane);   // L_{d,k} = A_{d,k} W_k^T
             __syncthreads();
             acc_to_stage(acc, X, wr, wc, lane);
-            acc_load(acc, P, ldp, d0, d0, wr, wc, lane);
             __syncthreads();
-            mfma_xyt<true>(acc, X, X, wr, wc, lane);    // A_dd - L L^T
-            acc_to_rows(acc, S, wr, wc, lane);
+            mfma_xyt<true>(cdd, X, X, wr, wc, lane);    // A_dd - L L^T
+            __syncthreads();                            // X / Y are rewritten below
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        diag_put(L, acc_row(wr, mi, lane, r), acc_col(wc, ni, lane), cdd[mi][ni][r]);
         } else {
             const int row = t >> 2, c0 = (t & 3) * 16;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) S[row * (NB + 1) + c0 + q] = P[(long)row * ldp + c0 + q];
+            for (int q = 0; q < 16; ++q) diag_put(L, row, c0 + q, P[(long)row * ldp + c0 + q]);
         }
         __syncthreads();
-        factor_diag(S, X, rinv, &cnt, W + (long)d * NB * NB, d, info);
+        factor_diag(L, rinv, &cnt, W + (long)d * NB * NB, d, info);
         return;
     }
 
@@ -312,7 +468,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, lo
         d4 acc[2][2];
         acc_zero(acc);
         mfma_xyt<false>(acc, X, Y, wr, wc, lane);
-        acc_store(acc, P, ldp, i0, k0, wr, wc, lane);
+        acc_store(acc, Lm, ldp, i0, k0, wr, wc, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();                                 // every wave's stores have drained
         if (t == 0) {
@@ -356,8 +512,8 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, lo
     __syncthreads();
     if (!ok_sh) return;
     const int k0 = k * NB;
-    stage_tile(X, P, ldp, i * NB, k0);
-    if (i != j) stage_tile(Y, P, ldp, j * NB, k0);
+    stage_tile(X, Lm, ldp, i * NB, k0);
+    if (i != j) stage_tile(Y, Lm, ldp, j * NB, k0);
     d4 acc[2][2];
     acc_load(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
     __syncthreads();
@@ -369,7 +525,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, lo
 // Workgroup b owns block w = T-1-b.  For c = T-1 .. w+1 it waits for x_c (flag), accumulating
 // s_w += L_cw^T x_c with the next L_cw tile prefetched; then x_w = W_w^T (z_w - s_w).
 // z_{T-1} = W_{T-1} b_{T-1} is formed here (the factor launches form z_0 .. z_{T-2}).
-__global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ P, long ldp, int T, int n,
+__global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm, long ldp, int T, int n,
                                                   const double* __restrict__ W, const double* __restrict__ bv,
                                                   const double* __restrict__ zv, double* xw, double* __restrict__ x,
                                                   int* flags, int epoch, int* info) {
@@ -395,7 +551,7 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ P, 
     double Lv[16], Ln[16];
     auto load_blk = [&](double (&dst)[16], int c) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dst[r] = P[(long)(c * NB + q * 16 + r) * ldp + w0 + j];
+        for (int r = 0; r < 16; ++r) dst[r] = Lm[(long)(c * NB + q * 16 + r) * ldp + w0 + j];
     };
     if (w + 1 < T) load_blk(Lv, T - 1);
     for (int c = T - 1; c > w; --c) {
@@ -459,8 +615,9 @@ __global__ void k_chol_prep(const double* __restrict__ A, long lda, int n, doubl
 int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo) {
     const int T = (n + NB - 1) / NB, N = T * NB;
     const long ldp = N;
-    void *P = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr;
+    void *P = nullptr, *Lm = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr;
     PNOL_CHECK(ws_get(ctx, "chol4_P", sizeof(double) * (size_t)N * ldp, &P));
+    PNOL_CHECK(ws_get(ctx, "chol4_L", sizeof(double) * (size_t)N * ldp, &Lm));
     PNOL_CHECK(ws_get(ctx, "chol4_W", sizeof(double) * (size_t)T * NB * NB, &W));
     PNOL_CHECK(ws_get(ctx, "chol4_b", sizeof(double) * (size_t)N, &bv));
     PNOL_CHECK(ws_get(ctx, "chol4_z", sizeof(double) * (size_t)N, &zv));
@@ -483,11 +640,12 @@ int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs
         const int R = T - 1 - k;
         const int grid = k < 0 ? 1 : R + R * (R + 1) / 2;
         const int epoch = ++ctx->chol4_epoch;
-        hipLaunchKernelGGL(k_chol_step, dim3(grid), dim3(256), 0, ctx->stream, (double*)P, ldp, T, k, (double*)W,
+        hipLaunchKernelGGL(k_chol_step, dim3(grid), dim3(256), 0, ctx->stream, (double*)P, (double*)Lm, ldp, T, k,
+                           (double*)W,
                            (double*)bv, (double*)zv, rowflag, epoch, dinfo);
     }
     const int epoch = ++ctx->chol4_epoch;
-    hipLaunchKernelGGL(k_chol_bwd, dim3(T), dim3(256), 0, ctx->stream, (const double*)P, ldp, T, n, (const double*)W,
+    hipLaunchKernelGGL(k_chol_bwd, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n, (const double*)W,
                        (const double*)bv, (const double*)zv, (double*)xw, sigma, bwdflag, epoch, dinfo);
     return launch_check();
 }

@@ -244,6 +244,32 @@ def test_cholesky_m4_keeps_A_and_matches_per_panel(ctx):
         assert np.linalg.norm(_np(s) - x) <= 1e-12 * np.linalg.norm(x) * c
 
 
+def test_cholesky_m4_bitwise_under_contention(ctx):
+    """Method 4 hands tiles between workgroups of one launch through flags; its result must not
+    depend on scheduling.  Large GEMMs on a second stream perturb which workgroups run when;
+    every solve must equal the solo solve bitwise."""
+    import torch
+    rng = np.random.default_rng(21)
+    n = 1500
+    J = rng.standard_normal((1700, n))
+    A = J.T @ J + 0.1 * np.eye(n)
+    b = rng.standard_normal(n)
+    At, bt = ctx.tensor(A), ctx.tensor(b)
+    ref, info = ctx.solve(At, bt, method=4)
+    ref = _np(ref)
+    assert info == 1
+    side = torch.cuda.Stream()
+    X = torch.randn(4096, 4096, device="cuda", dtype=torch.float64)
+    for rep in range(6):
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                X = (X @ X) * 1e-3
+        sigma, info = ctx.solve(At, bt, method=4)
+        assert info == 1
+        assert np.array_equal(_np(sigma), ref), rep
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("n", [200, 1000])
 def test_cholesky_falls_back_to_lu_on_indefinite(ctx, oracle, n):
     rng = np.random.default_rng(9)

@@ -1,0 +1,73 @@
+// Times the diagonal-tile factor of the method-4 Cholesky (chol.hip factor_diag) in one
+// workgroup with s_memtime stamps; checks W = L^{-1} against the host.  Build:
+//   hipcc -O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -I include \
+//     -I parallelnonlinearoptimizationlibrary_amd/csrc tools/microbench/diag_timing.hip -o tools/microbench/diag_timing
+#include "../../parallelnonlinearoptimizationlibrary_amd/csrc/kernels/chol.hip"
+
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+namespace pnol {
+int ws_get(pnol_ctx*, const char*, size_t, void**) { return PNOL_ERR_ARG; }   // unused here
+}
+
+__global__ __launch_bounds__(256, 2) void k_diag_time(const double* A, double* W, int* info, long long* st) {
+    using namespace pnol;
+    __shared__ __attribute__((aligned(16))) double smem[2 * kStage];
+    __shared__ double rinv[NB];
+    __shared__ int cnt;
+    const int t = threadIdx.x;
+    const DiagLds L = diag_lds(smem);
+    if (t == 0) cnt = 0;
+    const int row = t >> 2, c0 = (t & 3) * 16;
+    for (int q = 0; q < 16; ++q) diag_put(L, row, c0 + q, A[row * 64 + c0 + q]);
+    __syncthreads();
+    if (t == 0) st[31] = __builtin_amdgcn_s_memtime();
+    factor_diag<true>(L, rinv, &cnt, W, 0, info, st);
+}
+
+int main() {
+    const int n = 64;
+    std::vector<double> M(n * n), A(n * n);
+    unsigned long long s = 12345;
+    for (auto& v : M) { s = s * 6364136223846793005ULL + 1442695040888963407ULL; v = ((s >> 11) * 0x1.0p-53) - 0.5; }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double acc = (i == j) ? 1.0 : 0.0;
+            for (int k = 0; k < n; ++k) acc += M[i * n + k] * M[j * n + k];
+            A[i * n + j] = acc;
+        }
+    double *dA, *dW; int* dinfo; long long* dst;
+    hipMalloc(&dA, 8 * n * n); hipMalloc(&dW, 8 * n * n); hipMalloc(&dinfo, 4); hipMalloc(&dst, 8 * 32);
+    hipMemcpy(dA, A.data(), 8 * n * n, hipMemcpyHostToDevice);
+    for (int rep = 0; rep < 3; ++rep) {
+        hipMemset(dinfo, 0, 4); hipMemset(dst, 0, 8 * 32);
+        hipLaunchKernelGGL(k_diag_time, dim3(1), dim3(256), 0, 0, dA, dW, dinfo, dst);
+        hipDeviceSynchronize();
+    }
+    std::vector<long long> st(32); std::vector<double> W(n * n); int info = 0;
+    hipMemcpy(st.data(), dst, 8 * 32, hipMemcpyDeviceToHost);
+    hipMemcpy(W.data(), dW, 8 * n * n, hipMemcpyDeviceToHost);
+    hipMemcpy(&info, dinfo, 4, hipMemcpyDeviceToHost);
+    // check: W A W^T = I  (W = L^{-1}, A = L L^T)
+    double err = 0;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double acc = 0;
+            for (int k = 0; k < n; ++k) {
+                double wa = 0;
+                for (int l = 0; l < n; ++l) wa += W[i * n + l] * A[l * n + k];
+                acc += wa * W[j * n + k];
+            }
+            err = std::fmax(err, std::fabs(acc - (i == j)));
+        }
+    const long long b = st[31];
+    printf("{\"info\": %d, \"max|W A W^T - I|\": %.3e, \"cycles\": {", info, err);
+    const char* names[] = {"p1_j0", "p1_j8", "p1_j16", "p1_j24", "p1_end", "w11_end", "b1", "-", "p3_start",
+                           "p3_j0", "p3_j8", "p3_j16", "p3_j24", "p3_end", "w22_end", "b3", "p4_end"};
+    for (int i = 0; i < 17; ++i)
+        if (i != 7) printf("%s\"%s\": %lld", i ? ", " : "", names[i], st[i] ? st[i] - b : -1LL);
+    printf("}}\n");
+    return 0;
+}
