@@ -325,17 +325,17 @@ __global__ __launch_bounds__(256) void k_linres_fd(const double* __restrict__ A,
 // broadcast to all points, so per k a thread reads RM A values and one x value for RM * PN
 // fmas.  Each accumulator is still the objective's sequential fma chain: bit-identical to
 // k_linres_fd and to the host evaluation.
-template <bool EVEN, int RM, int PN>
-__global__ __launch_bounds__(256) void k_linres_fd2(const double* __restrict__ A, const double* __restrict__ y,
+template <bool EVEN, int RM, int PN, int OCC = 1, int KB = kBK>
+__global__ __launch_bounds__(256, OCC) void k_linres_fd2(const double* __restrict__ A, const double* __restrict__ y,
                                                     const double* __restrict__ x, const double* __restrict__ h, int m,
                                                     int n, int j0, int cnt, const double* __restrict__ F0,
                                                     const double* __restrict__ C, double* __restrict__ JT, long ldjt) {
     constexpr int BM = 16 * RM, BN = 16 * PN;
     constexpr int TPR = 256 / BM;      // threads staging one A row
-    constexpr int KPT = kBK / TPR;     // consecutive k per staging thread (== RM)
-    __shared__ __attribute__((aligned(16))) double As[kBK][BM];
-    __shared__ __attribute__((aligned(16))) double Bs[kBK][BN];
-    __shared__ __attribute__((aligned(16))) double xs[kBK];
+    constexpr int KPT = KB / TPR;      // consecutive k per staging thread
+    __shared__ __attribute__((aligned(16))) double As[KB][BM];
+    __shared__ __attribute__((aligned(16))) double Bs[KB][BN];
+    __shared__ __attribute__((aligned(16))) double xs[KB];
     const int nmt = (m + BM - 1) / BM, nnt = (cnt + BN - 1) / BN;
     const int v = xcd_remap(blockIdx.x, nmt * nnt);
     const int mt = v / nnt, nt = v % nnt;
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(256) void k_linres_fd2(const double* __restrict__ A
     const bool rowok = m0 + lrow < m;
     double areg[KPT];
     auto load_a = [&](int k0) {
-        if (EVEN && rowok && k0 + kBK <= n) {
+        if (EVEN && rowok && k0 + KB <= n) {
             const double2* p = reinterpret_cast<const double2*>(A + arow + k0 + lk);
 #pragma unroll
             for (int q = 0; q < KPT / 2; ++q) { double2 w = p[q]; areg[2 * q] = w.x; areg[2 * q + 1] = w.y; }
@@ -370,18 +370,16 @@ __global__ __launch_bounds__(256) void k_linres_fd2(const double* __restrict__ A
             }
         }
     };
-    const int nk = (n + kBK - 1) / kBK;
     load_a(ks);
-    for (int kc = ks / kBK; kc < nk; ++kc) {
-        const int k0 = kc * kBK;
-        const bool window = k0 <= jlast && k0 + kBK > jfirst;   // uniform over the workgroup
+    for (int k0 = ks; k0 < n; k0 += KB) {
+        const bool window = k0 <= jlast && k0 + KB > jfirst;   // uniform over the workgroup
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < KPT; ++q) As[lk + q][lrow] = areg[q];
-        if (t < kBK) xs[t] = k0 + t < n ? x[k0 + t] : 0.0;
+        if (t < KB) xs[t] = k0 + t < n ? x[k0 + t] : 0.0;
         if (window) {
 #pragma unroll
-            for (int q = 0; q < PN; ++q) {
+            for (int q = 0; q < KB * BN / 256; ++q) {
                 const int e = t + 256 * q;
                 const int k = e / BN, jj = e % BN;
                 const int kk = k0 + k;
@@ -393,10 +391,10 @@ __global__ __launch_bounds__(256) void k_linres_fd2(const double* __restrict__ A
             }
         }
         __syncthreads();
-        if (kc + 1 < nk) load_a(k0 + kBK);
+        if (k0 + KB < n) load_a(k0 + KB);
         if (window) {
 #pragma unroll
-            for (int k = 0; k < kBK; ++k) {
+            for (int k = 0; k < KB; ++k) {
                 double a[RM], b[PN];
                 const double2* ap = reinterpret_cast<const double2*>(&As[k][ty * RM]);
 #pragma unroll
@@ -412,7 +410,7 @@ __global__ __launch_bounds__(256) void k_linres_fd2(const double* __restrict__ A
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < kBK; ++k) {
+            for (int k = 0; k < KB; ++k) {
                 double a[RM];
                 const double2* ap = reinterpret_cast<const double2*>(&As[k][ty * RM]);
 #pragma unroll
@@ -426,6 +424,133 @@ __global__ __launch_bounds__(256) void k_linres_fd2(const double* __restrict__ A
                 if (k & 1) __builtin_amdgcn_sched_barrier(0);
             }
         }
+    }
+    // epilogue: F = acc - y; J = (F - F0) / h
+#pragma unroll
+    for (int j = 0; j < PN; ++j) {
+        const int p = pbase + tx * PN + j;
+        if (p >= cnt) continue;
+        const double hj = h[j0 + p];
+        double* out = JT + (long)p * ldjt;
+#pragma unroll
+        for (int i = 0; i < RM; ++i) {
+            const int row = m0 + ty * RM + i;
+            if (row < m) out[row] = ((acc[i][j] - y[row]) - F0[row]) / hj;
+        }
+    }
+}
+
+// Batched FD GEMM, scalar-x form.  Thread (ty, tx) = (t / TX, t % TX) owns RM residual rows
+// and PN consecutive points; workgroup tile BM = (256 / TX) RM rows x BN = TX PN points.
+// Per k a thread reads its RM values of A (one LDS vector read, k-major double-buffered
+// stages padded against bank conflicts) and x[k] through the scalar cache (uniform address,
+// an SGPR operand of the fma), then issues RM * PN fmas.  Outside the perturbation window
+// every point's operand is x[k]; inside it (uniform per stage) each point selects
+// x[j] + h[j] at its own column k == j.  Every accumulator is still the objective's
+// sequential fma chain resumed from the base-chain checkpoint: bit-identical to k_linres_fd.
+template <bool EVEN, int RM, int PN, int TX>
+__global__ __launch_bounds__(256) void k_linres_fd3(const double* __restrict__ A, const double* __restrict__ y,
+                                                    const double* __restrict__ x, const double* __restrict__ h, int m,
+                                                    int n, int j0, int cnt, const double* __restrict__ F0,
+                                                    const double* __restrict__ C, double* __restrict__ JT, long ldjt) {
+    constexpr int TY = 256 / TX, BM = TY * RM, BN = TX * PN, LDA = BM + 2;
+    constexpr int SPT = BM * kBK / 256;   // A values staged per thread per stage
+    constexpr int TPR = kBK / SPT;        // staging threads per A row
+    static_assert(RM == 2 || RM == 4, "RM");
+    static_assert(SPT % 2 == 0 && TPR * SPT == kBK, "staging shape");
+    __shared__ __attribute__((aligned(16))) double As[2][kBK][LDA];
+    const int nmt = (m + BM - 1) / BM, nnt = (cnt + BN - 1) / BN;
+    const int v = xcd_remap(blockIdx.x, nmt * nnt);
+    const int mt = v / nnt, nt = v % nnt;
+    const int m0 = mt * BM, pbase = nt * BN;
+    const int t = threadIdx.x, tx = t % TX, ty = t / TX;
+    const int jfirst = j0 + pbase, jlast = j0 + min(pbase + BN, cnt) - 1;
+    const int ks = (jfirst / kBK) * kBK;
+    const int jc0 = jfirst + tx * PN;   // this thread's first point column
+
+    double acc[RM][PN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+        const int row = min(m0 + ty * RM + i, m - 1);
+        const double c0 = ks > 0 ? C[(long)(ks / kCkpt) * m + row] : 0.0;
+#pragma unroll
+        for (int j = 0; j < PN; ++j) acc[i][j] = c0;
+    }
+    double xph[PN];   // the perturbed coordinate of each point, formed as the reference forms it
+#pragma unroll
+    for (int j = 0; j < PN; ++j) {
+        const int jc = min(jc0 + j, n - 1);
+        xph[j] = x[jc] + h[jc];
+    }
+
+    const int lrow = t / TPR, lk = (t % TPR) * SPT;
+    const long arow = (long)min(m0 + lrow, m - 1) * n;
+    const bool rowok = m0 + lrow < m;
+    double areg[SPT];
+    auto load_a = [&](int k0) {
+        if (EVEN && rowok && k0 + kBK <= n) {
+            const double2* p = reinterpret_cast<const double2*>(A + arow + k0 + lk);
+#pragma unroll
+            for (int q = 0; q < SPT / 2; ++q) { double2 w = p[q]; areg[2 * q] = w.x; areg[2 * q + 1] = w.y; }
+        } else {
+#pragma unroll
+            for (int q = 0; q < SPT; ++q) {
+                const int k = k0 + lk + q;
+                areg[q] = (rowok && k < n) ? A[arow + k] : 0.0;
+            }
+        }
+    };
+    auto store_a = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < SPT; ++q) As[buf][lk + q][lrow] = areg[q];
+    };
+    const int nk = (n + kBK - 1) / kBK;
+    int kc = ks / kBK;
+    load_a(kc * kBK);
+    store_a(0);
+    __syncthreads();
+    for (int buf = 0; kc < nk; ++kc, buf ^= 1) {
+        const int k0 = kc * kBK;
+        if (kc + 1 < nk) load_a(k0 + kBK);
+        const bool window = k0 <= jlast && k0 + kBK > jfirst;   // uniform over the workgroup
+        if (window) {
+#pragma unroll
+            for (int k = 0; k < kBK; ++k) {
+                const int kk = k0 + k;
+                const double xk = kk < n ? x[kk] : 0.0;
+                double a[RM];
+#pragma unroll
+                for (int i = 0; i < RM; i += 2) {
+                    const double2 w = *reinterpret_cast<const double2*>(&As[buf][k][ty * RM + i]);
+                    a[i] = w.x; a[i + 1] = w.y;
+                }
+#pragma unroll
+                for (int j = 0; j < PN; ++j) {
+                    const double b = (kk == jc0 + j) ? xph[j] : xk;
+#pragma unroll
+                    for (int i = 0; i < RM; ++i) acc[i][j] = fma(a[i], b, acc[i][j]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kBK; ++k) {
+                const int kk = k0 + k;
+                const double xk = (EVEN || kk < n) ? x[min(kk, n - 1)] : 0.0;
+                double a[RM];
+#pragma unroll
+                for (int i = 0; i < RM; i += 2) {
+                    const double2 w = *reinterpret_cast<const double2*>(&As[buf][k][ty * RM + i]);
+                    a[i] = w.x; a[i + 1] = w.y;
+                }
+#pragma unroll
+                for (int i = 0; i < RM; ++i)
+#pragma unroll
+                    for (int j = 0; j < PN; ++j) acc[i][j] = fma(a[i], xk, acc[i][j]);
+                if (k & 1) __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (kc + 1 < nk) store_a(buf ^ 1);
+        __syncthreads();
     }
     // epilogue: F = acc - y; J = (F - F0) / h
 #pragma unroll
@@ -554,7 +679,7 @@ int launch_fd_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
         static const int fdk = [] {
             const char* e = std::getenv("PNOL_FD_KERNEL");
             const int v = e ? std::atoi(e) : 3;
-            return (v >= 1 && v <= 3) ? v : 3;
+            return (v >= 1 && v <= 8) ? v : 3;
         }();
         const bool even = (o->n % 2) == 0;
         ScopedTimer tm(ctx, "fd_jacobian");
@@ -575,6 +700,34 @@ int launch_fd_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
             else
                 hipLaunchKernelGGL((k_linres_fd2<false, 8, 8>), nwg(128, 128), dim3(256), 0, ctx->stream, o->p0, o->p1,
                                    x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
+        } else if (fdk == 4) {
+            if (even)
+                hipLaunchKernelGGL((k_linres_fd3<true, 2, 16, 8>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0,
+                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
+            else
+                hipLaunchKernelGGL((k_linres_fd3<false, 2, 16, 8>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0,
+                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
+        } else if (fdk == 5) {
+            if (even)
+                hipLaunchKernelGGL((k_linres_fd3<true, 4, 8, 16>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0,
+                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
+            else
+                hipLaunchKernelGGL((k_linres_fd3<false, 4, 8, 16>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0,
+                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
+        } else if (fdk == 7 || fdk == 8) {
+            if (fdk == 7)
+                hipLaunchKernelGGL((k_linres_fd2<true, 4, 8, 1, 32>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0,
+                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
+            else
+                hipLaunchKernelGGL((k_linres_fd2<true, 4, 8, 1, 64>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0,
+                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
+        } else if (fdk == 6) {
+            if (even)
+                hipLaunchKernelGGL((k_linres_fd3<true, 4, 16, 8>), nwg(128, 128), dim3(256), 0, ctx->stream, o->p0,
+                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
+            else
+                hipLaunchKernelGGL((k_linres_fd3<false, 4, 16, 8>), nwg(128, 128), dim3(256), 0, ctx->stream, o->p0,
+                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
         } else {
             if (even)
                 hipLaunchKernelGGL((k_linres_fd2<true, 4, 8>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0, o->p1,
