@@ -68,6 +68,8 @@ int pnol_memcpy_d2h(pnol_ctx* ctx, void* dst, const void* src, size_t bytes);  /
  * D is n x n row-major with leading dimension ldd (doubles, even, 16-byte aligned base).
  * n <= PNOL_SEQ_MAX uses reference summation order (bitwise equal to the CPU path). */
 #define PNOL_SEQ_MAX 64
+/* columns per FD point tile (the FD GEMM's point-tile width, the multi-GPU split unit) */
+#define PNOL_FD_TILE 128
 int pnol_hg_d(pnol_ctx* ctx, const double* D, int ldd, const double* g, double* p, int n);
 /* y = -A x for a rows x cols row-major A (the same streaming kernel; also rhs = -J^T F). */
 int pnol_gemv_neg_d(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y);
@@ -143,6 +145,10 @@ int pnol_fd_gradient_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const dou
  * F0 = F(x) (computed here when compute_f0, else read), JT row (j - j0) = (F(x + h_j e_j) - F0)/h_j. */
 int pnol_fd_jacobian_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, int j0, int cnt,
                        double* F0, int compute_f0, double* JT, int ldjt);
+/* The FD Jacobian rows of a tile list (columns [start[t], start[t] + count[t]), count <=
+ * PNOL_FD_TILE), column c written to JT + c * ldjt; one base-chain pass for all tiles. */
+int pnol_fd_jacobian_tiles_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, const int* start,
+                             const int* count, int ntiles, double* F0, int compute_f0, double* JT, int ldjt);
 
 /* ---- communicator (replaces MPI_COMM_WORLD on the FD / pool paths) ------------------- */
 /* RCCL over xGMI: one process per GPU.  Exchange the 128-byte id out of band (rank 0 creates). */
@@ -157,6 +163,14 @@ int pnol_comm_size(int* nranks, int* rank);
 int pnol_comm_allgather_d(pnol_ctx* ctx, const double* send, double* recv, size_t count);
 /* contiguous column block owned by `rank` of `nranks` over `ncols` columns (also the host split) */
 void pnol_block_range(int ncols, int nranks, int rank, int* begin, int* count);
+/* Cost-balanced FD column tiles of `rank` (LevMarqMPI's Jacobian split, replacing the
+ * round-robin owners of PNOL_Objective.cpp:110-121 / 228-240): PNOL_FD_TILE-column tiles
+ * dealt in snake order.  Writes up to cap (start, count) pairs; returns the tile count. */
+int pnol_fd_tiles(int ncols, int nranks, int rank, int* start, int* count, int cap);
+/* Every rank ends with all ncols rows of buf (row c at buf + c * ld) from their pnol_fd_tiles
+ * owners: replaces the per-column MPI_Allreduce of PNOL_Objective.cpp:280-288 (RCCL:
+ * grouped point-to-point straight into place; host backend: allgather + unpack). */
+int pnol_comm_share_fd_rows_d(pnol_ctx* ctx, double* buf, int ld, int ncols);
 
 /* ---- whole-solver drivers: the C++ drop-in classes run on built-in objectives --------- */
 /* params arrays follow the classes' setParams order (see the headers in include/). */

@@ -8,7 +8,7 @@ drop-in classes of include/*.hpp).  This package only loads and drives it:
   build     hipcc build of the library (used by __graft_entry__.build())
 """
 from ._lib import (PNOL_OK, PNOL_SEQ_MAX, OBJ_CUBIC, OBJ_EXPCURVE, OBJ_LINRES, OBJ_POWER, OBJ_QUADRATIC,
-                   OBJ_ROSENBROCK, PnolError, block_range, device_count, lib)
+                   OBJ_ROSENBROCK, PnolError, block_range, device_count, fd_tiles, lib)
 
-__all__ = ["lib", "device_count", "block_range", "PnolError", "PNOL_OK", "PNOL_SEQ_MAX", "OBJ_ROSENBROCK",
+__all__ = ["lib", "device_count", "block_range", "fd_tiles", "PnolError", "PNOL_OK", "PNOL_SEQ_MAX", "OBJ_ROSENBROCK",
            "OBJ_POWER", "OBJ_QUADRATIC", "OBJ_EXPCURVE", "OBJ_CUBIC", "OBJ_LINRES"]

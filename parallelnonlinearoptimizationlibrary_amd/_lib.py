@@ -75,6 +75,7 @@ _SIGS = {
     "pnol_dobj_eval_d": (_i, [_vp, _vp, _vp, _vp]),
     "pnol_fd_gradient_d": (_i, [_vp, _vp, _vp, _vp, _i, _i, _vp, _vp]),
     "pnol_fd_jacobian_d": (_i, [_vp, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _i]),
+    "pnol_fd_jacobian_tiles_d": (_i, [_vp, _vp, _vp, _vp, C.POINTER(_i), C.POINTER(_i), _i, _vp, _i, _vp, _i]),
     "pnol_comm_unique_id": (_i, [C.c_char_p]),
     "pnol_comm_init_rccl": (_i, [_vp, _i, _i, C.c_char_p]),
     "pnol_comm_init_host": (_i, [_i, _i, ALLGATHER_FN, _vp]),
@@ -82,6 +83,8 @@ _SIGS = {
     "pnol_comm_size": (_i, [C.POINTER(_i), C.POINTER(_i)]),
     "pnol_comm_allgather_d": (_i, [_vp, _vp, _vp, _sz]),
     "pnol_block_range": (None, [_i, _i, _i, C.POINTER(_i), C.POINTER(_i)]),
+    "pnol_fd_tiles": (_i, [_i, _i, _i, C.POINTER(_i), C.POINTER(_i), _i]),
+    "pnol_comm_share_fd_rows_d": (_i, [_vp, _vp, _i, _i]),
     "pnol_run_bfgs": (_i, [_i, _vp, _i, _dp, _i, _dp, _i, _dp, _dp, C.POINTER(Result)]),
     "pnol_run_levmarq": (_i, [_i, _vp, _i, _dp, _dp, _i, _dp, _dp, _i, C.POINTER(Result)]),
     "pnol_host_fd_jacobian": (_i, [HOST_MULTI_FN, _vp, _dp, _dp, _i, _i, _i, _dp]),
@@ -132,6 +135,16 @@ def device_count() -> int:
     c = C.c_int(0)
     check(lib().pnol_device_count(C.byref(c)), "pnol_device_count")
     return c.value
+
+
+def fd_tiles(ncols: int, nranks: int, rank: int):
+    """The cost-balanced FD column tiles of `rank`: [(start, count), ...] (pnol_fd_tiles)."""
+    cap = ncols // 1 + 1
+    st, ct = (C.c_int * cap)(), (C.c_int * cap)()
+    k = lib().pnol_fd_tiles(ncols, nranks, rank, st, ct, cap)
+    if k < 0:
+        raise PnolError(-k, "pnol_fd_tiles")
+    return [(st[i], ct[i]) for i in range(k)]
 
 
 def block_range(ncols: int, nranks: int, rank: int):

@@ -198,4 +198,11 @@ int pnol_fd_jacobian_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const dou
     return launch_fd_jacobian(ctx, obj, x, h, j0, cnt, F0, compute_f0, JT, ldjt);
 }
 
+int pnol_fd_jacobian_tiles_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, const int* start,
+                             const int* count, int ntiles, double* F0, int compute_f0, double* JT, int ldjt) {
+    PNOL_CHECK(set_device(ctx));
+    if (ntiles < 0 || (ntiles > 0 && (!start || !count))) return PNOL_ERR_ARG;
+    return launch_fd_jacobian_tiles(ctx, obj, x, h, start, count, ntiles, F0, compute_f0, JT, 0, ldjt);
+}
+
 }  // extern "C"

@@ -1,6 +1,7 @@
 // levmarq.cpp -- LevMarq and LevMarqMPI (drop-in for Source/LevenbergMarquardt.cpp and
 // Source/LevenbergMarquardtMPI.cpp).  Both share one device-resident loop; the MPI form
-// shards the FD Jacobian columns over the communicator and allgathers J^T.
+// shards the FD Jacobian columns over the communicator (cost-balanced tiles) and shares the
+// rows of J^T between the ranks.
 #include <cmath>
 #include <cstdio>
 #include <iostream>
@@ -27,13 +28,15 @@ void print_vec(const std::vector<double>& v) {
     std::printf("\n");
 }
 
-// Device state of one LM solve.  JT holds J column-major (one FD column per row, ld = ldjt)
-// with room for P * ceil(n/P) rows so a rank's block and the allgather share one buffer.
+// Device state of one LM solve.  JT holds J column-major (one FD column per row, ld = ldjt,
+// n rows in natural column order).  LevMarqMPI: each rank evaluates its cost-balanced FD
+// tiles (fd_tiles_of) in place and comm_share_rows fills in the other ranks' rows.
 class LMDevice {
   public:
     LMDevice(pnol_ctx* ctx, int n, int m, int nranks)
-        : ctx_(ctx), n_(n), m_(m), ldjt_(even_ld(m)), lda_(even_ld(n)), per_((n + nranks - 1) / nranks) {
-        JT_.reset(ctx, (size_t)nranks * per_ * ldjt_);
+        : ctx_(ctx), n_(n), m_(m), ldjt_(even_ld(m)), lda_(even_ld(n)) {
+        (void)nranks;
+        JT_.reset(ctx, (size_t)n * ldjt_);
         A_.reset(ctx, (size_t)n * lda_);
         rhs_.reset(ctx, n); sigma_.reset(ctx, n); x_.reset(ctx, n); h_.reset(ctx, n);
         F_.reset(ctx, m); Fprev_.reset(ctx, m); F0_.reset(ctx, m);
@@ -55,31 +58,33 @@ class LMDevice {
     // J^T at X (LevenbergMarquardt.cpp:55 / LevenbergMarquardtMPI.cpp:60)
     void jacobian(MultiObjective* obj, std::vector<double>& X, std::vector<double>& dX, bool sharded) {
         const int P = sharded ? comm_size() : 1, r = sharded ? comm_rank() : 0;
-        int b = 0, cnt = 0;
-        block_range(n_, P, r, &b, &cnt);
+        std::vector<int> st, ct;
+        fd_tiles_of(n_, P, r, st, ct);
+        int cnt = 0;
+        for (int c : ct) cnt += c;
         if (pnol_dobj* d = obj->deviceObjective()) {
             x_.upload(X);
             h_.upload(dX);
-            check(pnol_fd_jacobian_d(ctx_, d, x_.get(), h_.get(), b, cnt, F0_.get(), 1, JT_.get() + (size_t)b * ldjt_,
-                                     ldjt_),
+            check(pnol_fd_jacobian_tiles_d(ctx_, d, x_.get(), h_.get(), st.data(), ct.data(), (int)st.size(),
+                                           F0_.get(), 1, JT_.get(), ldjt_),
                   "fd_jacobian");
             obj->countEvals(cnt + 1);
         } else {
-            // host objective: the reference's column loop for this rank's block, one upload
-            std::vector<double> F0(m_), FdX(m_), XdX(n_), blk((size_t)per_ * ldjt_, 0.0);
+            // host objective: the reference's column loop over this rank's tiles, one upload per tile
+            std::vector<double> F0(m_), FdX(m_), XdX(n_), blk((size_t)kFdTileCols * ldjt_, 0.0);
             obj->objEval(X, F0);
-            for (int q = 0; q < cnt; ++q) {
-                const int j = b + q;
-                XdX = X;
-                XdX[j] = XdX[j] + dX[j];
-                obj->objEval(XdX, FdX);
-                for (int i = 0; i < m_; ++i) blk[(size_t)q * ldjt_ + i] = (FdX[i] - F0[i]) / dX[j];
+            for (size_t t = 0; t < st.size(); ++t) {
+                for (int q = 0; q < ct[t]; ++q) {
+                    const int j = st[t] + q;
+                    XdX = X;
+                    XdX[j] = XdX[j] + dX[j];
+                    obj->objEval(XdX, FdX);
+                    for (int i = 0; i < m_; ++i) blk[(size_t)q * ldjt_ + i] = (FdX[i] - F0[i]) / dX[j];
+                }
+                JT_.upload(blk.data(), (size_t)ct[t] * ldjt_, (size_t)st[t] * ldjt_);
             }
-            if (cnt > 0) JT_.upload(blk.data(), (size_t)cnt * ldjt_, (size_t)b * ldjt_);
         }
-        if (P > 1)
-            check(comm_allgather_device(ctx_, JT_.get() + (size_t)r * per_ * ldjt_, JT_.get(), (size_t)per_ * ldjt_),
-                  "allgather(J)");
+        if (P > 1) check(comm_share_rows(ctx_, JT_.get(), ldjt_, n_), "share(J)");
     }
 
     // sigma = (J^T J + lambda diag(J^T J))^{-1} (-J^T F)   (LevenbergMarquardt.cpp:59-83);
@@ -100,7 +105,7 @@ class LMDevice {
 
   private:
     pnol_ctx* ctx_;
-    int n_, m_, ldjt_, lda_, per_;
+    int n_, m_, ldjt_, lda_;
     DevVec JT_, A_, rhs_, sigma_, x_, h_, F_, Fprev_, F0_;
 };
 

@@ -20,7 +20,9 @@
 //                        perturbation window (k_linres_fd: the full-B-tile form)
 #include "../pnol_internal.hpp"
 
+#include <algorithm>
 #include <cstdlib>
+#include <vector>
 
 namespace pnol {
 namespace {
@@ -208,114 +210,27 @@ __global__ __launch_bounds__(256) void k_linres_eval(const double* __restrict__ 
     if (t < 64 && row < m && F) F[row] = y ? acc - y[row] : acc;
 }
 
-// Batched FD GEMM.  Workgroup tile 128 residual rows x 64 points, K staged 16 at a time;
-// thread (ty, tx) = (t >> 4, t & 15) owns rows ty*8..+8 and points tx*4..+4 (32 fp64
-// accumulators), every accumulator a sequential fma chain over k = 0..n-1.
-// Prefix sharing: the chain of point j equals the base chain for every k < j (x is only
-// perturbed at k = j), so a tile whose first point is column jmin starts at
+// Batched FD GEMM.  Prefix sharing: the chain of point j equals the base chain for every k < j
+// (x is only perturbed at k = j), so a tile whose first point is column jmin starts at
 // ks = 16 * floor(jmin / 16) from the base chain's checkpoint C[ks / 16] and runs k = ks..n-1.
 // Same fma sequence per point, hence bit-identical output; about half the flops of the
 // full-length chains.
-constexpr int kBM = 128, kBN = 64, kBK = 16;
+constexpr int kBK = 16;
+constexpr int kFdTile = PNOL_FD_TILE;   // columns per point tile (BN of every launched variant)
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     const int xcd = orig % kNumXcd, q = nwg / kNumXcd, r = nwg % kNumXcd;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / kNumXcd;
 }
 
-template <bool EVEN>
-__global__ __launch_bounds__(256) void k_linres_fd(const double* __restrict__ A, const double* __restrict__ y,
-                                                   const double* __restrict__ x, const double* __restrict__ h, int m,
-                                                   int n, int j0, int cnt, const double* __restrict__ F0,
-                                                   const double* __restrict__ C, double* __restrict__ JT, long ldjt) {
-    __shared__ __attribute__((aligned(16))) double As[kBK][kBM];
-    __shared__ __attribute__((aligned(16))) double Bs[kBK][kBN];
-    const int nmt = (m + kBM - 1) / kBM, nnt = (cnt + kBN - 1) / kBN;
-    const int v = xcd_remap(blockIdx.x, nmt * nnt);
-    const int mt = v / nnt, nt = v % nnt;
-    const int m0 = mt * kBM, pbase = nt * kBN;       // pbase: point index relative to j0
-    const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
-
-    const int ks = ((j0 + pbase) / kBK) * kBK;       // kBK == kCkpt
-    double acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int row = min(m0 + ty * 8 + i, m - 1);
-        const double c0 = ks > 0 ? C[(long)(ks / kCkpt) * m + row] : 0.0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = c0;
-    }
-
-    // A stage: thread loads row (t >> 1), k-offset (t & 1) * 8, 8 doubles
-    const int lrow = t >> 1, lk = (t & 1) * 8;
-    const long arow = (long)min(m0 + lrow, m - 1) * n;
-    const bool rowok = m0 + lrow < m;
-    double areg[8];
-    auto load_a = [&](int k0) {
-        if (EVEN && rowok && k0 + kBK <= n) {
-            const double2* p = reinterpret_cast<const double2*>(A + arow + k0 + lk);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) { double2 w = p[q]; areg[2 * q] = w.x; areg[2 * q + 1] = w.y; }
-        } else {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int k = k0 + lk + q;
-                areg[q] = (rowok && k < n) ? A[arow + k] : 0.0;
-            }
-        }
-    };
-    const int nk = (n + kBK - 1) / kBK;
-    load_a(ks);
-    for (int kc = ks / kBK; kc < nk; ++kc) {
-        const int k0 = kc * kBK;
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 8; ++q) As[lk + q][lrow] = areg[q];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = t + 256 * q;
-            const int k = e / kBN, jj = e % kBN;
-            const int kk = k0 + k;
-            const int p = pbase + jj;
-            const int jcol = j0 + p;
-            double val = kk < n ? x[kk] : 0.0;
-            if (p < cnt && kk == jcol) val = x[kk] + h[jcol];
-            Bs[k][jj] = val;
-        }
-        __syncthreads();
-        if (kc + 1 < nk) load_a(k0 + kBK);
-#pragma unroll
-        for (int k = 0; k < kBK; ++k) {
-            double a[8], b[4];
-            const double2* ap = reinterpret_cast<const double2*>(&As[k][ty * 8]);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) { double2 w = ap[q]; a[2 * q] = w.x; a[2 * q + 1] = w.y; }
-            const double2* bp = reinterpret_cast<const double2*>(&Bs[k][tx * 4]);
-#pragma unroll
-            for (int q = 0; q < 2; ++q) { double2 w = bp[q]; b[2 * q] = w.x; b[2 * q + 1] = w.y; }
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = fma(a[i], b[j], acc[i][j]);
-        }
-    }
-    // epilogue: F = acc - y; J = (F - F0) / h
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int p = pbase + tx * 4 + j;
-        if (p >= cnt) continue;
-        const double hj = h[j0 + p];
-        double* out = JT + (long)p * ldjt;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int row = m0 + ty * 8 + i;
-            if (row < m) {
-                const double F = acc[i][j] - y[row];
-                out[row] = (F - F0[row]) / hj;
-            }
-        }
-    }
-}
+// Point tiles of one FD GEMM launch (kernel argument): columns [start[t], start[t] + count[t]).
+constexpr int kFdMaxTiles = 64;
+struct FdTiles {
+    int ntiles;
+    int jbase;   // JT row of column c is c - jbase
+    int start[kFdMaxTiles];
+    int count[kFdMaxTiles];
+};
 
 // Batched FD GEMM, x-broadcast form.  Thread (ty, tx) = (t >> 4, t & 15) owns RM rows and
 // PN points (RM * PN accumulators); workgroup tile (16 RM) rows x (16 PN) points.  The B
@@ -328,7 +243,7 @@ __global__ __launch_bounds__(256) void k_linres_fd(const double* __restrict__ A,
 template <bool EVEN, int RM, int PN, int OCC = 1, int KB = kBK>
 __global__ __launch_bounds__(256, OCC) void k_linres_fd2(const double* __restrict__ A, const double* __restrict__ y,
                                                     const double* __restrict__ x, const double* __restrict__ h, int m,
-                                                    int n, int j0, int cnt, const double* __restrict__ F0,
+                                                    int n, const FdTiles tl, const double* __restrict__ F0,
                                                     const double* __restrict__ C, double* __restrict__ JT, long ldjt) {
     constexpr int BM = 16 * RM, BN = 16 * PN;
     constexpr int TPR = 256 / BM;      // threads staging one A row
@@ -336,10 +251,11 @@ __global__ __launch_bounds__(256, OCC) void k_linres_fd2(const double* __restric
     __shared__ __attribute__((aligned(16))) double As[KB][BM];
     __shared__ __attribute__((aligned(16))) double Bs[KB][BN];
     __shared__ __attribute__((aligned(16))) double xs[KB];
-    const int nmt = (m + BM - 1) / BM, nnt = (cnt + BN - 1) / BN;
+    const int nmt = (m + BM - 1) / BM, nnt = tl.ntiles;
     const int v = xcd_remap(blockIdx.x, nmt * nnt);
     const int mt = v / nnt, nt = v % nnt;
-    const int m0 = mt * BM, pbase = nt * BN;
+    const int m0 = mt * BM;
+    const int j0 = tl.start[nt], cnt = tl.count[nt], pbase = 0;   // this tile's columns
     const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
     const int jfirst = j0 + pbase, jlast = j0 + min(pbase + BN, cnt) - 1;   // perturbed columns of the tile
     const int ks = (jfirst / kBK) * kBK;
@@ -431,134 +347,7 @@ __global__ __launch_bounds__(256, OCC) void k_linres_fd2(const double* __restric
         const int p = pbase + tx * PN + j;
         if (p >= cnt) continue;
         const double hj = h[j0 + p];
-        double* out = JT + (long)p * ldjt;
-#pragma unroll
-        for (int i = 0; i < RM; ++i) {
-            const int row = m0 + ty * RM + i;
-            if (row < m) out[row] = ((acc[i][j] - y[row]) - F0[row]) / hj;
-        }
-    }
-}
-
-// Batched FD GEMM, scalar-x form.  Thread (ty, tx) = (t / TX, t % TX) owns RM residual rows
-// and PN consecutive points; workgroup tile BM = (256 / TX) RM rows x BN = TX PN points.
-// Per k a thread reads its RM values of A (one LDS vector read, k-major double-buffered
-// stages padded against bank conflicts) and x[k] through the scalar cache (uniform address,
-// an SGPR operand of the fma), then issues RM * PN fmas.  Outside the perturbation window
-// every point's operand is x[k]; inside it (uniform per stage) each point selects
-// x[j] + h[j] at its own column k == j.  Every accumulator is still the objective's
-// sequential fma chain resumed from the base-chain checkpoint: bit-identical to k_linres_fd.
-template <bool EVEN, int RM, int PN, int TX>
-__global__ __launch_bounds__(256) void k_linres_fd3(const double* __restrict__ A, const double* __restrict__ y,
-                                                    const double* __restrict__ x, const double* __restrict__ h, int m,
-                                                    int n, int j0, int cnt, const double* __restrict__ F0,
-                                                    const double* __restrict__ C, double* __restrict__ JT, long ldjt) {
-    constexpr int TY = 256 / TX, BM = TY * RM, BN = TX * PN, LDA = BM + 2;
-    constexpr int SPT = BM * kBK / 256;   // A values staged per thread per stage
-    constexpr int TPR = kBK / SPT;        // staging threads per A row
-    static_assert(RM == 2 || RM == 4, "RM");
-    static_assert(SPT % 2 == 0 && TPR * SPT == kBK, "staging shape");
-    __shared__ __attribute__((aligned(16))) double As[2][kBK][LDA];
-    const int nmt = (m + BM - 1) / BM, nnt = (cnt + BN - 1) / BN;
-    const int v = xcd_remap(blockIdx.x, nmt * nnt);
-    const int mt = v / nnt, nt = v % nnt;
-    const int m0 = mt * BM, pbase = nt * BN;
-    const int t = threadIdx.x, tx = t % TX, ty = t / TX;
-    const int jfirst = j0 + pbase, jlast = j0 + min(pbase + BN, cnt) - 1;
-    const int ks = (jfirst / kBK) * kBK;
-    const int jc0 = jfirst + tx * PN;   // this thread's first point column
-
-    double acc[RM][PN];
-#pragma unroll
-    for (int i = 0; i < RM; ++i) {
-        const int row = min(m0 + ty * RM + i, m - 1);
-        const double c0 = ks > 0 ? C[(long)(ks / kCkpt) * m + row] : 0.0;
-#pragma unroll
-        for (int j = 0; j < PN; ++j) acc[i][j] = c0;
-    }
-    double xph[PN];   // the perturbed coordinate of each point, formed as the reference forms it
-#pragma unroll
-    for (int j = 0; j < PN; ++j) {
-        const int jc = min(jc0 + j, n - 1);
-        xph[j] = x[jc] + h[jc];
-    }
-
-    const int lrow = t / TPR, lk = (t % TPR) * SPT;
-    const long arow = (long)min(m0 + lrow, m - 1) * n;
-    const bool rowok = m0 + lrow < m;
-    double areg[SPT];
-    auto load_a = [&](int k0) {
-        if (EVEN && rowok && k0 + kBK <= n) {
-            const double2* p = reinterpret_cast<const double2*>(A + arow + k0 + lk);
-#pragma unroll
-            for (int q = 0; q < SPT / 2; ++q) { double2 w = p[q]; areg[2 * q] = w.x; areg[2 * q + 1] = w.y; }
-        } else {
-#pragma unroll
-            for (int q = 0; q < SPT; ++q) {
-                const int k = k0 + lk + q;
-                areg[q] = (rowok && k < n) ? A[arow + k] : 0.0;
-            }
-        }
-    };
-    auto store_a = [&](int buf) {
-#pragma unroll
-        for (int q = 0; q < SPT; ++q) As[buf][lk + q][lrow] = areg[q];
-    };
-    const int nk = (n + kBK - 1) / kBK;
-    int kc = ks / kBK;
-    load_a(kc * kBK);
-    store_a(0);
-    __syncthreads();
-    for (int buf = 0; kc < nk; ++kc, buf ^= 1) {
-        const int k0 = kc * kBK;
-        if (kc + 1 < nk) load_a(k0 + kBK);
-        const bool window = k0 <= jlast && k0 + kBK > jfirst;   // uniform over the workgroup
-        if (window) {
-#pragma unroll
-            for (int k = 0; k < kBK; ++k) {
-                const int kk = k0 + k;
-                const double xk = kk < n ? x[kk] : 0.0;
-                double a[RM];
-#pragma unroll
-                for (int i = 0; i < RM; i += 2) {
-                    const double2 w = *reinterpret_cast<const double2*>(&As[buf][k][ty * RM + i]);
-                    a[i] = w.x; a[i + 1] = w.y;
-                }
-#pragma unroll
-                for (int j = 0; j < PN; ++j) {
-                    const double b = (kk == jc0 + j) ? xph[j] : xk;
-#pragma unroll
-                    for (int i = 0; i < RM; ++i) acc[i][j] = fma(a[i], b, acc[i][j]);
-                }
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < kBK; ++k) {
-                const int kk = k0 + k;
-                const double xk = (EVEN || kk < n) ? x[min(kk, n - 1)] : 0.0;
-                double a[RM];
-#pragma unroll
-                for (int i = 0; i < RM; i += 2) {
-                    const double2 w = *reinterpret_cast<const double2*>(&As[buf][k][ty * RM + i]);
-                    a[i] = w.x; a[i + 1] = w.y;
-                }
-#pragma unroll
-                for (int i = 0; i < RM; ++i)
-#pragma unroll
-                    for (int j = 0; j < PN; ++j) acc[i][j] = fma(a[i], xk, acc[i][j]);
-                if (k & 1) __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        if (kc + 1 < nk) store_a(buf ^ 1);
-        __syncthreads();
-    }
-    // epilogue: F = acc - y; J = (F - F0) / h
-#pragma unroll
-    for (int j = 0; j < PN; ++j) {
-        const int p = pbase + tx * PN + j;
-        if (p >= cnt) continue;
-        const double hj = h[j0 + p];
-        double* out = JT + (long)p * ldjt;
+        double* out = JT + (long)(j0 + p - tl.jbase) * ldjt;
 #pragma unroll
         for (int i = 0; i < RM; ++i) {
             const int row = m0 + ty * RM + i;
@@ -652,91 +441,102 @@ int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
     return launch_check();
 }
 
+// FD Jacobian rows for the point tiles [start[t], start[t] + count[t]) (count <= kFdTile),
+// column c written to JT row c - jbase.  Linear residual: one base-chain pass (F0 and the
+// prefix checkpoints), then the FD GEMM over all tiles in launches of <= kFdMaxTiles tiles.
+int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, const int* start,
+                             const int* count, int ntiles, double* F0, int compute_f0, double* JT, int jbase,
+                             int ldjt) {
+    if (!o || !x || !h || !F0 || is_scalar_kind(o->kind) || ntiles < 0 || ldjt < o->m) return PNOL_ERR_ARG;
+    for (int t = 0; t < ntiles; ++t)
+        if (start[t] < 0 || count[t] < 0 || count[t] > kFdTile || start[t] + count[t] > o->n || start[t] < jbase)
+            return PNOL_ERR_ARG;
+    int total = 0;
+    for (int t = 0; t < ntiles; ++t) total += count[t];
+    if (total > 0 && !JT) return PNOL_ERR_ARG;
+    if (o->kind != PNOL_OBJ_LINRES || total == 0) {
+        if (compute_f0) PNOL_CHECK(launch_dobj_eval(ctx, o, x, F0));
+        for (int t = 0; t < ntiles; ++t)
+            if (count[t] > 0)
+                PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, start[t], count[t], F0, 0,
+                                              JT + (size_t)(start[t] - jbase) * ldjt, ldjt));
+        return PNOL_OK;
+    }
+    // one pass of the base chain: F0 (when asked) and the prefix checkpoints
+    void* C = nullptr;
+    const int ncp = (o->n + kCkpt - 1) / kCkpt;
+    PNOL_CHECK(ws_get(ctx, "linres_ckpt", sizeof(double) * (size_t)o->m * (ncp > 1 ? ncp : 1), &C));
+    double* f0_out = compute_f0 ? F0 : nullptr;
+    {
+        ScopedTimer tm(ctx, "fd_ckpt");
+        if ((o->n % 2) == 0)
+            hipLaunchKernelGGL((k_linres_eval<true, true>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0,
+                               ctx->stream, o->p0, x, o->p1, o->m, o->n, f0_out, (double*)C);
+        else
+            hipLaunchKernelGGL((k_linres_eval<false, true>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0,
+                               ctx->stream, o->p0, x, o->p1, o->m, o->n, f0_out, (double*)C);
+    }
+    PNOL_CHECK(launch_check());
+    // PNOL_FD_KERNEL selects the FD GEMM (tuning; all variants are bitwise equal):
+    // 2 = x-broadcast 128 x 128 tiles (8 x 8 per thread), 3 = 64 x 128 (4 x 8) with 16-deep K
+    // stages, 4 (default) = 64 x 128 with 32-deep K stages.
+    static const int fdk = [] {
+        const char* e = std::getenv("PNOL_FD_KERNEL");
+        const int v = e ? std::atoi(e) : 4;
+        return (v >= 2 && v <= 4) ? v : 4;
+    }();
+    const bool even = (o->n % 2) == 0;
+    ScopedTimer tm(ctx, "fd_jacobian");
+    const double* Cc = (const double*)C;
+    for (int t0 = 0; t0 < ntiles; t0 += kFdMaxTiles) {
+        FdTiles tl;
+        tl.ntiles = std::min(kFdMaxTiles, ntiles - t0);
+        tl.jbase = jbase;
+        for (int t = 0; t < tl.ntiles; ++t) {
+            tl.start[t] = start[t0 + t];
+            tl.count[t] = count[t0 + t];
+        }
+        const dim3 g1(((o->m + 127) / 128) * tl.ntiles), g2(((o->m + 63) / 64) * tl.ntiles);
+        if (fdk == 2) {
+            if (even)
+                hipLaunchKernelGGL((k_linres_fd2<true, 8, 8>), g1, dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
+                                   o->n, tl, F0, Cc, JT, (long)ldjt);
+            else
+                hipLaunchKernelGGL((k_linres_fd2<false, 8, 8>), g1, dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
+                                   o->n, tl, F0, Cc, JT, (long)ldjt);
+        } else if (fdk == 3) {
+            if (even)
+                hipLaunchKernelGGL((k_linres_fd2<true, 4, 8>), g2, dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
+                                   o->n, tl, F0, Cc, JT, (long)ldjt);
+            else
+                hipLaunchKernelGGL((k_linres_fd2<false, 4, 8>), g2, dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
+                                   o->n, tl, F0, Cc, JT, (long)ldjt);
+        } else {
+            if (even)
+                hipLaunchKernelGGL((k_linres_fd2<true, 4, 8, 1, 32>), g2, dim3(256), 0, ctx->stream, o->p0, o->p1, x, h,
+                                   o->m, o->n, tl, F0, Cc, JT, (long)ldjt);
+            else
+                hipLaunchKernelGGL((k_linres_fd2<false, 4, 8, 1, 32>), g2, dim3(256), 0, ctx->stream, o->p0, o->p1, x,
+                                   h, o->m, o->n, tl, F0, Cc, JT, (long)ldjt);
+        }
+        PNOL_CHECK(launch_check());
+    }
+    return PNOL_OK;
+}
+
 int launch_fd_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int j0, int cnt, double* F0,
                        int compute_f0, double* JT, int ldjt) {
     if (!o || !x || !h || !F0 || is_scalar_kind(o->kind)) return PNOL_ERR_ARG;
     if (j0 < 0 || cnt < 0 || j0 + cnt > o->n || ldjt < o->m) return PNOL_ERR_ARG;
     if (o->kind == PNOL_OBJ_LINRES && cnt > 0) {
-        if (!JT) return PNOL_ERR_ARG;
-        // one pass of the base chain: F0 (when asked) and the prefix checkpoints
-        void* C = nullptr;
-        const int ncp = (o->n + kCkpt - 1) / kCkpt;
-        PNOL_CHECK(ws_get(ctx, "linres_ckpt", sizeof(double) * (size_t)o->m * (ncp > 1 ? ncp : 1), &C));
-        double* f0_out = compute_f0 ? F0 : nullptr;
-        {
-            ScopedTimer tm(ctx, "fd_ckpt");
-            if ((o->n % 2) == 0)
-                hipLaunchKernelGGL((k_linres_eval<true, true>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0,
-                                   ctx->stream, o->p0, x, o->p1, o->m, o->n, f0_out, (double*)C);
-            else
-                hipLaunchKernelGGL((k_linres_eval<false, true>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0,
-                                   ctx->stream, o->p0, x, o->p1, o->m, o->n, f0_out, (double*)C);
+        // the contiguous block as consecutive kFdTile-column tiles
+        std::vector<int> st, ct;
+        for (int c = j0; c < j0 + cnt; c += kFdTile) {
+            st.push_back(c);
+            ct.push_back(std::min(kFdTile, j0 + cnt - c));
         }
-        PNOL_CHECK(launch_check());
-        // PNOL_FD_KERNEL selects the FD GEMM (tuning): 1 = 128 x 64-point tile with a full B tile
-        // every stage; 2 = x-broadcast 128 x 128 (8 x 8 per thread); 3 (default) = x-broadcast
-        // 64 x 128 (4 x 8 per thread).
-        static const int fdk = [] {
-            const char* e = std::getenv("PNOL_FD_KERNEL");
-            const int v = e ? std::atoi(e) : 3;
-            return (v >= 1 && v <= 8) ? v : 3;
-        }();
-        const bool even = (o->n % 2) == 0;
-        ScopedTimer tm(ctx, "fd_jacobian");
-        const double* F0c = F0;
-        const double* Cc = (const double*)C;
-        auto nwg = [&](int bm, int bn) { return dim3(((o->m + bm - 1) / bm) * ((cnt + bn - 1) / bn)); };
-        if (fdk == 1) {
-            if (even)
-                hipLaunchKernelGGL((k_linres_fd<true>), nwg(kBM, kBN), dim3(256), 0, ctx->stream, o->p0, o->p1, x, h,
-                                   o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
-            else
-                hipLaunchKernelGGL((k_linres_fd<false>), nwg(kBM, kBN), dim3(256), 0, ctx->stream, o->p0, o->p1, x, h,
-                                   o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
-        } else if (fdk == 2) {
-            if (even)
-                hipLaunchKernelGGL((k_linres_fd2<true, 8, 8>), nwg(128, 128), dim3(256), 0, ctx->stream, o->p0, o->p1,
-                                   x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
-            else
-                hipLaunchKernelGGL((k_linres_fd2<false, 8, 8>), nwg(128, 128), dim3(256), 0, ctx->stream, o->p0, o->p1,
-                                   x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
-        } else if (fdk == 4) {
-            if (even)
-                hipLaunchKernelGGL((k_linres_fd3<true, 2, 16, 8>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0,
-                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
-            else
-                hipLaunchKernelGGL((k_linres_fd3<false, 2, 16, 8>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0,
-                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
-        } else if (fdk == 5) {
-            if (even)
-                hipLaunchKernelGGL((k_linres_fd3<true, 4, 8, 16>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0,
-                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
-            else
-                hipLaunchKernelGGL((k_linres_fd3<false, 4, 8, 16>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0,
-                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
-        } else if (fdk == 7 || fdk == 8) {
-            if (fdk == 7)
-                hipLaunchKernelGGL((k_linres_fd2<true, 4, 8, 1, 32>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0,
-                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
-            else
-                hipLaunchKernelGGL((k_linres_fd2<true, 4, 8, 1, 64>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0,
-                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
-        } else if (fdk == 6) {
-            if (even)
-                hipLaunchKernelGGL((k_linres_fd3<true, 4, 16, 8>), nwg(128, 128), dim3(256), 0, ctx->stream, o->p0,
-                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
-            else
-                hipLaunchKernelGGL((k_linres_fd3<false, 4, 16, 8>), nwg(128, 128), dim3(256), 0, ctx->stream, o->p0,
-                                   o->p1, x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
-        } else {
-            if (even)
-                hipLaunchKernelGGL((k_linres_fd2<true, 4, 8>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0, o->p1,
-                                   x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
-            else
-                hipLaunchKernelGGL((k_linres_fd2<false, 4, 8>), nwg(64, 128), dim3(256), 0, ctx->stream, o->p0, o->p1,
-                                   x, h, o->m, o->n, j0, cnt, F0c, Cc, JT, (long)ldjt);
-        }
-        return launch_check();
+        return launch_fd_jacobian_tiles(ctx, o, x, h, st.data(), ct.data(), (int)st.size(), F0, compute_f0, JT, j0,
+                                        ldjt);
     }
     if (compute_f0) PNOL_CHECK(launch_dobj_eval(ctx, o, x, F0));
     if (cnt == 0) return PNOL_OK;

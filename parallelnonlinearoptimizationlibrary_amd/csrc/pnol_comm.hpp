@@ -2,6 +2,7 @@
 #pragma once
 
 #include <cstddef>
+#include <vector>
 
 #include "pnol_amd.h"
 
@@ -11,6 +12,12 @@ int comm_size();
 int comm_rank();
 // contiguous ceil-sized column block of `rank`
 void block_range(int ncols, int nranks, int rank, int* begin, int* count);
+// cost-balanced FD column tiles (PNOL_FD_TILE columns each, dealt in snake order)
+constexpr int kFdTileCols = PNOL_FD_TILE;
+int fd_tile_owner(int tile, int nranks);
+void fd_tiles_of(int ncols, int nranks, int rank, std::vector<int>& start, std::vector<int>& count);
+// every rank ends with all ncols rows of buf (row c at buf + c * ld), owners per fd_tiles_of
+int comm_share_rows(pnol_ctx* ctx, double* buf, size_t ld, int ncols);
 // recv[r*count + i] = send_r[i]; host buffers (any backend)
 int comm_allgather_host(pnol_ctx* ctx, const double* send, double* recv, size_t count);
 // device buffers (RCCL backend native; host backend bounces through host memory)

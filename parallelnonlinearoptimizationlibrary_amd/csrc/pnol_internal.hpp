@@ -130,6 +130,9 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
 int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
 int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt,
                        double* f0, double* g);
+int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, const int* start,
+                             const int* count, int ntiles, double* F0, int compute_f0, double* JT, int jbase,
+                             int ldjt);
 int launch_fd_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int j0, int cnt,
                        double* F0, int compute_f0, double* JT, int ldjt);
 int launch_synthetic_quadratic(pnol_ctx* ctx, unsigned long long seed, int n, double bscale, double* d, double* b);

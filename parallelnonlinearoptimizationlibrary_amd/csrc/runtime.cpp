@@ -9,6 +9,8 @@
 #include <cstring>
 
 #include "pnol_comm.hpp"
+
+#include <algorithm>
 #include "pnol_internal.hpp"
 
 namespace pnol {
@@ -65,6 +67,78 @@ void block_range(int ncols, int nranks, int rank, int* begin, int* count) {
     if (e > ncols) e = ncols;
     *begin = b;
     *count = e - b;
+}
+
+// Cost-balanced FD column tiles: the ceil(ncols / tile) tiles are dealt to the ranks in
+// snake order (0, 1, .., P-1, P-1, .., 0, 0, 1, ..).  With prefix sharing the cost of FD
+// column j falls linearly with j, so each rank's sum pairs an expensive tile with a cheap
+// one; contiguous blocks would leave rank 0 with ~2x the mean work at P = 8.
+int fd_tile_owner(int tile, int nranks) {
+    const int round = tile / nranks, pos = tile % nranks;
+    return (round & 1) ? nranks - 1 - pos : pos;
+}
+
+void fd_tiles_of(int ncols, int nranks, int rank, std::vector<int>& start, std::vector<int>& count) {
+    start.clear();
+    count.clear();
+    const int nt = (ncols + kFdTileCols - 1) / kFdTileCols;
+    for (int t = 0; t < nt; ++t) {
+        if (fd_tile_owner(t, nranks) != rank) continue;
+        start.push_back(t * kFdTileCols);
+        count.push_back(std::min(kFdTileCols, ncols - t * kFdTileCols));
+    }
+}
+
+// Every rank ends with all ncols rows of buf (row c at buf + c * ld); rank r contributes the
+// rows of its fd_tiles_of tiles.  RCCL: one group of point-to-point sends / receives straight
+// into place (each tile goes owner -> every peer over its own xGMI link).  Host backend:
+// pack, allgather through host memory, unpack.
+int comm_share_rows(pnol_ctx* ctx, double* buf, size_t ld, int ncols) {
+    const int P = g_comm.nranks, me = g_comm.rank;
+    if (g_comm.kind == 0 || P == 1) return PNOL_OK;
+    const int nt = (ncols + kFdTileCols - 1) / kFdTileCols;
+    if (g_comm.kind == 1) {
+        ScopedTimer tm(ctx, "allgather");
+        if (ncclGroupStart() != ncclSuccess) return PNOL_ERR_COMM;
+        for (int t = 0; t < nt; ++t) {
+            const int o = fd_tile_owner(t, P);
+            const size_t c0 = (size_t)t * kFdTileCols, rows = std::min(kFdTileCols, ncols - t * kFdTileCols);
+            double* p = buf + c0 * ld;
+            if (o == me) {
+                for (int q = 0; q < P; ++q)
+                    if (q != me && ncclSend(p, rows * ld, ncclDouble, q, g_comm.nccl, ctx->stream) != ncclSuccess) {
+                        ncclGroupEnd();
+                        return PNOL_ERR_COMM;
+                    }
+            } else if (ncclRecv(p, rows * ld, ncclDouble, o, g_comm.nccl, ctx->stream) != ncclSuccess) {
+                ncclGroupEnd();
+                return PNOL_ERR_COMM;
+            }
+        }
+        if (ncclGroupEnd() != ncclSuccess) return PNOL_ERR_COMM;
+        return PNOL_OK;
+    }
+    // host backend: every rank packs at most ceil(nt / P) tiles into one slot of the gather
+    const int slot_tiles = (nt + P - 1) / P;
+    const size_t slot = (size_t)slot_tiles * kFdTileCols * ld;
+    void *sv = nullptr, *rv = nullptr;
+    PNOL_CHECK(ws_get(ctx, "share_send", sizeof(double) * slot, &sv));
+    PNOL_CHECK(ws_get(ctx, "share_recv", sizeof(double) * slot * P, &rv));
+    double *send = (double*)sv, *recv = (double*)rv;
+    std::vector<int> st, ct;
+    fd_tiles_of(ncols, P, me, st, ct);
+    for (size_t i = 0; i < st.size(); ++i)
+        PNOL_HIP(hipMemcpyAsync(send + i * kFdTileCols * ld, buf + (size_t)st[i] * ld, sizeof(double) * ct[i] * ld,
+                                hipMemcpyDeviceToDevice, ctx->stream));
+    PNOL_CHECK(comm_allgather_device(ctx, send, recv, slot));
+    for (int r = 0; r < P; ++r) {
+        if (r == me) continue;
+        fd_tiles_of(ncols, P, r, st, ct);
+        for (size_t i = 0; i < st.size(); ++i)
+            PNOL_HIP(hipMemcpyAsync(buf + (size_t)st[i] * ld, recv + r * slot + i * kFdTileCols * ld,
+                                    sizeof(double) * ct[i] * ld, hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    return PNOL_OK;
 }
 
 int comm_allgather_host(pnol_ctx* ctx, const double* send, double* recv, size_t count) {
@@ -361,6 +435,22 @@ int pnol_comm_allgather_d(pnol_ctx* ctx, const double* send, double* recv, size_
 
 void pnol_block_range(int ncols, int nranks, int rank, int* begin, int* count) {
     block_range(ncols, nranks, rank, begin, count);
+}
+
+int pnol_fd_tiles(int ncols, int nranks, int rank, int* start, int* count, int cap) {
+    if (ncols < 0 || nranks < 1 || rank < 0 || rank >= nranks) return -PNOL_ERR_ARG;
+    std::vector<int> st, ct;
+    fd_tiles_of(ncols, nranks, rank, st, ct);
+    for (size_t i = 0; i < st.size() && (int)i < cap; ++i) {
+        if (start) start[i] = st[i];
+        if (count) count[i] = ct[i];
+    }
+    return (int)st.size();
+}
+
+int pnol_comm_share_fd_rows_d(pnol_ctx* ctx, double* buf, int ld, int ncols) {
+    if (!ctx || !buf || ld < 1 || ncols < 0) return PNOL_ERR_ARG;
+    return comm_share_rows(ctx, buf, (size_t)ld, ncols);
 }
 
 }  // extern "C"

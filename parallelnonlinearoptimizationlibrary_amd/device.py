@@ -187,6 +187,18 @@ class DeviceObjective:
         return F0, JT
 
 
+    def fd_jacobian_tiles(self, x, h, tiles, JT, F0=None, compute_f0=True):
+        """FD rows of the (start, count) tiles into JT (row c = column c); returns (F0, JT)."""
+        F0 = self.ctx.empty(self.m) if F0 is None else F0
+        k = len(tiles)
+        st = (C.c_int * max(k, 1))(*[t[0] for t in tiles])
+        ct = (C.c_int * max(k, 1))(*[t[1] for t in tiles])
+        L.check(L.lib().pnol_fd_jacobian_tiles_d(self.ctx.h, self.h, _ptr(x), _ptr(h), st, ct, k, _ptr(F0),
+                                                 int(compute_f0), _ptr(JT), JT.stride(0)),
+                "pnol_fd_jacobian_tiles_d")
+        return F0, JT
+
+
 def run_bfgs(obj: DeviceObjective, x0, params, which=0, host_eval=False, lb=None, ub=None):
     """Run the C++ drop-in BFGS (0), BFGS_MPI (1) or BFGS_Bnd (2) on a device objective."""
     X = np.array(x0, dtype=np.float64)

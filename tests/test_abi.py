@@ -50,3 +50,24 @@ def test_block_range_partitions_columns(n, P):
         assert c >= 0 and (c == 0 or b == r * per)
         seen.extend(range(b, b + c))
     assert seen == list(range(n))
+
+
+@pytest.mark.parametrize("n,P", [(2048, 8), (2048, 4), (2048, 2), (2048, 3), (2000, 8), (100, 4), (1, 1), (4096, 8)])
+def test_fd_tiles_partition_and_balance(n, P):
+    """LevMarqMPI's FD split: every column exactly once, tiles of PNOL_FD_TILE columns, and with
+    prefix sharing (column j costs ~ n - 16 floor(j0 / 16) for its tile start j0) the per-rank
+    cost within a few percent of the mean whenever every rank holds an even tile count."""
+    from parallelnonlinearoptimizationlibrary_amd import fd_tiles
+    cols, cost = [], []
+    for r in range(P):
+        tl = fd_tiles(n, P, r)
+        c = 0
+        for s0, cnt in tl:
+            assert s0 % 128 == 0 and 0 < cnt <= 128
+            cols.extend(range(s0, s0 + cnt))
+            c += cnt * (n - s0)
+        cost.append(c)
+    assert sorted(cols) == list(range(n))
+    nt = -(-n // 128)
+    if nt % (2 * P) == 0:
+        assert max(cost) <= 1.05 * (sum(cost) / P)

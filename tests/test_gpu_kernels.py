@@ -362,6 +362,33 @@ def test_fd_jacobian_linres_bitwise(ctx, oracle, m, n, j0, cnt):
     assert np.array_equal(_np(F0b), oracle.obj_eval_multi(o, x))
 
 
+@pytest.mark.parametrize("m,n,P", [(513, 700, 3), (300, 1000, 4), (257, 2048, 8), (130, 129, 2)])
+def test_fd_jacobian_tiles_bitwise(ctx, oracle, m, n, P):
+    """LevMarqMPI's cost-balanced tile sets (pnol_fd_tiles), each rank's tiles evaluated in
+    place: the union is bitwise the oracle's FD Jacobian and untouched rows stay untouched."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L, fd_tiles
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    A, xs, y = oracle.linres_data(m, n)
+    d = DeviceObjective(ctx, L.OBJ_LINRES, n, m, A, y)
+    x = np.linspace(-0.5, 0.5, n); h = np.full(n, 1e-7)
+    o = oracle.Obj(oracle.LINRES, n, m, A, y)
+    ref = oracle.fd_jacobian(o, x, h).T
+    full = np.zeros((n, m))
+    for r in range(P):
+        tiles = fd_tiles(n, P, r)
+        JT = ctx.tensor(np.full((n, m), 7.0))
+        F0, JT = d.fd_jacobian_tiles(ctx.tensor(x), ctx.tensor(h), tiles, JT)
+        got = _np(JT)
+        mine = np.zeros(n, dtype=bool)
+        for s0, c in tiles:
+            mine[s0:s0 + c] = True
+        assert np.array_equal(got[mine], ref[mine]), r
+        assert np.all(got[~mine] == 7.0)
+        assert np.array_equal(_np(F0), oracle.obj_eval_multi(o, x))
+        full[mine] = got[mine]
+    assert np.array_equal(full, ref)
+
+
 def test_synthetic_data_matches_oracle_stream(ctx, oracle):
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective

@@ -1,4 +1,4 @@
-"""Time the FD Jacobian GEMM variants (PNOL_FD_KERNEL=1..6, argv selects; default 1 2 3) on the bench workload (linres
+"""Time the FD Jacobian GEMM variants (PNOL_FD_KERNEL=2..4, argv selects; default all) on the bench workload (linres
 m=16384, n=2048, all columns), HIP-event timers on the context stream, one child process per
 variant (the selector is read once per process).  Also checks the variants are bitwise equal."""
 import json
@@ -37,7 +37,7 @@ print(json.dumps(out))
 
 if __name__ == "__main__":
     shas = set()
-    for v in (sys.argv[1:] or ["1", "2", "3"]):
+    for v in (sys.argv[1:] or ["2", "3", "4"]):
         env = dict(os.environ, PNOL_FD_KERNEL=v)
         p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
         if p.returncode != 0:
