@@ -66,13 +66,13 @@ def pmc_traffic():
         return {}
 
 
-def fd_flop_executed(m, n, j0, cnt, bn=64, bk=16):
-    """fp64 flops k_linres_fd runs for points [j0, j0+cnt): each 64-point tile continues the
-    base chain from the checkpoint at ks = 16*floor(first column / 16) to k = n-1."""
+def fd_flop_executed(m, n, tiles, bk=16):
+    """fp64 flops the FD GEMM runs for the (start, count) point tiles: each tile continues the
+    base chain from the checkpoint at ks = 16*floor(start / 16) to k = n-1 for all its points."""
     tot = 0
-    for pb in range(0, cnt, bn):
-        ks = ((j0 + pb) // bk) * bk
-        tot += min(bn, cnt - pb) * (n - ks)
+    for s0, cnt in tiles:
+        ks = (s0 // bk) * bk
+        tot += cnt * (n - ks)
     return 2.0 * m * tot
 
 
@@ -214,6 +214,15 @@ def main():
         elapsed = float(tt.item())
     timers = {k: _timer(L, dctx, k) for k in ("fd_jacobian", "fd_ckpt", "linres_eval", "syrk", "syrk_reduce", "jtr",
                                               "solve", "allgather")}
+    # per-step kernel times, max over ranks (the slowest rank sets the pace)
+    per_local = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timers.items()}
+    if world > 1:
+        keys = sorted(per_local)
+        tv = torch.tensor([per_local[k] for k in keys], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tv, op=dist.ReduceOp.MAX)
+        per_max = dict(zip(keys, tv.tolist()))
+    else:
+        per_max = dict(per_local)
     L.check(L.lib().pnol_ctx_enable_timers(dctx, 0), "timers")
     err = float(np.max(np.abs(X - obj.xstar)) / np.max(np.abs(obj.xstar)))
 
@@ -222,12 +231,14 @@ def main():
         hg = bench_hg(ctx, HG_N)
         hg4096 = bench_hg(ctx, 4096)
     if rank == 0:
-        per = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timers.items()}
+        per = per_local
         syrk_ms = per["syrk"]
         jtj_flop = float(m) * n * (n + 1)                   # unique entries of the symmetric result
-        my_cols = -(-n // world)
+        from parallelnonlinearoptimizationlibrary_amd import fd_tiles
+        my_tiles = fd_tiles(n, world, rank)                  # this rank's cost-balanced FD tiles
+        my_cols = sum(c for _, c in my_tiles)
         fd_flop_nominal = 2.0 * m * n * my_cols              # full-length chains for this rank's points
-        fd_flop = fd_flop_executed(m, n, 0, my_cols)          # prefix-shared chains actually run
+        fd_flop = fd_flop_executed(m, n, my_tiles)           # prefix-shared chains actually run
         pmc = pmc_traffic()
         roofline = {
             "kernel": "k_syrk_tile (J^T J, fp64 MFMA v_mfma_f64_16x16x4_f64)",
@@ -238,7 +249,7 @@ def main():
         roofline["frac"] = roofline["achieved"] / FP64_PEAK_TFLOPS if roofline["achieved"] else None
         fd_ms = per["fd_jacobian"]
         rooflines = {
-            "fd_jacobian": {"kernel": "k_linres_fd (batched FD GEMM, fp64 VALU fma, prefix-shared chains)",
+            "fd_jacobian": {"kernel": "k_linres_fd2<4,8,KB=32> (batched FD GEMM, fp64 VALU fma, prefix-shared chains)",
                             "bound": "valu_fp64", "ms": fd_ms,
                             "achieved": fd_flop / (fd_ms * 1e-3) / 1e12 if fd_ms else None,
                             "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "flop_executed": fd_flop,
@@ -269,11 +280,14 @@ def main():
             "dtype": "f64",
             "data": "synthetic (splitmix64 seed 0x5EED2018, r(x)=Ax-y generated in HBM)",
             "config": {"workload": f"LevenbergMarquardt{'MPI' if world > 1 else ''} m={m} n={n}, "
-                                   f"FD columns {'sharded over ' + str(world) + ' GPUs + RCCL allgather' if world > 1 else 'on 1 GPU'}",
+                                   f"FD columns {'in cost-balanced tiles over ' + str(world) + ' GPUs + RCCL row exchange' if world > 1 else 'on 1 GPU'}",
                        "m": m, "n": n, "parallelism": f"fd-columns x{world}" if world > 1 else "single"},
             "roofline": roofline,
             "rooflines": rooflines,
             "kernel_ms_per_step": per,
+            "kernel_ms_per_step_max_over_ranks": per_max,
+            # the north star's strong-scaling quantity: sharded FD Jacobian + row exchange
+            "fd_jacobian_ms_max_over_ranks": per_max["fd_jacobian"] + per_max["fd_ckpt"] + per_max["allgather"],
             "converged_rel_err_vs_xstar": err,
             "bfgs_hg": hg, "bfgs_hg_n4096": hg4096 if hg else None,
             "cpu_baseline": cpu,
