@@ -212,8 +212,8 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    timers = {k: _timer(L, dctx, k) for k in ("fd_jacobian", "fd_ckpt", "linres_eval", "syrk", "syrk_reduce", "jtr",
-                                              "solve", "allgather")}
+    timers = {k: _timer(L, dctx, k) for k in ("fd_jtj", "fd_jacobian", "fd_ckpt", "linres_eval", "syrk", "syrk_rows",
+                                              "syrk_reduce", "jtr", "solve", "allgather")}
     # per-step kernel times, max over ranks (the slowest rank sets the pace)
     per_local = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timers.items()}
     if world > 1:

@@ -145,6 +145,14 @@ int pnol_fd_gradient_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const dou
  * F0 = F(x) (computed here when compute_f0, else read), JT row (j - j0) = (F(x + h_j e_j) - F0)/h_j. */
 int pnol_fd_jacobian_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, int j0, int cnt,
                        double* F0, int compute_f0, double* JT, int ldjt);
+/* One LevMarq Jacobian + normal matrix, pipelined (LevenbergMarquardt.cpp:55-73): the FD
+ * Jacobian of all n columns into JT (as pnol_fd_jacobian_d with j0 = 0) and A = J^T J with
+ * A_ii = (1 + lambda) (J^T J)_ii (as pnol_jtj_d).  The FD column chunks run on the context
+ * stream and the J^T J tile rows each chunk completes on a second stream, so the VALU-bound
+ * FD GEMM and the MFMA-bound J^T J overlap.  Bitwise the same JT and A as the two calls;
+ * nchunks <= 1 runs them back to back. */
+int pnol_fd_jtj_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0, int compute_f0,
+                  double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, int nchunks);
 /* The FD Jacobian rows of a tile list (columns [start[t], start[t] + count[t]), count <=
  * PNOL_FD_TILE), column c written to JT + c * ldjt; one base-chain pass for all tiles. */
 int pnol_fd_jacobian_tiles_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, const int* start,

@@ -198,6 +198,13 @@ int pnol_fd_jacobian_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const dou
     return launch_fd_jacobian(ctx, obj, x, h, j0, cnt, F0, compute_f0, JT, ldjt);
 }
 
+int pnol_fd_jtj_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0, int compute_f0,
+                  double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, int nchunks) {
+    PNOL_CHECK(set_device(ctx));
+    if (!obj || !x || !h || !F0 || !JT || !A || ldjt < obj->m || lda < obj->n) return PNOL_ERR_ARG;
+    return launch_fd_jtj(ctx, obj, x, h, F0, compute_f0, JT, ldjt, lambda, A, lda, jtj_diag, nchunks);
+}
+
 int pnol_fd_jacobian_tiles_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, const int* start,
                              const int* count, int ntiles, double* F0, int compute_f0, double* JT, int ldjt) {
     PNOL_CHECK(set_device(ctx));

@@ -3,6 +3,7 @@
 // shards the FD Jacobian columns over the communicator (cost-balanced tiles) and shares the
 // rows of J^T between the ranks.
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <iostream>
 #include <utility>
@@ -87,10 +88,32 @@ class LMDevice {
         if (P > 1) check(comm_share_rows(ctx_, JT_.get(), ldjt_, n_), "share(J)");
     }
 
+    // Single process, device objective: the FD Jacobian and A = J^T J + lambda diag(J^T J) in
+    // one call (PNOL_FD_CHUNKS > 1 pipelines FD column chunks beside the J^T J rows they
+    // complete; at cfg 3 that measured slower than back to back, so the default is 1);
+    // bitwise the same J and A as jacobian() + the J^T J of step().
+    bool jacobianAndNormal(MultiObjective* obj, std::vector<double>& X, std::vector<double>& dX, double lambda) {
+        pnol_dobj* d = obj->deviceObjective();
+        if (!d) return false;
+        static const int chunks = [] {
+            const char* e = std::getenv("PNOL_FD_CHUNKS");
+            return e ? std::atoi(e) : 1;   // measured: chunked overlap is slower at cfg 3
+        }();
+        x_.upload(X);
+        h_.upload(dX);
+        check(pnol_fd_jtj_d(ctx_, d, x_.get(), h_.get(), F0_.get(), 1, JT_.get(), ldjt_, lambda, A_.get(), lda_,
+                            nullptr, chunks),
+              "fd_jtj");
+        obj->countEvals(n_ + 1);
+        return true;
+    }
+
     // sigma = (J^T J + lambda diag(J^T J))^{-1} (-J^T F)   (LevenbergMarquardt.cpp:59-83);
-    // LevMarqMPI splits the J^T J tiles over the ranks (bitwise the same A)
-    void step(double lambda, std::vector<double>& sigma, bool sharded) {
-        if (sharded && comm_size() > 1)
+    // LevMarqMPI splits the J^T J tiles over the ranks (bitwise the same A).  have_A: A was
+    // already formed by jacobianAndNormal.
+    void step(double lambda, std::vector<double>& sigma, bool sharded, bool have_A = false) {
+        if (have_A) {
+        } else if (sharded && comm_size() > 1)
             check(pnol_jtj_mpi_d(ctx_, JT_.get(), ldjt_, m_, n_, lambda, A_.get(), lda_, nullptr), "jtj");
         else
             check(pnol_jtj_d(ctx_, JT_.get(), ldjt_, m_, n_, lambda, A_.get(), lda_, nullptr), "jtj");
@@ -129,8 +152,9 @@ void lm_solve(MultiObjective* obj, const LMParams& P, bool sharded, std::vector<
     int iter = 0;
     double xdiff2Norm = P.xMinDiff * 2;
     while (iter < P.maxIter) {
-        dev.jacobian(obj, X, dX, sharded);
-        dev.step(lambda, sigma, sharded);
+        const bool have_A = !sharded && dev.jacobianAndNormal(obj, X, dX, lambda);
+        if (!have_A) dev.jacobian(obj, X, dX, sharded);
+        dev.step(lambda, sigma, sharded, have_A);
         Xprev = X;
         Fprev = F;
         dev.saveF();

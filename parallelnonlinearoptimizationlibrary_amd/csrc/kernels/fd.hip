@@ -446,7 +446,7 @@ int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
 // prefix checkpoints), then the FD GEMM over all tiles in launches of <= kFdMaxTiles tiles.
 int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, const int* start,
                              const int* count, int ntiles, double* F0, int compute_f0, double* JT, int jbase,
-                             int ldjt) {
+                             int ldjt, int ckpt) {
     if (!o || !x || !h || !F0 || is_scalar_kind(o->kind) || ntiles < 0 || ldjt < o->m) return PNOL_ERR_ARG;
     for (int t = 0; t < ntiles; ++t)
         if (start[t] < 0 || count[t] < 0 || count[t] > kFdTile || start[t] + count[t] > o->n || start[t] < jbase)
@@ -467,7 +467,7 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
     const int ncp = (o->n + kCkpt - 1) / kCkpt;
     PNOL_CHECK(ws_get(ctx, "linres_ckpt", sizeof(double) * (size_t)o->m * (ncp > 1 ? ncp : 1), &C));
     double* f0_out = compute_f0 ? F0 : nullptr;
-    {
+    if (ckpt) {
         ScopedTimer tm(ctx, "fd_ckpt");
         if ((o->n % 2) == 0)
             hipLaunchKernelGGL((k_linres_eval<true, true>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0,
@@ -476,7 +476,7 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
             hipLaunchKernelGGL((k_linres_eval<false, true>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0,
                                ctx->stream, o->p0, x, o->p1, o->m, o->n, f0_out, (double*)C);
     }
-    PNOL_CHECK(launch_check());
+    if (ckpt) PNOL_CHECK(launch_check());
     // PNOL_FD_KERNEL selects the FD GEMM (tuning; all variants are bitwise equal):
     // 2 = x-broadcast 128 x 128 tiles (8 x 8 per thread), 3 = 64 x 128 (4 x 8) with 16-deep K
     // stages, 4 (default) = 64 x 128 with 32-deep K stages.

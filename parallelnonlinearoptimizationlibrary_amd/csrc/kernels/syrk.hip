@@ -19,6 +19,7 @@
 #include "../pnol_comm.hpp"
 
 #include <algorithm>
+#include <vector>
 
 namespace pnol {
 namespace {
@@ -75,7 +76,9 @@ __device__ __forceinline__ void store_stage(const StageRegs<TILE>& s, double* __
     for (int q = 0; q < NV; ++q) *reinterpret_cast<double2*>(dst + 2 * q) = s.v[q];
 }
 
-// MODE 0: write split-K partial tile to part; MODE 1: C = beta*C + alpha*acc (lower tiles).
+// MODE 0: write split-K partial tile to part; MODE 1: C = beta*C + alpha*acc (lower tiles);
+// MODE 2: as MODE 0, instantiated separately for the chunked launches of launch_fd_jtj (so a
+// kernel trace tells the whole-matrix launches and the pipelined row chunks apart).
 // TILE 128: waves 2 x 2 of 64 x 64 (4 x 4 MFMA blocks each); TILE 64: 2 x 2 of 32 x 32.
 template <int MODE, int TILE>
 __global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
@@ -146,7 +149,7 @@ __global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__
     // f64 MFMA C/D layout: lane l, register r -> row (l >> 4) + 4 r, column l & 15
     const int ocol = lane & 15;
     const int orow = lane >> 4;
-    if (MODE == 0) {
+    if (MODE == 0 || MODE == 2) {
         double* out = part + (long)blk * TILE * TILE;
 #pragma unroll
         for (int mi = 0; mi < NB; ++mi)
@@ -212,8 +215,8 @@ __global__ void k_syrk_unpack(const double* __restrict__ packed, int ntiles, int
 }
 
 __global__ void k_syrk_reduce(const double* __restrict__ part, int ntiles, int split_k, int n, double lambda,
-                              double* __restrict__ A, long lda, double* __restrict__ diag_out) {
-    const int t = blockIdx.y;
+                              double* __restrict__ A, long lda, double* __restrict__ diag_out, int tile0) {
+    const int t = tile0 + blockIdx.y;   // part holds this launch's tiles from tile0 on
     int ti, tj;
     tile_of(t, ti, tj);
     const double scale = 1 + lambda;
@@ -221,7 +224,7 @@ __global__ void k_syrk_reduce(const double* __restrict__ part, int ntiles, int s
         const int r = e / kTile, c = e % kTile;
         const int i = ti * kTile + r, j = tj * kTile + c;
         if (i >= n || j >= n || j > i) continue;
-        const double* p = part + ((long)t * split_k) * kTile * kTile + e;
+        const double* p = part + ((long)(t - tile0) * split_k) * kTile * kTile + e;
         double v = 0.0;
         for (int s = 0; s < split_k; ++s) v += p[(long)s * kTile * kTile];
         if (i == j) {
@@ -300,8 +303,90 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     PNOL_CHECK(launch_check());
     ScopedTimer tm(ctx, "syrk_reduce");
     hipLaunchKernelGGL(k_syrk_reduce, dim3(8, ntiles), dim3(256), 0, ctx->stream, (const double*)part, ntiles,
-                       split_k, n, lambda, A, (long)lda, jtj_diag);
+                       split_k, n, lambda, A, (long)lda, jtj_diag, 0);
     return launch_check();
+}
+
+int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldjt, int m, int n, double lambda,
+                    double* A, int lda, double* jtj_diag, int row_begin, int row_end) {
+    const int nt = (n + kTile - 1) / kTile;
+    const int ntiles = nt * (nt + 1) / 2;
+    if (row_begin < 0 || row_end > nt || row_begin >= row_end) return PNOL_ERR_ARG;
+    const int split_k = choose_split_k(ntiles, m, ctx->num_cu);
+    int kchunk = (m + split_k - 1) / split_k;
+    kchunk = (kchunk + kTK - 1) / kTK * kTK;
+    const int t0 = row_begin * (row_begin + 1) / 2, t1 = row_end * (row_end + 1) / 2;
+    void* part = nullptr;
+    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * split_k * kTile * kTile, &part));
+    double* mypart = (double*)part + (size_t)t0 * split_k * kTile * kTile;   // disjoint per row range
+    {
+        ScopedTimer tm(ctx, "syrk_rows", stream);
+        hipLaunchKernelGGL((k_syrk_tile<2, kTile>), dim3((t1 - t0) * split_k), dim3(256), 0, stream, JT, (long)ldjt, n,
+                           m, split_k, kchunk, mypart, (double*)nullptr, 0L, 1.0, 0.0, t0);
+    }
+    PNOL_CHECK(launch_check());
+    hipLaunchKernelGGL(k_syrk_reduce, dim3(8, t1 - t0), dim3(256), 0, stream, (const double*)mypart, t1 - t0, split_k,
+                       n, lambda, A, (long)lda, jtj_diag, t0);
+    return launch_check();
+}
+
+// FD Jacobian + J^T J, pipelined over column chunks.  The FD point tiles are the 128-column
+// blocks b = 0 .. nt-1, the same as the J^T J tile rows, so once FD blocks [0, b1) are done the
+// tile rows [.., b1) are computable.  Chunk c: FD blocks [b_c, b_{c+1}) on the context stream,
+// an event, then on the aux stream the J^T J rows [b_c, b_{c+1}).  The FD GEMM is VALU-bound
+// and the J^T J MFMA-bound, so the two overlap on the CUs.  FD costs fall with the column
+// index (prefix sharing) while J^T J rows grow, so chunk boundaries are placed at equal FD cost.
+// JT and A are bitwise those of launch_fd_jacobian + launch_jtj.
+int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
+                  double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, int nchunks) {
+    if (!o || !JT || !A) return PNOL_ERR_ARG;
+    const int n = o->n, m = o->m;
+    const int nt = (n + kTile - 1) / kTile;
+    if (o->kind != PNOL_OBJ_LINRES || nchunks <= 1 || nt < 2 || (n <= PNOL_SEQ_MAX && m <= 4096)) {
+        PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
+        ScopedTimer tm(ctx, "syrk");
+        return launch_jtj(ctx, JT, ldjt, m, n, lambda, A, lda, jtj_diag);
+    }
+    nchunks = std::min(nchunks, nt);
+    if (!ctx->aux_stream) PNOL_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
+    while ((int)ctx->aux_events.size() < nchunks + 1) {
+        hipEvent_t e;
+        PNOL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->aux_events.push_back(e);
+    }
+    // chunk boundaries at equal FD cost: block b costs ~ (n - 128 b) chain steps
+    std::vector<int> bnd(1, 0);
+    {
+        double total = 0;
+        for (int b = 0; b < nt; ++b) total += n - (double)b * kTile;
+        double acc = 0;
+        for (int b = 0; b < nt && (int)bnd.size() < nchunks; ++b) {
+            acc += n - (double)b * kTile;
+            if (acc >= total * bnd.size() / nchunks && b + 1 < nt) bnd.push_back(b + 1);
+        }
+        bnd.push_back(nt);
+    }
+    // the aux stream starts after everything already queued on the context stream
+    ScopedTimer tm(ctx, "fd_jtj");
+    PNOL_HIP(hipEventRecord(ctx->aux_events[nchunks], ctx->stream));
+    PNOL_HIP(hipStreamWaitEvent(ctx->aux_stream, ctx->aux_events[nchunks], 0));
+    std::vector<int> st, ct;
+    for (size_t c = 0; c + 1 < bnd.size(); ++c) {
+        st.clear();
+        ct.clear();
+        for (int b = bnd[c]; b < bnd[c + 1]; ++b) {
+            st.push_back(b * kTile);
+            ct.push_back(std::min(kTile, n - b * kTile));
+        }
+        PNOL_CHECK(launch_fd_jacobian_tiles(ctx, o, x, h, st.data(), ct.data(), (int)st.size(), F0, compute_f0, JT, 0,
+                                            ldjt, c == 0 ? 1 : 0));
+        PNOL_HIP(hipEventRecord(ctx->aux_events[c], ctx->stream));
+        PNOL_HIP(hipStreamWaitEvent(ctx->aux_stream, ctx->aux_events[c], 0));
+        PNOL_CHECK(launch_jtj_rows(ctx, ctx->aux_stream, JT, ldjt, m, n, lambda, A, lda, jtj_diag, bnd[c], bnd[c + 1]));
+    }
+    PNOL_HIP(hipEventRecord(ctx->aux_events[nchunks], ctx->aux_stream));
+    PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->aux_events[nchunks], 0));
+    return PNOL_OK;
 }
 
 int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, double alpha, double* C, int ldc,

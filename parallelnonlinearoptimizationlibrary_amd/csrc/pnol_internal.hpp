@@ -49,6 +49,8 @@ struct pnol_ctx {
     int* chol4_flags = nullptr;     // method-4 Cholesky: per-row panel flags + backward-solve flags
     int chol4_cap = 0;              // tile rows the flag buffer holds (2 * cap ints)
     int chol4_epoch = 0;            // last flag value handed out (monotonic; flags reset on regrow)
+    hipStream_t aux_stream = nullptr;   // second stream (J^T J rows beside the FD chunks), lazily created
+    std::vector<hipEvent_t> aux_events; // chunk-done events between the two streams
 };
 
 struct pnol_dobj {
@@ -87,11 +89,12 @@ int ws_get(pnol_ctx* ctx, const char* key, size_t bytes, void** out);
 // Scoped timer: records a start event now and a stop event at scope exit (when enabled).
 class ScopedTimer {
   public:
-    ScopedTimer(pnol_ctx* ctx, const char* name);
+    ScopedTimer(pnol_ctx* ctx, const char* name, hipStream_t stream = nullptr);
     ~ScopedTimer();
   private:
     pnol_ctx* ctx_;
     const char* name_;
+    hipStream_t stream_ = nullptr;
     hipEvent_t a_ = nullptr, b_ = nullptr;
 };
 
@@ -130,9 +133,19 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
 int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
 int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt,
                        double* f0, double* g);
+// ckpt: 1 = run the base-chain pass (F0 when compute_f0, prefix checkpoints), 0 = reuse the
+// checkpoints of the previous call at the same x (chunked launches of one Jacobian)
 int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, const int* start,
                              const int* count, int ntiles, double* F0, int compute_f0, double* JT, int jbase,
-                             int ldjt);
+                             int ldjt, int ckpt = 1);
+// J^T J tiles of tile rows [row_begin, row_end) (128 x 128 tiles, split_k of the whole matrix so
+// every tile is summed exactly as by launch_jtj), partials + reduce on `stream`
+int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldjt, int m, int n, double lambda,
+                    double* A, int lda, double* jtj_diag, int row_begin, int row_end);
+// FD Jacobian of all columns + A = J^T J (+ Marquardt diagonal), pipelined: FD column chunks on
+// the context stream, the J^T J tile rows they complete on a second stream
+int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
+                  double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, int nchunks);
 int launch_fd_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int j0, int cnt,
                        double* F0, int compute_f0, double* JT, int ldjt);
 int launch_synthetic_quadratic(pnol_ctx* ctx, unsigned long long seed, int n, double bscale, double* d, double* b);

@@ -183,15 +183,17 @@ int comm_allgather_device(pnol_ctx* ctx, const double* send, double* recv, size_
 // ---------------------------------------------------------------------------------------
 // kernel timers
 // ---------------------------------------------------------------------------------------
-ScopedTimer::ScopedTimer(pnol_ctx* ctx, const char* name) : ctx_(ctx), name_(name) {
+ScopedTimer::ScopedTimer(pnol_ctx* ctx, const char* name, hipStream_t stream)
+    : ctx_(ctx), name_(name), stream_(stream) {
     if (!ctx_ || !ctx_->timers.on) return;
+    if (!stream_) stream_ = ctx_->stream;
     if (hipEventCreate(&a_) != hipSuccess || hipEventCreate(&b_) != hipSuccess) { a_ = b_ = nullptr; return; }
-    (void)hipEventRecord(a_, ctx_->stream);
+    (void)hipEventRecord(a_, stream_);
 }
 
 ScopedTimer::~ScopedTimer() {
     if (!a_) return;
-    (void)hipEventRecord(b_, ctx_->stream);
+    (void)hipEventRecord(b_, stream_);
     ctx_->timers.pending[name_].push_back({a_, b_});
 }
 
@@ -293,6 +295,11 @@ int pnol_ctx_destroy(pnol_ctx* ctx) {
     for (auto& kv : ctx->ws.bufs)
         if (kv.second.first) (void)hipFree(kv.second.first);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    if (ctx->aux_stream) {
+        (void)hipStreamSynchronize(ctx->aux_stream);
+        (void)hipStreamDestroy(ctx->aux_stream);
+    }
+    for (hipEvent_t e : ctx->aux_events) (void)hipEventDestroy(e);
     if (ctx == g_default) g_default = nullptr;
     delete ctx;
     return PNOL_OK;

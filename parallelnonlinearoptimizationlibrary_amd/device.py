@@ -187,6 +187,15 @@ class DeviceObjective:
         return F0, JT
 
 
+    def fd_jtj(self, x, h, lam, JT, A, F0=None, compute_f0=True, nchunks=4, want_diag=False):
+        """Pipelined FD Jacobian (all columns) + A = J^T J with the Marquardt diagonal."""
+        F0 = self.ctx.empty(self.m) if F0 is None else F0
+        diag = self.ctx.empty(self.n) if want_diag else None
+        L.check(L.lib().pnol_fd_jtj_d(self.ctx.h, self.h, _ptr(x), _ptr(h), _ptr(F0), int(compute_f0), _ptr(JT),
+                                      JT.stride(0), C.c_double(lam), _ptr(A), A.stride(0), _ptr(diag), nchunks),
+                "pnol_fd_jtj_d")
+        return (F0, JT, A, diag) if want_diag else (F0, JT, A)
+
     def fd_jacobian_tiles(self, x, h, tiles, JT, F0=None, compute_f0=True):
         """FD rows of the (start, count) tiles into JT (row c = column c); returns (F0, JT)."""
         F0 = self.ctx.empty(self.m) if F0 is None else F0

@@ -389,6 +389,26 @@ def test_fd_jacobian_tiles_bitwise(ctx, oracle, m, n, P):
     assert np.array_equal(full, ref)
 
 
+@pytest.mark.parametrize("m,n,chunks", [(2000, 700, 4), (1500, 1000, 3), (513, 2048, 8), (300, 129, 2), (400, 300, 1)])
+def test_fd_jtj_pipelined_bitwise(ctx, m, n, chunks):
+    """The pipelined FD Jacobian + J^T J (two streams, chunked) equals the two separate calls
+    bitwise: JT, F0, A (with the Marquardt diagonal) and diag(J^T J)."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    d = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+    x = ctx.tensor(np.linspace(-0.5, 0.5, n)); h = ctx.tensor(np.full(n, 1e-7))
+    F0a, JTa = d.fd_jacobian(x, h, 0, n)
+    Aa, da = ctx.jtj(JTa, 0.37, want_diag=True)
+    JTb, Ab = ctx.empty(n, m), ctx.empty(n, n)
+    for _ in range(2):   # repeated: events / aux stream reuse
+        F0b, JTb, Ab, db = d.fd_jtj(x, h, 0.37, JTb, Ab, nchunks=chunks, want_diag=True)
+    ctx.synchronize()
+    assert np.array_equal(_np(JTb), _np(JTa))
+    assert np.array_equal(_np(F0b), _np(F0a))
+    assert np.array_equal(_np(Ab), _np(Aa))
+    assert np.array_equal(_np(db), _np(da))
+
+
 def test_synthetic_data_matches_oracle_stream(ctx, oracle):
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
