@@ -41,6 +41,7 @@ def _args():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hg", action="store_true")
+    ap.add_argument("--no-timers", action="store_true", help="no per-kernel HIP events in the timed region")
     ap.add_argument("--m", type=int, default=M_RES)
     ap.add_argument("--n", type=int, default=N_PAR)
     return ap.parse_args()
@@ -196,7 +197,7 @@ def main():
 
     run(args.warmup)
     torch.cuda.synchronize()
-    L.check(L.lib().pnol_ctx_enable_timers(dctx, 1), "timers")
+    L.check(L.lib().pnol_ctx_enable_timers(dctx, 0 if args.no_timers else 1), "timers")
     L.check(L.lib().pnol_ctx_reset_timers(dctx), "timers")
     if world > 1:
         dist.barrier()

@@ -4,6 +4,7 @@
 // rows of J^T between the ranks.
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <cstdio>
 #include <iostream>
 #include <utility>
@@ -43,10 +44,26 @@ class LMDevice {
         F_.reset(ctx, m); Fprev_.reset(ctx, m); F0_.reset(ctx, m);
     }
 
+    // x_ / h_ hold copies of host vectors; skip the transfer when the host vector is unchanged
+    // (the FD point after an accepted step is the point just evaluated; dX never changes)
+    static bool same(const std::vector<double>& a, const std::vector<double>& b) {   // bitwise (+0 != -0)
+        return a.size() == b.size() && std::memcmp(a.data(), b.data(), sizeof(double) * a.size()) == 0;
+    }
+    void uploadX(const std::vector<double>& X) {
+        if (same(X, xh_)) return;
+        x_.upload(X);
+        xh_ = X;
+    }
+    void uploadH(const std::vector<double>& dX) {
+        if (same(dX, hh_)) return;
+        h_.upload(dX);
+        hh_ = dX;
+    }
+
     // residuals at X into host F and device F_
     void evalResiduals(MultiObjective* obj, std::vector<double>& X, std::vector<double>& F) {
         if (pnol_dobj* d = obj->deviceObjective()) {
-            x_.upload(X);
+            uploadX(X);
             check(pnol_dobj_eval_d(ctx_, d, x_.get(), F_.get()), "objective eval");
             F_.download(F);
             obj->countEvals(1);
@@ -64,8 +81,8 @@ class LMDevice {
         int cnt = 0;
         for (int c : ct) cnt += c;
         if (pnol_dobj* d = obj->deviceObjective()) {
-            x_.upload(X);
-            h_.upload(dX);
+            uploadX(X);
+            uploadH(dX);
             check(pnol_fd_jacobian_tiles_d(ctx_, d, x_.get(), h_.get(), st.data(), ct.data(), (int)st.size(),
                                            F0_.get(), 1, JT_.get(), ldjt_),
                   "fd_jacobian");
@@ -99,8 +116,8 @@ class LMDevice {
             const char* e = std::getenv("PNOL_FD_CHUNKS");
             return e ? std::atoi(e) : 1;   // measured: chunked overlap is slower at cfg 3
         }();
-        x_.upload(X);
-        h_.upload(dX);
+        uploadX(X);
+        uploadH(dX);
         check(pnol_fd_jtj_d(ctx_, d, x_.get(), h_.get(), F0_.get(), 1, JT_.get(), ldjt_, lambda, A_.get(), lda_,
                             nullptr, chunks),
               "fd_jtj");
@@ -130,6 +147,7 @@ class LMDevice {
     pnol_ctx* ctx_;
     int n_, m_, ldjt_, lda_;
     DevVec JT_, A_, rhs_, sigma_, x_, h_, F_, Fprev_, F0_;
+    std::vector<double> xh_, hh_;   // host images of x_ and h_
 };
 
 void lm_solve(MultiObjective* obj, const LMParams& P, bool sharded, std::vector<double>& X, std::vector<double>& F0,
