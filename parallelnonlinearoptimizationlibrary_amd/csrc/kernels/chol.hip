@@ -39,15 +39,14 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     return __hiloint2double(hi, lo);
 }
 
-// 1/sqrt(x) to full double precision: hardware estimate + two Newton steps (r += r (1 - x r^2) / 2)
+// 1/sqrt(x) to full double precision: the hardware estimate (~2^-24 relative,
+// tools/microbench/rsq_acc.hip) and one third-order step, r (1 + e/2 + 3 e^2 / 8) with
+// e = 1 - x r^2 (error ~e^3 ~ 2^-72): a 5-deep dependent chain instead of 6 for two Newton steps
 __device__ __forceinline__ double rsqrt_nr(double x) {
-    double r = __builtin_amdgcn_rsq(x);
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-        const double e = fma(-x, r * r, 1.0);
-        r = fma(0.5 * r, e, r);
-    }
-    return r;
+    const double r = __builtin_amdgcn_rsq(x);
+    const double e = fma(-x, r * r, 1.0);
+    const double p = fma(e, 0.375, 0.5);
+    return fma(r * e, p, r);
 }
 
 // Stage the 64 x 64 tile at (r0, c0) of P into four 64 x 16 substages (row stride kPad):
@@ -174,7 +173,7 @@ __device__ __forceinline__ bool spin_ge(const int* f, int target, int* info) {
 // broadcast l_{J+1,J} to update its diagonal entry, so the next pivot (readlane + rsqrt +
 // two Newton steps) is issued before the rest of the rank-1 update, whose LDS broadcasts
 // and FMAs then overlap that latency chain.  Column J and 1/L_JJ go to LDS (Lc, rinv); every
-// 4 steps an LDS counter tells wave 1 how many columns are final.
+// 2 steps an LDS counter tells wave 1 how many columns are final.
 constexpr int kHalf = 32;
 constexpr int kS = kHalf + 1;   // row stride of the LDS copies of the tile halves
 
@@ -202,47 +201,61 @@ __device__ __forceinline__ void wait_lds_ge(const int* cnt, int target) {
         : "vcc", "memory");
 }
 
+// Column J's broadcast as wave 0 holds it for the rank-1 update: entries k = K0 .. 31 in pairs.
+template <int J>
+struct ColBuf {
+    static constexpr int K0 = (J + 2) & ~1, NR = (kHalf - K0) / 2;
+    double2 v[NR > 0 ? NR : 1];
+};
+
 // One step of a 32-wide panel (wave 0).  On entry piv / r are the pivot of column J and its
 // reciprocal square root; on exit those of column J + 1.  Lc is column-major with stride LDC.
+// Software-pipelined one step deep: step J's region holds its own pivot chain for column J + 1
+// (readlane, rsqrt) beside the tail of step J-1's rank-1 update (k >= J + 2, with the previous
+// column lp / cp still in registers), and only the entry k = J + 2 of its own update, which
+// the next pivot needs.  Each entry still receives its updates in column order.
 template <int J, int LDC, bool STAMP = false>
-__device__ __forceinline__ void panel_step(double (&a)[kHalf], double& piv, double& r, double* __restrict__ Lc,
+__device__ __forceinline__ void panel_step(double (&a)[kHalf], double& piv, double& r, double lp,
+                                           const ColBuf<J - 1>& cp, double* __restrict__ Lc,
                                            double* __restrict__ rinv, int* cnt, int cbase, int t, bool& bad,
                                            long long* st = nullptr) {
     if constexpr (STAMP && (J & 7) == 0) st[J >> 3] = __builtin_amdgcn_s_memtime();   // microbenchmark only
-    const double l = (t == J) ? piv * r : (t > J ? a[J] * r : 0.0);
+    // lane J: a[J] * r = piv / sqrt(piv), the diagonal; lanes t < J scale upper-triangle
+    // entries nobody reads (column J above the diagonal is never consumed)
+    const double l = a[J] * r, rJ = r;
     a[J] = l;
-    double pnext = 0.0;
     if constexpr (J + 1 < kHalf) {
-        // pivot path of column J + 1 first: it needs only the broadcast of l_{J+1,J}
+        // the critical chain: only l_{J+1,J} (a readlane) feeds the next pivot
         const double l1 = readlane_d(l, J + 1);
         a[J + 1] = fma(-l, l1, a[J + 1]);
-        pnext = readlane_d(a[J + 1], J + 1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    Lc[J * LDC + t] = l;
-    rinv[cbase + J] = r;   // every lane stores the same value: no divergent branch in the chain
-    if constexpr ((J & 3) == 3) lds_signal(cnt, cbase + J + 1);
-    if constexpr (J + 1 < kHalf) {
-        // the whole broadcast of column J is requested at once (one LDS latency), the next
-        // pivot's rsqrt chain runs under it, then the rank-1 update
-        constexpr int K0 = (J + 2) & ~1, NR = (kHalf - K0) / 2;
-        double2 cv[NR > 0 ? NR : 1];
-#pragma unroll
-        for (int q = 0; q < NR; ++q) cv[q] = *reinterpret_cast<const double2*>(Lc + J * LDC + K0 + 2 * q);
-        piv = pnext;
+        piv = readlane_d(a[J + 1], J + 1);
         bad |= !(piv > 0.0);
         r = rsqrt_nr(piv);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < NR; ++q) {
-            const int k = K0 + 2 * q;
-            if (k >= J + 2) a[k] = fma(-l, cv[q].x, a[k]);
-            a[k + 1] = fma(-l, cv[q].y, a[k + 1]);
-        }
-        asm volatile("" ::: "memory");   // keep the next steps' LDS reads from being hoisted here
-        __builtin_amdgcn_sched_barrier(0);
-        panel_step<J + 1, LDC, STAMP>(a, piv, r, Lc, rinv, cnt, cbase, t, bad, st);
     }
+    // beside it: the tail of step J-1's update (k >= J + 2) ...
+    if constexpr (J >= 1) {
+#pragma unroll
+        for (int q = 0; q < ColBuf<J - 1>::NR; ++q) {
+            const int k = ColBuf<J - 1>::K0 + 2 * q;
+            if (k >= J + 2) a[k] = fma(-lp, cp.v[q].x, a[k]);
+            if (k + 1 >= J + 2) a[k + 1] = fma(-lp, cp.v[q].y, a[k + 1]);
+        }
+    }
+    // ... and the one entry of step J's update the next step's chain needs (l_{J+2,J} by readlane)
+    if constexpr (J + 2 < kHalf) a[J + 2] = fma(-l, readlane_d(l, J + 2), a[J + 2]);
+    // column J to LDS (wave 1 and the rest of step J's update, applied in step J+1's region)
+    Lc[J * LDC + t] = l;
+    rinv[cbase + J] = rJ;   // every lane stores the same value: no divergent branch in the chain
+    if constexpr ((J & 1) == 1) lds_signal(cnt, cbase + J + 1);
+    ColBuf<J> cv;
+    if constexpr (J + 1 < kHalf) {
+#pragma unroll
+        for (int q = 0; q < ColBuf<J>::NR; ++q)
+            cv.v[q] = *reinterpret_cast<const double2*>(Lc + J * LDC + ColBuf<J>::K0 + 2 * q);
+    }
+    asm volatile("" ::: "memory");   // keep the next steps' LDS reads from being hoisted here
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (J + 1 < kHalf) panel_step<J + 1, LDC, STAMP>(a, piv, r, l, cv, Lc, rinv, cnt, cbase, t, bad, st);
 }
 
 // One step of the inverse of a 32 x 32 lower factor (wave 1, lane c = column c of W):
@@ -250,19 +263,35 @@ __device__ __forceinline__ void panel_step(double (&a)[kHalf], double& piv, doub
 template <int J, int LDC>
 __device__ __forceinline__ void inv_step(double (&y)[kHalf], const double* __restrict__ Lc,
                                          const double* __restrict__ rinv, const int* cnt, int cbase) {
-    if constexpr ((J & 3) == 0) wait_lds_ge(cnt, cbase + J + 4);
-    const double w = y[J] * rinv[cbase + J];
-    y[J] = w;
-    constexpr int K0 = (J + 1) & ~1;
+    // two columns per region (the signal granularity): both broadcasts and both reciprocals
+    // are requested at once, then the two substitution steps
+    static_assert((J & 1) == 0, "two steps per call");
+    wait_lds_ge(cnt, cbase + J + 2);
+    constexpr int K0 = (J + 1) & ~1, NR = (kHalf - K0) / 2;   // column J: entries from K0 (= J)
+    double2 c0[NR > 0 ? NR : 1], c1[NR > 0 ? NR : 1];
 #pragma unroll
-    for (int k = K0; k < kHalf; k += 2) {
-        const double2 c = *reinterpret_cast<const double2*>(Lc + J * LDC + k);
-        if (k >= J + 1) y[k] = fma(-c.x, w, y[k]);
-        y[k + 1] = fma(-c.y, w, y[k + 1]);
+    for (int q = 0; q < NR; ++q) {
+        c0[q] = *reinterpret_cast<const double2*>(Lc + J * LDC + K0 + 2 * q);
+        c1[q] = *reinterpret_cast<const double2*>(Lc + (J + 1) * LDC + K0 + 2 * q);
+    }
+    const double r0 = rinv[cbase + J], r1 = rinv[cbase + J + 1];
+    __builtin_amdgcn_sched_barrier(0);
+    const double w0 = y[J] * r0;
+    y[J] = w0;
+    y[J + 1] = fma(-c0[0].y, w0, y[J + 1]);   // K0 == J: c0[0] = (L_JJ, L_J+1,J)
+    const double w1 = y[J + 1] * r1;
+    y[J + 1] = w1;
+#pragma unroll
+    for (int q = 1; q < NR; ++q) {
+        const int k = K0 + 2 * q;
+        y[k] = fma(-c0[q].x, w0, y[k]);
+        y[k + 1] = fma(-c0[q].y, w0, y[k + 1]);
+        y[k] = fma(-c1[q].x, w1, y[k]);
+        y[k + 1] = fma(-c1[q].y, w1, y[k + 1]);
     }
     asm volatile("" ::: "memory");   // keep the next steps' LDS reads from being hoisted here
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (J + 1 < kHalf) inv_step<J + 1, LDC>(y, Lc, rinv, cnt, cbase);
+    if constexpr (J + 2 < kHalf) inv_step<J + 2, LDC>(y, Lc, rinv, cnt, cbase);
 }
 
 // Wave 1's part of a panel: W = L^{-1} of the 32 x 32 factor whose columns appear in Lc, stored
@@ -276,16 +305,27 @@ __device__ __forceinline__ void panel_inverse(const double* __restrict__ Lc, con
     for (int k = 0; k < kHalf; ++k) y[k] = (k == lane) ? 1.0 : 0.0;
     inv_step<0, LDC>(y, Lc, rinv, cnt, cbase);
 #pragma unroll
-    for (int k = 0; k < kHalf; ++k) Wl[lane < kHalf ? k * kHalf + lane : kHalf * kHalf + (lane - kHalf)] = y[k];
+    for (int k = 0; k < kHalf; ++k) Wl[lane < kHalf ? k * kS + lane : kHalf * kS + (lane - kHalf)] = y[k];
 }
 
 // 16 x 16 block of C = sum_k A(i, k) B(j, k) over K (v_mfma_f64_16x16x4_f64), accumulated into acc.
 template <int K, class FA, class FB>
 __device__ __forceinline__ d4 mfma_blk(d4 acc, FA fa, FB fb, int lane) {
     const int i = lane & 15, kq = lane >> 4;
+    double a[K / 4], b[K / 4];   // all fragments requested first: one LDS latency, not K / 4
 #pragma unroll
-    for (int kk = 0; kk < K; kk += 4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fa(i, kk + kq), fb(i, kk + kq), acc, 0, 0, 0);
-    return acc;
+    for (int q = 0; q < K / 4; ++q) {
+        a[q] = fa(i, 4 * q + kq);
+        b[q] = fb(i, 4 * q + kq);
+    }
+    // two independent accumulator chains (even / odd K steps) halve the dependent MFMA latency
+    d4 acc2 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < K / 4; q += 2) {
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], b[q], acc, 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q + 1], b[q + 1], acc2, 0, 0, 0);
+    }
+    return acc + acc2;
 }
 
 struct DiagLds {
@@ -293,8 +333,8 @@ struct DiagLds {
     double* S22;   // 32 x 32 bottom-right quarter, stride kS
     double* Lc1;   // P1 columns, column-major, stride 64
     double* Lc2;   // P3 columns, column-major, stride 64 (lanes >= 32 fill rows 32..63 with zeros)
-    double* W11;   // 32 x 32 row-major, then 32 doubles of discard space
-    double* W22;   // 32 x 32 row-major + 32 discard (in the Sl space)
+    double* W11;   // 32 x 32 row-major, row stride kS (conflict-free fragment reads), + 32 discard
+    double* W22;   // the same (in the Sl space)
     double* Tl;    // 32 x 32 row-major (in the Sl space)
 };
 
@@ -322,61 +362,76 @@ template <bool STAMP = false>
 __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict__ rinv, int* cnt,
                                             double* __restrict__ Wd, int d, int* info, long long* st = nullptr) {
     const int t = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
-    // P1
+    // The phases are chained by LDS words instead of workgroup barriers, so the inverse wave
+    // finishing W11 overlaps the S22 update:  cnt[0] = final panel columns, cnt[1] = W11 done,
+    // cnt[2] / cnt[3] = S22 quadrants (1,0) / (1,1) done.  All are zero on entry.
+    int* flags = cnt + 1;
+    const double* L21 = L.Lc1 + kHalf;
     if (wave == 0) {
-        double a[kHalf];
+        {   // P1
+            double a[kHalf];
 #pragma unroll
-        for (int k = 0; k < kHalf; ++k) a[k] = L.Sl[lane * kS + k];
-        double piv = readlane_d(a[0], 0);
-        bool bad = !(piv > 0.0);
-        double r = rsqrt_nr(piv);
-        panel_step<0, 64, STAMP>(a, piv, r, L.Lc1, rinv, cnt, 0, lane, bad, st);
-        if constexpr (STAMP) st[4] = __builtin_amdgcn_s_memtime();
-        if (bad && lane == 0) atomicCAS(info, 0, d * NB + 1);
+            for (int k = 0; k < kHalf; ++k) a[k] = L.Sl[lane * kS + k];
+            double piv = readlane_d(a[0], 0);
+            bool bad = !(piv > 0.0);
+            double r = rsqrt_nr(piv);
+            const ColBuf<-1> none{};
+            panel_step<0, 64, STAMP>(a, piv, r, 0.0, none, L.Lc1, rinv, cnt, 0, lane, bad, st);
+            if constexpr (STAMP) st[4] = __builtin_amdgcn_s_memtime();
+            if (bad && lane == 0) atomicCAS(info, 0, d * NB + 1);
+        }
+        {   // P2, quadrant (0,0): S22 -= L21 L21^T
+            d4 acc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = L.S22[((lane >> 4) + 4 * r) * kS + (lane & 15)];
+            acc = mfma_blk<kHalf>(acc, [&](int i, int k) { return -L21[k * 64 + i]; },
+                                  [&](int j, int k) { return L21[k * 64 + j]; }, lane);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) L.S22[((lane >> 4) + 4 * r) * kS + (lane & 15)] = acc[r];
+        }
+        if constexpr (STAMP) st[6] = __builtin_amdgcn_s_memtime();
+        wait_lds_ge(flags + 1, 1);
+        wait_lds_ge(flags + 2, 1);
+        {   // P3
+            double a[kHalf];
+#pragma unroll
+            for (int k = 0; k < kHalf; ++k) a[k] = lane < kHalf ? L.S22[lane * kS + k] : 0.0;
+            double piv = readlane_d(a[0], 0);
+            bool bad = !(piv > 0.0);
+            double r = rsqrt_nr(piv);
+            if constexpr (STAMP) st[8] = __builtin_amdgcn_s_memtime();
+            const ColBuf<-1> none{};
+            panel_step<0, 64, STAMP>(a, piv, r, 0.0, none, L.Lc2, rinv, cnt, kHalf, lane, bad, st + 9);
+            if constexpr (STAMP) st[13] = __builtin_amdgcn_s_memtime();
+            if (bad && lane == 0) atomicCAS(info, 0, d * NB + kHalf + 1);
+        }
     } else if (wave == 1) {
         panel_inverse<64>(L.Lc1, rinv, cnt, 0, L.W11, lane);
+        lds_signal(flags, 1);
         if constexpr (STAMP) st[5] = __builtin_amdgcn_s_memtime();
-    }
-    __syncthreads();
-    if constexpr (STAMP) if (wave == 0) st[6] = __builtin_amdgcn_s_memtime();
-    // P2: S22 -= L21 L21^T (quadrants (0,0), (1,0), (1,1) on waves 0, 2, 3)
-    if (wave != 1) {
-        const int qi = wave == 0 ? 0 : 1, qj = wave == 3 ? 1 : 0;
+        panel_inverse<64>(L.Lc2, rinv, cnt, kHalf, L.W22, lane);
+        if constexpr (STAMP) st[14] = __builtin_amdgcn_s_memtime();
+    } else {
+        const int qi = 1, qj = wave - 2;   // P2 quadrants (1,0) and (1,1)
+        wait_lds_ge(cnt, kHalf);
         d4 acc;
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[r] = L.S22[(qi * 16 + (lane >> 4) + 4 * r) * kS + qj * 16 + (lane & 15)];
-        const double* L21 = L.Lc1 + kHalf;
         acc = mfma_blk<kHalf>(acc, [&](int i, int k) { return -L21[k * 64 + qi * 16 + i]; },
                               [&](int j, int k) { return L21[k * 64 + qj * 16 + j]; }, lane);
 #pragma unroll
         for (int r = 0; r < 4; ++r) L.S22[(qi * 16 + (lane >> 4) + 4 * r) * kS + qj * 16 + (lane & 15)] = acc[r];
-    }
-    __syncthreads();
-    // P3 (+ T = L21 W11 on waves 2, 3)
-    if (wave == 0) {
-        double a[kHalf];
+        lds_signal(flags + wave - 1, 1);
+        // T = L21 W11, rows 16 (wave - 2) .. +16, once W11 is in LDS
+        wait_lds_ge(flags, 1);
+        const int ti = wave - 2;
 #pragma unroll
-        for (int k = 0; k < kHalf; ++k) a[k] = lane < kHalf ? L.S22[lane * kS + k] : 0.0;
-        double piv = readlane_d(a[0], 0);
-        bool bad = !(piv > 0.0);
-        double r = rsqrt_nr(piv);
-        if constexpr (STAMP) st[8] = __builtin_amdgcn_s_memtime();
-        panel_step<0, 64, STAMP>(a, piv, r, L.Lc2, rinv, cnt, kHalf, lane, bad, st + 9);
-        if constexpr (STAMP) st[13] = __builtin_amdgcn_s_memtime();
-        if (bad && lane == 0) atomicCAS(info, 0, d * NB + kHalf + 1);
-    } else if (wave == 1) {
-        panel_inverse<64>(L.Lc2, rinv, cnt, kHalf, L.W22, lane);
-        if constexpr (STAMP) st[14] = __builtin_amdgcn_s_memtime();
-    } else {
-        const int qi = wave - 2;
-        const double* L21 = L.Lc1 + kHalf;
+        for (int tj = 0; tj < 2; ++tj) {
+            d4 tacc = {0.0, 0.0, 0.0, 0.0};
+            tacc = mfma_blk<kHalf>(tacc, [&](int i, int k) { return L21[k * 64 + ti * 16 + i]; },
+                                   [&](int j, int k) { return L.W11[k * kS + tj * 16 + j]; }, lane);
 #pragma unroll
-        for (int qj = 0; qj < 2; ++qj) {
-            d4 acc = {0.0, 0.0, 0.0, 0.0};
-            acc = mfma_blk<kHalf>(acc, [&](int i, int k) { return L21[k * 64 + qi * 16 + i]; },
-                                  [&](int j, int k) { return L.W11[k * kHalf + qj * 16 + j]; }, lane);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) L.Tl[(qi * 16 + (lane >> 4) + 4 * r) * kHalf + qj * 16 + (lane & 15)] = acc[r];
+            for (int r = 0; r < 4; ++r) L.Tl[(ti * 16 + (lane >> 4) + 4 * r) * kHalf + tj * 16 + (lane & 15)] = tacc[r];
         }
     }
     __syncthreads();
@@ -385,7 +440,7 @@ __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict
     {
         const int qi = wave >> 1, qj = wave & 1;
         d4 acc = {0.0, 0.0, 0.0, 0.0};
-        acc = mfma_blk<kHalf>(acc, [&](int i, int k) { return -L.W22[(qi * 16 + i) * kHalf + k]; },
+        acc = mfma_blk<kHalf>(acc, [&](int i, int k) { return -L.W22[(qi * 16 + i) * kS + k]; },
                               [&](int j, int k) { return L.Tl[k * kHalf + qj * 16 + j]; }, lane);
 #pragma unroll
         for (int r = 0; r < 4; ++r) Wd[(kHalf + qi * 16 + (lane >> 4) + 4 * r) * NB + qj * 16 + (lane & 15)] = acc[r];
@@ -397,9 +452,9 @@ __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int r = r0 + 8 * q;
-            Wd[r * NB + c] = L.W11[r * kHalf + c];
+            Wd[r * NB + c] = L.W11[r * kS + c];
             Wd[r * NB + kHalf + c] = 0.0;
-            Wd[(kHalf + r) * NB + kHalf + c] = L.W22[r * kHalf + c];
+            Wd[(kHalf + r) * NB + kHalf + c] = L.W22[r * kS + c];
         }
     }
 }
@@ -415,7 +470,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
     __shared__ __attribute__((aligned(16))) double smem[2 * kStage];   // 73.7 KB
     __shared__ double rinv[NB];
     __shared__ double zsh[NB];
-    __shared__ int cnt;
+    __shared__ int cnt[4];   // diagonal-tile phase words (factor_diag)
     __shared__ int ok_sh;
     const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), wr = wave >> 1, wc = wave & 1;
     if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
@@ -427,7 +482,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
     if (b == 0) {   // ---------------- diagonal tile d = k + 1
         const int d = k + 1, d0 = d * NB;
         const DiagLds L = diag_lds(smem);
-        if (t == 0) cnt = 0;
+        if (t < 4) cnt[t] = 0;
         if (k >= 0) {
             const int k0 = k * NB;
             stage_tile(X, P, ldp, d0, k0);
@@ -456,7 +511,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
             for (int q = 0; q < 16; ++q) diag_put(L, row, c0 + q, P[(long)row * ldp + c0 + q]);
         }
         __syncthreads();
-        factor_diag(L, rinv, &cnt, W + (long)d * NB * NB, d, info);
+        factor_diag(L, rinv, cnt, W + (long)d * NB * NB, d, info);
         return;
     }
 

@@ -16,15 +16,15 @@ __global__ __launch_bounds__(256, 2) void k_diag_time(const double* A, double* W
     using namespace pnol;
     __shared__ __attribute__((aligned(16))) double smem[2 * kStage];
     __shared__ double rinv[NB];
-    __shared__ int cnt;
+    __shared__ int cnt[4];
     const int t = threadIdx.x;
     const DiagLds L = diag_lds(smem);
-    if (t == 0) cnt = 0;
+    if (t < 4) cnt[t] = 0;
     const int row = t >> 2, c0 = (t & 3) * 16;
     for (int q = 0; q < 16; ++q) diag_put(L, row, c0 + q, A[row * 64 + c0 + q]);
     __syncthreads();
     if (t == 0) st[31] = __builtin_amdgcn_s_memtime();
-    factor_diag<true>(L, rinv, &cnt, W, 0, info, st);
+    factor_diag<true>(L, rinv, cnt, W, 0, info, st);
 }
 
 int main() {
@@ -64,7 +64,7 @@ int main() {
         }
     const long long b = st[31];
     printf("{\"info\": %d, \"max|W A W^T - I|\": %.3e, \"cycles\": {", info, err);
-    const char* names[] = {"p1_j0", "p1_j8", "p1_j16", "p1_j24", "p1_end", "w11_end", "b1", "-", "p3_start",
+    const char* names[] = {"p1_j0", "p1_j8", "p1_j16", "p1_j24", "p1_end", "w11_end", "p2_q00_end", "-", "p3_start",
                            "p3_j0", "p3_j8", "p3_j16", "p3_j24", "p3_end", "w22_end", "b3", "p4_end"};
     for (int i = 0; i < 17; ++i)
         if (i != 7) printf("%s\"%s\": %lld", i ? ", " : "", names[i], st[i] ? st[i] - b : -1LL);
