@@ -89,6 +89,10 @@ int pnol_bfgs_pass_d(pnol_ctx* ctx, double* D, int ldd, int n,
                      const double* y, const double* g, double* u, double* w, double* v);
 /* D = I (BFGS_with_linesearch.cpp:46-56), or diag(scale) when scale != NULL (BFGS_bnd_linesearch.cpp:65-83) */
 int pnol_set_identity_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale);
+/* Dsub[a][b] = D[idx[a]][idx[b]] for a, b < nsub (idx: device ints, ascending, < n): the
+ * free-free block of D handed to the reduced problem, BFGS_with_bnd_linsearch_MPI.cpp:822-843 */
+int pnol_gather_submatrix_d(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub,
+                            double* Dsub, int lds);
 
 /* ---- Levenberg-Marquardt -------------------------------------------------------------- */
 /* A = JT JT^T (= J^T J) with A_ii = (1 + lambda) * (J^T J)_ii  (Marquardt scaling).
@@ -183,7 +187,8 @@ int pnol_comm_share_fd_rows_d(pnol_ctx* ctx, double* buf, int ld, int ncols);
 /* ---- whole-solver drivers: the C++ drop-in classes run on built-in objectives --------- */
 /* params arrays follow the classes' setParams order (see the headers in include/). */
 typedef struct { int iters; long evals; double f0; double fopt; } pnol_result;
-/* which: 0 = BFGS (12 params), 1 = BFGS_MPI (12 params), 2 = BFGS_Bnd (15 params) */
+/* which: 0 = BFGS (12 params), 1 = BFGS_MPI (12 params), 2 = BFGS_Bnd (15 params),
+ * 3 = BFGSBnd_MPI (14 params [+ pool size, update mode]) */
 int pnol_run_bfgs(int which, pnol_dobj* obj, int host_eval, const double* params, int nparams,
                   double* X, int n, const double* Xlb, const double* Xub, pnol_result* res);
 /* which: 0 = LevMarq, 1 = LevMarqMPI (6 params). F0/FOpt host arrays of m. */

@@ -59,6 +59,14 @@ class BFGSBndParams(C.Structure):  # BFGS_Bnd::setParams, BFGS_bnd_linesearch.hp
                 ("initHessFD", C.c_int), ("verbose", C.c_int)]
 
 
+class BFGSBndMPIParams(C.Structure):  # BFGSBnd_MPI::setParams, BFGS_with_bnd_linesearch_MPI.hpp:79
+    _fields_ = [("c1", C.c_double), ("c2", C.c_double), ("alphaMin", C.c_double), ("maxAlphaMult", C.c_double),
+                ("alphaGuess", C.c_double), ("maxIterLineSearch", C.c_int), ("dXGrad", C.c_double),
+                ("dXHess", C.c_double), ("maxIter", C.c_double), ("xMinDiff", C.c_double),
+                ("minGrad2Norm", C.c_double), ("FStepTolerance", C.c_double), ("initHessFD", C.c_int),
+                ("verbose", C.c_int)]
+
+
 _lib = None
 
 
@@ -290,6 +298,25 @@ def bfgs_bnd_findmin(o: Obj, x0, lb, ub, params):  # BFGS_Bnd::findMinBnd
     res = Result()
     lib().orc_bfgs_bnd_findmin(o.ref(), C.byref(prm), ptr(X), ptr(lb), ptr(ub), len(X), C.byref(res))
     return X, res
+
+
+def bfgs_bnd_mpi_findmin(o: Obj, x0, lb, ub, params, npool, nprocs=None):  # BFGSBnd_MPI::findMinBnd
+    """Returns (X, res, status); status -1 = a NaN/inf pool value (the reference's exit(0))."""
+    X = np.array(x0, dtype=np.float64)
+    lb = np.ascontiguousarray(lb, dtype=np.float64); ub = np.ascontiguousarray(ub, dtype=np.float64)
+    prm = BFGSBndMPIParams(*params)
+    res = Result()
+    st = lib().orc_bfgs_bnd_mpi_findmin(o.ref(), C.byref(prm), npool, nprocs or npool, ptr(X), ptr(lb), ptr(ub),
+                                        len(X), C.byref(res))
+    return X, res, st
+
+
+def check_alpha_pool_bnd(pool, x, lb, ub, p):  # checkAlphaPoolBnd, BFGS_with_bnd_linsearch_MPI.cpp:711-743
+    ap = np.array(pool, dtype=np.float64)
+    arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (x, lb, ub, p)]
+    bnd = C.c_int()
+    lib().orc_check_alpha_pool_bnd(C.byref(bnd), ptr(ap), len(ap), *[ptr(a) for a in arrs], len(arrs[0]))
+    return bool(bnd.value), ap
 
 
 def compute_alpha_bnd(x, lb, ub, p):  # computeAlphaBnd, BFGS_with_bnd_linsearch_MPI.cpp:665-708

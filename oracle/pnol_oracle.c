@@ -1023,6 +1023,263 @@ int orc_bfgs_bnd_findmin(orc_objective* o, const orc_bfgs_bnd_params* prm, doubl
 }
 
 /* ------------------------------------------------------------------------------------ */
+/* Bounded BFGS with a pooled secant line search, BFGS_with_bnd_linsearch_MPI.cpp         */
+/* ------------------------------------------------------------------------------------ */
+
+typedef struct {
+    orc_objective* o; const orc_bfgs_bnd_mpi_params* prm; int nfull; int npool; int nprocs; int failed;
+} bndmpi_ctx;
+
+/* checkAlphaPoolBnd, :711-743 */
+void orc_check_alpha_pool_bnd(int* bndIndicator, double* ap, int Np, const double* X, const double* Xlb,
+                              const double* Xub, const double* p, int n) {
+    *bndIndicator = 0;
+    double alphaBnd = orc_compute_alpha_bnd(X, Xlb, Xub, p, n);
+    for (int i = 0; i < Np; ++i)
+        if (ap[i] > alphaBnd) *bndIndicator = 1;
+    if (*bndIndicator) {
+        double deltaAlpha = alphaBnd / (Np);
+        for (int i = 0; i < Np; ++i) ap[i] = deltaAlpha * (i + 1);
+    }
+    for (int i = 0; i < Np; ++i)
+        if (ap[i] < 0) ap[i] = 0;
+}
+
+/* BFGSBnd_MPI::evalAlphaPoolMPI / lineSearchObj, :246-354 (rank-ordered, zero-padded sum;
+ * a NaN / inf value ends the solve, where the reference calls exit(0)) */
+static void bndmpi_eval_pool(bndmpi_ctx* c, const double* ap, double* pp, int N, const double* X,
+                             const double* p, int n, const double* cX, const unsigned char* cI) {
+    double* w = (double*)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    for (int rank = 0; rank < c->nprocs; ++rank)
+        for (int i = rank; i < N; i += c->nprocs) {
+            for (int k = 0; k < n; ++k) w[k] = X[k] + ap[i] * p[k];
+            pp[i] = 0.0 + orc_obj_eval_recur(c->o, w, cX, cI, c->nfull);
+            if (pp[i] != pp[i] || isinf(pp[i])) c->failed = 1;
+        }
+    free(w);
+}
+
+/* BFGSBnd_MPI::secantLineSearchBnd, :358-660 */
+static void bndmpi_line_search(bndmpi_ctx* c, const double* X, const double* Xlb, const double* Xub, double FX,
+                               const double* g, const double* p, int n, const double* cX,
+                               const unsigned char* cI, double* alphaOpt, double* Fopt) {
+    const orc_bfgs_bnd_mpi_params* P = c->prm;
+    int Np = c->npool;
+    double* ap = (double*)calloc((size_t)Np, sizeof(double));
+    double* pp = (double*)calloc((size_t)Np, sizeof(double));
+    double* apPrev = (double*)malloc(sizeof(double) * (size_t)Np);
+    double* ppPrev = (double*)calloc((size_t)Np, sizeof(double));
+    double* slope = (double*)calloc((size_t)Np, sizeof(double));
+    double* ap2 = (double*)calloc((size_t)Np + 2, sizeof(double));
+    double* pp2 = (double*)calloc((size_t)Np + 2, sizeof(double));
+    for (int i = 0; i < Np; ++i) apPrev[i] = -1;
+    *alphaOpt = 0; *Fopt = FX;
+    double a0 = 0, phi0 = FX, dphi0 = orc_util_dot(g, p, n);
+    int bnd = 0;
+    int idxMin = -(int)ceil((Np - 1.0) / 2.0);
+    int idxMax = (int)floor((Np - 1.0) / 2.0);
+    double r = pow(P->maxAlphaMult, 1.0 / (double)idxMax);
+    int idx = idxMin;
+    for (int k = 0; k < Np; ++k) { ap[k] = P->alphaGuess * pow(r, idx); idx++; }
+    int first = 1, zoom = 0;
+    for (int it = 0; it < P->maxIterLineSearch && first && !c->failed; ++it) {
+        orc_check_alpha_pool_bnd(&bnd, ap, Np, X, Xlb, Xub, p, n);
+        bndmpi_eval_pool(c, ap, pp, Np, X, p, n, cX, cI);
+        for (int i = 0; i < Np; ++i)
+            if (pp[i] > phi0 + P->c1 * ap[i] * dphi0) { zoom = 1; first = 0; }
+        slope[0] = (pp[0] - phi0) / (ap[0] - a0);
+        for (int i = 1; i < Np; ++i) slope[i] = (pp[i] - pp[i - 1]) / (ap[i] - ap[i - 1]);
+        if (first)
+            for (int i = 0; i < Np; ++i)
+                if (fabs(slope[i]) <= fabs(P->c2 * dphi0)) { zoom = 0; first = 0; }
+        if (first)
+            for (int i = 0; i < Np; ++i)
+                if (slope[i] >= 0) { zoom = 1; first = 0; }
+        if (first && !bnd) {
+            double amax; int imax;
+            vector_max(ap, Np, &amax, &imax);
+            r = pow(P->maxAlphaMult, 1.0 / (double)Np);
+            for (int i = 0; i < Np; ++i) {
+                apPrev[i] = ap[i]; ppPrev[i] = pp[i];
+                double power = i + 1;
+                ap[i] = amax * pow(r, power);
+            }
+        } else if (bnd) {
+            first = 0;
+        }
+    }
+    double alo, ahi, plo, phi;
+    if (apPrev[0] < 0) {
+        find_pool_bounds(ap, pp, Np, a0, phi0, &alo, &ahi, &plo, &phi);
+    } else {
+        double* ae = (double*)malloc(sizeof(double) * 2 * (size_t)Np);
+        double* pe = (double*)malloc(sizeof(double) * 2 * (size_t)Np);
+        for (int i = 0; i < Np; ++i) { ae[i] = apPrev[i]; ae[i + Np] = ap[i]; pe[i] = ppPrev[i]; pe[i + Np] = pp[i]; }
+        find_pool_bounds(ae, pe, 2 * Np, a0, phi0, &alo, &ahi, &plo, &phi);
+        free(ae); free(pe);
+    }
+    for (int it = 0; it < P->maxIterLineSearch && zoom && !c->failed; ++it) {
+        orc_util_linspace(alo, ahi, Np + 2, ap2);
+        pp2[0] = plo; pp2[Np + 1] = phi; ap2[0] = alo; ap2[Np + 1] = ahi;
+        for (int i = 0; i < Np; ++i) { ap[i] = ap2[i + 1]; pp[i] = pp2[i + 1]; }
+        bndmpi_eval_pool(c, ap, pp, Np, X, p, n, cX, cI);
+        for (int i = 0; i < Np; ++i) { ap2[i + 1] = ap[i]; pp2[i + 1] = pp[i]; }
+        for (int i = 0; i < Np; ++i) slope[i] = (pp2[i + 1] - pp2[i]) / (ap2[i + 1] - ap2[i]);
+        for (int i = 0; i < Np; ++i)
+            if (fabs(slope[i]) <= fabs(P->c2 * dphi0)) zoom = 0;
+        if (zoom) find_pool_bounds(ap2, pp2, Np + 2, a0, phi0, &alo, &ahi, &plo, &phi);
+        double a2max; int i2max;
+        vector_max(ap2, Np + 2, &a2max, &i2max);
+        if (a2max < P->alphaMin) zoom = 0;
+    }
+    /* minimum of the last evaluated pool, :651-655 */
+    double pmin; int imin;
+    vector_min(pp, Np, &pmin, &imin);
+    *alphaOpt = ap[imin];
+    *Fopt = pmin;
+    free(ap); free(pp); free(apPrev); free(ppPrev); free(slope); free(ap2); free(pp2);
+}
+
+static void bndmpi_main_loop(bndmpi_ctx* c, double* F, double* X, double* g, double* D, double* Xlb, double* Xub,
+                             double* dX, int n, double* cX, unsigned char* cI, int* optimFlag, int* recurFlag);
+
+/* BFGSBnd_MPI::boundaryAssessment, :748-934 (top level only: n == nfull) */
+static void bndmpi_assess(bndmpi_ctx* c, double* F, double* X, const double* p, double* g, double* D,
+                          double* Xlb, double* Xub, double* dX, double* cX, unsigned char* cI, int* optimFlag,
+                          int* recurFlag) {
+    const orc_bfgs_bnd_mpi_params* P = c->prm;
+    int Ndim = c->nfull, bndFlag = 0, iR = 0;
+    for (int i = 0; i < Ndim; ++i) {
+        if (!cI[i]) {
+            if ((fabs(X[iR] - Xlb[iR]) < P->dXGrad) && (p[iR] < 0)) { bndFlag = 1; cI[i] = 1; cX[i] = X[iR]; }
+            else if (fabs(X[iR] - Xub[iR]) < P->dXGrad && (p[iR] > 0)) { bndFlag = 1; cI[i] = 1; cX[i] = X[iR]; }
+            iR++;
+        }
+    }
+    int Nconst = 0;
+    for (int i = 0; i < Ndim; ++i) Nconst += cI[i];
+    int nr = Ndim - Nconst;
+    if (!(bndFlag && nr > 0)) return;
+    double FR = *F;
+    double* XR = (double*)malloc(sizeof(double) * (size_t)nr);
+    double* gR = (double*)malloc(sizeof(double) * (size_t)nr);
+    double* lbR = (double*)malloc(sizeof(double) * (size_t)nr);
+    double* ubR = (double*)malloc(sizeof(double) * (size_t)nr);
+    double* dXR = (double*)malloc(sizeof(double) * (size_t)nr);
+    double* DR = (double*)malloc(sizeof(double) * (size_t)nr * nr);
+    int ir = 0;
+    for (int i = 0; i < Ndim; ++i) {
+        if (cI[i]) continue;
+        XR[ir] = X[i]; gR[ir] = g[i]; lbR[ir] = Xlb[i]; ubR[ir] = Xub[i]; dXR[ir] = dX[i];
+        int jr = 0;
+        for (int j = 0; j < Ndim; ++j)
+            if (!cI[j]) { DR[(size_t)ir * nr + jr] = D[(size_t)i * Ndim + j]; jr++; }
+        ir++;
+    }
+    *recurFlag = 1;
+    bndmpi_main_loop(c, &FR, XR, gR, DR, lbR, ubR, dXR, nr, cX, cI, optimFlag, recurFlag);
+    ir = 0;
+    for (int i = 0; i < Ndim; ++i)
+        if (!cI[i]) { X[i] = XR[ir]; g[i] = gR[ir]; Xlb[i] = lbR[ir]; Xub[i] = ubR[ir]; dX[i] = dXR[ir]; ir++; }
+    /* F keeps its pre-recursion value (FRecur is not copied back, :845-864) */
+    set_identity(D, Ndim);
+    orc_fd_gradient_sharded(c->o, X, dX, g, Ndim, c->nprocs);
+    for (int i = 0; i < Ndim; ++i) {
+        cI[i] = 0;
+        if ((fabs(X[i] - Xlb[i]) < P->dXGrad) && (g[i] > 0)) { cI[i] = 1; cX[i] = X[i]; }
+        else if (fabs(X[i] - Xub[i]) < P->dXGrad && (g[i] < 0)) { cI[i] = 1; cX[i] = X[i]; }
+    }
+    Nconst = 0;
+    for (int i = 0; i < Ndim; ++i) Nconst += cI[i];
+    *optimFlag = Nconst == 0;
+    *recurFlag = 0;
+    free(XR); free(gR); free(lbR); free(ubR); free(dXR); free(DR);
+}
+
+/* BFGSBnd_MPI::mainBFGSLoop, :84-243 */
+static void bndmpi_main_loop(bndmpi_ctx* c, double* F, double* X, double* g, double* D, double* Xlb, double* Xub,
+                             double* dX, int n, double* cX, unsigned char* cI, int* optimFlag, int* recurFlag) {
+    const orc_bfgs_bnd_mpi_params* P = c->prm;
+    size_t nb = sizeof(double) * (size_t)(n > 0 ? n : 1);
+    double* gprev = (double*)malloc(nb);
+    double* p = (double*)malloc(nb);
+    double* s = (double*)malloc(nb);
+    double* y = (double*)malloc(nb);
+    double* Xprev = (double*)calloc((size_t)(n > 0 ? n : 1), sizeof(double));
+    double Fprev = 2 * *F;
+    memcpy(gprev, g, sizeof(double) * (size_t)n);
+    orc_util_matvec(D, g, p, n, n);
+    for (int i = 0; i < n; ++i) p[i] = -p[i];
+    int iter = 0, maxIter = (int)P->maxIter;
+    double xdiff = P->xMinDiff * 2, gnorm = 2 * P->minGrad2Norm, alpha = P->alphaMin * 2;
+    while (iter < maxIter && xdiff > P->xMinDiff && gnorm > P->minGrad2Norm && alpha > P->alphaMin && *optimFlag &&
+           !c->failed) {
+        double Fopt;
+        bndmpi_line_search(c, X, Xlb, Xub, *F, g, p, n, cX, cI, &alpha, &Fopt);
+        if (*F - Fopt < P->FStepTolerance) {
+            orc_fd_gradient_recur(c->o, X, dX, g, n, cX, cI, c->nfull);
+            for (int i = 0; i < n; ++i) p[i] = -g[i];
+            bndmpi_line_search(c, X, Xlb, Xub, *F, g, p, n, cX, cI, &alpha, &Fopt);
+        }
+        if (c->failed) break;
+        for (int i = 0; i < n; ++i) { Xprev[i] = X[i]; X[i] = X[i] + alpha * p[i]; }
+        Fprev = *F;
+        *F = Fopt;
+        orc_fd_gradient_recur(c->o, X, dX, g, n, cX, cI, c->nfull);
+        for (int i = 0; i < n; ++i) { s[i] = alpha * p[i]; y[i] = g[i] - gprev[i]; }
+        if (orc_util_dot(y, s, n) != 0) orc_update_hessian_inv(D, y, s, n);
+        memcpy(gprev, g, sizeof(double) * (size_t)n);
+        orc_util_matvec(D, g, p, n, n);
+        for (int i = 0; i < n; ++i) p[i] = -p[i];
+        if (*F > Fprev) *optimFlag = 0;
+        xdiff = 0;
+        for (int i = 0; i < n; ++i) xdiff += fabs(X[i] - Xprev[i]);
+        gnorm = orc_util_norm2(g, n);
+        if (!*recurFlag) bndmpi_assess(c, F, X, p, g, D, Xlb, Xub, dX, cX, cI, optimFlag, recurFlag);
+        iter++;
+    }
+    free(gprev); free(p); free(s); free(y); free(Xprev);
+}
+
+/* BFGSBnd_MPI::findMinBnd, BFGS_with_bnd_linsearch_MPI.cpp:14-81, with Npool = npool and the
+ * FD gradients sharded over nprocs owners (values do not depend on nprocs).  Returns -1
+ * when a pool value is NaN / inf (the reference's exit(0) path). */
+int orc_bfgs_bnd_mpi_findmin(orc_objective* o, const orc_bfgs_bnd_mpi_params* prm, int npool, int nprocs,
+                             double* X, const double* Xlb_in, const double* Xub_in, int n, orc_result* res) {
+    bndmpi_ctx c = {o, prm, n, npool, nprocs, 0};
+    double* Xlb = (double*)malloc(sizeof(double) * (size_t)n);
+    double* Xub = (double*)malloc(sizeof(double) * (size_t)n);
+    memcpy(Xlb, Xlb_in, sizeof(double) * (size_t)n);
+    memcpy(Xub, Xub_in, sizeof(double) * (size_t)n);
+    double* cX = (double*)calloc((size_t)n, sizeof(double));
+    unsigned char* cI = (unsigned char*)calloc((size_t)n, 1);
+    double* dX = (double*)malloc(sizeof(double) * (size_t)n);
+    double* g = (double*)calloc((size_t)n, sizeof(double));
+    double* D = (double*)malloc(sizeof(double) * (size_t)n * n);
+    for (int i = 0; i < n; ++i) dX[i] = prm->dXGrad;
+    orc_check_box_bounds(X, Xlb, Xub, n);
+    if (prm->initHessFD) {
+        double* B = (double*)malloc(sizeof(double) * (size_t)n * n);
+        double* dXH = (double*)malloc(sizeof(double) * (size_t)n);
+        for (int i = 0; i < n; ++i) dXH[i] = prm->dXHess;
+        orc_fd_hessian(o, X, dXH, B, n);
+        orc_util_matinv(B, D, n);
+        free(B); free(dXH);
+    } else {
+        set_identity(D, n);
+    }
+    long ev0 = o->evals;
+    orc_fd_gradient_sharded(o, X, dX, g, n, nprocs);
+    double F = orc_obj_eval(o, X);
+    res->f0 = F;
+    int optimFlag = 1, recurFlag = 0;
+    bndmpi_main_loop(&c, &F, X, g, D, Xlb, Xub, dX, n, cX, cI, &optimFlag, &recurFlag);
+    res->fopt = F; res->iters = 0; res->evals = o->evals - ev0;
+    free(Xlb); free(Xub); free(cX); free(cI); free(dX); free(g); free(D);
+    return c.failed ? -1 : 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
 /* synthetic inputs                                                                       */
 /* ------------------------------------------------------------------------------------ */
 

@@ -116,6 +116,17 @@ typedef struct {   /* BFGS_Bnd::setParams, BFGS_bnd_linesearch.hpp:80 */
 /* BFGS_Bnd::findMinBnd, BFGS_bnd_linesearch.cpp:15-113 */
 int orc_bfgs_bnd_findmin(orc_objective* o, const orc_bfgs_bnd_params* prm, double* X, const double* Xlb,
                          const double* Xub, int n, orc_result* res);
+typedef struct {   /* BFGSBnd_MPI::setParams, BFGS_with_bnd_linesearch_MPI.hpp:79 */
+    double c1, c2, alphaMin, maxAlphaMult, alphaGuess; int maxIterLineSearch;
+    double dXGrad, dXHess; double maxIter; double xMinDiff, minGrad2Norm, FStepTolerance; int initHessFD;
+    int verbose;
+} orc_bfgs_bnd_mpi_params;
+/* BFGSBnd_MPI::findMinBnd, BFGS_with_bnd_linsearch_MPI.cpp:14-81 (Npool = npool, FD over nprocs) */
+int orc_bfgs_bnd_mpi_findmin(orc_objective* o, const orc_bfgs_bnd_mpi_params* prm, int npool, int nprocs,
+                             double* X, const double* Xlb, const double* Xub, int n, orc_result* res);
+/* checkAlphaPoolBnd, BFGS_with_bnd_linsearch_MPI.cpp:711-743 */
+void orc_check_alpha_pool_bnd(int* bndIndicator, double* alphaPool, int npool, const double* X, const double* Xlb,
+                              const double* Xub, const double* p, int n);
 double orc_compute_alpha_bnd(const double* X, const double* Xlb, const double* Xub, const double* p, int n);
 void orc_check_box_bounds(double* X, const double* Xlb, const double* Xub, int n);
 

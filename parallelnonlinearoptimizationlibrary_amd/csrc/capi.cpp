@@ -50,6 +50,12 @@ int pnol_set_identity_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* 
     return launch_set_identity(ctx, D, ldd, n, scale);
 }
 
+int pnol_gather_submatrix_d(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub,
+                            double* Dsub, int lds) {
+    PNOL_CHECK(set_device(ctx));
+    return launch_gather_sub(ctx, D, ldd, n, idx, nsub, Dsub, lds);
+}
+
 int pnol_jtj_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                double* jtj_diag) {
     PNOL_CHECK(set_device(ctx));

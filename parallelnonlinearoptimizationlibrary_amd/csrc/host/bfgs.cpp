@@ -19,34 +19,6 @@ void print_vec(const std::vector<double>& v) {
     std::printf("\n");
 }
 
-// D0 = inverse of the FD Hessian (initHessFD), column by column on the device
-void init_from_fd_hessian(Objective* obj, std::vector<double>& X, double dXHess, DenseInverseHessian& D) {
-    const int n = (int)X.size();
-    std::vector<double> dXH(n, dXHess);
-    std::vector<std::vector<double>> B;
-    obj->hessianApproximation(X, dXH, B);
-    pnol_ctx* ctx = require_ctx();
-    const int ld = even_ld(n);
-    std::vector<double> hB((size_t)n * ld, 0.0);
-    for (int i = 0; i < n; ++i)
-        for (int j = 0; j < n; ++j) hB[(size_t)i * ld + j] = B[i][j];
-    DevVec dA(ctx, hB.size()), de(ctx, n), dc(ctx, n);
-    std::vector<std::vector<double>> Dinv(n, std::vector<double>(n));
-    std::vector<double> e(n, 0.0), c(n);
-    for (int j = 0; j < n; ++j) {
-        // matrixInverse via per-column solves; the solve consumes its matrix
-        dA.upload(hB);
-        e[j] = 1.0;
-        de.upload(e);
-        int info = 0;
-        check(pnol_solve_d(ctx, dA.get(), ld, de.get(), dc.get(), n, 2, &info), "solve(initHessFD)");
-        dc.download(c);
-        for (int i = 0; i < n; ++i) Dinv[i][j] = c[i];
-        e[j] = 0.0;
-    }
-    D.setMatrix(Dinv);
-}
-
 }  // namespace
 
 double cubicInterpMin(double alo, double ahi, double plo, double phi, double dlo, double dhi, vector<double>& X,

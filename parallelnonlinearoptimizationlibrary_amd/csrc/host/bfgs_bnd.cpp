@@ -286,23 +286,7 @@ void BFGS_Bnd::findMinBnd(vector<double>& X, vector<double>& Xlb, vector<double>
     pnol_ctx* ctx = require_ctx();
     DenseInverseHessian D(ctx, n, updateMode);
     if (initHessFD) {
-        std::vector<double> dXH(n, dXHess);
-        std::vector<std::vector<double>> B;
-        objPtr->hessianApproximation(X, dXH, B);
-        const int ld = even_ld(n);
-        std::vector<double> hB((size_t)n * ld, 0.0), e(n, 0.0), c(n);
-        for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) hB[(size_t)i * ld + j] = B[i][j];
-        DevVec dA(ctx, hB.size()), de(ctx, n), dc(ctx, n);
-        std::vector<std::vector<double>> Dinv(n, std::vector<double>(n));
-        for (int j = 0; j < n; ++j) {
-            dA.upload(hB); e[j] = 1.0; de.upload(e);
-            int info = 0;
-            check(pnol_solve_d(ctx, dA.get(), ld, de.get(), dc.get(), n, 2, &info), "solve(initHessFD)");
-            dc.download(c);
-            for (int i = 0; i < n; ++i) Dinv[i][j] = c[i];
-            e[j] = 0.0;
-        }
-        D.setMatrix(Dinv);
+        init_from_fd_hessian(objPtr, X, dXHess, D);
     } else if (!initialScalingVec.empty()) {
         D.setIdentity(&initialScalingVec);
     } else {

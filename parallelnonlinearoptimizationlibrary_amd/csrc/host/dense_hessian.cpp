@@ -3,6 +3,8 @@
 
 #include <cmath>
 
+#include "PNOL_Objective.hpp"
+
 namespace pnol {
 
 DenseInverseHessian::DenseInverseHessian(pnol_ctx* ctx, int n, int mode)
@@ -28,6 +30,17 @@ void DenseInverseHessian::setMatrix(const std::vector<std::vector<double>>& D) {
     for (int i = 0; i < n_; ++i)
         for (int j = 0; j < n_; ++j) h[(size_t)i * ld_ + j] = D[i][j];
     D_.upload(h.data(), h.size());
+    pending_ = false;
+}
+
+void DenseInverseHessian::setSubmatrixOf(DenseInverseHessian& src, const std::vector<int>& idx) {
+    if ((int)idx.size() != n_) throw std::runtime_error("setSubmatrixOf: index count != n");
+    src.materialize();
+    DevVec di(ctx_, (idx.size() + 1) / 2);   // ints in a double-sized device buffer
+    check(pnol_memcpy_h2d(ctx_, di.get(), idx.data(), sizeof(int) * idx.size()), "h2d");
+    check(pnol_gather_submatrix_d(ctx_, src.D_.get(), src.ld_, src.n_, reinterpret_cast<const int*>(di.get()), n_,
+                                  D_.get(), ld_),
+          "gather_submatrix");
     pending_ = false;
 }
 
@@ -105,5 +118,34 @@ void DenseInverseHessian::update(const std::vector<double>& y, const std::vector
         for (int i = 0; i < n_; ++i) (*pnext)[i] = -(v[i] + hs_[i] * ag + hb_[i] * sg);
     }
 }
+
+// D0 = inverse of the FD Hessian (initHessFD), column by column on the device
+void init_from_fd_hessian(Objective* obj, std::vector<double>& X, double dXHess, DenseInverseHessian& D) {
+    const int n = (int)X.size();
+    std::vector<double> dXH(n, dXHess);
+    std::vector<std::vector<double>> B;
+    obj->hessianApproximation(X, dXH, B);
+    pnol_ctx* ctx = require_ctx();
+    const int ld = even_ld(n);
+    std::vector<double> hB((size_t)n * ld, 0.0);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) hB[(size_t)i * ld + j] = B[i][j];
+    DevVec dA(ctx, hB.size()), de(ctx, n), dc(ctx, n);
+    std::vector<std::vector<double>> Dinv(n, std::vector<double>(n));
+    std::vector<double> e(n, 0.0), c(n);
+    for (int j = 0; j < n; ++j) {
+        // matrixInverse via per-column solves; the solve consumes its matrix
+        dA.upload(hB);
+        e[j] = 1.0;
+        de.upload(e);
+        int info = 0;
+        check(pnol_solve_d(ctx, dA.get(), ld, de.get(), dc.get(), n, 2, &info), "solve(initHessFD)");
+        dc.download(c);
+        for (int i = 0; i < n; ++i) Dinv[i][j] = c[i];
+        e[j] = 0.0;
+    }
+    D.setMatrix(Dinv);
+}
+
 
 }  // namespace pnol

@@ -14,6 +14,8 @@
 
 #include "device_util.hpp"
 
+class Objective;
+
 namespace pnol {
 
 class DenseInverseHessian {
@@ -26,6 +28,8 @@ class DenseInverseHessian {
     void setIdentity(const std::vector<double>* diagScale = nullptr);
     void setMatrix(const std::vector<std::vector<double>>& D);
     void getMatrix(std::vector<std::vector<double>>& D);
+    // this = src[idx][idx] (idx ascending, size n()), gathered on the device
+    void setSubmatrixOf(DenseInverseHessian& src, const std::vector<int>& idx);
 
     // p = -D g
     void direction(const std::vector<double>& g, std::vector<double>& p);
@@ -45,5 +49,9 @@ class DenseInverseHessian {
     bool pending_ = false;
     std::vector<double> hs_, ha_, hb_; // host copies of the pending correction
 };
+
+// D0 = inverse of the FD Hessian (initHessFD: hessianApproximation + matrixInverse,
+// PNOL_Objective.cpp:38-85), column by column through the reference-order device LU
+void init_from_fd_hessian(Objective* obj, std::vector<double>& X, double dXHess, DenseInverseHessian& D);
 
 }  // namespace pnol

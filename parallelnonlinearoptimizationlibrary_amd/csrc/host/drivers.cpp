@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "BFGS_bnd_linesearch.hpp"
+#include "BFGS_with_bnd_linesearch_MPI.hpp"
 #include "BFGS_with_linesearch.hpp"
 #include "BFGS_with_linesearch_MPI.hpp"
 #include "LevenbergMarquardt.hpp"
@@ -172,6 +173,16 @@ int pnol_run_bfgs(int which, pnol_dobj* obj, int host_eval, const double* p, int
             BFGS_Bnd b;
             b.setParams(p[0], p[1], p[2], p[3], p[4], p[5], (int)p[6], p[7], p[8], p[9], p[10], p[11], p[12],
                         p[13] != 0, (int)p[14]);
+            if (np > 15) b.setUpdateMode((int)p[15]);
+            b.setObjPtr(o);
+            std::vector<double> lb(Xlb, Xlb + n), ub(Xub, Xub + n);
+            b.findMinBnd(x, lb, ub, f0, fopt);
+        } else if (which == 3) {
+            if (np < 14 || !Xlb || !Xub) throw std::runtime_error("BFGSBnd_MPI needs 14 params and bounds");
+            BFGSBnd_MPI b;
+            b.setParams(p[0], p[1], p[2], p[3], p[4], (int)p[5], p[6], p[7], p[8], p[9], p[10], p[11], p[12] != 0,
+                        p[13] != 0);
+            if (np > 14) b.setPoolSize((int)p[14]);
             if (np > 15) b.setUpdateMode((int)p[15]);
             b.setObjPtr(o);
             std::vector<double> lb(Xlb, Xlb + n), ub(Xub, Xub + n);

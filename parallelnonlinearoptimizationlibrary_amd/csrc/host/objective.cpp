@@ -152,13 +152,31 @@ void Objective::gradientApproximationMPIRecur(vector<double>& X, vector<double>&
     block_range(N, P, r, &b, &cnt);
     const int per = (N + P - 1) / P > 0 ? (N + P - 1) / P : 1;
     std::vector<double> mine(per, 0.0), all((size_t)P * per, 0.0);
-    const double F = objEvalRecur(X, constantX, constantIndicator);
-    std::vector<double> XdX(N);
-    for (int q = 0; q < cnt; ++q) {
-        const int i = b + q;
-        XdX = X;
-        XdX[i] = XdX[i] + dX[i];
-        mine[q] = (objEvalRecur(XdX, constantX, constantIndicator) - F) / dX[i];
+    if (pnol_dobj* d = deviceObjective((int)constantX.size())) {
+        // the rank's free coordinates [b, b+cnt) span full indices [map[b], map[b+cnt-1]]: one
+        // batched launch over that span (frozen coordinates inside it are evaluated and dropped)
+        std::vector<double> Xf = scatter_full(X, constantX, constantIndicator);
+        std::vector<double> hf(Xf.size(), 1.0);
+        std::vector<int> map;
+        for (size_t i = 0, ir = 0; i < constantX.size(); ++i)
+            if (!constantIndicator[i]) { map.push_back((int)i); hf[i] = dX[ir++]; }
+        if (cnt > 0) {
+            const int f0i = map[b], span = map[b + cnt - 1] - f0i + 1;
+            std::vector<double> gs(span);
+            double F = 0;
+            device_gradient(d, Xf, hf, f0i, span, &F, gs.data());
+            for (int q = 0; q < cnt; ++q) mine[q] = gs[map[b + q] - f0i];
+        }
+        countEvals(cnt + 1);
+    } else {
+        const double F = objEvalRecur(X, constantX, constantIndicator);
+        std::vector<double> XdX(N);
+        for (int q = 0; q < cnt; ++q) {
+            const int i = b + q;
+            XdX = X;
+            XdX[i] = XdX[i] + dX[i];
+            mine[q] = (objEvalRecur(XdX, constantX, constantIndicator) - F) / dX[i];
+        }
     }
     check(comm_allgather_host(nullptr, mine.data(), all.data(), (size_t)per), "allgather(gradient recur)");
     dFdX.resize(N);

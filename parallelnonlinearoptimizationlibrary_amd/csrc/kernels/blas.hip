@@ -496,6 +496,16 @@ __global__ void k_set_identity(double* __restrict__ D, long ldd, int n, const do
     }
 }
 
+// Dsub[a][b] = D[idx[a]][idx[b]]: one workgroup per destination row (idx ascending, so the
+// source reads of a row stay within one row of D and mostly coalesce)
+__global__ void k_gather_sub(const double* __restrict__ D, long ldd, const int* __restrict__ idx, int nsub,
+                             double* __restrict__ Dsub, long lds) {
+    for (int a = blockIdx.x; a < nsub; a += gridDim.x) {
+        const double* row = D + (long)idx[a] * ldd;
+        for (int b = threadIdx.x; b < nsub; b += blockDim.x) Dsub[(long)a * lds + b] = row[idx[b]];
+    }
+}
+
 __global__ void k_fill(double* __restrict__ p, size_t count, double value) {
     for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < count; k += (size_t)gridDim.x * blockDim.x)
         p[k] = value;
@@ -619,6 +629,15 @@ int launch_set_identity(pnol_ctx* ctx, double* D, int ldd, int n, const double* 
     long total = (long)n * ldd;
     int blocks = (int)std::min<long>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(k_set_identity, dim3(blocks), dim3(256), 0, ctx->stream, D, (long)ldd, n, scale);
+    return launch_check();
+}
+
+int launch_gather_sub(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub, double* Dsub,
+                      int lds) {
+    if (!D || !idx || !Dsub || nsub < 0 || nsub > n || ldd < n || lds < nsub) return PNOL_ERR_ARG;
+    if (nsub == 0) return PNOL_OK;
+    hipLaunchKernelGGL(k_gather_sub, dim3(std::min(nsub, 8192)), dim3(256), 0, ctx->stream, D, (long)ldd, idx, nsub,
+                       Dsub, (long)lds);
     return launch_check();
 }
 

@@ -116,6 +116,8 @@ int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p
                      const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
                      double* v);
 int launch_set_identity(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale);
+int launch_gather_sub(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub, double* Dsub,
+                      int lds);
 
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                double* jtj_diag);

@@ -16,7 +16,7 @@ def main():
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
-    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_levmarq
+    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_bfgs, run_levmarq
     from parallelnonlinearoptimizationlibrary_amd.dist import HostComm
     comm = HostComm(rank, world)
     ctx = Context(0)
@@ -30,7 +30,15 @@ def main():
     L.check(L.lib().pnol_jtj_mpi_d(ctx.h, JT.data_ptr(), m, m, n, 0.25, A.data_ptr(), n, diag.data_ptr()),
             "pnol_jtj_mpi_d")
     ctx.synchronize()
-    np.savez(os.path.join(out, f"rank{rank}.npz"), X=X, A=A.cpu().numpy(), diag=diag.cpu().numpy())
+    # BFGSBnd_MPI, testBFGSBnd_MPI start (Examples.cpp:90-120): Npool = world, pool entries
+    # round-robin over the ranks, FD gradients sharded
+    nb = 10
+    x0 = np.full(nb, 3.0); x0[0] = -0.5
+    lb = np.full(nb, -5.0); lb[0] = -1.0
+    Pb = [1e-4, 0.1, 1e-16, 4, 1, 1000, 1e-7, 1e-3, 200, 1e-5, 1e-5, 1e-5, 0, 0]
+    Xb, resb = run_bfgs(DeviceObjective(ctx, L.OBJ_ROSENBROCK, nb), x0, Pb, which=3, lb=lb, ub=np.full(nb, 5.0))
+    np.savez(os.path.join(out, f"rank{rank}.npz"), X=X, A=A.cpu().numpy(), diag=diag.cpu().numpy(), Xb=Xb,
+             fb=np.array([resb.fopt]))
     comm.close()
     dist.barrier()
     dist.destroy_process_group()

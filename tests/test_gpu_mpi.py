@@ -1,4 +1,4 @@
-"""LevMarqMPI on the device with more than one rank: two processes share the box's one GPU and
+"""LevMarqMPI and BFGSBnd_MPI on the device with more than one rank: two processes share the box's one GPU and
 exchange through the host communicator backend (gloo allgather callback).  The sharded FD
 Jacobian (column blocks + allgather) and the tile-sharded J^T J (pnol_jtj_mpi_d) must give
 results bitwise equal to the single-rank device run -- the reference's MPI results are
@@ -25,7 +25,7 @@ def _free_port():
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_levmarq_mpi_ranks_bitwise_equal_single(tmp_path, world):
+def test_levmarq_mpi_ranks_bitwise_equal_single(tmp_path, world, oracle):
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_levmarq
     m, n = 2000, 300     # 6 J^T J tiles: uneven tile ranges at world = 3 / 4
@@ -59,3 +59,14 @@ def test_levmarq_mpi_ranks_bitwise_equal_single(tmp_path, world):
         assert np.array_equal(z["X"], X1), r
         assert np.array_equal(z["A"], A1), r
         assert np.array_equal(z["diag"], d1), r
+    # BFGSBnd_MPI across the ranks equals the reference at np = world
+    nb = 10
+    x0 = np.full(nb, 3.0); x0[0] = -0.5
+    lb = np.full(nb, -5.0); lb[0] = -1.0
+    Pb = [1e-4, 0.1, 1e-16, 4, 1, 1000, 1e-7, 1e-3, 200, 1e-5, 1e-5, 1e-5, 0, 0]
+    Xo, reso, st = oracle.bfgs_bnd_mpi_findmin(oracle.rosenbrock(nb), x0, lb, np.full(nb, 5.0), Pb, world)
+    assert st == 0
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        assert np.array_equal(z["Xb"], Xo), r
+        assert z["fb"][0] == reso.fopt, r

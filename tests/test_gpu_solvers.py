@@ -136,6 +136,88 @@ def test_bfgs_bnd_matches_oracle(ctx, oracle, case):
     assert res.fopt == reso.fopt
 
 
+BND_MPI_P = [1e-4, 0.1, 1e-16, 4, 1, 1000, 1e-7, 1e-3, 200, 1e-5, 1e-5, 1e-5, 0, 0]   # Examples.cpp:112
+
+
+def _testBFGSBnd_MPI_start():
+    n = 10      # Examples.cpp:90-105
+    x0 = np.full(n, 3.0); x0[0] = -0.5; x0[1] = 3.0
+    lb = np.full(n, -5.0); lb[0] = -1.0
+    return n, x0, lb, np.full(n, 5.0)
+
+
+@pytest.mark.parametrize("npool", [2, 3, 4, 8])
+def test_bfgs_bnd_mpi_matches_oracle(ctx, oracle, npool):
+    """BFGSBnd_MPI (testBFGSBnd_MPI, Examples.cpp:90-120) with Npool trial steps in one process
+    equals the reference at np = Npool bitwise: X, fOpt and the evaluation count.  X[0] ends on
+    its lower bound, so the run goes through boundaryAssessment's recursion."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_bfgs
+    n, x0, lb, ub = _testBFGSBnd_MPI_start()
+    X, res = run_bfgs(_obj(ctx, L.OBJ_ROSENBROCK, n), x0, BND_MPI_P + [npool], which=3, lb=lb, ub=ub)
+    Xo, reso, st = oracle.bfgs_bnd_mpi_findmin(oracle.rosenbrock(n), x0, lb, ub, BND_MPI_P, npool)
+    assert st == 0
+    assert np.array_equal(X, Xo), (npool, X, Xo)
+    assert res.fopt == reso.fopt and res.f0 == reso.f0
+    assert res.evals == reso.evals
+    assert np.all(X >= lb) and np.all(X <= ub)
+
+
+@pytest.mark.parametrize("case", [
+    ("lower-active", 3, [-1.0, 2.0, 2.0], [-1.0] * 3, [5.0] * 3),
+    ("upper-active", 3, [0.0, 0.0, 0.0], [-2.0] * 3, [0.5] * 3),
+    ("interior", 4, [2.0] * 4, [-5.0] * 4, [5.0] * 4),
+])
+def test_bfgs_bnd_mpi_box_cases(ctx, oracle, case):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_bfgs
+    name, n, x0, lb, ub = case
+    X, res = run_bfgs(_obj(ctx, L.OBJ_ROSENBROCK, n), x0, BND_MPI_P + [4], which=3, lb=lb, ub=ub)
+    Xo, reso, st = oracle.bfgs_bnd_mpi_findmin(oracle.rosenbrock(n), x0, lb, ub, BND_MPI_P, 4)
+    assert st == 0
+    assert np.array_equal(X, Xo), name
+    assert res.fopt == reso.fopt
+
+
+def test_bfgs_bnd_mpi_quadratic_fast_mode(ctx, oracle):
+    """n = 160 > PNOL_SEQ_MAX: fused lazy rank-2 passes, and the reduced problem starts from the
+    free-free block of D gathered on the device (pnol_gather_submatrix_d).  Tolerance: the
+    fused pass sums in a different order than the reference's O(n^3) update, so X is compared
+    with the oracle within the FD-limited basin (h = 1e-6), as for BFGS fast mode."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective, run_bfgs
+    n = 160
+    dd, bb = oracle.quadratic_data(n)
+    lb, ub = np.full(n, -0.25), np.full(n, 0.25)
+    P = [1e-4, 0.1, 1e-16, 4, 1, 200, 1e-6, 1e-3, 100, 1e-9, 1e-6, 1e-9, 0, 0]
+    X, res = run_bfgs(DeviceObjective(ctx, L.OBJ_QUADRATIC, n, 0, dd, bb), np.zeros(n), P + [4], which=3,
+                      lb=lb, ub=ub)
+    Xo, reso, st = oracle.bfgs_bnd_mpi_findmin(oracle.Obj(oracle.QUADRATIC, n, 0, dd, bb), np.zeros(n), lb, ub,
+                                               P, 4)
+    assert st == 0
+    assert np.all(X >= lb) and np.all(X <= ub)
+    assert res.fopt <= res.f0
+    assert np.max(np.abs(X - Xo)) <= 2e-4, np.max(np.abs(X - Xo))
+    assert abs(res.fopt - reso.fopt) <= 1e-6 * abs(reso.fopt)
+
+
+def test_gather_submatrix(ctx):
+    """pnol_gather_submatrix_d: D[idx][idx] bitwise (BFGS_with_bnd_linsearch_MPI.cpp:832-840)."""
+    import torch
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    rng = np.random.default_rng(5)
+    for n, k in ((7, 3), (300, 211), (1000, 999)):
+        D = rng.standard_normal((n, n))
+        idx = np.sort(rng.choice(n, size=k, replace=False)).astype(np.int32)
+        dD = ctx.tensor(D)
+        di = torch.from_numpy(idx).to(dD.device)
+        out = ctx.empty(k, k)
+        L.check(L.lib().pnol_gather_submatrix_d(ctx.h, dD.data_ptr(), n, n, di.data_ptr(), k, out.data_ptr(), k),
+                "gather")
+        ctx.synchronize()
+        assert np.array_equal(out.cpu().numpy(), D[np.ix_(idx, idx)])
+
+
 @pytest.mark.parametrize("n", [200, 1000])
 def test_bfgs_quadratic_fast_mode(ctx, oracle, n):
     """n > PNOL_SEQ_MAX: fused lazy rank-2 passes; converges to the quadratic's minimiser and
