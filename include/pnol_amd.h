@@ -188,7 +188,8 @@ int pnol_comm_share_fd_rows_d(pnol_ctx* ctx, double* buf, int ld, int ncols);
 /* params arrays follow the classes' setParams order (see the headers in include/). */
 typedef struct { int iters; long evals; double f0; double fopt; } pnol_result;
 /* which: 0 = BFGS (12 params), 1 = BFGS_MPI (12 params), 2 = BFGS_Bnd (15 params),
- * 3 = BFGSBnd_MPI (14 params [+ pool size, update mode]) */
+ * 3 = BFGSBnd_MPI (14 params [+ pool size, update mode]),
+ * 4 = BFGS_Bnd_MPI_SW (15 params [+ Nprocs-equivalent pool size, update mode]) */
 int pnol_run_bfgs(int which, pnol_dobj* obj, int host_eval, const double* params, int nparams,
                   double* X, int n, const double* Xlb, const double* Xub, pnol_result* res);
 /* which: 0 = LevMarq, 1 = LevMarqMPI (6 params). F0/FOpt host arrays of m. */

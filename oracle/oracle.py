@@ -311,6 +311,15 @@ def bfgs_bnd_mpi_findmin(o: Obj, x0, lb, ub, params, npool, nprocs=None):  # BFG
     return X, res, st
 
 
+def bfgs_bnd_mpi_sw_findmin(o: Obj, x0, lb, ub, params, procs):  # BFGS_Bnd_MPI_SW::findMinBnd
+    X = np.array(x0, dtype=np.float64)
+    lb = np.ascontiguousarray(lb, dtype=np.float64); ub = np.ascontiguousarray(ub, dtype=np.float64)
+    prm = BFGSBndParams(*params)
+    res = Result()
+    lib().orc_bfgs_bnd_mpi_sw_findmin(o.ref(), C.byref(prm), procs, ptr(X), ptr(lb), ptr(ub), len(X), C.byref(res))
+    return X, res
+
+
 def check_alpha_pool_bnd(pool, x, lb, ub, p):  # checkAlphaPoolBnd, BFGS_with_bnd_linsearch_MPI.cpp:711-743
     ap = np.array(pool, dtype=np.float64)
     arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (x, lb, ub, p)]

@@ -793,6 +793,9 @@ static double cubic_interp_min_simple(double aa, double ab, double pa, double pb
 
 typedef struct {
     orc_objective* o; const orc_bfgs_bnd_params* prm; int nfull; int totalIter; int maxIter;
+    int sw;             /* 1: BFGS_Bnd_MPI_SW's pooled line search (Nprocs = procs) */
+    int procs;
+    int* optimFlag;     /* the SW class member, cleared by a NaN / inf pool value */
 } bnd_ctx;
 
 /* BFGS_Bnd::lineSearchObj / lineSearchFDDerivative, :465-496 */
@@ -879,6 +882,148 @@ static void bnd_line_search(bnd_ctx* c, const double* X, const double* Xlb, cons
         else if (phi0 < phii) { *aOpt = 0; *Fopt = phi0; }
         else { *aOpt = ai; *Fopt = phii; }
     }
+}
+
+/* ---- BFGS_Bnd_MPI_SW's pooled Wolfe search, BFGS_bnd_linesearch_MPI_SW.cpp ---- */
+
+/* evaluateAlphaPoolAndDerivativesIndicator / evaluateAlphaPoolAndDerivatives, :552-699:
+ * flagged entries, dealt round-robin to the ranks; a NaN / inf value becomes 1e10 and
+ * clears optimFlag */
+static void sw_eval_pool(bnd_ctx* c, const double* ap, double* pp, double* dp, const int* ev, int N,
+                         const double* X, const double* p, int n, const double* cX, const unsigned char* cI) {
+    int* sel = (int*)malloc(sizeof(int) * (size_t)(N > 0 ? N : 1));
+    int ns = 0;
+    for (int i = 0; i < N; ++i) if (ev[i] == 1) sel[ns++] = i;
+    for (int rank = 0; rank < c->procs; ++rank)
+        for (int t = rank; t < ns; t += c->procs) {
+            int i = sel[t];
+            double phi = bnd_ls_obj(c, ap[i], X, p, n, cX, cI);
+            double dphi = bnd_ls_deriv(c, ap[i], phi, X, p, n, cX, cI);
+            if (phi != phi || isinf(phi)) phi = 1e10;
+            pp[i] = 0.0 + phi;
+            dp[i] = 0.0 + dphi;
+        }
+    for (int t = 0; t < ns; ++t)
+        if (pp[sel[t]] == 1e10) *c->optimFlag = 0;
+    free(sel);
+}
+
+/* computeZoomRegion, :399-431 (neighbour index clamped to the pool, see the C++ note) */
+static void sw_zoom_region(const double* ap, const double* pp, const double* dp, int N, double* aa, double* ab,
+                           double* pa, double* pb, double* da, double* db) {
+    double pmin; int im;
+    vector_min(pp, N, &pmin, &im);
+    int lo, hi;
+    if (dp[im] > 0) { lo = im - 1 >= 0 ? im - 1 : 0; hi = im; }
+    else { lo = im; hi = im + 1 < N ? im + 1 : N - 1; }
+    *aa = ap[lo]; *ab = ap[hi]; *pa = pp[lo]; *pb = pp[hi]; *da = dp[lo]; *db = dp[hi];
+}
+
+/* computeZoomPool, :434-482 */
+static void sw_zoom_pool(double aa, double ab, double pa, double pb, double da, double db, double* ap, double* pp,
+                         double* dp, int* ev, int N) {
+    double ac = cubic_interp_min_simple(aa, ab, pa, pb, da, db);
+    if (ac == (aa + ab) / 2) {
+        orc_util_linspace(aa, ab, N, ap);
+    } else {
+        double* al = (double*)malloc(sizeof(double) * (size_t)(N - 1));
+        orc_util_linspace(aa, ab, N - 1, al);
+        ap[0] = al[0];
+        int il = 1;
+        for (int i = 1; i < N; ++i) {
+            if (ac >= al[il - 1] && ac <= al[il]) { ap[i] = ac; ac = -1; }
+            else { ap[i] = al[il]; il++; }
+        }
+        free(al);
+    }
+    for (int i = 0; i < N; ++i) ev[i] = 1;
+    pp[0] = pa; dp[0] = da; ev[0] = 0;
+    pp[N - 1] = pb; dp[N - 1] = db; ev[N - 1] = 0;
+}
+
+/* BFGS_Bnd_MPI_SW::lineSearchZoomBnd, :484-548 */
+static void sw_zoom(bnd_ctx* c, double aa, double ab, double pa, double pb, double da, double db, double phi0,
+                    double dphi0, const double* X, const double* p, int n, const double* cX,
+                    const unsigned char* cI, int* iter_ls, double* aOpt, double* pOpt) {
+    const orc_bfgs_bnd_params* P = c->prm;
+    int N = c->procs + 2;
+    int* ev = (int*)malloc(sizeof(int) * (size_t)N);
+    double* ap = (double*)calloc((size_t)N, sizeof(double));
+    double* pp = (double*)calloc((size_t)N, sizeof(double));
+    double* dp = (double*)calloc((size_t)N, sizeof(double));
+    int zoom = 1, success = 0;
+    while (*iter_ls < P->maxIterLineSearch && (ab - aa > P->alphaTol) && zoom) {
+        sw_zoom_pool(aa, ab, pa, pb, da, db, ap, pp, dp, ev, N);
+        sw_eval_pool(c, ap, pp, dp, ev, N, X, p, n, cX, cI);
+        for (int i = 1; i < N - 1; ++i)
+            if ((pp[i] <= phi0 + P->c1 * ap[i] * dphi0) && (fabs(dp[i]) <= fabs(P->c2 * dphi0))) {
+                zoom = 0; success = 1;
+            }
+        if (!success) sw_zoom_region(ap, pp, dp, N, &aa, &ab, &pa, &pb, &da, &db);
+        (*iter_ls)++;
+    }
+    double pmin; int im;
+    vector_min(pp, N, &pmin, &im);
+    *aOpt = ap[im]; *pOpt = pmin;
+    free(ev); free(ap); free(pp); free(dp);
+}
+
+/* BFGS_Bnd_MPI_SW::cubicInterpolationLineSearchBnd, :209-397 */
+static void sw_line_search(bnd_ctx* c, const double* X, const double* Xlb, const double* Xub, double FX,
+                           const double* g, const double* p, int n, const double* cX, const unsigned char* cI,
+                           double* aOpt, double* Fopt) {
+    const orc_bfgs_bnd_params* P = c->prm;
+    int procs = c->procs, N = procs + 1;
+    int* ev = (int*)malloc(sizeof(int) * (size_t)N);
+    double* ap = (double*)calloc((size_t)N, sizeof(double));
+    double* pp = (double*)calloc((size_t)N, sizeof(double));
+    double* dp = (double*)calloc((size_t)N, sizeof(double));
+    double phi0 = FX, dphi0 = orc_util_dot(g, p, n), pOpt = FX;
+    *aOpt = 0; *Fopt = FX;
+    for (int i = 0; i < N; ++i) ev[i] = 1;
+    ev[0] = 0; ap[0] = 0; pp[0] = phi0; dp[0] = dphi0;
+    double amax = orc_compute_alpha_bnd(X, Xlb, Xub, p, n);
+    double ai = P->alphaGuess;
+    if (ai > amax) ai = amax;
+    double delta = ai / procs;
+    for (int i = 1; i < N; ++i) ap[i] = delta * i;
+    int iter_ls = 0, extend = 1, zoom = 0;
+    while (iter_ls < P->maxIterLineSearch && extend) {
+        sw_eval_pool(c, ap, pp, dp, ev, N, X, p, n, cX, cI);
+        for (int i = 1; i < N; ++i)
+            if ((pp[i] > phi0 + P->c1 * ap[i] * dphi0) || (pp[i] >= pp[0] && iter_ls > 1)) { extend = 0; zoom = 1; }
+        for (int i = 1; i < N; ++i)
+            if (fabs(dp[i]) <= fabs(P->c2 * dphi0)) { extend = 0; zoom = 0; }
+        for (int i = 1; i < N; ++i)
+            if (dp[i] >= 0) { extend = 0; zoom = 1; }
+        if (extend && ap[N - 1] == amax) { extend = 0; zoom = 0; }
+        if (extend) {
+            double an = (procs + 1) * ap[N - 1];
+            if (an > amax) an = amax;
+            orc_util_linspace(ap[N - 1], an, N, ap);
+            for (int i = 0; i < N; ++i) ev[i] = 1;
+            ev[0] = 0;
+            pp[0] = pp[N - 1];
+            dp[0] = dp[N - 1];
+        }
+        iter_ls++;
+    }
+    double pmin; int im;
+    if (zoom) {
+        double aa, ab, pa, pb, da, db;
+        sw_zoom_region(ap, pp, dp, N, &aa, &ab, &pa, &pb, &da, &db);
+        if (ab - aa > P->alphaTol) {
+            sw_zoom(c, aa, ab, pa, pb, da, db, phi0, dphi0, X, p, n, cX, cI, &iter_ls, aOpt, &pOpt);
+        } else {
+            vector_min(pp, N, &pmin, &im);
+            *aOpt = ap[im]; pOpt = pmin;
+        }
+    } else {
+        vector_min(pp, N, &pmin, &im);
+        *aOpt = ap[im]; pOpt = pmin;
+    }
+    *Fopt = pOpt;
+    free(ev); free(ap); free(pp); free(dp);
 }
 
 static void bnd_main_loop(bnd_ctx* c, double* F, double* X, double* g, double* D, double* Xlb, double* Xub,
@@ -969,7 +1114,8 @@ static void bnd_main_loop(bnd_ctx* c, double* F, double* X, double* g, double* D
         orc_util_matvec(D, g, p, n, n);
         for (int i = 0; i < n; ++i) p[i] = -p[i];
         double alpha, Fopt;
-        bnd_line_search(c, X, Xlb, Xub, *F, g, p, n, cX, cI, &alpha, &Fopt);
+        if (c->sw) sw_line_search(c, X, Xlb, Xub, *F, g, p, n, cX, cI, &alpha, &Fopt);
+        else bnd_line_search(c, X, Xlb, Xub, *F, g, p, n, cX, cI, &alpha, &Fopt);
         for (int i = 0; i < n; ++i) { Xprev[i] = X[i]; X[i] = X[i] + alpha * p[i]; }
         *F = Fopt;
         memcpy(gprev, g, sizeof(double) * (size_t)n);
@@ -989,7 +1135,7 @@ static void bnd_main_loop(bnd_ctx* c, double* F, double* X, double* g, double* D
 /* BFGS_Bnd::findMinBnd, BFGS_bnd_linesearch.cpp:15-113 (no dXGradVec / initialScalingVec) */
 int orc_bfgs_bnd_findmin(orc_objective* o, const orc_bfgs_bnd_params* prm, double* X, const double* Xlb_in,
                          const double* Xub_in, int n, orc_result* res) {
-    bnd_ctx c = {o, prm, n, 0, (int)prm->maxIter};
+    bnd_ctx c = {o, prm, n, 0, (int)prm->maxIter, 0, 1, NULL};
     double* Xlb = (double*)malloc(sizeof(double) * (size_t)n);
     double* Xub = (double*)malloc(sizeof(double) * (size_t)n);
     memcpy(Xlb, Xlb_in, sizeof(double) * (size_t)n);
@@ -1016,6 +1162,43 @@ int orc_bfgs_bnd_findmin(orc_objective* o, const orc_bfgs_bnd_params* prm, doubl
     double F = orc_obj_eval_recur(o, X, cX, cI, n);
     res->f0 = F;
     int optimFlag = 1, recurFlag = 0;
+    bnd_main_loop(&c, &F, X, g, D, Xlb, Xub, dX, n, cX, cI, &optimFlag, &recurFlag);
+    res->fopt = F; res->iters = c.totalIter; res->evals = o->evals - ev0;
+    free(Xlb); free(Xub); free(cX); free(cI); free(dX); free(g); free(D);
+    return 0;
+}
+
+/* BFGS_Bnd_MPI_SW::findMinBnd, BFGS_bnd_linesearch_MPI_SW.cpp:12-113, with Nprocs = procs
+ * (gradients through the Recur FD engine: the sharded MPIRecur form gives the same values) */
+int orc_bfgs_bnd_mpi_sw_findmin(orc_objective* o, const orc_bfgs_bnd_params* prm, int procs, double* X,
+                                const double* Xlb_in, const double* Xub_in, int n, orc_result* res) {
+    int optimFlag = 1, recurFlag = 0;
+    bnd_ctx c = {o, prm, n, 0, (int)prm->maxIter, 1, procs, &optimFlag};
+    double* Xlb = (double*)malloc(sizeof(double) * (size_t)n);
+    double* Xub = (double*)malloc(sizeof(double) * (size_t)n);
+    memcpy(Xlb, Xlb_in, sizeof(double) * (size_t)n);
+    memcpy(Xub, Xub_in, sizeof(double) * (size_t)n);
+    orc_check_box_bounds(X, Xlb, Xub, n);
+    double* cX = (double*)calloc((size_t)n, sizeof(double));
+    unsigned char* cI = (unsigned char*)calloc((size_t)n, 1);
+    double* dX = (double*)malloc(sizeof(double) * (size_t)n);
+    double* g = (double*)calloc((size_t)n, sizeof(double));
+    double* D = (double*)malloc(sizeof(double) * (size_t)n * n);
+    for (int i = 0; i < n; ++i) dX[i] = prm->dXGrad;
+    if (prm->initHessFD) {
+        double* B = (double*)malloc(sizeof(double) * (size_t)n * n);
+        double* dXH = (double*)malloc(sizeof(double) * (size_t)n);
+        for (int i = 0; i < n; ++i) dXH[i] = prm->dXHess;
+        orc_fd_hessian(o, X, dXH, B, n);
+        orc_util_matinv(B, D, n);
+        free(B); free(dXH);
+    } else {
+        set_identity(D, n);
+    }
+    long ev0 = o->evals;
+    orc_fd_gradient_recur(o, X, dX, g, n, cX, cI, n);
+    double F = orc_obj_eval_recur(o, X, cX, cI, n);
+    res->f0 = F;
     bnd_main_loop(&c, &F, X, g, D, Xlb, Xub, dX, n, cX, cI, &optimFlag, &recurFlag);
     res->fopt = F; res->iters = c.totalIter; res->evals = o->evals - ev0;
     free(Xlb); free(Xub); free(cX); free(cI); free(dX); free(g); free(D);

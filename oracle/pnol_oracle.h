@@ -116,6 +116,10 @@ typedef struct {   /* BFGS_Bnd::setParams, BFGS_bnd_linesearch.hpp:80 */
 /* BFGS_Bnd::findMinBnd, BFGS_bnd_linesearch.cpp:15-113 */
 int orc_bfgs_bnd_findmin(orc_objective* o, const orc_bfgs_bnd_params* prm, double* X, const double* Xlb,
                          const double* Xub, int n, orc_result* res);
+/* BFGS_Bnd_MPI_SW::findMinBnd, BFGS_bnd_linesearch_MPI_SW.cpp:12-113 (same setParams as BFGS_Bnd;
+ * Nprocs = procs: pools of procs + 1 / procs + 2) */
+int orc_bfgs_bnd_mpi_sw_findmin(orc_objective* o, const orc_bfgs_bnd_params* prm, int procs, double* X,
+                                const double* Xlb, const double* Xub, int n, orc_result* res);
 typedef struct {   /* BFGSBnd_MPI::setParams, BFGS_with_bnd_linesearch_MPI.hpp:79 */
     double c1, c2, alphaMin, maxAlphaMult, alphaGuess; int maxIterLineSearch;
     double dXGrad, dXHess; double maxIter; double xMinDiff, minGrad2Norm, FStepTolerance; int initHessFD;

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "BFGS_bnd_linesearch.hpp"
+#include "BFGS_bnd_linesearch_MPI_SW.hpp"
 #include "BFGS_with_bnd_linesearch_MPI.hpp"
 #include "BFGS_with_linesearch.hpp"
 #include "BFGS_with_linesearch_MPI.hpp"
@@ -184,6 +185,16 @@ int pnol_run_bfgs(int which, pnol_dobj* obj, int host_eval, const double* p, int
                         p[13] != 0);
             if (np > 14) b.setPoolSize((int)p[14]);
             if (np > 15) b.setUpdateMode((int)p[15]);
+            b.setObjPtr(o);
+            std::vector<double> lb(Xlb, Xlb + n), ub(Xub, Xub + n);
+            b.findMinBnd(x, lb, ub, f0, fopt);
+        } else if (which == 4) {
+            if (np < 15 || !Xlb || !Xub) throw std::runtime_error("BFGS_Bnd_MPI_SW needs 15 params and bounds");
+            BFGS_Bnd_MPI_SW b;
+            b.setParams(p[0], p[1], p[2], p[3], p[4], p[5], (int)p[6], p[7], p[8], p[9], p[10], p[11], p[12],
+                        p[13] != 0, (int)p[14]);
+            if (np > 15) b.setPoolSize((int)p[15]);
+            if (np > 16) b.setUpdateMode((int)p[16]);
             b.setObjPtr(o);
             std::vector<double> lb(Xlb, Xlb + n), ub(Xub, Xub + n);
             b.findMinBnd(x, lb, ub, f0, fopt);

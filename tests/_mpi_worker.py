@@ -37,8 +37,12 @@ def main():
     lb = np.full(nb, -5.0); lb[0] = -1.0
     Pb = [1e-4, 0.1, 1e-16, 4, 1, 1000, 1e-7, 1e-3, 200, 1e-5, 1e-5, 1e-5, 0, 0]
     Xb, resb = run_bfgs(DeviceObjective(ctx, L.OBJ_ROSENBROCK, nb), x0, Pb, which=3, lb=lb, ub=np.full(nb, 5.0))
+    # BFGS_Bnd_MPI_SW, testBFGSBndMPISW (Examples.cpp:12-45): pools of world + 1 / world + 2
+    Psw = [1e-4, 0.8, 1e-6, 1, 1e-10, 2, 50, 1e-5, 1e-6, 1e-3, 200, 1e-5, 1e-5, 0, -1]
+    Xs, ress = run_bfgs(DeviceObjective(ctx, L.OBJ_ROSENBROCK, 3), [-1.0, 2.0, 2.0], Psw, which=4, lb=[-1.0] * 3,
+                        ub=[5.0] * 3)
     np.savez(os.path.join(out, f"rank{rank}.npz"), X=X, A=A.cpu().numpy(), diag=diag.cpu().numpy(), Xb=Xb,
-             fb=np.array([resb.fopt]))
+             fb=np.array([resb.fopt]), Xs=Xs, fs=np.array([ress.fopt]))
     comm.close()
     dist.barrier()
     dist.destroy_process_group()

@@ -1,4 +1,4 @@
-"""LevMarqMPI and BFGSBnd_MPI on the device with more than one rank: two processes share the box's one GPU and
+"""LevMarqMPI, BFGSBnd_MPI and BFGS_Bnd_MPI_SW on the device with more than one rank: two processes share the box's one GPU and
 exchange through the host communicator backend (gloo allgather callback).  The sharded FD
 Jacobian (column blocks + allgather) and the tile-sharded J^T J (pnol_jtj_mpi_d) must give
 results bitwise equal to the single-rank device run -- the reference's MPI results are
@@ -70,3 +70,11 @@ def test_levmarq_mpi_ranks_bitwise_equal_single(tmp_path, world, oracle):
         z = np.load(tmp_path / f"rank{r}.npz")
         assert np.array_equal(z["Xb"], Xo), r
         assert z["fb"][0] == reso.fopt, r
+    # BFGS_Bnd_MPI_SW across the ranks equals the reference at np = world
+    Psw = [1e-4, 0.8, 1e-6, 1, 1e-10, 2, 50, 1e-5, 1e-6, 1e-3, 200, 1e-5, 1e-5, 0, -1]
+    Xo, reso = oracle.bfgs_bnd_mpi_sw_findmin(oracle.rosenbrock(3), [-1.0, 2.0, 2.0], [-1.0] * 3, [5.0] * 3, Psw,
+                                              world)
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        assert np.array_equal(z["Xs"], Xo), r
+        assert z["fs"][0] == reso.fopt, r

@@ -201,6 +201,40 @@ def test_bfgs_bnd_mpi_quadratic_fast_mode(ctx, oracle):
     assert abs(res.fopt - reso.fopt) <= 1e-6 * abs(reso.fopt)
 
 
+SW_P = [1e-4, 0.8, 1e-6, 1, 1e-10, 2, 50, 1e-5, 1e-6, 1e-3, 200, 1e-5, 1e-5, 0, -1]   # Examples.cpp:37
+
+
+@pytest.mark.parametrize("procs", [1, 2, 3, 4, 8])
+def test_bfgs_bnd_mpi_sw_matches_oracle(ctx, oracle, procs):
+    """BFGS_Bnd_MPI_SW (testBFGSBndMPISW, Examples.cpp:12-45) with the pools of a procs-rank run
+    (procs + 1 bracketing, procs + 2 zoom) equals the reference at np = procs: X, fOpt, evals.
+    At np = 1 the search is degenerate (it stops at x0 after two steps)."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_bfgs
+    x0, lb, ub = [-1.0, 2.0, 2.0], [-1.0] * 3, [5.0] * 3
+    X, res = run_bfgs(_obj(ctx, L.OBJ_ROSENBROCK, 3), x0, SW_P + [procs], which=4, lb=lb, ub=ub)
+    Xo, reso = oracle.bfgs_bnd_mpi_sw_findmin(oracle.rosenbrock(3), x0, lb, ub, SW_P, procs)
+    assert np.array_equal(X, Xo), (procs, X, Xo)
+    assert res.fopt == reso.fopt and res.evals == reso.evals
+    if procs > 1:
+        np.testing.assert_allclose(X, 1.0, atol=1e-3)
+
+
+@pytest.mark.parametrize("case", [
+    ("testBFGSBnd-geometry", 5, [2.0] * 5, [-5.0] * 5, [5.0] * 5),
+    ("upper-active", 3, [0.0, 0.0, 0.0], [-2.0] * 3, [0.5] * 3),
+    ("testBFGSBnd_MPI-geometry", 10, [-0.5, 3.0] + [3.0] * 8, [-1.0] + [-5.0] * 9, [5.0] * 10),
+])
+def test_bfgs_bnd_mpi_sw_box_cases(ctx, oracle, case):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_bfgs
+    name, n, x0, lb, ub = case
+    X, res = run_bfgs(_obj(ctx, L.OBJ_ROSENBROCK, n), x0, SW_P + [4], which=4, lb=lb, ub=ub)
+    Xo, reso = oracle.bfgs_bnd_mpi_sw_findmin(oracle.rosenbrock(n), x0, lb, ub, SW_P, 4)
+    assert np.array_equal(X, Xo), name
+    assert res.fopt == reso.fopt
+
+
 def test_gather_submatrix(ctx):
     """pnol_gather_submatrix_d: D[idx][idx] bitwise (BFGS_with_bnd_linsearch_MPI.cpp:832-840)."""
     import torch

@@ -167,3 +167,18 @@ def test_bfgs_bnd_mpi_oracle_properties(oracle):
         assert abs(outs[npool][1] - 4.0) < 1e-5
     X1, r1, _ = oracle.bfgs_bnd_mpi_findmin(oracle.rosenbrock(n), x0, lb, ub, Pb, 4, nprocs=1)
     assert np.array_equal(X1, outs[4][0]) and r1.fopt == outs[4][1]
+
+
+def test_bfgs_bnd_mpi_sw_oracle_properties(oracle):
+    """BFGS_Bnd_MPI_SW restatement on testBFGSBndMPISW (Examples.cpp:12-45).  No reference output
+    is recorded for it (parity unpinned beyond the shared, pinned pieces), so: at np = 1 the
+    search is degenerate and stops at x0 (SURVEY 8(a) probe), at np >= 2 it reaches the
+    Rosenbrock minimum inside the box."""
+    P = (1e-4, 0.8, 1e-6, 1, 1e-10, 2, 50, 1e-5, 1e-6, 1e-3, 200, 1e-5, 1e-5, 0, -1)
+    x0, lb, ub = [-1.0, 2.0, 2.0], [-1.0] * 3, [5.0] * 3
+    X, res = oracle.bfgs_bnd_mpi_sw_findmin(oracle.rosenbrock(3), x0, lb, ub, P, 1)
+    assert X.tolist() == x0 and res.fopt == res.f0
+    for procs in (2, 3, 4, 8):
+        X, res = oracle.bfgs_bnd_mpi_sw_findmin(oracle.rosenbrock(3), x0, lb, ub, P, procs)
+        np.testing.assert_allclose(X, 1.0, atol=1e-3)
+        assert res.fopt < 1e-6
