@@ -67,14 +67,35 @@ def pmc_traffic():
         return {}
 
 
-def fd_flop_executed(m, n, tiles, bk=16):
-    """fp64 flops the FD GEMM runs for the (start, count) point tiles: each tile continues the
-    base chain from the checkpoint at ks = 16*floor(start / 16) to k = n-1 for all its points."""
+def fd_flop_executed(m, n, tiles, bk=16, pw=32):
+    """fp64 flops the FD GEMM runs for the (start, count) point tiles: each wave's 32 points
+    continue the base chain from the checkpoint at ks = 16*floor(c0 / 16) (c0 = the wave's first
+    column) to k = n-1 (k_linres_fdP<true>, the default kernel)."""
     tot = 0
     for s0, cnt in tiles:
-        ks = (s0 // bk) * bk
-        tot += cnt * (n - ks)
+        for p0 in range(0, cnt, pw):
+            c0 = s0 + p0
+            tot += min(pw, cnt - p0) * (n - (c0 // bk) * bk)
     return 2.0 * m * tot
+
+
+def fd_flop_minimal(m, tiles, n):
+    """The flops no bitwise FD evaluation of the sequential fma chain can avoid: point j must
+    run its own chain from k = j (its first differing term) to n-1."""
+    return 2.0 * m * sum(n - j for s0, cnt in tiles for j in range(s0, s0 + cnt))
+
+
+def pmc_valu():
+    """VALU-busy fractions of the hot kernels from the newest committed PMC summary
+    (profiles/r*_pmc_fd_valu.json, tools/pmc_valu.py), or {}."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_fd_valu.json")))
+    if not files:
+        return {}
+    try:
+        return json.load(open(files[-1])).get("kernels", {})
+    except (OSError, ValueError):
+        return {}
 
 
 def bench_hg(ctx, n, reps=20):
@@ -250,11 +271,15 @@ def main():
         roofline["frac"] = roofline["achieved"] / FP64_PEAK_TFLOPS if roofline["achieved"] else None
         fd_ms = per["fd_jacobian"]
         rooflines = {
-            "fd_jacobian": {"kernel": "k_linres_fd2<4,8,KB=32> (batched FD GEMM, fp64 VALU fma, prefix-shared chains)",
+            "fd_jacobian": {"kernel": "k_linres_fdP<true> (batched FD evaluation, row per lane, fp64 VALU fma with "
+                                      "the x_k operand in SGPRs, prefix-shared chains)",
                             "bound": "valu_fp64", "ms": fd_ms,
                             "achieved": fd_flop / (fd_ms * 1e-3) / 1e12 if fd_ms else None,
                             "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "flop_executed": fd_flop,
+                            "flop_minimal": fd_flop_minimal(m, my_tiles, n),
                             "flop_nominal_full_chains": fd_flop_nominal,
+                            "valu_busy_pmc": next((v.get("valu_busy_frac") for k, v in pmc_valu().items()
+                                                   if "k_linres_fdP" in k), None),
                             "ckpt_ms": per["fd_ckpt"]},
             "jtj": dict(roofline, ms=syrk_ms),
         }

@@ -174,6 +174,7 @@ int pnol_dobj_destroy(pnol_dobj* o) {
     if (o->p0) (void)hipFree(o->p0);
     if (o->p1) (void)hipFree(o->p1);
     if (o->p2) (void)hipFree(o->p2);
+    if (o->at) (void)hipFree(o->at);
     delete o;
     return PNOL_OK;
 }

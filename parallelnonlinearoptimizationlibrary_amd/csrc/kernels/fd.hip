@@ -356,6 +356,184 @@ __global__ __launch_bounds__(256, OCC) void k_linres_fd2(const double* __restric
     }
 }
 
+// ---- row-panel k-major forms: one residual row per lane, no LDS --------------------------
+// AP holds A in 64-row panels, k-major inside a panel: AP[(rb * n + k) * 64 + r] = A[64 rb + r][k]
+// (rows past m are zero).  A wave owning a panel streams it front to back -- 512 contiguous
+// bytes per k -- and the x_k operand is wave-uniform (scalar loads, the SGPR operand of
+// v_fmac_f64), so the FD GEMM's broadcast stages are pure VALU: 32 fmas per 8-byte load.
+constexpr int kPanel = 64;
+
+__device__ __forceinline__ const double* panel_col(const double* AP, int n, int rb, int k) {
+    return AP + ((long)rb * n + k) * kPanel;
+}
+
+// A (m x n row-major) -> AP, through 64 x 64 LDS tiles (padded against bank conflicts)
+__global__ __launch_bounds__(256) void k_to_panels(const double* __restrict__ A, int m, int n, double* __restrict__ AP) {
+    __shared__ double tile[64][65];
+    const int rb = blockIdx.y, r0 = rb * 64, c0 = blockIdx.x * 64;
+    const int tc = threadIdx.x & 63, tr = threadIdx.x >> 6;
+    for (int r = tr; r < 64; r += 4) tile[r][tc] = (r0 + r < m && c0 + tc < n) ? A[(long)(r0 + r) * n + c0 + tc] : 0.0;
+    __syncthreads();
+    for (int c = tr; c < 64; c += 4)
+        if (c0 + c < n) AP[((long)rb * n + c0 + c) * kPanel + tc] = tile[tc][c];
+}
+
+// r = A x - y from AP: lane = row, the objective's fma chain over k ascending; CKPT also
+// stores the chain value before every kCkpt-th column (C[(k / kCkpt) * m + row], k > 0).
+// One wave per panel (m / 64 waves): the chain is sequential, so the stream is kept deep --
+// two 16-column blocks (16 KB per wave) in flight while one is consumed.
+template <bool CKPT>
+__global__ __launch_bounds__(64) void k_linres_evalP(const double* __restrict__ AP, const double* __restrict__ x,
+                                                     const double* __restrict__ y, int m, int n,
+                                                     double* __restrict__ F, double* __restrict__ C) {
+    const int rb = blockIdx.x, row = rb * kPanel + threadIdx.x;
+    const double* a = panel_col(AP, n, rb, 0) + threadIdx.x;
+    constexpr int U = kCkpt;
+    double acc = 0.0;
+    auto load = [&](double (&v)[U], int k) {
+        const double* ak = a + (size_t)k * kPanel;
+#pragma unroll
+        for (int q = 0; q < U; ++q) v[q] = __builtin_nontemporal_load(ak + q * kPanel);
+    };
+    auto step = [&](const double (&v)[U], int k) {
+        if (CKPT && k > 0 && row < m) C[(long)(k / kCkpt) * m + row] = acc;
+#pragma unroll
+        for (int q = 0; q < U; ++q) acc = fma(v[q], x[k + q], acc);
+    };
+    const int nb = n / U;   // full blocks
+    int k = 0;
+    if (nb > 0) {
+        double b0[U], b1[U], b2[U];
+        load(b0, 0);
+        if (nb > 1) load(b1, U);
+        int blk = 0;
+        // three-deep rotation: blocks blk+1 and blk+2 in flight while blk is consumed
+        while (blk < nb) {
+            if (blk + 2 < nb) load(b2, (blk + 2) * U);
+            step(b0, blk * U);
+            if (++blk >= nb) break;
+            if (blk + 2 < nb) load(b0, (blk + 2) * U);
+            step(b1, blk * U);
+            if (++blk >= nb) break;
+            if (blk + 2 < nb) load(b1, (blk + 2) * U);
+            step(b2, blk * U);
+            ++blk;
+        }
+        k = nb * U;
+    }
+    if (CKPT && k > 0 && k < n && row < m) C[(long)(k / kCkpt) * m + row] = acc;
+    for (; k < n; ++k) acc = fma(a[(size_t)k * kPanel], x[k], acc);
+    if (row < m && F) F[row] = y ? acc - y[row] : acc;
+}
+
+// FD GEMM from AP.  Workgroup = 4 waves on the same 64-row panel (one row per lane), wave w
+// owning points [32w, 32w + 32) of the tile and starting from the base-chain checkpoint at
+// the tile's first column (WAVE_KS: at its own first column).  Per k a lane does 32 fmas:
+// x_k for every point except the one whose column is k, which gets x_k + h_k
+// (XdX[j] = X[j] + dX[j]).  The next 8 k of the panel are in flight while the current 8 are
+// consumed.  Bit-identical to the host evaluation, like k_linres_fd2.
+constexpr int kPW = 32;   // points per wave
+
+template <bool WAVE_KS>
+__global__ __launch_bounds__(256) void k_linres_fdP(const double* __restrict__ AP, const double* __restrict__ y,
+                                                    const double* __restrict__ x, const double* __restrict__ h, int m,
+                                                    int n, const FdTiles tl, const double* __restrict__ F0,
+                                                    const double* __restrict__ C, double* __restrict__ JT, long ldjt) {
+    // Longest work first: the host sorts the tiles by first column (the chains of tile t run
+    // k = ks_t .. n-1), and blockIdx walks all panels of tile 0, then of tile 1, ..., so the
+    // short tiles fill the tail.  Panel mt lands on XCD mt % 8 for every tile (L2 reuse).
+    const int nmt = (m + kPanel - 1) / kPanel;
+    const int nt = blockIdx.x / nmt, mt = blockIdx.x % nmt;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int j0 = tl.start[nt], cnt = tl.count[nt];
+    const int pw0 = w * kPW;
+    if (pw0 >= cnt) return;                 // wave-uniform; the kernel has no barriers
+    const int np = min(kPW, cnt - pw0);
+    const int c0 = j0 + pw0;                // first column of this wave
+    const int ks = WAVE_KS ? (c0 / kBK) * kBK : (j0 / kBK) * kBK;
+    const int row = mt * kPanel + lane, rowc = min(row, m - 1);
+    const double* a = panel_col(AP, n, mt, 0) + lane;
+
+    double acc[kPW];
+    {
+        const double c = ks > 0 ? C[(long)(ks / kCkpt) * m + rowc] : 0.0;
+#pragma unroll
+        for (int j = 0; j < kPW; ++j) acc[j] = c;
+    }
+    // k in [kb, ke): every point multiplies by x_k; blocks of 8, ping-pong prefetch of the
+    // next block (no register copies)
+    auto step8 = [&](const double (&av)[8], int k) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const double xk = x[k + q];
+#pragma unroll
+            for (int j = 0; j < kPW; ++j) acc[j] = fma(av[q], xk, acc[j]);
+        }
+    };
+    auto load8 = [&](double (&av)[8], int k) {
+        const double* ak = a + (size_t)k * kPanel;   // one address, immediate offsets q * 512 B
+#pragma unroll
+        for (int q = 0; q < 8; ++q) av[q] = ak[q * kPanel];
+    };
+    auto bcast = [&](int kb, int ke) {
+        int k = kb;
+        if (k + 8 <= ke) {
+            double p0[8], p1[8];
+            load8(p0, k);
+            while (true) {
+                if (k + 16 > ke) { step8(p0, k); k += 8; break; }
+                load8(p1, k + 8);
+                step8(p0, k);
+                k += 8;
+                if (k + 16 > ke) { step8(p1, k); k += 8; break; }
+                load8(p0, k + 8);
+                step8(p1, k);
+                k += 8;
+            }
+        }
+        for (; k < ke; ++k) {
+            const double av = a[(long)k * kPanel], xk = x[k];
+#pragma unroll
+            for (int j = 0; j < kPW; ++j) acc[j] = fma(av, xk, acc[j]);
+        }
+    };
+    bcast(ks, c0);
+    // the window: point kk is perturbed at k = c0 + kk
+    const int klen = min(kPW, n - c0);
+    if (klen == kPW) {
+#pragma unroll
+        for (int q0 = 0; q0 < kPW; q0 += 8) {
+            double av[8];
+            load8(av, c0 + q0);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int kk = q0 + q;
+                const double xk = x[c0 + kk], xp = xk + h[c0 + kk];
+#pragma unroll
+                for (int j = 0; j < kPW; ++j) acc[j] = fma(av[q], j == kk ? xp : xk, acc[j]);
+            }
+        }
+    } else {
+        for (int kk = 0; kk < klen; ++kk) {
+            const double av = a[(long)(c0 + kk) * kPanel];
+            const double xk = x[c0 + kk], xp = xk + h[c0 + kk];
+#pragma unroll
+            for (int j = 0; j < kPW; ++j) acc[j] = fma(av, j == kk ? xp : xk, acc[j]);
+        }
+    }
+    bcast(c0 + klen, n);
+    // epilogue: F = acc - y; J = (F - F0) / h
+    if (row < m) {
+        const double yr = y[row], f0 = F0[row];
+#pragma unroll
+        for (int j = 0; j < kPW; ++j)
+            if (j < np) {
+                const int col = c0 + j;
+                JT[(long)(col - tl.jbase) * ldjt + row] = ((acc[j] - yr) - f0) / h[col];
+            }
+    }
+}
+
 // ---- synthetic data, splitmix64 counter stream ---------------------------
 __global__ void k_synth_quadratic(unsigned long long seed, int n, double bscale, double* d, double* b) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -405,7 +583,10 @@ int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out) 
             return launch_check();
         case PNOL_OBJ_LINRES: {
             ScopedTimer tm(ctx, "linres_eval");
-            if (o->n % 2 == 0)
+            if (o->at)
+                hipLaunchKernelGGL((k_linres_evalP<false>), dim3((o->m + kPanel - 1) / kPanel), dim3(64), 0, ctx->stream,
+                                   (const double*)o->at, x, o->p1, o->m, o->n, out, (double*)nullptr);
+            else if (o->n % 2 == 0)
                 hipLaunchKernelGGL((k_linres_eval<true, false>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0, ctx->stream,
                                    o->p0, x, o->p1, o->m, o->n, out, (double*)nullptr);
             else
@@ -416,6 +597,16 @@ int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out) 
         default:
             return PNOL_ERR_UNSUPPORTED;
     }
+}
+
+// The row-panel k-major copy of a linear residual's A (objective data never changes after creation).
+static int ensure_panels(pnol_ctx* ctx, pnol_dobj* o) {
+    if (o->at) return PNOL_OK;
+    const int nrb = (o->m + kPanel - 1) / kPanel;
+    PNOL_HIP(hipMalloc(&o->at, sizeof(double) * (size_t)nrb * kPanel * o->n));
+    hipLaunchKernelGGL(k_to_panels, dim3((o->n + 63) / 64, nrb), dim3(256), 0, ctx->stream, (const double*)o->p0, o->m,
+                       o->n, o->at);
+    return launch_check();
 }
 
 int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt, double* f0,
@@ -462,12 +653,27 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
                                               JT + (size_t)(start[t] - jbase) * ldjt, ldjt));
         return PNOL_OK;
     }
+    // PNOL_FD_KERNEL selects the FD GEMM (tuning; all variants are bitwise equal):
+    // 2 = x-broadcast 128 x 128 tiles (8 x 8 per thread), 3 = 64 x 128 (4 x 8) with 16-deep K
+    // stages, 4 = 64 x 128 with 32-deep K stages, 5 = lane-per-row form on the row-panel copy
+    // of A (tile-aligned starts), 6 (default) = the same with per-wave starts.
+    static const int fdk = [] {
+        const char* e = std::getenv("PNOL_FD_KERNEL");
+        const int v = e ? std::atoi(e) : 6;
+        return (v >= 2 && v <= 6) ? v : 6;
+    }();
+    const bool kmajor = fdk >= 5;
+    if (kmajor) PNOL_CHECK(ensure_panels(ctx, o));
     // one pass of the base chain: F0 (when asked) and the prefix checkpoints
     void* C = nullptr;
     const int ncp = (o->n + kCkpt - 1) / kCkpt;
     PNOL_CHECK(ws_get(ctx, "linres_ckpt", sizeof(double) * (size_t)o->m * (ncp > 1 ? ncp : 1), &C));
     double* f0_out = compute_f0 ? F0 : nullptr;
-    if (ckpt) {
+    if (ckpt && kmajor) {
+        ScopedTimer tm(ctx, "fd_ckpt");
+        hipLaunchKernelGGL((k_linres_evalP<true>), dim3((o->m + kPanel - 1) / kPanel), dim3(64), 0, ctx->stream, (const double*)o->at,
+                           x, o->p1, o->m, o->n, f0_out, (double*)C);
+    } else if (ckpt) {
         ScopedTimer tm(ctx, "fd_ckpt");
         if ((o->n % 2) == 0)
             hipLaunchKernelGGL((k_linres_eval<true, true>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0,
@@ -477,27 +683,29 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
                                ctx->stream, o->p0, x, o->p1, o->m, o->n, f0_out, (double*)C);
     }
     if (ckpt) PNOL_CHECK(launch_check());
-    // PNOL_FD_KERNEL selects the FD GEMM (tuning; all variants are bitwise equal):
-    // 2 = x-broadcast 128 x 128 tiles (8 x 8 per thread), 3 = 64 x 128 (4 x 8) with 16-deep K
-    // stages, 4 (default) = 64 x 128 with 32-deep K stages.
-    static const int fdk = [] {
-        const char* e = std::getenv("PNOL_FD_KERNEL");
-        const int v = e ? std::atoi(e) : 4;
-        return (v >= 2 && v <= 4) ? v : 4;
-    }();
     const bool even = (o->n % 2) == 0;
     ScopedTimer tm(ctx, "fd_jacobian");
     const double* Cc = (const double*)C;
+    // tiles in order of first column (longest chains first; outputs go by column)
+    std::vector<int> ord(ntiles);
+    for (int t = 0; t < ntiles; ++t) ord[t] = t;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return start[a] < start[b]; });
     for (int t0 = 0; t0 < ntiles; t0 += kFdMaxTiles) {
         FdTiles tl;
         tl.ntiles = std::min(kFdMaxTiles, ntiles - t0);
         tl.jbase = jbase;
         for (int t = 0; t < tl.ntiles; ++t) {
-            tl.start[t] = start[t0 + t];
-            tl.count[t] = count[t0 + t];
+            tl.start[t] = start[ord[t0 + t]];
+            tl.count[t] = count[ord[t0 + t]];
         }
         const dim3 g1(((o->m + 127) / 128) * tl.ntiles), g2(((o->m + 63) / 64) * tl.ntiles);
-        if (fdk == 2) {
+        if (fdk == 5) {
+            hipLaunchKernelGGL((k_linres_fdP<false>), g2, dim3(256), 0, ctx->stream, (const double*)o->at, o->p1, x, h,
+                               o->m, o->n, tl, F0, Cc, JT, (long)ldjt);
+        } else if (fdk == 6) {
+            hipLaunchKernelGGL((k_linres_fdP<true>), g2, dim3(256), 0, ctx->stream, (const double*)o->at, o->p1, x, h,
+                               o->m, o->n, tl, F0, Cc, JT, (long)ldjt);
+        } else if (fdk == 2) {
             if (even)
                 hipLaunchKernelGGL((k_linres_fd2<true, 8, 8>), g1, dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
                                    o->n, tl, F0, Cc, JT, (long)ldjt);

@@ -61,6 +61,7 @@ struct pnol_dobj {
     double* p0 = nullptr;     // device data (see pnol_dobj_kind)
     double* p1 = nullptr;
     double* p2 = nullptr;     // derived device data (e.g. pow(xData,3) for the cubic)
+    double* at = nullptr;     // LINRES: A in 64-row k-major panels (fd.hip), built on first FD use
     size_t len0 = 0, len1 = 0;
     pnol_ctx* ctx = nullptr;
 };

@@ -41,4 +41,10 @@ if [ "${PMC:-0}" = "1" ]; then
       python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_write.log 2>&1
   rc=$?; echo "pmc write rc=$rc"; [ "$rc" -eq 0 ] || exit $rc
 fi
+if [ "${VALU:-0}" = "1" ]; then
+  timeout -k 10 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
+      SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_valu -o pmc --output-format csv -- \
+      python3 tools/fd_only.py 4 > gpurun_out/pmc_valu.log 2>&1
+  rc=$?; echo "pmc valu rc=$rc"; [ "$rc" -eq 0 ] || exit $rc
+fi
 exit 0

@@ -25,9 +25,11 @@ ctx.synchronize()
 L.check(L.lib().pnol_ctx_enable_timers(ctx.h, 1), "t"); L.check(L.lib().pnol_ctx_reset_timers(ctx.h), "t")
 for _ in range(5):
     obj.fd_jacobian(x, h, 0, n, JT=JT, F0=F0)
+for _ in range(5):
+    obj.eval(x)
 ctx.synchronize()
 out = {}
-for k in ("fd_jacobian", "fd_ckpt"):
+for k in ("fd_jacobian", "fd_ckpt", "linres_eval"):
     ms, c = C.c_double(), C.c_int()
     L.lib().pnol_ctx_timer(ctx.h, k.encode(), C.byref(ms), C.byref(c))
     out[k] = ms.value / max(c.value, 1)
