@@ -60,6 +60,16 @@ int pnol_ctx_timer(pnol_ctx* ctx, const char* name, double* total_ms, int* count
 int pnol_malloc(pnol_ctx* ctx, size_t bytes, void** dptr);
 int pnol_free(pnol_ctx* ctx, void* dptr);
 int pnol_memcpy_h2d(pnol_ctx* ctx, void* dst, const void* src, size_t bytes);  /* synchronous */
+/* Pinned host memory, and a device-to-host copy into it queued on the context stream (no
+ * wait); completion is observed through an event recorded after it. */
+int pnol_host_alloc(void** p, size_t bytes);
+int pnol_host_free(void* p);
+int pnol_memcpy_d2h_async(pnol_ctx* ctx, void* dst_pinned, const void* src, size_t bytes);
+typedef struct pnol_event pnol_event;
+int pnol_event_create(pnol_ctx* ctx, pnol_event** ev);
+int pnol_event_record(pnol_ctx* ctx, pnol_event* ev);   /* after everything queued so far */
+int pnol_event_wait(pnol_event* ev);                    /* host waits (busy-poll) */
+int pnol_event_destroy(pnol_event* ev);
 int pnol_memcpy_d2h(pnol_ctx* ctx, void* dst, const void* src, size_t bytes);  /* synchronous */
 
 /* ---- BFGS dense inverse Hessian ------------------------------------------------------ */
@@ -120,6 +130,13 @@ int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const do
  * or -1 on a singular matrix. */
 int pnol_solve_d(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n,
                  int method, int* info);
+/* The method-4 Cholesky solve queued without any host wait: *dinfo (a device int) ends 0 on
+ * success, nonzero when a pivot was not positive (sigma is then undefined and the caller
+ * falls back to pnol_solve_d with method 2; A is left intact).  Lets the LM loop keep the
+ * device busy while the host checks the previous trial point. */
+int pnol_solve_async_d(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo);
+/* z = x + y (the LM trial point X + sigma on the device: the same IEEE add as the host's) */
+int pnol_add_d(pnol_ctx* ctx, const double* x, const double* y, double* z, int n);
 
 /* ---- device objectives and the batched finite-difference engine ---------------------- */
 enum pnol_dobj_kind {
@@ -141,12 +158,19 @@ int pnol_dobj_destroy(pnol_dobj* obj);
 int pnol_dobj_info(pnol_dobj* obj, int* kind, int* n, int* m);
 /* f = objEval(x) (scalar kinds, out[0]) or F = objEval(x) (residual kinds, out[0..m)) */
 int pnol_dobj_eval_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, double* out);
+/* f = objEval(x) as pnol_dobj_eval_d; for a linear residual the base chain's prefix
+ * checkpoints of x are kept in the context, so the next pnol_fd_jtj_d / pnol_fd_jacobian_tiles_d
+ * on the same (obj, x) with compute_f0 = 2 (F0 = this out) skips its base-chain pass
+ * (LevenbergMarquardt.cpp:95 trial point -> :55 Jacobian point after an accepted step). */
+int pnol_dobj_eval_ckpt_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, double* out);
 /* Forward differences, Objective::gradientApproximation (PNOL_Objective.cpp:12-34):
  * f0 = f(x); g_i = (f(x + h_i e_i) - f0) / h_i for i in [i0, i0 + cnt).  g gets cnt values. */
 int pnol_fd_gradient_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, int i0, int cnt,
                        double* f0, double* g);
 /* MultiObjective::gradientApproximation (PNOL_Objective.cpp:165-197) for columns [j0, j0+cnt):
- * F0 = F(x) (computed here when compute_f0, else read), JT row (j - j0) = (F(x + h_j e_j) - F0)/h_j. */
+ * F0 = F(x) (computed here when compute_f0, else read), JT row (j - j0) = (F(x + h_j e_j) - F0)/h_j.
+ * compute_f0 = 2 (pnol_fd_jtj_d / pnol_fd_jacobian_tiles_d): F0 was filled by
+ * pnol_dobj_eval_ckpt_d(ctx, obj, x, F0) and x is unchanged since. */
 int pnol_fd_jacobian_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, int j0, int cnt,
                        double* F0, int compute_f0, double* JT, int ldjt);
 /* One LevMarq Jacobian + normal matrix, pipelined (LevenbergMarquardt.cpp:55-73): the FD

@@ -59,6 +59,13 @@ _SIGS = {
     "pnol_free": (_i, [_vp, _vp]),
     "pnol_memcpy_h2d": (_i, [_vp, _vp, _vp, _sz]),
     "pnol_memcpy_d2h": (_i, [_vp, _vp, _vp, _sz]),
+    "pnol_host_alloc": (_i, [C.POINTER(_vp), _sz]),
+    "pnol_host_free": (_i, [_vp]),
+    "pnol_memcpy_d2h_async": (_i, [_vp, _vp, _vp, _sz]),
+    "pnol_event_create": (_i, [_vp, C.POINTER(_vp)]),
+    "pnol_event_record": (_i, [_vp, _vp]),
+    "pnol_event_wait": (_i, [_vp]),
+    "pnol_event_destroy": (_i, [_vp]),
     "pnol_hg_d": (_i, [_vp, _vp, _i, _vp, _vp, _i]),
     "pnol_gemv_neg_d": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
     "pnol_bfgs_update_exact_d": (_i, [_vp, _vp, _i, _vp, _vp, _i]),
@@ -69,11 +76,14 @@ _SIGS = {
     "pnol_jtj_mpi_d": (_i, [_vp, _vp, _i, _i, _i, _d, _vp, _i, _vp]),
     "pnol_jtr_d": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
     "pnol_solve_d": (_i, [_vp, _vp, _i, _vp, _vp, _i, _i, C.POINTER(_i)]),
+    "pnol_solve_async_d": (_i, [_vp, _vp, _i, _vp, _vp, _i, _vp]),
+    "pnol_add_d": (_i, [_vp, _vp, _vp, _vp, _i]),
     "pnol_dobj_create": (_i, [_vp, _i, _i, _i, _dp, _sz, _dp, _sz, _d, C.POINTER(_vp)]),
     "pnol_dobj_create_synthetic": (_i, [_vp, _i, _i, _i, C.c_ulonglong, _d, _dp, C.POINTER(_vp)]),
     "pnol_dobj_destroy": (_i, [_vp]),
     "pnol_dobj_info": (_i, [_vp, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i)]),
     "pnol_dobj_eval_d": (_i, [_vp, _vp, _vp, _vp]),
+    "pnol_dobj_eval_ckpt_d": (_i, [_vp, _vp, _vp, _vp]),
     "pnol_fd_gradient_d": (_i, [_vp, _vp, _vp, _vp, _i, _i, _vp, _vp]),
     "pnol_fd_jacobian_d": (_i, [_vp, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _i]),
     "pnol_fd_jtj_d": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp, _i, _d, _vp, _i, _vp, _i]),

@@ -50,6 +50,18 @@ int pnol_set_identity_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* 
     return launch_set_identity(ctx, D, ldd, n, scale);
 }
 
+int pnol_add_d(pnol_ctx* ctx, const double* x, const double* y, double* z, int n) {
+    PNOL_CHECK(set_device(ctx));
+    return launch_add(ctx, x, y, z, n);
+}
+
+int pnol_solve_async_d(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo) {
+    PNOL_CHECK(set_device(ctx));
+    if (!A || !rhs || !sigma || !dinfo || n <= 0 || lda < n) return PNOL_ERR_ARG;
+    ScopedTimer tm(ctx, "solve");
+    return launch_chol_solve(ctx, A, lda, rhs, sigma, n, dinfo);
+}
+
 int pnol_gather_submatrix_d(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub,
                             double* Dsub, int lds) {
     PNOL_CHECK(set_device(ctx));
@@ -192,6 +204,11 @@ int pnol_dobj_eval_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, double* out
     return launch_dobj_eval(ctx, obj, x, out);
 }
 
+int pnol_dobj_eval_ckpt_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, double* out) {
+    PNOL_CHECK(set_device(ctx));
+    return launch_dobj_eval_ckpt(ctx, obj, x, out);
+}
+
 int pnol_fd_gradient_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, int i0, int cnt,
                        double* f0, double* g) {
     PNOL_CHECK(set_device(ctx));
@@ -209,13 +226,14 @@ int pnol_fd_jtj_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* 
                   double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, int nchunks) {
     PNOL_CHECK(set_device(ctx));
     if (!obj || !x || !h || !F0 || !JT || !A || ldjt < obj->m || lda < obj->n) return PNOL_ERR_ARG;
+    if (compute_f0 < 0 || compute_f0 > 2) return PNOL_ERR_ARG;
     return launch_fd_jtj(ctx, obj, x, h, F0, compute_f0, JT, ldjt, lambda, A, lda, jtj_diag, nchunks);
 }
 
 int pnol_fd_jacobian_tiles_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, const int* start,
                              const int* count, int ntiles, double* F0, int compute_f0, double* JT, int ldjt) {
     PNOL_CHECK(set_device(ctx));
-    if (ntiles < 0 || (ntiles > 0 && (!start || !count))) return PNOL_ERR_ARG;
+    if (ntiles < 0 || (ntiles > 0 && (!start || !count)) || compute_f0 < 0 || compute_f0 > 2) return PNOL_ERR_ARG;
     return launch_fd_jacobian_tiles(ctx, obj, x, h, start, count, ntiles, F0, compute_f0, JT, 0, ldjt);
 }
 

@@ -53,6 +53,7 @@ class LMDevice {
         if (same(X, xh_)) return;
         x_.upload(X);
         xh_ = X;
+        ckpt_valid_ = false;
     }
     void uploadH(const std::vector<double>& dX) {
         if (same(dX, hh_)) return;
@@ -64,7 +65,9 @@ class LMDevice {
     void evalResiduals(MultiObjective* obj, std::vector<double>& X, std::vector<double>& F) {
         if (pnol_dobj* d = obj->deviceObjective()) {
             uploadX(X);
-            check(pnol_dobj_eval_d(ctx_, d, x_.get(), F_.get()), "objective eval");
+            // also keeps the base chain's checkpoints of x for the Jacobian of an accepted step
+            check(pnol_dobj_eval_ckpt_d(ctx_, d, x_.get(), F_.get()), "objective eval");
+            ckpt_valid_ = true;
             F_.download(F);
             obj->countEvals(1);
         } else {
@@ -118,8 +121,10 @@ class LMDevice {
         }();
         uploadX(X);
         uploadH(dX);
-        check(pnol_fd_jtj_d(ctx_, d, x_.get(), h_.get(), F0_.get(), 1, JT_.get(), ldjt_, lambda, A_.get(), lda_,
-                            nullptr, chunks),
+        // x_ still holds the point F_ was evaluated at: reuse F_ and its checkpoints
+        const bool reuse = ckpt_valid_;
+        check(pnol_fd_jtj_d(ctx_, d, x_.get(), h_.get(), reuse ? F_.get() : F0_.get(), reuse ? 2 : 1, JT_.get(),
+                            ldjt_, lambda, A_.get(), lda_, nullptr, chunks),
               "fd_jtj");
         obj->countEvals(n_ + 1);
         return true;
@@ -140,15 +145,165 @@ class LMDevice {
         sigma_.download(sigma);
     }
 
-    void saveF() { std::swap(F_, Fprev_); }      // Fprev <- F (the next eval overwrites F_)
-    void restoreF() { std::swap(F_, Fprev_); }
+    void saveF() { std::swap(F_, Fprev_); ckpt_valid_ = false; }   // Fprev <- F (the next eval overwrites F_)
+    void restoreF() { std::swap(F_, Fprev_); ckpt_valid_ = false; }
 
   private:
     pnol_ctx* ctx_;
     int n_, m_, ldjt_, lda_;
     DevVec JT_, A_, rhs_, sigma_, x_, h_, F_, Fprev_, F0_;
     std::vector<double> xh_, hh_;   // host images of x_ and h_
+    bool ckpt_valid_ = false;       // F_ = F(x_) and the context's checkpoints are x_'s
 };
+
+// The single-process LM loop on a device objective with one host wait per trip
+// (n > PNOL_SEQ_MAX; PNOL_LM_ASYNC=0 selects the general loop below).  A trip is queued whole
+// on the context stream: FD Jacobian + A at x_i, -J^T F_i, the Cholesky solve (no status
+// readback in between), x_{i+1} = x_i + sigma_i and F(x_{i+1}) with its checkpoints on the
+// device, then sigma_i, F(x_{i+1}) and the solve status into pinned memory behind one event.
+// The host then replays the reference's decision (LevenbergMarquardt.cpp:87-160).  A
+// non-positive Cholesky pivot is redone with the reference-order LU, as pnol_solve_d does.
+// (Queueing trip i+1 before deciding step i was measured: a rejected step then costs a whole
+// wasted trip, and the post-convergence steps of the bench are mostly rejections.)
+class LMAsync {
+  public:
+    LMAsync(pnol_ctx* ctx, pnol_dobj* d, int n, int m) : ctx_(ctx), d_(d), n_(n), m_(m), ldjt_(even_ld(m)),
+                                                          lda_(even_ld(n)) {
+        JT_.reset(ctx, (size_t)n * ldjt_);
+        A_.reset(ctx, (size_t)n * lda_);
+        rhs_.reset(ctx, n);
+        h_.reset(ctx, n);
+        for (int s = 0; s < 2; ++s) {
+            x_[s].reset(ctx, n);
+            F_[s].reset(ctx, m);
+            sig_[s].reset(ctx, n);
+            info_[s].reset(ctx, 1);
+            check(pnol_host_alloc(&pin_[s], sizeof(double) * ((size_t)n + m + 1)), "host_alloc");
+            check(pnol_event_create(ctx, &ev_[s]), "event_create");
+        }
+    }
+    ~LMAsync() {
+        (void)pnol_ctx_synchronize(ctx_);
+        for (int s = 0; s < 2; ++s) {
+            (void)pnol_host_free(pin_[s]);
+            (void)pnol_event_destroy(ev_[s]);
+        }
+    }
+    double* x(int s) { return x_[s].get(); }
+    double* F(int s) { return F_[s].get(); }
+    const double* sigma_h(int s) const { return static_cast<const double*>(pin_[s]); }
+    const double* Fnext_h(int s) const { return static_cast<const double*>(pin_[s]) + n_; }
+    int info_h(int s) const { return *reinterpret_cast<const int*>(static_cast<const double*>(pin_[s]) + n_ + m_); }
+    void uploadH(const std::vector<double>& dX) { h_.upload(dX); }
+
+    // trip at x_[s] (F_[s] = F(x_[s]); ckpt: its checkpoints are current) -> sigma, x_[s^1], F_[s^1]
+    void enqueue(int s, double lambda, bool ckpt) {
+        check(pnol_fd_jtj_d(ctx_, d_, x_[s].get(), h_.get(), F_[s].get(), ckpt ? 2 : 1, JT_.get(), ldjt_, lambda,
+                            A_.get(), lda_, nullptr, 1),
+              "fd_jtj");
+        check(pnol_jtr_d(ctx_, JT_.get(), ldjt_, m_, n_, F_[s].get(), rhs_.get()), "jtr");
+        int* di = reinterpret_cast<int*>(info_[s].get());
+        check(pnol_solve_async_d(ctx_, A_.get(), lda_, rhs_.get(), sig_[s].get(), n_, di), "solve");
+        finish(s);
+    }
+    // the rest of a trip once sigma_[s] is known: trial point, its residuals, copies back
+    void finish(int s) {
+        check(pnol_add_d(ctx_, x_[s].get(), sig_[s].get(), x_[s ^ 1].get(), n_), "add");
+        check(pnol_dobj_eval_ckpt_d(ctx_, d_, x_[s ^ 1].get(), F_[s ^ 1].get()), "objective eval");
+        double* pin = static_cast<double*>(pin_[s]);
+        check(pnol_memcpy_d2h_async(ctx_, pin, sig_[s].get(), sizeof(double) * n_), "d2h");
+        check(pnol_memcpy_d2h_async(ctx_, pin + n_, F_[s ^ 1].get(), sizeof(double) * m_), "d2h");
+        check(pnol_memcpy_d2h_async(ctx_, pin + n_ + m_, info_[s].get(), sizeof(int)), "d2h");
+        check(pnol_event_record(ctx_, ev_[s]), "event");
+    }
+    void wait(int s) { check(pnol_event_wait(ev_[s]), "event wait"); }
+    // the reference-order LU for a trip whose Cholesky reported a non-positive pivot (A intact)
+    void redo_lu(int s) {
+        check(pnol_ctx_synchronize(ctx_), "sync");
+        int info = 0;
+        check(pnol_solve_d(ctx_, A_.get(), lda_, rhs_.get(), sig_[s].get(), n_, 2, &info), "solve");
+        finish(s);
+        wait(s);
+    }
+
+  private:
+    pnol_ctx* ctx_;
+    pnol_dobj* d_;
+    int n_, m_, ldjt_, lda_;
+    DevVec JT_, A_, rhs_, h_, x_[2], F_[2], sig_[2], info_[2];
+    void* pin_[2] = {nullptr, nullptr};
+    pnol_event* ev_[2] = {nullptr, nullptr};
+};
+
+bool lm_async_enabled() {
+    const char* e = std::getenv("PNOL_LM_ASYNC");   // read per solve (tests compare both loops)
+    return !e || std::atoi(e) != 0;
+}
+
+void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, std::vector<double>& X,
+                    std::vector<double>& F0, std::vector<double>& FOpt) {
+    const int n = (int)X.size();
+    const int m = (int)F0.size();
+    pnol_ctx* ctx = require_ctx();
+    LMAsync dev(ctx, d, n, m);
+    double lambda = P.lambda0;
+    std::vector<double> dX(n, P.dXGrad), F(m), Fnew(m), sigma(n);
+    dev.uploadH(dX);
+    int s = 0;
+    check(pnol_memcpy_h2d(ctx, dev.x(s), X.data(), sizeof(double) * n), "h2d");
+    check(pnol_dobj_eval_ckpt_d(ctx, d, dev.x(s), dev.F(s)), "objective eval");
+    check(pnol_memcpy_d2h(ctx, F0.data(), dev.F(s), sizeof(double) * m), "d2h");
+    obj->countEvals(1);
+    F = F0;
+    double nrm = norm2(F);
+    double chiSq = nrm * nrm;
+    int iter = 0;
+    double xdiff2Norm = P.xMinDiff * 2;
+    bool ckpt = true;   // the checkpoints in the context are those of x_[s]
+    while (iter < P.maxIter) {
+        dev.enqueue(s, lambda, ckpt);
+        dev.wait(s);
+        if (dev.info_h(s) != 0) dev.redo_lu(s);
+        obj->countEvals(n + 1);        // the trip's Jacobian
+        obj->countEvals(1);            // its trial point
+        std::memcpy(sigma.data(), dev.sigma_h(s), sizeof(double) * n);
+        std::memcpy(Fnew.data(), dev.Fnext_h(s), sizeof(double) * m);
+        const double chiSqPrev = chiSq;
+        nrm = norm2(Fnew);
+        chiSq = nrm * nrm;
+        if (chiSq >= chiSqPrev || chiSq != chiSq) {
+            if (P.verbose > 1)
+                std::cout << "Step " << iter << " failed with chiSq = " << chiSq << ", chiSqPrev = " << chiSqPrev
+                          << ",  increasing lambda: " << lambda << " --> " << lambda * P.lambdaFactor << std::endl;
+            chiSq = chiSqPrev;
+            lambda = lambda * P.lambdaFactor;
+            ckpt = false;              // x_[s], F_[s] stand; the trial point's eval took the checkpoints
+        } else {
+            lambda = lambda / P.lambdaFactor;
+            for (int i = 0; i < n; ++i) X[i] = X[i] + sigma[i];   // == x_[s^1] (same IEEE add)
+            F = Fnew;
+            s ^= 1;
+            ckpt = true;
+            xdiff2Norm = norm2(sigma);
+            if (xdiff2Norm < P.xMinDiff) break;
+        }
+        if (P.verbose > 0 && iter % 10 == 0) {
+            std::cout << "At iter = " << iter << " the xdiff 2Norm = " << xdiff2Norm << ", chi^2 = " << chiSq
+                      << ", and params: ";
+            print_vec(X);
+        }
+        iter++;
+    }
+    FOpt = F;
+    if (P.verbose >= 0) {
+        std::cout << std::endl << "-----------------------------------------------------------------------------------" << std::endl;
+        std::cout << "Completed Levenberg Marquardt." << std::endl;
+        std::cout << "At iter = " << iter << " the xdiff 2Norm = " << xdiff2Norm << ", chi^2 = " << chiSq
+                  << ", and  optimal params: " << std::endl;
+        print_vec(X);
+        std::cout << "-----------------------------------------------------------------------------------" << std::endl << std::endl;
+    }
+}
 
 void lm_solve(MultiObjective* obj, const LMParams& P, bool sharded, std::vector<double>& X, std::vector<double>& F0,
               std::vector<double>& FOpt) {
@@ -156,6 +311,8 @@ void lm_solve(MultiObjective* obj, const LMParams& P, bool sharded, std::vector<
     const int m = (int)F0.size();
     const int rank = sharded ? comm_rank() : 0;
     const bool loud = rank == ROOT_ID;
+    if (!sharded && n > PNOL_SEQ_MAX && lm_async_enabled())
+        if (pnol_dobj* d = obj->deviceObjective()) return lm_solve_async(obj, d, P, X, F0, FOpt);
     pnol_ctx* ctx = require_ctx();
     LMDevice dev(ctx, n, m, sharded ? comm_size() : 1);
 

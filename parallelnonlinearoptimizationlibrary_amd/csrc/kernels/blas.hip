@@ -506,6 +506,11 @@ __global__ void k_gather_sub(const double* __restrict__ D, long ldd, const int* 
     }
 }
 
+// z = x + y (the LM trial point X + sigma, the same IEEE add as the host's)
+__global__ void k_add(const double* __restrict__ x, const double* __restrict__ y, double* __restrict__ z, int n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) z[i] = x[i] + y[i];
+}
+
 __global__ void k_fill(double* __restrict__ p, size_t count, double value) {
     for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < count; k += (size_t)gridDim.x * blockDim.x)
         p[k] = value;
@@ -638,6 +643,13 @@ int launch_gather_sub(pnol_ctx* ctx, const double* D, int ldd, int n, const int*
     if (nsub == 0) return PNOL_OK;
     hipLaunchKernelGGL(k_gather_sub, dim3(std::min(nsub, 8192)), dim3(256), 0, ctx->stream, D, (long)ldd, idx, nsub,
                        Dsub, (long)lds);
+    return launch_check();
+}
+
+int launch_add(pnol_ctx* ctx, const double* x, const double* y, double* z, int n) {
+    if (!x || !y || !z || n < 0) return PNOL_ERR_ARG;
+    if (n == 0) return PNOL_OK;
+    hipLaunchKernelGGL(k_add, dim3(std::min((n + 255) / 256, 1024)), dim3(256), 0, ctx->stream, x, y, z, n);
     return launch_check();
 }
 

@@ -609,6 +609,27 @@ static int ensure_panels(pnol_ctx* ctx, pnol_dobj* o) {
     return launch_check();
 }
 
+// F = F(x), and for a linear residual also the prefix checkpoints of x, kept in the context
+// for the next FD call on (o, x) with compute_f0 == 2 (the LM trial point becomes the next
+// Jacobian point when the step is accepted).
+int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out) {
+    if (!o || !x || !out) return PNOL_ERR_ARG;
+    if (o->kind != PNOL_OBJ_LINRES) return launch_dobj_eval(ctx, o, x, out);
+    PNOL_CHECK(ensure_panels(ctx, o));
+    void* C = nullptr;
+    const int ncp = (o->n + kCkpt - 1) / kCkpt;
+    PNOL_CHECK(ws_get(ctx, "linres_ckpt", sizeof(double) * (size_t)o->m * (ncp > 1 ? ncp : 1), &C));
+    {
+        ScopedTimer tm(ctx, "linres_eval");
+        hipLaunchKernelGGL((k_linres_evalP<true>), dim3((o->m + kPanel - 1) / kPanel), dim3(64), 0, ctx->stream,
+                           (const double*)o->at, x, o->p1, o->m, o->n, out, (double*)C);
+    }
+    ctx->ckpt_obj = o;
+    ctx->ckpt_x = x;
+    return launch_check();
+}
+
+
 int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt, double* f0,
                        double* g) {
     if (!o || !x || !h || !is_scalar_kind(o->kind)) return PNOL_ERR_ARG;
@@ -646,7 +667,7 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
     for (int t = 0; t < ntiles; ++t) total += count[t];
     if (total > 0 && !JT) return PNOL_ERR_ARG;
     if (o->kind != PNOL_OBJ_LINRES || total == 0) {
-        if (compute_f0) PNOL_CHECK(launch_dobj_eval(ctx, o, x, F0));
+        if (compute_f0 == 1) PNOL_CHECK(launch_dobj_eval(ctx, o, x, F0));
         for (int t = 0; t < ntiles; ++t)
             if (count[t] > 0)
                 PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, start[t], count[t], F0, 0,
@@ -664,11 +685,18 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
     }();
     const bool kmajor = fdk >= 5;
     if (kmajor) PNOL_CHECK(ensure_panels(ctx, o));
-    // one pass of the base chain: F0 (when asked) and the prefix checkpoints
+    // one pass of the base chain: F0 (when asked) and the prefix checkpoints -- skipped when
+    // compute_f0 == 2 and the context's checkpoints are those of (o, x) from
+    // launch_dobj_eval_ckpt (F0 then already holds F(x))
     void* C = nullptr;
     const int ncp = (o->n + kCkpt - 1) / kCkpt;
     PNOL_CHECK(ws_get(ctx, "linres_ckpt", sizeof(double) * (size_t)o->m * (ncp > 1 ? ncp : 1), &C));
-    double* f0_out = compute_f0 ? F0 : nullptr;
+    double* f0_out = compute_f0 == 1 ? F0 : nullptr;
+    if (compute_f0 == 2 && kmajor && ctx->ckpt_obj == o && ctx->ckpt_x == x) ckpt = 0;
+    if (ckpt) {
+        ctx->ckpt_obj = kmajor ? o : nullptr;
+        ctx->ckpt_x = x;
+    }
     if (ckpt && kmajor) {
         ScopedTimer tm(ctx, "fd_ckpt");
         hipLaunchKernelGGL((k_linres_evalP<true>), dim3((o->m + kPanel - 1) / kPanel), dim3(64), 0, ctx->stream, (const double*)o->at,

@@ -19,6 +19,7 @@
 #include "../pnol_comm.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 namespace pnol {
@@ -80,7 +81,7 @@ __device__ __forceinline__ void store_stage(const StageRegs<TILE>& s, double* __
 // MODE 2: as MODE 0, instantiated separately for the chunked launches of launch_fd_jtj (so a
 // kernel trace tells the whole-matrix launches and the pipelined row chunks apart).
 // TILE 128: waves 2 x 2 of 64 x 64 (4 x 4 MFMA blocks each); TILE 64: 2 x 2 of 32 x 32.
-template <int MODE, int TILE>
+template <int MODE, int TILE, bool XMAP = false>
 __global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
                                                       int split_k, int kchunk, double* __restrict__ part,
                                                       double* __restrict__ C, long ldc, double alpha,
@@ -88,9 +89,23 @@ __global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__
     constexpr int WT = TILE / 2, NB = WT / 16;
     __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
 
-    const int blk = blockIdx.x;              // partial slot (local to this launch)
-    const int t = tile0 + blk / split_k;     // lower-triangle tile index
-    const int sidx = blk % split_k;
+    // XMAP (split_k a multiple of 8): the K slices s = xcd, xcd + 8, ... go to the XCD that
+    // dispatch slot blockIdx % 8 lands on, all tiles of one slice before the next, so the
+    // workgroups resident on an XCD stream the same JT columns and share them in its L2.
+    // Otherwise consecutive workgroups are the slices of one tile.
+    int blk, t, sidx;
+    if (XMAP) {
+        const int xcd = blockIdx.x % kNumXcd, local = blockIdx.x / kNumXcd;
+        const int ntl = gridDim.x / split_k;
+        sidx = xcd + kNumXcd * (local / ntl);
+        const int tl = local % ntl;
+        blk = tl * split_k + sidx;           // partial slot: the same layout as below
+        t = tile0 + tl;
+    } else {
+        blk = blockIdx.x;                    // partial slot (local to this launch)
+        t = tile0 + blk / split_k;           // lower-triangle tile index
+        sidx = blk % split_k;
+    }
     int ti, tj;
     tile_of(t, ti, tj);
     const bool diag = ti == tj;
@@ -263,6 +278,11 @@ __global__ void k_jtj_seq(const double* __restrict__ JT, long ldjt, int m, int n
 // of partial tiles; ties go to the smaller split (less reduce traffic).  At n = 2048
 // (136 tiles) on 256 CUs this is 7 (952 WGs, 93% of 4 rounds) instead of 4 (544, 71%).
 static int choose_split_k(int ntiles, int K, int ncu) {
+    static const int forced = [] {
+        const char* e = std::getenv("PNOL_SYRK_SPLIT");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (forced > 0) return std::min(forced, std::max(1, (K + kTK - 1) / kTK));
     if (ncu <= 0) ncu = 256;
     const int kmax = (K + 255) / 256;
     int best = 1;
@@ -278,6 +298,14 @@ static int choose_split_k(int ntiles, int K, int ncu) {
         }
     }
     return best;
+}
+
+static bool syrk_xmap() {
+    static const bool on = [] {
+        const char* e = std::getenv("PNOL_SYRK_XMAP");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
 }
 
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
@@ -297,8 +325,12 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * split_k * kTile * kTile, &part));
     {
         ScopedTimer tm(ctx, "syrk");
-        hipLaunchKernelGGL((k_syrk_tile<0, kTile>), dim3(ntiles * split_k), dim3(256), 0, ctx->stream, JT, (long)ldjt, n, m,
-                           split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0, 0);
+        if (syrk_xmap() && split_k % kNumXcd == 0)
+            hipLaunchKernelGGL((k_syrk_tile<0, kTile, true>), dim3(ntiles * split_k), dim3(256), 0, ctx->stream, JT,
+                               (long)ldjt, n, m, split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0, 0);
+        else
+            hipLaunchKernelGGL((k_syrk_tile<0, kTile>), dim3(ntiles * split_k), dim3(256), 0, ctx->stream, JT,
+                               (long)ldjt, n, m, split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0, 0);
     }
     PNOL_CHECK(launch_check());
     ScopedTimer tm(ctx, "syrk_reduce");

@@ -30,6 +30,7 @@ struct Timers {
     bool on = false;
     std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::map<std::string, std::pair<double, int>> done;
+    std::vector<hipEvent_t> free_events;   // recycled after resolve (event creation is not free)
 };
 }  // namespace pnol
 
@@ -40,8 +41,10 @@ struct pnol_ctx {
     hipStream_t stream = nullptr;   // active stream (own or caller-provided)
     int num_cu = 0;
     pnol::Workspace ws;
-    double* pinned = nullptr;       // small host staging buffer (scalars back from the device)
+    void* pinned = nullptr;         // pinned host staging for pnol_memcpy_* (grown on demand)
     size_t pinned_bytes = 0;
+    const pnol_dobj* ckpt_obj = nullptr;   // the objective whose prefix checkpoints are in "linres_ckpt"
+    const double* ckpt_x = nullptr;        // ... and the device x they were computed at
     int* solve_flags = nullptr;     // per-block ready flags of the triangular solves (workspace)
     int solve_epoch = 0;            // value the flags of the current solve are set to
     void* chol_tasks = nullptr;     // uploaded tile-DAG task table (workspace) and its tile count
@@ -117,6 +120,7 @@ int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p
                      const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
                      double* v);
 int launch_set_identity(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale);
+int launch_add(pnol_ctx* ctx, const double* x, const double* y, double* z, int n);
 int launch_gather_sub(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub, double* Dsub,
                       int lds);
 
@@ -134,6 +138,7 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
                  int* info);
 
 int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
+int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
 int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt,
                        double* f0, double* g);
 // ckpt: 1 = run the base-chain pass (F0 when compute_f0, prefix checkpoints), 0 = reuse the

@@ -187,7 +187,16 @@ ScopedTimer::ScopedTimer(pnol_ctx* ctx, const char* name, hipStream_t stream)
     : ctx_(ctx), name_(name), stream_(stream) {
     if (!ctx_ || !ctx_->timers.on) return;
     if (!stream_) stream_ = ctx_->stream;
-    if (hipEventCreate(&a_) != hipSuccess || hipEventCreate(&b_) != hipSuccess) { a_ = b_ = nullptr; return; }
+    auto& pool = ctx_->timers.free_events;
+    for (hipEvent_t* e : {&a_, &b_}) {
+        if (!pool.empty()) {
+            *e = pool.back();
+            pool.pop_back();
+        } else if (hipEventCreate(e) != hipSuccess) {
+            a_ = b_ = nullptr;
+            return;
+        }
+    }
     (void)hipEventRecord(a_, stream_);
 }
 
@@ -207,8 +216,8 @@ static void resolve_timers(pnol_ctx* ctx) {
                 acc.first += ms;
                 acc.second += 1;
             }
-            (void)hipEventDestroy(ev.first);
-            (void)hipEventDestroy(ev.second);
+            ctx->timers.free_events.push_back(ev.first);
+            ctx->timers.free_events.push_back(ev.second);
         }
         kv.second.clear();
     }
@@ -300,6 +309,13 @@ int pnol_ctx_destroy(pnol_ctx* ctx) {
         (void)hipStreamDestroy(ctx->aux_stream);
     }
     for (hipEvent_t e : ctx->aux_events) (void)hipEventDestroy(e);
+    for (auto& kv : ctx->timers.pending)
+        for (auto& ev : kv.second) {
+            (void)hipEventDestroy(ev.first);
+            (void)hipEventDestroy(ev.second);
+        }
+    for (hipEvent_t e : ctx->timers.free_events) (void)hipEventDestroy(e);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx == g_default) g_default = nullptr;
     delete ctx;
     return PNOL_OK;
@@ -370,10 +386,36 @@ int pnol_free(pnol_ctx* ctx, void* dptr) {
     return PNOL_OK;
 }
 
+// Host <-> device copies of the solvers' small vectors (x, sigma, residuals): through a
+// pinned staging buffer, so the DMA engine copies directly instead of the runtime's pageable
+// bounce path.  Large copies (> 64 MiB) go direct.
+static void* staging(pnol_ctx* ctx, size_t bytes) {
+    constexpr size_t kMaxStage = 64u << 20;
+    if (bytes > kMaxStage) return nullptr;
+    if (ctx->pinned_bytes < bytes) {
+        if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+        ctx->pinned = nullptr;
+        ctx->pinned_bytes = 0;
+        size_t cap = 64 * 1024;
+        while (cap < bytes) cap *= 2;
+        if (hipHostMalloc(&ctx->pinned, cap, hipHostMallocDefault) != hipSuccess) {
+            ctx->pinned = nullptr;
+            return nullptr;
+        }
+        ctx->pinned_bytes = cap;
+    }
+    return ctx->pinned;
+}
+
 int pnol_memcpy_h2d(pnol_ctx* ctx, void* dst, const void* src, size_t bytes) {
     if (!ctx || (!dst && bytes) || (!src && bytes)) return PNOL_ERR_ARG;
     if (!bytes) return PNOL_OK;
-    PNOL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    if (void* st = staging(ctx, bytes)) {
+        std::memcpy(st, src, bytes);
+        PNOL_HIP(hipMemcpyAsync(dst, st, bytes, hipMemcpyHostToDevice, ctx->stream));
+    } else {
+        PNOL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    }
     PNOL_HIP(hipStreamSynchronize(ctx->stream));
     return PNOL_OK;
 }
@@ -381,8 +423,75 @@ int pnol_memcpy_h2d(pnol_ctx* ctx, void* dst, const void* src, size_t bytes) {
 int pnol_memcpy_d2h(pnol_ctx* ctx, void* dst, const void* src, size_t bytes) {
     if (!ctx || (!dst && bytes) || (!src && bytes)) return PNOL_ERR_ARG;
     if (!bytes) return PNOL_OK;
-    PNOL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
-    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    if (void* st = staging(ctx, bytes)) {
+        PNOL_HIP(hipMemcpyAsync(st, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        PNOL_HIP(hipStreamSynchronize(ctx->stream));
+        std::memcpy(dst, st, bytes);
+    } else {
+        PNOL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return PNOL_OK;
+}
+
+int pnol_host_alloc(void** p, size_t bytes) {
+    if (!p) return PNOL_ERR_ARG;
+    *p = nullptr;
+    PNOL_HIP(hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault));
+    return PNOL_OK;
+}
+
+int pnol_host_free(void* p) {
+    if (p) PNOL_HIP(hipHostFree(p));
+    return PNOL_OK;
+}
+
+int pnol_memcpy_d2h_async(pnol_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (!ctx || (!dst && bytes) || (!src && bytes)) return PNOL_ERR_ARG;
+    if (bytes) PNOL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    return PNOL_OK;
+}
+
+struct pnol_event {
+    hipEvent_t e = nullptr;
+    int device = 0;
+};
+
+int pnol_event_create(pnol_ctx* ctx, pnol_event** out) {
+    if (!ctx || !out) return PNOL_ERR_ARG;
+    PNOL_HIP(hipSetDevice(ctx->device));
+    auto* ev = new pnol_event();
+    ev->device = ctx->device;
+    if (hipEventCreateWithFlags(&ev->e, hipEventDisableTiming) != hipSuccess) {
+        delete ev;
+        return PNOL_ERR_HIP;
+    }
+    *out = ev;
+    return PNOL_OK;
+}
+
+int pnol_event_record(pnol_ctx* ctx, pnol_event* ev) {
+    if (!ctx || !ev) return PNOL_ERR_ARG;
+    PNOL_HIP(hipEventRecord(ev->e, ctx->stream));
+    return PNOL_OK;
+}
+
+// Busy-polls: the host wakes as soon as the event completes (a blocking wait returns
+// tens of microseconds late, which the LM loop pays on every trip).
+int pnol_event_wait(pnol_event* ev) {
+    if (!ev) return PNOL_ERR_ARG;
+    for (;;) {
+        const hipError_t q = hipEventQuery(ev->e);
+        if (q == hipSuccess) return PNOL_OK;
+        if (q != hipErrorNotReady) return PNOL_ERR_HIP;
+    }
+}
+
+int pnol_event_destroy(pnol_event* ev) {
+    if (!ev) return PNOL_ERR_ARG;
+    (void)hipSetDevice(ev->device);
+    (void)hipEventDestroy(ev->e);
+    delete ev;
     return PNOL_OK;
 }
 

@@ -170,6 +170,12 @@ class DeviceObjective:
         L.check(L.lib().pnol_dobj_eval_d(self.ctx.h, self.h, _ptr(x), _ptr(out)), "pnol_dobj_eval_d")
         return out
 
+    def eval_ckpt(self, x, out=None):
+        """F(x), keeping a linear residual's prefix checkpoints of x for a compute_f0=2 FD call."""
+        out = self.ctx.empty(self.m if self.m else 1) if out is None else out
+        L.check(L.lib().pnol_dobj_eval_ckpt_d(self.ctx.h, self.h, _ptr(x), _ptr(out)), "pnol_dobj_eval_ckpt_d")
+        return out
+
     def fd_gradient(self, x, h, i0=0, cnt=None):
         cnt = self.n - i0 if cnt is None else cnt
         f0, g = self.ctx.empty(1), self.ctx.empty(max(cnt, 1))

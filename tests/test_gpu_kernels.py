@@ -389,6 +389,30 @@ def test_fd_jacobian_tiles_bitwise(ctx, oracle, m, n, P):
     assert np.array_equal(full, ref)
 
 
+@pytest.mark.parametrize("m,n", [(513, 700), (300, 129), (1000, 2048)])
+def test_fd_checkpoint_reuse_bitwise(ctx, oracle, m, n):
+    """pnol_dobj_eval_ckpt_d then an FD call with compute_f0 = 2 (the LM accepted-step path)
+    skips the base-chain pass and stays bitwise; checkpoints of another x are not reused."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L, fd_tiles
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    A, xs, y = oracle.linres_data(m, n)
+    d = DeviceObjective(ctx, L.OBJ_LINRES, n, m, A, y)
+    o = oracle.Obj(oracle.LINRES, n, m, A, y)
+    x = np.linspace(-0.5, 0.5, n); h = np.full(n, 1e-7)
+    x2 = np.linspace(0.3, -0.2, n)
+    ref = oracle.fd_jacobian(o, x, h).T
+    tiles = fd_tiles(n, 1, 0)
+    dx, dx2, dh = ctx.tensor(x), ctx.tensor(x2), ctx.tensor(h)
+    F = d.eval_ckpt(dx)
+    assert np.array_equal(_np(F), oracle.obj_eval_multi(o, x))
+    _, JT = d.fd_jacobian_tiles(dx, dh, tiles, ctx.empty(n, m), F0=F, compute_f0=2)
+    assert np.array_equal(_np(JT), ref)
+    # checkpoints now belong to x2: an FD call at x with compute_f0 = 2 must recompute them
+    d.eval_ckpt(dx2)
+    _, JT = d.fd_jacobian_tiles(dx, dh, tiles, ctx.empty(n, m), F0=F, compute_f0=2)
+    assert np.array_equal(_np(JT), ref)
+
+
 @pytest.mark.parametrize("m,n,chunks", [(2000, 700, 4), (1500, 1000, 3), (513, 2048, 8), (300, 129, 2), (400, 300, 1)])
 def test_fd_jtj_pipelined_bitwise(ctx, m, n, chunks):
     """The pipelined FD Jacobian + J^T J (two streams, chunked) equals the two separate calls

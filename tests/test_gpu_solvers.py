@@ -103,6 +103,34 @@ def test_lm_linres_large(ctx, oracle, m, n):
     assert rel(X, xs) <= 1e-8
 
 
+@pytest.mark.parametrize("m,n,lam0,iters", [(600, 100, 0.001, 12), (3000, 257, 0.001, 10), (2000, 300, 50.0, 9),
+                                           (1000, 129, 1e-9, 12)])
+def test_lm_one_wait_loop_equals_general_loop(ctx, oracle, m, n, lam0, iters):
+    """The LM loop with one host wait per trip (n > PNOL_SEQ_MAX: the trip is queued whole, the
+    trial point formed and evaluated on the device) replays the general loop exactly: X, F0,
+    FOpt and the evaluation count are bitwise those of PNOL_LM_ASYNC=0, through accepted
+    steps, the rejected ones after convergence (xMinDiff = 0 keeps the loop running) and a
+    large starting lambda."""
+    import os
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_levmarq
+    A, xs, y = oracle.linres_data(m, n)
+    params = (lam0, 10, 1e-7, iters, 0.0, -1)
+    out = {}
+    for mode in ("1", "0"):
+        os.environ["PNOL_LM_ASYNC"] = mode
+        try:
+            d = _obj(ctx, L.OBJ_LINRES, n, m, A, y)
+            out[mode] = run_levmarq(d, np.zeros(n), params)
+        finally:
+            os.environ.pop("PNOL_LM_ASYNC", None)
+    (Xa, F0a, FOa, ra), (Xs, F0s, FOs, rs) = out["1"], out["0"]
+    assert np.array_equal(Xa, Xs)
+    assert np.array_equal(F0a, F0s) and np.array_equal(FOa, FOs)
+    assert ra.evals == rs.evals
+    assert rel(Xa, xs) <= 1e-8
+
+
 def test_bfgs_mpi_pool_matches_oracle(ctx, oracle):
     """BFGS_MPI with Npool = 8 in one process equals the reference at np = 8, including the
     zero-pool defect (f = 0)."""
