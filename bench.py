@@ -263,7 +263,7 @@ def main():
         fd_flop = fd_flop_executed(m, n, my_tiles)           # prefix-shared chains actually run
         pmc = pmc_traffic()
         roofline = {
-            "kernel": "k_syrk_tile (J^T J, fp64 MFMA v_mfma_f64_16x16x4_f64)",
+            "kernel": "k_syrk_tile<0,128,8 waves> (J^T J, fp64 MFMA v_mfma_f64_16x16x4_f64)",
             "bound": "mfma", "achieved": jtj_flop / (syrk_ms * 1e-3) / 1e12 if syrk_ms else None,
             "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "traffic": pmc.get("k_syrk_tile<0, 128>", {}).get("traffic_bytes_per_launch"),

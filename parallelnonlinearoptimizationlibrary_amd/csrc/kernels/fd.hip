@@ -380,8 +380,11 @@ __global__ __launch_bounds__(256) void k_to_panels(const double* __restrict__ A,
 
 // r = A x - y from AP: lane = row, the objective's fma chain over k ascending; CKPT also
 // stores the chain value before every kCkpt-th column (C[(k / kCkpt) * m + row], k > 0).
-// One wave per panel (m / 64 waves): the chain is sequential, so the stream is kept deep --
-// two 16-column blocks (16 KB per wave) in flight while one is consumed.
+// One wave per panel (m / 64 waves, about one per CU): the chain is sequential, so the panel
+// stream is kept deep -- a ring of kRing 16-column blocks (kRing * 8 KB per wave) in flight
+// while one is consumed.
+constexpr int kRing = 6;
+
 template <bool CKPT>
 __global__ __launch_bounds__(64) void k_linres_evalP(const double* __restrict__ AP, const double* __restrict__ x,
                                                      const double* __restrict__ y, int m, int n,
@@ -390,37 +393,34 @@ __global__ __launch_bounds__(64) void k_linres_evalP(const double* __restrict__ 
     const double* a = panel_col(AP, n, rb, 0) + threadIdx.x;
     constexpr int U = kCkpt;
     double acc = 0.0;
-    auto load = [&](double (&v)[U], int k) {
-        const double* ak = a + (size_t)k * kPanel;
+    const int nb = n / U;   // full blocks
+    double ring[kRing][U];
+    auto load = [&](int r, int blk) {
+        const double* ak = a + (size_t)blk * U * kPanel;
 #pragma unroll
-        for (int q = 0; q < U; ++q) v[q] = __builtin_nontemporal_load(ak + q * kPanel);
+        for (int q = 0; q < U; ++q) ring[r][q] = __builtin_nontemporal_load(ak + q * kPanel);
     };
-    auto step = [&](const double (&v)[U], int k) {
+    auto step = [&](int r, int blk) {
+        const int k = blk * U;
         if (CKPT && k > 0 && row < m) C[(long)(k / kCkpt) * m + row] = acc;
 #pragma unroll
-        for (int q = 0; q < U; ++q) acc = fma(v[q], x[k + q], acc);
+        for (int q = 0; q < U; ++q) acc = fma(ring[r][q], x[k + q], acc);
     };
-    const int nb = n / U;   // full blocks
-    int k = 0;
-    if (nb > 0) {
-        double b0[U], b1[U], b2[U];
-        load(b0, 0);
-        if (nb > 1) load(b1, U);
-        int blk = 0;
-        // three-deep rotation: blocks blk+1 and blk+2 in flight while blk is consumed
-        while (blk < nb) {
-            if (blk + 2 < nb) load(b2, (blk + 2) * U);
-            step(b0, blk * U);
-            if (++blk >= nb) break;
-            if (blk + 2 < nb) load(b0, (blk + 2) * U);
-            step(b1, blk * U);
-            if (++blk >= nb) break;
-            if (blk + 2 < nb) load(b1, (blk + 2) * U);
-            step(b2, blk * U);
-            ++blk;
+#pragma unroll
+    for (int r = 0; r < kRing; ++r)
+        if (r < nb) load(r, r);
+    int blk = 0;
+    for (; blk + kRing <= nb; blk += kRing) {
+#pragma unroll
+        for (int r = 0; r < kRing; ++r) {
+            step(r, blk + r);
+            if (blk + r + kRing < nb) load(r, blk + r + kRing);
         }
-        k = nb * U;
     }
+#pragma unroll
+    for (int r = 0; r < kRing; ++r)
+        if (blk + r < nb) step(r, blk + r);
+    int k = nb * U;
     if (CKPT && k > 0 && k < n && row < m) C[(long)(k / kCkpt) * m + row] = acc;
     for (; k < n; ++k) acc = fma(a[(size_t)k * kPanel], x[k], acc);
     if (row < m && F) F[row] = y ? acc - y[row] : acc;

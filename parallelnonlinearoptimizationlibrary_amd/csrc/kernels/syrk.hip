@@ -42,13 +42,13 @@ __device__ __forceinline__ void tile_of(int t, int& ti, int& tj) {
 // Stage loader: TILE rows x 16 doubles of X starting at (row0, k0) into registers.
 // 256 threads: TPR = 256 / TILE threads per row, each owning 16 / TPR consecutive columns.
 // Rows >= nr and columns >= kend read as 0.
-template <int TILE>
-struct StageRegs { double2 v[TILE / 32]; };
+template <int TILE, int NT = 256>
+struct StageRegs { double2 v[TILE * 8 / NT]; };
 
-template <int TILE>
-__device__ __forceinline__ void load_stage(StageRegs<TILE>& s, const double* __restrict__ X, long ldx, int nr,
+template <int TILE, int NT = 256>
+__device__ __forceinline__ void load_stage(StageRegs<TILE, NT>& s, const double* __restrict__ X, long ldx, int nr,
                                            int row0, int k0, int kend, bool full) {
-    constexpr int TPR = 256 / TILE, CPT = 16 / TPR, NV = CPT / 2;
+    constexpr int TPR = NT / TILE, CPT = 16 / TPR, NV = CPT / 2;
     const int t = threadIdx.x;
     const int row = row0 + t / TPR;
     const int kc = k0 + (t % TPR) * CPT;
@@ -68,9 +68,9 @@ __device__ __forceinline__ void load_stage(StageRegs<TILE>& s, const double* __r
     }
 }
 
-template <int TILE>
-__device__ __forceinline__ void store_stage(const StageRegs<TILE>& s, double* __restrict__ lds) {
-    constexpr int TPR = 256 / TILE, CPT = 16 / TPR, NV = CPT / 2;
+template <int TILE, int NT = 256>
+__device__ __forceinline__ void store_stage(const StageRegs<TILE, NT>& s, double* __restrict__ lds) {
+    constexpr int TPR = NT / TILE, CPT = 16 / TPR, NV = CPT / 2;
     const int t = threadIdx.x;
     double* dst = lds + (t / TPR) * kPad + (t % TPR) * CPT;
 #pragma unroll
@@ -81,12 +81,20 @@ __device__ __forceinline__ void store_stage(const StageRegs<TILE>& s, double* __
 // MODE 2: as MODE 0, instantiated separately for the chunked launches of launch_fd_jtj (so a
 // kernel trace tells the whole-matrix launches and the pipelined row chunks apart).
 // TILE 128: waves 2 x 2 of 64 x 64 (4 x 4 MFMA blocks each); TILE 64: 2 x 2 of 32 x 32.
-template <int MODE, int TILE, bool XMAP = false>
-__global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
+// NW = 4: waves 2 x 2, each (TILE/2)^2; NW = 8: waves 2 x 4, each TILE/2 x TILE/4 (half the
+// accumulators per wave, so twice the waves per SIMD hide the stage boundaries).
+// MODE 3: as MODE 0, then the last of a tile's split_k workgroups to finish (counter cnt[t],
+// agent-scope release/acquire) sums the tile's partials in slice order -- the same fixed
+// order as k_syrk_reduce, so bitwise the same A -- and writes A = the tile with the
+// Marquardt diagonal (alpha = lambda) and its mirror; cnt[t] is reset for the next launch.
+template <int MODE, int TILE, bool XMAP = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
                                                       int split_k, int kchunk, double* __restrict__ part,
                                                       double* __restrict__ C, long ldc, double alpha,
-                                                      double beta, int tile0) {
-    constexpr int WT = TILE / 2, NB = WT / 16;
+                                                      double beta, int tile0, int* __restrict__ cnt = nullptr,
+                                                      double* __restrict__ diag_out = nullptr) {
+    constexpr int NT = 64 * NW, WC = NW / 2;
+    constexpr int WTM = TILE / 2, WTN = TILE / WC, NBM = WTM / 16, NBN = WTN / 16;
     __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
 
     // XMAP (split_k a multiple of 8): the K slices s = xcd, xcd + 8, ... go to the XCD that
@@ -116,20 +124,20 @@ __global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int wr = wave >> 1, wc = wave & 1;
+    const int wr = wave / WC, wc = wave % WC;
     const bool ldx_even = (ldx & 1) == 0;
 
-    d4 acc[NB][NB];
+    d4 acc[NBM][NBN];
 #pragma unroll
-    for (int i = 0; i < NB; ++i)
+    for (int i = 0; i < NBM; ++i)
 #pragma unroll
-        for (int j = 0; j < NB; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+        for (int j = 0; j < NBN; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
 
-    StageRegs<TILE> ps, qs;
+    StageRegs<TILE, NT> ps, qs;
     if (nstages > 0) {
         bool full = ldx_even && (kbeg + kTK <= kend);
-        load_stage(ps, X, ldx, nr, prow0, kbeg, kend, full);
-        if (!diag) load_stage(qs, X, ldx, nr, qrow0, kbeg, kend, full);
+        load_stage<TILE, NT>(ps, X, ldx, nr, prow0, kbeg, kend, full);
+        if (!diag) load_stage<TILE, NT>(qs, X, ldx, nr, qrow0, kbeg, kend, full);
     }
     const int frow = lane & 15;
     const int fk = lane >> 4;
@@ -137,26 +145,26 @@ __global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__
         const int buf = st & 1;
         double* P = lds[buf][0];
         double* Q = diag ? lds[buf][0] : lds[buf][1];
-        store_stage(ps, P);
-        if (!diag) store_stage(qs, Q);
+        store_stage<TILE, NT>(ps, P);
+        if (!diag) store_stage<TILE, NT>(qs, Q);
         __syncthreads();
         if (st + 1 < nstages) {
             const int k0 = kbeg + (st + 1) * kTK;
             bool full = ldx_even && (k0 + kTK <= kend);
-            load_stage(ps, X, ldx, nr, prow0, k0, kend, full);
-            if (!diag) load_stage(qs, X, ldx, nr, qrow0, k0, kend, full);
+            load_stage<TILE, NT>(ps, X, ldx, nr, prow0, k0, kend, full);
+            if (!diag) load_stage<TILE, NT>(qs, X, ldx, nr, qrow0, k0, kend, full);
         }
 #pragma unroll
         for (int kk = 0; kk < kTK / 4; ++kk) {
-            double a[NB], b[NB];
+            double a[NBM], b[NBN];
 #pragma unroll
-            for (int mi = 0; mi < NB; ++mi) a[mi] = P[(wr * WT + mi * 16 + frow) * kPad + kk * 4 + fk];
+            for (int mi = 0; mi < NBM; ++mi) a[mi] = P[(wr * WTM + mi * 16 + frow) * kPad + kk * 4 + fk];
 #pragma unroll
-            for (int ni = 0; ni < NB; ++ni) b[ni] = Q[(wc * WT + ni * 16 + frow) * kPad + kk * 4 + fk];
+            for (int ni = 0; ni < NBN; ++ni) b[ni] = Q[(wc * WTN + ni * 16 + frow) * kPad + kk * 4 + fk];
 #pragma unroll
-            for (int mi = 0; mi < NB; ++mi)
+            for (int mi = 0; mi < NBM; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < NB; ++ni)
+                for (int ni = 0; ni < NBN; ++ni)
                     acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
         }
     }
@@ -164,27 +172,61 @@ __global__ __launch_bounds__(256, 2) void k_syrk_tile(const double* __restrict__
     // f64 MFMA C/D layout: lane l, register r -> row (l >> 4) + 4 r, column l & 15
     const int ocol = lane & 15;
     const int orow = lane >> 4;
-    if (MODE == 0 || MODE == 2) {
+    if (MODE == 0 || MODE == 2 || MODE == 3) {
         double* out = part + (long)blk * TILE * TILE;
 #pragma unroll
-        for (int mi = 0; mi < NB; ++mi)
+        for (int mi = 0; mi < NBM; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < NB; ++ni)
+            for (int ni = 0; ni < NBN; ++ni)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    int row = wr * WT + mi * 16 + orow + 4 * r;
-                    int col = wc * WT + ni * 16 + ocol;
+                    int row = wr * WTM + mi * 16 + orow + 4 * r;
+                    int col = wc * WTN + ni * 16 + ocol;
                     out[row * TILE + col] = acc[mi][ni][r];
                 }
+        if (MODE == 3) {
+            __shared__ int s_last;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                const int old = __hip_atomic_fetch_add(cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_last = old == split_k - 1;
+                if (s_last) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                }
+            }
+            __syncthreads();
+            if (s_last) {
+                const double scale = 1 + alpha;
+                const double* p0 = part + ((long)(t - tile0) * split_k) * TILE * TILE;
+                for (int e = threadIdx.x; e < TILE * TILE; e += NT) {
+                    const int r = e / TILE, c = e % TILE;
+                    const int i = prow0 + r, j = qrow0 + c;
+                    if (i >= nr || j >= nr || j > i) continue;
+                    double v = 0.0;
+                    for (int s2 = 0; s2 < split_k; ++s2) v += p0[(long)s2 * TILE * TILE + e];
+                    if (i == j) {
+                        if (diag_out) diag_out[i] = v;
+                        C[(long)i * ldc + i] = scale * v;
+                    } else {
+                        C[(long)i * ldc + j] = v;
+                        C[(long)j * ldc + i] = v;
+                    }
+                }
+                if (threadIdx.x == 0) cnt[t] = 0;
+            }
+        }
     } else {
 #pragma unroll
-        for (int mi = 0; mi < NB; ++mi)
+        for (int mi = 0; mi < NBM; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < NB; ++ni)
+            for (int ni = 0; ni < NBN; ++ni)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    int i = prow0 + wr * WT + mi * 16 + orow + 4 * r;
-                    int j = qrow0 + wc * WT + ni * 16 + ocol;
+                    int i = prow0 + wr * WTM + mi * 16 + orow + 4 * r;
+                    int j = qrow0 + wc * WTN + ni * 16 + ocol;
                     if (i < nr && j < nr && j <= i) {
                         double* c = C + (long)i * ldc + j;
                         *c = beta * (*c) + alpha * acc[mi][ni][r];
@@ -300,6 +342,28 @@ static int choose_split_k(int ntiles, int K, int ncu) {
     return best;
 }
 
+// J^T J variant (tuning; every variant sums each element in the same order):
+// PNOL_SYRK_NW = 8 (default) or 4 waves per 128 x 128 tile; PNOL_SYRK_FUSED = 1 reduces the
+// split-K partials inside the tile kernel (MODE 3), 0 (default) runs k_syrk_reduce after it.
+// Measured at m = 16384, n = 2048: 8 waves 1.35 ms vs 4 waves 1.40 ms; the fused reduce 1.51 ms
+// vs 1.35 + 0.06 ms -- every tile's last slice finishes in the final round, so the in-kernel
+// reduces all land in the tail instead of overlapping the MFMA work.
+static int syrk_nw() {
+    static const int nw = [] {
+        const char* e = std::getenv("PNOL_SYRK_NW");
+        return (e && std::atoi(e) == 4) ? 4 : 8;
+    }();
+    return nw;
+}
+
+static bool syrk_fused() {
+    static const bool on = [] {
+        const char* e = std::getenv("PNOL_SYRK_FUSED");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+
 static bool syrk_xmap() {
     static const bool on = [] {
         const char* e = std::getenv("PNOL_SYRK_XMAP");
@@ -323,9 +387,28 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     kchunk = (kchunk + kTK - 1) / kTK * kTK;
     void* part = nullptr;
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * split_k * kTile * kTile, &part));
+    if (syrk_fused()) {
+        // partial tiles + the last-arriving workgroup's fixed-order reduce in one launch
+        void* cnt = nullptr;
+        PNOL_CHECK(ws_get_zeroed(ctx, "syrk_cnt", sizeof(int) * (size_t)ntiles, &cnt));
+        ScopedTimer tm(ctx, "syrk");
+        if (syrk_nw() == 4)
+            hipLaunchKernelGGL((k_syrk_tile<3, kTile, false, 4>), dim3(ntiles * split_k), dim3(256), 0, ctx->stream,
+                               JT, (long)ldjt, n, m, split_k, kchunk, (double*)part, A, (long)lda, lambda, 0.0, 0,
+                               (int*)cnt, jtj_diag);
+        else
+            hipLaunchKernelGGL((k_syrk_tile<3, kTile, false, 8>), dim3(ntiles * split_k), dim3(512), 0, ctx->stream,
+                               JT, (long)ldjt, n, m, split_k, kchunk, (double*)part, A, (long)lda, lambda, 0.0, 0,
+                               (int*)cnt, jtj_diag);
+        return launch_check();
+    }
     {
         ScopedTimer tm(ctx, "syrk");
-        if (syrk_xmap() && split_k % kNumXcd == 0)
+        if (syrk_nw() == 8)
+            hipLaunchKernelGGL((k_syrk_tile<0, kTile, false, 8>), dim3(ntiles * split_k), dim3(512), 0, ctx->stream,
+                               JT, (long)ldjt, n, m, split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0,
+                               0);
+        else if (syrk_xmap() && split_k % kNumXcd == 0)
             hipLaunchKernelGGL((k_syrk_tile<0, kTile, true>), dim3(ntiles * split_k), dim3(256), 0, ctx->stream, JT,
                                (long)ldjt, n, m, split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0, 0);
         else
@@ -353,7 +436,7 @@ int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldj
     double* mypart = (double*)part + (size_t)t0 * split_k * kTile * kTile;   // disjoint per row range
     {
         ScopedTimer tm(ctx, "syrk_rows", stream);
-        hipLaunchKernelGGL((k_syrk_tile<2, kTile>), dim3((t1 - t0) * split_k), dim3(256), 0, stream, JT, (long)ldjt, n,
+        hipLaunchKernelGGL((k_syrk_tile<2, kTile, false, 8>), dim3((t1 - t0) * split_k), dim3(512), 0, stream, JT, (long)ldjt, n,
                            m, split_k, kchunk, mypart, (double*)nullptr, 0L, 1.0, 0.0, t0);
     }
     PNOL_CHECK(launch_check());
@@ -460,7 +543,7 @@ int launch_jtj_sharded(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, 
     if (cnt > 0) {
         {
             ScopedTimer tm(ctx, "syrk");
-            hipLaunchKernelGGL((k_syrk_tile<0, kTile>), dim3(cnt * split_k), dim3(256), 0, ctx->stream, JT, (long)ldjt,
+            hipLaunchKernelGGL((k_syrk_tile<0, kTile, false, 8>), dim3(cnt * split_k), dim3(512), 0, ctx->stream, JT, (long)ldjt,
                                n, m, split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0, t0);
         }
         PNOL_CHECK(launch_check());

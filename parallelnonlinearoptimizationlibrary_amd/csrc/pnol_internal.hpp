@@ -89,6 +89,7 @@ namespace pnol {
 
 // Returns a device scratch buffer of at least `bytes` for `key` (grows, keeps contents undefined).
 int ws_get(pnol_ctx* ctx, const char* key, size_t bytes, void** out);
+int ws_get_zeroed(pnol_ctx* ctx, const char* key, size_t bytes, void** out);
 
 // Scoped timer: records a start event now and a stop event at scope exit (when enabled).
 class ScopedTimer {

@@ -36,6 +36,16 @@ int ws_get(pnol_ctx* ctx, const char* key, size_t bytes, void** out) {
     return PNOL_OK;
 }
 
+// ws_get whose buffer reads as zero when (re)allocated (flag / counter arrays)
+int ws_get_zeroed(pnol_ctx* ctx, const char* key, size_t bytes, void** out) {
+    if (!ctx || !out) return PNOL_ERR_ARG;
+    auto it = ctx->ws.bufs.find(key);
+    const void* before = it == ctx->ws.bufs.end() ? nullptr : it->second.first;
+    PNOL_CHECK(ws_get(ctx, key, bytes, out));
+    if (*out != before) PNOL_HIP(hipMemsetAsync(*out, 0, ctx->ws.bufs[key].second, ctx->stream));
+    return PNOL_OK;
+}
+
 static bool is_gfx950(int dev) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;

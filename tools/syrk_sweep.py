@@ -1,6 +1,6 @@
 """Time J^T J (k_syrk_tile + k_syrk_reduce) on the bench shape (m=16384, n=2048, random JT) for
-SYRK variants given as "split:xmap" arguments (PNOL_SYRK_SPLIT / PNOL_SYRK_XMAP, read once per
-process, so one child per variant).  split 0 = the default choice."""
+SYRK variants given as "split:xmap:nw:fused" arguments (PNOL_SYRK_SPLIT / _XMAP / _NW / _FUSED,
+read once per process, so one child per variant).  split 0 = the default choice."""
 import json
 import os
 import subprocess
@@ -15,6 +15,7 @@ from parallelnonlinearoptimizationlibrary_amd import _lib as L
 from parallelnonlinearoptimizationlibrary_amd.device import Context
 m, n = 16384, 2048
 ctx = Context(0)
+torch.manual_seed(1234)
 JT = torch.randn(n, m, dtype=torch.float64, device="cuda")
 for _ in range(2):
     ctx.jtj(JT, 0.25)
@@ -31,13 +32,15 @@ for k in ("syrk", "syrk_reduce"):
 out["tflops"] = m * n * (n + 1) / (out["syrk"] * 1e-3) / 1e12
 ref = (JT @ JT.T); ref.diagonal().mul_(1.25)
 out["relerr"] = float((A - ref).abs().max() / ref.abs().max())
+import hashlib
+out["sha"] = hashlib.sha1(A.cpu().numpy().tobytes()).hexdigest()[:12]
 print(json.dumps(out))
 """ % ROOT
 
 if __name__ == "__main__":
-    for v in (sys.argv[1:] or ["0:0", "8:0", "8:1", "16:1"]):
-        sp, xm = v.split(":")
-        env = dict(os.environ, PNOL_SYRK_SPLIT=sp, PNOL_SYRK_XMAP=xm)
+    for v in (sys.argv[1:] or ["0:0:4:0", "0:0:8:0", "0:0:8:1"]):
+        sp, xm, nw, fu = (v.split(":") + ["8", "1"][len(v.split(":")) - 2:])[:4]
+        env = dict(os.environ, PNOL_SYRK_SPLIT=sp, PNOL_SYRK_XMAP=xm, PNOL_SYRK_NW=nw, PNOL_SYRK_FUSED=fu)
         p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
         if p.returncode != 0:
             print(p.stderr[-2000:])
