@@ -44,7 +44,15 @@ def _args():
     ap.add_argument("--no-timers", action="store_true", help="no per-kernel HIP events in the timed region")
     ap.add_argument("--m", type=int, default=M_RES)
     ap.add_argument("--n", type=int, default=N_PAR)
+    ap.add_argument("--host-comm", action="store_true",
+                    help="rehearsal on one GPU: gloo + the library's host communicator instead of RCCL")
     return ap.parse_args()
+
+
+def _red_dev():
+    """Device for collective scratch tensors: cuda under nccl (RCCL), cpu under gloo."""
+    import torch.distributed as dist
+    return "cuda" if dist.get_backend() == "nccl" else "cpu"
 
 
 def _timer(L, ctx_h, name):
@@ -142,6 +150,41 @@ def bench_hg(ctx, n, reps=20):
     }
 
 
+def bench_hg_sharded(h, n, world, rank, reps=20):
+    """BFGS D row-sharded over the ranks (pnol_hg_mpi_d, collective): each rank streams its
+    rows of D and the row shards of p are allgathered.  Returns the whole-job rate
+    (8 n^2 + 16 n bytes / max-over-ranks time, allgather included)."""
+    import ctypes as C
+    import torch
+    import torch.distributed as dist
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    rb, rc = C.c_int(), C.c_int()
+    L.check(L.lib().pnol_bfgs_rows(n, world, rank, C.byref(rb), C.byref(rc)), "bfgs_rows")
+    D = torch.randn(max(rc.value, 1), n, dtype=torch.float64, device="cuda")
+    g = torch.randn(n, dtype=torch.float64, device="cuda")
+    p = torch.empty(n, dtype=torch.float64, device="cuda")
+
+    def once():
+        L.check(L.lib().pnol_hg_mpi_d(h, D.data_ptr(), n, g.data_ptr(), p.data_ptr(), n), "hg_mpi")
+
+    for _ in range(3):
+        once()
+    L.check(L.lib().pnol_ctx_synchronize(h), "sync")
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        once()
+    L.check(L.lib().pnol_ctx_synchronize(h), "sync")
+    t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=_red_dev())
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = float(t.item())
+    del D
+    torch.cuda.empty_cache()
+    byts = 8.0 * n * n + 16.0 * n
+    return {"n": n, "ranks": world, "rows_per_rank": rc.value, "hg_us": t * 1e6, "hg_GBps_whole_job": byts / t / 1e9,
+            "note": "host-timed (allgather included), warm cache; per-rank HBM share 1/P of D"}
+
+
 def cpu_baseline(m, n, budget_s=20.0):
     """Oracle (CPU restatement of the reference, 1 thread) on a bounded sample of one LM loop
     trip at (m, n): FD residual evaluations (the n+1 columns), rows of J^T J (the reference's
@@ -185,9 +228,13 @@ def main():
     from parallelnonlinearoptimizationlibrary_amd.dist import env_rank_world, init_rccl
 
     rank, world, local = env_rank_world()
+    if args.host_comm:   # ranks may share the box's GPUs in the rehearsal
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     os.environ["PNOL_DEVICE"] = str(local)
-    if world > 1:
+    if world > 1 and args.host_comm:
+        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    elif world > 1:
         dist.init_process_group("nccl", init_method="env://", rank=rank, world_size=world,
                                 device_id=torch.device("cuda", local))
 
@@ -196,7 +243,11 @@ def main():
     # the C++ drop-in classes run on the process default context: bind its timers
     dctx = C.c_void_p()
     L.check(L.lib().pnol_default_ctx(C.byref(dctx)), "pnol_default_ctx")
-    if world > 1:
+    host_comm = None
+    if world > 1 and args.host_comm:
+        from parallelnonlinearoptimizationlibrary_amd.dist import HostComm
+        host_comm = HostComm(rank, world)
+    elif world > 1:
         class _Ctx:  # RCCL communicator on the solver's context
             h = dctx
         init_rccl(_Ctx, rank, world)
@@ -231,7 +282,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=_red_dev())
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     timers = {k: _timer(L, dctx, k) for k in ("fd_jtj", "fd_jacobian", "fd_ckpt", "linres_eval", "syrk", "syrk_rows",
@@ -240,7 +291,7 @@ def main():
     per_local = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timers.items()}
     if world > 1:
         keys = sorted(per_local)
-        tv = torch.tensor([per_local[k] for k in keys], dtype=torch.float64, device="cuda")
+        tv = torch.tensor([per_local[k] for k in keys], dtype=torch.float64, device=_red_dev())
         dist.all_reduce(tv, op=dist.ReduceOp.MAX)
         per_max = dict(zip(keys, tv.tolist()))
     else:
@@ -248,6 +299,9 @@ def main():
     L.check(L.lib().pnol_ctx_enable_timers(dctx, 0), "timers")
     err = float(np.max(np.abs(X - obj.xstar)) / np.max(np.abs(obj.xstar)))
 
+    hg_sharded = None
+    if world > 1 and not args.no_hg:
+        hg_sharded = bench_hg_sharded(dctx, HG_N, world, rank)
     hg = None
     if rank == 0 and not args.no_hg:
         hg = bench_hg(ctx, HG_N)
@@ -315,7 +369,7 @@ def main():
             # the north star's strong-scaling quantity: sharded FD Jacobian + row exchange
             "fd_jacobian_ms_max_over_ranks": per_max["fd_jacobian"] + per_max["fd_ckpt"] + per_max["allgather"],
             "converged_rel_err_vs_xstar": err,
-            "bfgs_hg": hg, "bfgs_hg_n4096": hg4096 if hg else None,
+            "bfgs_hg": hg, "bfgs_hg_n4096": hg4096 if hg else None, "bfgs_hg_row_sharded": hg_sharded,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

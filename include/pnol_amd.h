@@ -99,6 +99,18 @@ int pnol_bfgs_pass_d(pnol_ctx* ctx, double* D, int ldd, int n,
                      const double* y, const double* g, double* u, double* w, double* v);
 /* D = I (BFGS_with_linesearch.cpp:46-56), or diag(scale) when scale != NULL (BFGS_bnd_linesearch.cpp:65-83) */
 int pnol_set_identity_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale);
+/* BFGS D row-sharded over the communicator (the reference keeps a full D per rank,
+ * BFGS_with_linesearch_MPI.cpp:31-55): rank r holds rows [begin, begin + count) of D
+ * (pnol_bfgs_rows: shards of whole 256-row tiles), stored from Dsh with leading dimension ldd.
+ * Every function below is collective; each rank gets the full n-vectors back, bitwise the
+ * same as the one-GPU pnol_hg_d / pnol_bfgs_pass_d on the whole D (same per-row order, the
+ * column partials of w summed in the same fixed tile order). */
+int pnol_bfgs_rows(int n, int nranks, int rank, int* begin, int* count);
+int pnol_set_identity_rows_d(pnol_ctx* ctx, double* Dsh, int ldd, int n, const double* scale);
+int pnol_hg_mpi_d(pnol_ctx* ctx, const double* Dsh, int ldd, const double* g, double* p, int n);
+int pnol_bfgs_pass_mpi_d(pnol_ctx* ctx, double* Dsh, int ldd, int n, const double* s_p, const double* a_p,
+                         const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
+                         double* v);
 /* Dsub[a][b] = D[idx[a]][idx[b]] for a, b < nsub (idx: device ints, ascending, < n): the
  * free-free block of D handed to the reduced problem, BFGS_with_bnd_linsearch_MPI.cpp:822-843 */
 int pnol_gather_submatrix_d(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub,

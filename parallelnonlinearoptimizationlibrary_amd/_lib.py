@@ -71,6 +71,10 @@ _SIGS = {
     "pnol_bfgs_update_exact_d": (_i, [_vp, _vp, _i, _vp, _vp, _i]),
     "pnol_bfgs_pass_d": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
     "pnol_set_identity_d": (_i, [_vp, _vp, _i, _i, _vp]),
+    "pnol_bfgs_rows": (_i, [_i, _i, _i, C.POINTER(_i), C.POINTER(_i)]),
+    "pnol_set_identity_rows_d": (_i, [_vp, _vp, _i, _i, _vp]),
+    "pnol_hg_mpi_d": (_i, [_vp, _vp, _i, _vp, _vp, _i]),
+    "pnol_bfgs_pass_mpi_d": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
     "pnol_gather_submatrix_d": (_i, [_vp, _vp, _i, _i, _vp, _i, _vp, _i]),
     "pnol_jtj_d": (_i, [_vp, _vp, _i, _i, _i, _d, _vp, _i, _vp]),
     "pnol_jtj_mpi_d": (_i, [_vp, _vp, _i, _i, _i, _d, _vp, _i, _vp]),

@@ -4,6 +4,9 @@
 #include <cstring>
 #include <vector>
 
+#include <algorithm>
+
+#include "pnol_comm.hpp"
 #include "pnol_internal.hpp"
 
 using namespace pnol;
@@ -72,6 +75,86 @@ int pnol_jtj_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
                double* jtj_diag) {
     PNOL_CHECK(set_device(ctx));
     return launch_jtj(ctx, JT, ldjt, m, n, lambda, A, lda, jtj_diag);
+}
+
+// ---- BFGS D row-sharded over the communicator ----------------------------
+static int bfgs_rows_per(int n, int P) {
+    const int per = (n + P - 1) / P;
+    return (per + 255) / 256 * 256;   // whole fused-pass row tiles
+}
+
+}  // extern "C" (reopened below)
+
+extern "C" int pnol_bfgs_rows(int n, int nranks, int rank, int* begin, int* count) {
+    if (n <= 0 || nranks <= 0 || rank < 0 || rank >= nranks || !begin || !count) return PNOL_ERR_ARG;
+    const int per = bfgs_rows_per(n, nranks);
+    *begin = std::min(n, rank * per);
+    *count = std::min(n, *begin + per) - *begin;
+    return PNOL_OK;
+}
+
+namespace {
+
+// part_w of the fused pass: every rank's row tiles, in place (rank r's tiles at r * tiles_per)
+int pass_w_allgather(pnol_ctx* ctx, double* part_w, int n, int nrowt) {
+    (void)nrowt;
+    const int P = comm_size(), r = comm_rank();
+    const size_t cnt = (size_t)(bfgs_rows_per(n, P) / 256) * n;
+    return comm_allgather_device(ctx, part_w + (size_t)r * cnt, part_w, cnt);
+}
+
+// full n-vector from per-rank row shards written in place at global offsets of buf
+// (buf holds P * rows_per doubles), then copied to out
+int rows_allgather(pnol_ctx* ctx, double* buf, int n, double* out) {
+    const int P = comm_size(), r = comm_rank();
+    const size_t per = (size_t)bfgs_rows_per(n, P);
+    PNOL_CHECK(comm_allgather_device(ctx, buf + (size_t)r * per, buf, per));
+    if (out) PNOL_HIP(hipMemcpyAsync(out, buf, sizeof(double) * n, hipMemcpyDeviceToDevice, ctx->stream));
+    return PNOL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pnol_set_identity_rows_d(pnol_ctx* ctx, double* Dsh, int ldd, int n, const double* scale) {
+    PNOL_CHECK(set_device(ctx));
+    int b = 0, c = 0;
+    PNOL_CHECK(pnol_bfgs_rows(n, comm_size(), comm_rank(), &b, &c));
+    return launch_set_identity(ctx, Dsh, ldd, n, scale, b, b + c);
+}
+
+int pnol_hg_mpi_d(pnol_ctx* ctx, const double* Dsh, int ldd, const double* g, double* p, int n) {
+    PNOL_CHECK(set_device(ctx));
+    if (!Dsh || !g || !p || n <= 0 || ldd < n) return PNOL_ERR_ARG;
+    const int P = comm_size();
+    int b = 0, c = 0;
+    PNOL_CHECK(pnol_bfgs_rows(n, P, comm_rank(), &b, &c));
+    ScopedTimer tm(ctx, "hg");
+    void* buf = nullptr;
+    PNOL_CHECK(ws_get(ctx, "hg_rows", sizeof(double) * (size_t)P * bfgs_rows_per(n, P), &buf));
+    double* pb = (double*)buf;
+    if (c > 0) PNOL_CHECK(launch_gemv_neg(ctx, Dsh, ldd, c, n, g, pb + b));   // row i: the whole-matrix order
+    return rows_allgather(ctx, pb, n, p);
+}
+
+int pnol_bfgs_pass_mpi_d(pnol_ctx* ctx, double* Dsh, int ldd, int n, const double* s_p, const double* a_p,
+                         const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
+                         double* v) {
+    PNOL_CHECK(set_device(ctx));
+    const int P = comm_size();
+    int b = 0, c = 0;
+    PNOL_CHECK(pnol_bfgs_rows(n, P, comm_rank(), &b, &c));
+    ScopedTimer tm(ctx, "bfgs_pass");
+    const size_t span = (size_t)P * bfgs_rows_per(n, P);
+    void *ub = nullptr, *vb = nullptr;
+    PNOL_CHECK(ws_get(ctx, "pass_rows_u", sizeof(double) * span, &ub));
+    PNOL_CHECK(ws_get(ctx, "pass_rows_v", sizeof(double) * span, &vb));
+    PNOL_CHECK(launch_bfgs_pass(ctx, Dsh, ldd, n, s_p, a_p, b_p, write_back, y, g, u ? (double*)ub : nullptr, w,
+                                v ? (double*)vb : nullptr, b, b + c, P > 1 ? pass_w_allgather : nullptr));
+    if (u) PNOL_CHECK(rows_allgather(ctx, (double*)ub, n, u));
+    if (v) PNOL_CHECK(rows_allgather(ctx, (double*)vb, n, v));
+    return PNOL_OK;
 }
 
 int pnol_jtj_mpi_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,

@@ -206,7 +206,7 @@ void BFGSBnd_MPI::boundaryAssessment(double& F, vector<double>& X, vector<double
             XR.push_back(X[i]); gR.push_back(dFdX[i]); lbR.push_back(Xlb[i]); ubR.push_back(Xub[i]);
             dXR.push_back(dX[i]); idx.push_back(i);
         }
-    DenseInverseHessian DR(require_ctx(), nr, updateMode);
+    DenseInverseHessian DR(require_ctx(), nr, updateMode, true);
     DR.setSubmatrixOf(D, idx);
     recurFlag = true;
     mainBFGSLoop(FRecur, XR, gR, DR, lbR, ubR, dXR, cX, cI, optimFlag, recurFlag);
@@ -299,7 +299,7 @@ void BFGSBnd_MPI::findMinBnd(vector<double>& X, vector<double>& Xlb, vector<doub
     std::vector<double> cX(n, 0.0), dX(n, dXGrad), dFdX(n, 0.0);
     std::vector<bool> cI(n, false);
     checkBoxBounds(X, Xlb, Xub);
-    DenseInverseHessian D(require_ctx(), n, updateMode);
+    DenseInverseHessian D(require_ctx(), n, updateMode, true);   // row-sharded over the ranks
     if (initHessFD) init_from_fd_hessian(objPtr, X, dXHess, D);
     else D.setIdentity();
     objPtr->gradientApproximationMPI(X, dX, dFdX);

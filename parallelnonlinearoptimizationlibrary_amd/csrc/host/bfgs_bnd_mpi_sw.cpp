@@ -286,7 +286,7 @@ void BFGS_Bnd_MPI_SW::boundaryAssessment(double& F, vector<double>& X, vector<do
                 ubR.push_back(Xub[icur]); dXR.push_back(dX[icur]);
             }
         // the reduced problem starts along steepest descent (scaled if a scaling was set)
-        DenseInverseHessian DR(require_ctx(), nr, updateMode);
+        DenseInverseHessian DR(require_ctx(), nr, updateMode, true);
         if (!initialScalingVec.empty()) {
             std::vector<double> scaleR;
             for (int i = 0; i < Ndim; ++i) if (!cI[i]) scaleR.push_back(initialScalingVec[i]);
@@ -384,7 +384,7 @@ void BFGS_Bnd_MPI_SW::findMinBnd(vector<double>& X, vector<double>& Xlb, vector<
     std::vector<bool> cI(n, false);
     if (!dXGradVec.empty())
         for (int i = 0; i < n; ++i) dX[i] = dXGradVec[i];
-    DenseInverseHessian D(require_ctx(), n, updateMode);
+    DenseInverseHessian D(require_ctx(), n, updateMode, true);   // row-sharded over the ranks
     if (initHessFD) init_from_fd_hessian(objPtr, X, dXHess, D);
     else if (!initialScalingVec.empty()) D.setIdentity(&initialScalingVec);
     else D.setIdentity();

@@ -145,7 +145,7 @@ void BFGS_MPI::findMin(vector<double>& X, double& f0, double& fOpt) {
     const int n = (int)X.size();
     const int rank = comm_rank();
     pnol_ctx* ctx = require_ctx();
-    DenseInverseHessian D(ctx, n, updateMode);
+    DenseInverseHessian D(ctx, n, updateMode, true);   // row-sharded over the ranks
     if (initHessFD) {
         init_from_fd_hessian(objPtr, X, dXHess, D);
     } else {

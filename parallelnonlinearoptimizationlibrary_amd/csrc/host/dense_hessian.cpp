@@ -2,39 +2,61 @@
 #include "dense_hessian.hpp"
 
 #include <cmath>
+#include <cstdlib>
 
 #include "PNOL_Objective.hpp"
 
 namespace pnol {
 
-DenseInverseHessian::DenseInverseHessian(pnol_ctx* ctx, int n, int mode)
+static bool shard_enabled() {
+    const char* e = std::getenv("PNOL_BFGS_SHARD");
+    return !e || std::atoi(e) != 0;
+}
+
+DenseInverseHessian::DenseInverseHessian(pnol_ctx* ctx, int n, int mode, bool shard)
     : ctx_(ctx), n_(n), ld_(even_ld(n)), exact_(mode == 1 || (mode == 0 && n <= PNOL_SEQ_MAX)) {
-    D_.reset(ctx, (size_t)n * ld_);
+    rb_ = 0;
+    rc_ = n;
+    if (shard && !exact_ && comm_size() > 1 && shard_enabled()) {
+        sharded_ = true;
+        check(pnol_bfgs_rows(n, comm_size(), comm_rank(), &rb_, &rc_), "bfgs_rows");
+    }
+    D_.reset(ctx, (size_t)(rc_ > 0 ? rc_ : 1) * ld_);
     y_.reset(ctx, n); s_.reset(ctx, n); g_.reset(ctx, n);
     u_.reset(ctx, n); w_.reset(ctx, n); v_.reset(ctx, n);
     if (!exact_) { ps_.reset(ctx, n); pa_.reset(ctx, n); pb_.reset(ctx, n); }
 }
 
 void DenseInverseHessian::setIdentity(const std::vector<double>* diagScale) {
+    const double* scale = nullptr;
     if (diagScale) {
         g_.upload(diagScale->data(), (size_t)n_);
-        check(pnol_set_identity_d(ctx_, D_.get(), ld_, n_, g_.get()), "set_identity");
-    } else {
-        check(pnol_set_identity_d(ctx_, D_.get(), ld_, n_, nullptr), "set_identity");
+        scale = g_.get();
     }
+    if (sharded_) check(pnol_set_identity_rows_d(ctx_, D_.get(), ld_, n_, scale), "set_identity");
+    else check(pnol_set_identity_d(ctx_, D_.get(), ld_, n_, scale), "set_identity");
     pending_ = false;
 }
 
 void DenseInverseHessian::setMatrix(const std::vector<std::vector<double>>& D) {
-    std::vector<double> h((size_t)n_ * ld_, 0.0);
-    for (int i = 0; i < n_; ++i)
-        for (int j = 0; j < n_; ++j) h[(size_t)i * ld_ + j] = D[i][j];
+    std::vector<double> h((size_t)(rc_ > 0 ? rc_ : 1) * ld_, 0.0);
+    for (int i = 0; i < rc_; ++i)
+        for (int j = 0; j < n_; ++j) h[(size_t)i * ld_ + j] = D[rb_ + i][j];
     D_.upload(h.data(), h.size());
     pending_ = false;
 }
 
 void DenseInverseHessian::setSubmatrixOf(DenseInverseHessian& src, const std::vector<int>& idx) {
     if ((int)idx.size() != n_) throw std::runtime_error("setSubmatrixOf: index count != n");
+    if (sharded_ || src.sharded_) {
+        // rare (boundary recursion): through the host, every rank holding the whole source
+        std::vector<std::vector<double>> full, sub(n_, std::vector<double>(n_));
+        src.getMatrix(full);
+        for (int a = 0; a < n_; ++a)
+            for (int b = 0; b < n_; ++b) sub[a][b] = full[idx[a]][idx[b]];
+        setMatrix(sub);
+        return;
+    }
     src.materialize();
     DevVec di(ctx_, (idx.size() + 1) / 2);   // ints in a double-sized device buffer
     check(pnol_memcpy_h2d(ctx_, di.get(), idx.data(), sizeof(int) * idx.size()), "h2d");
@@ -44,35 +66,51 @@ void DenseInverseHessian::setSubmatrixOf(DenseInverseHessian& src, const std::ve
     pending_ = false;
 }
 
+int DenseInverseHessian::pass(const double* sp, const double* ap, const double* bp, int wb, const double* y,
+                              const double* g, double* u, double* w, double* v) {
+    if (sharded_) return pnol_bfgs_pass_mpi_d(ctx_, D_.get(), ld_, n_, sp, ap, bp, wb, y, g, u, w, v);
+    return pnol_bfgs_pass_d(ctx_, D_.get(), ld_, n_, sp, ap, bp, wb, y, g, u, w, v);
+}
+
 void DenseInverseHessian::materialize() {
     if (!pending_) return;
-    check(pnol_bfgs_pass_d(ctx_, D_.get(), ld_, n_, ps_.get(), pa_.get(), pb_.get(), 1, nullptr, nullptr, u_.get(),
-                           w_.get(), v_.get()),
+    check(pass(ps_.get(), pa_.get(), pb_.get(), 1, nullptr, nullptr, u_.get(), w_.get(), v_.get()),
           "bfgs_pass(materialize)");
     pending_ = false;
 }
 
 void DenseInverseHessian::getMatrix(std::vector<std::vector<double>>& D) {
     materialize();
-    std::vector<double> h((size_t)n_ * ld_);
-    D_.download(h.data(), h.size());
     D.assign(n_, std::vector<double>(n_));
+    if (!sharded_) {
+        std::vector<double> h((size_t)n_ * ld_);
+        D_.download(h.data(), h.size());
+        for (int i = 0; i < n_; ++i)
+            for (int j = 0; j < n_; ++j) D[i][j] = h[(size_t)i * ld_ + j];
+        return;
+    }
+    // every rank's rows, padded to the shard size, through the host allgather
+    int b0 = 0, per = 0;
+    check(pnol_bfgs_rows(n_, comm_size(), 0, &b0, &per), "bfgs_rows");
+    std::vector<double> mine((size_t)per * ld_, 0.0), all((size_t)per * ld_ * comm_size());
+    if (rc_ > 0) D_.download(mine.data(), (size_t)rc_ * ld_);
+    check(comm_allgather_host(ctx_, mine.data(), all.data(), mine.size()), "allgather(D)");
     for (int i = 0; i < n_; ++i)
-        for (int j = 0; j < n_; ++j) D[i][j] = h[(size_t)i * ld_ + j];
+        for (int j = 0; j < n_; ++j) D[i][j] = all[(size_t)i * ld_ + j];   // rank r's rows start at r * per
 }
 
 void DenseInverseHessian::direction(const std::vector<double>& g, std::vector<double>& p) {
     p.resize(n_);
     g_.upload(g);
     if (!pending_) {
-        check(pnol_hg_d(ctx_, D_.get(), ld_, g_.get(), v_.get(), n_), "hg");
+        if (sharded_) check(pnol_hg_mpi_d(ctx_, D_.get(), ld_, g_.get(), v_.get(), n_), "hg");
+        else check(pnol_hg_d(ctx_, D_.get(), ld_, g_.get(), v_.get(), n_), "hg");
         v_.download(p);   // v = -D g
         return;
     }
     // read-only pass over the stored D, then fold the pending correction in algebraically:
     // (D + s a^T + b s^T) g = D g + s (a.g) + b (s.g)
-    check(pnol_bfgs_pass_d(ctx_, D_.get(), ld_, n_, nullptr, nullptr, nullptr, 0, nullptr, g_.get(), u_.get(),
-                           w_.get(), v_.get()),
+    check(pass(nullptr, nullptr, nullptr, 0, nullptr, g_.get(), u_.get(), w_.get(), v_.get()),
           "bfgs_pass(direction)");
     std::vector<double> v(n_);
     v_.download(v);
@@ -92,9 +130,8 @@ void DenseInverseHessian::update(const std::vector<double>& y, const std::vector
     y_.upload(y);
     if (gnext) g_.upload(*gnext);
     // one pass: fold the pending correction in (write-back) and form D y, D^T y, D g_next
-    check(pnol_bfgs_pass_d(ctx_, D_.get(), ld_, n_, pending_ ? ps_.get() : nullptr, pending_ ? pa_.get() : nullptr,
-                           pending_ ? pb_.get() : nullptr, pending_ ? 1 : 0, y_.get(), gnext ? g_.get() : nullptr,
-                           u_.get(), w_.get(), v_.get()),
+    check(pass(pending_ ? ps_.get() : nullptr, pending_ ? pa_.get() : nullptr, pending_ ? pb_.get() : nullptr,
+               pending_ ? 1 : 0, y_.get(), gnext ? g_.get() : nullptr, u_.get(), w_.get(), v_.get()),
           "bfgs_pass(update)");
     std::vector<double> u(n_), w(n_), v;
     u_.download(u);

@@ -8,6 +8,10 @@
 //         the pending correction into D (write-back), and returns u = D y, w = D^T y and
 //         v = D g_next, from which the next correction and the next direction follow with
 //         O(n) vector algebra: 16 n^2 bytes of HBM traffic per BFGS iteration.
+// Row-sharded (fast mode, shard requested, more than one rank): each rank keeps
+// rows [rb, rb + rc) of D and the passes / H.g run on those rows only, the full n-vectors
+// assembled by allgathers (pnol_*_mpi_d) -- bitwise the one-GPU results, 1/P of the HBM
+// traffic per rank.
 #pragma once
 
 #include <vector>
@@ -20,8 +24,10 @@ namespace pnol {
 
 class DenseInverseHessian {
   public:
-    // mode: 0 auto (exact for n <= PNOL_SEQ_MAX), 1 exact, 2 fast
-    DenseInverseHessian(pnol_ctx* ctx, int n, int mode);
+    // mode: 0 auto (exact for n <= PNOL_SEQ_MAX), 1 exact, 2 fast; shard: row-shard D over the
+    // communicator when in fast mode with more than one rank (PNOL_BFGS_SHARD=0 disables)
+    DenseInverseHessian(pnol_ctx* ctx, int n, int mode, bool shard = false);
+    bool sharded() const { return sharded_; }
     int n() const { return n_; }
     bool exact() const { return exact_; }
 
@@ -39,10 +45,14 @@ class DenseInverseHessian {
 
   private:
     void materialize();   // fold a pending correction into D
+    int pass(const double* sp, const double* ap, const double* bp, int wb, const double* y, const double* g, double* u,
+             double* w, double* v);
 
     pnol_ctx* ctx_;
     int n_, ld_;
     bool exact_;
+    bool sharded_ = false;
+    int rb_ = 0, rc_ = 0;              // this rank's rows of D (all rows when not sharded)
     DevVec D_;
     DevVec y_, s_, g_, u_, w_, v_;     // staging vectors
     DevVec ps_, pa_, pb_;              // pending correction (fast mode)

@@ -347,10 +347,10 @@ __device__ __forceinline__ double butterfly16(double (&v)[16], int lane) {
 
 template <bool VEC>
 __device__ __forceinline__ void pass_load(double2 (&d)[kGroup], const double* __restrict__ D, long ldd, int n, int r0,
-                                          int colc) {
+                                          int colc, int rlast) {
 #pragma unroll
     for (int q = 0; q < kGroup; ++q) {
-        const long row = min(r0 + q, n - 1);
+        const long row = min(r0 + q, rlast);
         if (VEC) {
             // non-temporal: D is streamed once per pass (MI355X: ~1.6x the HBM rate of
             // cached loads for this access pattern, tools/sweep_hg.py)
@@ -367,16 +367,20 @@ __device__ __forceinline__ void pass_load(double2 (&d)[kGroup], const double* __
 // Rows of a 256-row tile are visited in groups of 8 starting at a tile-dependent group
 // (rotation: concurrently running tiles read different HBM channels); the next group's
 // 16-byte loads are issued before the current group is reduced (register double buffer).
+// Row shard form (BFGS D row-sharded over the ranks): D holds rows [rb, re) of the n x n
+// matrix (rb a multiple of kPassRows); row tiles, partial indices and outputs use global rows,
+// so every partial is the one the whole-matrix pass (rb = 0, re = n) would produce.
 template <bool PEND, bool WB, bool VEC>
-__global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ D, long ldd, int n,
+__global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ Dsh, long ldd, int n, int rb, int re,
                                                    const double* __restrict__ sp, const double* __restrict__ ap,
                                                    const double* __restrict__ bp, const double* __restrict__ y,
                                                    const double* __restrict__ g, double* __restrict__ part_u,
                                                    double* __restrict__ part_v, double* __restrict__ part_w) {
+    double* __restrict__ D = Dsh - (long)rb * ldd;   // global-row view (only rows [rb, re) touched)
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int ncolt = (n + kPassCols - 1) / kPassCols;
-    const int rt = blockIdx.x / ncolt;            // row tile
+    const int rt = rb / kPassRows + blockIdx.x / ncolt;   // global row tile
     const int ct = blockIdx.x % ncolt;            // column tile
     const int strip = ct * 4 + wave;              // 128-column strip index
     const int col = strip * 128 + 2 * lane;       // this lane's first column
@@ -395,21 +399,21 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ D, long 
     double w0 = 0.0, w1 = 0.0;
 
     const int r_begin = rt * kPassRows;
-    const int r_end = min(n, r_begin + kPassRows);
+    const int r_end = min(re, r_begin + kPassRows);
     const int ngroups = (r_end - r_begin + kGroup - 1) / kGroup;
     int grp = rt % ngroups;
     double2 cur[kGroup];
-    pass_load<VEC>(cur, D, ldd, n, r_begin + grp * kGroup, colc);
+    pass_load<VEC>(cur, D, ldd, n, r_begin + grp * kGroup, colc, r_end - 1);
     for (int t = 0; t < ngroups; ++t) {
         const int r0 = r_begin + grp * kGroup;
         const int gnext = (grp + 1 == ngroups) ? 0 : grp + 1;
         double2 nxt[kGroup];
-        if (t + 1 < ngroups) pass_load<VEC>(nxt, D, ldd, n, r_begin + gnext * kGroup, colc);
+        if (t + 1 < ngroups) pass_load<VEC>(nxt, D, ldd, n, r_begin + gnext * kGroup, colc, r_end - 1);
         double yr[kGroup], sr[kGroup], br[kGroup];
 #pragma unroll
         for (int q = 0; q < kGroup; ++q) {
-            const int row = min(r0 + q, n - 1);
-            yr[q] = (r0 + q < n) ? y[row] : 0.0;
+            const int row = min(r0 + q, r_end - 1);
+            yr[q] = (r0 + q < r_end) ? y[row] : 0.0;
             if (PEND) { sr[q] = sp[row]; br[q] = bp[row]; }
         }
         double vals[16];
@@ -423,7 +427,7 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ D, long 
             }
             if (!c0ok) { e0 = o0; }
             if (!c1ok) { e1 = o1; }
-            if (WB && r0 + q < n && c0ok) {
+            if (WB && r0 + q < r_end && c0ok) {
                 double* dst = D + (long)(r0 + q) * ldd + col;
                 if (VEC) {
                     __builtin_nontemporal_store(e0, dst);
@@ -443,7 +447,7 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ D, long 
         if ((lane & 3) == 0) {
             const int idx = ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
             const int row = r0 + (idx & 7);
-            if (row < n) {
+            if (row < r_end) {
                 if (idx < 8) part_u[(long)strip * n + row] = red;
                 else part_v[(long)strip * n + row] = red;
             }
@@ -462,7 +466,8 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ D, long 
 __global__ __launch_bounds__(256) void k_bfgs_pass_finish(int n, int nstrips, int nrowt, const double* __restrict__ part_u,
                                                           const double* __restrict__ part_v,
                                                           const double* __restrict__ part_w, double* __restrict__ u,
-                                                          double* __restrict__ v, double* __restrict__ w) {
+                                                          double* __restrict__ v, double* __restrict__ w, int ub,
+                                                          int ue) {
     __shared__ double red[3][4][64];
     const int il = threadIdx.x & 63, q = threadIdx.x >> 6;
     const int i = blockIdx.x * 64 + il;
@@ -480,16 +485,18 @@ __global__ __launch_bounds__(256) void k_bfgs_pass_finish(int n, int nstrips, in
     red[2][q][il] = sw;
     __syncthreads();
     if (q == 0 && i < n) {
-        if (u) u[i] = (red[0][0][il] + red[0][1][il]) + (red[0][2][il] + red[0][3][il]);
-        if (v) v[i] = (red[1][0][il] + red[1][1][il]) + (red[1][2][il] + red[1][3][il]);
+        const bool mine = i >= ub && i < ue;   // u, v: this shard's rows only
+        if (u && mine) u[i] = (red[0][0][il] + red[0][1][il]) + (red[0][2][il] + red[0][3][il]);
+        if (v && mine) v[i] = (red[1][0][il] + red[1][1][il]) + (red[1][2][il] + red[1][3][il]);
         if (w) w[i] = (red[2][0][il] + red[2][1][il]) + (red[2][2][il] + red[2][3][il]);
     }
 }
 
-__global__ void k_set_identity(double* __restrict__ D, long ldd, int n, const double* __restrict__ scale) {
-    long total = (long)n * ldd;
+// rows [rb, rb + nrows) of the identity (or diag(scale)), stored from D
+__global__ void k_set_identity(double* __restrict__ D, long ldd, int nrows, int rb, const double* __restrict__ scale) {
+    long total = (long)nrows * ldd;
     for (long k = (long)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += (long)gridDim.x * blockDim.x) {
-        long i = k / ldd, j = k % ldd;
+        long i = rb + k / ldd, j = k % ldd;
         double v = 0.0;
         if (i == j) v = scale ? scale[i] : 1.0;
         D[k] = v;
@@ -586,54 +593,66 @@ int launch_bfgs_update_exact(pnol_ctx* ctx, double* D, int ldd, const double* y,
     return launch_check();
 }
 
+// Whole matrix (rb = 0, re = n) or the row shard [rb, re) (rb a multiple of kPassRows).  With a
+// shard, pw_gather (non-null) runs between the pass and the finish: it must fill part_w with
+// every rank's row tiles (the LevMarq/BFGS communicator's allgather), and u / v come out for
+// rows [rb, re) only.
 int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p, const double* a_p,
                      const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
-                     double* v) {
-    if (!D || n <= 0 || ldd < n) return PNOL_ERR_ARG;
+                     double* v, int rb, int re, int (*pw_gather)(pnol_ctx*, double*, int, int)) {
+    if (re < 0) re = n;
+    if (!D || n <= 0 || ldd < n || rb < 0 || re > n || rb > re || (rb < re && rb % kPassRows)) return PNOL_ERR_ARG;
     const bool pend = s_p != nullptr;
     if (pend && (!a_p || !b_p)) return PNOL_ERR_ARG;
     const int ncolt = (n + kPassCols - 1) / kPassCols;
     const int nrowt = (n + kPassRows - 1) / kPassRows;
     const int nstrips = ncolt * 4;
+    const int myrowt = (re - rb + kPassRows - 1) / kPassRows;
     void *pu = nullptr, *pv = nullptr, *pw = nullptr, *zeros = nullptr;
     PNOL_CHECK(ws_get(ctx, "pass_part_u", sizeof(double) * (size_t)nstrips * n, &pu));
     PNOL_CHECK(ws_get(ctx, "pass_part_v", sizeof(double) * (size_t)nstrips * n, &pv));
-    PNOL_CHECK(ws_get(ctx, "pass_part_w", sizeof(double) * (size_t)nrowt * n, &pw));
+    // room for the allgather's padded layout: nranks * (tiles per rank) >= nrowt tiles
+    PNOL_CHECK(ws_get(ctx, "pass_part_w", sizeof(double) * (size_t)(nrowt + 64) * n, &pw));
     if (!y || !g) {
         PNOL_CHECK(ws_get(ctx, "pass_zeros", sizeof(double) * (size_t)n, &zeros));
         PNOL_CHECK(launch_fill(ctx, (double*)zeros, (size_t)n, 0.0));
         if (!y) y = (const double*)zeros;
         if (!g) g = (const double*)zeros;
     }
-    dim3 grd(nrowt * ncolt), blk(256);
     auto* P0 = (double*)pu; auto* P1 = (double*)pv; auto* P2 = (double*)pw;
-    const bool vec = (ldd % 2 == 0) && aligned16(D);
-#define PNOL_PASS(PE, W, V)                                                                                    \
-    hipLaunchKernelGGL((k_bfgs_pass<PE, W, V>), grd, blk, 0, ctx->stream, D, (long)ldd, n, s_p, a_p, b_p, y, g, \
-                       P0, P1, P2)
-    if (vec) {
-        if (pend && write_back) PNOL_PASS(true, true, true);
-        else if (pend) PNOL_PASS(true, false, true);
-        else if (write_back) PNOL_PASS(false, true, true);
-        else PNOL_PASS(false, false, true);
-    } else {
-        if (pend && write_back) PNOL_PASS(true, true, false);
-        else if (pend) PNOL_PASS(true, false, false);
-        else if (write_back) PNOL_PASS(false, true, false);
-        else PNOL_PASS(false, false, false);
-    }
+    if (myrowt > 0) {
+        dim3 grd(myrowt * ncolt), blk(256);
+        const bool vec = (ldd % 2 == 0) && aligned16(D);
+#define PNOL_PASS(PE, W, V)                                                                                        \
+    hipLaunchKernelGGL((k_bfgs_pass<PE, W, V>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb, re, s_p, a_p, b_p, y, \
+                       g, P0, P1, P2)
+        if (vec) {
+            if (pend && write_back) PNOL_PASS(true, true, true);
+            else if (pend) PNOL_PASS(true, false, true);
+            else if (write_back) PNOL_PASS(false, true, true);
+            else PNOL_PASS(false, false, true);
+        } else {
+            if (pend && write_back) PNOL_PASS(true, true, false);
+            else if (pend) PNOL_PASS(true, false, false);
+            else if (write_back) PNOL_PASS(false, true, false);
+            else PNOL_PASS(false, false, false);
+        }
 #undef PNOL_PASS
-    PNOL_CHECK(launch_check());
+        PNOL_CHECK(launch_check());
+    }
+    if (pw_gather) PNOL_CHECK(pw_gather(ctx, P2, n, nrowt));
     hipLaunchKernelGGL(k_bfgs_pass_finish, dim3((n + 63) / 64), dim3(256), 0, ctx->stream, n, nstrips, nrowt,
-                       (const double*)P0, (const double*)P1, (const double*)P2, u, v, w);
+                       (const double*)P0, (const double*)P1, (const double*)P2, u, v, w, rb, re);
     return launch_check();
 }
 
-int launch_set_identity(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale) {
-    if (!D || n <= 0 || ldd < n) return PNOL_ERR_ARG;
-    long total = (long)n * ldd;
+int launch_set_identity(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale, int rb, int re) {
+    if (re < 0) re = n;
+    if (!D || n <= 0 || ldd < n || rb < 0 || re > n || rb > re) return PNOL_ERR_ARG;
+    if (re == rb) return PNOL_OK;
+    long total = (long)(re - rb) * ldd;
     int blocks = (int)std::min<long>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(k_set_identity, dim3(blocks), dim3(256), 0, ctx->stream, D, (long)ldd, n, scale);
+    hipLaunchKernelGGL(k_set_identity, dim3(blocks), dim3(256), 0, ctx->stream, D, (long)ldd, re - rb, rb, scale);
     return launch_check();
 }
 

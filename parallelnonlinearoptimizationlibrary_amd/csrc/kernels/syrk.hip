@@ -271,26 +271,50 @@ __global__ void k_syrk_unpack(const double* __restrict__ packed, int ntiles, int
     }
 }
 
-__global__ void k_syrk_reduce(const double* __restrict__ part, int ntiles, int split_k, int n, double lambda,
-                              double* __restrict__ A, long lda, double* __restrict__ diag_out, int tile0) {
-    const int t = tile0 + blockIdx.y;   // part holds this launch's tiles from tile0 on
+// One 32 x 128 strip of a tile per workgroup (blockIdx.x = strip 0..3, blockIdx.y = tile):
+// sums the split-K partials in slice order (coalesced 16-byte reads), writes the lower part
+// row-wise, and writes the mirror from an LDS transpose so those stores are row-wise too.
+__global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ part, int ntiles, int split_k, int n,
+                                                     double lambda, double* __restrict__ A, long lda,
+                                                     double* __restrict__ diag_out, int tile0) {
+    constexpr int SR = 32;                                 // strip rows
+    __shared__ double st[SR][kTile + 1];
+    const int t = tile0 + blockIdx.y;                      // part holds this launch's tiles from tile0 on
     int ti, tj;
     tile_of(t, ti, tj);
     const double scale = 1 + lambda;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < kTile * kTile; e += gridDim.x * blockDim.x) {
-        const int r = e / kTile, c = e % kTile;
-        const int i = ti * kTile + r, j = tj * kTile + c;
-        if (i >= n || j >= n || j > i) continue;
-        const double* p = part + ((long)(t - tile0) * split_k) * kTile * kTile + e;
-        double v = 0.0;
-        for (int s = 0; s < split_k; ++s) v += p[(long)s * kTile * kTile];
-        if (i == j) {
-            if (diag_out) diag_out[i] = v;
-            A[(long)i * lda + i] = scale * v;
-        } else {
-            A[(long)i * lda + j] = v;
-            A[(long)j * lda + i] = v;
+    const int r0 = blockIdx.x * SR;
+    const double* p = part + ((long)(t - tile0) * split_k) * kTile * kTile + (long)r0 * kTile;
+    // 32 x 128 doubles = 2048 double2; 256 threads x 8
+    for (int q = threadIdx.x; q < SR * kTile / 2; q += 256) {
+        const int r = (2 * q) / kTile, c = (2 * q) % kTile;
+        double2 v = make_double2(0.0, 0.0);
+        for (int s2 = 0; s2 < split_k; ++s2) {
+            const double2 w = reinterpret_cast<const double2*>(p + (long)s2 * kTile * kTile)[q];
+            v.x += w.x;
+            v.y += w.y;
         }
+        st[r][c] = v.x;
+        st[r][c + 1] = v.y;
+        const int i = ti * kTile + r0 + r;
+        for (int h = 0; h < 2; ++h) {
+            const int j = tj * kTile + c + h;
+            const double val = h ? v.y : v.x;
+            if (i >= n || j >= n || j > i) continue;
+            if (i == j) {
+                if (diag_out) diag_out[i] = val;
+                A[(long)i * lda + i] = scale * val;
+            } else {
+                A[(long)i * lda + j] = val;
+            }
+        }
+    }
+    __syncthreads();
+    // mirror: A[j][i] = tile[i][j] for j > i; row j of A gets 32 consecutive columns i
+    for (int q = threadIdx.x; q < SR * kTile; q += 256) {
+        const int c = q / SR, r = q % SR;                  // consecutive threads: consecutive i
+        const int i = ti * kTile + r0 + r, j = tj * kTile + c;
+        if (i < n && j < n && j < i) A[(long)j * lda + i] = st[r][c];
     }
 }
 
@@ -417,7 +441,7 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     }
     PNOL_CHECK(launch_check());
     ScopedTimer tm(ctx, "syrk_reduce");
-    hipLaunchKernelGGL(k_syrk_reduce, dim3(8, ntiles), dim3(256), 0, ctx->stream, (const double*)part, ntiles,
+    hipLaunchKernelGGL(k_syrk_reduce, dim3(kTile / 32, ntiles), dim3(256), 0, ctx->stream, (const double*)part, ntiles,
                        split_k, n, lambda, A, (long)lda, jtj_diag, 0);
     return launch_check();
 }
@@ -440,7 +464,7 @@ int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldj
                            m, split_k, kchunk, mypart, (double*)nullptr, 0L, 1.0, 0.0, t0);
     }
     PNOL_CHECK(launch_check());
-    hipLaunchKernelGGL(k_syrk_reduce, dim3(8, t1 - t0), dim3(256), 0, stream, (const double*)mypart, t1 - t0, split_k,
+    hipLaunchKernelGGL(k_syrk_reduce, dim3(kTile / 32, t1 - t0), dim3(256), 0, stream, (const double*)mypart, t1 - t0, split_k,
                        n, lambda, A, (long)lda, jtj_diag, t0);
     return launch_check();
 }

@@ -119,8 +119,8 @@ int launch_gemv_neg_seq(pnol_ctx* ctx, const double* A, int lda, int rows, int c
 int launch_bfgs_update_exact(pnol_ctx* ctx, double* D, int ldd, const double* y, const double* s, int n);
 int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p, const double* a_p,
                      const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
-                     double* v);
-int launch_set_identity(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale);
+                     double* v, int rb = 0, int re = -1, int (*pw_gather)(pnol_ctx*, double*, int, int) = nullptr);
+int launch_set_identity(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale, int rb = 0, int re = -1);
 int launch_add(pnol_ctx* ctx, const double* x, const double* y, double* z, int n);
 int launch_gather_sub(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub, double* Dsub,
                       int lds);

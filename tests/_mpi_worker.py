@@ -41,8 +41,32 @@ def main():
     Psw = [1e-4, 0.8, 1e-6, 1, 1e-10, 2, 50, 1e-5, 1e-6, 1e-3, 200, 1e-5, 1e-5, 0, -1]
     Xs, ress = run_bfgs(DeviceObjective(ctx, L.OBJ_ROSENBROCK, 3), [-1.0, 2.0, 2.0], Psw, which=4, lb=[-1.0] * 3,
                         ub=[5.0] * 3)
+    # BFGS D row-sharded: this rank's rows through the collective pass / H.g
+    import ctypes as C
+    nD = 700
+    rng = np.random.default_rng(3)
+    Dfull = rng.standard_normal((nD, nD))
+    g, yv, sv, av, bv = (rng.standard_normal(nD) for _ in range(5))
+    rb, rc = C.c_int(), C.c_int()
+    L.check(L.lib().pnol_bfgs_rows(nD, world, rank, C.byref(rb), C.byref(rc)), "bfgs_rows")
+    rb, rc = rb.value, rc.value
+    Dsh = ctx.tensor(Dfull[rb:rb + rc] if rc > 0 else np.zeros((1, nD)))
+    dg, dy, ds, da, db = (ctx.tensor(a) for a in (g, yv, sv, av, bv))
+    p = ctx.empty(nD)
+    L.check(L.lib().pnol_hg_mpi_d(ctx.h, Dsh.data_ptr(), nD, dg.data_ptr(), p.data_ptr(), nD), "hg_mpi")
+    u, w, v = ctx.empty(nD), ctx.empty(nD), ctx.empty(nD)
+    L.check(L.lib().pnol_bfgs_pass_mpi_d(ctx.h, Dsh.data_ptr(), nD, nD, ds.data_ptr(), da.data_ptr(), db.data_ptr(), 1,
+                                         dy.data_ptr(), dg.data_ptr(), u.data_ptr(), w.data_ptr(), v.data_ptr()),
+            "pass_mpi")
+    ctx.synchronize()
+    # BFGS_MPI, fast mode (fused passes) on the synthetic quadratic with D row-sharded; pool 4
+    nq = 300
+    Pq = [1e-4, 0.9, 4, 1, 1000, 1e-6, 1e-3, 40, 1e-9, 1e-6, 0, 0, 4, 1, 2]
+    Xq, resq = run_bfgs(DeviceObjective.synthetic(ctx, L.OBJ_QUADRATIC, nq), np.zeros(nq), Pq, which=1)
     np.savez(os.path.join(out, f"rank{rank}.npz"), X=X, A=A.cpu().numpy(), diag=diag.cpu().numpy(), Xb=Xb,
-             fb=np.array([resb.fopt]), Xs=Xs, fs=np.array([ress.fopt]))
+             fb=np.array([resb.fopt]), Xs=Xs, fs=np.array([ress.fopt]), hg=p.cpu().numpy(), u=u.cpu().numpy(),
+             w=w.cpu().numpy(), v=v.cpu().numpy(), Drows=Dsh.cpu().numpy()[:rc], rows=np.array([rb, rc]), Xq=Xq,
+             fq=np.array([resq.fopt]))
     comm.close()
     dist.barrier()
     dist.destroy_process_group()

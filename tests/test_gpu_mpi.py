@@ -78,3 +78,32 @@ def test_levmarq_mpi_ranks_bitwise_equal_single(tmp_path, world, oracle):
         z = np.load(tmp_path / f"rank{r}.npz")
         assert np.array_equal(z["Xs"], Xo), r
         assert z["fs"][0] == reso.fopt, r
+    # BFGS D row-sharded: the collective H.g / fused pass equal the whole-matrix kernels bitwise,
+    # and BFGS_MPI in fast mode gives the single-rank trajectory bitwise
+    import torch
+    nD = 700
+    rng = np.random.default_rng(3)
+    Dfull = rng.standard_normal((nD, nD))
+    g, yv, sv, av, bv = (rng.standard_normal(nD) for _ in range(5))
+    dD = ctx.tensor(Dfull)
+    hg = ctx.hg(dD, ctx.tensor(g)).cpu().numpy()
+    u, w, v = (t.cpu().numpy() for t in ctx.bfgs_pass(dD, ctx.tensor(yv), ctx.tensor(g),
+                                                       pending=(ctx.tensor(sv), ctx.tensor(av), ctx.tensor(bv)),
+                                                       write_back=True))
+    Dafter = dD.cpu().numpy()
+    covered = 0
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        assert np.array_equal(z["hg"], hg), r
+        assert np.array_equal(z["u"], u) and np.array_equal(z["w"], w) and np.array_equal(z["v"], v), r
+        rb, rc = z["rows"]
+        assert np.array_equal(z["Drows"], Dafter[rb:rb + rc]), r
+        covered += rc
+    assert covered == nD
+    from parallelnonlinearoptimizationlibrary_amd.device import run_bfgs
+    Pq = [1e-4, 0.9, 4, 1, 1000, 1e-6, 1e-3, 40, 1e-9, 1e-6, 0, 0, 4, 1, 2]
+    Xq1, resq1 = run_bfgs(DeviceObjective.synthetic(ctx, L.OBJ_QUADRATIC, 300), np.zeros(300), Pq, which=1)
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        assert np.array_equal(z["Xq"], Xq1), r
+        assert z["fq"][0] == resq1.fopt, r
