@@ -130,6 +130,27 @@ int pnol_jtj_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
  * Bitwise equal to pnol_jtj_d for any rank count; with one rank it is pnol_jtj_d. */
 int pnol_jtj_mpi_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda,
                    double* A, int lda, double* jtj_diag);
+/* LevMarqMPI on the m-sliced Jacobian.  J^T J and J^T F are summed over
+ * PNOL_LM_SLICES slices of the m residual rows by one fixed tree, so the rows can be split
+ * over up to PNOL_LM_SLICES ranks with bitwise the one-GPU results (pnol_jtj_d / pnol_jtr_d).
+ * Layout: slice s is an n x slice_rows row-major block at JTs + s * n * slice_rows (FD column
+ * j, residual rows [s slice_rows, (s + 1) slice_rows)); jt_elems = PNOL_LM_SLICES * n * slice_rows. */
+#define PNOL_LM_SLICES 8
+int pnol_lm_sliced_layout(int m, int n, int* slice_rows, size_t* jt_elems);
+/* LevenbergMarquardtMPI.cpp:60 + PNOL_Objective.cpp:202-299 (gradientApproximationMPI's column
+ * loop and its MPI_Allreduce): this rank's cost-balanced FD tiles (pnol_fd_tiles) for all
+ * residual rows into JTs, then each m-slice of them to the rank holding that slice (one group of
+ * RCCL point-to-point transfers).  Linear-residual device objectives; compute_f0 as for
+ * pnol_fd_jacobian_tiles_d. */
+int pnol_lm_jacobian_mpi_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0,
+                           int compute_f0, double* JTs);
+/* LevenbergMarquardtMPI.cpp:64-80 from this rank's slices of pnol_lm_jacobian_mpi_d: A = J^T J
+ * with A_ii = (1 + lambda) (J^T J)_ii and rhs = -(J^T F) on every rank.  Partial tiles of the
+ * rank's slices, their tree nodes to each tile's owner (point-to-point), the owners merge, one
+ * allgather.  Bitwise pnol_jtj_d + pnol_jtr_d of the row-major J^T for any rank count
+ * <= PNOL_LM_SLICES.  n > PNOL_SEQ_MAX or m > 4096. */
+int pnol_lm_normal_mpi_d(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F,
+                         double* A, int lda, double* rhs, double* jtj_diag);
 /* rhs = -(J^T F), LevenbergMarquardt.cpp:78-80 */
 int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
 /* sigma = A^{-1} rhs, replacing luSolve(A, rhs, sigma), LevenbergMarquardt.cpp:83.

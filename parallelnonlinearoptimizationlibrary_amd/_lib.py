@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(HERE, "libpnol_amd.so")
 PNOL_OK, PNOL_ERR_ARG, PNOL_ERR_HIP, PNOL_ERR_NOMEM, PNOL_ERR_NODEVICE = 0, 1, 2, 3, 4
 PNOL_ERR_SINGULAR, PNOL_ERR_COMM, PNOL_ERR_UNSUPPORTED = 5, 6, 7
 PNOL_SEQ_MAX = 64
+LM_SLICES = 8          # PNOL_LM_SLICES: m-slices of the LevMarqMPI J^T J / J^T F summation tree
 
 OBJ_ROSENBROCK, OBJ_POWER, OBJ_QUADRATIC = 0, 1, 4
 OBJ_EXPCURVE, OBJ_CUBIC, OBJ_LINRES = 10, 11, 12
@@ -78,6 +79,9 @@ _SIGS = {
     "pnol_gather_submatrix_d": (_i, [_vp, _vp, _i, _i, _vp, _i, _vp, _i]),
     "pnol_jtj_d": (_i, [_vp, _vp, _i, _i, _i, _d, _vp, _i, _vp]),
     "pnol_jtj_mpi_d": (_i, [_vp, _vp, _i, _i, _i, _d, _vp, _i, _vp]),
+    "pnol_lm_sliced_layout": (_i, [_i, _i, C.POINTER(_i), C.POINTER(_sz)]),
+    "pnol_lm_jacobian_mpi_d": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp]),
+    "pnol_lm_normal_mpi_d": (_i, [_vp, _vp, _i, _i, _d, _vp, _vp, _i, _vp, _vp]),
     "pnol_jtr_d": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
     "pnol_solve_d": (_i, [_vp, _vp, _i, _vp, _vp, _i, _i, C.POINTER(_i)]),
     "pnol_solve_async_d": (_i, [_vp, _vp, _i, _vp, _vp, _i, _vp]),

@@ -163,6 +163,28 @@ int pnol_jtj_mpi_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, doub
     return launch_jtj_sharded(ctx, JT, ldjt, m, n, lambda, A, lda, jtj_diag);
 }
 
+int pnol_lm_sliced_layout(int m, int n, int* slice_rows, size_t* jt_elems) {
+    static_assert(PNOL_LM_SLICES == kLmSlices, "slice count");
+    if (m <= 0 || n <= 0) return PNOL_ERR_ARG;
+    const int mS = lm_slice_rows(m);
+    if (slice_rows) *slice_rows = mS;
+    if (jt_elems) *jt_elems = (size_t)kLmSlices * n * mS;
+    return PNOL_OK;
+}
+
+int pnol_lm_jacobian_mpi_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0,
+                           int compute_f0, double* JTs) {
+    PNOL_CHECK(set_device(ctx));
+    if (!obj || !x || !h || !F0 || !JTs || compute_f0 < 0 || compute_f0 > 2) return PNOL_ERR_ARG;
+    return launch_lm_jacobian(ctx, obj, x, h, F0, compute_f0, JTs);
+}
+
+int pnol_lm_normal_mpi_d(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F, double* A,
+                         int lda, double* rhs, double* jtj_diag) {
+    PNOL_CHECK(set_device(ctx));
+    return launch_lm_normal(ctx, JTs, m, n, lambda, F, A, lda, rhs, jtj_diag);
+}
+
 int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs) {
     PNOL_CHECK(set_device(ctx));
     if (!JT || !F || !rhs || m <= 0 || n <= 0 || ldjt < m) return PNOL_ERR_ARG;

@@ -165,11 +165,20 @@ class LMDevice {
 // non-positive Cholesky pivot is redone with the reference-order LU, as pnol_solve_d does.
 // (Queueing trip i+1 before deciding step i was measured: a rejected step then costs a whole
 // wasted trip, and the post-convergence steps of the bench are mostly rejections.)
+//
+// LevMarqMPI (sliced = true) runs the same loop with the Jacobian split by residual-row
+// slices: each rank evaluates its FD column tiles for all rows and sends every m-slice of them
+// to the slice's rank (pnol_lm_jacobian_mpi_d); each rank forms its slices' share of J^T J and
+// J^T F and one reduce-scatter + allgather assemble A and -J^T F on every rank
+// (pnol_lm_normal_mpi_d).  The collectives are queued on the same stream, so the trip still
+// has one host wait; A, rhs and hence the trajectory are bitwise the single-GPU ones.
 class LMAsync {
   public:
-    LMAsync(pnol_ctx* ctx, pnol_dobj* d, int n, int m) : ctx_(ctx), d_(d), n_(n), m_(m), ldjt_(even_ld(m)),
-                                                          lda_(even_ld(n)) {
-        JT_.reset(ctx, (size_t)n * ldjt_);
+    LMAsync(pnol_ctx* ctx, pnol_dobj* d, int n, int m, bool sliced)
+        : ctx_(ctx), d_(d), n_(n), m_(m), ldjt_(even_ld(m)), lda_(even_ld(n)), sliced_(sliced) {
+        size_t jt = (size_t)n * ldjt_;
+        if (sliced) check(pnol_lm_sliced_layout(m, n, nullptr, &jt), "sliced layout");
+        JT_.reset(ctx, jt);
         A_.reset(ctx, (size_t)n * lda_);
         rhs_.reset(ctx, n);
         h_.reset(ctx, n);
@@ -198,10 +207,18 @@ class LMAsync {
 
     // trip at x_[s] (F_[s] = F(x_[s]); ckpt: its checkpoints are current) -> sigma, x_[s^1], F_[s^1]
     void enqueue(int s, double lambda, bool ckpt) {
-        check(pnol_fd_jtj_d(ctx_, d_, x_[s].get(), h_.get(), F_[s].get(), ckpt ? 2 : 1, JT_.get(), ldjt_, lambda,
-                            A_.get(), lda_, nullptr, 1),
-              "fd_jtj");
-        check(pnol_jtr_d(ctx_, JT_.get(), ldjt_, m_, n_, F_[s].get(), rhs_.get()), "jtr");
+        if (sliced_) {
+            check(pnol_lm_jacobian_mpi_d(ctx_, d_, x_[s].get(), h_.get(), F_[s].get(), ckpt ? 2 : 1, JT_.get()),
+                  "fd_jacobian");
+            check(pnol_lm_normal_mpi_d(ctx_, JT_.get(), m_, n_, lambda, F_[s].get(), A_.get(), lda_, rhs_.get(),
+                                       nullptr),
+                  "normal equations");
+        } else {
+            check(pnol_fd_jtj_d(ctx_, d_, x_[s].get(), h_.get(), F_[s].get(), ckpt ? 2 : 1, JT_.get(), ldjt_, lambda,
+                                A_.get(), lda_, nullptr, 1),
+                  "fd_jtj");
+            check(pnol_jtr_d(ctx_, JT_.get(), ldjt_, m_, n_, F_[s].get(), rhs_.get()), "jtr");
+        }
         int* di = reinterpret_cast<int*>(info_[s].get());
         check(pnol_solve_async_d(ctx_, A_.get(), lda_, rhs_.get(), sig_[s].get(), n_, di), "solve");
         finish(s);
@@ -230,6 +247,7 @@ class LMAsync {
     pnol_ctx* ctx_;
     pnol_dobj* d_;
     int n_, m_, ldjt_, lda_;
+    bool sliced_;
     DevVec JT_, A_, rhs_, h_, x_[2], F_[2], sig_[2], info_[2];
     void* pin_[2] = {nullptr, nullptr};
     pnol_event* ev_[2] = {nullptr, nullptr};
@@ -240,12 +258,29 @@ bool lm_async_enabled() {
     return !e || std::atoi(e) != 0;
 }
 
-void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, std::vector<double>& X,
+// The sliced LevMarqMPI form: linear-residual device objectives, up to PNOL_LM_SLICES ranks
+// (PNOL_LM_SLICED=0 keeps the column-sharded general loop)
+bool lm_sliced_ok(pnol_dobj* d) {
+    const char* e = std::getenv("PNOL_LM_SLICED");
+    if (e && std::atoi(e) == 0) return false;
+    int kind = 0, n = 0, m = 0;
+    return pnol_dobj_info(d, &kind, &n, &m) == PNOL_OK && kind == PNOL_OBJ_LINRES && comm_size() <= PNOL_LM_SLICES;
+}
+
+void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool sharded, std::vector<double>& X,
                     std::vector<double>& F0, std::vector<double>& FOpt) {
     const int n = (int)X.size();
     const int m = (int)F0.size();
+    const bool loud = !sharded || comm_rank() == ROOT_ID;
     pnol_ctx* ctx = require_ctx();
-    LMAsync dev(ctx, d, n, m);
+    LMAsync dev(ctx, d, n, m, sharded);
+    int own_cols = n;   // FD columns this rank evaluates per Jacobian (LevMarqMPI: its tiles)
+    if (sharded) {
+        std::vector<int> st, ct;
+        fd_tiles_of(n, comm_size(), comm_rank(), st, ct);
+        own_cols = 0;
+        for (int c : ct) own_cols += c;
+    }
     double lambda = P.lambda0;
     std::vector<double> dX(n, P.dXGrad), F(m), Fnew(m), sigma(n);
     dev.uploadH(dX);
@@ -264,7 +299,7 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, std::v
         dev.enqueue(s, lambda, ckpt);
         dev.wait(s);
         if (dev.info_h(s) != 0) dev.redo_lu(s);
-        obj->countEvals(n + 1);        // the trip's Jacobian
+        obj->countEvals(own_cols + 1); // the trip's Jacobian
         obj->countEvals(1);            // its trial point
         std::memcpy(sigma.data(), dev.sigma_h(s), sizeof(double) * n);
         std::memcpy(Fnew.data(), dev.Fnext_h(s), sizeof(double) * m);
@@ -272,7 +307,7 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, std::v
         nrm = norm2(Fnew);
         chiSq = nrm * nrm;
         if (chiSq >= chiSqPrev || chiSq != chiSq) {
-            if (P.verbose > 1)
+            if (sharded ? (P.verbose >= 1 && loud) : (P.verbose > 1))
                 std::cout << "Step " << iter << " failed with chiSq = " << chiSq << ", chiSqPrev = " << chiSqPrev
                           << ",  increasing lambda: " << lambda << " --> " << lambda * P.lambdaFactor << std::endl;
             chiSq = chiSqPrev;
@@ -287,7 +322,7 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, std::v
             xdiff2Norm = norm2(sigma);
             if (xdiff2Norm < P.xMinDiff) break;
         }
-        if (P.verbose > 0 && iter % 10 == 0) {
+        if ((sharded ? (P.verbose >= 1 && loud) : (P.verbose > 0)) && iter % 10 == 0) {
             std::cout << "At iter = " << iter << " the xdiff 2Norm = " << xdiff2Norm << ", chi^2 = " << chiSq
                       << ", and params: ";
             print_vec(X);
@@ -295,7 +330,7 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, std::v
         iter++;
     }
     FOpt = F;
-    if (P.verbose >= 0) {
+    if (P.verbose >= 0 && loud) {
         std::cout << std::endl << "-----------------------------------------------------------------------------------" << std::endl;
         std::cout << "Completed Levenberg Marquardt." << std::endl;
         std::cout << "At iter = " << iter << " the xdiff 2Norm = " << xdiff2Norm << ", chi^2 = " << chiSq
@@ -311,8 +346,9 @@ void lm_solve(MultiObjective* obj, const LMParams& P, bool sharded, std::vector<
     const int m = (int)F0.size();
     const int rank = sharded ? comm_rank() : 0;
     const bool loud = rank == ROOT_ID;
-    if (!sharded && n > PNOL_SEQ_MAX && lm_async_enabled())
-        if (pnol_dobj* d = obj->deviceObjective()) return lm_solve_async(obj, d, P, X, F0, FOpt);
+    if (n > PNOL_SEQ_MAX && lm_async_enabled())
+        if (pnol_dobj* d = obj->deviceObjective())
+            if (!sharded || lm_sliced_ok(d)) return lm_solve_async(obj, d, P, sharded, X, F0, FOpt);
     pnol_ctx* ctx = require_ctx();
     LMDevice dev(ctx, n, m, sharded ? comm_size() : 1);
 

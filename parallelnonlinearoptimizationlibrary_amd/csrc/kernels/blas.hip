@@ -132,18 +132,19 @@ __global__ __launch_bounds__(256) void k_gemv_neg(const double* __restrict__ A, 
 // fewer concurrent DRAM streams open than with a wave per row.  NT: non-temporal loads
 // (D is streamed once; keep it out of L2 / MALL).  Partial sums are combined in a fixed
 // order through LDS.
-template <int R, bool NT>
-__global__ __launch_bounds__(256) void k_gemv_neg_wg(const double* __restrict__ A, long lda, int rows, int cols,
-                                                     const double* __restrict__ x, double* __restrict__ y) {
+// VEC = false: the same arithmetic with 8-byte loads (rows not 16-byte aligned)
+template <int R, bool NT, bool VEC = true>
+__device__ __forceinline__ void gemv_neg_wg_body(const double* __restrict__ A, long lda, int rows, int cols,
+                                                 const double* __restrict__ x, double* __restrict__ y) {
     __shared__ double part[4][R];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const long row0 = (long)blockIdx.x * R;
     const double2* __restrict__ xv = reinterpret_cast<const double2*>(x);
-    const double2* arow[R];
+    const double* arow[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         long rr = row0 + r < rows ? row0 + r : rows - 1;
-        arow[r] = reinterpret_cast<const double2*>(A + rr * lda);
+        arow[r] = A + rr * lda;
     }
     double acc0[R], acc1[R];
 #pragma unroll
@@ -151,7 +152,9 @@ __global__ __launch_bounds__(256) void k_gemv_neg_wg(const double* __restrict__ 
     const int pairs = cols >> 1;
     constexpr int SC = kU * kWave;
     const int nfull = pairs / SC;
-    auto ld = [&](const double2* p) -> double2 {
+    auto ld = [&](const double* q) -> double2 {
+        if (!VEC) return make_double2(q[0], q[1]);
+        const double2* p = reinterpret_cast<const double2*>(q);
         if (NT) {
             double2 v;
             v.x = __builtin_nontemporal_load(&p->x);
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(256) void k_gemv_neg_wg(const double* __restrict__ 
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int u = 0; u < kU; ++u) cur[r][u] = ld(&arow[r][sc * SC + u * kWave + lane]);
+            for (int u = 0; u < kU; ++u) cur[r][u] = ld(arow[r] + 2 * (sc * SC + u * kWave + lane));
         for (sc += 4; sc < nfull; sc += 4) {
             double2 nxt[R][kU], nxtx[kU];
 #pragma unroll
@@ -176,7 +179,7 @@ __global__ __launch_bounds__(256) void k_gemv_neg_wg(const double* __restrict__ 
 #pragma unroll
             for (int r = 0; r < R; ++r)
 #pragma unroll
-                for (int u = 0; u < kU; ++u) nxt[r][u] = ld(&arow[r][sc * SC + u * kWave + lane]);
+                for (int u = 0; u < kU; ++u) nxt[r][u] = ld(arow[r] + 2 * (sc * SC + u * kWave + lane));
             gemv_fma<R>(cur, curx, acc0, acc1);
 #pragma unroll
             for (int r = 0; r < R; ++r)
@@ -192,7 +195,8 @@ __global__ __launch_bounds__(256) void k_gemv_neg_wg(const double* __restrict__ 
             double2 xr = xv[c];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                double2 a = arow[r][c];
+                double2 a = VEC ? reinterpret_cast<const double2*>(arow[r])[c]
+                                : make_double2(arow[r][2 * c], arow[r][2 * c + 1]);
                 acc0[r] = fma(a.x, xr.x, acc0[r]);
                 acc1[r] = fma(a.y, xr.y, acc1[r]);
             }
@@ -216,6 +220,24 @@ __global__ __launch_bounds__(256) void k_gemv_neg_wg(const double* __restrict__ 
         const int r = threadIdx.x;
         y[row0 + r] = -((part[0][r] + part[1][r]) + (part[2][r] + part[3][r]));
     }
+}
+
+template <int R, bool NT>
+__global__ __launch_bounds__(256) void k_gemv_neg_wg(const double* __restrict__ A, long lda, int rows, int cols,
+                                                     const double* __restrict__ x, double* __restrict__ y) {
+    gemv_neg_wg_body<R, NT>(A, lda, rows, cols, x, y);
+}
+
+// -J^T F per m-slice (LevMarq / LevMarqMPI, syrk.hip): blockIdx.y = slice s0 + y of J^T (at
+// A + s * sstride, row stride lda) against F[s mS, (s + 1) mS) -> y[blockIdx.y * rows + j].
+template <int R, bool VEC>
+__global__ __launch_bounds__(256) void k_gemv_neg_slices(const double* __restrict__ A, long lda, long sstride, int rows,
+                                                         int m, int mS, int s0, const double* __restrict__ x,
+                                                         double* __restrict__ y) {
+    const int s = s0 + blockIdx.y;
+    const int cols = max(0, min(mS, m - s * mS));
+    gemv_neg_wg_body<R, true, VEC>(A + (long)s * sstride, lda, rows, cols, x + (long)s * mS,
+                                   y + (long)blockIdx.y * rows);
 }
 
 // any lda / alignment: one wave per row, 8-byte loads, 4 in flight per lane
@@ -572,6 +594,29 @@ int launch_gemv_neg(pnol_ctx* ctx, const double* A, int lda, int rows, int cols,
         hipLaunchKernelGGL((k_gemv_neg<2>), dim3(blocks), dim3(256), 0, ctx->stream, A, (long)lda, rows, cols, x, y);
     else
         hipLaunchKernelGGL((k_gemv_neg<1>), dim3(blocks), dim3(256), 0, ctx->stream, A, (long)lda, rows, cols, x, y);
+    return launch_check();
+}
+
+int launch_gemv_neg_slices(pnol_ctx* ctx, const double* A, int lda, long sstride, int rows, int m, int mS, int s0,
+                           int nsl, const double* x, double* y) {
+    if (!A || !x || !y || rows <= 0 || nsl <= 0 || (mS & 1) || !aligned16(x)) return PNOL_ERR_ARG;
+    // rows per workgroup (PNOL_JTR_ROWS = 1, 2 or 4; tuning -- each row's sum is the same for all)
+    static const int R = [] {
+        const char* e = std::getenv("PNOL_JTR_ROWS");
+        const int v = e ? std::atoi(e) : 2;
+        return (v == 1 || v == 4) ? v : 2;
+    }();
+    // 16-byte row loads when every row start is 16-byte aligned; the same sums otherwise
+    const bool vec = !((lda & 1) || (sstride & 1) || !aligned16(A));
+    const dim3 grid((rows + R - 1) / R, nsl);
+#define PNOL_SLICES(RR, V) \
+    hipLaunchKernelGGL((k_gemv_neg_slices<RR, V>), grid, dim3(256), 0, ctx->stream, A, (long)lda, sstride, rows, m, mS, s0, x, y)
+    if (vec) {
+        if (R == 1) PNOL_SLICES(1, true); else if (R == 4) PNOL_SLICES(4, true); else PNOL_SLICES(2, true);
+    } else {
+        if (R == 1) PNOL_SLICES(1, false); else if (R == 4) PNOL_SLICES(4, false); else PNOL_SLICES(2, false);
+    }
+#undef PNOL_SLICES
     return launch_check();
 }
 

@@ -19,6 +19,7 @@
 //                        resume from base-chain checkpoints and broadcast x outside the
 //                        perturbation window (k_linres_fd: the full-B-tile form)
 #include "../pnol_internal.hpp"
+#include "../pnol_comm.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -438,7 +439,8 @@ template <bool WAVE_KS>
 __global__ __launch_bounds__(256) void k_linres_fdP(const double* __restrict__ AP, const double* __restrict__ y,
                                                     const double* __restrict__ x, const double* __restrict__ h, int m,
                                                     int n, const FdTiles tl, const double* __restrict__ F0,
-                                                    const double* __restrict__ C, double* __restrict__ JT, long ldjt) {
+                                                    const double* __restrict__ C, double* __restrict__ JT, long ldjt,
+                                                    int mS, long sstride) {
     // Longest work first: the host sorts the tiles by first column (the chains of tile t run
     // k = ks_t .. n-1), and blockIdx walks all panels of tile 0, then of tile 1, ..., so the
     // short tiles fill the tail.  Panel mt lands on XCD mt % 8 for every tile (L2 reuse).
@@ -525,11 +527,14 @@ __global__ __launch_bounds__(256) void k_linres_fdP(const double* __restrict__ A
     // epilogue: F = acc - y; J = (F - F0) / h
     if (row < m) {
         const double yr = y[row], f0 = F0[row];
+        // row r of J: slice r / mS of the sliced layout (mS >= m: plain row-major J^T)
+        const int sl = (mt * kPanel) / mS;
+        double* out = JT + (long)sl * sstride + (row - sl * mS);
 #pragma unroll
         for (int j = 0; j < kPW; ++j)
             if (j < np) {
                 const int col = c0 + j;
-                JT[(long)(col - tl.jbase) * ldjt + row] = ((acc[j] - yr) - f0) / h[col];
+                out[(long)(col - tl.jbase) * ldjt] = ((acc[j] - yr) - f0) / h[col];
             }
     }
 }
@@ -658,8 +663,16 @@ int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
 // prefix checkpoints), then the FD GEMM over all tiles in launches of <= kFdMaxTiles tiles.
 int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, const int* start,
                              const int* count, int ntiles, double* F0, int compute_f0, double* JT, int jbase,
-                             int ldjt, int ckpt) {
-    if (!o || !x || !h || !F0 || is_scalar_kind(o->kind) || ntiles < 0 || ldjt < o->m) return PNOL_ERR_ARG;
+                             int ldjt, int ckpt, int mS, long sstride) {
+    const bool sliced = mS > 0;
+    if (!o || !x || !h || !F0 || is_scalar_kind(o->kind) || ntiles < 0 || ldjt < (sliced ? mS : o->m))
+        return PNOL_ERR_ARG;
+    if (sliced && (o->kind != PNOL_OBJ_LINRES || mS % kPanel != 0 || sstride < (long)o->n * ldjt))
+        return PNOL_ERR_UNSUPPORTED;
+    if (!sliced) {
+        mS = o->m;   // one slice: plain row-major J^T
+        sstride = 0;
+    }
     for (int t = 0; t < ntiles; ++t)
         if (start[t] < 0 || count[t] < 0 || count[t] > kFdTile || start[t] + count[t] > o->n || start[t] < jbase)
             return PNOL_ERR_ARG;
@@ -683,7 +696,7 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
         const int v = e ? std::atoi(e) : 6;
         return (v >= 2 && v <= 6) ? v : 6;
     }();
-    const bool kmajor = fdk >= 5;
+    const bool kmajor = fdk >= 5 || sliced;   // the sliced layout is written by the row-panel kernel
     if (kmajor) PNOL_CHECK(ensure_panels(ctx, o));
     // one pass of the base chain: F0 (when asked) and the prefix checkpoints -- skipped when
     // compute_f0 == 2 and the context's checkpoints are those of (o, x) from
@@ -729,10 +742,10 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
         const dim3 g1(((o->m + 127) / 128) * tl.ntiles), g2(((o->m + 63) / 64) * tl.ntiles);
         if (fdk == 5) {
             hipLaunchKernelGGL((k_linres_fdP<false>), g2, dim3(256), 0, ctx->stream, (const double*)o->at, o->p1, x, h,
-                               o->m, o->n, tl, F0, Cc, JT, (long)ldjt);
-        } else if (fdk == 6) {
+                               o->m, o->n, tl, F0, Cc, JT, (long)ldjt, mS, sstride);
+        } else if (fdk == 6 || sliced) {
             hipLaunchKernelGGL((k_linres_fdP<true>), g2, dim3(256), 0, ctx->stream, (const double*)o->at, o->p1, x, h,
-                               o->m, o->n, tl, F0, Cc, JT, (long)ldjt);
+                               o->m, o->n, tl, F0, Cc, JT, (long)ldjt, mS, sstride);
         } else if (fdk == 2) {
             if (even)
                 hipLaunchKernelGGL((k_linres_fd2<true, 8, 8>), g1, dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
@@ -809,6 +822,49 @@ int launch_synthetic_linres(pnol_ctx* ctx, unsigned long long seed, int m, int n
         hipLaunchKernelGGL((k_linres_eval<false, false>), dim3((m + kEvRows - 1) / kEvRows), dim3(256), 0, ctx->stream,
                            (const double*)A, (const double*)xstar, (const double*)nullptr, m, n, y, (double*)nullptr);
     return launch_check();
+}
+
+// LevMarqMPI Jacobian on the sliced J^T layout (pnol_lm_sliced_layout): this rank evaluates its
+// cost-balanced FD tiles (fd_tiles_of) for every residual row, then sends each m-slice of
+// them to the rank that holds the slice (lm_rank_slices) -- one group of point-to-point
+// transfers, 1/P of the J^T an allgather would move.  Each rank ends with every FD column of
+// its own slices, which is all launch_lm_normal reads.
+int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
+                       double* JTs) {
+    if (!o || !JTs || o->kind != PNOL_OBJ_LINRES) return PNOL_ERR_UNSUPPORTED;
+    const int P = comm_size(), me = comm_rank(), n = o->n;
+    if (P > kLmSlices) return PNOL_ERR_UNSUPPORTED;
+    const int mS = lm_slice_rows(o->m);
+    const long sstr = (long)n * mS;
+    std::vector<int> st, ct;
+    fd_tiles_of(n, P, me, st, ct);
+    PNOL_CHECK(launch_fd_jacobian_tiles(ctx, o, x, h, st.data(), ct.data(), (int)st.size(), F0, compute_f0, JTs, 0, mS,
+                                        1, mS, sstr));
+    if (P == 1) return PNOL_OK;
+    // runs of consecutive tiles per rank: one transfer per (run, slice)
+    std::vector<std::vector<std::pair<int, int>>> runs(P);
+    for (int q = 0; q < P; ++q) {
+        fd_tiles_of(n, P, q, st, ct);
+        for (size_t i = 0; i < st.size(); ++i) {
+            if (!runs[q].empty() && runs[q].back().first + runs[q].back().second == st[i])
+                runs[q].back().second += ct[i];
+            else
+                runs[q].push_back({st[i], ct[i]});
+        }
+    }
+    ScopedTimer tm(ctx, "exchange_J");
+    return comm_exchange(ctx, JTs, JTs, [&](int q, int d, std::vector<XBlock>& bl) {
+        bl.clear();
+        int s0, s1;
+        lm_rank_slices(P, d, &s0, &s1);
+        for (int s = s0; s < s1; ++s) {
+            if ((long)s * mS >= o->m) break;
+            for (auto& r : runs[q]) {
+                const size_t off = (size_t)s * sstr + (size_t)r.first * mS;
+                bl.push_back({off, off, (size_t)r.second * mS});
+            }
+        }
+    });
 }
 
 }  // namespace pnol

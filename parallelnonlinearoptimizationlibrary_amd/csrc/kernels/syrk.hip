@@ -83,16 +83,12 @@ __device__ __forceinline__ void store_stage(const StageRegs<TILE, NT>& s, double
 // TILE 128: waves 2 x 2 of 64 x 64 (4 x 4 MFMA blocks each); TILE 64: 2 x 2 of 32 x 32.
 // NW = 4: waves 2 x 2, each (TILE/2)^2; NW = 8: waves 2 x 4, each TILE/2 x TILE/4 (half the
 // accumulators per wave, so twice the waves per SIMD hide the stage boundaries).
-// MODE 3: as MODE 0, then the last of a tile's split_k workgroups to finish (counter cnt[t],
-// agent-scope release/acquire) sums the tile's partials in slice order -- the same fixed
-// order as k_syrk_reduce, so bitwise the same A -- and writes A = the tile with the
-// Marquardt diagonal (alpha = lambda) and its mirror; cnt[t] is reset for the next launch.
 template <int MODE, int TILE, bool XMAP = false, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
-                                                      int split_k, int kchunk, double* __restrict__ part,
+                                                      int split_k, int kchunk, int sub, int slice0, int mS,
+                                                      long sstride, double* __restrict__ part,
                                                       double* __restrict__ C, long ldc, double alpha,
-                                                      double beta, int tile0, int* __restrict__ cnt = nullptr,
-                                                      double* __restrict__ diag_out = nullptr) {
+                                                      double beta, int tile0) {
     constexpr int NT = 64 * NW, WC = NW / 2;
     constexpr int WTM = TILE / 2, WTN = TILE / WC, NBM = WTM / 16, NBN = WTN / 16;
     __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
@@ -118,8 +114,13 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
     tile_of(t, ti, tj);
     const bool diag = ti == tj;
     const int prow0 = ti * TILE, qrow0 = tj * TILE;
-    const int kbeg = sidx * kchunk;
-    const int kend = min(K, kbeg + kchunk);
+    // K slice sidx = sub-chunk u of m-slice `slice` (columns [slice * mS, (slice + 1) * mS) of
+    // the operand, stored at X + slice * sstride with row stride ldx; sstride == mS is the
+    // plain row-major layout)
+    const int slice = slice0 + sidx / sub, u = sidx % sub;
+    X += (long)slice * (sstride - mS);
+    const int kbeg = slice * mS + u * kchunk;
+    const int kend = min(K, min((slice + 1) * mS, kbeg + kchunk));
     const int nstages = kend > kbeg ? (kend - kbeg + kTK - 1) / kTK : 0;
 
     const int lane = threadIdx.x & 63;
@@ -172,7 +173,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
     // f64 MFMA C/D layout: lane l, register r -> row (l >> 4) + 4 r, column l & 15
     const int ocol = lane & 15;
     const int orow = lane >> 4;
-    if (MODE == 0 || MODE == 2 || MODE == 3) {
+    if (MODE == 0 || MODE == 2) {
         double* out = part + (long)blk * TILE * TILE;
 #pragma unroll
         for (int mi = 0; mi < NBM; ++mi)
@@ -184,40 +185,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                     int col = wc * WTN + ni * 16 + ocol;
                     out[row * TILE + col] = acc[mi][ni][r];
                 }
-        if (MODE == 3) {
-            __shared__ int s_last;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                const int old = __hip_atomic_fetch_add(cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_last = old == split_k - 1;
-                if (s_last) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                }
-            }
-            __syncthreads();
-            if (s_last) {
-                const double scale = 1 + alpha;
-                const double* p0 = part + ((long)(t - tile0) * split_k) * TILE * TILE;
-                for (int e = threadIdx.x; e < TILE * TILE; e += NT) {
-                    const int r = e / TILE, c = e % TILE;
-                    const int i = prow0 + r, j = qrow0 + c;
-                    if (i >= nr || j >= nr || j > i) continue;
-                    double v = 0.0;
-                    for (int s2 = 0; s2 < split_k; ++s2) v += p0[(long)s2 * TILE * TILE + e];
-                    if (i == j) {
-                        if (diag_out) diag_out[i] = v;
-                        C[(long)i * ldc + i] = scale * v;
-                    } else {
-                        C[(long)i * ldc + j] = v;
-                        C[(long)j * ldc + i] = v;
-                    }
-                }
-                if (threadIdx.x == 0) cnt[t] = 0;
-            }
-        }
     } else {
 #pragma unroll
         for (int mi = 0; mi < NBM; ++mi)
@@ -235,32 +202,120 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
     }
 }
 
-// Tile-sharded J^T J (LevMarqMPI): sum one launch's partials per tile in the same fixed
-// order, packed[tl * 128^2 + e] = raw (J^T J) tile values (no Marquardt scaling).
-__global__ void k_syrk_reduce_packed(const double* __restrict__ part, int split_k, double* __restrict__ packed) {
-    const int tl = blockIdx.y;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < kTile * kTile; e += gridDim.x * blockDim.x) {
-        const double* p = part + ((long)tl * split_k) * kTile * kTile + e;
-        double v = 0.0;
-        for (int s = 0; s < split_k; ++s) v += p[(long)s * kTile * kTile];
-        packed[(long)tl * kTile * kTile + e] = v;
+// ---- the m-slice summation tree ------------------------------------------------------------
+// J^T J and J^T F are summed over the residual rows in kLmSlices m-slices (slice s: rows
+// [s mS, (s + 1) mS)).  A slice's value ("leaf") is the sequential sum from 0.0 of its
+// sub-chunk partials; the leaves are combined by the fixed pairwise tree
+// ((l0 + l1) + (l2 + l3)) + ((l4 + l5) + (l6 + l7)).  A LevMarqMPI rank holding slices [a, b)
+// reduces its leaves to the maximal dyadic nodes of that tree inside [a, b) (tree_merge on the
+// leaves it has); the owner of an output merges the nodes of all ranks the same way.  Every
+// node is the same IEEE sum wherever it is formed, so A and J^T F do not depend on P.
+constexpr int kS = kLmSlices;
+static_assert(kS == 8, "tree8 spells out the 8-leaf tree");
+
+// v[i]: the node starting at slice i, sz[i] its width (0: none); siblings of equal width merge
+// bottom up.  With all kS leaves present this is tree8.
+__device__ __forceinline__ void tree_merge(double (&v)[kS], int (&sz)[kS]) {
+#pragma unroll
+    for (int w = 1; w < kS; w *= 2)
+#pragma unroll
+        for (int i = 0; i < kS; i += 2 * w)
+            if (sz[i] == w && sz[i + w] == w) {
+                v[i] = v[i] + v[i + w];
+                sz[i] = 2 * w;
+                sz[i + w] = 0;
+            }
+}
+
+__device__ __forceinline__ double tree8(const double (&l)[kS]) {
+    return ((l[0] + l[1]) + (l[2] + l[3])) + ((l[4] + l[5]) + (l[6] + l[7]));
+}
+
+// Leaves of slices [s0, s1) -- leaf s = sum over u < sub of
+// part[unit * ustride + ((s - s0) * sub + u) * sstride + e] -- merged into this range's dyadic
+// nodes, written in slice order to out[c * ocstride + unit * oustride + e].  blockIdx.y = unit.
+__global__ __launch_bounds__(256) void k_tree_nodes(const double* __restrict__ part, long ustride, long sstride,
+                                                    int sub, int s0, int s1, int elems, double* __restrict__ out,
+                                                    long ocstride, long oustride) {
+    const long unit = blockIdx.y;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < elems; e += gridDim.x * blockDim.x) {
+        double v[kS];
+        int sz[kS];
+#pragma unroll
+        for (int i = 0; i < kS; ++i) {
+            v[i] = 0.0;
+            sz[i] = 0;
+            if (i >= s0 && i < s1) {
+                const double* p = part + unit * ustride + (long)(i - s0) * sub * sstride + e;
+                double a = 0.0;
+                for (int u = 0; u < sub; ++u) a += p[(long)u * sstride];
+                v[i] = a;
+                sz[i] = 1;
+            }
+        }
+        tree_merge(v, sz);
+        int c = 0;
+#pragma unroll
+        for (int i = 0; i < kS; ++i)
+            if (sz[i]) out[(long)(c++) * ocstride + unit * oustride + e] = v[i];
     }
 }
 
-// Unpack the allgathered tile payloads (rank r's slot q holds tile r * tpr + q) into A:
-// lower triangle + mirror, A_ii = (1 + lambda) (J^T J)_ii -- the same writes as k_syrk_reduce.
-__global__ void k_syrk_unpack(const double* __restrict__ packed, int ntiles, int n, double lambda,
+// The nodes of all ranks (node at slice i: p[i], width w[i]; w[i] = 0 where no node starts)
+// merged to the root: out[e].
+struct TreeNodes {
+    const double* p[kS];
+    int w[kS];
+};
+
+__global__ __launch_bounds__(256) void k_tree_combine(const TreeNodes tn, long elems, double* __restrict__ out) {
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < elems; e += (long)gridDim.x * blockDim.x) {
+        double v[kS];
+        int sz[kS];
+#pragma unroll
+        for (int i = 0; i < kS; ++i) {
+            sz[i] = tn.w[i];
+            v[i] = sz[i] ? tn.p[i][e] : 0.0;
+        }
+        tree_merge(v, sz);
+        out[e] = v[0];
+    }
+}
+
+// Tile-sharded J^T J (pnol_jtj_mpi_d): one launch's partials per tile summed by the slice tree,
+// packed[tl * 128^2 + e] = raw (J^T J) tile values (no Marquardt scaling).
+__global__ void k_syrk_reduce_packed(const double* __restrict__ part, int sub, double* __restrict__ packed) {
+    const int tl = blockIdx.y;
+    const long E = kTile * kTile;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < kTile * kTile; e += gridDim.x * blockDim.x) {
+        const double* p = part + (long)tl * kS * sub * E + e;
+        double l[kS];
+#pragma unroll
+        for (int s = 0; s < kS; ++s) {
+            double a = 0.0;
+            for (int u = 0; u < sub; ++u) a += p[(long)(s * sub + u) * E];
+            l[s] = a;
+        }
+        packed[(long)tl * E + e] = tree8(l);
+    }
+}
+
+// Unpack allgathered tile payloads (tile t in rank t / tpr's slot of `slot` doubles, at
+// (t % tpr) * 128^2) into A: lower triangle + mirror, A_ii = (1 + lambda) (J^T J)_ii -- the
+// same writes as k_syrk_reduce.
+__global__ void k_syrk_unpack(const double* __restrict__ packed, int ntiles, int n, double lambda, long slot, int tpr,
                               double* __restrict__ A, long lda, double* __restrict__ diag_out) {
     const int t = blockIdx.y;
     if (t >= ntiles) return;
     int ti, tj;
     tile_of(t, ti, tj);
     const double scale = 1 + lambda;
+    const double* src = packed + (long)(t / tpr) * slot + (long)(t % tpr) * kTile * kTile;
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < kTile * kTile; e += gridDim.x * blockDim.x) {
         const int r = e / kTile, c = e % kTile;
         const int i = ti * kTile + r, j = tj * kTile + c;
         if (i >= n || j >= n || j > i) continue;
-        const double v = packed[(long)t * kTile * kTile + e];
+        const double v = src[e];
         if (i == j) {
             if (diag_out) diag_out[i] = v;
             A[(long)i * lda + i] = scale * v;
@@ -272,11 +327,15 @@ __global__ void k_syrk_unpack(const double* __restrict__ packed, int ntiles, int
 }
 
 // One 32 x 128 strip of a tile per workgroup (blockIdx.x = strip 0..3, blockIdx.y = tile):
-// sums the split-K partials in slice order (coalesced 16-byte reads), writes the lower part
+// sums the partials by the slice tree (coalesced 16-byte reads), writes the lower part
 // row-wise, and writes the mirror from an LDS transpose so those stores are row-wise too.
-__global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ part, int ntiles, int split_k, int n,
+// SUB > 0: the sub-chunk count at compile time (all kS * SUB loads of an element in flight at
+// once); SUB = 0: runtime `sub`.
+template <int SUB>
+__global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ part, int ntiles, int sub_rt, int n,
                                                      double lambda, double* __restrict__ A, long lda,
                                                      double* __restrict__ diag_out, int tile0) {
+    const int sub = SUB > 0 ? SUB : sub_rt;
     constexpr int SR = 32;                                 // strip rows
     __shared__ double st[SR][kTile + 1];
     const int t = tile0 + blockIdx.y;                      // part holds this launch's tiles from tile0 on
@@ -284,22 +343,31 @@ __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ 
     tile_of(t, ti, tj);
     const double scale = 1 + lambda;
     const int r0 = blockIdx.x * SR;
-    const double* p = part + ((long)(t - tile0) * split_k) * kTile * kTile + (long)r0 * kTile;
+    const long E = kTile * kTile;
+    const double* p = part + ((long)(t - tile0) * kS * sub) * E + (long)r0 * kTile;
     // 32 x 128 doubles = 2048 double2; 256 threads x 8
     for (int q = threadIdx.x; q < SR * kTile / 2; q += 256) {
         const int r = (2 * q) / kTile, c = (2 * q) % kTile;
-        double2 v = make_double2(0.0, 0.0);
-        for (int s2 = 0; s2 < split_k; ++s2) {
-            const double2 w = reinterpret_cast<const double2*>(p + (long)s2 * kTile * kTile)[q];
-            v.x += w.x;
-            v.y += w.y;
+        double lx[kS], ly[kS];
+#pragma unroll
+        for (int s = 0; s < kS; ++s) {
+            double ax = 0.0, ay = 0.0;
+#pragma unroll
+            for (int u = 0; u < (SUB > 0 ? SUB : sub); ++u) {
+                const double2 w = reinterpret_cast<const double2*>(p + (long)(s * sub + u) * E)[q];
+                ax += w.x;
+                ay += w.y;
+            }
+            lx[s] = ax;
+            ly[s] = ay;
         }
-        st[r][c] = v.x;
-        st[r][c + 1] = v.y;
+        const double vx = tree8(lx), vy = tree8(ly);
+        st[r][c] = vx;
+        st[r][c + 1] = vy;
         const int i = ti * kTile + r0 + r;
         for (int h = 0; h < 2; ++h) {
             const int j = tj * kTile + c + h;
-            const double val = h ? v.y : v.x;
+            const double val = h ? vy : vx;
             if (i >= n || j >= n || j > i) continue;
             if (i == j) {
                 if (diag_out) diag_out[i] = val;
@@ -338,40 +406,53 @@ __global__ void k_jtj_seq(const double* __restrict__ JT, long ldjt, int m, int n
 
 }  // namespace
 
-// Split-K factor: the workgroups are dispatched in rounds of one per CU, so the kernel takes
-// ceil(nwg / ncu) rounds of (K / split) work.  Pick the split whose last round is fullest
-// (nwg / (ncu * rounds) closest to 1), with K slices of >= 256 columns and at most 160 MB
-// of partial tiles; ties go to the smaller split (less reduce traffic).  At n = 2048
-// (136 tiles) on 256 CUs this is 7 (952 WGs, 93% of 4 rounds) instead of 4 (544, 71%).
-static int choose_split_k(int ntiles, int K, int ncu) {
+// K split: kLmSlices m-slices of mS rows (a multiple of 64, so an FD row panel never straddles
+// two), each cut into `sub` chunks.  sub depends on (m, n) only -- never on the number of
+// ranks -- so every A element is summed the same way on any P.  Default: enough workgroups to
+// fill the chip (>= 2048 = 256 CUs x 2 resident x 4 rounds), chunks >= 256 columns.  At
+// m = 16384, n = 2048 (136 tiles) sub = 2: 2176 workgroups of K = 1024 (measured: SYRK 1.33 ms
+// + reduce 0.09 ms, vs 1.42 + 0.05 ms at sub = 1).  PNOL_SYRK_SUB overrides.
+struct SliceCfg {
+    int mS, sub, kchunk;
+};
+
+// k_syrk_reduce with the sub-chunk count as a template constant where it is 1, 2 or 4
+template <typename... Args>
+static void launch_reduce(dim3 grid, dim3 block, size_t shm, hipStream_t st, const double* part, int ntiles, int sub,
+                          Args... args) {
+    if (sub == 1)
+        hipLaunchKernelGGL(k_syrk_reduce<1>, grid, block, shm, st, part, ntiles, sub, args...);
+    else if (sub == 2)
+        hipLaunchKernelGGL(k_syrk_reduce<2>, grid, block, shm, st, part, ntiles, sub, args...);
+    else if (sub == 4)
+        hipLaunchKernelGGL(k_syrk_reduce<4>, grid, block, shm, st, part, ntiles, sub, args...);
+    else
+        hipLaunchKernelGGL(k_syrk_reduce<0>, grid, block, shm, st, part, ntiles, sub, args...);
+}
+
+static SliceCfg slice_cfg(int m, int ntiles) {
     static const int forced = [] {
-        const char* e = std::getenv("PNOL_SYRK_SPLIT");
+        const char* e = std::getenv("PNOL_SYRK_SUB");
         return e ? std::atoi(e) : 0;
     }();
-    if (forced > 0) return std::min(forced, std::max(1, (K + kTK - 1) / kTK));
-    if (ncu <= 0) ncu = 256;
-    const int kmax = (K + 255) / 256;
-    int best = 1;
-    double best_time = 1e30;
-    for (int s = 1; s <= 64 && s <= kmax; ++s) {
-        const double part_mb = (double)ntiles * s * kTile * kTile * 8.0 / 1e6;
-        if (s > 1 && part_mb > 160.0) break;
-        const long rounds = ((long)ntiles * s + ncu - 1) / ncu;
-        const double time = (double)rounds / s;   // in units of one whole-K tile
-        if (time < best_time * 0.995) {
-            best = s;
-            best_time = time;
-        }
+    SliceCfg c;
+    c.mS = lm_slice_rows(m);
+    const int cap = std::max(1, c.mS / 256);
+    if (forced > 0) {
+        c.sub = std::min(forced, std::max(1, c.mS / kTK));
+    } else {
+        const int want = (2048 + ntiles * kS - 1) / (ntiles * kS);
+        c.sub = std::max(1, std::min(want, cap));
     }
-    return best;
+    c.kchunk = ((c.mS + c.sub - 1) / c.sub + kTK - 1) / kTK * kTK;
+    return c;
 }
 
 // J^T J variant (tuning; every variant sums each element in the same order):
-// PNOL_SYRK_NW = 8 (default) or 4 waves per 128 x 128 tile; PNOL_SYRK_FUSED = 1 reduces the
-// split-K partials inside the tile kernel (MODE 3), 0 (default) runs k_syrk_reduce after it.
-// Measured at m = 16384, n = 2048: 8 waves 1.35 ms vs 4 waves 1.40 ms; the fused reduce 1.51 ms
-// vs 1.35 + 0.06 ms -- every tile's last slice finishes in the final round, so the in-kernel
-// reduces all land in the tail instead of overlapping the MFMA work.
+// PNOL_SYRK_NW = 8 (default) or 4 waves per 128 x 128 tile.  Measured at m = 16384, n = 2048:
+// 8 waves 1.35 ms vs 4 waves 1.40 ms.  (A split-K reduce fused into the tile kernel by the last
+// arriving workgroup measured 1.51 ms vs 1.35 + 0.06: every tile's last slice finishes in the
+// final round, so the reduces all land in the tail; removed.)
 static int syrk_nw() {
     static const int nw = [] {
         const char* e = std::getenv("PNOL_SYRK_NW");
@@ -380,20 +461,34 @@ static int syrk_nw() {
     return nw;
 }
 
-static bool syrk_fused() {
-    static const bool on = [] {
-        const char* e = std::getenv("PNOL_SYRK_FUSED");
-        return e && std::atoi(e) != 0;
-    }();
-    return on;
-}
-
 static bool syrk_xmap() {
     static const bool on = [] {
         const char* e = std::getenv("PNOL_SYRK_XMAP");
         return e && std::atoi(e) != 0;
     }();
     return on;
+}
+
+// Partial tiles [tile0, tile0 + ntl) x slices [slice0, slice0 + nsl) x sub-chunks of
+// X (nr rows, K columns; slice s at X + s * sstride, row stride ldx) into
+// part[((t - tile0) * nsl * sub + (s - slice0) * sub + u) * 128^2].
+static void syrk_partials(pnol_ctx* ctx, hipStream_t stream, bool rows_variant, const double* X, long ldx,
+                          long sstride, int nr, int K, const SliceCfg& sc, int slice0, int nsl, int tile0, int ntl,
+                          double* part) {
+    const int split = nsl * sc.sub;
+    const dim3 grid(ntl * split);
+    if (rows_variant)
+        hipLaunchKernelGGL((k_syrk_tile<2, kTile, false, 8>), grid, dim3(512), 0, stream, X, ldx, nr, K, split,
+                           sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
+    else if (syrk_nw() == 8)
+        hipLaunchKernelGGL((k_syrk_tile<0, kTile, false, 8>), grid, dim3(512), 0, stream, X, ldx, nr, K, split,
+                           sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
+    else if (syrk_xmap() && split % kNumXcd == 0)
+        hipLaunchKernelGGL((k_syrk_tile<0, kTile, true>), grid, dim3(256), 0, stream, X, ldx, nr, K, split, sc.kchunk,
+                           sc.sub, slice0, sc.mS, sstride, part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
+    else
+        hipLaunchKernelGGL((k_syrk_tile<0, kTile>), grid, dim3(256), 0, stream, X, ldx, nr, K, split, sc.kchunk,
+                           sc.sub, slice0, sc.mS, sstride, part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
 }
 
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
@@ -406,43 +501,17 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     }
     const int nt = (n + kTile - 1) / kTile;
     const int ntiles = nt * (nt + 1) / 2;
-    const int split_k = choose_split_k(ntiles, m, ctx->num_cu);
-    int kchunk = (m + split_k - 1) / split_k;
-    kchunk = (kchunk + kTK - 1) / kTK * kTK;
+    const SliceCfg sc = slice_cfg(m, ntiles);
     void* part = nullptr;
-    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * split_k * kTile * kTile, &part));
-    if (syrk_fused()) {
-        // partial tiles + the last-arriving workgroup's fixed-order reduce in one launch
-        void* cnt = nullptr;
-        PNOL_CHECK(ws_get_zeroed(ctx, "syrk_cnt", sizeof(int) * (size_t)ntiles, &cnt));
-        ScopedTimer tm(ctx, "syrk");
-        if (syrk_nw() == 4)
-            hipLaunchKernelGGL((k_syrk_tile<3, kTile, false, 4>), dim3(ntiles * split_k), dim3(256), 0, ctx->stream,
-                               JT, (long)ldjt, n, m, split_k, kchunk, (double*)part, A, (long)lda, lambda, 0.0, 0,
-                               (int*)cnt, jtj_diag);
-        else
-            hipLaunchKernelGGL((k_syrk_tile<3, kTile, false, 8>), dim3(ntiles * split_k), dim3(512), 0, ctx->stream,
-                               JT, (long)ldjt, n, m, split_k, kchunk, (double*)part, A, (long)lda, lambda, 0.0, 0,
-                               (int*)cnt, jtj_diag);
-        return launch_check();
-    }
+    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * kS * sc.sub * kTile * kTile, &part));
     {
         ScopedTimer tm(ctx, "syrk");
-        if (syrk_nw() == 8)
-            hipLaunchKernelGGL((k_syrk_tile<0, kTile, false, 8>), dim3(ntiles * split_k), dim3(512), 0, ctx->stream,
-                               JT, (long)ldjt, n, m, split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0,
-                               0);
-        else if (syrk_xmap() && split_k % kNumXcd == 0)
-            hipLaunchKernelGGL((k_syrk_tile<0, kTile, true>), dim3(ntiles * split_k), dim3(256), 0, ctx->stream, JT,
-                               (long)ldjt, n, m, split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0, 0);
-        else
-            hipLaunchKernelGGL((k_syrk_tile<0, kTile>), dim3(ntiles * split_k), dim3(256), 0, ctx->stream, JT,
-                               (long)ldjt, n, m, split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0, 0);
+        syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part);
     }
     PNOL_CHECK(launch_check());
     ScopedTimer tm(ctx, "syrk_reduce");
-    hipLaunchKernelGGL(k_syrk_reduce, dim3(kTile / 32, ntiles), dim3(256), 0, ctx->stream, (const double*)part, ntiles,
-                       split_k, n, lambda, A, (long)lda, jtj_diag, 0);
+    launch_reduce(dim3(kTile / 32, ntiles), dim3(256), 0, ctx->stream, (const double*)part, ntiles,
+                       sc.sub, n, lambda, A, (long)lda, jtj_diag, 0);
     return launch_check();
 }
 
@@ -451,21 +520,19 @@ int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldj
     const int nt = (n + kTile - 1) / kTile;
     const int ntiles = nt * (nt + 1) / 2;
     if (row_begin < 0 || row_end > nt || row_begin >= row_end) return PNOL_ERR_ARG;
-    const int split_k = choose_split_k(ntiles, m, ctx->num_cu);
-    int kchunk = (m + split_k - 1) / split_k;
-    kchunk = (kchunk + kTK - 1) / kTK * kTK;
+    const SliceCfg sc = slice_cfg(m, ntiles);
     const int t0 = row_begin * (row_begin + 1) / 2, t1 = row_end * (row_end + 1) / 2;
+    const size_t per_tile = (size_t)kS * sc.sub * kTile * kTile;
     void* part = nullptr;
-    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * split_k * kTile * kTile, &part));
-    double* mypart = (double*)part + (size_t)t0 * split_k * kTile * kTile;   // disjoint per row range
+    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * per_tile, &part));
+    double* mypart = (double*)part + (size_t)t0 * per_tile;   // disjoint per row range
     {
         ScopedTimer tm(ctx, "syrk_rows", stream);
-        hipLaunchKernelGGL((k_syrk_tile<2, kTile, false, 8>), dim3((t1 - t0) * split_k), dim3(512), 0, stream, JT, (long)ldjt, n,
-                           m, split_k, kchunk, mypart, (double*)nullptr, 0L, 1.0, 0.0, t0);
+        syrk_partials(ctx, stream, true, JT, ldjt, sc.mS, n, m, sc, 0, kS, t0, t1 - t0, mypart);
     }
     PNOL_CHECK(launch_check());
-    hipLaunchKernelGGL(k_syrk_reduce, dim3(kTile / 32, t1 - t0), dim3(256), 0, stream, (const double*)mypart, t1 - t0, split_k,
-                       n, lambda, A, (long)lda, jtj_diag, t0);
+    launch_reduce(dim3(kTile / 32, t1 - t0), dim3(256), 0, stream, (const double*)mypart, t1 - t0,
+                       sc.sub, n, lambda, A, (long)lda, jtj_diag, t0);
     return launch_check();
 }
 
@@ -537,16 +604,15 @@ int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, do
     constexpr int kT = 64;
     const int nt = (nr + kT - 1) / kT;
     const int ntiles = nt * (nt + 1) / 2;
-    hipLaunchKernelGGL((k_syrk_tile<1, kT>), dim3(ntiles), dim3(256), 0, ctx->stream, X, (long)ldx, nr, K, 1, K,
-                       (double*)nullptr, C, (long)ldc, alpha, 1.0, 0);
+    hipLaunchKernelGGL((k_syrk_tile<1, kT>), dim3(ntiles), dim3(256), 0, ctx->stream, X, (long)ldx, nr, K, 1, K, 1, 0,
+                       K, (long)K, (double*)nullptr, C, (long)ldc, alpha, 1.0, 0);
     return launch_check();
 }
 
 // J^T J with the 128 x 128 tiles split over the communicator's ranks (contiguous ranges of
 // tpr = ceil(ntiles / P) tiles), then one allgather of the packed tiles (P * tpr * 128 KB).
-// The split-K factor comes from the global tile count, so every tile is summed exactly as on
-// one GPU: A is bitwise independent of P.  n <= PNOL_SEQ_MAX keeps the replicated
-// reference-order kernel.
+// Each tile is summed exactly as on one GPU (same K split, same slice tree): A is bitwise
+// independent of P.  n <= PNOL_SEQ_MAX keeps the replicated reference-order kernel.
 int launch_jtj_sharded(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                        double* jtj_diag) {
     const int P = comm_size(), rank = comm_rank();
@@ -554,37 +620,181 @@ int launch_jtj_sharded(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, 
     if (!JT || !A || m <= 0 || n <= 0 || ldjt < m || lda < n) return PNOL_ERR_ARG;
     const int nt = (n + kTile - 1) / kTile;
     const int ntiles = nt * (nt + 1) / 2;
-    const int split_k = choose_split_k(ntiles, m, ctx->num_cu);
-    int kchunk = (m + split_k - 1) / split_k;
-    kchunk = (kchunk + kTK - 1) / kTK * kTK;
+    const SliceCfg sc = slice_cfg(m, ntiles);
     const int tpr = (ntiles + P - 1) / P;
     const int t0 = std::min(ntiles, rank * tpr), cnt = std::min(ntiles, t0 + tpr) - t0;
-    const size_t tile_elems = (size_t)kTile * kTile;
+    const size_t E = (size_t)kTile * kTile;
     void *part = nullptr, *packed = nullptr;
-    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)std::max(cnt, 1) * split_k * tile_elems, &part));
-    PNOL_CHECK(ws_get(ctx, "syrk_packed", sizeof(double) * (size_t)P * tpr * tile_elems, &packed));
-    double* mine = (double*)packed + (size_t)rank * tpr * tile_elems;
+    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)std::max(cnt, 1) * kS * sc.sub * E, &part));
+    PNOL_CHECK(ws_get(ctx, "syrk_packed", sizeof(double) * (size_t)P * tpr * E, &packed));
+    double* mine = (double*)packed + (size_t)rank * tpr * E;
     if (cnt > 0) {
         {
             ScopedTimer tm(ctx, "syrk");
-            hipLaunchKernelGGL((k_syrk_tile<0, kTile, false, 8>), dim3(cnt * split_k), dim3(512), 0, ctx->stream, JT, (long)ldjt,
-                               n, m, split_k, kchunk, (double*)part, (double*)nullptr, 0L, 1.0, 0.0, t0);
+            syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, t0, cnt, (double*)part);
         }
         PNOL_CHECK(launch_check());
-        hipLaunchKernelGGL(k_syrk_reduce_packed, dim3(8, cnt), dim3(256), 0, ctx->stream, (const double*)part, split_k,
+        hipLaunchKernelGGL(k_syrk_reduce_packed, dim3(8, cnt), dim3(256), 0, ctx->stream, (const double*)part, sc.sub,
                            mine);
         PNOL_CHECK(launch_check());
     }
-    PNOL_CHECK(comm_allgather_device(ctx, mine, (double*)packed, (size_t)tpr * tile_elems));
+    PNOL_CHECK(comm_allgather_device(ctx, mine, (double*)packed, (size_t)tpr * E));
     ScopedTimer tm(ctx, "syrk_reduce");
     hipLaunchKernelGGL(k_syrk_unpack, dim3(8, ntiles), dim3(256), 0, ctx->stream, (const double*)packed, ntiles, n,
-                       lambda, A, (long)lda, jtj_diag);
+                       lambda, (long)tpr * E, tpr, A, (long)lda, jtj_diag);
+    return launch_check();
+}
+
+// The dyadic nodes of the slice tree inside [a, b), in slice order: (first slice, width).
+static void dyadic_nodes(int a, int b, std::vector<std::pair<int, int>>& out) {
+    out.clear();
+    int i = a;
+    while (i < b) {
+        int w = 1;
+        while (i % (2 * w) == 0 && i + 2 * w <= b && 2 * w <= kS) w *= 2;
+        out.push_back({i, w});
+        i += w;
+    }
+}
+
+// -J^T F on the m-slices [s0, s0 + nsl): jp[(s - s0) * n + j] = -sum_{k in slice s} JT_jk F_k
+// (JT slice s at JT + s * sstride, row stride ldjt), then the slice nodes of that range into
+// out[c * n + j] (one node = -J^T F itself when the range is all kLmSlices slices).
+static int jtr_slices(pnol_ctx* ctx, const double* JT, int ldjt, long sstride, int m, int n, int mS, int s0, int nsl,
+                      const double* F, double* out) {
+    void* jp = nullptr;
+    PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
+    PNOL_CHECK(launch_gemv_neg_slices(ctx, JT, ldjt, sstride, n, m, mS, s0, nsl, F, (double*)jp));
+    hipLaunchKernelGGL(k_tree_nodes, dim3((n + 255) / 256, 1), dim3(256), 0, ctx->stream, (const double*)jp, 0L,
+                       (long)n, 1, s0, s0 + nsl, n, out, (long)n, 0L);
     return launch_check();
 }
 
 int launch_jtr(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs) {
     if (n <= PNOL_SEQ_MAX && m <= 4096) return launch_gemv_neg_seq(ctx, JT, ldjt, n, m, F, rhs);
-    return launch_gemv_neg(ctx, JT, ldjt, n, m, F, rhs);
+    if (!JT || !F || !rhs || m <= 0 || n <= 0 || ldjt < m) return PNOL_ERR_ARG;
+    const int mS = lm_slice_rows(m);
+    return jtr_slices(ctx, JT, ldjt, mS, m, n, mS, 0, kS, F, rhs);
+}
+
+// LevMarqMPI normal equations on the m-sliced Jacobian (layout of pnol_lm_sliced_layout):
+// rank r holds every FD column of its m-slices [s0, s1) (lm_rank_slices).
+//   1. partial tiles of J^T J over its slices (all tiles), -J^T F over its slices;
+//   2. its slice-tree nodes of every tile; each tile's nodes go to the tile's owner (contiguous
+//      tile ranges of tpr tiles) -- one group of point-to-point sends (a reduce-scatter in the
+//      tree's order);
+//   3. the owner merges the nodes of its tiles; one allgather of (owned tiles + this rank's
+//      -J^T F nodes); every rank unpacks A and merges -J^T F.
+// Bitwise equal to launch_jtj + launch_jtr on the row-major J^T for every P <= kLmSlices.
+int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F, double* A,
+                     int lda, double* rhs, double* jtj_diag) {
+    if (!JTs || !F || !A || !rhs || m <= 0 || n <= 0 || lda < n) return PNOL_ERR_ARG;
+    if (n <= PNOL_SEQ_MAX && m <= 4096) return PNOL_ERR_UNSUPPORTED;   // reference-order kernels: row-major J^T
+    const int P = comm_size(), me = comm_rank();
+    if (P > kS) return PNOL_ERR_UNSUPPORTED;
+    const int nt = (n + kTile - 1) / kTile;
+    const int ntiles = nt * (nt + 1) / 2;
+    const SliceCfg sc = slice_cfg(m, ntiles);
+    const long sstr = (long)n * sc.mS;
+    const long E = (long)kTile * kTile;
+    int s0, s1;
+    lm_rank_slices(P, me, &s0, &s1);
+    const int nsl = s1 - s0;
+    void* part = nullptr;
+    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * std::max(nsl, 1) * sc.sub * E, &part));
+    if (nsl > 0) {
+        ScopedTimer tm(ctx, "syrk");
+        syrk_partials(ctx, ctx->stream, false, JTs, sc.mS, sstr, n, m, sc, s0, nsl, 0, ntiles, (double*)part);
+    }
+    PNOL_CHECK(launch_check());
+    if (P == 1) {
+        {
+            ScopedTimer tm(ctx, "syrk_reduce");
+            launch_reduce(dim3(kTile / 32, ntiles), dim3(256), 0, ctx->stream, (const double*)part,
+                               ntiles, sc.sub, n, lambda, A, (long)lda, jtj_diag, 0);
+        }
+        PNOL_CHECK(launch_check());
+        ScopedTimer tm(ctx, "jtr");
+        return jtr_slices(ctx, JTs, sc.mS, sstr, m, n, sc.mS, 0, kS, F, rhs);
+    }
+    // the global node list: rank q's nodes in slice order, ranks in order
+    std::vector<std::pair<int, int>> nodes;
+    std::vector<int> owner, first(P + 1, 0);
+    for (int q = 0; q < P; ++q) {
+        int a, b;
+        lm_rank_slices(P, q, &a, &b);
+        std::vector<std::pair<int, int>> nq;
+        dyadic_nodes(a, b, nq);
+        first[q] = (int)nodes.size();
+        for (auto& nd : nq) {
+            nodes.push_back(nd);
+            owner.push_back(q);
+        }
+    }
+    first[P] = (int)nodes.size();
+    const int NC = (int)nodes.size(), nn = first[me + 1] - first[me];
+    constexpr int kMaxNodes = 4;   // dyadic nodes of a slice range of an 8-leaf tree
+    const int tpr = (ntiles + P - 1) / P;
+    auto t0_of = [&](int d) { return std::min(ntiles, d * tpr); };
+    auto cnt_of = [&](int d) { return std::min(ntiles, t0_of(d) + tpr) - t0_of(d); };
+    const long slot = (long)tpr * E + (long)kMaxNodes * n;
+    void *nodebuf = nullptr, *recv = nullptr, *packed = nullptr;
+    PNOL_CHECK(ws_get(ctx, "lm_nodes", sizeof(double) * (size_t)std::max(nn, 1) * ntiles * E, &nodebuf));
+    PNOL_CHECK(ws_get(ctx, "lm_nodes_recv", sizeof(double) * (size_t)NC * tpr * E, &recv));
+    PNOL_CHECK(ws_get(ctx, "lm_packed", sizeof(double) * (size_t)P * slot, &packed));
+    double* mine = (double*)packed + (size_t)me * slot;
+    if (nsl > 0) {
+        ScopedTimer tm(ctx, "syrk_reduce");
+        hipLaunchKernelGGL(k_tree_nodes, dim3(kTile * kTile / 256 / 4, ntiles), dim3(256), 0, ctx->stream,
+                           (const double*)part, (long)nsl * sc.sub * E, E, sc.sub, s0, s1, (int)E,
+                           (double*)nodebuf, (long)ntiles * E, E);
+    }
+    PNOL_CHECK(launch_check());
+    // -J^T F nodes of my slices into the tail of my allgather slot
+    if (nsl > 0) {
+        ScopedTimer tm(ctx, "jtr");
+        PNOL_CHECK(jtr_slices(ctx, JTs, sc.mS, sstr, m, n, sc.mS, s0, nsl, F, mine + (long)tpr * E));
+    }
+    // reduce-scatter in tree order: rank q's nodes of owner d's tiles -> d
+    {
+        ScopedTimer tm(ctx, "exchange_A");
+        PNOL_CHECK(comm_exchange(ctx, (const double*)nodebuf, (double*)recv, [&](int q, int d, std::vector<XBlock>& bl) {
+            bl.clear();
+            if (cnt_of(d) == 0) return;
+            for (int c = first[q]; c < first[q + 1]; ++c)
+                bl.push_back({(size_t)((c - first[q]) * (long)ntiles + t0_of(d)) * E, (size_t)c * tpr * E,
+                              (size_t)cnt_of(d) * E});
+        }));
+    }
+    if (cnt_of(me) > 0) {
+        TreeNodes tn{};
+        for (int c = 0; c < NC; ++c) {
+            const int lo = nodes[c].first;
+            tn.w[lo] = nodes[c].second;
+            tn.p[lo] = owner[c] == me ? (const double*)nodebuf + ((long)(c - first[me]) * ntiles + t0_of(me)) * E
+                                      : (const double*)recv + (long)c * tpr * E;
+        }
+        ScopedTimer tm(ctx, "syrk_reduce");
+        const long el = (long)cnt_of(me) * E;
+        hipLaunchKernelGGL(k_tree_combine, dim3((unsigned)std::min<long>((el + 255) / 256, 4096)), dim3(256), 0,
+                           ctx->stream, tn, el, mine);
+        PNOL_CHECK(launch_check());
+    }
+    PNOL_CHECK(comm_allgather_device(ctx, mine, (double*)packed, (size_t)slot));
+    {
+        ScopedTimer tm(ctx, "syrk_reduce");
+        hipLaunchKernelGGL(k_syrk_unpack, dim3(8, ntiles), dim3(256), 0, ctx->stream, (const double*)packed, ntiles, n,
+                           lambda, slot, tpr, A, (long)lda, jtj_diag);
+        PNOL_CHECK(launch_check());
+        TreeNodes tr{};
+        for (int c = 0; c < NC; ++c) {
+            const int lo = nodes[c].first;
+            tr.w[lo] = nodes[c].second;
+            tr.p[lo] = (const double*)packed + (long)owner[c] * slot + (long)tpr * E + (long)(c - first[owner[c]]) * n;
+        }
+        hipLaunchKernelGGL(k_tree_combine, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, tr, (long)n, rhs);
+    }
+    return launch_check();
 }
 
 }  // namespace pnol

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <cstddef>
+#include <functional>
 #include <vector>
 
 #include "pnol_amd.h"
@@ -22,6 +23,15 @@ int comm_share_rows(pnol_ctx* ctx, double* buf, size_t ld, int ncols);
 int comm_allgather_host(pnol_ctx* ctx, const double* send, double* recv, size_t count);
 // device buffers (RCCL backend native; host backend bounces through host memory)
 int comm_allgather_device(pnol_ctx* ctx, const double* send, double* recv, size_t count);
+// Point-to-point exchange of device blocks: blocks(src, dst, out) lists what rank src sends to
+// rank dst (src != dst) -- soff into the sender's sbase, roff into the receiver's rbase, count
+// doubles -- and must give the same list on every rank.  RCCL: one group of sends / receives
+// on the context stream; host backend: packed through one allgather.
+struct XBlock {
+    size_t soff, roff, count;
+};
+int comm_exchange(pnol_ctx* ctx, const double* sbase, double* rbase,
+                  const std::function<void(int, int, std::vector<XBlock>&)>& blocks);
 // process default GPU context (nullptr when no gfx950 device is visible)
 pnol_ctx* default_ctx_or_null();
 

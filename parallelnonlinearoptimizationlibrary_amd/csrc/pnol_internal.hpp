@@ -116,6 +116,9 @@ inline int launch_check() {
 // ---- kernel launchers (defined in kernels/*.hip) ------------------------------------
 int launch_gemv_neg(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y);
 int launch_gemv_neg_seq(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y);
+// y[(s - s0) * rows + j] = -sum_{k in m-slice s} A_s[j][k] x[s mS + k], s in [s0, s0 + nsl)
+int launch_gemv_neg_slices(pnol_ctx* ctx, const double* A, int lda, long sstride, int rows, int m, int mS, int s0,
+                           int nsl, const double* x, double* y);
 int launch_bfgs_update_exact(pnol_ctx* ctx, double* D, int ldd, const double* y, const double* s, int n);
 int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p, const double* a_p,
                      const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
@@ -144,9 +147,11 @@ int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
                        double* f0, double* g);
 // ckpt: 1 = run the base-chain pass (F0 when compute_f0, prefix checkpoints), 0 = reuse the
 // checkpoints of the previous call at the same x (chunked launches of one Jacobian)
+// mS > 0: the sliced J^T layout (row r of J in slice r / mS at JT + (r / mS) * sstride, row
+// stride ldjt >= mS); linear residuals on the row-panel kernels only
 int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, const int* start,
                              const int* count, int ntiles, double* F0, int compute_f0, double* JT, int jbase,
-                             int ldjt, int ckpt = 1);
+                             int ldjt, int ckpt = 1, int mS = 0, long sstride = 0);
 // J^T J tiles of tile rows [row_begin, row_end) (128 x 128 tiles, split_k of the whole matrix so
 // every tile is summed exactly as by launch_jtj), partials + reduce on `stream`
 int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldjt, int m, int n, double lambda,
@@ -161,6 +166,25 @@ int launch_synthetic_quadratic(pnol_ctx* ctx, unsigned long long seed, int n, do
 int launch_synthetic_linres(pnol_ctx* ctx, unsigned long long seed, int m, int n, double* A, double* xstar,
                             double* y);
 int launch_fill(pnol_ctx* ctx, double* p, size_t count, double value);
+
+// ---- LM m-slices: J^T J and J^T F are summed over kLmSlices slices of the m
+// residual rows by a fixed tree (syrk.hip), so LevMarqMPI can split the rows over up to
+// kLmSlices ranks with bitwise the one-GPU A.  Sliced J^T layout: slice s is an n x mS
+// row-major block at JTs + s * n * mS (FD column j, rows [s mS, (s + 1) mS) of J).
+constexpr int kLmSlices = 8;
+inline int lm_slice_rows(int m) { return (((m + kLmSlices - 1) / kLmSlices) + 63) / 64 * 64; }
+// rank r of P (<= kLmSlices) holds slices [floor(r 8 / P), floor((r + 1) 8 / P))
+inline void lm_rank_slices(int P, int r, int* s0, int* s1) {
+    *s0 = r * kLmSlices / P;
+    *s1 = (r + 1) * kLmSlices / P;
+}
+// normal equations from the sliced J^T of this rank's slices (all FD columns): A (+ Marquardt
+// diagonal) and rhs = -J^T F on every rank (syrk.hip)
+int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F, double* A,
+                     int lda, double* rhs, double* jtj_diag);
+// this rank's FD tiles into the sliced J^T, then each slice's rows to the slice's rank (fd.hip)
+int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
+                       double* JTs);
 
 // number of XCDs (8 on MI355X): used only for blockIdx -> tile remaps (speed, never correctness)
 constexpr int kNumXcd = 8;

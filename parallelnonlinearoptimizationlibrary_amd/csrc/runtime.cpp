@@ -151,6 +151,77 @@ int comm_share_rows(pnol_ctx* ctx, double* buf, size_t ld, int ncols) {
     return PNOL_OK;
 }
 
+int comm_exchange(pnol_ctx* ctx, const double* sbase, double* rbase,
+                  const std::function<void(int, int, std::vector<XBlock>&)>& blocks) {
+    const int P = g_comm.nranks, me = g_comm.rank;
+    if (g_comm.kind == 0 || P == 1) return PNOL_OK;
+    std::vector<XBlock> bl;
+    if (g_comm.kind == 1) {
+        if (ncclGroupStart() != ncclSuccess) return PNOL_ERR_COMM;
+        bool ok = true;
+        for (int d = 0; d < P && ok; ++d) {
+            if (d == me) continue;
+            blocks(me, d, bl);
+            for (const XBlock& b : bl)
+                if (b.count && ncclSend(sbase + b.soff, b.count, ncclDouble, d, g_comm.nccl, ctx->stream) != ncclSuccess)
+                    ok = false;
+        }
+        for (int q = 0; q < P && ok; ++q) {
+            if (q == me) continue;
+            blocks(q, me, bl);
+            for (const XBlock& b : bl)
+                if (b.count && ncclRecv(rbase + b.roff, b.count, ncclDouble, q, g_comm.nccl, ctx->stream) != ncclSuccess)
+                    ok = false;
+        }
+        if (ncclGroupEnd() != ncclSuccess || !ok) return PNOL_ERR_COMM;
+        return PNOL_OK;
+    }
+    // host backend: every rank packs all its outgoing blocks (destinations in order) into one
+    // slot of the largest rank's size; one allgather; receivers pick their blocks out
+    auto out_size = [&](int q) {
+        size_t t = 0;
+        for (int d = 0; d < P; ++d) {
+            if (d == q) continue;
+            blocks(q, d, bl);
+            for (const XBlock& b : bl) t += b.count;
+        }
+        return t;
+    };
+    size_t slot = 1;
+    for (int q = 0; q < P; ++q) slot = std::max(slot, out_size(q));
+    void *sv = nullptr, *rv = nullptr;
+    PNOL_CHECK(ws_get(ctx, "xchg_send", sizeof(double) * slot, &sv));
+    PNOL_CHECK(ws_get(ctx, "xchg_recv", sizeof(double) * slot * P, &rv));
+    double *send = (double*)sv, *recv = (double*)rv;
+    size_t off = 0;
+    for (int d = 0; d < P; ++d) {
+        if (d == me) continue;
+        blocks(me, d, bl);
+        for (const XBlock& b : bl) {
+            if (b.count)
+                PNOL_HIP(hipMemcpyAsync(send + off, sbase + b.soff, sizeof(double) * b.count, hipMemcpyDeviceToDevice,
+                                        ctx->stream));
+            off += b.count;
+        }
+    }
+    PNOL_CHECK(comm_allgather_device(ctx, send, recv, slot));
+    for (int q = 0; q < P; ++q) {
+        if (q == me) continue;
+        off = 0;
+        for (int d = 0; d < P; ++d) {
+            if (d == q) continue;
+            blocks(q, d, bl);
+            for (const XBlock& b : bl) {
+                if (d == me && b.count)
+                    PNOL_HIP(hipMemcpyAsync(rbase + b.roff, recv + (size_t)q * slot + off, sizeof(double) * b.count,
+                                            hipMemcpyDeviceToDevice, ctx->stream));
+                off += b.count;
+            }
+        }
+    }
+    return PNOL_OK;
+}
+
 int comm_allgather_host(pnol_ctx* ctx, const double* send, double* recv, size_t count) {
     if (g_comm.kind == 0) {
         std::memcpy(recv, send, sizeof(double) * count);

@@ -116,6 +116,16 @@ class Context:
         L.check(L.lib().pnol_jtr_d(self.h, _ptr(JT), JT.stride(0), m, n, _ptr(F), _ptr(rhs)), "pnol_jtr_d")
         return rhs
 
+    def lm_normal_mpi(self, JTs, m, n, lam, F, A=None, rhs=None, want_diag=False):
+        """LevMarqMPI normal equations from this rank's slices of the m-sliced J^T (layout
+        lm_sliced_layout): A = J^T J with A_ii *= (1+lam), rhs = -J^T F, on every rank."""
+        A = self.empty(n, n) if A is None else A
+        rhs = self.empty(n) if rhs is None else rhs
+        diag = self.empty(n) if want_diag else None
+        L.check(L.lib().pnol_lm_normal_mpi_d(self.h, _ptr(JTs), m, n, C.c_double(lam), _ptr(F), _ptr(A), A.stride(0),
+                                             _ptr(rhs), _ptr(diag)), "pnol_lm_normal_mpi_d")
+        return (A, rhs, diag) if want_diag else (A, rhs)
+
     def solve(self, A, rhs, method=0):
         """sigma = A^{-1} rhs; A is overwritten.  Returns (sigma, info)."""
         n = rhs.numel()
@@ -202,6 +212,15 @@ class DeviceObjective:
                 "pnol_fd_jtj_d")
         return (F0, JT, A, diag) if want_diag else (F0, JT, A)
 
+    def lm_jacobian_mpi(self, x, h, JTs=None, F0=None, compute_f0=True):
+        """This rank's FD tiles for all rows into the m-sliced J^T, then each slice to its rank."""
+        if JTs is None:
+            JTs = self.ctx.empty(lm_sliced_layout(self.m, self.n)[1])
+        F0 = self.ctx.empty(self.m) if F0 is None else F0
+        L.check(L.lib().pnol_lm_jacobian_mpi_d(self.ctx.h, self.h, _ptr(x), _ptr(h), _ptr(F0), int(compute_f0),
+                                               _ptr(JTs)), "pnol_lm_jacobian_mpi_d")
+        return F0, JTs
+
     def fd_jacobian_tiles(self, x, h, tiles, JT, F0=None, compute_f0=True):
         """FD rows of the (start, count) tiles into JT (row c = column c); returns (F0, JT)."""
         F0 = self.ctx.empty(self.m) if F0 is None else F0
@@ -212,6 +231,24 @@ class DeviceObjective:
                                                  int(compute_f0), _ptr(JT), JT.stride(0)),
                 "pnol_fd_jacobian_tiles_d")
         return F0, JT
+
+
+def lm_sliced_layout(m, n):
+    """(slice_rows, number of doubles) of the m-sliced J^T: slice s = rows [s*mS, (s+1)*mS) of J,
+    an n x mS row-major block at offset s*n*mS."""
+    mS, tot = C.c_int(), C.c_size_t()
+    L.check(L.lib().pnol_lm_sliced_layout(m, n, C.byref(mS), C.byref(tot)), "pnol_lm_sliced_layout")
+    return mS.value, tot.value
+
+
+def to_sliced(JT, mS):
+    """numpy n x m J^T -> the sliced layout (PNOL_LM_SLICES blocks of n x mS, zero padded)."""
+    n, m = JT.shape
+    out = np.zeros((L.LM_SLICES, n, mS))
+    for s in range(L.LM_SLICES):
+        blk = JT[:, s * mS:(s + 1) * mS]
+        out[s, :, :blk.shape[1]] = blk
+    return out
 
 
 def run_bfgs(obj: DeviceObjective, x0, params, which=0, host_eval=False, lb=None, ub=None):

@@ -12,6 +12,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     out, m, n = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    lm_only = len(sys.argv) > 4 and sys.argv[4] == "lm"
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
@@ -30,6 +31,22 @@ def main():
     L.check(L.lib().pnol_jtj_mpi_d(ctx.h, JT.data_ptr(), m, m, n, 0.25, A.data_ptr(), n, diag.data_ptr()),
             "pnol_jtj_mpi_d")
     ctx.synchronize()
+    # the m-sliced normal equations (pnol_lm_normal_mpi_d) on the same JT and a random F:
+    # every rank uploads the whole sliced layout and reads only its own slices
+    from parallelnonlinearoptimizationlibrary_amd.device import lm_sliced_layout, to_sliced
+    mS, _ = lm_sliced_layout(m, n)
+    JTs = ctx.tensor(to_sliced(JT.cpu().numpy(), mS).reshape(-1))
+    Fr = ctx.tensor(np.random.default_rng(12).standard_normal(m))
+    As, rs, ds = ctx.lm_normal_mpi(JTs, m, n, 0.25, Fr, want_diag=True)
+    ctx.synchronize()
+    res = dict(X=X, A=A.cpu().numpy(), diag=diag.cpu().numpy(), As=As.cpu().numpy(), rs=rs.cpu().numpy(),
+               ds=ds.cpu().numpy())
+    if lm_only:
+        np.savez(os.path.join(out, f"rank{rank}.npz"), **res)
+        comm.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     # BFGSBnd_MPI, testBFGSBnd_MPI start (Examples.cpp:90-120): Npool = world, pool entries
     # round-robin over the ranks, FD gradients sharded
     nb = 10
@@ -63,7 +80,7 @@ def main():
     nq = 300
     Pq = [1e-4, 0.9, 4, 1, 1000, 1e-6, 1e-3, 40, 1e-9, 1e-6, 0, 0, 4, 1, 2]
     Xq, resq = run_bfgs(DeviceObjective.synthetic(ctx, L.OBJ_QUADRATIC, nq), np.zeros(nq), Pq, which=1)
-    np.savez(os.path.join(out, f"rank{rank}.npz"), X=X, A=A.cpu().numpy(), diag=diag.cpu().numpy(), Xb=Xb,
+    np.savez(os.path.join(out, f"rank{rank}.npz"), **res, Xb=Xb,
              fb=np.array([resb.fopt]), Xs=Xs, fs=np.array([ress.fopt]), hg=p.cpu().numpy(), u=u.cpu().numpy(),
              w=w.cpu().numpy(), v=v.cpu().numpy(), Drows=Dsh.cpu().numpy()[:rc], rows=np.array([rb, rc]), Xq=Xq,
              fq=np.array([resq.fopt]))

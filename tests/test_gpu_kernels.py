@@ -413,6 +413,41 @@ def test_fd_checkpoint_reuse_bitwise(ctx, oracle, m, n):
     assert np.array_equal(_np(JT), ref)
 
 
+@pytest.mark.parametrize("m,n", [(2000, 300), (5000, 1000), (777, 129), (16384, 2048)])
+def test_lm_sliced_jacobian_and_normal_bitwise(ctx, m, n):
+    """One rank of the m-sliced LevMarqMPI path: pnol_lm_jacobian_mpi_d writes the same J values
+    into the sliced layout, and pnol_lm_normal_mpi_d gives A, diag(J^T J) and -J^T F bitwise
+    equal to pnol_fd_jacobian_d + pnol_jtj_d + pnol_jtr_d (one summation tree on both paths)."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective, lm_sliced_layout
+    d = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+    x = ctx.tensor(np.linspace(-0.5, 0.5, n)); h = ctx.tensor(np.full(n, 1e-7))
+    F0a, JTa = d.fd_jacobian(x, h, 0, n)
+    Aa, da = ctx.jtj(JTa, 0.37, want_diag=True)
+    ra = ctx.jtr(JTa, F0a)
+    mS, tot = lm_sliced_layout(m, n)
+    assert mS % 64 == 0 and L.LM_SLICES * mS >= m and tot == L.LM_SLICES * n * mS
+    F0b, JTs = d.lm_jacobian_mpi(x, h)
+    Ab, rb, db = ctx.lm_normal_mpi(JTs, m, n, 0.37, F0b, want_diag=True)
+    ctx.synchronize()
+    assert np.array_equal(_np(F0b), _np(F0a))
+    js = _np(JTs).reshape(L.LM_SLICES, n, mS)
+    ja = _np(JTa)
+    for s in range(L.LM_SLICES):
+        w = min(mS, max(0, m - s * mS))
+        assert np.array_equal(js[s, :, :w], ja[:, s * mS:s * mS + w]), s
+    assert np.array_equal(_np(Ab), _np(Aa))
+    assert np.array_equal(_np(db), _np(da))
+    assert np.array_equal(_np(rb), _np(ra))
+    # and the tree sums are the sums: fp64 torch reference
+    import torch
+    J = JTa.double()
+    ref = J @ J.T
+    assert float((torch.diagonal(Ab) / 1.37 - torch.diagonal(ref)).abs().max() / ref.abs().max()) < 1e-12
+    rr = -(J @ F0a)
+    assert float((rb - rr).abs().max() / rr.abs().max()) < 1e-12
+
+
 @pytest.mark.parametrize("m,n,chunks", [(2000, 700, 4), (1500, 1000, 3), (513, 2048, 8), (300, 129, 2), (400, 300, 1)])
 def test_fd_jtj_pipelined_bitwise(ctx, m, n, chunks):
     """The pipelined FD Jacobian + J^T J (two streams, chunked) equals the two separate calls

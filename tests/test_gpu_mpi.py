@@ -24,18 +24,15 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_levmarq_mpi_ranks_bitwise_equal_single(tmp_path, world, oracle):
-    from parallelnonlinearoptimizationlibrary_amd import _lib as L
-    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_levmarq
-    m, n = 2000, 300     # 6 J^T J tiles: uneven tile ranges at world = 3 / 4
+def _run_workers(tmp_path, world, m, n, *extra):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", PNOL_DEVICE="0",
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_mpi_worker.py"), str(tmp_path),
-                                       str(m), str(n)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+                                       str(m), str(n), *extra], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT))
     outs = []
     for p in procs:
         try:
@@ -47,18 +44,47 @@ def test_levmarq_mpi_ranks_bitwise_equal_single(tmp_path, world, oracle):
         outs.append(o.decode(errors="replace"))
     assert all(p.returncode == 0 for p in procs), "\n".join(o[-3000:] for o in outs)
 
+
+def _check_levmarq_and_normal(tmp_path, world, m, n):
+    """LevMarqMPI X, the tile-split J^T J and the m-sliced normal equations of every rank equal
+    the single-GPU LevMarq / pnol_jtj_d / pnol_jtr_d bitwise."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_levmarq
     ctx = Context(0)
     obj = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
     X1, *_ = run_levmarq(obj, np.zeros(n), (0.001, 10.0, 1e-7, 5, 0.0, -1), which=0)
     rng = np.random.default_rng(11)
     JT = ctx.tensor(rng.standard_normal((n, m)))
     A1, d1 = ctx.jtj(JT, 0.25, want_diag=True)
-    A1, d1 = A1.cpu().numpy(), d1.cpu().numpy()
+    r1 = ctx.jtr(JT, ctx.tensor(np.random.default_rng(12).standard_normal(m)))
+    A1, d1, r1 = A1.cpu().numpy(), d1.cpu().numpy(), r1.cpu().numpy()
     for r in range(world):
         z = np.load(tmp_path / f"rank{r}.npz")
         assert np.array_equal(z["X"], X1), r
         assert np.array_equal(z["A"], A1), r
         assert np.array_equal(z["diag"], d1), r
+        assert np.array_equal(z["As"], A1), r
+        assert np.array_equal(z["ds"], d1), r
+        assert np.array_equal(z["rs"], r1), r
+
+
+@pytest.mark.parametrize("world", [4, 5, 8])
+def test_levmarq_mpi_m_sliced_more_ranks(tmp_path, world):
+    """The m-sliced LevMarqMPI path at 4, 5 and 8 ranks (one slice per rank at 8; uneven
+    dyadic slice covers at 5), bitwise the single-GPU results."""
+    m, n = 1500, 200
+    _run_workers(tmp_path, world, m, n, "lm")
+    _check_levmarq_and_normal(tmp_path, world, m, n)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_levmarq_mpi_ranks_bitwise_equal_single(tmp_path, world, oracle):
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_bfgs
+    m, n = 2000, 300     # 6 J^T J tiles: uneven tile ranges at world = 3 / 4
+    _run_workers(tmp_path, world, m, n)
+    _check_levmarq_and_normal(tmp_path, world, m, n)
+    ctx = Context(0)
     # BFGSBnd_MPI across the ranks equals the reference at np = world
     nb = 10
     x0 = np.full(nb, 3.0); x0[0] = -0.5
