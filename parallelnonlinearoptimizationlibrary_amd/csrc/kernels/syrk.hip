@@ -85,8 +85,8 @@ __device__ __forceinline__ void store_stage(const StageRegs<TILE, NT>& s, double
 // accumulators per wave, so twice the waves per SIMD hide the stage boundaries).
 template <int MODE, int TILE, bool XMAP = false, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
-                                                      int split_k, int kchunk, int sub, int slice0, int mS,
-                                                      long sstride, double* __restrict__ part,
+                                                      int split_k, int kfirst, int kchunk, int sub, int slice0,
+                                                      int mS, long sstride, int umajor, double* __restrict__ part,
                                                       double* __restrict__ C, long ldc, double alpha,
                                                       double beta, int tile0) {
     constexpr int NT = 64 * NW, WC = NW / 2;
@@ -105,6 +105,15 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
         const int tl = local % ntl;
         blk = tl * split_k + sidx;           // partial slot: the same layout as below
         t = tile0 + tl;
+    } else if (umajor) {
+        // every (tile, slice)'s chunk 0 first, then chunk 1, ...: with a long chunk 0 the short
+        // chunks fill the last dispatch round instead of leaving it part-empty
+        const int ntl = gridDim.x / split_k, nsl = split_k / sub;
+        const int u0 = blockIdx.x / (ntl * nsl), rest = blockIdx.x % (ntl * nsl);
+        const int tl = rest / nsl;
+        sidx = (rest % nsl) * sub + u0;
+        blk = tl * split_k + sidx;
+        t = tile0 + tl;
     } else {
         blk = blockIdx.x;                    // partial slot (local to this launch)
         t = tile0 + blk / split_k;           // lower-triangle tile index
@@ -119,8 +128,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
     // plain row-major layout)
     const int slice = slice0 + sidx / sub, u = sidx % sub;
     X += (long)slice * (sstride - mS);
-    const int kbeg = slice * mS + u * kchunk;
-    const int kend = min(K, min((slice + 1) * mS, kbeg + kchunk));
+    // sub-chunk 0 is [0, kfirst) of the slice, chunk u >= 1 [kfirst + (u-1) kchunk, + kchunk)
+    const int kbeg = slice * mS + (u == 0 ? 0 : kfirst + (u - 1) * kchunk);
+    const int kend = min(K, min((slice + 1) * mS, u == 0 ? slice * mS + kfirst : kbeg + kchunk));
     const int nstages = kend > kbeg ? (kend - kbeg + kTK - 1) / kTK : 0;
 
     const int lane = threadIdx.x & 63;
@@ -331,12 +341,11 @@ __global__ void k_syrk_unpack(const double* __restrict__ packed, int ntiles, int
 // row-wise, and writes the mirror from an LDS transpose so those stores are row-wise too.
 // SUB > 0: the sub-chunk count at compile time (all kS * SUB loads of an element in flight at
 // once); SUB = 0: runtime `sub`.
-template <int SUB>
+template <int SUB, int SR = 32>
 __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ part, int ntiles, int sub_rt, int n,
                                                      double lambda, double* __restrict__ A, long lda,
                                                      double* __restrict__ diag_out, int tile0) {
-    const int sub = SUB > 0 ? SUB : sub_rt;
-    constexpr int SR = 32;                                 // strip rows
+    const int sub = SUB > 0 ? SUB : sub_rt;                // SR: strip rows
     __shared__ double st[SR][kTile + 1];
     const int t = tile0 + blockIdx.y;                      // part holds this launch's tiles from tile0 on
     int ti, tj;
@@ -346,6 +355,7 @@ __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ 
     const long E = kTile * kTile;
     const double* p = part + ((long)(t - tile0) * kS * sub) * E + (long)r0 * kTile;
     // 32 x 128 doubles = 2048 double2; 256 threads x 8
+#pragma unroll 2
     for (int q = threadIdx.x; q < SR * kTile / 2; q += 256) {
         const int r = (2 * q) / kTile, c = (2 * q) % kTile;
         double lx[kS], ly[kS];
@@ -413,21 +423,36 @@ __global__ void k_jtj_seq(const double* __restrict__ JT, long ldjt, int m, int n
 // m = 16384, n = 2048 (136 tiles) sub = 2: 2176 workgroups of K = 1024 (measured: SYRK 1.33 ms
 // + reduce 0.09 ms, vs 1.42 + 0.05 ms at sub = 1).  PNOL_SYRK_SUB overrides.
 struct SliceCfg {
-    int mS, sub, kchunk;
+    int mS, sub, kfirst, kchunk;
 };
 
 // k_syrk_reduce with the sub-chunk count as a template constant where it is 1, 2 or 4
+// (grid.x = 128 / 32 strips per tile at SR = 32; SR = 16 launches twice the workgroups)
+template <int SR, typename... Args>
+static void launch_reduce_sr(dim3 grid, dim3 block, size_t shm, hipStream_t st, const double* part, int ntiles,
+                             int sub, Args... args) {
+    grid.x = grid.x * 32 / SR;
+    if (sub == 1)
+        hipLaunchKernelGGL((k_syrk_reduce<1, SR>), grid, block, shm, st, part, ntiles, sub, args...);
+    else if (sub == 2)
+        hipLaunchKernelGGL((k_syrk_reduce<2, SR>), grid, block, shm, st, part, ntiles, sub, args...);
+    else if (sub == 4)
+        hipLaunchKernelGGL((k_syrk_reduce<4, SR>), grid, block, shm, st, part, ntiles, sub, args...);
+    else
+        hipLaunchKernelGGL((k_syrk_reduce<0, SR>), grid, block, shm, st, part, ntiles, sub, args...);
+}
+
 template <typename... Args>
 static void launch_reduce(dim3 grid, dim3 block, size_t shm, hipStream_t st, const double* part, int ntiles, int sub,
                           Args... args) {
-    if (sub == 1)
-        hipLaunchKernelGGL(k_syrk_reduce<1>, grid, block, shm, st, part, ntiles, sub, args...);
-    else if (sub == 2)
-        hipLaunchKernelGGL(k_syrk_reduce<2>, grid, block, shm, st, part, ntiles, sub, args...);
-    else if (sub == 4)
-        hipLaunchKernelGGL(k_syrk_reduce<4>, grid, block, shm, st, part, ntiles, sub, args...);
-    else
-        hipLaunchKernelGGL(k_syrk_reduce<0>, grid, block, shm, st, part, ntiles, sub, args...);
+    static const int sr = [] {
+        const char* e = std::getenv("PNOL_REDUCE_SR");
+        return e ? std::atoi(e) : 16;
+    }();
+    if (sr == 32)
+        launch_reduce_sr<32>(grid, block, shm, st, part, ntiles, sub, args...);
+    else   // 16-row strips (default): 70 us vs 77 us for 32-row strips at n = 2048, sub = 2
+        launch_reduce_sr<16>(grid, block, shm, st, part, ntiles, sub, args...);
 }
 
 static SliceCfg slice_cfg(int m, int ntiles) {
@@ -445,6 +470,19 @@ static SliceCfg slice_cfg(int m, int ntiles) {
         c.sub = std::max(1, std::min(want, cap));
     }
     c.kchunk = ((c.mS + c.sub - 1) / c.sub + kTK - 1) / kTK * kTK;
+    c.kfirst = c.kchunk;
+    // Chunk 0 takes 75% of the slice (PNOL_SYRK_FIRST = percent; the rest split evenly over
+    // chunks 1..sub-1) and is dispatched first (PNOL_SYRK_UMAJOR): 1088 long workgroups, then
+    // 1088 short ones that fill the tail of the last dispatch round.  Measured at m = 16384,
+    // n = 2048: 1.265 ms vs 1.326 ms for two equal chunks (tools/syrk_sweep.py).
+    static const int first_pct = [] {
+        const char* e = std::getenv("PNOL_SYRK_FIRST");
+        return e ? std::atoi(e) : 75;
+    }();
+    if (c.sub >= 2 && first_pct > 0 && first_pct < 100) {
+        c.kfirst = std::max(kTK, (int)((long)c.mS * first_pct / 100) / kTK * kTK);
+        c.kchunk = ((c.mS - c.kfirst + c.sub - 2) / (c.sub - 1) + kTK - 1) / kTK * kTK;
+    }
     return c;
 }
 
@@ -459,6 +497,14 @@ static int syrk_nw() {
         return (e && std::atoi(e) == 4) ? 4 : 8;
     }();
     return nw;
+}
+
+static int syrk_umajor() {
+    static const int v = [] {
+        const char* e = std::getenv("PNOL_SYRK_UMAJOR");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
 }
 
 static bool syrk_xmap() {
@@ -479,16 +525,16 @@ static void syrk_partials(pnol_ctx* ctx, hipStream_t stream, bool rows_variant, 
     const dim3 grid(ntl * split);
     if (rows_variant)
         hipLaunchKernelGGL((k_syrk_tile<2, kTile, false, 8>), grid, dim3(512), 0, stream, X, ldx, nr, K, split,
-                           sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
+                           sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
     else if (syrk_nw() == 8)
         hipLaunchKernelGGL((k_syrk_tile<0, kTile, false, 8>), grid, dim3(512), 0, stream, X, ldx, nr, K, split,
-                           sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
+                           sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
     else if (syrk_xmap() && split % kNumXcd == 0)
-        hipLaunchKernelGGL((k_syrk_tile<0, kTile, true>), grid, dim3(256), 0, stream, X, ldx, nr, K, split, sc.kchunk,
-                           sc.sub, slice0, sc.mS, sstride, part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
+        hipLaunchKernelGGL((k_syrk_tile<0, kTile, true>), grid, dim3(256), 0, stream, X, ldx, nr, K, split, sc.kfirst,
+                           sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
     else
-        hipLaunchKernelGGL((k_syrk_tile<0, kTile>), grid, dim3(256), 0, stream, X, ldx, nr, K, split, sc.kchunk,
-                           sc.sub, slice0, sc.mS, sstride, part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
+        hipLaunchKernelGGL((k_syrk_tile<0, kTile>), grid, dim3(256), 0, stream, X, ldx, nr, K, split, sc.kfirst,
+                           sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
 }
 
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
@@ -604,8 +650,8 @@ int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, do
     constexpr int kT = 64;
     const int nt = (nr + kT - 1) / kT;
     const int ntiles = nt * (nt + 1) / 2;
-    hipLaunchKernelGGL((k_syrk_tile<1, kT>), dim3(ntiles), dim3(256), 0, ctx->stream, X, (long)ldx, nr, K, 1, K, 1, 0,
-                       K, (long)K, (double*)nullptr, C, (long)ldc, alpha, 1.0, 0);
+    hipLaunchKernelGGL((k_syrk_tile<1, kT>), dim3(ntiles), dim3(256), 0, ctx->stream, X, (long)ldx, nr, K, 1, K, K, 1,
+                       0, K, (long)K, 0, (double*)nullptr, C, (long)ldc, alpha, 1.0, 0);
     return launch_check();
 }
 
