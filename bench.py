@@ -93,11 +93,11 @@ def fd_flop_minimal(m, tiles, n):
     return 2.0 * m * sum(n - j for s0, cnt in tiles for j in range(s0, s0 + cnt))
 
 
-def pmc_valu():
-    """VALU-busy fractions of the hot kernels from the newest committed PMC summary
-    (profiles/r*_pmc_fd_valu.json, tools/pmc_valu.py), or {}."""
+def pmc_valu(kind="fd_valu"):
+    """VALU- (or MFMA-) busy fractions of the hot kernels from the newest committed PMC summary
+    (profiles/r*_pmc_fd_valu.json / r*_pmc_syrk_mfma.json, tools/pmc_valu.py), or {}."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_fd_valu.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{kind}.json")))
     if not files:
         return {}
     try:
@@ -322,6 +322,8 @@ def main():
             "bound": "mfma", "achieved": jtj_flop / (syrk_ms * 1e-3) / 1e12 if syrk_ms else None,
             "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "traffic": pmc.get("k_syrk_tile<0, 128>", {}).get("traffic_bytes_per_launch"),
+            "mfma_busy_pmc": next((v.get("mfma_busy_frac") for k, v in pmc_valu("syrk_mfma").items()
+                                   if "k_syrk_tile" in k), None),
         }
         roofline["frac"] = roofline["achieved"] / FP64_PEAK_TFLOPS if roofline["achieved"] else None
         fd_ms = per["fd_jacobian"]

@@ -47,4 +47,9 @@ if [ "${VALU:-0}" = "1" ]; then
       python3 tools/fd_only.py 4 > gpurun_out/pmc_valu.log 2>&1
   rc=$?; echo "pmc valu rc=$rc"; [ "$rc" -eq 0 ] || exit $rc
 fi
+if [ "${MFMA:-0}" = "1" ]; then
+  timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_mfma -o pmc \
+      --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_mfma.log 2>&1
+  rc=$?; echo "pmc mfma rc=$rc"; [ "$rc" -eq 0 ] || exit $rc
+fi
 exit 0

@@ -25,6 +25,8 @@ for name, d in vals.items():
     e = {"counters_per_launch": avg, "launches": len(next(iter(d.values())))}
     if "SQ_ACTIVE_INST_VALU" in avg and "GRBM_GUI_ACTIVE" in avg:
         e["valu_busy_frac"] = 4 * avg["SQ_ACTIVE_INST_VALU"] / (avg["GRBM_GUI_ACTIVE"] / 8 * 1024)
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and "GRBM_GUI_ACTIVE" in avg:
+        e["mfma_busy_frac"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (avg["GRBM_GUI_ACTIVE"] / 8 * 1024)
     if "SQ_WAVE_CYCLES" in avg:
         w = avg["SQ_WAVE_CYCLES"]
         e["wave_cycle_split"] = {k: avg[k] / w for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY")
