@@ -267,9 +267,18 @@ def main():
                 "pnol_run_levmarq")
         return X
 
+    # warmup with every per-kernel timer on: the full breakdown (untimed); the timed region
+    # keeps only the timers of the kernels priced below (each timer adds two event records
+    # between launches, ~1.5% of a trip with all of them on)
+    names = ("fd_jtj", "fd_jacobian", "fd_ckpt", "linres_eval", "syrk", "syrk_rows", "syrk_reduce", "jtr", "solve",
+             "allgather", "exchange_J", "exchange_A")
+    L.check(L.lib().pnol_ctx_enable_timers(dctx, 0 if args.no_timers else 1), "timers")
+    L.check(L.lib().pnol_ctx_reset_timers(dctx), "timers")
     run(args.warmup)
     torch.cuda.synchronize()
-    L.check(L.lib().pnol_ctx_enable_timers(dctx, 0 if args.no_timers else 1), "timers")
+    breakdown = {k: _timer(L, dctx, k) for k in names}
+    breakdown = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in breakdown.items()}
+    L.check(L.lib().pnol_ctx_enable_timers(dctx, 0 if args.no_timers else 2), "timers")
     L.check(L.lib().pnol_ctx_reset_timers(dctx), "timers")
     if world > 1:
         dist.barrier()
@@ -285,9 +294,7 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=_red_dev())
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    timers = {k: _timer(L, dctx, k) for k in ("fd_jtj", "fd_jacobian", "fd_ckpt", "linres_eval", "syrk", "syrk_rows",
-                                              "syrk_reduce", "jtr", "solve", "allgather", "exchange_J",
-                                              "exchange_A")}
+    timers = {k: _timer(L, dctx, k) for k in names}
     # per-step kernel times, max over ranks (the slowest rank sets the pace)
     per_local = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timers.items()}
     if world > 1:
@@ -367,7 +374,8 @@ def main():
                        "m": m, "n": n, "parallelism": f"fd-columns+m-slices x{world}" if world > 1 else "single"},
             "roofline": roofline,
             "rooflines": rooflines,
-            "kernel_ms_per_step": per,
+            "kernel_ms_per_step": per,   # timed region: the priced kernels only
+            "kernel_ms_per_call_warmup_breakdown": breakdown,   # every timer, warmup trips (untimed)
             "kernel_ms_per_step_max_over_ranks": per_max,
             # the north star's strong-scaling quantity: the sharded FD Jacobian + its exchange
             # (m-slice point-to-point exchange; the column-row allgather with PNOL_LM_SLICED=0)

@@ -52,7 +52,9 @@ int pnol_default_ctx(pnol_ctx** out);
 
 /* Per-kernel HIP-event timers on the context's stream (off by default).  Names: "fd_jacobian",
  * "fd_ckpt", "fd_gradient", "linres_eval", "syrk", "syrk_reduce", "jtr", "solve", "hg",
- * "bfgs_pass", "allgather".  total_ms sums the recorded launches since the last reset. */
+ * "bfgs_pass", "allgather", "exchange_J", "exchange_A".  total_ms sums the recorded launches
+ * since the last reset.  on = 2 times only "fd_jacobian", "fd_ckpt", "syrk", "exchange_J",
+ * "allgather", "hg" and "bfgs_pass" (fewer event records between launches). */
 int pnol_ctx_enable_timers(pnol_ctx* ctx, int on);
 int pnol_ctx_reset_timers(pnol_ctx* ctx);
 int pnol_ctx_timer(pnol_ctx* ctx, const char* name, double* total_ms, int* count);

@@ -27,7 +27,7 @@ struct Workspace {
 namespace pnol {
 // start/stop event pairs per kernel name, resolved lazily (pnol_ctx_timer)
 struct Timers {
-    bool on = false;
+    int on = 0;   // 0 off, 1 every timer, 2 only the roofline / scaling kernels (hot_timer)
     std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::map<std::string, std::pair<double, int>> done;
     std::vector<hipEvent_t> free_events;   // recycled after resolve (event creation is not free)

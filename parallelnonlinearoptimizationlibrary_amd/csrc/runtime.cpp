@@ -264,9 +264,18 @@ int comm_allgather_device(pnol_ctx* ctx, const double* send, double* recv, size_
 // ---------------------------------------------------------------------------------------
 // kernel timers
 // ---------------------------------------------------------------------------------------
+// mode 2: the kernels bench.py prices against a roofline or a scaling target; each timer
+// costs two event records between launches (~5 us of dispatch gap each)
+static bool hot_timer(const char* name) {
+    for (const char* h : {"fd_jacobian", "fd_ckpt", "syrk", "exchange_J", "allgather", "hg", "bfgs_pass"})
+        if (std::strcmp(name, h) == 0) return true;
+    return false;
+}
+
 ScopedTimer::ScopedTimer(pnol_ctx* ctx, const char* name, hipStream_t stream)
     : ctx_(ctx), name_(name), stream_(stream) {
     if (!ctx_ || !ctx_->timers.on) return;
+    if (ctx_->timers.on == 2 && !hot_timer(name)) return;
     if (!stream_) stream_ = ctx_->stream;
     auto& pool = ctx_->timers.free_events;
     for (hipEvent_t* e : {&a_, &b_}) {
@@ -434,7 +443,7 @@ int pnol_default_ctx(pnol_ctx** out) {
 
 int pnol_ctx_enable_timers(pnol_ctx* ctx, int on) {
     if (!ctx) return PNOL_ERR_ARG;
-    ctx->timers.on = on != 0;
+    ctx->timers.on = on == 2 ? 2 : (on != 0 ? 1 : 0);
     return PNOL_OK;
 }
 
