@@ -182,12 +182,14 @@ class LMAsync {
         A_.reset(ctx, (size_t)n * lda_);
         rhs_.reset(ctx, n);
         h_.reset(ctx, n);
+        // trip s's results side by side -- sigma_s | F(x_s + sigma_s) | solve status -- so one
+        // copy brings them to the host; F(x_[s]) is trip s^1's middle part
+        np_ = even_ld(n);
+        mp_ = even_ld(m);
         for (int s = 0; s < 2; ++s) {
             x_[s].reset(ctx, n);
-            F_[s].reset(ctx, m);
-            sig_[s].reset(ctx, n);
-            info_[s].reset(ctx, 1);
-            check(pnol_host_alloc(&pin_[s], sizeof(double) * ((size_t)n + m + 1)), "host_alloc");
+            trip_[s].reset(ctx, (size_t)np_ + mp_ + 2);
+            check(pnol_host_alloc(&pin_[s], sizeof(double) * ((size_t)np_ + mp_ + 2)), "host_alloc");
             check(pnol_event_create(ctx, &ev_[s]), "event_create");
         }
     }
@@ -199,38 +201,36 @@ class LMAsync {
         }
     }
     double* x(int s) { return x_[s].get(); }
-    double* F(int s) { return F_[s].get(); }
+    double* F(int s) { return trip_[s ^ 1].get() + np_; }   // F(x_[s])
+    double* sig(int s) { return trip_[s].get(); }
+    int* info(int s) { return reinterpret_cast<int*>(trip_[s].get() + np_ + mp_); }
     const double* sigma_h(int s) const { return static_cast<const double*>(pin_[s]); }
-    const double* Fnext_h(int s) const { return static_cast<const double*>(pin_[s]) + n_; }
-    int info_h(int s) const { return *reinterpret_cast<const int*>(static_cast<const double*>(pin_[s]) + n_ + m_); }
+    const double* Fnext_h(int s) const { return static_cast<const double*>(pin_[s]) + np_; }
+    int info_h(int s) const { return *reinterpret_cast<const int*>(static_cast<const double*>(pin_[s]) + np_ + mp_); }
     void uploadH(const std::vector<double>& dX) { h_.upload(dX); }
 
     // trip at x_[s] (F_[s] = F(x_[s]); ckpt: its checkpoints are current) -> sigma, x_[s^1], F_[s^1]
     void enqueue(int s, double lambda, bool ckpt) {
         if (sliced_) {
-            check(pnol_lm_jacobian_mpi_d(ctx_, d_, x_[s].get(), h_.get(), F_[s].get(), ckpt ? 2 : 1, JT_.get()),
+            check(pnol_lm_jacobian_mpi_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 2 : 1, JT_.get()),
                   "fd_jacobian");
-            check(pnol_lm_normal_mpi_d(ctx_, JT_.get(), m_, n_, lambda, F_[s].get(), A_.get(), lda_, rhs_.get(),
+            check(pnol_lm_normal_mpi_d(ctx_, JT_.get(), m_, n_, lambda, F(s), A_.get(), lda_, rhs_.get(),
                                        nullptr),
                   "normal equations");
         } else {
-            check(pnol_fd_jtj_d(ctx_, d_, x_[s].get(), h_.get(), F_[s].get(), ckpt ? 2 : 1, JT_.get(), ldjt_, lambda,
+            check(pnol_fd_jtj_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 2 : 1, JT_.get(), ldjt_, lambda,
                                 A_.get(), lda_, nullptr, 1),
                   "fd_jtj");
-            check(pnol_jtr_d(ctx_, JT_.get(), ldjt_, m_, n_, F_[s].get(), rhs_.get()), "jtr");
+            check(pnol_jtr_d(ctx_, JT_.get(), ldjt_, m_, n_, F(s), rhs_.get()), "jtr");
         }
-        int* di = reinterpret_cast<int*>(info_[s].get());
-        check(pnol_solve_async_d(ctx_, A_.get(), lda_, rhs_.get(), sig_[s].get(), n_, di), "solve");
+        check(pnol_solve_async_d(ctx_, A_.get(), lda_, rhs_.get(), sig(s), n_, info(s)), "solve");
         finish(s);
     }
     // the rest of a trip once sigma_[s] is known: trial point, its residuals, copies back
     void finish(int s) {
-        check(pnol_add_d(ctx_, x_[s].get(), sig_[s].get(), x_[s ^ 1].get(), n_), "add");
-        check(pnol_dobj_eval_ckpt_d(ctx_, d_, x_[s ^ 1].get(), F_[s ^ 1].get()), "objective eval");
-        double* pin = static_cast<double*>(pin_[s]);
-        check(pnol_memcpy_d2h_async(ctx_, pin, sig_[s].get(), sizeof(double) * n_), "d2h");
-        check(pnol_memcpy_d2h_async(ctx_, pin + n_, F_[s ^ 1].get(), sizeof(double) * m_), "d2h");
-        check(pnol_memcpy_d2h_async(ctx_, pin + n_ + m_, info_[s].get(), sizeof(int)), "d2h");
+        check(pnol_add_d(ctx_, x_[s].get(), sig(s), x_[s ^ 1].get(), n_), "add");
+        check(pnol_dobj_eval_ckpt_d(ctx_, d_, x_[s ^ 1].get(), F(s ^ 1)), "objective eval");
+        check(pnol_memcpy_d2h_async(ctx_, pin_[s], trip_[s].get(), sizeof(double) * ((size_t)np_ + mp_ + 1)), "d2h");
         check(pnol_event_record(ctx_, ev_[s]), "event");
     }
     void wait(int s) { check(pnol_event_wait(ev_[s]), "event wait"); }
@@ -238,7 +238,7 @@ class LMAsync {
     void redo_lu(int s) {
         check(pnol_ctx_synchronize(ctx_), "sync");
         int info = 0;
-        check(pnol_solve_d(ctx_, A_.get(), lda_, rhs_.get(), sig_[s].get(), n_, 2, &info), "solve");
+        check(pnol_solve_d(ctx_, A_.get(), lda_, rhs_.get(), sig(s), n_, 2, &info), "solve");
         finish(s);
         wait(s);
     }
@@ -248,7 +248,8 @@ class LMAsync {
     pnol_dobj* d_;
     int n_, m_, ldjt_, lda_;
     bool sliced_;
-    DevVec JT_, A_, rhs_, h_, x_[2], F_[2], sig_[2], info_[2];
+    int np_ = 0, mp_ = 0;
+    DevVec JT_, A_, rhs_, h_, x_[2], trip_[2];
     void* pin_[2] = {nullptr, nullptr};
     pnol_event* ev_[2] = {nullptr, nullptr};
 };
