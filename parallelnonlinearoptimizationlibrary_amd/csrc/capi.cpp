@@ -80,7 +80,7 @@ int pnol_jtj_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
 // ---- BFGS D row-sharded over the communicator ----------------------------
 static int bfgs_rows_per(int n, int P) {
     const int per = (n + P - 1) / P;
-    return (per + 255) / 256 * 256;   // whole fused-pass row tiles
+    return (per + 255) / 256 * 256;   // whole fused-pass row tiles (bfgs_pass_rows divides 256)
 }
 
 }  // extern "C" (reopened below)
@@ -99,7 +99,7 @@ namespace {
 int pass_w_allgather(pnol_ctx* ctx, double* part_w, int n, int nrowt) {
     (void)nrowt;
     const int P = comm_size(), r = comm_rank();
-    const size_t cnt = (size_t)(bfgs_rows_per(n, P) / 256) * n;
+    const size_t cnt = (size_t)(bfgs_rows_per(n, P) / bfgs_pass_rows(n)) * n;
     return comm_allgather_device(ctx, part_w + (size_t)r * cnt, part_w, cnt);
 }
 

@@ -321,7 +321,6 @@ __global__ void k_bfgs_exact_2(const double* __restrict__ T, double* __restrict_
 // 128-column strip; column partials (w = Dc^T y) stay in registers and are written per
 // 256-row tile.  k_bfgs_pass_finish sums the partials in a fixed order: deterministic.
 // ------------------------------------------------------------------------------------
-constexpr int kPassRows = 256;
 constexpr int kPassCols = 512;
 constexpr int kGroup = 8;
 
@@ -390,10 +389,10 @@ __device__ __forceinline__ void pass_load(double2 (&d)[kGroup], const double* __
 // (rotation: concurrently running tiles read different HBM channels); the next group's
 // 16-byte loads are issued before the current group is reduced (register double buffer).
 // Row shard form (BFGS D row-sharded over the ranks): D holds rows [rb, re) of the n x n
-// matrix (rb a multiple of kPassRows); row tiles, partial indices and outputs use global rows,
+// matrix (rb a multiple of the row-tile height); row tiles, partial indices and outputs use global rows,
 // so every partial is the one the whole-matrix pass (rb = 0, re = n) would produce.
 template <bool PEND, bool WB, bool VEC>
-__global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ Dsh, long ldd, int n, int rb, int re,
+__global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ Dsh, long ldd, int n, int rb, int re, int prows,
                                                    const double* __restrict__ sp, const double* __restrict__ ap,
                                                    const double* __restrict__ bp, const double* __restrict__ y,
                                                    const double* __restrict__ g, double* __restrict__ part_u,
@@ -402,7 +401,7 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ Dsh, lon
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int ncolt = (n + kPassCols - 1) / kPassCols;
-    const int rt = rb / kPassRows + blockIdx.x / ncolt;   // global row tile
+    const int rt = rb / prows + blockIdx.x / ncolt;   // global row tile (prows = bfgs_pass_rows(n))
     const int ct = blockIdx.x % ncolt;            // column tile
     const int strip = ct * 4 + wave;              // 128-column strip index
     const int col = strip * 128 + 2 * lane;       // this lane's first column
@@ -420,8 +419,8 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ Dsh, lon
     }
     double w0 = 0.0, w1 = 0.0;
 
-    const int r_begin = rt * kPassRows;
-    const int r_end = min(re, r_begin + kPassRows);
+    const int r_begin = rt * prows;
+    const int r_end = min(re, r_begin + prows);
     const int ngroups = (r_end - r_begin + kGroup - 1) / kGroup;
     int grp = rt % ngroups;
     double2 cur[kGroup];
@@ -638,21 +637,32 @@ int launch_bfgs_update_exact(pnol_ctx* ctx, double* D, int ldd, const double* y,
     return launch_check();
 }
 
-// Whole matrix (rb = 0, re = n) or the row shard [rb, re) (rb a multiple of kPassRows).  With a
+// Whole matrix (rb = 0, re = n) or the row shard [rb, re) (rb a multiple of bfgs_pass_rows(n)).  With a
 // shard, pw_gather (non-null) runs between the pass and the finish: it must fill part_w with
 // every rank's row tiles (the LevMarq/BFGS communicator's allgather), and u / v come out for
 // rows [rb, re) only.
+int bfgs_pass_rows(int n) {
+    static const int forced = [] {
+        const char* e = std::getenv("PNOL_PASS_ROWS");
+        const int v = e ? std::atoi(e) : 0;
+        return (v == 64 || v == 128 || v == 256) ? v : 0;
+    }();
+    if (forced) return forced;
+    return n >= 8192 ? 256 : 128;
+}
+
 int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p, const double* a_p,
                      const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
                      double* v, int rb, int re, int (*pw_gather)(pnol_ctx*, double*, int, int)) {
     if (re < 0) re = n;
-    if (!D || n <= 0 || ldd < n || rb < 0 || re > n || rb > re || (rb < re && rb % kPassRows)) return PNOL_ERR_ARG;
+    const int prows = bfgs_pass_rows(n);
+    if (!D || n <= 0 || ldd < n || rb < 0 || re > n || rb > re || (rb < re && rb % prows)) return PNOL_ERR_ARG;
     const bool pend = s_p != nullptr;
     if (pend && (!a_p || !b_p)) return PNOL_ERR_ARG;
     const int ncolt = (n + kPassCols - 1) / kPassCols;
-    const int nrowt = (n + kPassRows - 1) / kPassRows;
+    const int nrowt = (n + prows - 1) / prows;
     const int nstrips = ncolt * 4;
-    const int myrowt = (re - rb + kPassRows - 1) / kPassRows;
+    const int myrowt = (re - rb + prows - 1) / prows;
     void *pu = nullptr, *pv = nullptr, *pw = nullptr, *zeros = nullptr;
     PNOL_CHECK(ws_get(ctx, "pass_part_u", sizeof(double) * (size_t)nstrips * n, &pu));
     PNOL_CHECK(ws_get(ctx, "pass_part_v", sizeof(double) * (size_t)nstrips * n, &pv));
@@ -669,7 +679,7 @@ int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p
         dim3 grd(myrowt * ncolt), blk(256);
         const bool vec = (ldd % 2 == 0) && aligned16(D);
 #define PNOL_PASS(PE, W, V)                                                                                        \
-    hipLaunchKernelGGL((k_bfgs_pass<PE, W, V>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb, re, s_p, a_p, b_p, y, \
+    hipLaunchKernelGGL((k_bfgs_pass<PE, W, V>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb, re, prows, s_p, a_p, b_p, y, \
                        g, P0, P1, P2)
         if (vec) {
             if (pend && write_back) PNOL_PASS(true, true, true);

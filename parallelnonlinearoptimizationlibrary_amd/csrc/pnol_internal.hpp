@@ -186,6 +186,11 @@ int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lamb
 int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
                        double* JTs);
 
+// Row-tile height of the fused BFGS pass (w = D^T y partials are per row tile): 256 rows when
+// that still gives >= 512 workgroups (n >= 8192), else 128 (n = 4096: 256 workgroups instead of
+// 128).  A function of n only, so the row-sharded pass sums exactly as the whole-matrix one.
+int bfgs_pass_rows(int n);   // blas.hip (PNOL_PASS_ROWS = 64 / 128 / 256 overrides; tuning)
+
 // number of XCDs (8 on MI355X): used only for blockIdx -> tile remaps (speed, never correctness)
 constexpr int kNumXcd = 8;
 
