@@ -78,6 +78,7 @@ __device__ __forceinline__ void store_stage(const StageRegs<TILE, NT>& s, double
 }
 
 // MODE 0: write split-K partial tile to part; MODE 1: C = beta*C + alpha*acc (lower tiles);
+// MODE 4: 64 x 64 tiles into the 128 x 128 partial layout of MODE 0 (see the store below);
 // MODE 2: as MODE 0, instantiated separately for the chunked launches of launch_fd_jtj (so a
 // kernel trace tells the whole-matrix launches and the pipelined row chunks apart).
 // TILE 128: waves 2 x 2 of 64 x 64 (4 x 4 MFMA blocks each); TILE 64: 2 x 2 of 32 x 32.
@@ -183,8 +184,21 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
     // f64 MFMA C/D layout: lane l, register r -> row (l >> 4) + 4 r, column l & 15
     const int ocol = lane & 15;
     const int orow = lane >> 4;
-    if (MODE == 0 || MODE == 2) {
-        double* out = part + (long)blk * TILE * TILE;
+    if (MODE == 0 || MODE == 2 || MODE == 4) {
+        // MODE 4 (TILE 64, tile0 = 0): the quadrant (ti & 1, tj & 1) of the 128 x 128 partial
+        // tile (ti / 2, tj / 2) -- the same partial layout, and every element summed in the same
+        // order as by the 128-row kernel (one MFMA accumulator chain over the same K range)
+        double* out;
+        int ld;
+        if (MODE == 4) {
+            const int t128 = (ti >> 1) * ((ti >> 1) + 1) / 2 + (tj >> 1);
+            out = part + ((long)t128 * split_k + sidx) * (4 * TILE * TILE) + (long)(ti & 1) * TILE * (2 * TILE) +
+                  (tj & 1) * TILE;
+            ld = 2 * TILE;
+        } else {
+            out = part + (long)blk * TILE * TILE;
+            ld = TILE;
+        }
 #pragma unroll
         for (int mi = 0; mi < NBM; ++mi)
 #pragma unroll
@@ -193,7 +207,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                 for (int r = 0; r < 4; ++r) {
                     int row = wr * WTM + mi * 16 + orow + 4 * r;
                     int col = wc * WTN + ni * 16 + ocol;
-                    out[row * TILE + col] = acc[mi][ni][r];
+                    out[row * ld + col] = acc[mi][ni][r];
                 }
     } else {
 #pragma unroll
@@ -507,6 +521,17 @@ static int syrk_umajor() {
     return v;
 }
 
+// 64 x 64 output tiles (MODE 4) instead of 128 x 128 for the whole-matrix launches: 4x the
+// workgroups (4 per CU), the same per-element sums.  Measured at m = 16384, n = 2048 on the
+// sliced J^T (16 KB row stride): 1.23 ms vs 1.29 ms, and a rank of an 8-GPU LevMarqMPI (one
+// m-slice) gets 1056 workgroups instead of 272; on the row-major J^T (128 KB row stride) the
+// 64-row tiles are slower (1.35 vs 1.28 ms), so that layout keeps 128.  PNOL_SYRK_T64 = 0 / 1
+// forces either (read per call: tests switch it).
+static bool syrk_t64(bool sliced) {
+    const char* e = std::getenv("PNOL_SYRK_T64");
+    return e ? std::atoi(e) != 0 : sliced;
+}
+
 static bool syrk_xmap() {
     static const bool on = [] {
         const char* e = std::getenv("PNOL_SYRK_XMAP");
@@ -520,10 +545,15 @@ static bool syrk_xmap() {
 // part[((t - tile0) * nsl * sub + (s - slice0) * sub + u) * 128^2].
 static void syrk_partials(pnol_ctx* ctx, hipStream_t stream, bool rows_variant, const double* X, long ldx,
                           long sstride, int nr, int K, const SliceCfg& sc, int slice0, int nsl, int tile0, int ntl,
-                          double* part) {
+                          double* part, bool t64 = false) {
     const int split = nsl * sc.sub;
     const dim3 grid(ntl * split);
-    if (rows_variant)
+    if (t64) {   // all tiles (tile0 = 0): ntl counts the 64 x 64 lower tiles
+        const int nt64 = (nr + 63) / 64;
+        hipLaunchKernelGGL((k_syrk_tile<4, 64>), dim3(nt64 * (nt64 + 1) / 2 * split), dim3(256), 0, stream, X, ldx, nr,
+                           K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part,
+                           (double*)nullptr, 0L, 1.0, 0.0, 0);
+    } else if (rows_variant)
         hipLaunchKernelGGL((k_syrk_tile<2, kTile, false, 8>), grid, dim3(512), 0, stream, X, ldx, nr, K, split,
                            sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
     else if (syrk_nw() == 8)
@@ -552,7 +582,8 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * kS * sc.sub * kTile * kTile, &part));
     {
         ScopedTimer tm(ctx, "syrk");
-        syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part);
+        syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
+                      syrk_t64(false));
     }
     PNOL_CHECK(launch_check());
     ScopedTimer tm(ctx, "syrk_reduce");
@@ -748,9 +779,10 @@ int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lamb
     const int nsl = s1 - s0;
     void* part = nullptr;
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * std::max(nsl, 1) * sc.sub * E, &part));
+    const bool t64 = syrk_t64(true);
     if (nsl > 0) {
         ScopedTimer tm(ctx, "syrk");
-        syrk_partials(ctx, ctx->stream, false, JTs, sc.mS, sstr, n, m, sc, s0, nsl, 0, ntiles, (double*)part);
+        syrk_partials(ctx, ctx->stream, false, JTs, sc.mS, sstr, n, m, sc, s0, nsl, 0, ntiles, (double*)part, t64);
     }
     PNOL_CHECK(launch_check());
     if (P == 1) {

@@ -413,11 +413,14 @@ def test_fd_checkpoint_reuse_bitwise(ctx, oracle, m, n):
     assert np.array_equal(_np(JT), ref)
 
 
-@pytest.mark.parametrize("m,n", [(2000, 300), (5000, 1000), (777, 129), (16384, 2048)])
-def test_lm_sliced_jacobian_and_normal_bitwise(ctx, m, n):
+@pytest.mark.parametrize("m,n,t64", [(2000, 300, "0"), (5000, 1000, "0"), (777, 129, "0"), (16384, 2048, "0"),
+                                     (5000, 1000, "1"), (777, 129, "1"), (16384, 2048, "1")])
+def test_lm_sliced_jacobian_and_normal_bitwise(ctx, m, n, t64, monkeypatch):
     """One rank of the m-sliced LevMarqMPI path: pnol_lm_jacobian_mpi_d writes the same J values
     into the sliced layout, and pnol_lm_normal_mpi_d gives A, diag(J^T J) and -J^T F bitwise
-    equal to pnol_fd_jacobian_d + pnol_jtj_d + pnol_jtr_d (one summation tree on both paths)."""
+    equal to pnol_fd_jacobian_d + pnol_jtj_d + pnol_jtr_d (one summation tree on both paths).
+    t64 = "1": the 64 x 64-tile SYRK the ranks of an 8-GPU run use (same per-element sums)."""
+    monkeypatch.setenv("PNOL_SYRK_T64", t64)
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective, lm_sliced_layout
     d = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
