@@ -414,7 +414,8 @@ def test_fd_checkpoint_reuse_bitwise(ctx, oracle, m, n):
 
 
 @pytest.mark.parametrize("m,n,t64", [(2000, 300, "0"), (5000, 1000, "0"), (777, 129, "0"), (16384, 2048, "0"),
-                                     (5000, 1000, "1"), (777, 129, "1"), (16384, 2048, "1")])
+                                     (5000, 1000, "1"), (777, 129, "1"), (16384, 2048, "1"), (300, 100, "0"),
+                                     (300, 100, "1"), (4100, 65, "1")])
 def test_lm_sliced_jacobian_and_normal_bitwise(ctx, m, n, t64, monkeypatch):
     """One rank of the m-sliced LevMarqMPI path: pnol_lm_jacobian_mpi_d writes the same J values
     into the sliced layout, and pnol_lm_normal_mpi_d gives A, diag(J^T J) and -J^T F bitwise

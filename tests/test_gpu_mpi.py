@@ -68,11 +68,11 @@ def _check_levmarq_and_normal(tmp_path, world, m, n):
         assert np.array_equal(z["rs"], r1), r
 
 
-@pytest.mark.parametrize("world", [4, 5, 8])
-def test_levmarq_mpi_m_sliced_more_ranks(tmp_path, world):
-    """The m-sliced LevMarqMPI path at 4, 5 and 8 ranks (one slice per rank at 8; uneven
-    dyadic slice covers at 5), bitwise the single-GPU results."""
-    m, n = 1500, 200
+@pytest.mark.parametrize("world,m,n", [(4, 1500, 200), (5, 1500, 200), (8, 1500, 200), (8, 600, 130), (6, 700, 129)])
+def test_levmarq_mpi_m_sliced_more_ranks(tmp_path, world, m, n):
+    """The m-sliced LevMarqMPI path at 4 to 8 ranks (one slice per rank at 8; uneven dyadic
+    slice covers at 5 and 6; m = 600 leaves slices 5-7 empty, so three ranks own no rows; ranks
+    without FD tiles or without J^T J tiles), bitwise the single-GPU results."""
     _run_workers(tmp_path, world, m, n, "lm")
     _check_levmarq_and_normal(tmp_path, world, m, n)
 
