@@ -459,6 +459,45 @@ __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict
     }
 }
 
+// ---- the diagonal workgroup's two products, balanced over its 4 waves --------------------
+// L = A_{d,k} W_k^T with W_k lower triangular: wave w forms the 16-row strip w of L; output
+// block column jb needs only K blocks kb <= jb, so every wave issues 4 (1 + 2 + 3 + 4) = 40
+// MFMAs instead of the 64 of a 32 x 32 quadrant over the full K.  Each element's K steps run in
+// ascending order in one accumulator.
+__device__ __forceinline__ void diag_l_strip(d4 (&acc)[4], const double* __restrict__ X, const double* __restrict__ Y,
+                                             int w, int lane) {
+    const int frow = lane & 15, fk = lane >> 4;
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) acc[jb] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const double a = X[kb * kSub + (w * 16 + frow) * kPad + kk * 4 + fk];
+#pragma unroll
+            for (int jb = kb; jb < 4; ++jb) {
+                const double b = Y[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
+                acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[jb], 0, 0, 0);
+            }
+        }
+}
+
+// the strip into LDS in the substage layout (L as the operand of the second product)
+__device__ __forceinline__ void diag_strip_to_stage(const d4 (&acc)[4], double* __restrict__ X, int w, int lane) {
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) X[jb * kSub + (w * 16 + (lane >> 4) + 4 * r) * kPad + (lane & 15)] = acc[jb][r];
+}
+
+// A_dd - L L^T on the 10 lower 16 x 16 blocks (ib >= jb) only -- the factor never reads the
+// upper ones -- 3 / 3 / 2 / 2 blocks per wave (48 MFMAs on the busiest wave instead of 64)
+__device__ __forceinline__ int diag_blk(int w, int s) {   // (ib << 2) | jb, or -1
+    constexpr int tab[4][3] = {{(3 << 2) | 0, (3 << 2) | 1, 0}, {(3 << 2) | 2, (3 << 2) | 3, (1 << 2) | 0},
+                               {(2 << 2) | 0, (2 << 2) | 1, -1}, {(2 << 2) | 2, (1 << 2) | 1, -1}};
+    return tab[w][s];
+}
+
 // ---- one panel step ---------------------------------------------------------------------
 // Launch k (-1 <= k <= T-2), R = T-1-k.  blockIdx 0: the diagonal tile k+1; 1..R: panel rows
 // i = k+1 .. T-1; then the update tiles (i, j), k+1 <= j <= i, (i, j) != (k+1, k+1), by columns.
@@ -487,24 +526,44 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
             const int k0 = k * NB;
             stage_tile(X, P, ldp, d0, k0);
             stage_tile(Y, W + (long)k * NB * NB, NB, 0, 0);
-            d4 cdd[2][2];
-            acc_load(cdd, P, ldp, d0, d0, wr, wc, lane);   // in flight during the first product
+            d4 cdd[3];   // this wave's lower blocks of A_dd, in flight during the first product
+#pragma unroll
+            for (int sb = 0; sb < 3; ++sb) {
+                const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    cdd[sb][r] = bl < 0 ? 0.0
+                                        : P[(long)(d0 + ib * 16 + (lane >> 4) + 4 * r) * ldp + d0 + jb * 16 + (lane & 15)];
+            }
             __syncthreads();
-            d4 acc[2][2];
-            acc_zero(acc);
-            mfma_xyt<false>(acc, X, Y, wr, wc, lane);   // L_{d,k} = A_{d,k} W_k^T
+            d4 lst[4];
+            diag_l_strip(lst, X, Y, wave, lane);        // L_{d,k} = A_{d,k} W_k^T, strip `wave`
             __syncthreads();
-            acc_to_stage(acc, X, wr, wc, lane);
+            diag_strip_to_stage(lst, X, wave, lane);
             __syncthreads();
-            mfma_xyt<true>(cdd, X, X, wr, wc, lane);    // A_dd - L L^T
+            const int frow = lane & 15, fk = lane >> 4;
+#pragma unroll
+            for (int sb = 0; sb < 3; ++sb) {           // A_dd - L L^T, lower blocks
+                const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
+                if (bl < 0) continue;                   // wave-uniform
+#pragma unroll
+                for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) {
+                        const double a = -X[kb * kSub + (ib * 16 + frow) * kPad + kk * 4 + fk];
+                        const double b = X[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
+                        cdd[sb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, cdd[sb], 0, 0, 0);
+                    }
+            }
             __syncthreads();                            // X / Y are rewritten below
 #pragma unroll
-            for (int mi = 0; mi < 2; ++mi)
+            for (int sb = 0; sb < 3; ++sb) {
+                const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
+                if (bl < 0) continue;
 #pragma unroll
-                for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        diag_put(L, acc_row(wr, mi, lane, r), acc_col(wc, ni, lane), cdd[mi][ni][r]);
+                for (int r = 0; r < 4; ++r)
+                    diag_put(L, ib * 16 + (lane >> 4) + 4 * r, jb * 16 + (lane & 15), cdd[sb][r]);
+            }
         } else {
             const int row = t >> 2, c0 = (t & 3) * 16;
 #pragma unroll
