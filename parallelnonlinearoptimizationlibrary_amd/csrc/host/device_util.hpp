@@ -71,10 +71,13 @@ inline int even_ld(int n) { return (n + 1) & ~1; }
 
 // reference utility restatements used by the host-side control logic (sequential order,
 // identical to the CPU oracle's)
-inline double seq_dot(const std::vector<double>& a, const std::vector<double>& b) {
+inline double seq_dot(const double* a, const double* b, size_t n) {
     double s = 0.0;
-    for (size_t i = 0; i < a.size(); ++i) s = s + a[i] * b[i];
+    for (size_t i = 0; i < n; ++i) s = s + a[i] * b[i];
     return s;
+}
+inline double seq_dot(const std::vector<double>& a, const std::vector<double>& b) {
+    return seq_dot(a.data(), b.data(), a.size());
 }
 
 }  // namespace pnol

@@ -283,7 +283,7 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool s
         for (int c : ct) own_cols += c;
     }
     double lambda = P.lambda0;
-    std::vector<double> dX(n, P.dXGrad), F(m), Fnew(m), sigma(n);
+    std::vector<double> dX(n, P.dXGrad), F(m);
     dev.uploadH(dX);
     int s = 0;
     check(pnol_memcpy_h2d(ctx, dev.x(s), X.data(), sizeof(double) * n), "h2d");
@@ -302,10 +302,12 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool s
         if (dev.info_h(s) != 0) dev.redo_lu(s);
         obj->countEvals(own_cols + 1); // the trip's Jacobian
         obj->countEvals(1);            // its trial point
-        std::memcpy(sigma.data(), dev.sigma_h(s), sizeof(double) * n);
-        std::memcpy(Fnew.data(), dev.Fnext_h(s), sizeof(double) * m);
+        // chi^2 straight from the pinned copy (no host copy of F: the accepted F stays on the
+        // device and is downloaded once at the end)
+        const double* sig_h = dev.sigma_h(s);
+        const double* Fn = dev.Fnext_h(s);
         const double chiSqPrev = chiSq;
-        nrm = norm2(Fnew);
+        nrm = std::sqrt(seq_dot(Fn, Fn, (size_t)m));
         chiSq = nrm * nrm;
         if (chiSq >= chiSqPrev || chiSq != chiSq) {
             if (sharded ? (P.verbose >= 1 && loud) : (P.verbose > 1))
@@ -316,11 +318,10 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool s
             ckpt = false;              // x_[s], F_[s] stand; the trial point's eval took the checkpoints
         } else {
             lambda = lambda / P.lambdaFactor;
-            for (int i = 0; i < n; ++i) X[i] = X[i] + sigma[i];   // == x_[s^1] (same IEEE add)
-            F = Fnew;
+            for (int i = 0; i < n; ++i) X[i] = X[i] + sig_h[i];   // == x_[s^1] (same IEEE add)
             s ^= 1;
             ckpt = true;
-            xdiff2Norm = norm2(sigma);
+            xdiff2Norm = std::sqrt(seq_dot(sig_h, sig_h, (size_t)n));
             if (xdiff2Norm < P.xMinDiff) break;
         }
         if ((sharded ? (P.verbose >= 1 && loud) : (P.verbose > 0)) && iter % 10 == 0) {
@@ -330,7 +331,8 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool s
         }
         iter++;
     }
-    FOpt = F;
+    FOpt.resize(m);
+    check(pnol_memcpy_d2h(ctx, FOpt.data(), dev.F(s), sizeof(double) * m), "d2h");   // F(x_[s]) = F(X)
     if (P.verbose >= 0 && loud) {
         std::cout << std::endl << "-----------------------------------------------------------------------------------" << std::endl;
         std::cout << "Completed Levenberg Marquardt." << std::endl;
