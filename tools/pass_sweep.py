@@ -1,6 +1,6 @@
-"""Fused BFGS pass / H.g timing at n = 4096 and 8192 for the row-tile heights given as
-arguments (PNOL_PASS_ROWS, read once per process: one child per value), cold Infinity Cache.
-    python tools/pass_sweep.py 64 128 256"""
+"""Fused BFGS pass / H.g timing at n = 4096 and 8192, cold Infinity Cache, one child process per
+setting (the tuning variables are read once per process): arguments VAR=value, e.g.
+    python tools/pass_sweep.py PNOL_PASS_ROWS=128 PNOL_PASS_ROWS=256 PNOL_GEMV_ROWS=1"""
 import json
 import os
 import subprocess
@@ -17,12 +17,14 @@ print(json.dumps({n: bench.bench_hg(ctx, n) for n in (4096, 8192)}))
 """ % ROOT
 
 if __name__ == "__main__":
-    for v in sys.argv[1:] or ["128", "256"]:
-        p = subprocess.run([sys.executable, "-c", CHILD], env=dict(os.environ, PNOL_PASS_ROWS=v), capture_output=True,
+    for v in sys.argv[1:] or ["PNOL_PASS_ROWS=128", "PNOL_PASS_ROWS=256"]:
+        k, _, val = v.partition("=")
+        p = subprocess.run([sys.executable, "-c", CHILD], env=dict(os.environ, **{k: val}), capture_output=True,
                            text=True, timeout=300)
         if p.returncode != 0:
             print(p.stderr[-2000:])
             sys.exit(p.returncode)
         d = json.loads(p.stdout.strip().splitlines()[-1])
-        print(v, {n: (round(r["fused_pass_us"], 1), round(r["fused_pass_frac_of_hbm"], 3)) for n, r in d.items()},
-              flush=True)
+        print(v, {n: {"hg_us": round(r["hg_us"], 1), "hg_frac": round(r["hg_frac_of_hbm"], 3),
+                      "pass_us": round(r["fused_pass_us"], 1), "pass_frac": round(r["fused_pass_frac_of_hbm"], 3)}
+                  for n, r in d.items()}, flush=True)
