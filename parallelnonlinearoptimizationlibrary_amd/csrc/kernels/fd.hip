@@ -22,6 +22,7 @@
 #include "../pnol_comm.hpp"
 
 #include <algorithm>
+#include <memory>
 #include <cstdlib>
 #include <vector>
 
@@ -711,9 +712,10 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
         ctx->ckpt_x = x;
     }
     if (ckpt && kmajor) {
-        ScopedTimer tm(ctx, "fd_ckpt");
-        hipLaunchKernelGGL((k_linres_evalP<true>), dim3((o->m + kPanel - 1) / kPanel), dim3(64), 0, ctx->stream, (const double*)o->at,
-                           x, o->p1, o->m, o->n, f0_out, (double*)C);
+        LaunchTimer tm(ctx, "fd_ckpt");
+        hipExtLaunchKernelGGL((k_linres_evalP<true>), dim3((o->m + kPanel - 1) / kPanel), dim3(64), 0, ctx->stream,
+                              tm.start(), tm.stop(), 0, (const double*)o->at, x, (const double*)o->p1, o->m, o->n,
+                              f0_out, (double*)C);
     } else if (ckpt) {
         ScopedTimer tm(ctx, "fd_ckpt");
         if ((o->n % 2) == 0)
@@ -725,7 +727,12 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
     }
     if (ckpt) PNOL_CHECK(launch_check());
     const bool even = (o->n % 2) == 0;
-    ScopedTimer tm(ctx, "fd_jacobian");
+    // the row-panel kernels carry their timer events in the dispatch (LaunchTimer); the tuning
+    // variants keep a ScopedTimer
+    std::unique_ptr<LaunchTimer> lt;
+    std::unique_ptr<ScopedTimer> stm;
+    if (kmajor) lt.reset(new LaunchTimer(ctx, "fd_jacobian"));
+    else stm.reset(new ScopedTimer(ctx, "fd_jacobian"));
     const double* Cc = (const double*)C;
     // tiles in order of first column (longest chains first; outputs go by column)
     std::vector<int> ord(ntiles);
@@ -740,12 +747,19 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
             tl.count[t] = count[ord[t0 + t]];
         }
         const dim3 g1(((o->m + 127) / 128) * tl.ntiles), g2(((o->m + 63) / 64) * tl.ntiles);
-        if (fdk == 5) {
-            hipLaunchKernelGGL((k_linres_fdP<false>), g2, dim3(256), 0, ctx->stream, (const double*)o->at, o->p1, x, h,
-                               o->m, o->n, tl, F0, Cc, JT, (long)ldjt, mS, sstride);
-        } else if (fdk == 6 || sliced) {
-            hipLaunchKernelGGL((k_linres_fdP<true>), g2, dim3(256), 0, ctx->stream, (const double*)o->at, o->p1, x, h,
-                               o->m, o->n, tl, F0, Cc, JT, (long)ldjt, mS, sstride);
+        hipEvent_t ea = nullptr, eb = nullptr;
+        if (lt) {
+            ea = t0 == 0 ? lt->start() : nullptr;
+            eb = t0 + kFdMaxTiles >= ntiles ? lt->stop() : nullptr;
+        }
+        if (fdk == 5 && !sliced) {
+            hipExtLaunchKernelGGL((k_linres_fdP<false>), g2, dim3(256), 0, ctx->stream, ea, eb, 0, (const double*)o->at,
+                                  (const double*)o->p1, x, h, o->m, o->n, tl, (const double*)F0, Cc, JT, (long)ldjt,
+                                  mS, sstride);
+        } else if (fdk == 6 || kmajor) {
+            hipExtLaunchKernelGGL((k_linres_fdP<true>), g2, dim3(256), 0, ctx->stream, ea, eb, 0, (const double*)o->at,
+                                  (const double*)o->p1, x, h, o->m, o->n, tl, (const double*)F0, Cc, JT, (long)ldjt,
+                                  mS, sstride);
         } else if (fdk == 2) {
             if (even)
                 hipLaunchKernelGGL((k_linres_fd2<true, 8, 8>), g1, dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,

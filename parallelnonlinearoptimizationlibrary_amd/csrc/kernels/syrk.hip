@@ -548,22 +548,23 @@ static void syrk_partials(pnol_ctx* ctx, hipStream_t stream, bool rows_variant, 
                           double* part, bool t64 = false) {
     const int split = nsl * sc.sub;
     const dim3 grid(ntl * split);
+    LaunchTimer tm(ctx, rows_variant ? "syrk_rows" : "syrk");
     if (t64) {   // all tiles (tile0 = 0): ntl counts the 64 x 64 lower tiles
         const int nt64 = (nr + 63) / 64;
-        hipLaunchKernelGGL((k_syrk_tile<4, 64>), dim3(nt64 * (nt64 + 1) / 2 * split), dim3(256), 0, stream, X, ldx, nr,
+        hipExtLaunchKernelGGL((k_syrk_tile<4, 64>), dim3(nt64 * (nt64 + 1) / 2 * split), dim3(256), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr,
                            K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part,
                            (double*)nullptr, 0L, 1.0, 0.0, 0);
     } else if (rows_variant)
-        hipLaunchKernelGGL((k_syrk_tile<2, kTile, false, 8>), grid, dim3(512), 0, stream, X, ldx, nr, K, split,
+        hipExtLaunchKernelGGL((k_syrk_tile<2, kTile, false, 8>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr, K, split,
                            sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
     else if (syrk_nw() == 8)
-        hipLaunchKernelGGL((k_syrk_tile<0, kTile, false, 8>), grid, dim3(512), 0, stream, X, ldx, nr, K, split,
+        hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, false, 8>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr, K, split,
                            sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
     else if (syrk_xmap() && split % kNumXcd == 0)
-        hipLaunchKernelGGL((k_syrk_tile<0, kTile, true>), grid, dim3(256), 0, stream, X, ldx, nr, K, split, sc.kfirst,
+        hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, true>), grid, dim3(256), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr, K, split, sc.kfirst,
                            sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
     else
-        hipLaunchKernelGGL((k_syrk_tile<0, kTile>), grid, dim3(256), 0, stream, X, ldx, nr, K, split, sc.kfirst,
+        hipExtLaunchKernelGGL((k_syrk_tile<0, kTile>), grid, dim3(256), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr, K, split, sc.kfirst,
                            sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
 }
 
@@ -580,11 +581,8 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     const SliceCfg sc = slice_cfg(m, ntiles);
     void* part = nullptr;
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * kS * sc.sub * kTile * kTile, &part));
-    {
-        ScopedTimer tm(ctx, "syrk");
-        syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
-                      syrk_t64(false));
-    }
+    syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
+                  syrk_t64(false));
     PNOL_CHECK(launch_check());
     ScopedTimer tm(ctx, "syrk_reduce");
     launch_reduce(dim3(kTile / 32, ntiles), dim3(256), 0, ctx->stream, (const double*)part, ntiles,
@@ -603,10 +601,7 @@ int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldj
     void* part = nullptr;
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * per_tile, &part));
     double* mypart = (double*)part + (size_t)t0 * per_tile;   // disjoint per row range
-    {
-        ScopedTimer tm(ctx, "syrk_rows", stream);
-        syrk_partials(ctx, stream, true, JT, ldjt, sc.mS, n, m, sc, 0, kS, t0, t1 - t0, mypart);
-    }
+    syrk_partials(ctx, stream, true, JT, ldjt, sc.mS, n, m, sc, 0, kS, t0, t1 - t0, mypart);
     PNOL_CHECK(launch_check());
     launch_reduce(dim3(kTile / 32, t1 - t0), dim3(256), 0, stream, (const double*)mypart, t1 - t0,
                        sc.sub, n, lambda, A, (long)lda, jtj_diag, t0);
@@ -627,8 +622,7 @@ int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h,
     const int nt = (n + kTile - 1) / kTile;
     if (o->kind != PNOL_OBJ_LINRES || nchunks <= 1 || nt < 2 || (n <= PNOL_SEQ_MAX && m <= 4096)) {
         PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
-        ScopedTimer tm(ctx, "syrk");
-        return launch_jtj(ctx, JT, ldjt, m, n, lambda, A, lda, jtj_diag);
+        return launch_jtj(ctx, JT, ldjt, m, n, lambda, A, lda, jtj_diag);   // times "syrk" itself
     }
     nchunks = std::min(nchunks, nt);
     if (!ctx->aux_stream) PNOL_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
@@ -706,10 +700,7 @@ int launch_jtj_sharded(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, 
     PNOL_CHECK(ws_get(ctx, "syrk_packed", sizeof(double) * (size_t)P * tpr * E, &packed));
     double* mine = (double*)packed + (size_t)rank * tpr * E;
     if (cnt > 0) {
-        {
-            ScopedTimer tm(ctx, "syrk");
-            syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, t0, cnt, (double*)part);
-        }
+        syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, t0, cnt, (double*)part);
         PNOL_CHECK(launch_check());
         hipLaunchKernelGGL(k_syrk_reduce_packed, dim3(8, cnt), dim3(256), 0, ctx->stream, (const double*)part, sc.sub,
                            mine);
@@ -780,10 +771,8 @@ int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lamb
     void* part = nullptr;
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * std::max(nsl, 1) * sc.sub * E, &part));
     const bool t64 = syrk_t64(true);
-    if (nsl > 0) {
-        ScopedTimer tm(ctx, "syrk");
+    if (nsl > 0)
         syrk_partials(ctx, ctx->stream, false, JTs, sc.mS, sstr, n, m, sc, s0, nsl, 0, ntiles, (double*)part, t64);
-    }
     PNOL_CHECK(launch_check());
     if (P == 1) {
         {

@@ -2,6 +2,7 @@
 // C++ drop-in classes.  Not installed; the public surface is include/pnol_amd.h.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -100,6 +101,22 @@ class ScopedTimer {
     pnol_ctx* ctx_;
     const char* name_;
     hipStream_t stream_ = nullptr;
+    hipEvent_t a_ = nullptr, b_ = nullptr;
+};
+
+// Timer events carried by the kernel dispatch itself (hipExtLaunchKernel start / stop events):
+// no extra packets between launches, unlike ScopedTimer's two event records (~5-7 us of
+// dispatch gap each).  start() / stop() are nullptr when the timer is off; a sequence of
+// launches passes start() to the first and stop() to the last.
+class LaunchTimer {
+  public:
+    LaunchTimer(pnol_ctx* ctx, const char* name);
+    ~LaunchTimer();
+    hipEvent_t start() const { return a_; }
+    hipEvent_t stop() const { return b_; }
+  private:
+    pnol_ctx* ctx_;
+    const char* name_;
     hipEvent_t a_ = nullptr, b_ = nullptr;
 };
 

@@ -290,6 +290,25 @@ ScopedTimer::ScopedTimer(pnol_ctx* ctx, const char* name, hipStream_t stream)
     (void)hipEventRecord(a_, stream_);
 }
 
+LaunchTimer::LaunchTimer(pnol_ctx* ctx, const char* name) : ctx_(ctx), name_(name) {
+    if (!ctx_ || !ctx_->timers.on) return;
+    if (ctx_->timers.on == 2 && !hot_timer(name)) return;
+    auto& pool = ctx_->timers.free_events;
+    for (hipEvent_t* e : {&a_, &b_}) {
+        if (!pool.empty()) {
+            *e = pool.back();
+            pool.pop_back();
+        } else if (hipEventCreate(e) != hipSuccess) {
+            a_ = b_ = nullptr;
+            return;
+        }
+    }
+}
+
+LaunchTimer::~LaunchTimer() {
+    if (a_) ctx_->timers.pending[name_].push_back({a_, b_});
+}
+
 ScopedTimer::~ScopedTimer() {
     if (!a_) return;
     (void)hipEventRecord(b_, stream_);
