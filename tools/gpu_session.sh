@@ -4,7 +4,6 @@
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-STEPS="${STEPS:-10}"
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }   # 1 = test/assert failures, not a fault
 
 if [ "${MB:-0}" = "1" ]; then
@@ -17,7 +16,7 @@ ok $rc || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log
 ok $rc || exit $rc
-timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err
+timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?; echo "bench rc=$rc"; tail -c 3000 gpurun_out/bench.json
 ok $rc || exit $rc
 if [ "${PROFILE:-1}" = "1" ]; then
