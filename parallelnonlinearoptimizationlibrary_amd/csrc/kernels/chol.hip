@@ -214,11 +214,28 @@ struct ColBuf {
 // (readlane, rsqrt) beside the tail of step J-1's rank-1 update (k >= J + 2, with the previous
 // column lp / cp still in registers), and only the entry k = J + 2 of its own update, which
 // the next pivot needs.  Each entry still receives its updates in column order.
-template <int J, int LDC, bool STAMP = false>
+// SPLIT > 0 (the first panel): the updates of entries k >= SPLIT + 2 by columns < SPLIT are
+// the helper wave's (panel_helper); wave 0 takes those entries over from LDS at step SPLIT,
+// after its pivot chain.  Every entry still receives the same fmas in column order.
+// kHelpCols: the columns whose updates of entries >= kHelpK the helpers apply; wave 0 takes
+// the entries over at step kHandoff.  Measured
+// (tools/microbench/diag_timing.hip): the first panel 10.5k -> 9.3k cycles with 16 columns and
+// two helper waves (12 or 14 columns: no better -- the helpers trail wave 0 by ~800 cycles of
+// LDS signal and read latency at the hand-off either way).
+#ifndef PNOL_CHOL_HELP_COLS
+#define PNOL_CHOL_HELP_COLS 16
+#endif
+constexpr int kSplit = 16, kHelpK = kSplit + 2, kHelpCols = PNOL_CHOL_HELP_COLS;
+// the hand-off step: before column kHelpCols's tail reaches the helpers' entries, and before
+// step kHelpK - 2's immediate update of entry kHelpK
+constexpr int kHandoff = kHelpCols + 1 < kHelpK - 2 ? kHelpCols + 1 : kHelpK - 2;
+static_assert(kHelpCols <= kSplit, "helpers apply at most the first kSplit columns");
+
+template <int J, int LDC, bool STAMP = false, int SPLIT = 0>
 __device__ __forceinline__ void panel_step(double (&a)[kHalf], double& piv, double& r, double lp,
                                            const ColBuf<J - 1>& cp, double* __restrict__ Lc,
                                            double* __restrict__ rinv, int* cnt, int cbase, int t, bool& bad,
-                                           long long* st = nullptr) {
+                                           long long* st = nullptr, const double* hs = nullptr) {
     if constexpr (STAMP && (J & 7) == 0) st[J >> 3] = __builtin_amdgcn_s_memtime();   // microbenchmark only
     // lane J: a[J] * r = piv / sqrt(piv), the diagonal; lanes t < J scale upper-triangle
     // entries nobody reads (column J above the diagonal is never consumed)
@@ -232,13 +249,21 @@ __device__ __forceinline__ void panel_step(double (&a)[kHalf], double& piv, doub
         bad |= !(piv > 0.0);
         r = rsqrt_nr(piv);
     }
+    if constexpr (SPLIT > 0 && J == kHandoff) {
+        // take over entries k >= SPLIT + 2, updated by the helper wave with columns 0 .. SPLIT-1
+        wait_lds_ge(cnt + 4, 1);
+        wait_lds_ge(cnt + 5, 1);
+#pragma unroll
+        for (int k = SPLIT + 2; k < kHalf; ++k) a[k] = hs[t * (kHalf - SPLIT - 2) + k - SPLIT - 2];
+    }
     // beside it: the tail of step J-1's update (k >= J + 2) ...
     if constexpr (J >= 1) {
+        constexpr int KLIM = (SPLIT > 0 && J - 1 < kHelpCols) ? kHelpK : kHalf;   // helpers' entries excluded
 #pragma unroll
         for (int q = 0; q < ColBuf<J - 1>::NR; ++q) {
             const int k = ColBuf<J - 1>::K0 + 2 * q;
-            if (k >= J + 2) a[k] = fma(-lp, cp.v[q].x, a[k]);
-            if (k + 1 >= J + 2) a[k + 1] = fma(-lp, cp.v[q].y, a[k + 1]);
+            if (k >= J + 2 && k < KLIM) a[k] = fma(-lp, cp.v[q].x, a[k]);
+            if (k + 1 >= J + 2 && k + 1 < KLIM) a[k + 1] = fma(-lp, cp.v[q].y, a[k + 1]);
         }
     }
     // ... and the one entry of step J's update the next step's chain needs (l_{J+2,J} by readlane)
@@ -255,7 +280,44 @@ __device__ __forceinline__ void panel_step(double (&a)[kHalf], double& piv, doub
     }
     asm volatile("" ::: "memory");   // keep the next steps' LDS reads from being hoisted here
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (J + 1 < kHalf) panel_step<J + 1, LDC, STAMP>(a, piv, r, l, cv, Lc, rinv, cnt, cbase, t, bad, st);
+    if constexpr (J + 1 < kHalf)
+        panel_step<J + 1, LDC, STAMP, SPLIT>(a, piv, r, l, cv, Lc, rinv, cnt, cbase, t, bad, st, hs);
+}
+
+// The helper waves of the first panel: entries k in [K0, K1) (K0 >= kHelpK) of every row take
+// the updates of columns 0 .. kSplit-1 here (the same fma(-l_row, l_k, entry) in column
+// order), then go to LDS for wave 0 (its flag).  Columns are read in pairs once wave 0 has signalled them.
+template <int LDC, int K0, int K1>
+__device__ __forceinline__ void panel_helper(const double* __restrict__ Sl, const double* __restrict__ Lc, int* cnt,
+                                             double* __restrict__ hs, int* flag, int lane) {
+    constexpr int NB_ = K1 - K0, NH = kHalf - kHelpK;
+    static_assert(NB_ % 2 == 0 && K0 % 2 == 0, "pairs of entries");
+    double b[NB_];
+#pragma unroll
+    for (int i = 0; i < NB_; ++i) b[i] = Sl[lane * kS + K0 + i];
+#pragma unroll 1
+    for (int c = 0; c < kHelpCols; c += 2) {   // two columns per signal, all their reads in flight at once
+        wait_lds_ge(cnt, c + 2);
+        const double lt0 = Lc[c * LDC + lane], lt1 = Lc[(c + 1) * LDC + lane];
+        double2 k0[NB_ / 2], k1[NB_ / 2];
+#pragma unroll
+        for (int i = 0; i < NB_ / 2; ++i) {
+            k0[i] = *reinterpret_cast<const double2*>(Lc + c * LDC + K0 + 2 * i);
+            k1[i] = *reinterpret_cast<const double2*>(Lc + (c + 1) * LDC + K0 + 2 * i);
+        }
+#pragma unroll
+        for (int i = 0; i < NB_ / 2; ++i) {
+            b[2 * i] = fma(-lt0, k0[i].x, b[2 * i]);
+            b[2 * i + 1] = fma(-lt0, k0[i].y, b[2 * i + 1]);
+            b[2 * i] = fma(-lt1, k1[i].x, b[2 * i]);
+            b[2 * i + 1] = fma(-lt1, k1[i].y, b[2 * i + 1]);
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int i = 0; i < NB_; ++i) hs[lane * NH + K0 - kHelpK + i] = b[i];
+    lds_signal(flag, 1);   // in order after the data writes (one wave's LDS ops are ordered)
 }
 
 // One step of the inverse of a 32 x 32 lower factor (wave 1, lane c = column c of W):
@@ -364,7 +426,8 @@ __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict
     const int t = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
     // The phases are chained by LDS words instead of workgroup barriers, so the inverse wave
     // finishing W11 overlaps the S22 update:  cnt[0] = final panel columns, cnt[1] = W11 done,
-    // cnt[2] / cnt[3] = S22 quadrants (1,0) / (1,1) done.  All are zero on entry.
+    // cnt[2] / cnt[3] = S22 quadrants (1,0) / (1,1) done, cnt[4] / cnt[5] = the helpers' entries
+    // are in LDS.  All are zero on entry.
     int* flags = cnt + 1;
     const double* L21 = L.Lc1 + kHalf;
     if (wave == 0) {
@@ -376,7 +439,7 @@ __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict
             bool bad = !(piv > 0.0);
             double r = rsqrt_nr(piv);
             const ColBuf<-1> none{};
-            panel_step<0, 64, STAMP>(a, piv, r, 0.0, none, L.Lc1, rinv, cnt, 0, lane, bad, st);
+            panel_step<0, 64, STAMP, kSplit>(a, piv, r, 0.0, none, L.Lc1, rinv, cnt, 0, lane, bad, st, L.Lc2);
             if constexpr (STAMP) st[4] = __builtin_amdgcn_s_memtime();
             if (bad && lane == 0) atomicCAS(info, 0, d * NB + 1);
         }
@@ -413,6 +476,9 @@ __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict
         if constexpr (STAMP) st[14] = __builtin_amdgcn_s_memtime();
     } else {
         const int qi = 1, qj = wave - 2;   // P2 quadrants (1,0) and (1,1)
+        // the first panel's helpers (entries 18..23 / 24..31); Lc2 is free until P3
+        if (wave == 2) panel_helper<64, kHelpK, 24>(L.Sl, L.Lc1, cnt, L.Lc2, cnt + 4, lane);
+        else panel_helper<64, 24, kHalf>(L.Sl, L.Lc1, cnt, L.Lc2, cnt + 5, lane);
         wait_lds_ge(cnt, kHalf);
         d4 acc;
 #pragma unroll
@@ -509,7 +575,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
     __shared__ __attribute__((aligned(16))) double smem[2 * kStage];   // 73.7 KB
     __shared__ double rinv[NB];
     __shared__ double zsh[NB];
-    __shared__ int cnt[4];   // diagonal-tile phase words (factor_diag)
+    __shared__ int cnt[6];   // diagonal-tile phase words (factor_diag)
     __shared__ int ok_sh;
     const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), wr = wave >> 1, wc = wave & 1;
     if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
@@ -521,7 +587,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
     if (b == 0) {   // ---------------- diagonal tile d = k + 1
         const int d = k + 1, d0 = d * NB;
         const DiagLds L = diag_lds(smem);
-        if (t < 4) cnt[t] = 0;
+        if (t < 6) cnt[t] = 0;
         if (k >= 0) {
             const int k0 = k * NB;
             stage_tile(X, P, ldp, d0, k0);
