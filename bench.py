@@ -297,6 +297,9 @@ def main():
     timers = {k: _timer(L, dctx, k) for k in names}
     # per-step kernel times, max over ranks (the slowest rank sets the pace)
     per_local = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timers.items()}
+    # the checkpoint pass runs only on the trips after a rejected step (an accepted step's
+    # trial-point evaluation already made them): its cost per trip, not per call
+    per_local["fd_ckpt_per_step"] = timers["fd_ckpt"][0] / max(args.steps, 1)
     if world > 1:
         keys = sorted(per_local)
         tv = torch.tensor([per_local[k] for k in keys], dtype=torch.float64, device=_red_dev())
@@ -344,7 +347,7 @@ def main():
                             "flop_nominal_full_chains": fd_flop_nominal,
                             "valu_busy_pmc": next((v.get("valu_busy_frac") for k, v in pmc_valu().items()
                                                    if "k_linres_fdP" in k), None),
-                            "ckpt_ms": per["fd_ckpt"]},
+                            "ckpt_ms_per_call": per["fd_ckpt"], "ckpt_ms_per_step": per["fd_ckpt_per_step"]},
             "jtj": dict(roofline, ms=syrk_ms),
         }
         if hg:
@@ -379,7 +382,7 @@ def main():
             "kernel_ms_per_step_max_over_ranks": per_max,
             # the north star's strong-scaling quantity: the sharded FD Jacobian + its exchange
             # (m-slice point-to-point exchange; the column-row allgather with PNOL_LM_SLICED=0)
-            "fd_jacobian_ms_max_over_ranks": per_max["fd_jacobian"] + per_max["fd_ckpt"] + (
+            "fd_jacobian_ms_max_over_ranks": per_max["fd_jacobian"] + per_max["fd_ckpt_per_step"] + (
                 per_max["exchange_J"] if per_max["exchange_J"] > 0 else per_max["allgather"]),
             "converged_rel_err_vs_xstar": err,
             "bfgs_hg": hg, "bfgs_hg_n4096": hg4096 if hg else None, "bfgs_hg_row_sharded": hg_sharded,
