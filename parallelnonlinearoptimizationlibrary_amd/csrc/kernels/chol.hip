@@ -739,6 +739,9 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm,
         for (int r = 0; r < 16; ++r) dst[r] = Lm[(long)(c * NB + q * 16 + r) * ldp + w0 + j];
     };
     if (w + 1 < T) load_blk(Lv, T - 1);
+    double wr[16];   // W_w's column j, rows q*16 .. +16: requested before the chain, not after it
+#pragma unroll
+    for (int r = 0; r < 16; ++r) wr[r] = Ww[(q * 16 + r) * NB + j];
     for (int c = T - 1; c > w; --c) {
         if (c - 1 > w) load_blk(Ln, c - 1);
         if (t == 0) ok_sh = spin_ge(flags + c, epoch, info);
@@ -761,7 +764,7 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm,
     __syncthreads();
     double s = 0.0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s = fma(Ww[(q * 16 + r) * NB + j], vsh[q * 16 + r], s);
+    for (int r = 0; r < 16; ++r) s = fma(wr[r], vsh[q * 16 + r], s);
     part[q][j] = s;
     __syncthreads();
     if (t < NB) {   // wave 0 alone stores x_w
