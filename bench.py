@@ -5,7 +5,10 @@ at N>1, one process per GPU, FD columns sharded with an RCCL allgather): the bat
 finite-difference Jacobian of the synthetic dense residual r(x) = A x - y (SURVEY 8(d)
 cfg 3/4, splitmix64 seed 0x5EED2018, data generated in HBM), J^T J on fp64 MFMA with the
 Marquardt diagonal, -J^T F, the damped Cholesky solve, F(x + sigma) and the accept/reject
-test.  Every trip does the full work (no Jacobian reuse across rejected steps).
+test.  Every trip recomputes the whole Jacobian (all n perturbed evaluations), J^T J, -J^T F
+and the solve, also after a rejected step, as the reference does.  F(x) and its prefix
+checkpoints depend on x alone and are kept from the evaluation that made them (the trial
+point's, or the trip before a rejection); the evaluation counter still counts F(x) per trip.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -297,8 +300,8 @@ def main():
     timers = {k: _timer(L, dctx, k) for k in names}
     # per-step kernel times, max over ranks (the slowest rank sets the pace)
     per_local = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timers.items()}
-    # the checkpoint pass runs only on the trips after a rejected step (an accepted step's
-    # trial-point evaluation already made them): its cost per trip, not per call
+    # the checkpoint pass runs only when no slot holds x's checkpoints (the first trip; the
+    # trial-point evaluation and the two slots cover accepted and rejected steps): per trip
     per_local["fd_ckpt_per_step"] = timers["fd_ckpt"][0] / max(args.steps, 1)
     if world > 1:
         keys = sorted(per_local)

@@ -315,7 +315,8 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool s
                           << ",  increasing lambda: " << lambda << " --> " << lambda * P.lambdaFactor << std::endl;
             chiSq = chiSqPrev;
             lambda = lambda * P.lambdaFactor;
-            ckpt = false;              // x_[s], F_[s] stand; the trial point's eval took the checkpoints
+            ckpt = true;               // x_[s], F_[s] stand, and so do x_[s]'s checkpoints (the
+                                       // trial point's went to the other slot)
         } else {
             lambda = lambda / P.lambdaFactor;
             for (int i = 0; i < n; ++i) X[i] = X[i] + sig_h[i];   // == x_[s^1] (same IEEE add)

@@ -615,6 +615,30 @@ static int ensure_panels(pnol_ctx* ctx, pnol_dobj* o) {
     return launch_check();
 }
 
+// The two checkpoint slots.  An LM trip holds the checkpoints of its Jacobian point x_s and
+// writes those of the trial point x_t: with two slots a rejected step (x_s stands) finds x_s's
+// still in place and skips the base-chain pass.
+static int ckpt_find(pnol_ctx* ctx, const pnol_dobj* o, const double* x) {
+    for (int s = 0; s < 2; ++s)
+        if (o && ctx->ckpt_obj[s] == o && ctx->ckpt_x[s] == x) return s;
+    return -1;
+}
+static int ckpt_buf(pnol_ctx* ctx, const pnol_dobj* o, int slot, void** C) {
+    const int ncp = (o->n + kCkpt - 1) / kCkpt;
+    ctx->ckpt_use[slot] = ++ctx->ckpt_clock;
+    return ws_get(ctx, slot ? "linres_ckpt1" : "linres_ckpt0", sizeof(double) * (size_t)o->m * (ncp > 1 ? ncp : 1), C);
+}
+// the slot the checkpoints of (o, x) are written to: its own if tagged, else the least recent;
+// tagged (o, x) (obj nullptr: written but never reused)
+static int ckpt_claim(pnol_ctx* ctx, const pnol_dobj* o, const double* x, bool reusable, void** C) {
+    int s = ckpt_find(ctx, o, x);
+    if (s < 0) s = ctx->ckpt_use[0] <= ctx->ckpt_use[1] ? 0 : 1;
+    ctx->ckpt_obj[s] = reusable ? o : nullptr;
+    ctx->ckpt_x[s] = x;
+    ctx->ckpt_last = s;
+    return ckpt_buf(ctx, o, s, C);
+}
+
 // F = F(x), and for a linear residual also the prefix checkpoints of x, kept in the context
 // for the next FD call on (o, x) with compute_f0 == 2 (the LM trial point becomes the next
 // Jacobian point when the step is accepted).
@@ -623,15 +647,12 @@ int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* 
     if (o->kind != PNOL_OBJ_LINRES) return launch_dobj_eval(ctx, o, x, out);
     PNOL_CHECK(ensure_panels(ctx, o));
     void* C = nullptr;
-    const int ncp = (o->n + kCkpt - 1) / kCkpt;
-    PNOL_CHECK(ws_get(ctx, "linres_ckpt", sizeof(double) * (size_t)o->m * (ncp > 1 ? ncp : 1), &C));
+    PNOL_CHECK(ckpt_claim(ctx, o, x, true, &C));
     {
         ScopedTimer tm(ctx, "linres_eval");
         hipLaunchKernelGGL((k_linres_evalP<true>), dim3((o->m + kPanel - 1) / kPanel), dim3(64), 0, ctx->stream,
                            (const double*)o->at, x, o->p1, o->m, o->n, out, (double*)C);
     }
-    ctx->ckpt_obj = o;
-    ctx->ckpt_x = x;
     return launch_check();
 }
 
@@ -703,13 +724,16 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
     // compute_f0 == 2 and the context's checkpoints are those of (o, x) from
     // launch_dobj_eval_ckpt (F0 then already holds F(x))
     void* C = nullptr;
-    const int ncp = (o->n + kCkpt - 1) / kCkpt;
-    PNOL_CHECK(ws_get(ctx, "linres_ckpt", sizeof(double) * (size_t)o->m * (ncp > 1 ? ncp : 1), &C));
     double* f0_out = compute_f0 == 1 ? F0 : nullptr;
-    if (compute_f0 == 2 && kmajor && ctx->ckpt_obj == o && ctx->ckpt_x == x) ckpt = 0;
-    if (ckpt) {
-        ctx->ckpt_obj = kmajor ? o : nullptr;
-        ctx->ckpt_x = x;
+    const int have = (compute_f0 == 2 && kmajor) ? ckpt_find(ctx, o, x) : -1;
+    if (have >= 0) {
+        ckpt = 0;
+        ctx->ckpt_last = have;
+        PNOL_CHECK(ckpt_buf(ctx, o, have, &C));
+    } else if (ckpt) {
+        PNOL_CHECK(ckpt_claim(ctx, o, x, kmajor, &C));
+    } else {   // the caller's previous call on (o, x) wrote them (chunked FD: chunks after the first)
+        PNOL_CHECK(ckpt_buf(ctx, o, ctx->ckpt_last, &C));
     }
     if (ckpt && kmajor) {
         LaunchTimer tm(ctx, "fd_ckpt");

@@ -44,8 +44,13 @@ struct pnol_ctx {
     pnol::Workspace ws;
     void* pinned = nullptr;         // pinned host staging for pnol_memcpy_* (grown on demand)
     size_t pinned_bytes = 0;
-    const pnol_dobj* ckpt_obj = nullptr;   // the objective whose prefix checkpoints are in "linres_ckpt"
-    const double* ckpt_x = nullptr;        // ... and the device x they were computed at
+    // two slots of linear-residual prefix checkpoints ("linres_ckpt0/1"), each tagged with the
+    // objective and the device x it was computed at; use = last-use stamp (least recent is reused)
+    const pnol_dobj* ckpt_obj[2] = {nullptr, nullptr};
+    const double* ckpt_x[2] = {nullptr, nullptr};
+    unsigned long ckpt_use[2] = {0, 0};
+    unsigned long ckpt_clock = 0;
+    int ckpt_last = 0;   // the slot written last
     int* solve_flags = nullptr;     // per-block ready flags of the triangular solves (workspace)
     int solve_epoch = 0;            // value the flags of the current solve are set to
     void* chol_tasks = nullptr;     // uploaded tile-DAG task table (workspace) and its tile count
