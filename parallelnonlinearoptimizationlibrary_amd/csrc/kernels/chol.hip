@@ -568,17 +568,35 @@ __device__ __forceinline__ int diag_blk(int w, int s) {   // (ib << 2) | jb, or 
 // Launch k (-1 <= k <= T-2), R = T-1-k.  blockIdx 0: the diagonal tile k+1; 1..R: panel rows
 // i = k+1 .. T-1; then the update tiles (i, j), k+1 <= j <= i, (i, j) != (k+1, k+1), by columns.
 // Waits only ever target lower blockIdx (the panel workgroups), and every wait is capped.
+// Launch -1 is also the prep: block 0 resets info and factors tile 0 straight from A while
+// blocks 1.. copy A into the padded P (identity on the padded diagonal) and rhs into bv.
 __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, double* __restrict__ Lm, long ldp,
                                                    int T, int k, double* __restrict__ W, double* __restrict__ bv,
                                                    double* __restrict__ zv, int* __restrict__ rowflag, int epoch,
-                                                   int* __restrict__ info) {
+                                                   int* __restrict__ info, const double* __restrict__ A, long lda,
+                                                   int n, const double* __restrict__ rhs) {
     __shared__ __attribute__((aligned(16))) double smem[2 * kStage];   // 73.7 KB
     __shared__ double rinv[NB];
     __shared__ double zsh[NB];
     __shared__ int cnt[6];   // diagonal-tile phase words (factor_diag)
     __shared__ int ok_sh;
     const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), wr = wave >> 1, wc = wave & 1;
-    if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+    if (k < 0 && blockIdx.x > 0) {   // prep: rows b-1, b-1+G, ... of P
+        const int N = T * NB, G = gridDim.x - 1;
+        for (int r = blockIdx.x - 1; r < N; r += G) {
+            double* pr = P + (long)r * ldp;
+            const double* ar = A + (long)r * lda;
+            for (int c = t; c < N; c += 256) pr[c] = (r < n && c < n) ? ar[c] : (r == c ? 1.0 : 0.0);
+        }
+        if (blockIdx.x == 1)
+            for (int r = t; r < N; r += 256) bv[r] = r < n ? rhs[r] : 0.0;
+        return;
+    }
+    if (k < 0) {
+        if (t == 0) __hip_atomic_store(info, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+        return;
+    }
     double* X = smem;
     double* Y = smem + kStage;
     const int R = T - 1 - k;
@@ -633,7 +651,10 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
         } else {
             const int row = t >> 2, c0 = (t & 3) * 16;
 #pragma unroll
-            for (int q = 0; q < 16; ++q) diag_put(L, row, c0 + q, P[(long)row * ldp + c0 + q]);
+            for (int q = 0; q < 16; ++q) {
+                const int c = c0 + q;
+                diag_put(L, row, c, (row < n && c < n) ? A[(long)row * lda + c] : (row == c ? 1.0 : 0.0));
+            }
         }
         __syncthreads();
         factor_diag(L, rinv, cnt, W + (long)d * NB * NB, d, info);
@@ -776,20 +797,6 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm,
     }
 }
 
-// P = A zero-padded to N x N (identity on the padded diagonal), bv = rhs zero-padded, info = 0
-__global__ void k_chol_prep(const double* __restrict__ A, long lda, int n, double* __restrict__ P, long ldp, int N,
-                            const double* __restrict__ rhs, double* __restrict__ bv, int* __restrict__ info) {
-    const long total = (long)N * N;
-    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-        const int r = (int)(e / N), c = (int)(e % N);
-        P[(long)r * ldp + c] = (r < n && c < n) ? A[(long)r * lda + c] : (r == c ? 1.0 : 0.0);
-    }
-    if (blockIdx.x == 0) {
-        for (int r = threadIdx.x; r < N; r += blockDim.x) bv[r] = r < n ? rhs[r] : 0.0;
-        if (threadIdx.x == 0) *info = 0;
-    }
-}
-
 }  // namespace
 
 // Solve A sigma = rhs (A SPD, untouched) by the lookahead tile Cholesky; *dinfo (device) != 0
@@ -815,16 +822,13 @@ int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs
     }
     int* rowflag = ctx->chol4_flags;
     int* bwdflag = ctx->chol4_flags + ctx->chol4_cap;
-    const long total = (long)N * N;
-    hipLaunchKernelGGL(k_chol_prep, dim3((int)std::min<long>((total + 255) / 256, 4096)), dim3(256), 0, ctx->stream,
-                       A, (long)lda, n, (double*)P, ldp, N, rhs, (double*)bv, dinfo);
     for (int k = -1; k <= T - 2; ++k) {
         const int R = T - 1 - k;
-        const int grid = k < 0 ? 1 : R + R * (R + 1) / 2;
+        const int grid = k < 0 ? 1 + std::min(N, 1024) : R + R * (R + 1) / 2;
         const int epoch = ++ctx->chol4_epoch;
         hipLaunchKernelGGL(k_chol_step, dim3(grid), dim3(256), 0, ctx->stream, (double*)P, (double*)Lm, ldp, T, k,
                            (double*)W,
-                           (double*)bv, (double*)zv, rowflag, epoch, dinfo);
+                           (double*)bv, (double*)zv, rowflag, epoch, dinfo, A, (long)lda, n, rhs);
     }
     const int epoch = ++ctx->chol4_epoch;
     hipLaunchKernelGGL(k_chol_bwd, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n, (const double*)W,
