@@ -376,7 +376,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (splitmix64 seed 0x5EED2018, r(x)=Ax-y generated in HBM)",
             "config": {"workload": f"LevenbergMarquardt{'MPI' if world > 1 else ''} m={m} n={n}, "
-                                   f"FD columns {'in cost-balanced tiles over ' + str(world) + ' GPUs, J rows exchanged by m-slice (RCCL p2p), J^T J + J^T F by m-slice + reduce-scatter/allgather' if world > 1 else 'on 1 GPU'}",
+                                   f"FD columns {'in cost-balanced tiles over ' + str(world) + ' GPUs, J rows exchanged by m-slice (' + ('host communicator over gloo: one-GPU rehearsal' if args.host_comm else 'RCCL p2p') + '), J^T J + J^T F by m-slice + reduce-scatter/allgather' if world > 1 else 'on 1 GPU'}",
                        "m": m, "n": n, "parallelism": f"fd-columns+m-slices x{world}" if world > 1 else "single"},
             "roofline": roofline,
             "rooflines": rooflines,

@@ -51,4 +51,10 @@ if [ "${MFMA:-0}" = "1" ]; then
       --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_mfma.log 2>&1
   rc=$?; echo "pmc mfma rc=$rc"; [ "$rc" -eq 0 ] || exit $rc
 fi
+if [ "${HOSTCOMM:-0}" = "1" ]; then   # the N>1 bench path rehearsed on one GPU (gloo + host communicator)
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+      --master-port 29517 bench.py --gpus 2 --host-comm --steps 5 --warmup 2 --no-cpu-baseline \
+      > gpurun_out/bench_hostcomm2.json 2> gpurun_out/bench_hostcomm2.err
+  rc=$?; echo "hostcomm rc=$rc"; tail -c 600 gpurun_out/bench_hostcomm2.json; [ "$rc" -eq 0 ] || exit $rc
+fi
 exit 0

@@ -24,7 +24,7 @@ def load(dirname, counter):
             if row.get("Counter_Name") != counter:
                 continue
             name = row.get("Kernel_Name", "?")
-            per[name].append(float(row["Counter_Value"]))
+            per[(name, int(row.get("Grid_Size") or 0))].append(float(row["Counter_Value"]))
     return per
 
 
@@ -42,28 +42,31 @@ def short(name):
 def main():
     fdir, wdir, out = sys.argv[1], sys.argv[2], sys.argv[3]
     fetch, write = load(fdir, "FETCH_SIZE"), load(wdir, "WRITE_SIZE")
+    # one entry per kernel and grid size (the bench launches H.g and the fused pass at n = 8192
+    # and 4096: averaging them would mix two problem sizes); the plain kernel key holds the
+    # largest grid, the bench's headline size
     res = {}
-    for name in set(fetch) | set(write):
+    for key in sorted(set(fetch) | set(write), key=lambda kg: kg[1]):
+        name, grid = key
         k = short(name)
         if not k:
             continue
-        fv, wv = fetch.get(name, []), write.get(name, [])
+        fv, wv = fetch.get(key, []), write.get(key, [])
         if not fv or not wv:
             continue
         fb = 2.0 * 1e3 * sum(fv) / len(fv)      # kB -> B, x2 gfx950 wide-read correction
         wb = 1e3 * sum(wv) / len(wv)
-        e = res.setdefault(k, {"fetch_bytes_per_launch": 0.0, "write_bytes_per_launch": 0.0, "launches": 0,
-                               "kernel": name[:120]})
-        e["fetch_bytes_per_launch"] = fb
-        e["write_bytes_per_launch"] = wb
-        e["traffic_bytes_per_launch"] = fb + wb
-        e["launches"] = len(fv)
+        e = {"fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb, "traffic_bytes_per_launch": fb + wb,
+             "launches": len(fv), "grid_size": grid, "kernel": name[:120]}
+        res[f"{k}@grid{grid}"] = e
+        res[k] = e   # ascending grids: the largest wins
     json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
-                         "FETCH doubled per MI355X_MICROARCH.md gfx950 correction",
+                         "FETCH doubled per MI355X_MICROARCH.md gfx950 correction; per kernel and grid size",
                "kernels": res}, open(out, "w"), indent=1)
     for k, v in sorted(res.items()):
-        print(f"{k:24s} fetch {v['fetch_bytes_per_launch']/1e6:10.2f} MB  write {v['write_bytes_per_launch']/1e6:10.2f} MB"
-              f"  launches {v['launches']}")
+        if "@" in k:
+            print(f"{k:40s} fetch {v['fetch_bytes_per_launch']/1e6:10.2f} MB  write {v['write_bytes_per_launch']/1e6:10.2f} MB"
+                  f"  launches {v['launches']}")
 
 
 if __name__ == "__main__":
