@@ -49,6 +49,7 @@ def _args():
     ap.add_argument("--n", type=int, default=N_PAR)
     ap.add_argument("--host-comm", action="store_true",
                     help="rehearsal on one GPU: gloo + the library's host communicator instead of RCCL")
+    ap.add_argument("--no-bfgs", action="store_true", help="skip the BFGS cfg-2 / BFGS_Bnd cfg-5 solve blocks")
     return ap.parse_args()
 
 
@@ -188,6 +189,67 @@ def bench_hg_sharded(h, n, world, rank, reps=20):
             "note": "host-timed (allgather included), warm cache; per-rank HBM share 1/P of D"}
 
 
+CFG2_P = [1e-4, 0.9, 1e-6, 1, 1000, 1e-6, 1e-3, 200, 1e-9, 1e-6, 0, 0]      # BFGS setParams order (tests)
+CFG5_P = [1e-4, 0.8, 1e-6, 1, 1e-10, 2, 50, 1e-5, 1e-6, 1e-3, 200, 1e-5, 1e-5, 0, -1]   # testBFGSBnd, Examples.cpp:75
+
+
+def _box_qp_solution(d, b, lb, ub, sweeps=400):
+    """KKT point of the cfg-5 box QP (tridiagonal diag(d) + 0.25 off-diagonals): projected
+    red-black Gauss-Seidel, contraction <= 0.5 per sweep (a check of the solve, not timed)."""
+    n = len(d)
+    x = np.zeros(n)
+    for _ in range(sweeps):
+        for par in (0, 1):
+            i = np.arange(par, n, 2)
+            nb = np.where(i + 1 < n, x[np.minimum(i + 1, n - 1)], 0.0) + np.where(i >= 1, x[np.maximum(i - 1, 0)], 0.0)
+            x[i] = np.clip((b[i] - 0.25 * nb) / d[i], lb[i], ub[i])
+    return x
+
+
+def bench_bfgs_solve(ctx, which, n, bscale, params, bounds=None):
+    """One whole BFGS (which=0, cfg 2) or BFGS_Bnd (which=2, cfg 5) solve of the synthetic
+    quadratic generated in HBM, with the per-phase host profile and the device kernel timers."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective, run_bfgs
+    obj = DeviceObjective.synthetic(ctx, L.OBJ_QUADRATIC, n, 0, bscale=bscale)
+    dctx = C.c_void_p()
+    L.check(L.lib().pnol_default_ctx(C.byref(dctx)), "pnol_default_ctx")
+    L.check(L.lib().pnol_ctx_enable_timers(dctx, 1), "timers")
+    L.check(L.lib().pnol_ctx_reset_timers(dctx), "timers")
+    prof = {}
+    lb, ub = bounds if bounds else (None, None)
+    t0 = time.perf_counter()
+    out = run_bfgs(obj, np.zeros(n), params, which=which, lb=lb, ub=ub, profile=prof,
+                   trace_cap=(1 << 20) if which == 2 else 0)
+    wall = time.perf_counter() - t0
+    X, res = out[0], out[1]
+    kern = {k: _timer(L, dctx, k) for k in ("fd_gradient", "bfgs_pass", "hg")}
+    L.check(L.lib().pnol_ctx_enable_timers(dctx, 0), "timers")
+    it = max(int(prof.get("iterations", 0)), 1)
+    blk = {"n": n, "iterations": int(prof.get("iterations", 0)), "evals": int(res.evals), "seconds": wall,
+           "ms_per_iteration": wall / it * 1e3, "iterations_per_s": it / wall, "f0": res.f0, "fopt": res.fopt,
+           "phases_ms_per_iteration": {k: prof[k] / it * 1e3 for k in ("fd_gradient_s", "line_search_s", "update_s")},
+           "other_ms_per_iteration": (prof["total_s"] - prof["fd_gradient_s"] - prof["line_search_s"]
+                                      - prof["update_s"]) / it * 1e3,
+           "line_search_points": int(prof["line_search_points"]), "gradient_calls": int(prof["gradient_calls"]),
+           "kernel_ms_total": {k: v[0] for k, v in kern.items()}, "kernel_launches": {k: v[1] for k, v in kern.items()}}
+    kern_ms = sum(v[0] for v in kern.values())
+    blk["kernel_ms_per_iteration"] = kern_ms / it
+    blk["iteration_over_kernel_sum"] = (wall * 1e3 / it) / (kern_ms / it) if kern_ms > 0 else None
+    if which == 2:
+        import oracle as O   # test infrastructure: only the splitmix64 data stream, for the KKT check
+        d, b = O.quadratic_data(n, bscale=bscale)
+        xs = _box_qp_solution(d, b, lb, ub)
+        tr = out[2]
+        blk.update({"max_recursion_depth": int(prof["max_recursion_depth"]),
+                    "inside_box": bool(np.all(X >= lb) and np.all(X <= ub)),
+                    "f_trace_nonincreasing": bool(np.all(np.diff(tr) <= 0)),
+                    "active_bounds": int(np.sum(np.abs(X - lb) < 1e-5) + np.sum(np.abs(X - ub) < 1e-5)),
+                    "max_abs_err_vs_kkt_point": float(np.max(np.abs(X - xs)))})
+    obj.close()
+    return blk
+
+
 def cpu_baseline(m, n, budget_s=20.0):
     """Oracle (CPU restatement of the reference, 1 thread) on a bounded sample of one LM loop
     trip at (m, n): FD residual evaluations (the n+1 columns), rows of J^T J (the reference's
@@ -320,23 +382,43 @@ def main():
     if rank == 0 and not args.no_hg:
         hg = bench_hg(ctx, HG_N)
         hg4096 = bench_hg(ctx, 4096)
+        hg16384 = bench_hg(ctx, 16384)      # cfg 5: D = 2.15 GB
+    bfgs2 = bnd5 = None
+    if rank == 0 and not args.no_bfgs:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        bfgs2 = bench_bfgs_solve(ctx, 0, 4096, 1.0, CFG2_P)
+        n5 = 16384
+        bnd5 = bench_bfgs_solve(ctx, 2, n5, 4.0, CFG5_P, bounds=(np.full(n5, -0.5), np.full(n5, 0.5)))
     if rank == 0:
         per = per_local
         syrk_ms = per["syrk"]
-        jtj_flop = float(m) * n * (n + 1)                   # unique entries of the symmetric result
+        # J^T J flops of the SYRK this rank ran: all m rows on one GPU; at N > 1 (LevMarqMPI on
+        # m-slices) only the rows of its own slices (unique entries of the symmetric result)
+        if world > 1:
+            mS = C.c_int()
+            L.check(L.lib().pnol_lm_sliced_layout(m, n, C.byref(mS), None), "pnol_lm_sliced_layout")
+            s0, s1 = rank * L.LM_SLICES // world, (rank + 1) * L.LM_SLICES // world
+            jtj_rows = max(0, min(m, s1 * mS.value) - s0 * mS.value)
+        else:
+            jtj_rows = m
+        jtj_flop = float(jtj_rows) * n * (n + 1)
         from parallelnonlinearoptimizationlibrary_amd import fd_tiles
         my_tiles = fd_tiles(n, world, rank)                  # this rank's cost-balanced FD tiles
         my_cols = sum(c for _, c in my_tiles)
         fd_flop_nominal = 2.0 * m * n * my_cols              # full-length chains for this rank's points
         fd_flop = fd_flop_executed(m, n, my_tiles)           # prefix-shared chains actually run
         pmc = pmc_traffic()
+        one_gpu = world == 1
         roofline = {
-            "kernel": "k_syrk_tile<0,128,8 waves> (J^T J, fp64 MFMA v_mfma_f64_16x16x4_f64)",
+            "kernel": ("k_syrk_tile<0,128,8 waves> (J^T J, fp64 MFMA v_mfma_f64_16x16x4_f64)" if one_gpu else
+                       "k_syrk_tile<4,64> on this rank's m-slices (J^T J share, fp64 MFMA v_mfma_f64_16x16x4_f64)"),
             "bound": "mfma", "achieved": jtj_flop / (syrk_ms * 1e-3) / 1e12 if syrk_ms else None,
             "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "traffic": pmc.get("k_syrk_tile<0, 128>", {}).get("traffic_bytes_per_launch"),
+            "flop_per_launch": jtj_flop, "rows": jtj_rows,
+            # PMC passes exist for the one-GPU kernel only; the sliced kernel's traffic is unmeasured
+            "traffic": pmc.get("k_syrk_tile<0, 128>", {}).get("traffic_bytes_per_launch") if one_gpu else None,
             "mfma_busy_pmc": next((v.get("mfma_busy_frac") for k, v in pmc_valu("syrk_mfma").items()
-                                   if "k_syrk_tile" in k), None),
+                                   if "k_syrk_tile" in k), None) if one_gpu else None,
         }
         roofline["frac"] = roofline["achieved"] / FP64_PEAK_TFLOPS if roofline["achieved"] else None
         fd_ms = per["fd_jacobian"]
@@ -388,7 +470,10 @@ def main():
             "fd_jacobian_ms_max_over_ranks": per_max["fd_jacobian"] + per_max["fd_ckpt_per_step"] + (
                 per_max["exchange_J"] if per_max["exchange_J"] > 0 else per_max["allgather"]),
             "converged_rel_err_vs_xstar": err,
-            "bfgs_hg": hg, "bfgs_hg_n4096": hg4096 if hg else None, "bfgs_hg_row_sharded": hg_sharded,
+            "bfgs_hg": hg, "bfgs_hg_n4096": hg4096 if hg else None, "bfgs_hg_n16384": hg16384 if hg else None,
+            "bfgs_hg_row_sharded": hg_sharded,
+            "bfgs_cfg2_solve": bfgs2, "bfgs_bnd_cfg5_solve": bnd5,
+            "comm": {"backend": ("host-gloo" if args.host_comm else "rccl") if world > 1 else "none", "ranks": world},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

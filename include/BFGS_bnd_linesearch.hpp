@@ -38,9 +38,14 @@ class BFGS_Bnd : public AlgorithmBnd {
     int verbose;
     int totalIter;
     int updateMode = 0;
+    bool assessRecursed = false;          // the last boundaryAssessment re-optimised a reduced problem
+    vector<double>* fTrace = nullptr;     // extension: F after every iteration (any recursion level)
+    double* profile = nullptr;            // extension: per-phase seconds and counts
+    int depth = 0;
 
   public:
     void findMinBnd(vector<double>& X, vector<double>& Xlb, vector<double>& Xub, double& f0, double& fOpt);
+    void findMinBndBody(vector<double>& X, vector<double>& Xlb, vector<double>& Xub, double& f0, double& fOpt);
     void mainBFGSLoop(double& F, vector<double>& X, vector<double>& dFdX, pnol::DenseInverseHessian& D,
                       vector<double>& Xlb, vector<double>& Xub, vector<double>& dX, vector<double>& constantX,
                       vector<bool>& constantIndicator, bool& optimFlag, int& recurFlag);
@@ -72,6 +77,12 @@ class BFGS_Bnd : public AlgorithmBnd {
     void setGradVec(vector<double>& v) { dXGradVec.assign(v.begin(), v.end()); }
     void setinitialScalingVec(vector<double>& v) { initialScalingVec.assign(v.begin(), v.end()); }
     void setUpdateMode(int mode) { updateMode = mode; }
+    // --- MI355X extensions (diagnostics; the reference has no counterpart) ---
+    void setFTrace(vector<double>* trace) { fTrace = trace; }
+    // 8 doubles: iterations, total, FD gradient, line search, D update seconds, line-search
+    // points, gradient calls, deepest recursion level
+    void setProfile(double* prof) { profile = prof; }
+    int getTotalIter() const { return totalIter; }
 
     BFGS_Bnd()
         : c1(1e-4), c2(0.9), dalpha(1e-6), alphaGuess(1), alphaTol(1e-20), alphaMult(2), maxIterLineSearch(50),

@@ -57,6 +57,7 @@ class BFGS_Bnd_MPI_SW : public AlgorithmBnd {
 
   public:
     void findMinBnd(vector<double>& X, vector<double>& Xlb, vector<double>& Xub, double& f0, double& fOpt);
+    void findMinBndBody(vector<double>& X, vector<double>& Xlb, vector<double>& Xub, double& f0, double& fOpt);
     void mainBFGSLoop(double& F, vector<double>& X, vector<double>& dFdX, pnol::DenseInverseHessian& D,
                       vector<double>& Xlb, vector<double>& Xub, vector<double>& dX, vector<double>& constantX,
                       vector<bool>& constantIndicator);

@@ -35,6 +35,7 @@ class BFGS : public Algorithm {
     bool verbose;
     // MI355X: 0 = auto (exact for n <= PNOL_SEQ_MAX), 1 = exact, 2 = fast
     int updateMode = 0;
+    double* profile = nullptr;   // extension: per-phase seconds and counts (pnol_run_bfgs_ex)
 
   public:
     void findMin(vector<double>& X, double& f0, double& fOpt);
@@ -56,6 +57,9 @@ class BFGS : public Algorithm {
         initHessFD = initHessFDIn; verbose = verboseIn;
     }
     void setUpdateMode(int mode) { updateMode = mode; }
+    // --- MI355X extension (diagnostics): 8 doubles -- iterations, total, FD gradient, line
+    // search and D update seconds, line-search points, gradient calls, unused
+    void setProfile(double* prof) { profile = prof; }
 
     BFGS()
         : c1(1e-4), c2(0.9), dalpha(1e-6), alphaGuess(1), maxIterLineSearch(1000), dXGrad(1e-6), dXHess(1e-3),

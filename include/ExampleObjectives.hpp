@@ -198,8 +198,12 @@ class QuadraticObjective : public Objective {
     // device-only construction around an existing (e.g. device-generated) objective
     explicit QuadraticObjective(pnol_dobj* o) { dev.attach(o); }
     double objEval(vector<double>& X) {
+        if (d.empty()) {   // device-only instance: one-point batch on the device
+            double f = 0;
+            objEvalBatch(X.data(), 1, (int)X.size(), &f);
+            return f;
+        }
         evals++;
-        if (d.empty()) return deviceEval(X);
         const size_t n = X.size();
         double f = 0.0;
         for (size_t i = 0; i < n; ++i) {
@@ -208,6 +212,16 @@ class QuadraticObjective : public Objective {
             f = f + t;
         }
         return f;
+    }
+    // line-search points and pools of a device-only instance run on the device in one batch
+    // (context scratch, one upload and one download: no allocation per call)
+    void objEvalBatch(const double* Xs, int nPts, int n, double* f) {
+        if (!d.empty()) return Objective::objEvalBatch(Xs, nPts, n, f);
+        pnol_ctx* ctx = nullptr;
+        if (pnol_default_ctx(&ctx) != PNOL_OK) throw std::runtime_error("pnol_amd: no device");
+        evals += nPts;
+        if (pnol_dobj_eval_batch(ctx, dev.current(), Xs, nPts, f) != PNOL_OK)
+            throw std::runtime_error("pnol_amd: device objective eval failed");
     }
     pnol_dobj* deviceObjective(int n) {
         (void)n;
@@ -218,24 +232,6 @@ class QuadraticObjective : public Objective {
     void countEvals(long k) { evals += k; }
     void useDevice(bool on) { dev.enabled = on; }
     long getEvals() { return evals; }
-
-  private:
-    // single-point evaluation on the device (device-only instances)
-    double deviceEval(vector<double>& X) {
-        pnol_ctx* ctx = nullptr;
-        if (pnol_default_ctx(&ctx) != PNOL_OK) throw std::runtime_error("pnol_amd: no device");
-        void *dx = nullptr, *df = nullptr;
-        pnol_malloc(ctx, sizeof(double) * X.size(), &dx);
-        pnol_malloc(ctx, sizeof(double), &df);
-        pnol_memcpy_h2d(ctx, dx, X.data(), sizeof(double) * X.size());
-        int st = pnol_dobj_eval_d(ctx, dev.current(), (const double*)dx, (double*)df);
-        double f = 0;
-        pnol_memcpy_d2h(ctx, &f, df, sizeof(double));
-        pnol_free(ctx, dx);
-        pnol_free(ctx, df);
-        if (st != PNOL_OK) throw std::runtime_error("pnol_amd: device objective eval failed");
-        return f;
-    }
 };
 
 // ---- residual objectives -----------------------------------------------------------------

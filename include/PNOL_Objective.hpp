@@ -14,6 +14,13 @@
  *     (pnol_fd_gradient_d / pnol_fd_jacobian_d), bitwise equal to the host values for the
  *     transcendental-free objectives.  countEvals() lets such an objective keep its
  *     evaluation counter in step with the reference (one count per point).
+ *   - Any objective may override objEvalBatch(): the FD engine hands it every batch of
+ *     independent points at once (the N+1 gradient points, the Jacobian columns, the FD
+ *     Hessian's triples) and the line searches hand it their trial points (the Wolfe pair
+ *     phi(alpha), phi(alpha + dalpha); the MPI classes' pools).  The default loops over
+ *     objEval in the reference's evaluation order, so a plain objEval-only objective sees
+ *     exactly the reference's calls.  Overriding it is how a user objective runs its own batch
+ *     on the GPU (or on host threads) without becoming a built-in device objective.
  */
 #ifndef PNOL_AMD_OBJECTIVE_HPP_
 #define PNOL_AMD_OBJECTIVE_HPP_
@@ -36,6 +43,8 @@ class Objective {
     virtual double objEval(vector<double>& X) = 0;
 
     // --- MI355X extension hooks (defaults keep the reference's host behaviour) ---
+    // f[k] = f(point k) for the nPts points of Xs (row-major nPts x n); default: objEval in order
+    virtual void objEvalBatch(const double* Xs, int nPts, int n, double* f);
     // device objective for n-parameter points, or nullptr for host evaluation
     virtual pnol_dobj* deviceObjective(int n) { (void)n; return nullptr; }
     virtual void countEvals(long points) { (void)points; }
@@ -61,6 +70,8 @@ class MultiObjective {
     // F(X), one residual per data point (reference: PNOL_Objective.hpp:57); F is pre-sized
     virtual void objEval(vector<double>& X, vector<double>& F) = 0;
 
+    // F rows k*m .. k*m+m-1 = F(point k) for the nPts points of Xs (nPts x n); default: objEval in order
+    virtual void objEvalBatch(const double* Xs, int nPts, int n, double* F, int m);
     virtual pnol_dobj* deviceObjective() { return nullptr; }
     virtual void countEvals(long points) { (void)points; }
 

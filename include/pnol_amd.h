@@ -99,6 +99,13 @@ int pnol_bfgs_update_exact_d(pnol_ctx* ctx, double* D, int ldd, const double* y,
 int pnol_bfgs_pass_d(pnol_ctx* ctx, double* D, int ldd, int n,
                      const double* s_p, const double* a_p, const double* b_p, int write_back,
                      const double* y, const double* g, double* u, double* w, double* v);
+/* pnol_bfgs_pass_d with write_back on a D that is diag(scale) (I when scale == NULL) and is not
+ * read: the pending correction (required) is folded into the synthesised diagonal and the result
+ * written to D, u/w/v as above -- the first update after a reset (BFGS_bnd_linesearch.cpp:607-616,
+ * 647) costs 8 n^2 bytes instead of the 8 n^2 identity write plus the 16 n^2 pass. */
+int pnol_bfgs_pass_ident_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale, const double* s_p,
+                           const double* a_p, const double* b_p, const double* y, const double* g, double* u, double* w,
+                           double* v);
 /* D = I (BFGS_with_linesearch.cpp:46-56), or diag(scale) when scale != NULL (BFGS_bnd_linesearch.cpp:65-83) */
 int pnol_set_identity_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale);
 /* BFGS D row-sharded over the communicator (the reference keeps a full D per rank,
@@ -113,6 +120,10 @@ int pnol_hg_mpi_d(pnol_ctx* ctx, const double* Dsh, int ldd, const double* g, do
 int pnol_bfgs_pass_mpi_d(pnol_ctx* ctx, double* Dsh, int ldd, int n, const double* s_p, const double* a_p,
                          const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
                          double* v);
+/* pnol_bfgs_pass_ident_d on this rank's rows (collective) */
+int pnol_bfgs_pass_ident_mpi_d(pnol_ctx* ctx, double* Dsh, int ldd, int n, const double* scale, const double* s_p,
+                               const double* a_p, const double* b_p, const double* y, const double* g, double* u,
+                               double* w, double* v);
 /* Dsub[a][b] = D[idx[a]][idx[b]] for a, b < nsub (idx: device ints, ascending, < n): the
  * free-free block of D handed to the reduced problem, BFGS_with_bnd_linsearch_MPI.cpp:822-843 */
 int pnol_gather_submatrix_d(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub,
@@ -202,6 +213,15 @@ int pnol_dobj_eval_ckpt_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, double
  * f0 = f(x); g_i = (f(x + h_i e_i) - f0) / h_i for i in [i0, i0 + cnt).  g gets cnt values. */
 int pnol_fd_gradient_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, int i0, int cnt,
                        double* f0, double* g);
+/* Host-pointer forms (return with the results on the host; context scratch + pinned staging, one
+ * upload and one download, no allocation): the per-iteration FD gradient of the C++ classes
+ * (PNOL_Objective.cpp:12-34; g gets cnt values, *f0 = f(x)), and a batch of single evaluations
+ * (line-search trial points and pool entries, BFGS_with_linesearch.cpp:144-174,
+ * BFGS_with_linesearch_MPI.cpp:163-223): out[k] = f(Xs row k) for scalar kinds, out rows
+ * k*m .. k*m+m-1 = F(Xs row k) for residual kinds; Xs is npts x n row-major. */
+int pnol_fd_gradient(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, int i0, int cnt, double* f0,
+                     double* g);
+int pnol_dobj_eval_batch(pnol_ctx* ctx, pnol_dobj* obj, const double* Xs, int npts, double* out);
 /* MultiObjective::gradientApproximation (PNOL_Objective.cpp:165-197) for columns [j0, j0+cnt):
  * F0 = F(x) (computed here when compute_f0, else read), JT row (j - j0) = (F(x + h_j e_j) - F0)/h_j.
  * compute_f0 = 2 (pnol_fd_jtj_d / pnol_fd_jacobian_tiles_d): F0 was filled by
@@ -251,6 +271,14 @@ typedef struct { int iters; long evals; double f0; double fopt; } pnol_result;
  * 4 = BFGS_Bnd_MPI_SW (15 params [+ Nprocs-equivalent pool size, update mode]) */
 int pnol_run_bfgs(int which, pnol_dobj* obj, int host_eval, const double* params, int nparams,
                   double* X, int n, const double* Xlb, const double* Xub, pnol_result* res);
+/* pnol_run_bfgs plus diagnostics.  BFGS (0) and BFGS_Bnd (2): res->iters = the iteration count
+ * (BFGS_Bnd: totalIter); profile (8 doubles, nullable) = iterations, total seconds, FD-gradient
+ * seconds, line-search seconds, D update / direction seconds, line-search points evaluated,
+ * gradient calls, deepest boundaryAssessment recursion.  BFGS_Bnd: F after every iteration of
+ * any recursion level in ftrace[0 .. min(cap, *ntrace)) (nullable). */
+int pnol_run_bfgs_ex(int which, pnol_dobj* obj, int host_eval, const double* params, int nparams, double* X, int n,
+                     const double* Xlb, const double* Xub, pnol_result* res, double* ftrace, int trace_cap,
+                     int* ntrace, double* profile);
 /* which: 0 = LevMarq, 1 = LevMarqMPI (6 params). F0/FOpt host arrays of m. */
 int pnol_run_levmarq(int which, pnol_dobj* obj, int host_eval, const double* params, double* X, int n,
                      double* F0, double* FOpt, int m, pnol_result* res);

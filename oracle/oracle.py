@@ -300,6 +300,20 @@ def bfgs_bnd_findmin(o: Obj, x0, lb, ub, params):  # BFGS_Bnd::findMinBnd
     return X, res
 
 
+def bfgs_bnd_findmin_ex(o: Obj, x0, lb, ub, params, rank2=False, trace_cap=0):
+    """BFGS_Bnd::findMinBnd with the rank-2 update form (rank2) and an F trace; returns
+    (X, res, ftrace, max recursion depth)."""
+    X = np.array(x0, dtype=np.float64)
+    lb = np.ascontiguousarray(lb, dtype=np.float64); ub = np.ascontiguousarray(ub, dtype=np.float64)
+    prm = BFGSBndParams(*params)
+    res = Result()
+    tr = np.zeros(max(trace_cap, 1))
+    depth = C.c_int()
+    lib().orc_bfgs_bnd_findmin_ex(o.ref(), C.byref(prm), ptr(X), ptr(lb), ptr(ub), len(X), C.byref(res),
+                                  int(rank2), ptr(tr), trace_cap, C.byref(depth))
+    return X, res, tr[: min(res.iters, trace_cap)], depth.value
+
+
 def bfgs_bnd_mpi_findmin(o: Obj, x0, lb, ub, params, npool, nprocs=None):  # BFGSBnd_MPI::findMinBnd
     """Returns (X, res, status); status -1 = a NaN/inf pool value (the reference's exit(0))."""
     X = np.array(x0, dtype=np.float64)

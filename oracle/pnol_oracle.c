@@ -796,6 +796,10 @@ typedef struct {
     int sw;             /* 1: BFGS_Bnd_MPI_SW's pooled line search (Nprocs = procs) */
     int procs;
     int* optimFlag;     /* the SW class member, cleared by a NaN / inf pool value */
+    int rank2;          /* 1: updateHessianInv in its O(n^2) rank-2 form (large-n parity runs) */
+    double* ftrace;     /* optional: F after every mainBFGSLoop iteration (any recursion level) */
+    int trace_cap;
+    int depth, max_depth; /* boundaryAssessment recursion depth (diagnostics) */
 } bnd_ctx;
 
 /* BFGS_Bnd::lineSearchObj / lineSearchFDDerivative, :465-496 */
@@ -1068,7 +1072,9 @@ static void bnd_assess(bnd_ctx* c, double* F, double* X, const double* p, double
             }
         set_identity(DR, nr);
         *recurFlag = 1;
+        if (++c->depth > c->max_depth) c->max_depth = c->depth;
         bnd_main_loop(c, &FR, XR, gR, DR, lbR, ubR, dXR, nr, cX, cI, optimFlag, recurFlag);
+        c->depth--;
         ir = 0;
         for (icur = 0; icur < ncur; ++icur)
             if (!cIcur[icur]) {
@@ -1121,11 +1127,13 @@ static void bnd_main_loop(bnd_ctx* c, double* F, double* X, double* g, double* D
         memcpy(gprev, g, sizeof(double) * (size_t)n);
         orc_fd_gradient_recur(c->o, X, dX, g, n, cX, cI, c->nfull);
         for (int i = 0; i < n; ++i) { s[i] = alpha * p[i]; y[i] = g[i] - gprev[i]; }
-        orc_update_hessian_inv(D, y, s, n);
+        if (c->rank2) orc_update_hessian_inv_rank2(D, y, s, n);
+        else orc_update_hessian_inv(D, y, s, n);
         bnd_assess(c, F, X, p, g, D, Xlb, Xub, dX, n, cX, cI, optimFlag, recurFlag);
         xdiff = 0;
         for (int i = 0; i < n; ++i) xdiff += fabs(X[i] - Xprev[i]);
         gnorm = orc_util_norm2(g, n);
+        if (c->ftrace && c->totalIter < c->trace_cap) c->ftrace[c->totalIter] = *F;
         iter++;
         c->totalIter++;
     }
@@ -1135,7 +1143,13 @@ static void bnd_main_loop(bnd_ctx* c, double* F, double* X, double* g, double* D
 /* BFGS_Bnd::findMinBnd, BFGS_bnd_linesearch.cpp:15-113 (no dXGradVec / initialScalingVec) */
 int orc_bfgs_bnd_findmin(orc_objective* o, const orc_bfgs_bnd_params* prm, double* X, const double* Xlb_in,
                          const double* Xub_in, int n, orc_result* res) {
-    bnd_ctx c = {o, prm, n, 0, (int)prm->maxIter, 0, 1, NULL};
+    return orc_bfgs_bnd_findmin_ex(o, prm, X, Xlb_in, Xub_in, n, res, 0, NULL, 0, NULL);
+}
+
+int orc_bfgs_bnd_findmin_ex(orc_objective* o, const orc_bfgs_bnd_params* prm, double* X, const double* Xlb_in,
+                            const double* Xub_in, int n, orc_result* res, int rank2, double* ftrace, int trace_cap,
+                            int* max_depth) {
+    bnd_ctx c = {o, prm, n, 0, (int)prm->maxIter, 0, 1, NULL, rank2, ftrace, trace_cap, 0, 0};
     double* Xlb = (double*)malloc(sizeof(double) * (size_t)n);
     double* Xub = (double*)malloc(sizeof(double) * (size_t)n);
     memcpy(Xlb, Xlb_in, sizeof(double) * (size_t)n);
@@ -1164,6 +1178,7 @@ int orc_bfgs_bnd_findmin(orc_objective* o, const orc_bfgs_bnd_params* prm, doubl
     int optimFlag = 1, recurFlag = 0;
     bnd_main_loop(&c, &F, X, g, D, Xlb, Xub, dX, n, cX, cI, &optimFlag, &recurFlag);
     res->fopt = F; res->iters = c.totalIter; res->evals = o->evals - ev0;
+    if (max_depth) *max_depth = c.max_depth;
     free(Xlb); free(Xub); free(cX); free(cI); free(dX); free(g); free(D);
     return 0;
 }
@@ -1173,7 +1188,7 @@ int orc_bfgs_bnd_findmin(orc_objective* o, const orc_bfgs_bnd_params* prm, doubl
 int orc_bfgs_bnd_mpi_sw_findmin(orc_objective* o, const orc_bfgs_bnd_params* prm, int procs, double* X,
                                 const double* Xlb_in, const double* Xub_in, int n, orc_result* res) {
     int optimFlag = 1, recurFlag = 0;
-    bnd_ctx c = {o, prm, n, 0, (int)prm->maxIter, 1, procs, &optimFlag};
+    bnd_ctx c = {o, prm, n, 0, (int)prm->maxIter, 1, procs, &optimFlag, 0, NULL, 0, 0, 0};
     double* Xlb = (double*)malloc(sizeof(double) * (size_t)n);
     double* Xub = (double*)malloc(sizeof(double) * (size_t)n);
     memcpy(Xlb, Xlb_in, sizeof(double) * (size_t)n);

@@ -116,6 +116,12 @@ typedef struct {   /* BFGS_Bnd::setParams, BFGS_bnd_linesearch.hpp:80 */
 /* BFGS_Bnd::findMinBnd, BFGS_bnd_linesearch.cpp:15-113 */
 int orc_bfgs_bnd_findmin(orc_objective* o, const orc_bfgs_bnd_params* prm, double* X, const double* Xlb,
                          const double* Xub, int n, orc_result* res);
+/* the same with the rank-2 O(n^2) form of updateHessianInv when rank2 != 0 (tractable at large n;
+ * the reference form sums in another order), F after every iteration in ftrace (nullable) and
+ * the deepest boundaryAssessment recursion in max_depth (nullable) */
+int orc_bfgs_bnd_findmin_ex(orc_objective* o, const orc_bfgs_bnd_params* prm, double* X, const double* Xlb,
+                            const double* Xub, int n, orc_result* res, int rank2, double* ftrace, int trace_cap,
+                            int* max_depth);
 /* BFGS_Bnd_MPI_SW::findMinBnd, BFGS_bnd_linesearch_MPI_SW.cpp:12-113 (same setParams as BFGS_Bnd;
  * Nprocs = procs: pools of procs + 1 / procs + 2) */
 int orc_bfgs_bnd_mpi_sw_findmin(orc_objective* o, const orc_bfgs_bnd_params* prm, int procs, double* X,

@@ -72,6 +72,8 @@ _SIGS = {
     "pnol_bfgs_update_exact_d": (_i, [_vp, _vp, _i, _vp, _vp, _i]),
     "pnol_bfgs_pass_d": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
     "pnol_set_identity_d": (_i, [_vp, _vp, _i, _i, _vp]),
+    "pnol_bfgs_pass_ident_d": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "pnol_bfgs_pass_ident_mpi_d": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "pnol_bfgs_rows": (_i, [_i, _i, _i, C.POINTER(_i), C.POINTER(_i)]),
     "pnol_set_identity_rows_d": (_i, [_vp, _vp, _i, _i, _vp]),
     "pnol_hg_mpi_d": (_i, [_vp, _vp, _i, _vp, _vp, _i]),
@@ -93,6 +95,8 @@ _SIGS = {
     "pnol_dobj_eval_d": (_i, [_vp, _vp, _vp, _vp]),
     "pnol_dobj_eval_ckpt_d": (_i, [_vp, _vp, _vp, _vp]),
     "pnol_fd_gradient_d": (_i, [_vp, _vp, _vp, _vp, _i, _i, _vp, _vp]),
+    "pnol_fd_gradient": (_i, [_vp, _vp, _dp, _dp, _i, _i, _dp, _dp]),
+    "pnol_dobj_eval_batch": (_i, [_vp, _vp, _dp, _i, _dp]),
     "pnol_fd_jacobian_d": (_i, [_vp, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _i]),
     "pnol_fd_jtj_d": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp, _i, _d, _vp, _i, _vp, _i]),
     "pnol_fd_jacobian_tiles_d": (_i, [_vp, _vp, _vp, _vp, C.POINTER(_i), C.POINTER(_i), _i, _vp, _i, _vp, _i]),
@@ -106,6 +110,8 @@ _SIGS = {
     "pnol_fd_tiles": (_i, [_i, _i, _i, C.POINTER(_i), C.POINTER(_i), _i]),
     "pnol_comm_share_fd_rows_d": (_i, [_vp, _vp, _i, _i]),
     "pnol_run_bfgs": (_i, [_i, _vp, _i, _dp, _i, _dp, _i, _dp, _dp, C.POINTER(Result)]),
+    "pnol_run_bfgs_ex": (_i, [_i, _vp, _i, _dp, _i, _dp, _i, _dp, _dp, C.POINTER(Result), _dp, _i, C.POINTER(_i),
+                              _dp]),
     "pnol_run_levmarq": (_i, [_i, _vp, _i, _dp, _dp, _i, _dp, _dp, _i, C.POINTER(Result)]),
     "pnol_host_fd_jacobian": (_i, [HOST_MULTI_FN, _vp, _dp, _dp, _i, _i, _i, _dp]),
 }

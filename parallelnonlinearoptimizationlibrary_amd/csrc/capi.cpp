@@ -48,6 +48,15 @@ int pnol_bfgs_pass_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p
     return launch_bfgs_pass(ctx, D, ldd, n, s_p, a_p, b_p, write_back, y, g, u, w, v);
 }
 
+int pnol_bfgs_pass_ident_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale, const double* s_p,
+                           const double* a_p, const double* b_p, const double* y, const double* g, double* u, double* w,
+                           double* v) {
+    PNOL_CHECK(set_device(ctx));
+    if (!s_p || !a_p || !b_p) return PNOL_ERR_ARG;
+    ScopedTimer tm(ctx, "bfgs_pass");
+    return launch_bfgs_pass(ctx, D, ldd, n, s_p, a_p, b_p, 1, y, g, u, w, v, 0, -1, nullptr, 1, scale);
+}
+
 int pnol_set_identity_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale) {
     PNOL_CHECK(set_device(ctx));
     return launch_set_identity(ctx, D, ldd, n, scale);
@@ -152,6 +161,26 @@ int pnol_bfgs_pass_mpi_d(pnol_ctx* ctx, double* Dsh, int ldd, int n, const doubl
     PNOL_CHECK(ws_get(ctx, "pass_rows_v", sizeof(double) * span, &vb));
     PNOL_CHECK(launch_bfgs_pass(ctx, Dsh, ldd, n, s_p, a_p, b_p, write_back, y, g, u ? (double*)ub : nullptr, w,
                                 v ? (double*)vb : nullptr, b, b + c, P > 1 ? pass_w_allgather : nullptr));
+    if (u) PNOL_CHECK(rows_allgather(ctx, (double*)ub, n, u));
+    if (v) PNOL_CHECK(rows_allgather(ctx, (double*)vb, n, v));
+    return PNOL_OK;
+}
+
+int pnol_bfgs_pass_ident_mpi_d(pnol_ctx* ctx, double* Dsh, int ldd, int n, const double* scale, const double* s_p,
+                               const double* a_p, const double* b_p, const double* y, const double* g, double* u,
+                               double* w, double* v) {
+    PNOL_CHECK(set_device(ctx));
+    if (!s_p || !a_p || !b_p) return PNOL_ERR_ARG;
+    const int P = comm_size();
+    int b = 0, c = 0;
+    PNOL_CHECK(pnol_bfgs_rows(n, P, comm_rank(), &b, &c));
+    ScopedTimer tm(ctx, "bfgs_pass");
+    const size_t span = (size_t)P * bfgs_rows_per(n, P);
+    void *ub = nullptr, *vb = nullptr;
+    PNOL_CHECK(ws_get(ctx, "pass_rows_u", sizeof(double) * span, &ub));
+    PNOL_CHECK(ws_get(ctx, "pass_rows_v", sizeof(double) * span, &vb));
+    PNOL_CHECK(launch_bfgs_pass(ctx, Dsh, ldd, n, s_p, a_p, b_p, 1, y, g, u ? (double*)ub : nullptr, w,
+                                v ? (double*)vb : nullptr, b, b + c, P > 1 ? pass_w_allgather : nullptr, 1, scale));
     if (u) PNOL_CHECK(rows_allgather(ctx, (double*)ub, n, u));
     if (v) PNOL_CHECK(rows_allgather(ctx, (double*)vb, n, v));
     return PNOL_OK;
@@ -319,6 +348,56 @@ int pnol_fd_gradient_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const dou
     PNOL_CHECK(set_device(ctx));
     ScopedTimer tm(ctx, "fd_gradient");
     return launch_fd_gradient(ctx, obj, x, h, i0, cnt, f0, g);
+}
+
+// Host-pointer forms for the C++ classes' per-iteration calls: the context's scratch and
+// pinned staging, one upload and one download per call (no allocation, one stream sync).
+int pnol_fd_gradient(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, int i0, int cnt, double* f0,
+                     double* g) {
+    PNOL_CHECK(set_device(ctx));
+    if (!obj || !x || !h || !f0 || (cnt > 0 && !g) || cnt < 0 || i0 < 0 || i0 + cnt > obj->n) return PNOL_ERR_ARG;
+    const size_t n = (size_t)obj->n, io = 2 * n + (size_t)cnt + 1;
+    void* dv = nullptr;
+    PNOL_CHECK(ws_get(ctx, "fdg_io", sizeof(double) * io, &dv));
+    double* dx = (double*)dv;
+    double *dh = dx + n, *dg = dh + n, *df = dg + cnt;
+    double* st = (double*)pinned_stage(ctx, sizeof(double) * io);
+    if (!st) return PNOL_ERR_NOMEM;
+    std::memcpy(st, x, sizeof(double) * n);
+    std::memcpy(st + n, h, sizeof(double) * n);
+    PNOL_HIP(hipMemcpyAsync(dx, st, sizeof(double) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+    {
+        ScopedTimer tm(ctx, "fd_gradient");
+        PNOL_CHECK(launch_fd_gradient(ctx, obj, dx, dh, i0, cnt, df, dg));
+    }
+    PNOL_HIP(hipMemcpyAsync(st + 2 * n, dg, sizeof(double) * ((size_t)cnt + 1), hipMemcpyDeviceToHost, ctx->stream));
+    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    if (cnt > 0) std::memcpy(g, st + 2 * n, sizeof(double) * cnt);
+    *f0 = st[2 * n + cnt];
+    return PNOL_OK;
+}
+
+int pnol_dobj_eval_batch(pnol_ctx* ctx, pnol_dobj* obj, const double* Xs, int npts, double* out) {
+    PNOL_CHECK(set_device(ctx));
+    if (!obj || npts < 0 || (npts > 0 && (!Xs || !out))) return PNOL_ERR_ARG;
+    if (npts == 0) return PNOL_OK;
+    const size_t n = (size_t)obj->n, per = obj->m > 0 ? (size_t)obj->m : 1;
+    const size_t nin = n * npts, nout = per * npts;
+    void* dv = nullptr;
+    PNOL_CHECK(ws_get(ctx, "batch_io", sizeof(double) * (nin + nout), &dv));
+    double *dX = (double*)dv, *dF = dX + nin;
+    double* st = (double*)pinned_stage(ctx, sizeof(double) * std::max(nin, nout));
+    if (st) {
+        std::memcpy(st, Xs, sizeof(double) * nin);
+        PNOL_HIP(hipMemcpyAsync(dX, st, sizeof(double) * nin, hipMemcpyHostToDevice, ctx->stream));
+    } else {
+        PNOL_HIP(hipMemcpyAsync(dX, Xs, sizeof(double) * nin, hipMemcpyHostToDevice, ctx->stream));
+    }
+    PNOL_CHECK(launch_eval_batch(ctx, obj, dX, npts, dF));
+    PNOL_HIP(hipMemcpyAsync(st ? st : out, dF, sizeof(double) * nout, hipMemcpyDeviceToHost, ctx->stream));
+    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    if (st) std::memcpy(out, st, sizeof(double) * nout);
+    return PNOL_OK;
 }
 
 int pnol_fd_jacobian_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, int j0, int cnt, double* F0,

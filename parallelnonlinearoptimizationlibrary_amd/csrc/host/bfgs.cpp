@@ -7,6 +7,7 @@
 
 #include "BFGS_with_linesearch.hpp"
 #include "dense_hessian.hpp"
+#include "line_points.hpp"
 
 using namespace pnol;
 
@@ -63,8 +64,13 @@ void BFGS::lineSearchZoom(double alo, double ahi, double plo, double phi, double
     int it = 0;
     for (; it < maxIterLineSearch; ++it) {
         const double aj = cubicInterpMin(alo, ahi, plo, phi, dlo, dhi, X, p);
-        const double pj = lineSearchObj(aj, X, p);
-        const double dj = lineSearchFDDerivative(aj, pj, X, p);
+        // lineSearchObj + lineSearchFDDerivative as one batch of two points
+        const double a2[2] = {aj, aj + dalpha};
+        double f2[2];
+        eval_line_points(objPtr, X, p, a2, 2, f2);
+        if (profile) profile[kProfPoints] += 2;
+        const double pj = f2[0];
+        const double dj = (f2[1] - pj) / dalpha;
         if (pj > phi0 + c1 * aj * dphi0 || pj >= plo) {
             ahi = aj; phi = pj; dhi = dj;
             continue;
@@ -89,8 +95,12 @@ void BFGS::cubicInterpolationLineSearch(vector<double>& X, double FX, vector<dou
     double aim1 = 0, pim1 = phi0, dim1 = dphi0;
     double ai = alphaGuess;
     for (int it = 0; it < maxIterLineSearch; ++it) {
-        const double pi = lineSearchObj(ai, X, p);
-        const double di = lineSearchFDDerivative(ai, pi, X, p);
+        const double a2[2] = {ai, ai + dalpha};
+        double f2[2];
+        eval_line_points(objPtr, X, p, a2, 2, f2);
+        if (profile) profile[kProfPoints] += 2;
+        const double pi = f2[0];
+        const double di = (f2[1] - pi) / dalpha;
         if ((pi > phi0 + c1 * ai * dphi0) || (pi >= pim1 && it > 1)) {
             lineSearchZoom(aim1, ai, pim1, pi, dim1, di, phi0, dphi0, X, p, alphaOpt, Fopt, dphiOpt);
             return;
@@ -112,13 +122,18 @@ void BFGS::cubicInterpolationLineSearch(vector<double>& X, double FX, vector<dou
 void BFGS::findMin(vector<double>& X, double& f0, double& fOpt) {
     // BFGS_with_linesearch.cpp:12-139
     const int n = (int)X.size();
+    PhaseClock total(prof_slot(profile, kProfTotal));
     pnol_ctx* ctx = require_ctx();
     DenseInverseHessian D(ctx, n, updateMode);
     if (initHessFD) init_from_fd_hessian(objPtr, X, dXHess, D);
     else D.setIdentity();
 
     std::vector<double> dX(n, dXGrad), dFdX(n), dFdXprev(n), p(n), pnext(n), s(n), y(n), Xprev(n);
-    objPtr->gradientApproximation(X, dX, dFdX);
+    {
+        PhaseClock t(prof_slot(profile, kProfGrad));
+        objPtr->gradientApproximation(X, dX, dFdX);
+        if (profile) profile[kProfGradCalls] += 1;
+    }
     double F = objPtr->objEval(X);
     f0 = F;
     int iter = 0;
@@ -126,15 +141,29 @@ void BFGS::findMin(vector<double>& X, double& f0, double& fOpt) {
     bool have_next = false;
     while (iter < maxIter && xdiff > xMinDiff && gnorm > minGrad2Norm) {
         dFdXprev = dFdX;
-        if (have_next) p = pnext;
-        else D.direction(dFdX, p);
+        if (have_next) {
+            p = pnext;
+        } else {
+            PhaseClock t(prof_slot(profile, kProfUpdate));
+            D.direction(dFdX, p);
+        }
         double alpha = 0, Fopt = 0;
-        cubicInterpolationLineSearch(X, F, dFdX, p, alpha, Fopt);
+        {
+            PhaseClock t(prof_slot(profile, kProfLineSearch));
+            cubicInterpolationLineSearch(X, F, dFdX, p, alpha, Fopt);
+        }
         for (int i = 0; i < n; ++i) { Xprev[i] = X[i]; X[i] = X[i] + alpha * p[i]; }
         F = Fopt;
-        objPtr->gradientApproximation(X, dX, dFdX);
+        {
+            PhaseClock t(prof_slot(profile, kProfGrad));
+            objPtr->gradientApproximation(X, dX, dFdX);
+            if (profile) profile[kProfGradCalls] += 1;
+        }
         for (int i = 0; i < n; ++i) { s[i] = alpha * p[i]; y[i] = dFdX[i] - dFdXprev[i]; }
-        D.update(y, s, &dFdX, &pnext);
+        {
+            PhaseClock t(prof_slot(profile, kProfUpdate));
+            D.update(y, s, &dFdX, &pnext);
+        }
         have_next = true;
         xdiff = 0;
         for (int i = 0; i < n; ++i) xdiff += std::fabs(X[i] - Xprev[i]);
@@ -146,6 +175,7 @@ void BFGS::findMin(vector<double>& X, double& f0, double& fOpt) {
         }
         iter = iter + 1;
     }
+    if (profile) profile[kProfIters] = iter;
     fOpt = F;
     if (verbose) {
         std::cout << std::endl << "-----------------------------------------------------------------------------------" << std::endl;

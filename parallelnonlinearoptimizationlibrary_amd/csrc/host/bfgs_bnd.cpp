@@ -7,7 +7,9 @@
 
 #include "../pnol_comm.hpp"
 #include "BFGS_bnd_linesearch.hpp"
+#include "deep_stack.hpp"
 #include "dense_hessian.hpp"
+#include "line_points.hpp"
 
 using namespace pnol;
 
@@ -80,8 +82,12 @@ void BFGS_Bnd::lineSearchZoomBnd(double aa, double ab, double pa, double pb, dou
     bool success = false;
     while (iter_ls < maxIterLineSearch && (ab - aa > alphaTol)) {
         const double ac = cubicInterpMinSimple(aa, ab, pa, pb, da, db);
-        const double pc = lineSearchObj(ac, X, p, cX, cI);
-        const double dc = lineSearchFDDerivative(ac, pc, X, p, cX, cI);
+        const double a2[2] = {ac, ac + dalpha};   // the (phi, FD slope) pair as one batch
+        double f2[2];
+        eval_line_points_recur(objPtr, X, p, a2, 2, cX, cI, f2);
+        if (profile) profile[kProfPoints] += 2;
+        const double pc = f2[0];
+        const double dc = (f2[1] - pc) / dalpha;
         double pmin = pa;
         if (pb < pa) pmin = pb;
         if (pc > phi0 + c1 * ac * dphi0 || pc >= pmin) {
@@ -118,8 +124,12 @@ void BFGS_Bnd::cubicInterpolationLineSearchBnd(vector<double>& X, vector<double>
     if (ai > amax) ai = amax;
     int iter_ls = 0;
     while (iter_ls < maxIterLineSearch) {
-        phii = lineSearchObj(ai, X, p, cX, cI);
-        const double di = lineSearchFDDerivative(ai, phii, X, p, cX, cI);
+        const double a2[2] = {ai, ai + dalpha};
+        double f2[2];
+        eval_line_points_recur(objPtr, X, p, a2, 2, cX, cI, f2);
+        if (profile) profile[kProfPoints] += 2;
+        phii = f2[0];
+        const double di = (f2[1] - phii) / dalpha;
         if ((phii > phi0 + c1 * ai * dphi0) || (phii >= pim1 && iter_ls > 1)) {
             lineSearchZoomBnd(aim1, ai, pim1, phii, dim1, di, phi0, dphi0, X, p, cX, cI, iter_ls, aOpt, Fopt, dOpt);
             success = true;
@@ -186,7 +196,9 @@ void BFGS_Bnd::boundaryAssessment(double& F, vector<double>& X, vector<double>& 
                 XR.push_back(X[icur]); gR.push_back(dFdX[icur]); lbR.push_back(Xlb[icur]);
                 ubR.push_back(Xub[icur]); dXR.push_back(dX[icur]);
             }
-        DenseInverseHessian DR(require_ctx(), nr, updateMode);
+        // the outer D is discarded while the reduced problem runs (reset below), so the
+        // reduced D takes over its device buffer: one n x n matrix for the whole recursion
+        DenseInverseHessian DR(D, nr, updateMode);
         std::vector<double> scaleR;
         if (!initialScalingVec.empty()) {
             for (int i = 0; i < Ndim; ++i) if (!cI[i]) scaleR.push_back(initialScalingVec[i]);
@@ -195,7 +207,11 @@ void BFGS_Bnd::boundaryAssessment(double& F, vector<double>& X, vector<double>& 
             DR.setIdentity();
         }
         recurFlag = true;
+        ++depth;
+        if (profile && depth > profile[kProfDepth]) profile[kProfDepth] = depth;
         mainBFGSLoop(FR, XR, gR, DR, lbR, ubR, dXR, cX, cI, optimFlag, recurFlag);
+        --depth;
+        assessRecursed = true;   // after the reduced loop, which clears it for its own levels
         int ir = 0;
         for (icur = 0; icur < ncur; ++icur)
             if (!cIcur[icur]) {
@@ -212,7 +228,11 @@ void BFGS_Bnd::boundaryAssessment(double& F, vector<double>& X, vector<double>& 
         } else {
             D.setIdentity();
         }
-        objPtr->gradientApproximationRecur(X, dX, dFdX, cX, cI);
+        {
+            PhaseClock t(prof_slot(profile, kProfGrad));
+            objPtr->gradientApproximationRecur(X, dX, dFdX, cX, cI);
+            if (profile) profile[kProfGradCalls] += 1;
+        }
         bool cont = false;
         for (icur = 0; icur < ncur; ++icur)
             if (cIcur[icur]) {
@@ -238,26 +258,49 @@ void BFGS_Bnd::mainBFGSLoop(double& F, vector<double>& X, vector<double>& dFdX, 
                             vector<bool>& cI, bool& optimFlag, int& recurFlag) {
     // BFGS_bnd_linesearch.cpp:116-201
     const int n = (int)X.size();
-    std::vector<double> gprev = dFdX, p(n), s(n), y(n), Xprev(n);
+    std::vector<double> p(n), pnext, Xprev(n);
+    bool have_next = false;
     int iter = 0;
     double xdiff = xMinDiff * 2, gnorm = 2 * minGrad2Norm;
     while (optimFlag && iter < maxIter && xdiff > xMinDiff && gnorm > minGrad2Norm && totalIter < maxIter) {
         if (verbose > 0 && comm_rank() == ROOT_ID)
             std::cout << std::endl << "Iter = " << iter << " of bounded BFGS search starting with previous F = " << F
                       << "." << std::endl;
-        D.direction(dFdX, p);
+        // p = -D g (:142-143); after an iteration without recursion it came out of the update's
+        // pass (the same bits: D and g are what the update left)
+        if (have_next) {
+            p.swap(pnext);
+        } else {
+            PhaseClock t(prof_slot(profile, kProfUpdate));
+            D.direction(dFdX, p);
+        }
         double alpha = 0, Fopt = 0;
-        cubicInterpolationLineSearchBnd(X, Xlb, Xub, F, dFdX, p, cX, cI, alpha, Fopt);
+        {
+            PhaseClock t(prof_slot(profile, kProfLineSearch));
+            cubicInterpolationLineSearchBnd(X, Xlb, Xub, F, dFdX, p, cX, cI, alpha, Fopt);
+        }
         for (int i = 0; i < n; ++i) { Xprev[i] = X[i]; X[i] = X[i] + alpha * p[i]; }
         F = Fopt;
-        gprev = dFdX;
-        objPtr->gradientApproximationRecur(X, dX, dFdX, cX, cI);
-        for (int i = 0; i < n; ++i) { s[i] = alpha * p[i]; y[i] = dFdX[i] - gprev[i]; }
-        D.update(y, s, nullptr, nullptr);
+        {
+            std::vector<double> gprev = dFdX, s(n), y(n);
+            {
+                PhaseClock t(prof_slot(profile, kProfGrad));
+                objPtr->gradientApproximationRecur(X, dX, dFdX, cX, cI);
+                if (profile) profile[kProfGradCalls] += 1;
+            }
+            for (int i = 0; i < n; ++i) { s[i] = alpha * p[i]; y[i] = dFdX[i] - gprev[i]; }
+            PhaseClock t(prof_slot(profile, kProfUpdate));
+            D.update(y, s, &dFdX, &pnext);
+        }   // s, y, gprev freed before a possible recursion (one level per frozen coordinate)
+        assessRecursed = false;
         boundaryAssessment(F, X, p, dFdX, D, Xlb, Xub, dX, cX, cI, optimFlag, recurFlag);
+        // a recursion reset D to I and recomputed the gradient: the fused direction is stale
+        have_next = !assessRecursed;
+        if (!have_next) std::vector<double>().swap(pnext);
         xdiff = 0;
         for (int i = 0; i < n; ++i) xdiff += std::fabs(X[i] - Xprev[i]);
         gnorm = std::sqrt(seq_dot(dFdX, dFdX));
+        if (fTrace) fTrace->push_back(F);
         if (verbose > 1 && comm_rank() == ROOT_ID) {
             std::cout << "  Step completed with F = " << F << " and mean abs xdiff is " << xdiff
                       << " and the grad2norm = " << gnorm << std::endl << "  X = ";
@@ -269,6 +312,16 @@ void BFGS_Bnd::mainBFGSLoop(double& F, vector<double>& X, vector<double>& dFdX, 
 }
 
 void BFGS_Bnd::findMinBnd(vector<double>& X, vector<double>& Xlb, vector<double>& Xub, double& f0, double& fOpt) {
+    // the active-set recursion goes one level deeper per frozen coordinate (about 11k levels
+    // at n = 16384, SURVEY 8(d) cfg 5): run it on a thread with a stack sized for that
+    PhaseClock total(prof_slot(profile, kProfTotal));
+    depth = 0;
+    run_deep([&] { findMinBndBody(X, Xlb, Xub, f0, fOpt); });
+    if (profile) profile[kProfIters] = totalIter;
+}
+
+void BFGS_Bnd::findMinBndBody(vector<double>& X, vector<double>& Xlb, vector<double>& Xub, double& f0,
+                              double& fOpt) {
     // BFGS_bnd_linesearch.cpp:15-113
     totalIter = 0;
     if (verbose >= 0 && comm_rank() == ROOT_ID) {
@@ -292,7 +345,11 @@ void BFGS_Bnd::findMinBnd(vector<double>& X, vector<double>& Xlb, vector<double>
     } else {
         D.setIdentity();
     }
-    objPtr->gradientApproximationRecur(X, dX, dFdX, cX, cI);
+    {
+        PhaseClock t(prof_slot(profile, kProfGrad));
+        objPtr->gradientApproximationRecur(X, dX, dFdX, cX, cI);
+        if (profile) profile[kProfGradCalls] += 1;
+    }
     double F = objPtr->objEvalRecur(X, cX, cI);
     f0 = F;
     bool optimFlag = true;

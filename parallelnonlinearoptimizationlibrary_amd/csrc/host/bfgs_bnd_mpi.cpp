@@ -11,6 +11,7 @@
 #include "../pnol_comm.hpp"
 #include "BFGS_with_bnd_linesearch_MPI.hpp"
 #include "dense_hessian.hpp"
+#include "line_points.hpp"
 
 using namespace pnol;
 
@@ -67,10 +68,9 @@ void BFGSBnd_MPI::evalAlphaPoolMPI(vector<double>& alphaPool, vector<double>& ph
     const int P = comm_size(), r = comm_rank();
     const int per = (N + P - 1) / P;
     std::vector<double> mine(per, 0.0), all((size_t)per * P, 0.0);
-    for (int q = 0; q < per; ++q) {
-        const int k = r + q * P;
-        if (k < N) mine[q] = lineSearchObj(alphaPool[k], X, p, cX, cI);
-    }
+    std::vector<double> mya;   // this rank's entries, one batch
+    for (int k = r; k < N; k += P) mya.push_back(alphaPool[k]);
+    eval_line_points_recur(objPtr, X, p, mya.data(), (int)mya.size(), cX, cI, mine.data());
     check(comm_allgather_host(nullptr, mine.data(), all.data(), (size_t)per), "allgather(alpha pool)");
     for (int k = 0; k < N; ++k) phiPool[k] = all[(size_t)(k % P) * per + k / P];
     for (int k = 0; k < N; ++k)
@@ -261,7 +261,8 @@ void BFGSBnd_MPI::mainBFGSLoop(double& F, vector<double>& X, vector<double>& dFd
         secantLineSearchBnd(X, Xlb, Xub, F, dFdX, p, alpha, Fopt, cX, cI);
         // a step that misses the tolerance is retried along steepest descent (:153-166)
         if (F - Fopt < FStepTolerance) {
-            if (verbose && comm_rank() == ROOT_ID)
+            // printed on the root rank whatever the verbosity (BFGS_with_bnd_linsearch_MPI.cpp:156-158)
+            if (comm_rank() == ROOT_ID)
                 std::cout << "Line search failed in the quasi-newton direction. Recomputing gradient and "
                           << "attempting steepest descent instead." << std::endl;
             objPtr->gradientApproximationMPIRecur(X, dX, dFdX, cX, cI);

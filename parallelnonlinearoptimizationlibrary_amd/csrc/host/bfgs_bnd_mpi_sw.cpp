@@ -9,7 +9,9 @@
 
 #include "../pnol_comm.hpp"
 #include "BFGS_bnd_linesearch_MPI_SW.hpp"
+#include "deep_stack.hpp"
 #include "dense_hessian.hpp"
+#include "line_points.hpp"
 
 using namespace pnol;
 
@@ -96,11 +98,16 @@ void BFGS_Bnd_MPI_SW::evaluateAlphaPoolAndDerivatives(vector<double>& ap, vector
     const int P = comm_size(), r = comm_rank();
     const int per = (N + P - 1) / P > 0 ? (N + P - 1) / P : 1;
     std::vector<double> mine(2 * (size_t)per, 0.0), all(2 * (size_t)per * P, 0.0);
+    // this rank's entries as one batch of (alpha, alpha + dalpha) pairs, in the reference's order
+    std::vector<double> mya, fv;
+    for (int k = r; k < N; k += P) { mya.push_back(ap[k]); mya.push_back(ap[k] + dalpha); }
+    fv.resize(mya.size());
+    eval_line_points_recur(objPtr, X, p, mya.data(), (int)mya.size(), cX, cI, fv.data());
     for (int q = 0; q < per; ++q) {
         const int k = r + q * P;
         if (k >= N) continue;
-        double phi = lineSearchObj(ap[k], X, p, cX, cI);
-        const double dphi = lineSearchFDDerivative(ap[k], phi, X, p, cX, cI);
+        double phi = fv[2 * q];
+        const double dphi = (fv[2 * q + 1] - phi) / dalpha;
         if (phi != phi || std::isinf(phi)) {
             phi = 1e10;
             std::cout << "Line search crashed with " << std::endl << phi << std::endl << "Ending search..." << std::endl;
@@ -286,7 +293,7 @@ void BFGS_Bnd_MPI_SW::boundaryAssessment(double& F, vector<double>& X, vector<do
                 ubR.push_back(Xub[icur]); dXR.push_back(dX[icur]);
             }
         // the reduced problem starts along steepest descent (scaled if a scaling was set)
-        DenseInverseHessian DR(require_ctx(), nr, updateMode, true);
+        DenseInverseHessian DR(D, nr, updateMode, true);   // D's buffer: it is reset on return
         if (!initialScalingVec.empty()) {
             std::vector<double> scaleR;
             for (int i = 0; i < Ndim; ++i) if (!cI[i]) scaleR.push_back(initialScalingVec[i]);
@@ -370,6 +377,12 @@ void BFGS_Bnd_MPI_SW::mainBFGSLoop(double& F, vector<double>& X, vector<double>&
 
 void BFGS_Bnd_MPI_SW::findMinBnd(vector<double>& X, vector<double>& Xlb, vector<double>& Xub, double& f0,
                                  double& fOpt) {
+    // the active-set recursion is one level per frozen coordinate (deep_stack.hpp)
+    run_deep([&] { findMinBndBody(X, Xlb, Xub, f0, fOpt); });
+}
+
+void BFGS_Bnd_MPI_SW::findMinBndBody(vector<double>& X, vector<double>& Xlb, vector<double>& Xub, double& f0,
+                                     double& fOpt) {
     // :12-113
     totalIter = 0;
     Nprocs = comm_size();

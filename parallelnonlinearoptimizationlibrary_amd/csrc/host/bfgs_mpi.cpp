@@ -8,6 +8,7 @@
 #include "../pnol_comm.hpp"
 #include "BFGS_with_linesearch_MPI.hpp"
 #include "dense_hessian.hpp"
+#include "line_points.hpp"
 
 using namespace pnol;
 
@@ -58,10 +59,9 @@ void BFGS_MPI::evalAlphaPoolMPI(vector<double>& alphaPool, vector<double>& phiPo
     const int P = comm_size(), r = comm_rank();
     const int per = (N + P - 1) / P;
     std::vector<double> mine(per, 0.0), all((size_t)per * P, 0.0);
-    for (int q = 0; q < per; ++q) {
-        const int k = r + q * P;
-        if (k < N) mine[q] = lineSearchObj(alphaPool[k], X, p);
-    }
+    std::vector<double> mya;   // this rank's entries, one batch
+    for (int k = r; k < N; k += P) mya.push_back(alphaPool[k]);
+    eval_line_points(objPtr, X, p, mya.data(), (int)mya.size(), mine.data());
     check(comm_allgather_host(nullptr, mine.data(), all.data(), (size_t)per), "allgather(alpha pool)");
     for (int k = 0; k < N; ++k) phiPool[k] = all[(size_t)(k % P) * per + k / P];
 }

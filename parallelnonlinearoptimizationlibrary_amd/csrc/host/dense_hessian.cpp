@@ -13,41 +13,110 @@ static bool shard_enabled() {
     return !e || std::atoi(e) != 0;
 }
 
-DenseInverseHessian::DenseInverseHessian(pnol_ctx* ctx, int n, int mode, bool shard)
-    : ctx_(ctx), n_(n), ld_(even_ld(n)), exact_(mode == 1 || (mode == 0 && n <= PNOL_SEQ_MAX)) {
+void DenseInverseHessian::init(int mode, bool shard) {
+    exact_ = mode == 1 || (mode == 0 && n_ <= PNOL_SEQ_MAX);
     rb_ = 0;
-    rc_ = n;
+    rc_ = n_;
     if (shard && !exact_ && comm_size() > 1 && shard_enabled()) {
         sharded_ = true;
-        check(pnol_bfgs_rows(n, comm_size(), comm_rank(), &rb_, &rc_), "bfgs_rows");
+        check(pnol_bfgs_rows(n_, comm_size(), comm_rank(), &rb_, &rc_), "bfgs_rows");
     }
-    D_.reset(ctx, (size_t)(rc_ > 0 ? rc_ : 1) * ld_);
-    y_.reset(ctx, n); s_.reset(ctx, n); g_.reset(ctx, n);
-    u_.reset(ctx, n); w_.reset(ctx, n); v_.reset(ctx, n);
-    if (!exact_) { ps_.reset(ctx, n); pa_.reset(ctx, n); pb_.reset(ctx, n); }
+    y_.reset(ctx_, n_); s_.reset(ctx_, n_); g_.reset(ctx_, n_);
+    u_.reset(ctx_, n_); w_.reset(ctx_, n_); v_.reset(ctx_, n_);
+    if (!exact_) { ps_.reset(ctx_, n_); pa_.reset(ctx_, n_); pb_.reset(ctx_, n_); }
+}
+
+DenseInverseHessian::DenseInverseHessian(pnol_ctx* ctx, int n, int mode, bool shard)
+    : ctx_(ctx), n_(n), ld_(even_ld(n)) {
+    init(mode, shard);
+    cap_ = (size_t)(rc_ > 0 ? rc_ : 1) * ld_;
+    D_.reset(ctx, cap_);
+    Dp_ = D_.get();
+    dev_ok_ = false;   // contents undefined until setIdentity / setMatrix
+}
+
+DenseInverseHessian::DenseInverseHessian(DenseInverseHessian& parent, int n, int mode, bool shard)
+    : ctx_(parent.ctx_), n_(n), ld_(even_ld(n)) {
+    init(mode, shard);
+    const size_t need = (size_t)(rc_ > 0 ? rc_ : 1) * ld_;
+    if (need <= parent.cap_ && parent.Dp_) {
+        Dp_ = parent.Dp_;
+        cap_ = parent.cap_;
+        parent.clobbered_ = true;
+    } else {
+        cap_ = need;
+        D_.reset(ctx_, cap_);
+        Dp_ = D_.get();
+    }
+    dev_ok_ = false;
+}
+
+const double* DenseInverseHessian::deviceScale() {
+    if (hscale_.empty()) return nullptr;
+    if (!dscale_ok_) {
+        if (dscale_.size() < (size_t)n_) dscale_.reset(ctx_, n_);
+        dscale_.upload(hscale_.data(), (size_t)n_);
+        dscale_ok_ = true;
+    }
+    return dscale_.get();
 }
 
 void DenseInverseHessian::setIdentity(const std::vector<double>* diagScale) {
-    const double* scale = nullptr;
-    if (diagScale) {
-        g_.upload(diagScale->data(), (size_t)n_);
-        scale = g_.get();
-    }
-    if (sharded_) check(pnol_set_identity_rows_d(ctx_, D_.get(), ld_, n_, scale), "set_identity");
-    else check(pnol_set_identity_d(ctx_, D_.get(), ld_, n_, scale), "set_identity");
+    // lazy: nothing is written until something has to read D itself (ensureDevice)
+    if (diagScale) hscale_.assign(diagScale->begin(), diagScale->begin() + n_);
+    else hscale_.clear();
+    dscale_ok_ = false;
+    ident_ = true;
+    dev_ok_ = false;
     pending_ = false;
+    clobbered_ = false;
+}
+
+void DenseInverseHessian::ensureDevice() {
+    if (clobbered_) throw std::runtime_error("DenseInverseHessian: D used while lent to a reduced problem");
+    if (dev_ok_) return;
+    if (!ident_) throw std::runtime_error("DenseInverseHessian: D used before it was set");
+    const double* scale = deviceScale();
+    if (sharded_) check(pnol_set_identity_rows_d(ctx_, Dp_, ld_, n_, scale), "set_identity");
+    else check(pnol_set_identity_d(ctx_, Dp_, ld_, n_, scale), "set_identity");
+    dev_ok_ = true;
+}
+
+// the diagonal shortcut is exact only for finite operands (0 * inf poisons a device row sum)
+bool DenseInverseHessian::identFinite(const std::vector<double>* a, const std::vector<double>* b) const {
+    for (const std::vector<double>* v : {a, b})
+        if (v)
+            for (int i = 0; i < n_; ++i)
+                if (!std::isfinite((*v)[i])) return false;
+    for (double x : hscale_)
+        if (!std::isfinite(x)) return false;
+    return true;
 }
 
 void DenseInverseHessian::setMatrix(const std::vector<std::vector<double>>& D) {
     std::vector<double> h((size_t)(rc_ > 0 ? rc_ : 1) * ld_, 0.0);
     for (int i = 0; i < rc_; ++i)
         for (int j = 0; j < n_; ++j) h[(size_t)i * ld_ + j] = D[rb_ + i][j];
-    D_.upload(h.data(), h.size());
+    check(pnol_memcpy_h2d(ctx_, Dp_, h.data(), sizeof(double) * h.size()), "h2d");
     pending_ = false;
+    ident_ = false;
+    dev_ok_ = true;
+    clobbered_ = false;
 }
 
 void DenseInverseHessian::setSubmatrixOf(DenseInverseHessian& src, const std::vector<int>& idx) {
     if ((int)idx.size() != n_) throw std::runtime_error("setSubmatrixOf: index count != n");
+    if (src.ident_ && !src.pending_) {
+        // a diagonal D's free-free block is the diagonal of the kept coordinates
+        if (src.hscale_.empty()) {
+            setIdentity();
+        } else {
+            std::vector<double> sub(n_);
+            for (int a = 0; a < n_; ++a) sub[a] = src.hscale_[idx[a]];
+            setIdentity(&sub);
+        }
+        return;
+    }
     if (sharded_ || src.sharded_) {
         // rare (boundary recursion): through the host, every rank holding the whole source
         std::vector<std::vector<double>> full, sub(n_, std::vector<double>(n_));
@@ -58,33 +127,52 @@ void DenseInverseHessian::setSubmatrixOf(DenseInverseHessian& src, const std::ve
         return;
     }
     src.materialize();
+    src.ensureDevice();
     DevVec di(ctx_, (idx.size() + 1) / 2);   // ints in a double-sized device buffer
     check(pnol_memcpy_h2d(ctx_, di.get(), idx.data(), sizeof(int) * idx.size()), "h2d");
-    check(pnol_gather_submatrix_d(ctx_, src.D_.get(), src.ld_, src.n_, reinterpret_cast<const int*>(di.get()), n_,
-                                  D_.get(), ld_),
+    check(pnol_gather_submatrix_d(ctx_, src.Dp_, src.ld_, src.n_, reinterpret_cast<const int*>(di.get()), n_, Dp_,
+                                  ld_),
           "gather_submatrix");
     pending_ = false;
+    ident_ = false;
+    dev_ok_ = true;
+    clobbered_ = false;
 }
 
 int DenseInverseHessian::pass(const double* sp, const double* ap, const double* bp, int wb, const double* y,
                               const double* g, double* u, double* w, double* v) {
-    if (sharded_) return pnol_bfgs_pass_mpi_d(ctx_, D_.get(), ld_, n_, sp, ap, bp, wb, y, g, u, w, v);
-    return pnol_bfgs_pass_d(ctx_, D_.get(), ld_, n_, sp, ap, bp, wb, y, g, u, w, v);
+    ensureDevice();
+    if (sharded_) return pnol_bfgs_pass_mpi_d(ctx_, Dp_, ld_, n_, sp, ap, bp, wb, y, g, u, w, v);
+    return pnol_bfgs_pass_d(ctx_, Dp_, ld_, n_, sp, ap, bp, wb, y, g, u, w, v);
+}
+
+// fold the pending correction into a stored diagonal without reading it
+int DenseInverseHessian::passIdent(const double* y, const double* g, double* u, double* w, double* v) {
+    if (clobbered_) throw std::runtime_error("DenseInverseHessian: D used while lent to a reduced problem");
+    const double* scale = deviceScale();
+    int st = sharded_ ? pnol_bfgs_pass_ident_mpi_d(ctx_, Dp_, ld_, n_, scale, ps_.get(), pa_.get(), pb_.get(), y, g, u, w, v)
+                      : pnol_bfgs_pass_ident_d(ctx_, Dp_, ld_, n_, scale, ps_.get(), pa_.get(), pb_.get(), y, g, u, w, v);
+    ident_ = false;
+    dev_ok_ = true;
+    return st;
 }
 
 void DenseInverseHessian::materialize() {
     if (!pending_) return;
-    check(pass(ps_.get(), pa_.get(), pb_.get(), 1, nullptr, nullptr, u_.get(), w_.get(), v_.get()),
-          "bfgs_pass(materialize)");
+    if (ident_) check(passIdent(nullptr, nullptr, u_.get(), w_.get(), v_.get()), "bfgs_pass(materialize)");
+    else
+        check(pass(ps_.get(), pa_.get(), pb_.get(), 1, nullptr, nullptr, u_.get(), w_.get(), v_.get()),
+              "bfgs_pass(materialize)");
     pending_ = false;
 }
 
 void DenseInverseHessian::getMatrix(std::vector<std::vector<double>>& D) {
     materialize();
+    ensureDevice();
     D.assign(n_, std::vector<double>(n_));
     if (!sharded_) {
         std::vector<double> h((size_t)n_ * ld_);
-        D_.download(h.data(), h.size());
+        check(pnol_memcpy_d2h(ctx_, h.data(), Dp_, sizeof(double) * h.size()), "d2h");
         for (int i = 0; i < n_; ++i)
             for (int j = 0; j < n_; ++j) D[i][j] = h[(size_t)i * ld_ + j];
         return;
@@ -93,7 +181,7 @@ void DenseInverseHessian::getMatrix(std::vector<std::vector<double>>& D) {
     int b0 = 0, per = 0;
     check(pnol_bfgs_rows(n_, comm_size(), 0, &b0, &per), "bfgs_rows");
     std::vector<double> mine((size_t)per * ld_, 0.0), all((size_t)per * ld_ * comm_size());
-    if (rc_ > 0) D_.download(mine.data(), (size_t)rc_ * ld_);
+    if (rc_ > 0) check(pnol_memcpy_d2h(ctx_, mine.data(), Dp_, sizeof(double) * (size_t)rc_ * ld_), "d2h");
     check(comm_allgather_host(ctx_, mine.data(), all.data(), mine.size()), "allgather(D)");
     for (int i = 0; i < n_; ++i)
         for (int j = 0; j < n_; ++j) D[i][j] = all[(size_t)i * ld_ + j];   // rank r's rows start at r * per
@@ -101,10 +189,24 @@ void DenseInverseHessian::getMatrix(std::vector<std::vector<double>>& D) {
 
 void DenseInverseHessian::direction(const std::vector<double>& g, std::vector<double>& p) {
     p.resize(n_);
+    if (ident_ && identFinite(&g, nullptr)) {
+        // D g for a stored diagonal: the one nonzero term of each row sum, 0.0 + d_i g_i (the
+        // device sums start from +0, so an exact zero product comes out +0)
+        std::vector<double> v(n_);
+        for (int i = 0; i < n_; ++i) v[i] = 0.0 + sc(i) * g[i];
+        if (!pending_) {
+            for (int i = 0; i < n_; ++i) p[i] = -v[i];
+            return;
+        }
+        const double ag = seq_dot(ha_, g), sg = seq_dot(hs_, g);
+        for (int i = 0; i < n_; ++i) p[i] = -(v[i] + hs_[i] * ag + hb_[i] * sg);
+        return;
+    }
     g_.upload(g);
     if (!pending_) {
-        if (sharded_) check(pnol_hg_mpi_d(ctx_, D_.get(), ld_, g_.get(), v_.get(), n_), "hg");
-        else check(pnol_hg_d(ctx_, D_.get(), ld_, g_.get(), v_.get(), n_), "hg");
+        ensureDevice();
+        if (sharded_) check(pnol_hg_mpi_d(ctx_, Dp_, ld_, g_.get(), v_.get(), n_), "hg");
+        else check(pnol_hg_d(ctx_, Dp_, ld_, g_.get(), v_.get(), n_), "hg");
         v_.download(p);   // v = -D g
         return;
     }
@@ -121,22 +223,36 @@ void DenseInverseHessian::direction(const std::vector<double>& g, std::vector<do
 void DenseInverseHessian::update(const std::vector<double>& y, const std::vector<double>& s,
                                  const std::vector<double>* gnext, std::vector<double>* pnext) {
     if (exact_) {
+        ensureDevice();
         y_.upload(y);
         s_.upload(s);
-        check(pnol_bfgs_update_exact_d(ctx_, D_.get(), ld_, y_.get(), s_.get(), n_), "bfgs_update_exact");
+        check(pnol_bfgs_update_exact_d(ctx_, Dp_, ld_, y_.get(), s_.get(), n_), "bfgs_update_exact");
+        ident_ = false;
         if (gnext && pnext) direction(*gnext, *pnext);
         return;
     }
-    y_.upload(y);
-    if (gnext) g_.upload(*gnext);
-    // one pass: fold the pending correction in (write-back) and form D y, D^T y, D g_next
-    check(pass(pending_ ? ps_.get() : nullptr, pending_ ? pa_.get() : nullptr, pending_ ? pb_.get() : nullptr,
-               pending_ ? 1 : 0, y_.get(), gnext ? g_.get() : nullptr, u_.get(), w_.get(), v_.get()),
-          "bfgs_pass(update)");
     std::vector<double> u(n_), w(n_), v;
-    u_.download(u);
-    w_.download(w);
-    if (gnext) { v.resize(n_); v_.download(v); }
+    if (gnext) v.resize(n_);
+    if (ident_ && !pending_ && identFinite(&y, gnext)) {
+        // u = D y, w = D^T y, v = D g of a stored diagonal, exactly as the pass sums them
+        for (int i = 0; i < n_; ++i) u[i] = w[i] = 0.0 + sc(i) * y[i];
+        if (gnext)
+            for (int i = 0; i < n_; ++i) v[i] = 0.0 + sc(i) * (*gnext)[i];
+    } else {
+        y_.upload(y);
+        if (gnext) g_.upload(*gnext);
+        // one pass: fold the pending correction in (write-back) and form D y, D^T y, D g_next
+        if (pending_ && ident_)
+            check(passIdent(y_.get(), gnext ? g_.get() : nullptr, u_.get(), w_.get(), v_.get()), "bfgs_pass(update)");
+        else
+            check(pass(pending_ ? ps_.get() : nullptr, pending_ ? pa_.get() : nullptr, pending_ ? pb_.get() : nullptr,
+                       pending_ ? 1 : 0, y_.get(), gnext ? g_.get() : nullptr, u_.get(), w_.get(), v_.get()),
+                  "bfgs_pass(update)");
+        if (pending_) ident_ = false;
+        u_.download(u);
+        w_.download(w);
+        if (gnext) v_.download(v);
+    }
     const double rho = 1 / seq_dot(y, s);
     const double beta = seq_dot(y, u);
     const double c = rho * rho * beta + rho;

@@ -12,6 +12,19 @@
 // rows [rb, rb + rc) of D and the passes / H.g run on those rows only, the full n-vectors
 // assembled by allgathers (pnol_*_mpi_d) -- bitwise the one-GPU results, 1/P of the HBM
 // traffic per rank.
+//
+// Identity state.  setIdentity() (D = I or diag(scale): BFGS_with_linesearch.cpp:46-56,
+// BFGS_bnd_linesearch.cpp:65-83, 607-616, 647) writes nothing: while D is a stored diagonal,
+// D g, D y and D^T y are the single products 0.0 + scale_i v_i the device sums would give
+// (every other term of each sum is an exact zero), formed on the host; the first fold of a
+// pending correction synthesises the diagonal instead of reading it (16 n^2 bytes saved), and
+// the identity is written out only when something must read D itself.  Non-finite inputs take
+// the device path (0 * inf must poison the whole row as it does there).
+//
+// Storage lending.  BFGS_Bnd's active-set recursion discards the outer D while the reduced
+// problem runs (it is reset to I on return, BFGS_bnd_linesearch.cpp:620, 647), so a reduced
+// D borrows its parent's device buffer: the whole recursion -- up to one level per iteration
+// at n = 16384 -- holds one n x n matrix (2.15 GB) instead of one per level.
 #pragma once
 
 #include <vector>
@@ -27,9 +40,13 @@ class DenseInverseHessian {
     // mode: 0 auto (exact for n <= PNOL_SEQ_MAX), 1 exact, 2 fast; shard: row-shard D over the
     // communicator when in fast mode with more than one rank (PNOL_BFGS_SHARD=0 disables)
     DenseInverseHessian(pnol_ctx* ctx, int n, int mode, bool shard = false);
+    // a reduced D on the device buffer of `parent` (when it fits; else its own): the parent's
+    // contents are forfeit until its next setIdentity / setMatrix
+    DenseInverseHessian(DenseInverseHessian& parent, int n, int mode, bool shard = false);
     bool sharded() const { return sharded_; }
     int n() const { return n_; }
     bool exact() const { return exact_; }
+    bool borrowed() const { return Dp_ != D_.get(); }
 
     void setIdentity(const std::vector<double>* diagScale = nullptr);
     void setMatrix(const std::vector<std::vector<double>>& D);
@@ -44,24 +61,39 @@ class DenseInverseHessian {
                 std::vector<double>* pnext);
 
   private:
+    void init(int mode, bool shard);
     void materialize();   // fold a pending correction into D
+    void ensureDevice();  // the stored D really in device memory (writes a lazy identity)
+    const double* deviceScale();
+    bool identFinite(const std::vector<double>* a, const std::vector<double>* b) const;
+    double sc(int i) const { return hscale_.empty() ? 1.0 : hscale_[i]; }
     int pass(const double* sp, const double* ap, const double* bp, int wb, const double* y, const double* g, double* u,
              double* w, double* v);
+    int passIdent(const double* y, const double* g, double* u, double* w, double* v);
 
     pnol_ctx* ctx_;
     int n_, ld_;
     bool exact_;
     bool sharded_ = false;
     int rb_ = 0, rc_ = 0;              // this rank's rows of D (all rows when not sharded)
-    DevVec D_;
+    DevVec D_;                         // own storage (empty when borrowed)
+    double* Dp_ = nullptr;             // the matrix: D_.get() or the lender's buffer
+    size_t cap_ = 0;                   // doubles available at Dp_ (lent on to reduced problems)
     DevVec y_, s_, g_, u_, w_, v_;     // staging vectors
     DevVec ps_, pa_, pb_;              // pending correction (fast mode)
+    DevVec dscale_;                    // device copy of the diagonal scale (lazy)
     bool pending_ = false;
     std::vector<double> hs_, ha_, hb_; // host copies of the pending correction
+    bool ident_ = false;               // stored D == diag(hscale_) (empty: I)
+    bool dev_ok_ = true;               // device memory holds the stored D
+    bool clobbered_ = false;           // buffer lent to a reduced problem since the last reset
+    bool dscale_ok_ = false;
+    std::vector<double> hscale_;
 };
 
 // D0 = inverse of the FD Hessian (initHessFD: hessianApproximation + matrixInverse,
-// PNOL_Objective.cpp:38-85), column by column through the reference-order device LU
+// PNOL_Objective.cpp:38-85, BFGS_with_linesearch.cpp:34-41): one device LU factorisation,
+// the n unit right-hand sides solved against it in the reference's per-column order
 void init_from_fd_hessian(Objective* obj, std::vector<double>& X, double dXHess, DenseInverseHessian& D);
 
 }  // namespace pnol

@@ -1,6 +1,7 @@
 // device_util.hpp -- small RAII helpers the C++ drop-in classes use on top of the C ABI.
 #pragma once
 
+#include <chrono>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -68,6 +69,28 @@ class DevVec {
 };
 
 inline int even_ld(int n) { return (n + 1) & ~1; }
+
+// Per-phase wall-clock accounting of a solve (extension diagnostics, pnol_run_bfgs_ex): adds
+// the seconds of its scope to *acc when acc is set.  Every timed phase ends with its results
+// on the host, so host time is the phase's time.
+class PhaseClock {
+  public:
+    explicit PhaseClock(double* acc) : acc_(acc) {
+        if (acc_) t0_ = std::chrono::steady_clock::now();
+    }
+    ~PhaseClock() {
+        if (acc_) *acc_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0_).count();
+    }
+
+  private:
+    double* acc_;
+    std::chrono::steady_clock::time_point t0_;
+};
+
+// slots of a solve profile (8 doubles)
+enum ProfileSlot { kProfIters = 0, kProfTotal, kProfGrad, kProfLineSearch, kProfUpdate, kProfPoints, kProfGradCalls,
+                   kProfDepth };
+inline double* prof_slot(double* prof, int k) { return prof ? prof + k : nullptr; }
 
 // reference utility restatements used by the host-side control logic (sequential order,
 // identical to the CPU oracle's)

@@ -3,6 +3,7 @@
 // callback-objective FD entry point for the host path of the FD engine.
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <exception>
 #include <vector>
 
@@ -59,11 +60,23 @@ class DriverScalar : public Objective {
                 throw std::runtime_error("DriverScalar: not a scalar objective");
         }
     }
+    // Trial points / pools: the host formula by default (an O(n) objective costs less on the
+    // host than a PCIe round trip); PNOL_DEVICE_POINTS=1 sends every batch to the device
+    // (pnol_dobj_eval_batch, the same bits) -- how the tests exercise the device batch path.
+    void objEvalBatch(const double* Xs, int nPts, int n, double* f) override {
+        if (host_only_ || !device_points() || n != d_->n) return Objective::objEvalBatch(Xs, nPts, n, f);
+        evals += nPts;
+        check(pnol_dobj_eval_batch(d_->ctx, d_, Xs, nPts, f), "dobj_eval_batch");
+    }
     pnol_dobj* deviceObjective(int n) override { return (host_only_ || n != d_->n) ? nullptr : d_; }
     void countEvals(long k) override { evals += k; }
     long evals = 0;
 
   private:
+    static bool device_points() {
+        const char* e = std::getenv("PNOL_DEVICE_POINTS");   // read per call (tests flip it)
+        return e && std::atoi(e) != 0;
+    }
     pnol_dobj* d_;
     bool host_only_;
     std::vector<double> p0_, p1_;
@@ -148,8 +161,19 @@ extern "C" {
 
 int pnol_run_bfgs(int which, pnol_dobj* obj, int host_eval, const double* p, int np, double* X, int n,
                   const double* Xlb, const double* Xub, pnol_result* res) {
-    if (!obj || !p || !X || n <= 0 || !res) return PNOL_ERR_ARG;
+    return pnol_run_bfgs_ex(which, obj, host_eval, p, np, X, n, Xlb, Xub, res, nullptr, 0, nullptr, nullptr);
+}
+
+int pnol_run_bfgs_ex(int which, pnol_dobj* obj, int host_eval, const double* p, int np, double* X, int n,
+                     const double* Xlb, const double* Xub, pnol_result* res, double* ftrace, int trace_cap,
+                     int* ntrace, double* profile) {
+    if (profile)
+        for (int k = 0; k < 8; ++k) profile[k] = 0.0;
+    if (!obj || !p || !X || n <= 0 || !res || trace_cap < 0 || (trace_cap > 0 && !ftrace)) return PNOL_ERR_ARG;
+    if (ntrace) *ntrace = 0;
     return guarded([&] {
+        std::vector<double> trace;
+        int iters = 0;
         DriverScalar o(obj, host_eval != 0);
         std::vector<double> x(X, X + n);
         double f0 = 0, fopt = 0;
@@ -159,7 +183,9 @@ int pnol_run_bfgs(int which, pnol_dobj* obj, int host_eval, const double* p, int
             b.setParams(p[0], p[1], p[2], p[3], (int)p[4], p[5], p[6], p[7], p[8], p[9], p[10] != 0, p[11] != 0);
             if (np > 12) b.setUpdateMode((int)p[12]);
             b.setObjPtr(o);
+            b.setProfile(profile);
             b.findMin(x, f0, fopt);
+            if (profile) iters = (int)profile[0];
         } else if (which == 1) {
             if (np < 12) throw std::runtime_error("BFGS_MPI needs 12 params");
             BFGS_MPI b;
@@ -176,8 +202,11 @@ int pnol_run_bfgs(int which, pnol_dobj* obj, int host_eval, const double* p, int
                         p[13] != 0, (int)p[14]);
             if (np > 15) b.setUpdateMode((int)p[15]);
             b.setObjPtr(o);
+            if (ftrace || ntrace) b.setFTrace(&trace);
+            b.setProfile(profile);
             std::vector<double> lb(Xlb, Xlb + n), ub(Xub, Xub + n);
             b.findMinBnd(x, lb, ub, f0, fopt);
+            iters = b.getTotalIter();
         } else if (which == 3) {
             if (np < 14 || !Xlb || !Xub) throw std::runtime_error("BFGSBnd_MPI needs 14 params and bounds");
             BFGSBnd_MPI b;
@@ -202,10 +231,12 @@ int pnol_run_bfgs(int which, pnol_dobj* obj, int host_eval, const double* p, int
             throw std::runtime_error("unknown BFGS variant");
         }
         for (int i = 0; i < n; ++i) X[i] = x[i];
-        res->iters = 0;
+        res->iters = iters;
         res->evals = o.evals;
         res->f0 = f0;
         res->fopt = fopt;
+        for (int k = 0; k < (int)trace.size() && k < trace_cap; ++k) ftrace[k] = trace[k];
+        if (ntrace) *ntrace = (int)trace.size();
     });
 }
 

@@ -91,16 +91,27 @@ class LMDevice {
                   "fd_jacobian");
             obj->countEvals(cnt + 1);
         } else {
-            // host objective: the reference's column loop over this rank's tiles, one upload per tile
-            std::vector<double> F0(m_), FdX(m_), XdX(n_), blk((size_t)kFdTileCols * ldjt_, 0.0);
-            obj->objEval(X, F0);
+            // host objective: the reference's column loop over this rank's tiles, each tile's
+            // points handed to objEvalBatch at once, one upload per tile.  LevMarqMPI: the
+            // reference sums the zero-padded values over the ranks, which turns -0.0 into +0.0
+            // (PNOL_Objective.cpp:279-286) -- reproduced by the + 0.0 at P > 1
+            const double pad = P > 1 ? 0.0 : -0.0;   // v + (-0.0) == v for every v
+            std::vector<double> F0(m_), FdX((size_t)kFdTileCols * m_), pts((size_t)kFdTileCols * n_),
+                blk((size_t)kFdTileCols * ldjt_, 0.0);
+            obj->objEvalBatch(X.data(), 1, n_, F0.data(), m_);
+            for (double& v : F0) v = v + pad;
             for (size_t t = 0; t < st.size(); ++t) {
                 for (int q = 0; q < ct[t]; ++q) {
                     const int j = st[t] + q;
-                    XdX = X;
-                    XdX[j] = XdX[j] + dX[j];
-                    obj->objEval(XdX, FdX);
-                    for (int i = 0; i < m_; ++i) blk[(size_t)q * ldjt_ + i] = (FdX[i] - F0[i]) / dX[j];
+                    double* row = pts.data() + (size_t)q * n_;
+                    std::memcpy(row, X.data(), sizeof(double) * n_);
+                    row[j] = row[j] + dX[j];
+                }
+                obj->objEvalBatch(pts.data(), ct[t], n_, FdX.data(), m_);
+                for (int q = 0; q < ct[t]; ++q) {
+                    const int j = st[t] + q;
+                    const double* Fj = FdX.data() + (size_t)q * m_;
+                    for (int i = 0; i < m_; ++i) blk[(size_t)q * ldjt_ + i] = ((Fj[i] + pad) - F0[i]) / dX[j];
                 }
                 JT_.upload(blk.data(), (size_t)ct[t] * ldjt_, (size_t)st[t] * ldjt_);
             }
@@ -310,9 +321,11 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool s
         nrm = std::sqrt(seq_dot(Fn, Fn, (size_t)m));
         chiSq = nrm * nrm;
         if (chiSq >= chiSqPrev || chiSq != chiSq) {
+            // the reference prints lambda / lambdaFactor --> lambda before the multiply
+            // (LevenbergMarquardt.cpp:107-111, LevenbergMarquardtMPI.cpp:112-116)
             if (sharded ? (P.verbose >= 1 && loud) : (P.verbose > 1))
                 std::cout << "Step " << iter << " failed with chiSq = " << chiSq << ", chiSqPrev = " << chiSqPrev
-                          << ",  increasing lambda: " << lambda << " --> " << lambda * P.lambdaFactor << std::endl;
+                          << ",  increasing lambda: " << lambda / P.lambdaFactor << " --> " << lambda << std::endl;
             chiSq = chiSqPrev;
             lambda = lambda * P.lambdaFactor;
             ckpt = true;               // x_[s], F_[s] stand, and so do x_[s]'s checkpoints (the
@@ -386,7 +399,7 @@ void lm_solve(MultiObjective* obj, const LMParams& P, bool sharded, std::vector<
             const bool talk = sharded ? (P.verbose >= 1 && loud) : (P.verbose > 1);
             if (talk)
                 std::cout << "Step " << iter << " failed with chiSq = " << chiSq << ", chiSqPrev = " << chiSqPrev
-                          << ",  increasing lambda: " << lambda << " --> " << lambda * P.lambdaFactor << std::endl;
+                          << ",  increasing lambda: " << lambda / P.lambdaFactor << " --> " << lambda << std::endl;
             chiSq = chiSqPrev;
             X = Xprev;
             F = Fprev;

@@ -1,10 +1,16 @@
 // objective.cpp -- the finite-difference engine of the drop-in Objective / MultiObjective.
 //
-// Host objectives follow the reference loops (PNOL_Objective.cpp) point by point; device
-// objectives evaluate every point of a block in one launch.  The *MPI forms shard the
-// columns in contiguous ceil(n/P) blocks and assemble with one allgather (RCCL over xGMI
-// on GPU ranks) -- the reference's zero-padded Allreduce(SUM) is an allgather in disguise
-// (x + 0 = x), so the assembled result is bitwise the serial one for any rank count.
+// Host objectives follow the reference loops (PNOL_Objective.cpp) point by point, handed to
+// objEvalBatch in batches of independent points (the default batch is the objEval loop in the
+// reference's order); device objectives evaluate every point of a block in one launch.  The
+// *MPI forms shard the columns in contiguous ceil(n/P) blocks and assemble with one allgather
+// (RCCL over xGMI on GPU ranks) -- the reference's zero-padded Allreduce(SUM) of the function
+// values is an allgather in disguise: x + 0 = x for every x but -0.0, which the sum turns into
+// +0.0 at P > 1.  Host objectives' values get that same + 0.0 at P > 1 (zero_pad_sum) before
+// the differences are formed; the built-in device objectives never produce -0.0 (their sums
+// start from +0.0), so the result is the reference's bit for bit at every rank count.
+#include <algorithm>
+#include <climits>
 #include <cstring>
 
 #include "../pnol_comm.hpp"
@@ -15,28 +21,42 @@ using namespace pnol;
 
 namespace {
 
-// f at x + h_i e_i for i in [b, b+cnt) into out[0..cnt), host objective
-void host_points(Objective* o, std::vector<double>& X, std::vector<double>& dX, int b, int cnt, double* out) {
-    std::vector<double> XdX(X.size());
-    for (int q = 0; q < cnt; ++q) {
-        const int i = b + q;
-        XdX = X;
-        XdX[i] = XdX[i] + dX[i];
-        out[q] = o->objEval(XdX);
+// points per objEvalBatch call: about 32 MiB of point and result data
+int batch_points(int n, int per_out) {
+    const size_t per = sizeof(double) * ((size_t)n + (size_t)per_out);
+    const size_t cap = ((size_t)32 << 20) / (per ? per : 1);
+    return (int)std::max<size_t>(1, std::min<size_t>(cap, INT_MAX / 2));
+}
+
+// f(point_k) for k in [0, total) through objEvalBatch, the points formed by make(k, row)
+template <class Make>
+void batched_eval(Objective* o, int n, int total, Make&& make, double* out) {
+    const int chunk = std::min(total, batch_points(n, 1));
+    if (total <= 0) return;
+    std::vector<double> buf((size_t)chunk * n);
+    for (int k = 0; k < total; k += chunk) {
+        const int np = std::min(chunk, total - k);
+        for (int q = 0; q < np; ++q) make(k + q, buf.data() + (size_t)q * n);
+        o->objEvalBatch(buf.data(), np, n, out + k);
     }
 }
 
-// device FD gradient for coordinates [b, b+cnt); returns f0 and g[0..cnt)
+// the reference's FD points: k == 0 and base -> X; else X + h_i e_i, i = b + k - base
+void host_points(Objective* o, const std::vector<double>& X, const std::vector<double>& dX, int b, int cnt, bool base,
+                 double* out) {
+    const int n = (int)X.size();
+    batched_eval(o, n, cnt + (base ? 1 : 0), [&](int k, double* row) {
+        std::memcpy(row, X.data(), sizeof(double) * n);
+        if (base && k == 0) return;
+        const int i = b + k - (base ? 1 : 0);
+        row[i] = row[i] + dX[i];   // XdX[i] = XdX[i] + dX[i]
+    }, out);
+}
+
+// device FD gradient for coordinates [b, b+cnt) (one upload, one launch pair, one download)
 void device_gradient(pnol_dobj* d, const std::vector<double>& X, const std::vector<double>& h, int b, int cnt,
                      double* f0, double* g) {
-    pnol_ctx* ctx = require_ctx();
-    const int n = (int)X.size();
-    DevVec dx(ctx, n), dh(ctx, n), dg(ctx, cnt > 0 ? cnt : 1), df(ctx, 1);
-    dx.upload(X);
-    dh.upload(h);
-    check(pnol_fd_gradient_d(ctx, d, dx.get(), dh.get(), b, cnt, df.get(), dg.get()), "fd_gradient");
-    if (cnt > 0) dg.download(g, (size_t)cnt);
-    df.download(f0, 1);
+    check(pnol_fd_gradient(require_ctx(), d, X.data(), h.data(), b, cnt, f0, g), "fd_gradient");
 }
 
 // scatter a reduced vector into the full one (objEvalRecur's mapping, PNOL_Objective.cpp:311-323)
@@ -48,9 +68,45 @@ std::vector<double> scatter_full(const std::vector<double>& Xr, const std::vecto
     return X;
 }
 
+// full index of every free (reduced) coordinate
+std::vector<int> free_map(const std::vector<bool>& cI) {
+    std::vector<int> map;
+    for (size_t i = 0; i < cI.size(); ++i)
+        if (!cI[i]) map.push_back((int)i);
+    return map;
+}
+
+// Recur FD values on the host: objEvalRecur(X) (base) and objEvalRecur(X + dX_i e_i) for the
+// reduced coordinates [b, b+cnt), as full points (scatter(X + dX_i e_i) == scatter(X) with
+// entry map[i] replaced by X_i + dX_i) through objEvalBatch
+void host_points_recur(Objective* o, const std::vector<double>& X, const std::vector<double>& dX, int b, int cnt,
+                       const std::vector<double>& cX, const std::vector<bool>& cI, double* out) {
+    const std::vector<double> Xf = scatter_full(X, cX, cI);
+    const std::vector<int> map = free_map(cI);
+    const int nf = (int)Xf.size();
+    batched_eval(o, nf, cnt + 1, [&](int k, double* row) {
+        std::memcpy(row, Xf.data(), sizeof(double) * nf);
+        if (k == 0) return;
+        const int i = b + k - 1;
+        row[map[i]] = X[i] + dX[i];
+    }, out);
+}
+
+// what the reference's zero-padded MPI_Allreduce(SUM) returns for a value one rank owns:
+// v + 0.0 + ... + 0.0 = v, except -0.0 -> +0.0 (PNOL_Objective.cpp:147-148, 279-286); one rank: v
+inline double zero_pad_sum(double v, int P) { return P > 1 ? v + 0.0 : v; }
+
 }  // namespace
 
 // ---- Objective -------------------------------------------------------------------------------
+
+void Objective::objEvalBatch(const double* Xs, int nPts, int n, double* f) {
+    std::vector<double> X(n);
+    for (int k = 0; k < nPts; ++k) {
+        X.assign(Xs + (size_t)k * n, Xs + (size_t)(k + 1) * n);
+        f[k] = objEval(X);
+    }
+}
 
 void Objective::gradientApproximation(vector<double>& X, vector<double>& dX, vector<double>& dFdX) {
     const int N = (int)X.size();
@@ -61,28 +117,53 @@ void Objective::gradientApproximation(vector<double>& X, vector<double>& dX, vec
         countEvals(N + 1);
         return;
     }
-    const double F = objEval(X);
-    std::vector<double> FdX(N);
-    host_points(this, X, dX, 0, N, FdX.data());
-    for (int i = 0; i < N; ++i) dFdX[i] = (FdX[i] - F) / dX[i];
+    std::vector<double> v(N + 1);   // F (base, evaluated first as the reference does), then FdX_i
+    host_points(this, X, dX, 0, N, true, v.data());
+    const double F = v[0];
+    for (int i = 0; i < N; ++i) dFdX[i] = (v[i + 1] - F) / dX[i];
 }
 
 void Objective::hessianApproximation(vector<double>& X, vector<double>& dX, vector<vector<double>>& B) {
-    // PNOL_Objective.cpp:38-85 (3 evaluations per upper-triangle pair, mirrored)
+    // PNOL_Objective.cpp:38-85: F, then per upper-triangle pair (i <= j) the points
+    // X + h_i e_i, X + h_j e_j, X + h_i e_i + h_j e_j in that order (the triples batched)
     const int N = (int)X.size();
     B.assign(N, vector<double>(N, 0.0));
-    const double F = objEval(X);
-    vector<double> Xi(N), Xj(N), Xij(N);
+    double F = 0;
+    {
+        std::vector<double> Xc = X;
+        objEvalBatch(Xc.data(), 1, N, &F);
+    }
+    std::vector<std::pair<int, int>> pairs;
+    pairs.reserve((size_t)N * (N + 1) / 2);
     for (int i = 0; i < N; ++i)
-        for (int j = i; j < N; ++j) {
-            Xi = X; Xj = X; Xij = X;
-            Xi[i] = Xi[i] + dX[i];
-            Xj[j] = Xj[j] + dX[j];
-            Xij[i] = Xij[i] + dX[i];
-            Xij[j] = Xij[j] + dX[j];
-            const double Fi = objEval(Xi), Fj = objEval(Xj), Fij = objEval(Xij);
+        for (int j = i; j < N; ++j) pairs.push_back({i, j});
+    const int npairs = (int)pairs.size();
+    const int chunk = std::max(1, batch_points(N, 1) / 3);
+    std::vector<double> pts, f;
+    for (int p0 = 0; p0 < npairs; p0 += chunk) {
+        const int np = std::min(chunk, npairs - p0);
+        pts.assign((size_t)3 * np * N, 0.0);
+        f.assign((size_t)3 * np, 0.0);
+        for (int q = 0; q < np; ++q) {
+            const int i = pairs[p0 + q].first, j = pairs[p0 + q].second;
+            double* xi = pts.data() + (size_t)(3 * q) * N;
+            double* xj = xi + N;
+            double* xij = xj + N;
+            std::memcpy(xi, X.data(), sizeof(double) * N);
+            std::memcpy(xj, X.data(), sizeof(double) * N);
+            std::memcpy(xij, X.data(), sizeof(double) * N);
+            xi[i] = xi[i] + dX[i];
+            xj[j] = xj[j] + dX[j];
+            xij[i] = xij[i] + dX[i];
+            xij[j] = xij[j] + dX[j];
+        }
+        objEvalBatch(pts.data(), 3 * np, N, f.data());
+        for (int q = 0; q < np; ++q) {
+            const int i = pairs[p0 + q].first, j = pairs[p0 + q].second;
+            const double Fi = f[3 * q], Fj = f[3 * q + 1], Fij = f[3 * q + 2];
             B[i][j] = (Fij - Fi - Fj + F) / (dX[i] * dX[j]);
         }
+    }
     for (int i = 0; i < N; ++i)
         for (int j = 0; j < i; ++j) B[i][j] = B[j][i];
 }
@@ -94,15 +175,16 @@ void Objective::gradientApproximationMPI(vector<double>& X, vector<double>& dX, 
     block_range(N, P, r, &b, &cnt);
     const int per = (N + P - 1) / P;
     std::vector<double> mine(per > 0 ? per : 1, 0.0), all((size_t)P * (per > 0 ? per : 1), 0.0);
-    double F = 0;
     if (pnol_dobj* d = deviceObjective(N)) {
+        double F = 0;
         device_gradient(d, X, dX, b, cnt, &F, mine.data());
         countEvals(cnt + 1);
     } else {
-        F = objEval(X);   // the base point, redundantly on every rank (deterministic)
-        std::vector<double> FdX(cnt > 0 ? cnt : 1);
-        host_points(this, X, dX, b, cnt, FdX.data());
-        for (int q = 0; q < cnt; ++q) mine[q] = (FdX[q] - F) / dX[b + q];
+        // the base point redundantly on every rank (deterministic), then this rank's block
+        std::vector<double> v(cnt + 1);
+        host_points(this, X, dX, b, cnt, true, v.data());
+        const double F = zero_pad_sum(v[0], P);
+        for (int q = 0; q < cnt; ++q) mine[q] = (zero_pad_sum(v[q + 1], P) - F) / dX[b + q];
     }
     check(comm_allgather_host(nullptr, mine.data(), all.data(), (size_t)(per > 0 ? per : 1)), "allgather(gradient)");
     dFdX.resize(N);
@@ -123,9 +205,8 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
         // perturbed point equals the reference's scatter(X + dX_i e_i) bit for bit
         std::vector<double> Xf = scatter_full(X, constantX, constantIndicator);
         std::vector<double> hf(Xf.size(), 1.0);
-        std::vector<int> map;
-        for (size_t i = 0, ir = 0; i < constantX.size(); ++i)
-            if (!constantIndicator[i]) { map.push_back((int)i); hf[i] = dX[ir++]; }
+        const std::vector<int> map = free_map(constantIndicator);
+        for (int i = 0; i < N; ++i) hf[map[i]] = dX[i];
         std::vector<double> gf(Xf.size());
         double F = 0;
         device_gradient(d, Xf, hf, 0, (int)Xf.size(), &F, gf.data());
@@ -133,14 +214,9 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
         for (int i = 0; i < N; ++i) dFdX[i] = gf[map[i]];
         return;
     }
-    const double F = objEvalRecur(X, constantX, constantIndicator);
-    std::vector<double> XdX(N);
-    for (int i = 0; i < N; ++i) {
-        XdX = X;
-        XdX[i] = XdX[i] + dX[i];
-        const double FdX = objEvalRecur(XdX, constantX, constantIndicator);
-        dFdX[i] = (FdX - F) / dX[i];
-    }
+    std::vector<double> v(N + 1);
+    host_points_recur(this, X, dX, 0, N, constantX, constantIndicator, v.data());
+    for (int i = 0; i < N; ++i) dFdX[i] = (v[i + 1] - v[0]) / dX[i];
 }
 
 void Objective::gradientApproximationMPIRecur(vector<double>& X, vector<double>& dX, vector<double>& dFdX,
@@ -157,9 +233,8 @@ void Objective::gradientApproximationMPIRecur(vector<double>& X, vector<double>&
         // batched launch over that span (frozen coordinates inside it are evaluated and dropped)
         std::vector<double> Xf = scatter_full(X, constantX, constantIndicator);
         std::vector<double> hf(Xf.size(), 1.0);
-        std::vector<int> map;
-        for (size_t i = 0, ir = 0; i < constantX.size(); ++i)
-            if (!constantIndicator[i]) { map.push_back((int)i); hf[i] = dX[ir++]; }
+        const std::vector<int> map = free_map(constantIndicator);
+        for (int i = 0; i < N; ++i) hf[map[i]] = dX[i];
         if (cnt > 0) {
             const int f0i = map[b], span = map[b + cnt - 1] - f0i + 1;
             std::vector<double> gs(span);
@@ -169,14 +244,10 @@ void Objective::gradientApproximationMPIRecur(vector<double>& X, vector<double>&
         }
         countEvals(cnt + 1);
     } else {
-        const double F = objEvalRecur(X, constantX, constantIndicator);
-        std::vector<double> XdX(N);
-        for (int q = 0; q < cnt; ++q) {
-            const int i = b + q;
-            XdX = X;
-            XdX[i] = XdX[i] + dX[i];
-            mine[q] = (objEvalRecur(XdX, constantX, constantIndicator) - F) / dX[i];
-        }
+        std::vector<double> v(cnt + 1);
+        host_points_recur(this, X, dX, b, cnt, constantX, constantIndicator, v.data());
+        const double F = zero_pad_sum(v[0], P);
+        for (int q = 0; q < cnt; ++q) mine[q] = (zero_pad_sum(v[q + 1], P) - F) / dX[b + q];
     }
     check(comm_allgather_host(nullptr, mine.data(), all.data(), (size_t)per), "allgather(gradient recur)");
     dFdX.resize(N);
@@ -185,19 +256,44 @@ void Objective::gradientApproximationMPIRecur(vector<double>& X, vector<double>&
 
 // ---- MultiObjective --------------------------------------------------------------------------
 
+void MultiObjective::objEvalBatch(const double* Xs, int nPts, int n, double* F, int m) {
+    std::vector<double> X(n), Fk(m);
+    for (int k = 0; k < nPts; ++k) {
+        X.assign(Xs + (size_t)k * n, Xs + (size_t)(k + 1) * n);
+        objEval(X, Fk);
+        std::memcpy(F + (size_t)k * m, Fk.data(), sizeof(double) * m);
+    }
+}
+
 namespace {
 
-// JT block rows [b, b+cnt) (ld = m) of a host multi-objective; F0 the base residuals
+// JT block rows [b, b+cnt) (ld = m) of a host multi-objective; F0 the base residuals.  The
+// columns go to objEvalBatch in batches.
 void host_jacobian_block(MultiObjective* o, std::vector<double>& X, std::vector<double>& dX, int m, int b, int cnt,
-                         const std::vector<double>& F0, double* JT) {
-    std::vector<double> XdX(X.size()), FdX(m);
-    for (int q = 0; q < cnt; ++q) {
-        const int j = b + q;
-        XdX = X;
-        XdX[j] = XdX[j] + dX[j];
-        o->objEval(XdX, FdX);
-        for (int i = 0; i < m; ++i) JT[(size_t)q * m + i] = (FdX[i] - F0[i]) / dX[j];
+                         const std::vector<double>& F0, double* JT, int P = 1) {
+    const int n = (int)X.size();
+    const int chunk = std::max(1, std::min(cnt, batch_points(n, m)));
+    std::vector<double> pts((size_t)chunk * n), FdX((size_t)chunk * m);
+    for (int q0 = 0; q0 < cnt; q0 += chunk) {
+        const int np = std::min(chunk, cnt - q0);
+        for (int q = 0; q < np; ++q) {
+            double* row = pts.data() + (size_t)q * n;
+            std::memcpy(row, X.data(), sizeof(double) * n);
+            const int j = b + q0 + q;
+            row[j] = row[j] + dX[j];
+        }
+        o->objEvalBatch(pts.data(), np, n, FdX.data(), m);
+        for (int q = 0; q < np; ++q) {
+            const int j = b + q0 + q;
+            const double* Fj = FdX.data() + (size_t)q * m;
+            double* dst = JT + (size_t)(q0 + q) * m;
+            for (int i = 0; i < m; ++i) dst[i] = (zero_pad_sum(Fj[i], P) - zero_pad_sum(F0[i], P)) / dX[j];
+        }
     }
+}
+
+void base_residuals(MultiObjective* o, std::vector<double>& X, std::vector<double>& F) {
+    o->objEvalBatch(X.data(), 1, (int)X.size(), F.data(), (int)F.size());
 }
 
 void device_jacobian(pnol_dobj* d, const std::vector<double>& X, const std::vector<double>& h, int m, bool sharded,
@@ -231,7 +327,7 @@ void MultiObjective::gradientApproximation(vector<double>& X, vector<double>& dX
         countEvals(n + 1);
     } else {
         std::vector<double> F(m);
-        objEval(X, F);
+        base_residuals(this, X, F);
         host_jacobian_block(this, X, dX, m, 0, n, F, JT.data());
     }
     for (int i = 0; i < m; ++i)
@@ -253,8 +349,8 @@ void MultiObjective::gradientApproximationMPI(vector<double>& X, vector<double>&
         block_range(n, P, r, &b, &cnt);
         const int per = (n + P - 1) / P > 0 ? (n + P - 1) / P : 1;
         std::vector<double> F(m), mine((size_t)per * m, 0.0), all((size_t)P * per * m, 0.0);
-        objEval(X, F);   // base residuals, redundantly per rank
-        host_jacobian_block(this, X, dX, m, b, cnt, F, mine.data());
+        base_residuals(this, X, F);   // base residuals, redundantly per rank
+        host_jacobian_block(this, X, dX, m, b, cnt, F, mine.data(), P);
         check(comm_allgather_host(nullptr, mine.data(), all.data(), (size_t)per * m), "allgather(jacobian)");
         std::memcpy(JT.data(), all.data(), sizeof(double) * JT.size());
     }

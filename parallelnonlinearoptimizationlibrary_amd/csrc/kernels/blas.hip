@@ -385,18 +385,32 @@ __device__ __forceinline__ void pass_load(double2 (&d)[kGroup], const double* __
     }
 }
 
+// IDS: the stored D is diag(scale) (I when scale is null) and is synthesised, not read (the
+// first fold of a pending correction after a reset writes D without reading it: 8 n^2 bytes)
+__device__ __forceinline__ void pass_ident(double2 (&d)[kGroup], const double* __restrict__ scale, int r0, int colc,
+                                           int rlast) {
+#pragma unroll
+    for (int q = 0; q < kGroup; ++q) {
+        const int row = min(r0 + q, rlast);
+        const double dv = scale ? scale[row] : 1.0;
+        d[q].x = row == colc ? dv : 0.0;
+        d[q].y = row == colc + 1 ? dv : 0.0;
+    }
+}
+
 // Rows of a 256-row tile are visited in groups of 8 starting at a tile-dependent group
 // (rotation: concurrently running tiles read different HBM channels); the next group's
 // 16-byte loads are issued before the current group is reduced (register double buffer).
 // Row shard form (BFGS D row-sharded over the ranks): D holds rows [rb, re) of the n x n
 // matrix (rb a multiple of the row-tile height); row tiles, partial indices and outputs use global rows,
 // so every partial is the one the whole-matrix pass (rb = 0, re = n) would produce.
-template <bool PEND, bool WB, bool VEC>
+template <bool PEND, bool WB, bool VEC, bool IDS = false>
 __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ Dsh, long ldd, int n, int rb, int re, int prows,
                                                    const double* __restrict__ sp, const double* __restrict__ ap,
                                                    const double* __restrict__ bp, const double* __restrict__ y,
                                                    const double* __restrict__ g, double* __restrict__ part_u,
-                                                   double* __restrict__ part_v, double* __restrict__ part_w) {
+                                                   double* __restrict__ part_v, double* __restrict__ part_w,
+                                                   const double* __restrict__ id_scale = nullptr) {
     double* __restrict__ D = Dsh - (long)rb * ldd;   // global-row view (only rows [rb, re) touched)
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -424,12 +438,16 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ Dsh, lon
     const int ngroups = (r_end - r_begin + kGroup - 1) / kGroup;
     int grp = rt % ngroups;
     double2 cur[kGroup];
-    pass_load<VEC>(cur, D, ldd, n, r_begin + grp * kGroup, colc, r_end - 1);
+    if (IDS) pass_ident(cur, id_scale, r_begin + grp * kGroup, col, r_end - 1);
+    else pass_load<VEC>(cur, D, ldd, n, r_begin + grp * kGroup, colc, r_end - 1);
     for (int t = 0; t < ngroups; ++t) {
         const int r0 = r_begin + grp * kGroup;
         const int gnext = (grp + 1 == ngroups) ? 0 : grp + 1;
         double2 nxt[kGroup];
-        if (t + 1 < ngroups) pass_load<VEC>(nxt, D, ldd, n, r_begin + gnext * kGroup, colc, r_end - 1);
+        if (t + 1 < ngroups) {
+            if (IDS) pass_ident(nxt, id_scale, r_begin + gnext * kGroup, col, r_end - 1);
+            else pass_load<VEC>(nxt, D, ldd, n, r_begin + gnext * kGroup, colc, r_end - 1);
+        }
         double yr[kGroup], sr[kGroup], br[kGroup];
 #pragma unroll
         for (int q = 0; q < kGroup; ++q) {
@@ -653,12 +671,15 @@ int bfgs_pass_rows(int n) {
 
 int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p, const double* a_p,
                      const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
-                     double* v, int rb, int re, int (*pw_gather)(pnol_ctx*, double*, int, int)) {
+                     double* v, int rb, int re, int (*pw_gather)(pnol_ctx*, double*, int, int), int ident_src,
+                     const double* id_scale) {
     if (re < 0) re = n;
     const int prows = bfgs_pass_rows(n);
     if (!D || n <= 0 || ldd < n || rb < 0 || re > n || rb > re || (rb < re && rb % prows)) return PNOL_ERR_ARG;
     const bool pend = s_p != nullptr;
     if (pend && (!a_p || !b_p)) return PNOL_ERR_ARG;
+    // the identity source is only meaningful for a fold with write-back (the only caller)
+    if (ident_src && (!pend || !write_back)) return PNOL_ERR_ARG;
     const int ncolt = (n + kPassCols - 1) / kPassCols;
     const int nrowt = (n + prows - 1) / prows;
     const int nstrips = ncolt * 4;
@@ -681,7 +702,14 @@ int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p
 #define PNOL_PASS(PE, W, V)                                                                                        \
     hipLaunchKernelGGL((k_bfgs_pass<PE, W, V>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb, re, prows, s_p, a_p, b_p, y, \
                        g, P0, P1, P2)
-        if (vec) {
+        if (ident_src) {
+            if (vec)
+                hipLaunchKernelGGL((k_bfgs_pass<true, true, true, true>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb,
+                                   re, prows, s_p, a_p, b_p, y, g, P0, P1, P2, id_scale);
+            else
+                hipLaunchKernelGGL((k_bfgs_pass<true, true, false, true>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb,
+                                   re, prows, s_p, a_p, b_p, y, g, P0, P1, P2, id_scale);
+        } else if (vec) {
             if (pend && write_back) PNOL_PASS(true, true, true);
             else if (pend) PNOL_PASS(true, false, true);
             else if (write_back) PNOL_PASS(false, true, true);

@@ -95,6 +95,53 @@ __global__ __launch_bounds__(256) void k_scalar_fd_values(const double* __restri
     if (active) vals[p] = f;
 }
 
+// vals[k] = f(X_k) for the row-major points Xs (npts x n): a batch of single evaluations
+// (line-search trial points, pool entries).  One workgroup per point: the terms of a 2048-
+// coordinate chunk are formed in parallel into LDS, then one lane adds them in index order --
+// the objective's own sequential sum, so the host objEval's bits.
+constexpr int kEvChunk = 2048;
+template <int KIND>
+__global__ __launch_bounds__(256) void k_eval_batch(const double* __restrict__ Xs, int n,
+                                                    const double* __restrict__ p0, const double* __restrict__ p1,
+                                                    double power, double* __restrict__ vals) {
+    __shared__ double terms[kEvChunk];
+    const double* __restrict__ X = Xs + (long)blockIdx.x * n;
+    const int nt = KIND == PNOL_OBJ_ROSENBROCK ? n - 1 : n;   // Rosenbrock: k < n - 1
+    double f = 0.0;
+    for (int c0 = 0; c0 < nt; c0 += kEvChunk) {
+        const int len = min(kEvChunk, nt - c0);
+        for (int e = threadIdx.x; e < len; e += blockDim.x) {
+            const int i = c0 + e;
+            const double xi = X[i];
+            double t;
+            if (KIND == PNOL_OBJ_ROSENBROCK) {
+                const double a = X[i + 1] - xi * xi, u = 1.0 - xi;
+                t = 100.0 * (a * a) + u * u;
+            } else if (KIND == PNOL_OBJ_QUADRATIC) {
+                t = (0.5 * p0[i] * xi) * xi - p1[i] * xi;
+                if (i + 1 < n) t = t + (0.25 * xi) * X[i + 1];
+            } else {
+                t = power == 2.0 ? xi * xi : pow(xi, power);
+            }
+            terms[e] = t;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int e = 0;
+            for (; e + 8 <= len; e += 8) {
+                double t8[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) t8[q] = terms[e + q];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) f = f + t8[q];
+            }
+            for (; e < len; ++e) f = f + terms[e];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) vals[blockIdx.x] = f;
+}
+
 __global__ void k_scalar_fd_finish(const double* __restrict__ vals, const double* __restrict__ h, int i0, int cnt,
                                    double* __restrict__ f0, double* __restrict__ g) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -603,6 +650,26 @@ int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out) 
         default:
             return PNOL_ERR_UNSUPPORTED;
     }
+}
+
+int launch_eval_batch(pnol_ctx* ctx, pnol_dobj* o, const double* Xs, int npts, double* out) {
+    if (!o || !Xs || !out || npts < 0) return PNOL_ERR_ARG;
+    if (npts == 0) return PNOL_OK;
+    if (!is_scalar_kind(o->kind)) {   // residual kinds: F of each point, rows of out (npts x m)
+        for (int k = 0; k < npts; ++k) PNOL_CHECK(launch_dobj_eval(ctx, o, Xs + (size_t)k * o->n, out + (size_t)k * o->m));
+        return PNOL_OK;
+    }
+    const dim3 grid(npts), blk(256);
+    if (o->kind == PNOL_OBJ_ROSENBROCK)
+        hipLaunchKernelGGL((k_eval_batch<PNOL_OBJ_ROSENBROCK>), grid, blk, 0, ctx->stream, Xs, o->n, o->p0, o->p1,
+                           o->power, out);
+    else if (o->kind == PNOL_OBJ_POWER)
+        hipLaunchKernelGGL((k_eval_batch<PNOL_OBJ_POWER>), grid, blk, 0, ctx->stream, Xs, o->n, o->p0, o->p1,
+                           o->power, out);
+    else
+        hipLaunchKernelGGL((k_eval_batch<PNOL_OBJ_QUADRATIC>), grid, blk, 0, ctx->stream, Xs, o->n, o->p0, o->p1,
+                           o->power, out);
+    return launch_check();
 }
 
 // The row-panel k-major copy of a linear residual's A (objective data never changes after creation).

@@ -93,6 +93,10 @@ namespace pnol {
         if (s_ != PNOL_OK) return s_; \
     } while (0)
 
+// The context's pinned host staging buffer, at least `bytes` (<= 64 MiB; nullptr above that or
+// on failure).  One user at a time: callers copy in, copy through the stream and synchronise.
+void* pinned_stage(pnol_ctx* ctx, size_t bytes);
+
 // Returns a device scratch buffer of at least `bytes` for `key` (grows, keeps contents undefined).
 int ws_get(pnol_ctx* ctx, const char* key, size_t bytes, void** out);
 int ws_get_zeroed(pnol_ctx* ctx, const char* key, size_t bytes, void** out);
@@ -144,7 +148,8 @@ int launch_gemv_neg_slices(pnol_ctx* ctx, const double* A, int lda, long sstride
 int launch_bfgs_update_exact(pnol_ctx* ctx, double* D, int ldd, const double* y, const double* s, int n);
 int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p, const double* a_p,
                      const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
-                     double* v, int rb = 0, int re = -1, int (*pw_gather)(pnol_ctx*, double*, int, int) = nullptr);
+                     double* v, int rb = 0, int re = -1, int (*pw_gather)(pnol_ctx*, double*, int, int) = nullptr,
+                     int ident_src = 0, const double* id_scale = nullptr);
 int launch_set_identity(pnol_ctx* ctx, double* D, int ldd, int n, const double* scale, int rb = 0, int re = -1);
 int launch_add(pnol_ctx* ctx, const double* x, const double* y, double* z, int n);
 int launch_gather_sub(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub, double* Dsub,
@@ -165,6 +170,8 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
 
 int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
 int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
+// out[k] = f(Xs row k) (scalar kinds) or out rows = F(Xs row k) (residual kinds), k < npts
+int launch_eval_batch(pnol_ctx* ctx, pnol_dobj* o, const double* Xs, int npts, double* out);
 int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt,
                        double* f0, double* g);
 // ckpt: 1 = run the base-chain pass (F0 when compute_f0, prefix checkpoints), 0 = reuse the

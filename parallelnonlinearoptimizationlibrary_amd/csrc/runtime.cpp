@@ -352,6 +352,27 @@ pnol_ctx* default_ctx_or_null() {
     return g_default;
 }
 
+// Host <-> device copies of the solvers' small vectors (x, sigma, residuals): through a
+// pinned staging buffer, so the DMA engine copies directly instead of the runtime's pageable
+// bounce path.  Large copies (> 64 MiB) go direct.
+void* pinned_stage(pnol_ctx* ctx, size_t bytes) {
+    constexpr size_t kMaxStage = 64u << 20;
+    if (bytes > kMaxStage) return nullptr;
+    if (ctx->pinned_bytes < bytes) {
+        if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+        ctx->pinned = nullptr;
+        ctx->pinned_bytes = 0;
+        size_t cap = 64 * 1024;
+        while (cap < bytes) cap *= 2;
+        if (hipHostMalloc(&ctx->pinned, cap, hipHostMallocDefault) != hipSuccess) {
+            ctx->pinned = nullptr;
+            return nullptr;
+        }
+        ctx->pinned_bytes = cap;
+    }
+    return ctx->pinned;
+}
+
 }  // namespace pnol
 
 using namespace pnol;
@@ -495,31 +516,10 @@ int pnol_free(pnol_ctx* ctx, void* dptr) {
     return PNOL_OK;
 }
 
-// Host <-> device copies of the solvers' small vectors (x, sigma, residuals): through a
-// pinned staging buffer, so the DMA engine copies directly instead of the runtime's pageable
-// bounce path.  Large copies (> 64 MiB) go direct.
-static void* staging(pnol_ctx* ctx, size_t bytes) {
-    constexpr size_t kMaxStage = 64u << 20;
-    if (bytes > kMaxStage) return nullptr;
-    if (ctx->pinned_bytes < bytes) {
-        if (ctx->pinned) (void)hipHostFree(ctx->pinned);
-        ctx->pinned = nullptr;
-        ctx->pinned_bytes = 0;
-        size_t cap = 64 * 1024;
-        while (cap < bytes) cap *= 2;
-        if (hipHostMalloc(&ctx->pinned, cap, hipHostMallocDefault) != hipSuccess) {
-            ctx->pinned = nullptr;
-            return nullptr;
-        }
-        ctx->pinned_bytes = cap;
-    }
-    return ctx->pinned;
-}
-
 int pnol_memcpy_h2d(pnol_ctx* ctx, void* dst, const void* src, size_t bytes) {
     if (!ctx || (!dst && bytes) || (!src && bytes)) return PNOL_ERR_ARG;
     if (!bytes) return PNOL_OK;
-    if (void* st = staging(ctx, bytes)) {
+    if (void* st = pinned_stage(ctx, bytes)) {
         std::memcpy(st, src, bytes);
         PNOL_HIP(hipMemcpyAsync(dst, st, bytes, hipMemcpyHostToDevice, ctx->stream));
     } else {
@@ -532,7 +532,7 @@ int pnol_memcpy_h2d(pnol_ctx* ctx, void* dst, const void* src, size_t bytes) {
 int pnol_memcpy_d2h(pnol_ctx* ctx, void* dst, const void* src, size_t bytes) {
     if (!ctx || (!dst && bytes) || (!src && bytes)) return PNOL_ERR_ARG;
     if (!bytes) return PNOL_OK;
-    if (void* st = staging(ctx, bytes)) {
+    if (void* st = pinned_stage(ctx, bytes)) {
         PNOL_HIP(hipMemcpyAsync(st, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
         PNOL_HIP(hipStreamSynchronize(ctx->stream));
         std::memcpy(dst, st, bytes);

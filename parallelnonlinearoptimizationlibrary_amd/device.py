@@ -251,18 +251,33 @@ def to_sliced(JT, mS):
     return out
 
 
-def run_bfgs(obj: DeviceObjective, x0, params, which=0, host_eval=False, lb=None, ub=None):
-    """Run the C++ drop-in BFGS (0), BFGS_MPI (1) or BFGS_Bnd (2) on a device objective."""
+PROFILE_KEYS = ("iterations", "total_s", "fd_gradient_s", "line_search_s", "update_s", "line_search_points",
+                "gradient_calls", "max_recursion_depth")
+
+
+def run_bfgs(obj: DeviceObjective, x0, params, which=0, host_eval=False, lb=None, ub=None, trace_cap=0,
+             profile=None):
+    """Run the C++ drop-in BFGS (0), BFGS_MPI (1), BFGS_Bnd (2), BFGSBnd_MPI (3) or
+    BFGS_Bnd_MPI_SW (4) on a device objective.  Returns (X, result), plus BFGS_Bnd's F after
+    every iteration (numpy array) when trace_cap > 0.  A dict passed as `profile` receives the
+    per-phase times and counts (PROFILE_KEYS)."""
     X = np.array(x0, dtype=np.float64)
     p = np.array(params, dtype=np.float64)
     res = L.Result()
-    lbp = _dptr(np.ascontiguousarray(lb, dtype=np.float64)) if lb is not None else None
-    ubp = _dptr(np.ascontiguousarray(ub, dtype=np.float64)) if ub is not None else None
     lba = np.ascontiguousarray(lb, dtype=np.float64) if lb is not None else None
     uba = np.ascontiguousarray(ub, dtype=np.float64) if ub is not None else None
-    L.check(L.lib().pnol_run_bfgs(which, obj.h, int(host_eval), _dptr(p), p.size, _dptr(X), X.size,
-                                  _dptr(lba) if lba is not None else lbp, _dptr(uba) if uba is not None else ubp,
-                                  C.byref(res)), "pnol_run_bfgs")
+    tr = np.zeros(max(trace_cap, 1))
+    nt = C.c_int(0)
+    prof = np.zeros(8)
+    L.check(L.lib().pnol_run_bfgs_ex(which, obj.h, int(host_eval), _dptr(p), p.size, _dptr(X), X.size,
+                                     _dptr(lba) if lba is not None else None,
+                                     _dptr(uba) if uba is not None else None, C.byref(res),
+                                     _dptr(tr) if trace_cap > 0 else None, trace_cap, C.byref(nt),
+                                     _dptr(prof) if profile is not None else None), "pnol_run_bfgs")
+    if profile is not None:
+        profile.update(zip(PROFILE_KEYS, prof.tolist()))
+    if trace_cap > 0:
+        return X, res, tr[: min(nt.value, trace_cap)]
     return X, res
 
 

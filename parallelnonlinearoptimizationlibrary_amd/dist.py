@@ -31,6 +31,12 @@ def init_rccl(ctx, rank: int, world: int):
     dist.broadcast(t, src=0)
     raw = bytes(t.cpu().tolist())
     L.check(L.lib().pnol_comm_init_rccl(ctx.h, world, rank, raw), "pnol_comm_init_rccl")
+    n, r = C.c_int(), C.c_int()
+    L.check(L.lib().pnol_comm_size(C.byref(n), C.byref(r)), "pnol_comm_size")
+    if rank == 0:
+        import sys
+        print(f"[pnol_amd] RCCL communicator: {n.value} ranks", file=sys.stderr, flush=True)
+    return n.value
 
 
 class HostComm:

@@ -116,6 +116,59 @@ def test_fused_update_sequence_matches_reference_form(ctx, oracle):
     assert np.allclose(_np(Dt), Dref, rtol=1e-11, atol=1e-11 * np.abs(Dref).max())
 
 
+@pytest.mark.parametrize("n", [7, 300, 1030, 4097])
+@pytest.mark.parametrize("scaled", [False, True])
+def test_bfgs_pass_ident_equals_pass_on_identity(ctx, n, scaled):
+    """pnol_bfgs_pass_ident_d (the stored diagonal synthesised, not read) is bitwise the
+    write-back pass over a real identity / diag(scale): u, w, v and the written D."""
+    import ctypes as C
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import _ptr
+    rng = np.random.default_rng(n + 11 * scaled)
+    y, g = rng.standard_normal(n), rng.standard_normal(n)
+    sp, ap, bp = rng.standard_normal(n), rng.standard_normal(n), rng.standard_normal(n)
+    scale = rng.uniform(0.5, 2.0, n) if scaled else None
+    ld = n + (n & 1)
+    Dref = ctx.empty(n, ld)
+    ctx.set_identity(Dref[:, :n], ctx.tensor(scale) if scaled else None)
+    pend = (ctx.tensor(sp), ctx.tensor(ap), ctx.tensor(bp))
+    yt, gt = ctx.tensor(y), ctx.tensor(g)
+    u0, w0, v0 = (_np(t) for t in ctx.bfgs_pass(Dref[:, :n], yt, gt, pend, True))
+    Dids = ctx.tensor(np.full((n, ld), np.nan))   # never read: NaN garbage must not leak in
+    u1, w1, v1 = ctx.empty(n), ctx.empty(n), ctx.empty(n)
+    st = ctx.tensor(scale) if scaled else None
+    L.check(L.lib().pnol_bfgs_pass_ident_d(ctx.h, _ptr(Dids), ld, n, _ptr(st), _ptr(pend[0]), _ptr(pend[1]),
+                                           _ptr(pend[2]), _ptr(yt), _ptr(gt), _ptr(u1), _ptr(w1), _ptr(v1)),
+            "pnol_bfgs_pass_ident_d")
+    assert np.array_equal(_np(u1), u0) and np.array_equal(_np(w1), w0) and np.array_equal(_np(v1), v0)
+    assert np.array_equal(_np(Dids)[:, :n], _np(Dref)[:, :n])
+
+
+@pytest.mark.parametrize("n", [4096, 8192])
+def test_fused_pass_vs_oracle_rank2_form_large(ctx, oracle, n):
+    """Two BFGS updates through the fused pass (lazy pending correction, folded with
+    write-back) vs the oracle's rank-2 restatement of updateHessianInv at the cfg-2 / north-star
+    sizes (the O(n^3) reference form is checked against the rank-2 one at n <= 257 above).
+    Tolerance: both sum the same terms in different orders -- 1e-12 of max|D| per entry."""
+    rng = np.random.default_rng(n)
+    D0 = np.eye(n) + 1e-3 * rng.standard_normal((n, n))
+    Dt = ctx.tensor(D0)
+    Dref = D0.copy()
+    pend = None
+    for it in range(2):
+        y = rng.standard_normal(n); s = rng.standard_normal(n) + 0.5 * y
+        u, w, _ = (_np(t) for t in ctx.bfgs_pass(Dt, ctx.tensor(y), None, pend, pend is not None))
+        rho = 1 / oracle.lib().orc_util_dot(oracle.ptr(y), oracle.ptr(s), n)
+        beta = np.dot(y, u); c = rho * rho * beta + rho
+        a = c * s - rho * w; b = -rho * u
+        pend = (ctx.tensor(s), ctx.tensor(a), ctx.tensor(b))
+        Dref = oracle.update_hessian_inv_rank2(Dref, y, s)
+    ctx.bfgs_pass(Dt, None, None, pend, True)
+    got = _np(Dt)
+    err = np.abs(got - Dref).max() / np.abs(Dref).max()
+    assert err <= 1e-12, err
+
+
 def test_set_identity(ctx):
     Dt = ctx.tensor(np.full((9, 9), 3.0))
     ctx.set_identity(Dt)

@@ -298,3 +298,127 @@ def test_bfgs_quadratic_fast_mode(ctx, oracle, n):
     # O(n^3) update, so the two runs stop at different points inside the FD-limited basin
     # (gtol 1e-6 with h = 1e-6); both sit within O(h) of x*.  Measured 3.9e-5 at n = 1000.
     assert rel(X, Xo) <= 2e-4
+
+
+# ---- config 5: BFGS_Bnd on the bounded quadratic (SURVEY 8(d) cfg 5) ----------------------
+CFG5_P = [1e-4, 0.8, 1e-6, 1, 1e-10, 2, 50, 1e-5, 1e-6, 1e-3, 200, 1e-5, 1e-5, 0, -1]   # testBFGSBnd, Examples.cpp:75
+
+
+def _box_qp_solution(d, b, lb, ub, sweeps=400):
+    """The exact minimiser of the cfg-5 quadratic over the box: f = sum 0.5 d x^2 - b x +
+    0.25 x_i x_{i+1} has the tridiagonal, strictly diagonally dominant Hessian diag(d) +
+    0.25 (off-diagonals), so projected red-black Gauss-Seidel converges linearly (factor
+    <= 0.5 / min d = 0.5 per sweep) to the unique KKT point."""
+    n = len(d)
+    x = np.zeros(n)
+    for _ in range(sweeps):
+        for par in (0, 1):
+            i = np.arange(par, n, 2)
+            nb = np.zeros(len(i))
+            nb += np.where(i + 1 < n, x[np.minimum(i + 1, n - 1)], 0.0)
+            nb += np.where(i - 1 >= 0, x[np.maximum(i - 1, 0)], 0.0)
+            x[i] = np.clip((b[i] - 0.25 * nb) / d[i], lb[i], ub[i])
+    return x
+
+
+def _quad_grad(d, b, x):
+    return d * x - b + 0.25 * (np.r_[x[1:], 0.0] + np.r_[0.0, x[:-1]])
+
+
+@pytest.mark.parametrize("n", [200, 500, 1000])
+def test_bfgs_bnd_fast_mode_cfg5_matches_oracle(ctx, oracle, n):
+    """Serial BFGS_Bnd in fast mode (n > PNOL_SEQ_MAX: lazy rank-2 passes, the diagonal-D
+    shortcuts, one borrowed device buffer for the whole active-set recursion) on the cfg-5
+    quadratic (b x 4, box [-0.5, 0.5]^n, x0 = 0, testBFGSBnd params): about 70% of the
+    coordinates end on a bound, each frozen by boundaryAssessment one level deeper.  Checked
+    against the oracle's BFGS_Bnd with the rank-2 update form (the O(n^3) form agrees with it
+    to 6e-17 at n = 200 / 300, tests/test_oracle_golden.py).  The device pass sums in another
+    order, so the last reduced problem stops at a slightly different point inside the gradient
+    tolerance (minGrad2Norm 1e-5 with FD steps of 1e-6): X is compared within 2e-6 (absolute,
+    |X| <= 0.5; measured 4.3e-7 at n = 500), F within 1e-10 relative, the active set exactly,
+    the iteration and evaluation counts within 5% (the recursion path is the same)."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective, run_bfgs
+    dd, bb = oracle.quadratic_data(n, bscale=4.0)
+    lb, ub = np.full(n, -0.5), np.full(n, 0.5)
+    X, res, tr = run_bfgs(DeviceObjective(ctx, L.OBJ_QUADRATIC, n, 0, dd, bb), np.zeros(n), CFG5_P, which=2,
+                          lb=lb, ub=ub, trace_cap=100000)
+    Xo, reso, tro, depth = oracle.bfgs_bnd_findmin_ex(oracle.Obj(oracle.QUADRATIC, n, 0, dd, bb), np.zeros(n),
+                                                      lb, ub, CFG5_P, rank2=True, trace_cap=100000)
+    assert depth > n // 2                      # the recursion really is one level per bound
+    assert np.all(X >= lb) and np.all(X <= ub)
+    act = lambda x: (np.abs(x - lb) < 1e-5).astype(int) - (np.abs(x - ub) < 1e-5).astype(int)
+    assert np.array_equal(act(X), act(Xo))
+    info = (np.max(np.abs(X - Xo)), res.fopt, reso.fopt, res.iters, reso.iters, res.evals, reso.evals)
+    assert np.max(np.abs(X - Xo)) <= 2e-6, info
+    assert abs(res.fopt - reso.fopt) <= 1e-10 * abs(reso.fopt), info
+    assert abs(res.iters - reso.iters) <= 0.05 * reso.iters and abs(res.evals - reso.evals) <= 0.05 * reso.evals, info
+    assert len(tr) == res.iters and np.all(np.diff(tr) <= 0)
+    xs = _box_qp_solution(dd, bb, lb, ub)
+    assert np.max(np.abs(X - xs)) <= 1e-4
+
+
+def test_bfgs_bnd_cfg5_full_size_properties(ctx):
+    """Config 5 at full size, n = 16384 (D = 2.15 GB on the device): the bounded quadratic with
+    data generated in HBM.  The oracle's update is O(n^2) per iteration over ~11k recursion
+    levels (hours on a CPU), so the run is checked by properties: every iterate inside the box,
+    F non-increasing along the trace, and X the box-constrained minimiser (the KKT point from
+    projected Gauss-Seidel on the exact tridiagonal Hessian) to within the FD gradient's
+    resolution (h = 1e-6, minGrad2Norm = 1e-5)."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective, run_bfgs
+    import oracle as O
+    n = 16384
+    obj = DeviceObjective.synthetic(ctx, L.OBJ_QUADRATIC, n, 0, bscale=4.0)
+    dd, bb = O.quadratic_data(n, bscale=4.0)        # the same splitmix64 stream (bitwise)
+    lb, ub = np.full(n, -0.5), np.full(n, 0.5)
+    X, res, tr = run_bfgs(obj, np.zeros(n), CFG5_P, which=2, lb=lb, ub=ub, trace_cap=1 << 20)
+    assert np.all(X >= lb) and np.all(X <= ub)
+    assert res.f0 == 0.0 and res.fopt < res.f0
+    assert len(tr) == res.iters and np.all(np.diff(tr) <= 0) and tr[-1] == res.fopt
+    xs = _box_qp_solution(dd, bb, lb, ub)
+    g = _quad_grad(dd, bb, X)
+    free = (X > lb + 1e-5) & (X < ub - 1e-5)
+    assert np.max(np.abs(g[free])) <= 1e-3
+    assert np.max(np.abs(X - xs)) <= 1e-3, np.max(np.abs(X - xs))
+    act = lambda x: (np.abs(x - lb) < 1e-5).astype(int) - (np.abs(x - ub) < 1e-5).astype(int)
+    assert np.mean(act(X) != act(xs)) <= 1e-3
+
+
+def test_trial_points_on_device_bitwise(ctx, oracle, monkeypatch):
+    """The line searches hand their trial points to objEvalBatch; PNOL_DEVICE_POINTS=1 makes
+    the driver objective evaluate every batch on the device (pnol_dobj_eval_batch: one
+    workgroup per point, the terms summed in index order).  The trajectories stay bitwise:
+    BFGS on 2-D Rosenbrock vs the recorded reference output, BFGS_MPI pools and BFGS_Bnd
+    (recursion, Recur scatter) vs the oracle."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_bfgs
+    monkeypatch.setenv("PNOL_DEVICE_POINTS", "1")
+    g = GOLD["bfgs_rosenbrock2_m12_1"]
+    X, res = run_bfgs(_obj(ctx, L.OBJ_ROSENBROCK, 2), g["x0"], g["params"])
+    assert X.tolist() == g["X"] and res.fopt == g["f"] and res.evals == g["evals"]
+    P = [1e-4, 0.1, 4, 1, 1000, 1e-7, 1e-3, 200, 1e-5, 1e-5, 0, 0]
+    Xo, _ = oracle.bfgs_mpi_findmin(oracle.rosenbrock(10), [10.0] * 10, P, 4)
+    X4, _ = run_bfgs(_obj(ctx, L.OBJ_ROSENBROCK, 10), [10.0] * 10, P + [4], which=1)
+    assert np.array_equal(X4, Xo)
+    Pb = [1e-4, 0.8, 1e-6, 1, 1e-10, 2, 50, 1e-5, 1e-6, 1e-3, 200, 1e-5, 1e-5, 0, -1]
+    x0, lb, ub = [0.0, 0.0, 0.0], [-2.0] * 3, [0.5] * 3
+    X, res = run_bfgs(_obj(ctx, L.OBJ_ROSENBROCK, 3), x0, Pb, which=2, lb=lb, ub=ub)
+    Xo, reso = oracle.bfgs_bnd_findmin(oracle.rosenbrock(3), x0, lb, ub, Pb)
+    assert np.array_equal(X, Xo) and res.evals == reso.evals
+
+
+def test_eval_batch_abi_bitwise(ctx, oracle):
+    """pnol_dobj_eval_batch on scalar kinds vs the oracle's objEval, point by point (n up to
+    5000 crosses the kernel's 2048-term LDS chunks)."""
+    import ctypes as C
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    rng = np.random.default_rng(3)
+    for kind, n, o in [(L.OBJ_ROSENBROCK, 7, oracle.rosenbrock(7)), (L.OBJ_ROSENBROCK, 5000, oracle.rosenbrock(5000)),
+                       (L.OBJ_QUADRATIC, 4097, oracle.quadratic(4097)), (L.OBJ_POWER, 300, oracle.power(300, 2))]:
+        d = _obj(ctx, kind, n, 0, o.p0, o.p1, 2.0)
+        Xs = np.ascontiguousarray(rng.uniform(-2, 2, (5, n)))
+        f = np.zeros(5)
+        dp = C.POINTER(C.c_double)
+        L.check(L.lib().pnol_dobj_eval_batch(ctx.h, d.h, Xs.ctypes.data_as(dp), 5, f.ctypes.data_as(dp)), "batch")
+        assert f.tolist() == [oracle.obj_eval(o, x) for x in Xs], (kind, n)

@@ -182,3 +182,28 @@ def test_bfgs_bnd_mpi_sw_oracle_properties(oracle):
         X, res = oracle.bfgs_bnd_mpi_sw_findmin(oracle.rosenbrock(3), x0, lb, ub, P, procs)
         np.testing.assert_allclose(X, 1.0, atol=1e-3)
         assert res.fopt < 1e-6
+
+
+@pytest.mark.parametrize("n", [200, 300])
+def test_bfgs_bnd_rank2_form_tracks_reference_form_cfg5(oracle, n):
+    """The oracle's BFGS_Bnd with updateHessianInv in its rank-2 form (used as the checker at
+    the cfg-5 sizes where the O(n^3) reference form is too slow) follows the reference form's
+    trajectory on the cfg-5 quadratic: same iterations, evaluations and active set, X within
+    1e-15.  Also pins the recursion depth (one level per coordinate frozen at a bound), the
+    monotone F trace and the KKT point."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_gpu_solvers import CFG5_P, _box_qp_solution
+    d, b = oracle.quadratic_data(n, bscale=4.0)
+    lb, ub = np.full(n, -0.5), np.full(n, 0.5)
+    o1, o2 = oracle.Obj(oracle.QUADRATIC, n, 0, d, b), oracle.Obj(oracle.QUADRATIC, n, 0, d, b)
+    X1, r1, t1, dep1 = oracle.bfgs_bnd_findmin_ex(o1, np.zeros(n), lb, ub, CFG5_P, rank2=False, trace_cap=10000)
+    X2, r2, t2, dep2 = oracle.bfgs_bnd_findmin_ex(o2, np.zeros(n), lb, ub, CFG5_P, rank2=True, trace_cap=10000)
+    assert np.max(np.abs(X1 - X2)) <= 1e-15
+    assert (r1.iters, r1.evals, dep1) == (r2.iters, r2.evals, dep2)
+    Xp, rp = oracle.bfgs_bnd_findmin(oracle.Obj(oracle.QUADRATIC, n, 0, d, b), np.zeros(n), lb, ub, CFG5_P)
+    assert np.array_equal(Xp, X1) and rp.evals == r1.evals       # _ex(rank2=0) is findMinBnd
+    nb = int(np.sum(np.abs(X1 - lb) < 1e-5) + np.sum(np.abs(X1 - ub) < 1e-5))
+    assert nb <= dep1 <= nb + n // 50   # a coordinate frozen on the way down can end free
+    assert len(t1) == r1.iters and np.all(np.diff(t1) <= 0)
+    assert np.max(np.abs(X1 - _box_qp_solution(d, b, lb, ub))) <= 1e-4
