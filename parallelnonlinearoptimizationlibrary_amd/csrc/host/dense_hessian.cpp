@@ -1,6 +1,7 @@
 // dense_hessian.cpp -- see dense_hessian.hpp.
 #include "dense_hessian.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 
@@ -21,9 +22,6 @@ void DenseInverseHessian::init(int mode, bool shard) {
         sharded_ = true;
         check(pnol_bfgs_rows(n_, comm_size(), comm_rank(), &rb_, &rc_), "bfgs_rows");
     }
-    y_.reset(ctx_, n_); s_.reset(ctx_, n_); g_.reset(ctx_, n_);
-    u_.reset(ctx_, n_); w_.reset(ctx_, n_); v_.reset(ctx_, n_);
-    if (!exact_) { ps_.reset(ctx_, n_); pa_.reset(ctx_, n_); pb_.reset(ctx_, n_); }
 }
 
 DenseInverseHessian::DenseInverseHessian(pnol_ctx* ctx, int n, int mode, bool shard)
@@ -32,6 +30,8 @@ DenseInverseHessian::DenseInverseHessian(pnol_ctx* ctx, int n, int mode, bool sh
     cap_ = (size_t)(rc_ > 0 ? rc_ : 1) * ld_;
     D_.reset(ctx, cap_);
     Dp_ = D_.get();
+    io_.reset(ctx_, (size_t)kSlots * n_);
+    iop_ = io_.get();
     dev_ok_ = false;   // contents undefined until setIdentity / setMatrix
 }
 
@@ -47,6 +47,12 @@ DenseInverseHessian::DenseInverseHessian(DenseInverseHessian& parent, int n, int
         cap_ = need;
         D_.reset(ctx_, cap_);
         Dp_ = D_.get();
+    }
+    if (n_ <= parent.n_ && parent.iop_) {
+        iop_ = parent.iop_;
+    } else {
+        io_.reset(ctx_, (size_t)kSlots * n_);
+        iop_ = io_.get();
     }
     dev_ok_ = false;
 }
@@ -139,8 +145,19 @@ void DenseInverseHessian::setSubmatrixOf(DenseInverseHessian& src, const std::ve
     clobbered_ = false;
 }
 
+void DenseInverseHessian::uploadPending() {
+    if (!pending_ || pend_dev_) return;
+    std::vector<double> sab(3 * (size_t)n_);   // s_p | a_p | b_p in one copy
+    std::copy(hs_.begin(), hs_.end(), sab.begin());
+    std::copy(ha_.begin(), ha_.end(), sab.begin() + n_);
+    std::copy(hb_.begin(), hb_.end(), sab.begin() + 2 * n_);
+    up(kPS, sab.data(), sab.size());
+    pend_dev_ = true;
+}
+
 int DenseInverseHessian::pass(const double* sp, const double* ap, const double* bp, int wb, const double* y,
                               const double* g, double* u, double* w, double* v) {
+    if (sp) uploadPending();
     ensureDevice();
     if (sharded_) return pnol_bfgs_pass_mpi_d(ctx_, Dp_, ld_, n_, sp, ap, bp, wb, y, g, u, w, v);
     return pnol_bfgs_pass_d(ctx_, Dp_, ld_, n_, sp, ap, bp, wb, y, g, u, w, v);
@@ -149,9 +166,10 @@ int DenseInverseHessian::pass(const double* sp, const double* ap, const double* 
 // fold the pending correction into a stored diagonal without reading it
 int DenseInverseHessian::passIdent(const double* y, const double* g, double* u, double* w, double* v) {
     if (clobbered_) throw std::runtime_error("DenseInverseHessian: D used while lent to a reduced problem");
+    uploadPending();
     const double* scale = deviceScale();
-    int st = sharded_ ? pnol_bfgs_pass_ident_mpi_d(ctx_, Dp_, ld_, n_, scale, ps_.get(), pa_.get(), pb_.get(), y, g, u, w, v)
-                      : pnol_bfgs_pass_ident_d(ctx_, Dp_, ld_, n_, scale, ps_.get(), pa_.get(), pb_.get(), y, g, u, w, v);
+    int st = sharded_ ? pnol_bfgs_pass_ident_mpi_d(ctx_, Dp_, ld_, n_, scale, slot(kPS), slot(kPA), slot(kPB), y, g, u, w, v)
+                      : pnol_bfgs_pass_ident_d(ctx_, Dp_, ld_, n_, scale, slot(kPS), slot(kPA), slot(kPB), y, g, u, w, v);
     ident_ = false;
     dev_ok_ = true;
     return st;
@@ -159,9 +177,9 @@ int DenseInverseHessian::passIdent(const double* y, const double* g, double* u, 
 
 void DenseInverseHessian::materialize() {
     if (!pending_) return;
-    if (ident_) check(passIdent(nullptr, nullptr, u_.get(), w_.get(), v_.get()), "bfgs_pass(materialize)");
+    if (ident_) check(passIdent(nullptr, nullptr, slot(kU), slot(kW), slot(kV)), "bfgs_pass(materialize)");
     else
-        check(pass(ps_.get(), pa_.get(), pb_.get(), 1, nullptr, nullptr, u_.get(), w_.get(), v_.get()),
+        check(pass(slot(kPS), slot(kPA), slot(kPB), 1, nullptr, nullptr, slot(kU), slot(kW), slot(kV)),
               "bfgs_pass(materialize)");
     pending_ = false;
 }
@@ -202,20 +220,20 @@ void DenseInverseHessian::direction(const std::vector<double>& g, std::vector<do
         for (int i = 0; i < n_; ++i) p[i] = -(v[i] + hs_[i] * ag + hb_[i] * sg);
         return;
     }
-    g_.upload(g);
+    up(kG, g.data(), (size_t)n_);
     if (!pending_) {
         ensureDevice();
-        if (sharded_) check(pnol_hg_mpi_d(ctx_, Dp_, ld_, g_.get(), v_.get(), n_), "hg");
-        else check(pnol_hg_d(ctx_, Dp_, ld_, g_.get(), v_.get(), n_), "hg");
-        v_.download(p);   // v = -D g
+        if (sharded_) check(pnol_hg_mpi_d(ctx_, Dp_, ld_, slot(kG), slot(kV), n_), "hg");
+        else check(pnol_hg_d(ctx_, Dp_, ld_, slot(kG), slot(kV), n_), "hg");
+        down(kV, p.data(), (size_t)n_);   // v = -D g
         return;
     }
     // read-only pass over the stored D, then fold the pending correction in algebraically:
     // (D + s a^T + b s^T) g = D g + s (a.g) + b (s.g)
-    check(pass(nullptr, nullptr, nullptr, 0, nullptr, g_.get(), u_.get(), w_.get(), v_.get()),
+    check(pass(nullptr, nullptr, nullptr, 0, nullptr, slot(kG), slot(kU), slot(kW), slot(kV)),
           "bfgs_pass(direction)");
     std::vector<double> v(n_);
-    v_.download(v);
+    down(kV, v.data(), (size_t)n_);
     const double ag = seq_dot(ha_, g), sg = seq_dot(hs_, g);
     for (int i = 0; i < n_; ++i) p[i] = -(v[i] + hs_[i] * ag + hb_[i] * sg);
 }
@@ -224,9 +242,11 @@ void DenseInverseHessian::update(const std::vector<double>& y, const std::vector
                                  const std::vector<double>* gnext, std::vector<double>* pnext) {
     if (exact_) {
         ensureDevice();
-        y_.upload(y);
-        s_.upload(s);
-        check(pnol_bfgs_update_exact_d(ctx_, Dp_, ld_, y_.get(), s_.get(), n_), "bfgs_update_exact");
+        std::vector<double> ys(2 * (size_t)n_);
+        std::copy(y.begin(), y.end(), ys.begin());
+        std::copy(s.begin(), s.end(), ys.begin() + n_);
+        up(kY, ys.data(), ys.size());   // y | s
+        check(pnol_bfgs_update_exact_d(ctx_, Dp_, ld_, slot(kY), slot(kG), n_), "bfgs_update_exact");
         ident_ = false;
         if (gnext && pnext) direction(*gnext, *pnext);
         return;
@@ -239,19 +259,23 @@ void DenseInverseHessian::update(const std::vector<double>& y, const std::vector
         if (gnext)
             for (int i = 0; i < n_; ++i) v[i] = 0.0 + sc(i) * (*gnext)[i];
     } else {
-        y_.upload(y);
-        if (gnext) g_.upload(*gnext);
+        std::vector<double> yg((gnext ? 2 : 1) * (size_t)n_);
+        std::copy(y.begin(), y.end(), yg.begin());
+        if (gnext) std::copy(gnext->begin(), gnext->end(), yg.begin() + n_);
+        up(kY, yg.data(), yg.size());   // y | g
         // one pass: fold the pending correction in (write-back) and form D y, D^T y, D g_next
         if (pending_ && ident_)
-            check(passIdent(y_.get(), gnext ? g_.get() : nullptr, u_.get(), w_.get(), v_.get()), "bfgs_pass(update)");
+            check(passIdent(slot(kY), gnext ? slot(kG) : nullptr, slot(kU), slot(kW), slot(kV)), "bfgs_pass(update)");
         else
-            check(pass(pending_ ? ps_.get() : nullptr, pending_ ? pa_.get() : nullptr, pending_ ? pb_.get() : nullptr,
-                       pending_ ? 1 : 0, y_.get(), gnext ? g_.get() : nullptr, u_.get(), w_.get(), v_.get()),
+            check(pass(pending_ ? slot(kPS) : nullptr, pending_ ? slot(kPA) : nullptr, pending_ ? slot(kPB) : nullptr,
+                       pending_ ? 1 : 0, slot(kY), gnext ? slot(kG) : nullptr, slot(kU), slot(kW), slot(kV)),
                   "bfgs_pass(update)");
         if (pending_) ident_ = false;
-        u_.download(u);
-        w_.download(w);
-        if (gnext) v_.download(v);
+        std::vector<double> uwv((gnext ? 3 : 2) * (size_t)n_);
+        down(kU, uwv.data(), uwv.size());   // u | w | v
+        std::copy(uwv.begin(), uwv.begin() + n_, u.begin());
+        std::copy(uwv.begin() + n_, uwv.begin() + 2 * n_, w.begin());
+        if (gnext) std::copy(uwv.begin() + 2 * n_, uwv.end(), v.begin());
     }
     const double rho = 1 / seq_dot(y, s);
     const double beta = seq_dot(y, u);
@@ -261,10 +285,8 @@ void DenseInverseHessian::update(const std::vector<double>& y, const std::vector
     hb_.resize(n_);
     for (int j = 0; j < n_; ++j) ha_[j] = c * s[j] - rho * w[j];
     for (int i = 0; i < n_; ++i) hb_[i] = -rho * u[i];
-    ps_.upload(hs_);
-    pa_.upload(ha_);
-    pb_.upload(hb_);
     pending_ = true;
+    pend_dev_ = false;
     if (gnext && pnext) {
         const double ag = seq_dot(ha_, *gnext), sg = seq_dot(hs_, *gnext);
         pnext->resize(n_);

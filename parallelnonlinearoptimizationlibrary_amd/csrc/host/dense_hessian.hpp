@@ -79,11 +79,25 @@ class DenseInverseHessian {
     DevVec D_;                         // own storage (empty when borrowed)
     double* Dp_ = nullptr;             // the matrix: D_.get() or the lender's buffer
     size_t cap_ = 0;                   // doubles available at Dp_ (lent on to reduced problems)
-    DevVec y_, s_, g_, u_, w_, v_;     // staging vectors
-    DevVec ps_, pa_, pb_;              // pending correction (fast mode)
+    // staging vectors in one device block, so each group crosses PCIe in one copy:
+    // [y | g | u | w | v | s_p | a_p | b_p] (exact mode: s in the g slot)
+    // (lent down the recursion with D: the parent does not stage anything while it waits)
+    DevVec io_;
+    double* iop_ = nullptr;
+    double* slot(int k) const { return iop_ + (size_t)k * n_; }
+    void up(int k, const double* src, size_t count) {
+        check(pnol_memcpy_h2d(ctx_, slot(k), src, sizeof(double) * count), "h2d");
+    }
+    void down(int k, double* dst, size_t count) const {
+        check(pnol_memcpy_d2h(ctx_, dst, slot(k), sizeof(double) * count), "d2h");
+    }
+    enum { kY = 0, kG, kU, kW, kV, kPS, kPA, kPB, kSlots };
     DevVec dscale_;                    // device copy of the diagonal scale (lazy)
     bool pending_ = false;
+    bool pend_dev_ = false;            // the pending correction is uploaded (lazily: most reduced
+                                       // problems of the recursion never fold theirs)
     std::vector<double> hs_, ha_, hb_; // host copies of the pending correction
+    void uploadPending();
     bool ident_ = false;               // stored D == diag(hscale_) (empty: I)
     bool dev_ok_ = true;               // device memory holds the stored D
     bool clobbered_ = false;           // buffer lent to a reduced problem since the last reset

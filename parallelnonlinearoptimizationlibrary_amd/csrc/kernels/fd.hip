@@ -142,6 +142,120 @@ __global__ __launch_bounds__(256) void k_eval_batch(const double* __restrict__ X
     if (threadIdx.x == 0) vals[blockIdx.x] = f;
 }
 
+// ---- FD gradient of the scalar objectives, term form ------------------------------------
+// f = sum_k t_k is accumulated in k order; perturbing coordinate j changes at most the terms
+// touching x_j (Rosenbrock / quadratic: t_{j-1} and t_j; power: t_j).  So every point's sum is
+// the sequence of the base terms T_k = t_k(x) with those two replaced, and T is formed once
+// (k_scalar_terms).  A wave owns 64 consecutive points: outside the window of terms any of its
+// lanes perturbs, the addend T_k is the same for all lanes -- one scalar load feeding one
+// v_add_f64 per term; inside the window each lane forms its own perturbed terms exactly as the
+// objective does.  Same additions in the same order as evaluating each point from scratch
+// (bitwise), one dependent add per term on the critical path instead of the whole term.
+template <int KIND>
+__device__ __forceinline__ int scalar_nterms(int n) { return KIND == PNOL_OBJ_ROSENBROCK ? max(n - 1, 0) : n; }
+
+// term k at the point whose coordinates k, k + 1 are xk, xk1 (the objective's own expression)
+template <int KIND>
+__device__ __forceinline__ double scalar_term(int k, int n, double xk, double xk1, const double* __restrict__ p0,
+                                              const double* __restrict__ p1, double power) {
+    if (KIND == PNOL_OBJ_ROSENBROCK) {
+        const double t = xk1 - xk * xk, u = 1.0 - xk;   // ExampleObjectives.hpp:93-96
+        return 100.0 * (t * t) + u * u;
+    } else if (KIND == PNOL_OBJ_QUADRATIC) {
+        double t = (0.5 * p0[k] * xk) * xk - p1[k] * xk;
+        if (k + 1 < n) t = t + (0.25 * xk) * xk1;
+        return t;
+    } else {
+        return power == 2.0 ? xk * xk : pow(xk, power);
+    }
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void k_scalar_terms(const double* __restrict__ x, int n, const double* __restrict__ p0,
+                                                      const double* __restrict__ p1, double power,
+                                                      double* __restrict__ T) {
+    const int nt = scalar_nterms<KIND>(n);
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nt; k += gridDim.x * blockDim.x)
+        T[k] = scalar_term<KIND>(k, n, x[k], k + 1 < n ? x[k + 1] : 0.0, p0, p1, power);
+}
+
+// Points q in [0, cnt] (q == cnt: the base point): vals[q] = f(x + h_j e_j), j = i0 + q.
+// T streams through LDS in chunks (cooperative coalesced loads); the uniform addends are LDS
+// broadcast reads, which -- unlike scalar loads, whose completion order is not fixed -- stay
+// in flight eight at a time ahead of the dependent add chain.
+constexpr int kTermChunk = 2048;   // 16 KB of terms per LDS stage
+
+// f + Tc[k0] + Tc[k0 + 1] + ... + Tc[k1 - 1], left to right: the next eight LDS reads are in
+// flight while the current eight are added (register double buffer)
+__device__ __forceinline__ double chain_sum(double f, const double* __restrict__ Tc, int k0, int k1) {
+    int k = k0;
+    if (k1 - k >= 16) {
+        double cur[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cur[q] = Tc[k + q];
+        for (; k + 16 <= k1; k += 8) {
+            double nxt[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) nxt[q] = Tc[k + 8 + q];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f = f + cur[q];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) f = f + cur[q];
+        k += 8;
+    }
+    for (; k < k1; ++k) f = f + Tc[k];
+    return f;
+}
+template <int KIND>
+__global__ __launch_bounds__(256) void k_scalar_fd_chain(const double* __restrict__ x, const double* __restrict__ h,
+                                                         int n, int i0, int cnt, const double* __restrict__ p0,
+                                                         const double* __restrict__ p1, double power,
+                                                         const double* __restrict__ T, double* __restrict__ vals) {
+    __shared__ double Ts[kTermChunk];
+    const int lane = threadIdx.x & 63;
+    const int q0 = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 64);
+    const int q = q0 + lane;
+    const bool active = q <= cnt;
+    const int j = (active && q < cnt) ? i0 + q : -1;            // perturbed coordinate, -1: base
+    const double xj = j >= 0 ? x[j] + h[j] : 0.0;                 // XdX[j] = X[j] + dX[j]
+    const int nt = scalar_nterms<KIND>(n);
+    // terms some lane of the wave perturbs: [w0, w1) (empty for a wave of base / idle lanes)
+    const int jlo = i0 + q0, jhi = i0 + min(q0 + 63, cnt - 1);
+    int w0 = nt, w1 = nt;
+    if (q0 < cnt) {
+        w0 = max(0, min(KIND == PNOL_OBJ_POWER ? jlo : jlo - 1, nt));
+        w1 = max(w0, min(jhi + 1, nt));
+    }
+    double f = 0.0;
+    for (int c0 = 0; c0 < nt; c0 += kTermChunk) {
+        const int c1 = min(c0 + kTermChunk, nt);
+        __syncthreads();
+        for (int e = threadIdx.x; e < c1 - c0; e += blockDim.x) Ts[e] = T[c0 + e];
+        __syncthreads();
+        const double* __restrict__ Tc = Ts - c0;   // Tc[k] = T[k] for k in [c0, c1)
+        int k = c0;
+        const int e0 = min(max(w0, c0), c1);
+        f = chain_sum(f, Tc, k, e0);
+        k = e0;
+        const int e1 = min(max(w1, c0), c1);
+        for (; k < e1; ++k) {
+            double t = Tc[k];
+            const bool touch = j >= 0 && (k == j || (KIND != PNOL_OBJ_POWER && k + 1 == j));
+            if (touch) {
+                const double xk = k == j ? xj : x[k];
+                const double xk1 = k + 1 < n ? (k + 1 == j ? xj : x[k + 1]) : 0.0;
+                t = scalar_term<KIND>(k, n, xk, xk1, p0, p1, power);
+            }
+            f = f + t;
+        }
+        f = chain_sum(f, Tc, k, c1);
+    }
+    if (active) vals[q] = f;
+}
+
 __global__ void k_scalar_fd_finish(const double* __restrict__ vals, const double* __restrict__ h, int i0, int cnt,
                                    double* __restrict__ f0, double* __restrict__ g) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -613,19 +727,8 @@ int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out) 
     switch (o->kind) {
         case PNOL_OBJ_ROSENBROCK:
         case PNOL_OBJ_POWER:
-        case PNOL_OBJ_QUADRATIC: {
-            // evaluate the base point only: cnt = 0 -> vals[0] = f(x)
-            if (o->kind == PNOL_OBJ_ROSENBROCK)
-                hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_ROSENBROCK>), dim3(1), dim3(64), 0, ctx->stream, x, x, o->n, 0, 0,
-                                   o->p0, o->p1, o->power, out);
-            else if (o->kind == PNOL_OBJ_POWER)
-                hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_POWER>), dim3(1), dim3(64), 0, ctx->stream, x, x, o->n, 0, 0,
-                                   o->p0, o->p1, o->power, out);
-            else
-                hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_QUADRATIC>), dim3(1), dim3(64), 0, ctx->stream, x, x, o->n, 0, 0,
-                                   o->p0, o->p1, o->power, out);
-            return launch_check();
-        }
+        case PNOL_OBJ_QUADRATIC:
+            return launch_eval_batch(ctx, o, x, 1, out);   // one point: terms in parallel, summed in order
         case PNOL_OBJ_EXPCURVE:
             hipLaunchKernelGGL((k_multi_eval<PNOL_OBJ_EXPCURVE>), dim3((o->m + 255) / 256), dim3(256), 0, ctx->stream, x, o->n,
                                o->m, o->p0, o->p1, o->p2, out);
@@ -724,24 +827,49 @@ int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* 
 }
 
 
+template <int KIND>
+static int launch_fd_chain(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt, double* T,
+                           double* V) {
+    const int nt = std::max(o->n - (KIND == PNOL_OBJ_ROSENBROCK ? 1 : 0), 1);
+    hipLaunchKernelGGL((k_scalar_terms<KIND>), dim3(std::min((nt + 255) / 256, 1024)), dim3(256), 0, ctx->stream, x, o->n,
+                       o->p0, o->p1, o->power, T);
+    PNOL_CHECK(launch_check());
+    const int waves = (cnt + 1 + 63) / 64;
+    hipLaunchKernelGGL((k_scalar_fd_chain<KIND>), dim3((waves + 3) / 4), dim3(256), 0, ctx->stream, x, h, o->n, i0, cnt,
+                       o->p0, o->p1, o->power, (const double*)T, V);
+    return launch_check();
+}
+
 int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt, double* f0,
                        double* g) {
     if (!o || !x || !h || !is_scalar_kind(o->kind)) return PNOL_ERR_ARG;
     if (i0 < 0 || cnt < 0 || i0 + cnt > o->n) return PNOL_ERR_ARG;
-    void* vals = nullptr;
+    void *vals = nullptr, *terms = nullptr;
     PNOL_CHECK(ws_get(ctx, "fd_vals", sizeof(double) * (size_t)(cnt + 1), &vals));
-    const int blocks = (cnt + 1 + 255) / 256;
-    double* V = (double*)vals;
-    if (o->kind == PNOL_OBJ_ROSENBROCK)
-        hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_ROSENBROCK>), dim3(blocks), dim3(256), 0, ctx->stream, x, h, o->n, i0,
-                           cnt, o->p0, o->p1, o->power, V);
-    else if (o->kind == PNOL_OBJ_POWER)
-        hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_POWER>), dim3(blocks), dim3(256), 0, ctx->stream, x, h, o->n, i0, cnt,
-                           o->p0, o->p1, o->power, V);
-    else
-        hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_QUADRATIC>), dim3(blocks), dim3(256), 0, ctx->stream, x, h, o->n, i0,
-                           cnt, o->p0, o->p1, o->power, V);
-    PNOL_CHECK(launch_check());
+    PNOL_CHECK(ws_get(ctx, "fd_terms", sizeof(double) * (size_t)o->n, &terms));
+    double *V = (double*)vals, *T = (double*)terms;
+    // PNOL_FD_SCALAR=0: the point-per-thread form (every term recomputed; tuning / cross-check)
+    static const bool chain = [] {
+        const char* e = std::getenv("PNOL_FD_SCALAR");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (chain) {
+        if (o->kind == PNOL_OBJ_ROSENBROCK) PNOL_CHECK(launch_fd_chain<PNOL_OBJ_ROSENBROCK>(ctx, o, x, h, i0, cnt, T, V));
+        else if (o->kind == PNOL_OBJ_POWER) PNOL_CHECK(launch_fd_chain<PNOL_OBJ_POWER>(ctx, o, x, h, i0, cnt, T, V));
+        else PNOL_CHECK(launch_fd_chain<PNOL_OBJ_QUADRATIC>(ctx, o, x, h, i0, cnt, T, V));
+    } else {
+        const int blocks = (cnt + 1 + 255) / 256;
+        if (o->kind == PNOL_OBJ_ROSENBROCK)
+            hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_ROSENBROCK>), dim3(blocks), dim3(256), 0, ctx->stream, x, h,
+                               o->n, i0, cnt, o->p0, o->p1, o->power, V);
+        else if (o->kind == PNOL_OBJ_POWER)
+            hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_POWER>), dim3(blocks), dim3(256), 0, ctx->stream, x, h, o->n,
+                               i0, cnt, o->p0, o->p1, o->power, V);
+        else
+            hipLaunchKernelGGL((k_scalar_fd_values<PNOL_OBJ_QUADRATIC>), dim3(blocks), dim3(256), 0, ctx->stream, x, h,
+                               o->n, i0, cnt, o->p0, o->p1, o->power, V);
+        PNOL_CHECK(launch_check());
+    }
     hipLaunchKernelGGL(k_scalar_fd_finish, dim3((cnt + 255) / 256 + 1), dim3(256), 0, ctx->stream, (const double*)V, h, i0,
                        cnt, f0, g);
     return launch_check();

@@ -351,6 +351,31 @@ def test_fd_gradient_rosenbrock_bitwise(ctx, oracle, n):
     assert np.array_equal(_np(gb), oracle.fd_gradient(o, x, h)[i0:i0 + cnt])
 
 
+@pytest.mark.parametrize("kind", ["rosenbrock", "quadratic", "power2"])
+@pytest.mark.parametrize("n,i0,cnt", [(1, 0, 1), (2, 1, 1), (63, 0, 63), (64, 0, 64), (65, 1, 64), (130, 3, 127),
+                                      (1000, 511, 200), (16384, 0, 16384), (16384, 8000, 100)])
+def test_fd_gradient_term_form_windows_bitwise(ctx, oracle, kind, n, i0, cnt):
+    """The term-form FD gradient (base terms once, per-wave perturbation windows, uniform adds
+    elsewhere) against the oracle's point-by-point evaluation, for blocks whose waves straddle
+    the start, the end and the middle of the coordinate range (the sharded and Recur paths
+    launch such blocks)."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    rng = np.random.default_rng(n + i0)
+    x = rng.uniform(-1.5, 1.5, n); h = rng.uniform(1e-7, 1e-6, n)
+    if kind == "rosenbrock":
+        d, o = DeviceObjective(ctx, L.OBJ_ROSENBROCK, n), oracle.rosenbrock(n)
+    elif kind == "quadratic":
+        dd, bb = oracle.quadratic_data(n, bscale=4.0)
+        d, o = DeviceObjective(ctx, L.OBJ_QUADRATIC, n, 0, dd, bb), oracle.Obj(oracle.QUADRATIC, n, 0, dd, bb)
+    else:   # (power 3 goes through the device pow(): ulp-close, tested by tolerance elsewhere)
+        d, o = DeviceObjective(ctx, L.OBJ_POWER, n, power=2.0), oracle.power(n, 2)
+    f0, g = d.fd_gradient(ctx.tensor(x), ctx.tensor(h), i0, cnt)
+    ref = oracle.fd_gradient(o, x, h)[i0:i0 + cnt]
+    assert np.array_equal(_np(g), ref)
+    assert _np(f0)[0] == oracle.obj_eval(o, x)
+
+
 @pytest.mark.parametrize("n", [3, 4096])
 def test_fd_gradient_quadratic_and_power_bitwise(ctx, oracle, n):
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
