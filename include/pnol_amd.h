@@ -224,8 +224,11 @@ int pnol_fd_gradient(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const doubl
 int pnol_dobj_eval_batch(pnol_ctx* ctx, pnol_dobj* obj, const double* Xs, int npts, double* out);
 /* MultiObjective::gradientApproximation (PNOL_Objective.cpp:165-197) for columns [j0, j0+cnt):
  * F0 = F(x) (computed here when compute_f0, else read), JT row (j - j0) = (F(x + h_j e_j) - F0)/h_j.
- * compute_f0 = 2 (pnol_fd_jtj_d / pnol_fd_jacobian_tiles_d): F0 was filled by
- * pnol_dobj_eval_ckpt_d(ctx, obj, x, F0) and x is unchanged since. */
+ * compute_f0 = 2 (pnol_fd_jtj_d / pnol_fd_jacobian_tiles_d / pnol_lm_jacobian_mpi_d): F0 was
+ * filled by pnol_dobj_eval_ckpt_d(ctx, obj, x, F0); its prefix checkpoints are reused when x's
+ * content is still the one they were made at (checked on the device; otherwise F0 and the
+ * checkpoints are recomputed, so updating x in place is safe).  compute_f0 = 3: the same without
+ * the check -- the caller guarantees x is unchanged (the library's LM loop). */
 int pnol_fd_jacobian_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, int j0, int cnt,
                        double* F0, int compute_f0, double* JT, int ldjt);
 /* One LevMarq Jacobian + normal matrix, pipelined (LevenbergMarquardt.cpp:55-73): the FD

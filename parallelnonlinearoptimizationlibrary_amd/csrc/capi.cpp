@@ -204,7 +204,7 @@ int pnol_lm_sliced_layout(int m, int n, int* slice_rows, size_t* jt_elems) {
 int pnol_lm_jacobian_mpi_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0,
                            int compute_f0, double* JTs) {
     PNOL_CHECK(set_device(ctx));
-    if (!obj || !x || !h || !F0 || !JTs || compute_f0 < 0 || compute_f0 > 2) return PNOL_ERR_ARG;
+    if (!obj || !x || !h || !F0 || !JTs || compute_f0 < 0 || compute_f0 > 3) return PNOL_ERR_ARG;
     return launch_lm_jacobian(ctx, obj, x, h, F0, compute_f0, JTs);
 }
 
@@ -410,14 +410,14 @@ int pnol_fd_jtj_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* 
                   double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, int nchunks) {
     PNOL_CHECK(set_device(ctx));
     if (!obj || !x || !h || !F0 || !JT || !A || ldjt < obj->m || lda < obj->n) return PNOL_ERR_ARG;
-    if (compute_f0 < 0 || compute_f0 > 2) return PNOL_ERR_ARG;
+    if (compute_f0 < 0 || compute_f0 > 3) return PNOL_ERR_ARG;
     return launch_fd_jtj(ctx, obj, x, h, F0, compute_f0, JT, ldjt, lambda, A, lda, jtj_diag, nchunks);
 }
 
 int pnol_fd_jacobian_tiles_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, const int* start,
                              const int* count, int ntiles, double* F0, int compute_f0, double* JT, int ldjt) {
     PNOL_CHECK(set_device(ctx));
-    if (ntiles < 0 || (ntiles > 0 && (!start || !count)) || compute_f0 < 0 || compute_f0 > 2) return PNOL_ERR_ARG;
+    if (ntiles < 0 || (ntiles > 0 && (!start || !count)) || compute_f0 < 0 || compute_f0 > 3) return PNOL_ERR_ARG;
     return launch_fd_jacobian_tiles(ctx, obj, x, h, start, count, ntiles, F0, compute_f0, JT, 0, ldjt);
 }
 

@@ -134,7 +134,7 @@ class LMDevice {
         uploadH(dX);
         // x_ still holds the point F_ was evaluated at: reuse F_ and its checkpoints
         const bool reuse = ckpt_valid_;
-        check(pnol_fd_jtj_d(ctx_, d, x_.get(), h_.get(), reuse ? F_.get() : F0_.get(), reuse ? 2 : 1, JT_.get(),
+        check(pnol_fd_jtj_d(ctx_, d, x_.get(), h_.get(), reuse ? F_.get() : F0_.get(), reuse ? 3 : 1, JT_.get(),
                             ldjt_, lambda, A_.get(), lda_, nullptr, chunks),
               "fd_jtj");
         obj->countEvals(n_ + 1);
@@ -223,13 +223,13 @@ class LMAsync {
     // trip at x_[s] (F_[s] = F(x_[s]); ckpt: its checkpoints are current) -> sigma, x_[s^1], F_[s^1]
     void enqueue(int s, double lambda, bool ckpt) {
         if (sliced_) {
-            check(pnol_lm_jacobian_mpi_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 2 : 1, JT_.get()),
+            check(pnol_lm_jacobian_mpi_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 3 : 1, JT_.get()),
                   "fd_jacobian");
             check(pnol_lm_normal_mpi_d(ctx_, JT_.get(), m_, n_, lambda, F(s), A_.get(), lda_, rhs_.get(),
                                        nullptr),
                   "normal equations");
         } else {
-            check(pnol_fd_jtj_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 2 : 1, JT_.get(), ldjt_, lambda,
+            check(pnol_fd_jtj_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 3 : 1, JT_.get(), ldjt_, lambda,
                                 A_.get(), lda_, nullptr, 1),
                   "fd_jtj");
             check(pnol_jtr_d(ctx_, JT_.get(), ldjt_, m_, n_, F(s), rhs_.get()), "jtr");

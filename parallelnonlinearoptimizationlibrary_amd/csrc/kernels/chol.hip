@@ -21,6 +21,7 @@
 #include "../pnol_internal.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace pnol {
 namespace {
@@ -797,6 +798,8 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm,
     }
 }
 
+__global__ void k_flag_info(int* info, int v) { *info = v; }
+
 }  // namespace
 
 // Solve A sigma = rhs (A SPD, untouched) by the lookahead tile Cholesky; *dinfo (device) != 0
@@ -833,7 +836,15 @@ int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs
     const int epoch = ++ctx->chol4_epoch;
     hipLaunchKernelGGL(k_chol_bwd, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n, (const double*)W,
                        (const double*)bv, (const double*)zv, (double*)xw, sigma, bwdflag, epoch, dinfo);
-    return launch_check();
+    PNOL_CHECK(launch_check());
+    // test hook (tests/test_gpu_solvers.py): report a non-positive pivot so the callers' LU
+    // fallback paths run on an SPD system (read per call: the tests flip it)
+    if (const char* e = std::getenv("PNOL_CHOL_FORCE_FALLBACK"))
+        if (std::atoi(e) != 0) {
+            hipLaunchKernelGGL(k_flag_info, dim3(1), dim3(1), 0, ctx->stream, dinfo, 1);
+            return launch_check();
+        }
+    return PNOL_OK;
 }
 
 }  // namespace pnol

@@ -548,11 +548,26 @@ __global__ __launch_bounds__(256) void k_to_panels(const double* __restrict__ A,
 // while one is consumed.
 constexpr int kRing = 6;
 
+// xsave (nullable): block 0 records x there -- the content the checkpoints belong to.
+// xcheck (nullable): the reuse check of a compute_f0 = 2 call -- every block first compares x
+// with the recorded copy bit for bit and stops when they agree (the checkpoints and F in place
+// are x's); otherwise it recomputes F and its checkpoints (the record is left as it was).
 template <bool CKPT>
 __global__ __launch_bounds__(64) void k_linres_evalP(const double* __restrict__ AP, const double* __restrict__ x,
                                                      const double* __restrict__ y, int m, int n,
-                                                     double* __restrict__ F, double* __restrict__ C) {
+                                                     double* __restrict__ F, double* __restrict__ C,
+                                                     double* __restrict__ xsave = nullptr,
+                                                     const double* __restrict__ xcheck = nullptr) {
     const int rb = blockIdx.x, row = rb * kPanel + threadIdx.x;
+    if (xcheck) {
+        bool diff = false;
+        const unsigned long long* xa = reinterpret_cast<const unsigned long long*>(x);
+        const unsigned long long* xb = reinterpret_cast<const unsigned long long*>(xcheck);
+        for (int k = threadIdx.x; k < n; k += 64) diff |= xa[k] != xb[k];
+        if (!__any(diff)) return;   // one wave per block: uniform
+    }
+    if (xsave && rb == 0)
+        for (int k = threadIdx.x; k < n; k += 64) xsave[k] = x[k];
     const double* a = panel_col(AP, n, rb, 0) + threadIdx.x;
     constexpr int U = kCkpt;
     double acc = 0.0;
@@ -741,7 +756,8 @@ int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out) 
             ScopedTimer tm(ctx, "linres_eval");
             if (o->at)
                 hipLaunchKernelGGL((k_linres_evalP<false>), dim3((o->m + kPanel - 1) / kPanel), dim3(64), 0, ctx->stream,
-                                   (const double*)o->at, x, o->p1, o->m, o->n, out, (double*)nullptr);
+                                   (const double*)o->at, x, o->p1, o->m, o->n, out, (double*)nullptr, (double*)nullptr,
+                                   (const double*)nullptr);
             else if (o->n % 2 == 0)
                 hipLaunchKernelGGL((k_linres_eval<true, false>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0, ctx->stream,
                                    o->p0, x, o->p1, o->m, o->n, out, (double*)nullptr);
@@ -787,26 +803,30 @@ static int ensure_panels(pnol_ctx* ctx, pnol_dobj* o) {
 
 // The two checkpoint slots.  An LM trip holds the checkpoints of its Jacobian point x_s and
 // writes those of the trial point x_t: with two slots a rejected step (x_s stands) finds x_s's
-// still in place and skips the base-chain pass.
+// still in place and skips the base-chain pass.  A slot is tagged with the objective's creation
+// id (never reused, unlike its address) and the device x pointer, and keeps a copy of x's
+// content (written by the kernel that makes the checkpoints), so a compute_f0 = 2 caller that
+// changed x in place gets a recomputation instead of stale checkpoints.
 static int ckpt_find(pnol_ctx* ctx, const pnol_dobj* o, const double* x) {
     for (int s = 0; s < 2; ++s)
-        if (o && ctx->ckpt_obj[s] == o && ctx->ckpt_x[s] == x) return s;
+        if (o && ctx->ckpt_oid[s] == o->id && ctx->ckpt_x[s] == x) return s;
     return -1;
 }
-static int ckpt_buf(pnol_ctx* ctx, const pnol_dobj* o, int slot, void** C) {
+static int ckpt_buf(pnol_ctx* ctx, const pnol_dobj* o, int slot, void** C, void** xcopy) {
     const int ncp = (o->n + kCkpt - 1) / kCkpt;
     ctx->ckpt_use[slot] = ++ctx->ckpt_clock;
+    PNOL_CHECK(ws_get(ctx, slot ? "linres_ckx1" : "linres_ckx0", sizeof(double) * (size_t)o->n, xcopy));
     return ws_get(ctx, slot ? "linres_ckpt1" : "linres_ckpt0", sizeof(double) * (size_t)o->m * (ncp > 1 ? ncp : 1), C);
 }
 // the slot the checkpoints of (o, x) are written to: its own if tagged, else the least recent;
-// tagged (o, x) (obj nullptr: written but never reused)
-static int ckpt_claim(pnol_ctx* ctx, const pnol_dobj* o, const double* x, bool reusable, void** C) {
+// tagged (o, x) (reusable false: written but never reused)
+static int ckpt_claim(pnol_ctx* ctx, const pnol_dobj* o, const double* x, bool reusable, void** C, void** xcopy) {
     int s = ckpt_find(ctx, o, x);
     if (s < 0) s = ctx->ckpt_use[0] <= ctx->ckpt_use[1] ? 0 : 1;
-    ctx->ckpt_obj[s] = reusable ? o : nullptr;
+    ctx->ckpt_oid[s] = reusable ? o->id : 0;
     ctx->ckpt_x[s] = x;
     ctx->ckpt_last = s;
-    return ckpt_buf(ctx, o, s, C);
+    return ckpt_buf(ctx, o, s, C, xcopy);
 }
 
 // F = F(x), and for a linear residual also the prefix checkpoints of x, kept in the context
@@ -816,12 +836,13 @@ int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* 
     if (!o || !x || !out) return PNOL_ERR_ARG;
     if (o->kind != PNOL_OBJ_LINRES) return launch_dobj_eval(ctx, o, x, out);
     PNOL_CHECK(ensure_panels(ctx, o));
-    void* C = nullptr;
-    PNOL_CHECK(ckpt_claim(ctx, o, x, true, &C));
+    void *C = nullptr, *xc = nullptr;
+    PNOL_CHECK(ckpt_claim(ctx, o, x, true, &C, &xc));
     {
         ScopedTimer tm(ctx, "linres_eval");
         hipLaunchKernelGGL((k_linres_evalP<true>), dim3((o->m + kPanel - 1) / kPanel), dim3(64), 0, ctx->stream,
-                           (const double*)o->at, x, o->p1, o->m, o->n, out, (double*)C);
+                           (const double*)o->at, x, o->p1, o->m, o->n, out, (double*)C, (double*)xc,
+                           (const double*)nullptr);
     }
     return launch_check();
 }
@@ -915,26 +936,31 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
     }();
     const bool kmajor = fdk >= 5 || sliced;   // the sliced layout is written by the row-panel kernel
     if (kmajor) PNOL_CHECK(ensure_panels(ctx, o));
-    // one pass of the base chain: F0 (when asked) and the prefix checkpoints -- skipped when
-    // compute_f0 == 2 and the context's checkpoints are those of (o, x) from
-    // launch_dobj_eval_ckpt (F0 then already holds F(x))
-    void* C = nullptr;
-    double* f0_out = compute_f0 == 1 ? F0 : nullptr;
-    const int have = (compute_f0 == 2 && kmajor) ? ckpt_find(ctx, o, x) : -1;
+    // one pass of the base chain: F0 (when asked) and the prefix checkpoints.  compute_f0 == 3
+    // (the library's own LM loop: x untouched since pnol_dobj_eval_ckpt_d) reuses a tagged
+    // slot outright; compute_f0 == 2 (ABI callers) reuses it only if x's content still matches
+    // the slot's record (checked on the device, else F0 and the checkpoints are recomputed);
+    // untagged, both recompute -- 2 including F0, which then cannot be trusted either.
+    void *C = nullptr, *xc = nullptr;
+    double* f0_out = (compute_f0 == 1 || compute_f0 == 2) ? F0 : nullptr;
+    const double* xcheck = nullptr;
+    const int have = (compute_f0 >= 2 && kmajor) ? ckpt_find(ctx, o, x) : -1;
     if (have >= 0) {
-        ckpt = 0;
         ctx->ckpt_last = have;
-        PNOL_CHECK(ckpt_buf(ctx, o, have, &C));
+        PNOL_CHECK(ckpt_buf(ctx, o, have, &C, &xc));
+        if (compute_f0 == 3 || !ckpt) ckpt = 0;
+        else xcheck = (const double*)xc;   // verify, recompute on a mismatch
     } else if (ckpt) {
-        PNOL_CHECK(ckpt_claim(ctx, o, x, kmajor, &C));
+        PNOL_CHECK(ckpt_claim(ctx, o, x, kmajor, &C, &xc));
+        if (compute_f0 == 3) f0_out = nullptr;
     } else {   // the caller's previous call on (o, x) wrote them (chunked FD: chunks after the first)
-        PNOL_CHECK(ckpt_buf(ctx, o, ctx->ckpt_last, &C));
+        PNOL_CHECK(ckpt_buf(ctx, o, ctx->ckpt_last, &C, &xc));
     }
     if (ckpt && kmajor) {
         LaunchTimer tm(ctx, "fd_ckpt");
         hipExtLaunchKernelGGL((k_linres_evalP<true>), dim3((o->m + kPanel - 1) / kPanel), dim3(64), 0, ctx->stream,
                               tm.start(), tm.stop(), 0, (const double*)o->at, x, (const double*)o->p1, o->m, o->n,
-                              f0_out, (double*)C);
+                              f0_out, (double*)C, xcheck ? (double*)nullptr : (double*)xc, xcheck);
     } else if (ckpt) {
         ScopedTimer tm(ctx, "fd_ckpt");
         if ((o->n % 2) == 0)

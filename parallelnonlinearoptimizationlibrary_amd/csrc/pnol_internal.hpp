@@ -5,6 +5,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstddef>
 #include <cstdio>
 #include <map>
@@ -46,7 +47,7 @@ struct pnol_ctx {
     size_t pinned_bytes = 0;
     // two slots of linear-residual prefix checkpoints ("linres_ckpt0/1"), each tagged with the
     // objective and the device x it was computed at; use = last-use stamp (least recent is reused)
-    const pnol_dobj* ckpt_obj[2] = {nullptr, nullptr};
+    unsigned long long ckpt_oid[2] = {0, 0};   // pnol_dobj::id (0: untagged)
     const double* ckpt_x[2] = {nullptr, nullptr};
     unsigned long ckpt_use[2] = {0, 0};
     unsigned long ckpt_clock = 0;
@@ -73,6 +74,12 @@ struct pnol_dobj {
     double* at = nullptr;     // LINRES: A in 64-row k-major panels (fd.hip), built on first FD use
     size_t len0 = 0, len1 = 0;
     pnol_ctx* ctx = nullptr;
+    unsigned long long id = pnol_dobj_next_id();   // unique per creation (checkpoint slot tags)
+  private:
+    static unsigned long long pnol_dobj_next_id() {
+        static std::atomic<unsigned long long> next{1};
+        return next++;
+    }
 };
 
 namespace pnol {

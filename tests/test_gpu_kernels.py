@@ -491,6 +491,41 @@ def test_fd_checkpoint_reuse_bitwise(ctx, oracle, m, n):
     assert np.array_equal(_np(JT), ref)
 
 
+@pytest.mark.parametrize("m,n", [(1000, 300), (4096, 2048)])
+def test_fd_checkpoint_reuse_is_content_keyed(ctx, oracle, m, n):
+    """compute_f0 = 2 after x was updated IN PLACE (same device pointer): the device check of
+    x against the slot's recorded content fails, so F0 and the checkpoints are recomputed --
+    the Jacobian and F0 are x's new ones, bitwise.  A new objective at a recycled address never
+    matches an old slot (slots are tagged by creation id).  compute_f0 = 3 (the LM loop's
+    trusted reuse) on an unchanged x stays bitwise."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L, fd_tiles
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    A, xs, y = oracle.linres_data(m, n)
+    o = oracle.Obj(oracle.LINRES, n, m, A, y)
+    x = np.linspace(-0.5, 0.5, n); x2 = np.linspace(0.3, -0.2, n); h = np.full(n, 1e-7)
+    tiles = fd_tiles(n, 1, 0)
+    d = DeviceObjective(ctx, L.OBJ_LINRES, n, m, A, y)
+    dx, dh = ctx.tensor(x), ctx.tensor(h)
+    F = d.eval_ckpt(dx)
+    dx.copy_(ctx.tensor(x2))                       # in place: same pointer, new content
+    _, JT = d.fd_jacobian_tiles(dx, dh, tiles, ctx.empty(n, m), F0=F, compute_f0=2)
+    assert np.array_equal(_np(JT), oracle.fd_jacobian(o, x2, h).T)
+    assert np.array_equal(_np(F), oracle.obj_eval_multi(o, x2))
+    # unchanged x: trusted reuse (3) and checked reuse (2) agree bitwise with a fresh call (1)
+    F2 = d.eval_ckpt(dx)
+    _, J3 = d.fd_jacobian_tiles(dx, dh, tiles, ctx.empty(n, m), F0=F2, compute_f0=3)
+    _, J1 = d.fd_jacobian_tiles(dx, dh, tiles, ctx.empty(n, m), F0=ctx.empty(m), compute_f0=1)
+    assert np.array_equal(_np(J3), _np(J1))
+    # a different objective (other data) created after this one is destroyed
+    d.close()
+    A2 = A[::-1].copy()
+    d2 = DeviceObjective(ctx, L.OBJ_LINRES, n, m, A2, y)
+    o2 = oracle.Obj(oracle.LINRES, n, m, A2, y)
+    Fz = ctx.tensor(oracle.obj_eval_multi(o2, x2))
+    _, J2 = d2.fd_jacobian_tiles(dx, dh, tiles, ctx.empty(n, m), F0=Fz, compute_f0=2)
+    assert np.array_equal(_np(J2), oracle.fd_jacobian(o2, x2, h).T)
+
+
 @pytest.mark.parametrize("m,n,t64", [(2000, 300, "0"), (5000, 1000, "0"), (777, 129, "0"), (16384, 2048, "0"),
                                      (5000, 1000, "1"), (777, 129, "1"), (16384, 2048, "1"), (300, 100, "0"),
                                      (300, 100, "1"), (4100, 65, "1")])

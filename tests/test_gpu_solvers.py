@@ -422,3 +422,27 @@ def test_eval_batch_abi_bitwise(ctx, oracle):
         dp = C.POINTER(C.c_double)
         L.check(L.lib().pnol_dobj_eval_batch(ctx.h, d.h, Xs.ctypes.data_as(dp), 5, f.ctypes.data_as(dp)), "batch")
         assert f.tolist() == [oracle.obj_eval(o, x) for x in Xs], (kind, n)
+
+
+@pytest.mark.parametrize("m,n", [(600, 100), (3000, 257)])
+def test_lm_one_wait_loop_lu_fallback_equals_general_loop(ctx, oracle, m, n, monkeypatch):
+    """The one-wait LM loop's fallback when the Cholesky reports a non-positive pivot (the
+    solve status packed after sigma and F(x + sigma) in the pinned trip buffer -> redo the trip
+    with the reference-order LU, levmarq.cpp redo_lu): forced on every trip by a test hook, the
+    trajectory (X, F0, FOpt, evaluation count) is bitwise the general loop's, whose
+    pnol_solve_d falls back to the same LU, and stays within 1e-10 of the oracle (whose
+    luSolve is that LU)."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_levmarq
+    A, xs, y = oracle.linres_data(m, n)
+    params = (0.001, 10, 1e-7, 8, 0.0, -1)
+    monkeypatch.setenv("PNOL_CHOL_FORCE_FALLBACK", "1")
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PNOL_LM_ASYNC", mode)
+        out[mode] = run_levmarq(_obj(ctx, L.OBJ_LINRES, n, m, A, y), np.zeros(n), params)
+    (Xa, F0a, FOa, ra), (Xs, F0s, FOs, rs) = out["1"], out["0"]
+    assert np.array_equal(Xa, Xs) and np.array_equal(F0a, F0s) and np.array_equal(FOa, FOs)
+    assert ra.evals == rs.evals
+    Xo, *_ = oracle.lm_findmin(oracle.Obj(oracle.LINRES, n, m, A, y), np.zeros(n), params)
+    assert rel(Xa, Xo) <= 1e-10
