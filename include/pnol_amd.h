@@ -181,6 +181,12 @@ int pnol_solve_d(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
  * falls back to pnol_solve_d with method 2; A is left intact).  Lets the LM loop keep the
  * device busy while the host checks the previous trial point. */
 int pnol_solve_async_d(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo);
+/* Binv = B^{-1} (n x n, row-major, device), bitwise the reference's matrixInverse: luSolve(B, e_c)
+ * for every column c (UtilityFunctionLibrary restatement) as ONE partial-pivoting
+ * elimination of [B | I] followed by per-column back substitution (the initHessFD inverse,
+ * BFGS_with_linesearch.cpp:34-41, BFGS_bnd_linesearch.cpp:55-63).  info (host, nullable): 0, or
+ * -1 after a zero pivot (the inverse then holds the inf / NaN the reference would produce). */
+int pnol_matrix_inverse_d(pnol_ctx* ctx, const double* B, int ldb, int n, double* Binv, int ldi, int* info);
 /* z = x + y (the LM trial point X + sigma on the device: the same IEEE add as the host's) */
 int pnol_add_d(pnol_ctx* ctx, const double* x, const double* y, double* z, int n);
 
@@ -288,6 +294,10 @@ int pnol_run_levmarq(int which, pnol_dobj* obj, int host_eval, const double* par
 /* Host-objective FD through the C++ MultiObjective with a C callback objective
  * (gradientApproximation / gradientApproximationMPI on the active communicator). */
 typedef void (*pnol_host_multi_fn)(const double* x, int n, double* F, int m, void* user);
+typedef double (*pnol_host_scalar_fn)(const double* x, int n, void* user);
+/* Objective::hessianApproximation (PNOL_Objective.cpp:38-85) of a C callback objective through the
+ * C++ FD engine (its points handed to objEvalBatch in the reference's order); B n x n row-major. */
+int pnol_host_fd_hessian(pnol_host_scalar_fn fn, void* user, const double* x, const double* h, int n, double* B);
 int pnol_host_fd_jacobian(pnol_host_multi_fn fn, void* user, const double* x, const double* h, int n, int m,
                           int sharded, double* J_rowmajor);
 

@@ -240,6 +240,13 @@ def lusolve(A, b):
     return x
 
 
+def matinv(A):  # matrixInverse (utility restatement): luSolve per unit column
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    Ai = np.zeros_like(A)
+    lib().orc_util_matinv(ptr(A), ptr(Ai), A.shape[0])
+    return Ai
+
+
 def update_hessian_inv(D, y, s):  # updateHessianInv, BFGS_with_linesearch.cpp:389-432
     D = np.array(D, dtype=np.float64, order="C")
     y = np.ascontiguousarray(y, dtype=np.float64); s = np.ascontiguousarray(s, dtype=np.float64)

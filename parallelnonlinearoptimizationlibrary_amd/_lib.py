@@ -40,6 +40,7 @@ class Result(C.Structure):
 
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, _vp, _vp, _sz, _vp)
 HOST_MULTI_FN = C.CFUNCTYPE(None, _dp, C.c_int, _dp, C.c_int, _vp)
+HOST_SCALAR_FN = C.CFUNCTYPE(C.c_double, _dp, C.c_int, _vp)
 
 # name -> (restype, argtypes)
 _SIGS = {
@@ -87,6 +88,7 @@ _SIGS = {
     "pnol_jtr_d": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
     "pnol_solve_d": (_i, [_vp, _vp, _i, _vp, _vp, _i, _i, C.POINTER(_i)]),
     "pnol_solve_async_d": (_i, [_vp, _vp, _i, _vp, _vp, _i, _vp]),
+    "pnol_matrix_inverse_d": (_i, [_vp, _vp, _i, _i, _vp, _i, C.POINTER(_i)]),
     "pnol_add_d": (_i, [_vp, _vp, _vp, _vp, _i]),
     "pnol_dobj_create": (_i, [_vp, _i, _i, _i, _dp, _sz, _dp, _sz, _d, C.POINTER(_vp)]),
     "pnol_dobj_create_synthetic": (_i, [_vp, _i, _i, _i, C.c_ulonglong, _d, _dp, C.POINTER(_vp)]),
@@ -113,6 +115,7 @@ _SIGS = {
     "pnol_run_bfgs_ex": (_i, [_i, _vp, _i, _dp, _i, _dp, _i, _dp, _dp, C.POINTER(Result), _dp, _i, C.POINTER(_i),
                               _dp]),
     "pnol_run_levmarq": (_i, [_i, _vp, _i, _dp, _dp, _i, _dp, _dp, _i, C.POINTER(Result)]),
+    "pnol_host_fd_hessian": (_i, [HOST_SCALAR_FN, _vp, _dp, _dp, _i, _dp]),
     "pnol_host_fd_jacobian": (_i, [HOST_MULTI_FN, _vp, _dp, _dp, _i, _i, _i, _dp]),
 }
 

@@ -62,6 +62,12 @@ int pnol_set_identity_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* 
     return launch_set_identity(ctx, D, ldd, n, scale);
 }
 
+int pnol_matrix_inverse_d(pnol_ctx* ctx, const double* B, int ldb, int n, double* Binv, int ldi, int* info) {
+    PNOL_CHECK(set_device(ctx));
+    ScopedTimer tm(ctx, "matrix_inverse");
+    return launch_matrix_inverse(ctx, B, ldb, n, Binv, ldi, info);
+}
+
 int pnol_add_d(pnol_ctx* ctx, const double* x, const double* y, double* z, int n) {
     PNOL_CHECK(set_device(ctx));
     return launch_add(ctx, x, y, z, n);

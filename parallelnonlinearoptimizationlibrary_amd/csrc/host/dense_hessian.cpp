@@ -294,32 +294,41 @@ void DenseInverseHessian::update(const std::vector<double>& y, const std::vector
     }
 }
 
-// D0 = inverse of the FD Hessian (initHessFD), column by column on the device
+void DenseInverseHessian::setInverseOf(const std::vector<std::vector<double>>& B) {
+    // matrixInverse(B, D) (BFGS_with_linesearch.cpp:40): one device elimination of [B | I]
+    // and per-column back substitution, bitwise the reference's per-column luSolve
+    std::vector<double> hB((size_t)n_ * n_);
+    for (int i = 0; i < n_; ++i)
+        for (int j = 0; j < n_; ++j) hB[(size_t)i * n_ + j] = B[i][j];
+    DevVec dB(ctx_, hB.size());
+    dB.upload(hB);
+    int info = 0;
+    if (!sharded_) {
+        if (clobbered_) throw std::runtime_error("DenseInverseHessian: D used while lent to a reduced problem");
+        check(pnol_matrix_inverse_d(ctx_, dB.get(), n_, n_, Dp_, ld_, &info), "matrix_inverse(initHessFD)");
+        pending_ = false;
+        ident_ = false;
+        dev_ok_ = true;
+        return;
+    }
+    DevVec dI(ctx_, (size_t)n_ * n_);   // row-sharded D: the whole inverse, then this rank's rows
+    check(pnol_matrix_inverse_d(ctx_, dB.get(), n_, n_, dI.get(), n_, &info), "matrix_inverse(initHessFD)");
+    std::vector<double> h((size_t)n_ * n_);
+    dI.download(h);
+    std::vector<std::vector<double>> Dm(n_, std::vector<double>(n_));
+    for (int i = 0; i < n_; ++i)
+        for (int j = 0; j < n_; ++j) Dm[i][j] = h[(size_t)i * n_ + j];
+    setMatrix(Dm);
+}
+
+// D0 = inverse of the FD Hessian (initHessFD): hessianApproximation (its points batched through
+// objEvalBatch) + the device matrixInverse
 void init_from_fd_hessian(Objective* obj, std::vector<double>& X, double dXHess, DenseInverseHessian& D) {
     const int n = (int)X.size();
     std::vector<double> dXH(n, dXHess);
     std::vector<std::vector<double>> B;
     obj->hessianApproximation(X, dXH, B);
-    pnol_ctx* ctx = require_ctx();
-    const int ld = even_ld(n);
-    std::vector<double> hB((size_t)n * ld, 0.0);
-    for (int i = 0; i < n; ++i)
-        for (int j = 0; j < n; ++j) hB[(size_t)i * ld + j] = B[i][j];
-    DevVec dA(ctx, hB.size()), de(ctx, n), dc(ctx, n);
-    std::vector<std::vector<double>> Dinv(n, std::vector<double>(n));
-    std::vector<double> e(n, 0.0), c(n);
-    for (int j = 0; j < n; ++j) {
-        // matrixInverse via per-column solves; the solve consumes its matrix
-        dA.upload(hB);
-        e[j] = 1.0;
-        de.upload(e);
-        int info = 0;
-        check(pnol_solve_d(ctx, dA.get(), ld, de.get(), dc.get(), n, 2, &info), "solve(initHessFD)");
-        dc.download(c);
-        for (int i = 0; i < n; ++i) Dinv[i][j] = c[i];
-        e[j] = 0.0;
-    }
-    D.setMatrix(Dinv);
+    D.setInverseOf(B);
 }
 
 

@@ -50,6 +50,8 @@ class DenseInverseHessian {
 
     void setIdentity(const std::vector<double>* diagScale = nullptr);
     void setMatrix(const std::vector<std::vector<double>>& D);
+    // D = B^{-1}, the reference's matrixInverse (initHessFD), computed on the device
+    void setInverseOf(const std::vector<std::vector<double>>& B);
     void getMatrix(std::vector<std::vector<double>>& D);
     // this = src[idx][idx] (idx ascending, size n()), gathered on the device
     void setSubmatrixOf(DenseInverseHessian& src, const std::vector<int>& idx);

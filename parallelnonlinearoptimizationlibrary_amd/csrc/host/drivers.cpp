@@ -144,6 +144,16 @@ class CallbackMulti : public MultiObjective {
     int m_;
 };
 
+class CallbackScalar : public Objective {
+  public:
+    CallbackScalar(pnol_host_scalar_fn fn, void* user) : fn_(fn), user_(user) {}
+    double objEval(vector<double>& X) override { return fn_(X.data(), (int)X.size(), user_); }
+
+  private:
+    pnol_host_scalar_fn fn_;
+    void* user_;
+};
+
 template <class F>
 int guarded(F&& body) {
     try {
@@ -265,6 +275,18 @@ int pnol_run_levmarq(int which, pnol_dobj* obj, int host_eval, const double* p, 
         for (int i = 0; i < m; ++i) { c0 = c0 + f0[i] * f0[i]; c1 = c1 + fopt[i] * fopt[i]; }
         res->f0 = c0;
         res->fopt = c1;
+    });
+}
+
+int pnol_host_fd_hessian(pnol_host_scalar_fn fn, void* user, const double* x, const double* h, int n, double* B) {
+    if (!fn || !x || !h || !B || n <= 0) return PNOL_ERR_ARG;
+    return guarded([&] {
+        CallbackScalar o(fn, user);
+        std::vector<double> X(x, x + n), dX(h, h + n);
+        std::vector<std::vector<double>> Bv;
+        o.hessianApproximation(X, dX, Bv);
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) B[(size_t)i * n + j] = Bv[i][j];
     });
 }
 

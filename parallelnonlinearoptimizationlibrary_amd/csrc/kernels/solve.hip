@@ -603,6 +603,75 @@ __global__ void k_lu_backsub(const double* __restrict__ M, const double* __restr
     *info = sing ? -1 : 2;
 }
 
+// ---- matrixInverse: one elimination, n right-hand sides -------------------------------------
+// The reference inverts column by column, luSolve(B, e_c): Gaussian elimination
+// with partial pivoting on a copy of B, the rhs updated b_i -= f_i b_k with the same f, then back
+// substitution.  The pivots and multipliers depend on B alone, so eliminating the augmented
+// [B | I] once applies exactly the operations each column's solve applies to its rhs (the rhs
+// rows swapped, then b_i - f_i b_k for every k in order), and the back substitution then runs
+// per column in the reference's order.  M is n x 2n (row stride ldm >= 2n).
+__global__ void k_luinv_pivot(double* __restrict__ M, long ldm, int n, double* __restrict__ f, int k) {
+    __shared__ int piv_sh;
+    const int t = threadIdx.x;
+    if (t == 0) {
+        int piv = k;
+        double best = fabs(M[(long)k * ldm + k]);
+        for (int i = k + 1; i < n; ++i) {
+            double v = fabs(M[(long)i * ldm + k]);
+            if (v > best) { best = v; piv = i; }
+        }
+        piv_sh = piv;
+    }
+    __syncthreads();
+    const int piv = piv_sh;
+    if (piv != k)
+        for (int j = t; j < 2 * n; j += blockDim.x) {   // the row of B and the rhs entries
+            double tmp = M[(long)k * ldm + j];
+            M[(long)k * ldm + j] = M[(long)piv * ldm + j];
+            M[(long)piv * ldm + j] = tmp;
+        }
+    __syncthreads();
+    const double akk = M[(long)k * ldm + k];
+    for (int i = k + 1 + t; i < n; i += blockDim.x) f[i] = M[(long)i * ldm + k] / akk;
+}
+
+// rows i > k: M[i][j] = M[i][j] - f_i M[k][j] for j in [k, 2n) -- B's columns from k as
+// luSolve's elimination, and every rhs column as its b_i = b_i - f_i b_k
+__global__ void k_luinv_eliminate(double* __restrict__ M, long ldm, int n, const double* __restrict__ f, int k) {
+    const int cols = 2 * n - k;
+    const long total = (long)(n - k - 1) * cols;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const int i = k + 1 + (int)(e / cols), j = k + (int)(e % cols);
+        M[(long)i * ldm + j] = M[(long)i * ldm + j] - f[i] * M[(long)k * ldm + j];
+    }
+}
+
+// column c of the inverse: x_i = (b_i - sum_{j > i} U_ij x_j) / U_ii, j ascending, i descending;
+// one thread per column (the U reads are the same address for the whole wave)
+__global__ void k_luinv_backsub(const double* __restrict__ M, long ldm, int n, double* __restrict__ X, long ldx,
+                                int* __restrict__ info) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    int sing = 0;
+    for (int i = n - 1; i >= 0; --i) {
+        const double* Ui = M + (long)i * ldm;
+        double s = Ui[n + c];
+        for (int j = i + 1; j < n; ++j) s = s - Ui[j] * X[(long)j * ldx + c];
+        const double d = Ui[i];
+        if (d == 0.0) sing = 1;
+        X[(long)i * ldx + c] = s / d;
+    }
+    if (sing) atomicExch(info, -1);
+}
+
+__global__ void k_luinv_load(const double* __restrict__ B, long ldb, int n, double* __restrict__ M, long ldm) {
+    const long total = (long)n * 2 * n;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const int i = (int)(e / (2 * n)), j = (int)(e % (2 * n));
+        M[(long)i * ldm + j] = j < n ? B[(long)i * ldb + j] : (j - n == i ? 1.0 : 0.0);
+    }
+}
+
 __global__ void k_copy_matrix(const double* __restrict__ A, long lda, double* __restrict__ M, int n) {
     long total = (long)n * n;
     for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x)
@@ -637,6 +706,36 @@ static int lu_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs, 
     hipLaunchKernelGGL(k_lu_backsub, dim3(1), dim3(64), 0, ctx->stream, (const double*)M, (const double*)b, n, sigma,
                        dinfo);
     return launch_check();
+}
+
+int launch_matrix_inverse(pnol_ctx* ctx, const double* B, int ldb, int n, double* Binv, int ldi, int* info_host) {
+    if (!B || !Binv || n <= 0 || ldb < n || ldi < n) return PNOL_ERR_ARG;
+    const long ldm = 2L * n;
+    void *M = nullptr, *f = nullptr, *di = nullptr;
+    PNOL_CHECK(ws_get(ctx, "luinv_M", sizeof(double) * (size_t)n * ldm, &M));
+    PNOL_CHECK(ws_get(ctx, "luinv_f", sizeof(double) * (size_t)n, &f));
+    PNOL_CHECK(ws_get(ctx, "luinv_info", sizeof(int) * 4, &di));
+    const long total = (long)n * ldm;
+    hipLaunchKernelGGL(k_luinv_load, dim3((int)std::min<long>((total + 255) / 256, 4096)), dim3(256), 0, ctx->stream, B,
+                       (long)ldb, n, (double*)M, ldm);
+    hipLaunchKernelGGL(k_set_int, dim3(1), dim3(1), 0, ctx->stream, (int*)di, 0);
+    for (int k = 0; k < n; ++k) {
+        hipLaunchKernelGGL(k_luinv_pivot, dim3(1), dim3(1024), 0, ctx->stream, (double*)M, ldm, n, (double*)f, k);
+        const long work = (long)(n - k - 1) * (2 * n - k);
+        if (work > 0) {
+            const int blocks = (int)std::max<long>(1, std::min<long>((work + 255) / 256, 4096));
+            hipLaunchKernelGGL(k_luinv_eliminate, dim3(blocks), dim3(256), 0, ctx->stream, (double*)M, ldm, n,
+                               (const double*)f, k);
+        }
+    }
+    hipLaunchKernelGGL(k_luinv_backsub, dim3((n + 63) / 64), dim3(64), 0, ctx->stream, (const double*)M, ldm, n, Binv,
+                       (long)ldi, (int*)di);
+    PNOL_CHECK(launch_check());
+    int h = 0;
+    PNOL_HIP(hipMemcpyAsync(&h, di, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    if (info_host) *info_host = h;
+    return PNOL_OK;
 }
 
 // Task list of the tile-DAG Cholesky in its lookahead topological order ({kind, k, i, j}).

@@ -171,6 +171,9 @@ int launch_jtr(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const do
 int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, double alpha, double* C,
                       int ldc, int split_k);
 
+// Binv = B^{-1} as the reference's matrixInverse (per-column luSolve), bitwise: one elimination
+// of [B | I], per-column back substitution; *info_host = -1 on a zero pivot (inf / NaN entries)
+int launch_matrix_inverse(pnol_ctx* ctx, const double* B, int ldb, int n, double* Binv, int ldi, int* info_host);
 int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo);
 int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n, int method,
                  int* info);

@@ -446,3 +446,53 @@ def test_lm_one_wait_loop_lu_fallback_equals_general_loop(ctx, oracle, m, n, mon
     assert ra.evals == rs.evals
     Xo, *_ = oracle.lm_findmin(oracle.Obj(oracle.LINRES, n, m, A, y), np.zeros(n), params)
     assert rel(Xa, Xo) <= 1e-10
+
+
+@pytest.mark.parametrize("n", [1, 7, 100, 300])
+def test_matrix_inverse_bitwise(ctx, oracle, n):
+    """pnol_matrix_inverse_d (one elimination of [B | I], per-column back substitution) equals
+    the reference's matrixInverse -- luSolve per unit column -- bit for bit, row swaps included."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import _ptr
+    import ctypes as C
+    rng = np.random.default_rng(n)
+    B = rng.standard_normal((n, n)) + (0.5 * n) * np.eye(n)[::-1]   # anti-diagonal weight: pivots swap rows
+    dB, out = ctx.tensor(B), ctx.empty(n, n)
+    info = C.c_int(7)
+    L.check(L.lib().pnol_matrix_inverse_d(ctx.h, _ptr(dB), n, n, _ptr(out), n, C.byref(info)), "matrix_inverse")
+    assert info.value == 0
+    assert np.array_equal(out.cpu().numpy(), oracle.matinv(B))
+
+
+@pytest.mark.parametrize("n,x0", [(2, [-1.2, 1.0]), (5, [3.0] * 5), (10, [0.5] * 10)])
+def test_bfgs_init_hess_fd_matches_oracle(ctx, oracle, n, x0):
+    """BFGS with initHessFD (BFGS_with_linesearch.cpp:34-41): D0 = matrixInverse of the FD
+    Hessian (hessianApproximation's points batched on the host, the inverse on the device);
+    exact mode (n <= PNOL_SEQ_MAX), so X, fOpt and the evaluation count equal the oracle's."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_bfgs
+    P = [1e-4, 0.9, 1e-6, 1, 1000, 1e-7, 1e-3, 100, 1e-5, 1e-5, 1, 0]
+    X, res = run_bfgs(_obj(ctx, L.OBJ_ROSENBROCK, n), x0, P)
+    Xo, reso, _ = oracle.bfgs_findmin(oracle.rosenbrock(n), x0, P)
+    assert np.array_equal(X, Xo) and res.fopt == reso.fopt
+    # the oracle's count starts after initHessFD; the objective's counter (ours) includes the
+    # FD Hessian's 1 + 3 n (n + 1) / 2 evaluations, as the reference objective's does
+    assert res.evals == reso.evals + 1 + 3 * n * (n + 1) // 2
+
+
+def test_bfgs_init_hess_fd_fast_mode_quadratic(ctx, oracle):
+    """initHessFD in fast mode (n = 300): the quadratic's FD Hessian is its tridiagonal Hessian
+    to O(h), so D0 ~ H^{-1} and BFGS converges in a few iterations; trajectory tolerance vs the
+    oracle as for the other fast-mode runs."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective, run_bfgs
+    n = 300
+    dd, bb = oracle.quadratic_data(n)
+    P = [1e-4, 0.9, 1e-6, 1, 1000, 1e-6, 1e-3, 50, 1e-9, 1e-6, 1, 0]
+    prof = {}
+    X, res = run_bfgs(DeviceObjective(ctx, L.OBJ_QUADRATIC, n, 0, dd, bb), np.zeros(n), P, profile=prof)
+    Xo, reso, _ = oracle.bfgs_findmin(oracle.Obj(oracle.QUADRATIC, n, 0, dd, bb), np.zeros(n), P)
+    H = np.diag(dd) + 0.25 * (np.eye(n, k=1) + np.eye(n, k=-1))
+    assert rel(X, np.linalg.solve(H, bb)) <= 2e-4
+    assert rel(X, Xo) <= 2e-4
+    assert prof["iterations"] <= 10

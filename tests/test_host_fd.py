@@ -30,3 +30,28 @@ def test_host_fd_jacobian_bitwise(oracle, factory, x0):
                                               J.ctypes.data_as(dp)), "host fd")
         ref = oracle.fd_jacobian(getattr(oracle, factory)(), x, h)
         assert np.array_equal(J, ref)
+
+
+@pytest.mark.parametrize("factory,n", [("rosenbrock", 2), ("rosenbrock", 5), ("quadratic", 30), ("goldstein", 2)])
+def test_host_fd_hessian_bitwise(oracle, factory, n):
+    """Objective::hessianApproximation of the C++ FD engine (PNOL_Objective.cpp:38-85: F, then
+    per upper-triangle pair the three points, batched through objEvalBatch) vs the oracle,
+    bitwise, with the reference's evaluation count 1 + 3 n (n + 1) / 2."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    obj = {"rosenbrock": lambda: oracle.rosenbrock(n), "quadratic": lambda: oracle.quadratic(n),
+           "goldstein": lambda: oracle.Obj(oracle.GOLDSTEIN, 2)}[factory]()
+    calls = []
+
+    def fn(x, nn, user):
+        calls.append(1)
+        return oracle.obj_eval(obj, np.ctypeslib.as_array(x, shape=(nn,)).copy())
+
+    cb = L.HOST_SCALAR_FN(fn)
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-1.5, 1.5, n); h = np.full(n, 1e-3)
+    B = np.zeros((n, n))
+    dp = C.POINTER(C.c_double)
+    L.check(L.lib().pnol_host_fd_hessian(cb, None, x.ctypes.data_as(dp), h.ctypes.data_as(dp), n,
+                                         B.ctypes.data_as(dp)), "host fd hessian")
+    assert np.array_equal(B, oracle.fd_hessian(obj, x, h))
+    assert len(calls) == 1 + 3 * n * (n + 1) // 2
