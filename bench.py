@@ -45,8 +45,9 @@ def _args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hg", action="store_true")
     ap.add_argument("--no-timers", action="store_true", help="no per-kernel HIP events in the timed region")
-    ap.add_argument("--m", type=int, default=M_RES)
-    ap.add_argument("--n", type=int, default=N_PAR)
+    # (not --m / --n: torch.distributed.run would take those for abbreviations of its own options)
+    ap.add_argument("--residuals", type=int, default=M_RES, help="m, residual rows (default: the metric's 16384)")
+    ap.add_argument("--params", type=int, default=N_PAR, help="n, parameters (default: the metric's 2048)")
     ap.add_argument("--host-comm", action="store_true",
                     help="rehearsal on one GPU: gloo + the library's host communicator instead of RCCL")
     ap.add_argument("--no-bfgs", action="store_true", help="skip the BFGS cfg-2 / BFGS_Bnd cfg-5 solve blocks")
@@ -303,7 +304,7 @@ def main():
         dist.init_process_group("nccl", init_method="env://", rank=rank, world_size=world,
                                 device_id=torch.device("cuda", local))
 
-    m, n = args.m, args.n
+    m, n = args.residuals, args.params
     ctx = Context(local)
     # the C++ drop-in classes run on the process default context: bind its timers
     dctx = C.c_void_p()

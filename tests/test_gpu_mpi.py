@@ -133,3 +133,33 @@ def test_levmarq_mpi_ranks_bitwise_equal_single(tmp_path, world, oracle):
         z = np.load(tmp_path / f"rank{r}.npz")
         assert np.array_equal(z["Xq"], Xq1), r
         assert z["fq"][0] == resq1.fopt, r
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_multi_rank_line_is_valid(tmp_path, world):
+    """bench.py's N > 1 line, rehearsed with `world` ranks on the box's one GPU over the host
+    communicator: the roofline prices the SYRK each rank actually ran -- its own m-slices' rows
+    (LevenbergMarquardtMPI.cpp:64-78 split by slice) -- so achieved = rows n (n + 1) / syrk time
+    and frac <= 1; the line names the communicator and its size, and carries the FD-Jacobian
+    strong-scaling quantity."""
+    import json
+    port = _free_port()
+    m, n = 8192, 1024
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(os.path.dirname(HERE), "bench.py"),
+           "--gpus", str(world), "--host-comm", "--steps", "3", "--warmup", "1", "--residuals", str(m), "--params", str(n),
+           "--no-cpu-baseline", "--no-hg", "--no-bfgs"]
+    r = subprocess.run(cmd, capture_output=True, timeout=300, env=dict(os.environ, PNOL_DEVICE="0"))
+    assert r.returncode == 0, r.stderr.decode(errors="replace")[-3000:]
+    line = json.loads([l for l in r.stdout.decode().splitlines() if l.startswith("{")][-1])
+    rf = line["roofline"]
+    mS = ((m + 7) // 8 + 63) // 64 * 64          # lm_slice_rows: 8 m-slices, 64-row multiples
+    rows = min(m, (8 // world) * mS)              # rank 0 holds slices [0, 8 / world)
+    assert rf["rows"] == rows and rf["flop_per_launch"] == float(rows) * n * (n + 1)
+    syrk_ms = line["kernel_ms_per_step"]["syrk"]
+    assert abs(rf["achieved"] - rf["flop_per_launch"] / (syrk_ms * 1e-3) / 1e12) <= 1e-9 * rf["achieved"]
+    assert 0 < rf["frac"] <= 1.0
+    assert rf["traffic"] is None
+    assert line["comm"] == {"backend": "host-gloo", "ranks": world} and line["n_gpus"] == world
+    assert line["fd_jacobian_ms_max_over_ranks"] > 0
+    assert "host communicator" in line["config"]["workload"]

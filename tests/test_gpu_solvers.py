@@ -496,3 +496,45 @@ def test_bfgs_init_hess_fd_fast_mode_quadratic(ctx, oracle):
     assert rel(X, np.linalg.solve(H, bb)) <= 2e-4
     assert rel(X, Xo) <= 2e-4
     assert prof["iterations"] <= 10
+
+
+def _run_user_levmarq(tmp_path, A, y, x0, params, threads):
+    import struct
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "examples", "user_levmarq")
+    if not os.path.exists(exe):   # normally built by __graft_entry__.build()
+        subprocess.run(["make", "-s", "-C", os.path.join(root, "examples")], check=True, timeout=120)
+    m, n = A.shape
+    fin, fout = str(tmp_path / f"in{threads}.bin"), str(tmp_path / f"out{threads}.bin")
+    with open(fin, "wb") as f:
+        f.write(struct.pack("3i", m, n, threads))
+        f.write(np.asarray(params, dtype=np.float64).tobytes())
+        for a in (A, y, x0):
+            f.write(np.ascontiguousarray(a, dtype=np.float64).tobytes())
+    r = subprocess.run([exe, fin, fout], capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    raw = open(fout, "rb").read()
+    X = np.frombuffer(raw[:8 * n], dtype=np.float64)
+    c0, c1 = np.frombuffer(raw[8 * n:8 * n + 16], dtype=np.float64)
+    evals, batches = np.frombuffer(raw[8 * n + 16:], dtype=np.int64)
+    return X, c0, c1, int(evals), int(batches)
+
+
+@pytest.mark.parametrize("m,n", [(600, 100), (3000, 257)])
+def test_user_program_own_multiobjective_levmarq(ctx, oracle, tmp_path, m, n):
+    """A C++ user program (examples/user_levmarq.cpp, INTEGRATION.md's g++ build line) with its
+    OWN MultiObjective (not a built-in: n > PNOL_SEQ_MAX, evaluated on the host through its
+    objEvalBatch override, which spreads each batch over host threads) runs LevMarq with the
+    J^T J / solve on the GPU.  Converged X within 1e-10 of the oracle's LevMarq; the thread
+    count does not change a bit; every Jacobian's points arrived as batches."""
+    A, xs, y = oracle.linres_data(m, n)
+    params = (0.001, 10, 1e-7, 6, 0.0)
+    X1, c01, c11, ev1, b1 = _run_user_levmarq(tmp_path, A, y, np.zeros(n), params, 1)
+    X4, c04, c14, ev4, b4 = _run_user_levmarq(tmp_path, A, y, np.zeros(n), params, 4)
+    assert np.array_equal(X1, X4) and c11 == c14 and ev1 == ev4
+    Xo, reso, F0o, FOo, _ = oracle.lm_findmin(oracle.Obj(oracle.LINRES, n, m, A, y), np.zeros(n), params + (-1,))
+    assert rel(X1, Xo) <= 1e-10
+    assert rel(X1, xs) <= 1e-8
+    assert ev1 == reso.evals, (ev1, reso.evals)
+    assert b1 >= 6   # one batch (or more) of FD points per Jacobian, plus the trial points
