@@ -252,36 +252,80 @@ def bench_bfgs_solve(ctx, which, n, bscale, params, bounds=None):
 
 
 def cpu_baseline(m, n, budget_s=20.0):
-    """Oracle (CPU restatement of the reference, 1 thread) on a bounded sample of one LM loop
-    trip at (m, n): FD residual evaluations (the n+1 columns), rows of J^T J (the reference's
-    matrixMultiply), the reference LU once; extrapolated to one full trip."""
+    """The reference path on the host cores: the oracle (the CPU restatement of the reference,
+    loop for loop) built -O3 -march=x86-64-v3 -ffp-contract=off (liboracle_fast.so), timed on a
+    bounded sample of one LM loop trip at (m, n) and extrapolated to the whole trip:
+      - residual evaluations (the n + 2 of a trip), 1 thread and P threads -- the reference's
+        MPI FD sharding (PNOL_Objective.cpp:202-299) as P concurrent evaluators;
+      - rows of J^T J with the reference's matrixMultiply, 1 and P threads;
+      - the reference LU (luSolve) at n = 1024, scaled by (n / 1024)^3.
+    value = LM trips per second with P threads (P = the host cores this process may use, at
+    most 16, the box's per-GPU CPU share).  Also the BFGS kernels' CPU counterparts: p = -D g at
+    n = 8192 (GB/s), the rank-2 update at n = 4096 and the reference's O(n^3) update form at
+    n = 512 (extrapolated by n^3 to 4096)."""
+    from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     O.build()
+    O.use_fast()
+    P = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
     A, xs, y = O.linres_data(m, n)
     o = O.Obj(O.LINRES, n, m, A, y)
     x = np.zeros(n)
     t0 = time.perf_counter(); k_eval = 0
-    while k_eval < 4 or (time.perf_counter() - t0 < budget_s * 0.3 and k_eval < 64):
+    while k_eval < 4 or (time.perf_counter() - t0 < budget_s * 0.15 and k_eval < 32):
         O.obj_eval_multi(o, x); k_eval += 1
     t_eval = (time.perf_counter() - t0) / k_eval
+    # P concurrent evaluators (ctypes releases the GIL inside the C call)
+    objs = [O.Obj(O.LINRES, n, m, A, y) for _ in range(P)]
+    with ThreadPoolExecutor(P) as ex:
+        list(ex.map(lambda q: O.obj_eval_multi(objs[q], x), range(P)))   # warm
+        t0 = time.perf_counter()
+        list(ex.map(lambda q: O.obj_eval_multi(objs[q % P], x), range(2 * P)))
+        t_eval_par = (time.perf_counter() - t0) / (2 * P)                  # per evaluation, amortised
     J = np.ascontiguousarray(A)                    # any m x n data: cost is data-independent
     JT = np.ascontiguousarray(J.T)
     t0 = time.perf_counter(); k_rows = 0
-    while k_rows < 2 or (time.perf_counter() - t0 < budget_s * 0.3 and k_rows < 64):
+    while k_rows < 2 or (time.perf_counter() - t0 < budget_s * 0.15 and k_rows < 32):
         O.matmul(JT[k_rows:k_rows + 1], J); k_rows += 1
     t_row = (time.perf_counter() - t0) / k_rows
+    with ThreadPoolExecutor(P) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(lambda q: O.matmul(JT[q:q + 1], J), range(P)))
+        t_row_par = (time.perf_counter() - t0) / P
     nl = min(n, 1024)
     Al = JT[:nl, :nl] @ JT[:nl, :nl].T + np.eye(nl)
     t0 = time.perf_counter(); O.lusolve(Al, np.ones(nl)); t_lu = (time.perf_counter() - t0) * (n / nl) ** 3
-    t_iter = t_eval * (n + 2) + t_row * n + t_lu
+    t_trip1 = t_eval * (n + 2) + t_row * n + t_lu
+    t_tripP = t_eval_par * (n + 2) + t_row_par * n + t_lu
+    # BFGS counterparts (single thread, the reference's sequential loops)
+    rng = np.random.default_rng(0)
+    nh = 8192
+    D = rng.standard_normal((nh, nh)); g = rng.standard_normal(nh)
+    t0 = time.perf_counter(); O.matvec(D, g); t_hg = time.perf_counter() - t0
+    del D
+    nu = 4096
+    D = np.eye(nu) + 1e-3 * rng.standard_normal((nu, nu)); yv = rng.standard_normal(nu); sv = yv + 0.1
+    t0 = time.perf_counter(); O.update_hessian_inv_rank2(D, yv, sv); t_r2 = time.perf_counter() - t0
+    del D
+    n3 = 512
+    D = np.eye(n3); y3 = rng.standard_normal(n3); s3 = y3 + 0.1
+    t0 = time.perf_counter(); O.update_hessian_inv(D, y3, s3); t_n3 = time.perf_counter() - t0
     return {
-        "value": 1.0 / t_iter, "unit": "LM iters/sec", "cores": 1, "kind": "port",
-        "sample": (f"oracle (C restatement, gcc -O2, 1 thread) at m={m}, n={n}: {k_eval} residual evals "
-                   f"({t_eval*1e3:.1f} ms each, x{n + 2} per trip), {k_rows} rows of J^T J "
-                   f"({t_row*1e3:.1f} ms each, x{n}), LU at n={nl} scaled by (n/{nl})^3 "
-                   f"({t_lu:.1f} s); extrapolated {t_iter:.1f} s per LM trip"),
-        "seconds_per_trip": t_iter,
+        "value": 1.0 / t_tripP, "unit": "LM iters/sec", "cores": P, "kind": "port",
+        "sample": (f"oracle (C restatement, gcc -O3 -march=x86-64-v3 -ffp-contract=off) at m={m}, n={n}: "
+                   f"{k_eval} residual evals on 1 thread ({t_eval*1e3:.1f} ms each) and {2 * P} on {P} threads "
+                   f"({t_eval_par*1e3:.1f} ms each amortised), x{n + 2} per trip; {k_rows} rows of J^T J on 1 thread "
+                   f"({t_row*1e3:.1f} ms each) and {P} on {P} threads ({t_row_par*1e3:.1f} ms each amortised), x{n}; "
+                   f"LU at n={nl} scaled by (n/{nl})^3 ({t_lu:.1f} s); extrapolated {t_tripP:.1f} s per LM trip on "
+                   f"{P} threads, {t_trip1:.1f} s on 1"),
+        "seconds_per_trip": t_tripP, "seconds_per_trip_1_thread": t_trip1, "iters_per_s_1_thread": 1.0 / t_trip1,
+        "threads": P,
+        "bfgs_cpu_1_thread": {
+            "hg_n8192_s": t_hg, "hg_n8192_GBps": 8.0 * nh * nh / t_hg / 1e9,
+            "rank2_update_n4096_s": t_r2,
+            "reference_update_n512_s": t_n3, "reference_update_n4096_s_extrapolated": t_n3 * (4096 / n3) ** 3,
+        },
     }
 
 

@@ -68,6 +68,16 @@ class BFGSBndMPIParams(C.Structure):  # BFGSBnd_MPI::setParams, BFGS_with_bnd_li
 
 
 _lib = None
+FAST_PATH = os.path.join(HERE, "liboracle_fast.so")
+
+
+def use_fast():
+    """Switch this process to liboracle_fast.so: the same restatement built -O3 -march=x86-64-v3
+    (still -ffp-contract=off), for bench.py's timed CPU baseline."""
+    global _lib, LIB_PATH
+    LIB_PATH = FAST_PATH
+    _lib = None
+    return lib()
 
 
 def build() -> str:

@@ -207,3 +207,17 @@ def test_bfgs_bnd_rank2_form_tracks_reference_form_cfg5(oracle, n):
     assert nb <= dep1 <= nb + n // 50   # a coordinate frozen on the way down can end free
     assert len(t1) == r1.iters and np.all(np.diff(t1) <= 0)
     assert np.max(np.abs(X1 - _box_qp_solution(d, b, lb, ub))) <= 1e-4
+
+
+def test_oracle_asan_ubsan_clean():
+    """The CPU restatement under AddressSanitizer + UndefinedBehaviorSanitizer: every
+    algorithm -- BFGS (with initHessFD), the BFGS_MPI pools 1..8 (the reference's findPoolBounds
+    reads past a 1-entry pool; the restatement's clamp must hold), LM, the sharded FD Jacobian,
+    BFGS_Bnd (+ rank-2 form), BFGSBnd_MPI, BFGS_Bnd_MPI_SW, matrixInverse, the FD Hessian -- runs
+    without an out-of-bounds access, leak or undefined operation."""
+    import subprocess
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    subprocess.run(["make", "-s", "-C", here, "asan"], check=True, timeout=300)
+    r = subprocess.run([os.path.join(here, "_asan", "oracle_asan_check")], capture_output=True, timeout=300,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1"))
+    assert r.returncode == 0 and b"clean" in r.stdout, r.stderr.decode(errors="replace")[-3000:]

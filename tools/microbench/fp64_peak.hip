@@ -1,31 +1,49 @@
 // fp64 peak microbenchmark for gfx950: v_mfma_f64_16x16x4_f64 and VALU v_fma_f64 throughput
-// with independent accumulator chains on every SIMD (confirm the 78.6 TF
-// denominator).  Prints one JSON line.   hipcc --offload-arch=gfx950 -O3 fp64_peak.hip
+// (confirm the 78.6 TF denominator).  Prints one JSON line.
+//   hipcc --offload-arch=gfx950 -O3 fp64_peak.hip -o fp64_peak
+//
+// The sustained TFLOP/s of a saturating kernel depends on the clock the chip holds under that
+// load (DVFS), so every wave also records the shader clock counter (s_memtime) and the constant
+// 100 MHz reference (s_memrealtime) around its loop.  That gives the clock actually sustained
+// and the issue rate in flops per cycle per CU -- the hardware rate, which times the 2.4 GHz peak
+// clock is the spec-sheet peak.  Launch configurations sweep waves per SIMD and independent
+// accumulator chains so the rate is the MFMA pipe's, not a latency bound.
 #include <hip/hip_runtime.h>
+
 #include <cstdio>
+#include <vector>
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) void k_mfma(double* out, int iters, double a0) {
-    d4 acc[8];
+template <int CH>
+__global__ __launch_bounds__(256) void k_mfma(double* out, long long* clk, int iters, double a0) {
+    d4 acc[CH];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = (d4){0, 0, 0, 0};
+    for (int i = 0; i < CH; ++i) acc[i] = (d4){0, 0, 0, 0};
     double a = a0 + threadIdx.x * 1e-9, b = 1.0 - threadIdx.x * 1e-9;
+    const long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[i], 0, 0, 0);
+        for (int i = 0; i < CH; ++i) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[i], 0, 0, 0);
     }
     double s = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+    for (int i = 0; i < CH; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+    const long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) == 0) {
+        const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        clk[2 * w] = t1 - t0;
+        clk[2 * w + 1] = r1 - r0;
+    }
     if (s == 12345.678) out[0] = s;
 }
 
-__global__ __launch_bounds__(256) void k_valu(double* out, int iters, double a0) {
+__global__ __launch_bounds__(256) void k_valu(double* out, long long* clk, int iters, double a0) {
     double acc[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = i;
     const double a = a0 + threadIdx.x * 1e-12, b = 1.0 - 1e-12;
+    const long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[i] = fma(acc[i], b, a);
@@ -33,40 +51,88 @@ __global__ __launch_bounds__(256) void k_valu(double* out, int iters, double a0)
     double s = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) s += acc[i];
+    const long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) == 0) {
+        const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        clk[2 * w] = t1 - t0;
+        clk[2 * w + 1] = r1 - r0;
+    }
     if (s == 12345.678) out[0] = s;
 }
 
-int main() {
-    int dev = 0, ncu = 0;
-    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    double* out;
-    hipMalloc(&out, 8);
+struct Run {
+    double ms, tflops, clock_ghz, flops_per_cycle_cu;
+};
+
+// flop_per_wave: flops one wave executes in the timed launch
+template <class Launch>
+static Run run(Launch launch, int blocks, double flop_per_wave, int ncu, long long* dclk) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    const int blocks = ncu * 8;   // 8 WGs x 4 waves per CU = 8 waves per SIMD
-    const int it_m = 4000, it_v = 20000;
+    launch(10);   // warm
+    hipEventRecord(e0);
+    launch(-1);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
     float ms = 0;
-    // MFMA: per wave per iteration 8 x (16*16*4*2) flop
-    hipLaunchKernelGGL(k_mfma, dim3(blocks), dim3(256), 0, 0, out, 10, 1.0);
-    hipEventRecord(e0);
-    hipLaunchKernelGGL(k_mfma, dim3(blocks), dim3(256), 0, 0, out, it_m, 1.0);
-    hipEventRecord(e1);
-    hipEventSynchronize(e1);
     hipEventElapsedTime(&ms, e0, e1);
-    const double mf = (double)blocks * 4 * it_m * 8 * 2048.0;
-    const double tf_mfma = mf / (ms * 1e-3) / 1e12;
-    // VALU: per thread per iteration 16 fma = 32 flop
-    hipLaunchKernelGGL(k_valu, dim3(blocks), dim3(256), 0, 0, out, 10, 1.0);
-    hipEventRecord(e0);
-    hipLaunchKernelGGL(k_valu, dim3(blocks), dim3(256), 0, 0, out, it_v, 1.0);
-    hipEventRecord(e1);
-    hipEventSynchronize(e1);
-    float ms2 = 0;
-    hipEventElapsedTime(&ms2, e0, e1);
-    const double vf = (double)blocks * 256 * it_v * 32.0;
-    const double tf_valu = vf / (ms2 * 1e-3) / 1e12;
-    std::printf("{\"cus\": %d, \"mfma_f64_16x16x4_tflops\": %.2f, \"mfma_ms\": %.3f, \"valu_fma_f64_tflops\": %.2f, "
-                "\"valu_ms\": %.3f}\n", ncu, tf_mfma, ms, tf_valu, ms2);
+    const int waves = blocks * 4;
+    std::vector<long long> h(2 * (size_t)waves);
+    hipMemcpy(h.data(), dclk, sizeof(long long) * h.size(), hipMemcpyDeviceToHost);
+    double cyc = 0, real = 0;
+    for (int w = 0; w < waves; ++w) {
+        cyc += (double)h[2 * w];
+        real += (double)h[2 * w + 1];
+    }
+    cyc /= waves;                   // shader clocks per wave loop
+    real /= waves;                  // 100 MHz ticks per wave loop
+    Run r;
+    r.ms = ms;
+    r.tflops = flop_per_wave * waves / (ms * 1e-3) / 1e12;
+    r.clock_ghz = cyc / real * 0.1;
+    // every wave runs its loop concurrently (all resident): the chip's flops per shader cycle
+    r.flops_per_cycle_cu = flop_per_wave * waves / cyc / ncu;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    return r;
+}
+
+int main() {
+    int ncu = 0;
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
+    double* out;
+    long long* clk;
+    hipMalloc(&out, 8);
+    hipMalloc(&clk, sizeof(long long) * 2 * ncu * 64);
+    std::printf("{\"cus\": %d, \"mfma_f64_16x16x4\": [", ncu);
+    bool first = true;
+    double best_fpc = 0, best_tf = 0;
+    for (int wps : {1, 2, 4, 8}) {            // waves per SIMD (WGs of 4 waves per CU)
+        for (int ch : {4, 8}) {
+            const int blocks = ncu * wps;
+            const int iters = 4000 * 8 / ch;
+            auto launch = [&](int it) {
+                const int n = it < 0 ? iters : it;
+                if (ch == 4) hipLaunchKernelGGL(k_mfma<4>, dim3(blocks), dim3(256), 0, 0, out, clk, n, 1.0);
+                else hipLaunchKernelGGL(k_mfma<8>, dim3(blocks), dim3(256), 0, 0, out, clk, n, 1.0);
+            };
+            const Run r = run(launch, blocks, (double)iters * ch * 2048.0, ncu, clk);
+            if (r.flops_per_cycle_cu > best_fpc) best_fpc = r.flops_per_cycle_cu;
+            if (r.tflops > best_tf) best_tf = r.tflops;
+            std::printf("%s{\"waves_per_simd\": %d, \"chains\": %d, \"ms\": %.3f, \"tflops\": %.2f, \"clock_ghz\": %.3f, "
+                        "\"flops_per_cycle_per_cu\": %.1f}",
+                        first ? "" : ", ", wps, ch, r.ms, r.tflops, r.clock_ghz, r.flops_per_cycle_cu);
+            first = false;
+        }
+    }
+    auto vlaunch = [&](int it) {
+        hipLaunchKernelGGL(k_valu, dim3(ncu * 8), dim3(256), 0, 0, out, clk, it < 0 ? 20000 : it, 1.0);
+    };
+    const Run v = run(vlaunch, ncu * 8, 20000.0 * 16 * 2 * 64, ncu, clk);
+    std::printf("], \"valu_fma_f64\": {\"tflops\": %.2f, \"clock_ghz\": %.3f, \"flops_per_cycle_per_cu\": %.1f}, "
+                "\"mfma_best_sustained_tflops\": %.2f, \"mfma_flops_per_cycle_per_cu\": %.1f, "
+                "\"mfma_peak_tflops_at_2p4ghz\": %.2f}\n",
+                v.tflops, v.clock_ghz, v.flops_per_cycle_cu, best_tf, best_fpc, best_fpc * ncu * 2.4e9 / 1e12);
     return 0;
 }
