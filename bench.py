@@ -331,6 +331,12 @@ def cpu_baseline(m, n, budget_s=20.0):
 
 def main():
     args = _args()
+    # the ONE JSON line goes to the real stdout; everything else written to fd 1 -- the drop-in
+    # solvers' console messages (BFGS_Bnd prints one per boundary recursion, as the reference
+    # does), library logs -- goes to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
@@ -521,7 +527,8 @@ def main():
             "comm": {"backend": ("host-gloo" if args.host_comm else "rccl") if world > 1 else "none", "ranks": world},
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

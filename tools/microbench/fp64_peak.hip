@@ -15,16 +15,27 @@
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-template <int CH>
+// CH independent accumulators; each chain has its own A / B operand registers (DISTINCT), or
+// all chains share one pair
+template <int CH, bool DISTINCT = false>
 __global__ __launch_bounds__(256) void k_mfma(double* out, long long* clk, int iters, double a0) {
     d4 acc[CH];
+    double a[DISTINCT ? CH : 1], b[DISTINCT ? CH : 1];
 #pragma unroll
     for (int i = 0; i < CH; ++i) acc[i] = (d4){0, 0, 0, 0};
-    double a = a0 + threadIdx.x * 1e-9, b = 1.0 - threadIdx.x * 1e-9;
+#pragma unroll
+    for (int i = 0; i < (DISTINCT ? CH : 1); ++i) {
+        a[i] = a0 + threadIdx.x * 1e-9 + i * 1e-12;
+        b[i] = 1.0 - threadIdx.x * 1e-9 - i * 1e-12;
+    }
     const long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
-        for (int i = 0; i < CH; ++i) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[i], 0, 0, 0);
+        for (int i = 0; i < CH; ++i)   // accumulators pinned in VGPRs (the builtin's form moved
+                                       // every accumulator VGPR <-> AGPR each iteration)
+            asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0"
+                         : "+v"(acc[i])
+                         : "v"(a[DISTINCT ? i : 0]), "v"(b[DISTINCT ? i : 0]));
     }
     double s = 0;
 #pragma unroll
@@ -108,21 +119,27 @@ int main() {
     std::printf("{\"cus\": %d, \"mfma_f64_16x16x4\": [", ncu);
     bool first = true;
     double best_fpc = 0, best_tf = 0;
-    for (int wps : {1, 2, 4, 8}) {            // waves per SIMD (WGs of 4 waves per CU)
-        for (int ch : {4, 8}) {
+    for (int wps : {1, 2, 4}) {            // workgroups of 4 waves per CU = waves per SIMD requested
+        for (int var = 0; var < 4; ++var) {   // chains 4 / 8 / 16, 8 with distinct operands
+            const int ch = var == 0 ? 4 : (var == 2 ? 16 : 8);
+            const bool dist = var == 3;
             const int blocks = ncu * wps;
             const int iters = 4000 * 8 / ch;
             auto launch = [&](int it) {
                 const int n = it < 0 ? iters : it;
-                if (ch == 4) hipLaunchKernelGGL(k_mfma<4>, dim3(blocks), dim3(256), 0, 0, out, clk, n, 1.0);
-                else hipLaunchKernelGGL(k_mfma<8>, dim3(blocks), dim3(256), 0, 0, out, clk, n, 1.0);
+                if (var == 0) hipLaunchKernelGGL((k_mfma<4>), dim3(blocks), dim3(256), 0, 0, out, clk, n, 1.0);
+                else if (var == 1) hipLaunchKernelGGL((k_mfma<8>), dim3(blocks), dim3(256), 0, 0, out, clk, n, 1.0);
+                else if (var == 2) hipLaunchKernelGGL((k_mfma<16>), dim3(blocks), dim3(256), 0, 0, out, clk, n, 1.0);
+                else hipLaunchKernelGGL((k_mfma<8, true>), dim3(blocks), dim3(256), 0, 0, out, clk, n, 1.0);
             };
             const Run r = run(launch, blocks, (double)iters * ch * 2048.0, ncu, clk);
-            if (r.flops_per_cycle_cu > best_fpc) best_fpc = r.flops_per_cycle_cu;
+            // flops per shader cycle per CU from the kernel time and the clock the waves measured
+            const double fpc = r.tflops * 1e12 / (r.clock_ghz * 1e9) / ncu;
+            if (fpc > best_fpc) best_fpc = fpc;
             if (r.tflops > best_tf) best_tf = r.tflops;
-            std::printf("%s{\"waves_per_simd\": %d, \"chains\": %d, \"ms\": %.3f, \"tflops\": %.2f, \"clock_ghz\": %.3f, "
-                        "\"flops_per_cycle_per_cu\": %.1f}",
-                        first ? "" : ", ", wps, ch, r.ms, r.tflops, r.clock_ghz, r.flops_per_cycle_cu);
+            std::printf("%s{\"waves_per_simd\": %d, \"chains\": %d, \"distinct_operands\": %s, \"ms\": %.3f, "
+                        "\"tflops\": %.2f, \"clock_ghz\": %.3f, \"flops_per_cycle_per_cu\": %.1f}",
+                        first ? "" : ", ", wps, ch, dist ? "true" : "false", r.ms, r.tflops, r.clock_ghz, fpc);
             first = false;
         }
     }
@@ -133,6 +150,7 @@ int main() {
     std::printf("], \"valu_fma_f64\": {\"tflops\": %.2f, \"clock_ghz\": %.3f, \"flops_per_cycle_per_cu\": %.1f}, "
                 "\"mfma_best_sustained_tflops\": %.2f, \"mfma_flops_per_cycle_per_cu\": %.1f, "
                 "\"mfma_peak_tflops_at_2p4ghz\": %.2f}\n",
-                v.tflops, v.clock_ghz, v.flops_per_cycle_cu, best_tf, best_fpc, best_fpc * ncu * 2.4e9 / 1e12);
+                v.tflops, v.clock_ghz, v.tflops * 1e12 / (v.clock_ghz * 1e9) / ncu, best_tf, best_fpc,
+                best_fpc * ncu * 2.4e9 / 1e12);
     return 0;
 }
