@@ -565,6 +565,24 @@ __device__ __forceinline__ int diag_blk(int w, int s) {   // (ib << 2) | jb, or 
     return tab[w][s];
 }
 
+#ifdef PNOL_CHOL_TIMELINE
+// tools/microbench/chol_timeline.hip only: per launch k + 1 and workgroup class (0 diagonal,
+// 1 panel, 2 update): first start, last end (100 MHz realtime)
+__device__ unsigned long long g_chol_tl[64 * 3 * 2];
+__device__ unsigned long long g_chol_clk[64 * 8];   // the diagonal workgroup's shader-clock stamps
+#define PNOL_CHOL_STAMP(k, i) \
+    if (threadIdx.x == 0 && (k) + 1 < 64) g_chol_clk[8 * ((k) + 1) + (i)] = __builtin_amdgcn_s_memtime();
+__device__ __forceinline__ void chol_tl_mark(int k, int cls, unsigned long long t0) {
+    if (threadIdx.x == 0 && k + 1 < 64) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        atomicMin(&g_chol_tl[((k + 1) * 3 + cls) * 2], t0);
+        atomicMax(&g_chol_tl[((k + 1) * 3 + cls) * 2 + 1], t1);
+    }
+}
+#else
+#define PNOL_CHOL_STAMP(k, i)
+#endif
+
 // ---- one panel step ---------------------------------------------------------------------
 // Launch k (-1 <= k <= T-2), R = T-1-k.  blockIdx 0: the diagonal tile k+1; 1..R: panel rows
 // i = k+1 .. T-1; then the update tiles (i, j), k+1 <= j <= i, (i, j) != (k+1, k+1), by columns.
@@ -582,6 +600,9 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
     __shared__ int cnt[6];   // diagonal-tile phase words (factor_diag)
     __shared__ int ok_sh;
     const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), wr = wave >> 1, wc = wave & 1;
+#ifdef PNOL_CHOL_TIMELINE
+    const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime(), ck0 = __builtin_amdgcn_s_memtime();
+#endif
     if (k < 0 && blockIdx.x > 0) {   // prep: rows b-1, b-1+G, ... of P
         const int N = T * NB, G = gridDim.x - 1;
         for (int r = blockIdx.x - 1; r < N; r += G) {
@@ -621,9 +642,11 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
                                         : P[(long)(d0 + ib * 16 + (lane >> 4) + 4 * r) * ldp + d0 + jb * 16 + (lane & 15)];
             }
             __syncthreads();
+            PNOL_CHOL_STAMP(k, 1)
             d4 lst[4];
             diag_l_strip(lst, X, Y, wave, lane);        // L_{d,k} = A_{d,k} W_k^T, strip `wave`
             __syncthreads();
+            PNOL_CHOL_STAMP(k, 2)
             diag_strip_to_stage(lst, X, wave, lane);
             __syncthreads();
             const int frow = lane & 15, fk = lane >> 4;
@@ -651,14 +674,25 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
             }
         } else {
             const int row = t >> 2, c0 = (t & 3) * 16;
+            double v[16];   // all 16 loads in flight before the first LDS store (clamped addresses)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = A[(long)min(row, n - 1) * lda + min(c0 + q, n - 1)];
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int c = c0 + q;
-                diag_put(L, row, c, (row < n && c < n) ? A[(long)row * lda + c] : (row == c ? 1.0 : 0.0));
+                diag_put(L, row, c, (row < n && c < n) ? v[q] : (row == c ? 1.0 : 0.0));
             }
         }
         __syncthreads();
+        PNOL_CHOL_STAMP(k, 3)
         factor_diag(L, rinv, cnt, W + (long)d * NB * NB, d, info);
+        PNOL_CHOL_STAMP(k, 4)
+#ifdef PNOL_CHOL_TIMELINE
+        __syncthreads();
+        chol_tl_mark(k, 0, tl0);
+        if (threadIdx.x == 0 && k + 1 < 64) g_chol_clk[8 * (k + 1)] = ck0;
+        PNOL_CHOL_STAMP(k, 7)
+#endif
         return;
     }
 
@@ -694,6 +728,9 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
             bv[i0 + t] -= s;
             if (b == 1) zv[k0 + t] = zsh[t];
         }
+#ifdef PNOL_CHOL_TIMELINE
+        chol_tl_mark(k, 1, tl0);
+#endif
         return;
     }
 
@@ -721,6 +758,9 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
     __syncthreads();
     mfma_xyt<true>(acc, X, i != j ? Y : X, wr, wc, lane);
     acc_store(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
+#ifdef PNOL_CHOL_TIMELINE
+    chol_tl_mark(k, 2, tl0);
+#endif
 }
 
 // ---- backward substitution L^T x = z ------------------------------------------------------

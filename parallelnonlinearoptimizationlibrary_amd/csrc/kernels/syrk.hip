@@ -77,6 +77,12 @@ __device__ __forceinline__ void store_stage(const StageRegs<TILE, NT>& s, double
     for (int q = 0; q < NV; ++q) *reinterpret_cast<double2*>(dst + 2 * q) = s.v[q];
 }
 
+#ifdef PNOL_SYRK_TIMELINE
+// tools/microbench/syrk_timeline.hip only: per workgroup start / end (100 MHz realtime) and
+// the hardware ids of the CU it ran on
+__device__ unsigned long long g_syrk_tl[3 * 65536];
+#endif
+
 // MODE 0: write split-K partial tile to part; MODE 1: C = beta*C + alpha*acc (lower tiles);
 // MODE 4: 64 x 64 tiles into the 128 x 128 partial layout of MODE 0 (see the store below);
 // MODE 2: as MODE 0, instantiated separately for the chunked launches of launch_fd_jtj (so a
@@ -93,6 +99,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
     constexpr int NT = 64 * NW, WC = NW / 2;
     constexpr int WTM = TILE / 2, WTN = TILE / WC, NBM = WTM / 16, NBN = WTN / 16;
     __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
+#ifdef PNOL_SYRK_TIMELINE
+    const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
     // XMAP (split_k a multiple of 8): the K slices s = xcd, xcd + 8, ... go to the XCD that
     // dispatch slot blockIdx % 8 lands on, all tiles of one slice before the next, so the
@@ -153,6 +162,10 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
     }
     const int frow = lane & 15;
     const int fk = lane >> 4;
+    // a wave whose sub-tile of a diagonal tile lies wholly above the diagonal computes nothing
+    // (only the lower triangle and the diagonal are ever read from a diagonal tile); it still
+    // stages its share of every K slice for the other waves
+    const bool idle = diag && wc * WTN >= wr * WTM + WTM;
     for (int st = 0; st < nstages; ++st) {
         const int buf = st & 1;
         double* P = lds[buf][0];
@@ -166,6 +179,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
             load_stage<TILE, NT>(ps, X, ldx, nr, prow0, k0, kend, full);
             if (!diag) load_stage<TILE, NT>(qs, X, ldx, nr, qrow0, k0, kend, full);
         }
+        if (idle) continue;   // wave-uniform
 #pragma unroll
         for (int kk = 0; kk < kTK / 4; ++kk) {
             double a[NBM], b[NBN];
@@ -224,6 +238,16 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                     }
                 }
     }
+#ifdef PNOL_SYRK_TIMELINE
+    if (threadIdx.x == 0) {
+        const unsigned long long tl1 = __builtin_amdgcn_s_memrealtime();
+        const unsigned hw = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));     // HW_ID
+        const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11));    // XCC_ID
+        g_syrk_tl[3 * blockIdx.x] = tl0;
+        g_syrk_tl[3 * blockIdx.x + 1] = tl1;
+        g_syrk_tl[3 * blockIdx.x + 2] = ((unsigned long long)xcc << 32) | hw;
+    }
+#endif
 }
 
 // ---- the m-slice summation tree ------------------------------------------------------------
