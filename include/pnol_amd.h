@@ -170,9 +170,11 @@ int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const do
  * method 0 = auto (n <= PNOL_SEQ_MAX: reference LU; else method 4, LU on a non-positive
  * pivot), 1 = Cholesky (per-panel launches), 2 = LU with partial pivoting (reference operation
  * order), 3 = Cholesky as one persistent tile-DAG launch (experimental), 4 = lookahead tile
- * Cholesky with diagonal-tile inverses, one launch per panel, forward solve folded in.
- * Methods 1 and 3 consume A (overwritten by its factor); method 4 factors a padded copy and
- * leaves A intact.  info (host, nullable) gets the method family used (1 = Cholesky, 2 = LU)
+ * Cholesky with diagonal-tile inverses, one launch per panel, forward solve folded in, 5 = the
+ * same factorisation (bitwise) as one persistent launch: one workgroup runs the diagonal chain,
+ * the others take the panel / update tiles from an ordered queue (the default of method 0;
+ * PNOL_CHOL_PERSIST=0 makes method 0 use 4).  Methods 1 and 3 consume A (overwritten by its
+ * factor); methods 4 and 5 factor a padded copy and leave A intact.  info (host, nullable) gets the method family used (1 = Cholesky, 2 = LU)
  * or -1 on a singular matrix. */
 int pnol_solve_d(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n,
                  int method, int* info);

@@ -229,7 +229,7 @@ int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const do
 
 int pnol_solve_d(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n, int method, int* info) {
     PNOL_CHECK(set_device(ctx));
-    if (method < 0 || method > 4) return PNOL_ERR_ARG;
+    if (method < 0 || method > 5) return PNOL_ERR_ARG;
     ScopedTimer tm(ctx, "solve");
     return launch_solve(ctx, A, lda, rhs, sigma, n, method, info);
 }

@@ -50,15 +50,47 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
     return fma(r * e, p, r);
 }
 
+// SC1: the persistent form's hand-offs between workgroups use sc1 (relaxed agent-scope atomic)
+// loads and stores for every handed-off byte instead of release / acquire fences
+// (MI355X_MICROARCH.md "Valid forms", table row 1: one workgroup per CU, every storing wave's
+// vmcnt(0) wait before the workgroup barrier and the one sc1 flag store).
+template <bool SC1>
+__device__ __forceinline__ double ldg(const double* p) {
+    if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <bool SC1>
+__device__ __forceinline__ void stg(double* p, double v) {
+    if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+// 16-byte sc1 load at byte offset `off` from a wave-uniform base (buffer_load_dwordx4 ... sc1;
+// 0x00020000: the gfx9 raw-buffer descriptor word 3, 32-bit data format)
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ double2 ld16_sc1(const double* base, unsigned off) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+    const v4i_t v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+    return __builtin_bit_cast(double2, v);
+}
+
 // Stage the 64 x 64 tile at (r0, c0) of P into four 64 x 16 substages (row stride kPad):
-// thread t owns row t >> 2 and the 16 columns of substage t & 3 (eight 16-byte loads).
+// thread t owns row t >> 2 and the 16 columns of substage t & 3 (eight 16-byte loads; SC1:
+// sixteen 8-byte sc1 loads).
+template <bool SC1 = false>
 __device__ __forceinline__ void stage_tile(double* __restrict__ dst, const double* __restrict__ P, long ldp, int r0,
                                            int c0) {
     const int t = threadIdx.x, row = t >> 2, sub = t & 3;
-    const double2* src = reinterpret_cast<const double2*>(P + (long)(r0 + row) * ldp + c0 + sub * 16);
     double2 v[8];
+    if constexpr (SC1) {
+        const double* base = P + (long)r0 * ldp + c0;   // wave-uniform
+        const unsigned off = (unsigned)((row * ldp + sub * 16) * 8);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = src[q];
+        for (int q = 0; q < 8; ++q) v[q] = ld16_sc1(base, off + 16 * q);
+    } else {
+        const double2* src = reinterpret_cast<const double2*>(P + (long)(r0 + row) * ldp + c0 + sub * 16);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = src[q];
+    }
     double2* d = reinterpret_cast<double2*>(dst + sub * kSub + row * kPad);
 #pragma unroll
     for (int q = 0; q < 8; ++q) d[q] = v[q];
@@ -102,6 +134,7 @@ __device__ __forceinline__ void acc_zero(d4 (&acc)[2][2]) {
         for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
 }
 
+template <bool SC1 = false>
 __device__ __forceinline__ void acc_load(d4 (&acc)[2][2], const double* __restrict__ P, long ldp, int r0, int c0,
                                          int wr, int wc, int lane) {
 #pragma unroll
@@ -110,9 +143,10 @@ __device__ __forceinline__ void acc_load(d4 (&acc)[2][2], const double* __restri
         for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                acc[mi][ni][r] = P[(long)(r0 + acc_row(wr, mi, lane, r)) * ldp + c0 + acc_col(wc, ni, lane)];
+                acc[mi][ni][r] = ldg<SC1>(P + (long)(r0 + acc_row(wr, mi, lane, r)) * ldp + c0 + acc_col(wc, ni, lane));
 }
 
+template <bool SC1 = false>
 __device__ __forceinline__ void acc_store(const d4 (&acc)[2][2], double* __restrict__ P, long ldp, int r0, int c0,
                                           int wr, int wc, int lane) {
 #pragma unroll
@@ -121,7 +155,7 @@ __device__ __forceinline__ void acc_store(const d4 (&acc)[2][2], double* __restr
         for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                P[(long)(r0 + acc_row(wr, mi, lane, r)) * ldp + c0 + acc_col(wc, ni, lane)] = acc[mi][ni][r];
+                stg<SC1>(P + (long)(r0 + acc_row(wr, mi, lane, r)) * ldp + c0 + acc_col(wc, ni, lane), acc[mi][ni][r]);
 }
 
 // accumulator -> LDS in the substage layout (the tile as the X operand of the next product)
@@ -421,7 +455,7 @@ __device__ __forceinline__ void diag_put(const DiagLds& L, int row, int col, dou
 
 // Factor the tile held in L.Sl / L.S22 and write W_d = L_dd^{-1} (64 x 64 row-major) to Wd.
 // STAMP: s_memtime stamps of the phases into st[0..31] (tools/microbench/diag_timing.hip only)
-template <bool STAMP = false>
+template <bool STAMP = false, bool SC1 = false>
 __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict__ rinv, int* cnt,
                                             double* __restrict__ Wd, int d, int* info, long long* st = nullptr) {
     const int t = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
@@ -510,7 +544,7 @@ __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict
         acc = mfma_blk<kHalf>(acc, [&](int i, int k) { return -L.W22[(qi * 16 + i) * kS + k]; },
                               [&](int j, int k) { return L.Tl[k * kHalf + qj * 16 + j]; }, lane);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Wd[(kHalf + qi * 16 + (lane >> 4) + 4 * r) * NB + qj * 16 + (lane & 15)] = acc[r];
+        for (int r = 0; r < 4; ++r) stg<SC1>(Wd + (kHalf + qi * 16 + (lane >> 4) + 4 * r) * NB + qj * 16 + (lane & 15), acc[r]);
     }
     if constexpr (STAMP) if (wave == 0) st[16] = __builtin_amdgcn_s_memtime();
     // W11, W22 and the zero upper-right block: thread t writes columns (t & 31) of rows t >> 5 + 8 q
@@ -519,9 +553,9 @@ __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int r = r0 + 8 * q;
-            Wd[r * NB + c] = L.W11[r * kS + c];
-            Wd[r * NB + kHalf + c] = 0.0;
-            Wd[(kHalf + r) * NB + kHalf + c] = L.W22[r * kS + c];
+            stg<SC1>(Wd + r * NB + c, L.W11[r * kS + c]);
+            stg<SC1>(Wd + r * NB + kHalf + c, 0.0);
+            stg<SC1>(Wd + (kHalf + r) * NB + kHalf + c, L.W22[r * kS + c]);
         }
     }
 }
@@ -583,6 +617,59 @@ __device__ __forceinline__ void chol_tl_mark(int k, int cls, unsigned long long 
 #define PNOL_CHOL_STAMP(k, i)
 #endif
 
+// The diagonal tile d = k + 1 (k >= 0) ready for factor_diag: L = A_{d,k} W_k^T (recomputed
+// here rather than waited for), A_dd - L L^T on its 10 lower 16 x 16 blocks, into the split LDS
+// copy L.  X / Y: the two staging areas (smem, smem + kStage).
+template <bool SC1 = false>
+__device__ __forceinline__ void diag_prepare(const double* __restrict__ P, long ldp, const double* __restrict__ W,
+                                             int k, double* __restrict__ X, double* __restrict__ Y, const DiagLds& L,
+                                             int wave, int lane) {
+    const int d0 = (k + 1) * NB;
+    const int k0 = k * NB;
+    stage_tile<SC1>(X, P, ldp, d0, k0);
+    stage_tile<SC1>(Y, W + (long)k * NB * NB, NB, 0, 0);
+    d4 cdd[3];   // this wave's lower blocks of A_dd, in flight during the first product
+#pragma unroll
+    for (int sb = 0; sb < 3; ++sb) {
+        const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            cdd[sb][r] = bl < 0 ? 0.0
+                                : ldg<SC1>(P + (long)(d0 + ib * 16 + (lane >> 4) + 4 * r) * ldp + d0 + jb * 16 + (lane & 15));
+    }
+    __syncthreads();
+    PNOL_CHOL_STAMP(k, 1)
+    d4 lst[4];
+    diag_l_strip(lst, X, Y, wave, lane);        // L_{d,k} = A_{d,k} W_k^T, strip `wave`
+    __syncthreads();
+    PNOL_CHOL_STAMP(k, 2)
+    diag_strip_to_stage(lst, X, wave, lane);
+    __syncthreads();
+    const int frow = lane & 15, fk = lane >> 4;
+#pragma unroll
+    for (int sb = 0; sb < 3; ++sb) {           // A_dd - L L^T, lower blocks
+        const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
+        if (bl < 0) continue;                   // wave-uniform
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const double a = -X[kb * kSub + (ib * 16 + frow) * kPad + kk * 4 + fk];
+                const double b = X[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
+                cdd[sb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, cdd[sb], 0, 0, 0);
+            }
+    }
+    __syncthreads();                            // X / Y are rewritten below
+#pragma unroll
+    for (int sb = 0; sb < 3; ++sb) {
+        const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
+        if (bl < 0) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            diag_put(L, ib * 16 + (lane >> 4) + 4 * r, jb * 16 + (lane & 15), cdd[sb][r]);
+    }
+}
+
 // ---- one panel step ---------------------------------------------------------------------
 // Launch k (-1 <= k <= T-2), R = T-1-k.  blockIdx 0: the diagonal tile k+1; 1..R: panel rows
 // i = k+1 .. T-1; then the update tiles (i, j), k+1 <= j <= i, (i, j) != (k+1, k+1), by columns.
@@ -593,7 +680,8 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
                                                    int T, int k, double* __restrict__ W, double* __restrict__ bv,
                                                    double* __restrict__ zv, int* __restrict__ rowflag, int epoch,
                                                    int* __restrict__ info, const double* __restrict__ A, long lda,
-                                                   int n, const double* __restrict__ rhs) {
+                                                   int n, const double* __restrict__ rhs, int* __restrict__ pflags,
+                                                   int npflags) {
     __shared__ __attribute__((aligned(16))) double smem[2 * kStage];   // 73.7 KB
     __shared__ double rinv[NB];
     __shared__ double zsh[NB];
@@ -612,6 +700,8 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
         }
         if (blockIdx.x == 1)
             for (int r = t; r < N; r += 256) bv[r] = r < n ? rhs[r] : 0.0;
+        if (blockIdx.x == gridDim.x - 1)   // the persistent form's progress words (k_chol_persist)
+            for (int q = t; q < npflags; q += 256) pflags[q] = 0;
         return;
     }
     if (k < 0) {
@@ -629,49 +719,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
         const DiagLds L = diag_lds(smem);
         if (t < 6) cnt[t] = 0;
         if (k >= 0) {
-            const int k0 = k * NB;
-            stage_tile(X, P, ldp, d0, k0);
-            stage_tile(Y, W + (long)k * NB * NB, NB, 0, 0);
-            d4 cdd[3];   // this wave's lower blocks of A_dd, in flight during the first product
-#pragma unroll
-            for (int sb = 0; sb < 3; ++sb) {
-                const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    cdd[sb][r] = bl < 0 ? 0.0
-                                        : P[(long)(d0 + ib * 16 + (lane >> 4) + 4 * r) * ldp + d0 + jb * 16 + (lane & 15)];
-            }
-            __syncthreads();
-            PNOL_CHOL_STAMP(k, 1)
-            d4 lst[4];
-            diag_l_strip(lst, X, Y, wave, lane);        // L_{d,k} = A_{d,k} W_k^T, strip `wave`
-            __syncthreads();
-            PNOL_CHOL_STAMP(k, 2)
-            diag_strip_to_stage(lst, X, wave, lane);
-            __syncthreads();
-            const int frow = lane & 15, fk = lane >> 4;
-#pragma unroll
-            for (int sb = 0; sb < 3; ++sb) {           // A_dd - L L^T, lower blocks
-                const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
-                if (bl < 0) continue;                   // wave-uniform
-#pragma unroll
-                for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-                    for (int kk = 0; kk < 4; ++kk) {
-                        const double a = -X[kb * kSub + (ib * 16 + frow) * kPad + kk * 4 + fk];
-                        const double b = X[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
-                        cdd[sb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, cdd[sb], 0, 0, 0);
-                    }
-            }
-            __syncthreads();                            // X / Y are rewritten below
-#pragma unroll
-            for (int sb = 0; sb < 3; ++sb) {
-                const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
-                if (bl < 0) continue;
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    diag_put(L, ib * 16 + (lane >> 4) + 4 * r, jb * 16 + (lane & 15), cdd[sb][r]);
-            }
+            diag_prepare(P, ldp, W, k, X, Y, L, wave, lane);
         } else {
             const int row = t >> 2, c0 = (t & 3) * 16;
             double v[16];   // all 16 loads in flight before the first LDS store (clamped addresses)
@@ -763,6 +811,178 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
 #endif
 }
 
+// ---- the persistent form (method 5) --------------------------------------------------------
+// The steps k = 0 .. T-2 of k_chol_step as ONE launch after the prep launch (k = -1, which also
+// factors tile 0 and zeroes the progress words):
+//   blockIdx 0     the diagonal chain: for d = 1 .. T-1, once tiles (d, d-1) and (d, d) hold
+//                  the updates of columns < d-1, diag_prepare + factor_diag -> W_d, published;
+//                  no launch boundary and no wait for the rest of step d-1's work;
+//   blockIdx >= 1  workers taking tasks from an atomic counter in step order -- step k's panel
+//                  rows i = k+1 .. T-1, then its update tiles by columns (the same task set as
+//                  the blocks of launch k) -- each waiting only on tasks handed out before it, or
+//                  on the diagonal chain, which itself waits only on tasks of steps <= d-2: the
+//                  queue drains without any assumption on co-residency.
+// Progress words (int, zeroed by the prep): wdone[d] (W_d published), lcnt[i] (panels of row i
+// stored in Lm), bcnt[i] (forward-substitution updates applied to b_i), ver[i * T + j] (update
+// steps applied to tile (i, j)); plus the task counter.  Hand-offs without fences: every byte
+// another workgroup reads (P, Lm, W, b) is stored and loaded sc1, every storing wave waits
+// vmcnt(0) before the workgroup barrier behind which one lane stores the word (sc1), and the
+// consumer's lane 0 polls it with sc1 loads before a barrier (MI355X_MICROARCH.md "Valid forms",
+// row 1; one workgroup per CU: __launch_bounds__(256, 1) and the register count).  Every tile, panel and b update is the same arithmetic in the same order as in
+// the per-step launches, so the result is bitwise method 4's.
+struct PersistWords {
+    int *wdone, *lcnt, *bcnt, *ver, *counter;
+};
+__device__ __forceinline__ PersistWords persist_words(int* f, int T) {
+    return {f, f + T, f + 2 * T, f + 3 * T, f + 3 * T + T * T};
+}
+
+// publish `v` into *w after every wave's (sc1) stores of this workgroup have completed
+__device__ __forceinline__ void publish(int* w, int v) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P, double* __restrict__ Lm, long ldp,
+                                                      int T, double* __restrict__ W, double* __restrict__ bv,
+                                                      double* __restrict__ zv, int* __restrict__ flags, int ntasks,
+                                                      int* __restrict__ info) {
+    __shared__ __attribute__((aligned(16))) double smem[2 * kStage];   // 73.7 KB
+    __shared__ double rinv[NB];
+    __shared__ double zsh[NB];
+    __shared__ int cnt[6];
+    __shared__ int task_sh, ok_sh;
+    const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), wr = wave >> 1, wc = wave & 1;
+    const PersistWords pw = persist_words(flags, T);
+    double* X = smem;
+    double* Y = smem + kStage;
+
+    if (blockIdx.x == 0) {   // ---------------- the diagonal chain
+        for (int d = 1; d < T; ++d) {
+            const int k = d - 1;
+#ifdef PNOL_CHOL_TIMELINE
+            const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime(), ck0 = __builtin_amdgcn_s_memtime();
+#endif
+            if (t == 0) {
+                const bool ok = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+                                spin_ge(pw.ver + d * T + k, k, info) && spin_ge(pw.ver + d * T + d, k, info);
+                ok_sh = ok;
+            }
+            __syncthreads();
+            if (!ok_sh) return;
+            PNOL_CHOL_STAMP(k, 5)
+            const DiagLds L = diag_lds(smem);
+            if (t < 6) cnt[t] = 0;
+            diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane);
+            __syncthreads();
+            PNOL_CHOL_STAMP(k, 3)
+            factor_diag<false, true>(L, rinv, cnt, W + (long)d * NB * NB, d, info);
+            PNOL_CHOL_STAMP(k, 4)
+            publish(pw.wdone + d, 1);   // its barrier also ends every read of this step's LDS
+#ifdef PNOL_CHOL_TIMELINE
+            chol_tl_mark(k, 0, tl0);
+            if (threadIdx.x == 0 && k + 1 < 64) g_chol_clk[8 * (k + 1)] = ck0;
+            PNOL_CHOL_STAMP(k, 7)
+#endif
+        }
+        return;
+    }
+
+    for (;;) {   // ---------------- workers
+        if (t == 0) task_sh = atomicAdd(pw.counter, 1);
+        __syncthreads();
+        int g = task_sh;
+        __syncthreads();   // task_sh is rewritten by the next claim
+        if (g >= ntasks) return;
+        int k = 0, R = T - 1;
+        for (;;) {   // step k holds R panel rows and R (R + 1) / 2 - 1 update tiles
+            const int S = R + R * (R + 1) / 2 - 1;
+            if (g < S) break;
+            g -= S;
+            ++k;
+            --R;
+        }
+        const int k0 = k * NB;
+        if (g < R) {   // ---- panel row i: L_ik = A_ik W_k^T, then b_i -= L_ik (W_k b_k)
+            const int i = k + 1 + g, i0 = i * NB;
+#ifdef PNOL_CHOL_TIMELINE
+            const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
+#endif
+            if (t == 0) {
+                // W_k (tile 0 comes from the prep launch), A_ik through column k-1, b_k complete,
+                // and b_i's earlier updates
+                const bool ok = (k == 0 || spin_ge(pw.wdone + k, 1, info)) && spin_ge(pw.ver + i * T + k, k, info) &&
+                                spin_ge(pw.bcnt + k, k, info) && spin_ge(pw.bcnt + i, k, info);
+                ok_sh = ok;
+            }
+            __syncthreads();
+            if (!ok_sh) return;
+            stage_tile<true>(X, P, ldp, i0, k0);
+            stage_tile<true>(Y, W + (long)k * NB * NB, NB, 0, 0);
+            __syncthreads();
+            d4 acc[2][2];
+            acc_zero(acc);
+            mfma_xyt<false>(acc, X, Y, wr, wc, lane);
+            acc_store<true>(acc, Lm, ldp, i0, k0, wr, wc, lane);
+            publish(pw.lcnt + i, k + 1);
+            acc_to_rows(acc, X, wr, wc, lane);   // X is free (the MFMA finished before the barrier)
+            if (t < NB) {
+                double s = 0.0;
+#pragma unroll 16
+                for (int j = 0; j < NB; ++j) s = fma(Y[(j >> 4) * kSub + t * kPad + (j & 15)], ldg<true>(bv + k0 + j), s);
+                zsh[t] = s;
+            }
+            __syncthreads();
+            if (t < NB) {
+                double s = 0.0;
+#pragma unroll 16
+                for (int j = 0; j < NB; ++j) s = fma(X[t * (NB + 1) + j], zsh[j], s);
+                stg<true>(bv + i0 + t, ldg<true>(bv + i0 + t) - s);
+                if (i == k + 1) stg<true>(zv + k0 + t, zsh[t]);
+            }
+            publish(pw.bcnt + i, k + 1);
+#ifdef PNOL_CHOL_TIMELINE
+            chol_tl_mark(k, 1, tl0);
+#endif
+            continue;
+        }
+        // ---- update tile (i, j) -= L_ik L_jk^T.  Full column order f: column k+1 holds
+        // f = 0 .. R-1 (tile (k+1+f, k+1); f = 0 is the diagonal chain's), column k+2 starts with
+        // (k+2, k+2) at f = R, and so on.  Step k's first two tasks are the tiles the chain needs
+        // next, f = 1 = (k+2, k+1) and f = R = (k+2, k+2); the rest follow in column order.
+        const int q = g - R;
+        int u = q == 0 ? 1 : (q == 1 ? R : (q < R ? q : q + 1));
+        int j = k + 1;
+        while (u >= T - j) {
+            u -= T - j;
+            ++j;
+        }
+        const int i = j + u;
+#ifdef PNOL_CHOL_TIMELINE
+        const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
+#endif
+        if (t == 0) {
+            const bool ok = spin_ge(pw.lcnt + i, k + 1, info) && spin_ge(pw.lcnt + j, k + 1, info) &&
+                            spin_ge(pw.ver + i * T + j, k, info);
+            ok_sh = ok;
+        }
+        __syncthreads();
+        if (!ok_sh) return;
+        stage_tile<true>(X, Lm, ldp, i * NB, k0);
+        if (i != j) stage_tile<true>(Y, Lm, ldp, j * NB, k0);
+        d4 acc[2][2];
+        acc_load<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
+        __syncthreads();
+        mfma_xyt<true>(acc, X, i != j ? Y : X, wr, wc, lane);
+        acc_store<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
+        publish(pw.ver + i * T + j, k + 1);
+#ifdef PNOL_CHOL_TIMELINE
+        chol_tl_mark(k, 2, tl0);
+#endif
+    }
+}
+
 // ---- backward substitution L^T x = z ------------------------------------------------------
 // Workgroup b owns block w = T-1-b.  For c = T-1 .. w+1 it waits for x_c (flag), accumulating
 // s_w += L_cw^T x_c with the next L_cw tile prefetched; then x_w = W_w^T (z_w - s_w).
@@ -844,7 +1064,21 @@ __global__ void k_flag_info(int* info, int v) { *info = v; }
 
 // Solve A sigma = rhs (A SPD, untouched) by the lookahead tile Cholesky; *dinfo (device) != 0
 // afterwards when a pivot failed or a chain timed out.
+// PNOL_CHOL_PERSIST = 0 / 1 (read per call: the tests switch it) selects the per-step launches
+// (method 4) or the persistent form; `variant` 4 / 5 forces one.
+static bool chol_persistent(int variant) {
+    if (variant == 4) return false;
+    if (variant == 5) return true;
+    const char* e = std::getenv("PNOL_CHOL_PERSIST");
+    return e ? std::atoi(e) != 0 : true;
+}
+
 int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo) {
+    return launch_chol_solve_v(ctx, A, lda, rhs, sigma, n, dinfo, 0);
+}
+
+int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo,
+                        int variant) {
     const int T = (n + NB - 1) / NB, N = T * NB;
     const long ldp = N;
     void *P = nullptr, *Lm = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr;
@@ -865,13 +1099,31 @@ int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs
     }
     int* rowflag = ctx->chol4_flags;
     int* bwdflag = ctx->chol4_flags + ctx->chol4_cap;
-    for (int k = -1; k <= T - 2; ++k) {
+    const bool persist = chol_persistent(variant) && T >= 2;
+    void* pf = nullptr;
+    const int npf = 3 * T + T * T + 1;
+    if (persist) PNOL_CHECK(ws_get(ctx, "chol5_words", sizeof(int) * (size_t)npf, &pf));
+    for (int k = -1; k <= (persist ? -1 : T - 2); ++k) {
         const int R = T - 1 - k;
-        const int grid = k < 0 ? 1 + std::min(N, 1024) : R + R * (R + 1) / 2;
+        const int grid = k < 0 ? 2 + std::min(N, 1024) : R + R * (R + 1) / 2;
         const int epoch = ++ctx->chol4_epoch;
         hipLaunchKernelGGL(k_chol_step, dim3(grid), dim3(256), 0, ctx->stream, (double*)P, (double*)Lm, ldp, T, k,
-                           (double*)W,
-                           (double*)bv, (double*)zv, rowflag, epoch, dinfo, A, (long)lda, n, rhs);
+                           (double*)W, (double*)bv, (double*)zv, rowflag, epoch, dinfo, A, (long)lda, n, rhs,
+                           (int*)pf, persist ? npf : 0);
+    }
+    if (persist) {
+        int ntasks = 0;
+        for (int R = T - 1; R >= 1; --R) ntasks += R + R * (R + 1) / 2 - 1;
+        // tuning knobs (read per call): PNOL_CHOL5_WORKERS = worker workgroups, PNOL_CHOL5_SOLO = 1:
+        // a dynamic LDS pad so no two workgroups share a CU (the diagonal chain runs alone)
+        const char* ew = std::getenv("PNOL_CHOL5_WORKERS");
+        const char* es = std::getenv("PNOL_CHOL5_SOLO");
+        const bool solo = es && std::atoi(es) != 0;
+        const int slots = (solo ? 1 : 2) * std::max(ctx->num_cu, 1) - 1;
+        const int want = ew ? std::atoi(ew) : slots;
+        const int workers = std::max(1, std::min(ntasks, want));
+        hipLaunchKernelGGL(k_chol_persist, dim3(1 + workers), dim3(256), solo ? 16384 : 0, ctx->stream, (double*)P,
+                           (double*)Lm, ldp, T, (double*)W, (double*)bv, (double*)zv, (int*)pf, ntasks, dinfo);
     }
     const int epoch = ++ctx->chol4_epoch;
     hipLaunchKernelGGL(k_chol_bwd, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n, (const double*)W,

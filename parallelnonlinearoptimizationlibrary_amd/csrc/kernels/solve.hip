@@ -815,10 +815,14 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
     PNOL_CHECK(ws_get(ctx, "solve_info", sizeof(int) * 4, &dinfo_v));
     int* dinfo = (int*)dinfo_v;
     int used = 0;
-    if (method == 0) method = (n <= PNOL_SEQ_MAX) ? 2 : 4;
-    if (method == 4) {
+    int variant = method;   // the tile Cholesky's form: 4 per-step launches, 5 persistent
+    if (method == 0) {
+        method = (n <= PNOL_SEQ_MAX) ? 2 : 4;
+        variant = 0;         // the default form (launch_chol_solve_v)
+    }
+    if (method == 4 || method == 5) {
         // lookahead tile Cholesky with diagonal inverses (chol.hip); A itself is not modified
-        PNOL_CHECK(launch_chol_solve(ctx, A, lda, rhs, sigma, n, dinfo));
+        PNOL_CHECK(launch_chol_solve_v(ctx, A, lda, rhs, sigma, n, dinfo, variant));
         int hinfo = 0;
         PNOL_HIP(hipMemcpyAsync(&hinfo, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
         PNOL_HIP(hipStreamSynchronize(ctx->stream));

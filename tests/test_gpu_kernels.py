@@ -231,7 +231,7 @@ def test_cholesky_solve(ctx, n, method):
     assert np.linalg.norm(_np(sigma) - x) <= 1e-10 * np.linalg.norm(x) * np.linalg.cond(A)
 
 
-@pytest.mark.parametrize("method", [1, 3, 4])
+@pytest.mark.parametrize("method", [1, 3, 4, 5])
 def test_cholesky_odd_leading_dimension(ctx, method):
     """Odd lda: scalar staging paths (no 16-byte loads)."""
     rng = np.random.default_rng(77)
@@ -247,7 +247,7 @@ def test_cholesky_odd_leading_dimension(ctx, method):
     assert np.linalg.norm(_np(sigma) - x) <= 1e-10 * np.linalg.norm(x) * np.linalg.cond(A)
 
 
-@pytest.mark.parametrize("method", [1, 4])
+@pytest.mark.parametrize("method", [1, 4, 5])
 def test_cholesky_repeated_solves_reuse_ready_flags(ctx, method):
     """The flag-chained solves tag each call with a new epoch; sizes that grow and shrink (the
     flag buffer is reallocated) and back-to-back calls must all be exact."""
@@ -297,10 +297,12 @@ def test_cholesky_m4_keeps_A_and_matches_per_panel(ctx):
         assert np.linalg.norm(_np(s) - x) <= 1e-12 * np.linalg.norm(x) * c
 
 
-def test_cholesky_m4_bitwise_under_contention(ctx):
-    """Method 4 hands tiles between workgroups of one launch through flags; its result must not
-    depend on scheduling.  Large GEMMs on a second stream perturb which workgroups run when;
-    every solve must equal the solo solve bitwise."""
+@pytest.mark.parametrize("method", [4, 5])
+def test_cholesky_m4_bitwise_under_contention(ctx, method):
+    """Methods 4 and 5 hand tiles between workgroups through flags (5: the whole factorisation
+    in one launch, tasks from a queue); the result must not depend on scheduling.  Large GEMMs
+    on a second stream perturb which workgroups run when; every solve must equal the solo
+    solve bitwise, and both forms give the same bits."""
     import torch
     rng = np.random.default_rng(21)
     n = 1500
@@ -317,10 +319,31 @@ def test_cholesky_m4_bitwise_under_contention(ctx):
         with torch.cuda.stream(side):
             for _ in range(3):
                 X = (X @ X) * 1e-3
-        sigma, info = ctx.solve(At, bt, method=4)
+        sigma, info = ctx.solve(At, bt, method=method)
         assert info == 1
         assert np.array_equal(_np(sigma), ref), rep
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("n", [65, 128, 300, 1000, 2048, 2111])
+def test_cholesky_persistent_equals_per_step_launches(ctx, n):
+    """Method 5 (one persistent launch: the diagonal chain in one workgroup, panels and updates
+    from an ordered task queue) performs every tile operation of method 4 in the same order:
+    sigma is bitwise equal, A is left intact, and method 0 (auto) uses it by default."""
+    rng = np.random.default_rng(n)
+    J = rng.standard_normal((n + 40, n))
+    A = J.T @ J + 0.5 * np.eye(n)
+    b = rng.standard_normal(n)
+    At, bt = ctx.tensor(A), ctx.tensor(b)
+    s4, i4 = ctx.solve(At, bt, method=4)
+    s5, i5 = ctx.solve(At, bt, method=5)
+    s0, i0 = ctx.solve(At, bt, method=0)
+    assert i4 == i5 == i0 == 1
+    assert np.array_equal(_np(At), A)
+    assert np.array_equal(_np(s5), _np(s4))
+    assert np.array_equal(_np(s0), _np(s4))
+    x = np.linalg.solve(A, b)
+    assert np.linalg.norm(_np(s5) - x) <= 1e-10 * np.linalg.norm(x) * np.linalg.cond(A)
 
 
 @pytest.mark.parametrize("n", [200, 1000])

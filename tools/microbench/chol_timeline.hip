@@ -52,8 +52,10 @@ int main(int argc, char** argv) {
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     float ms[6];
+    std::vector<unsigned long long> zero(64 * 8, 0);
     for (int r = 0; r < 6; ++r) {
         hipStreamSynchronize(ctx->stream);
+        hipMemcpyToSymbol(HIP_SYMBOL(g_chol_clk), zero.data(), sizeof(unsigned long long) * zero.size());
         hipMemcpyToSymbol(HIP_SYMBOL(g_chol_tl), init.data(), sizeof(unsigned long long) * init.size());
         hipEventRecord(e0, ctx->stream);
         if (launch_chol_solve(ctx, A, n, b, x, n, info) != PNOL_OK) return 1;
@@ -81,7 +83,7 @@ int main(int argc, char** argv) {
         sum_gap += gap;
         std::printf("%s{\"k\": %d, \"diag\": [%.2f, %.2f], \"panel\": [%.2f, %.2f], \"update\": [%.2f, %.2f], "
                     "\"gap_to_next_diag\": %.2f, \"diag_cycles\": %llu, \"diag_clock_ghz\": %.3f, "
-                    "\"stamps\": [%lld, %lld, %lld, %lld, %lld]}",
+                    "\"stamps\": [%lld, %lld, %lld, %lld, %lld, %lld]}",
                     s ? ", " : "", s - 1, ds, de, hp ? (at(s, 1, 0) - base) * 0.01 : -1.0,
                     hp ? (at(s, 1, 1) - base) * 0.01 : -1.0, hu ? (at(s, 2, 0) - base) * 0.01 : -1.0,
                     hu ? (at(s, 2, 1) - base) * 0.01 : -1.0, gap, ck[8 * s + 7] - ck[8 * s],
@@ -89,8 +91,13 @@ int main(int argc, char** argv) {
                     // cycles from the start: staged, L strip, A_dd - L L^T in LDS, factor done, end
                     s ? (long long)(ck[8 * s + 1] - ck[8 * s]) : 0LL, s ? (long long)(ck[8 * s + 2] - ck[8 * s]) : 0LL,
                     (long long)(ck[8 * s + 3] - ck[8 * s]), (long long)(ck[8 * s + 4] - ck[8 * s]),
-                    (long long)(ck[8 * s + 7] - ck[8 * s]));
+                    (long long)(ck[8 * s + 7] - ck[8 * s]),
+                    // persistent form: the end of the wait for the two tiles (0 in method 4)
+                    ck[8 * s + 5] ? (long long)(ck[8 * s + 5] - ck[8 * s]) : 0LL);
     }
-    std::printf("], \"sum_diag_us\": %.1f, \"sum_gap_us\": %.1f}\n", sum_diag, sum_gap);
+    std::printf("], \"sum_diag_us\": %.1f, \"sum_gap_us\": %.1f, \"workers\": \"%s\", \"solo\": \"%s\", "
+                "\"persist\": \"%s\"}\n", sum_diag, sum_gap, std::getenv("PNOL_CHOL5_WORKERS") ? std::getenv("PNOL_CHOL5_WORKERS") : "",
+                std::getenv("PNOL_CHOL5_SOLO") ? std::getenv("PNOL_CHOL5_SOLO") : "",
+                std::getenv("PNOL_CHOL_PERSIST") ? std::getenv("PNOL_CHOL_PERSIST") : "");
     return 0;
 }
