@@ -2,11 +2,18 @@
  * LevenbergMarquardtMPI.hpp  (MI355X-native PNOL drop-in)
  *
  * LevMarq with the finite-difference Jacobian columns sharded over the communicator --
- * the reference class LevMarqMPI (Source/LevenbergMarquardtMPI.hpp:27-60).  Each rank
- * evaluates a contiguous block of ceil(n / ranks) columns on its GPU; one RCCL allgather
- * over xGMI assembles J^T on every rank (replacing the n zero-padded MPI_Allreduce calls of
- * PNOL_Objective.cpp:279-288).  The assembled J is bitwise independent of the rank count,
- * so the whole trajectory is too, as in the reference.  Messages print on rank 0.
+ * the reference class LevMarqMPI (Source/LevenbergMarquardtMPI.hpp:27-60), which evaluates
+ * contiguous column blocks and assembles J with n zero-padded MPI_Allreduce calls
+ * (PNOL_Objective.cpp:279-288).  Here, for linear-residual device objectives:
+ *  - each rank evaluates a cost-balanced set of 128-column FD tiles (snake order,
+ *    pnol_fd_tiles) for every residual row;
+ *  - the residual rows are cut into 8 m-slices; each slice of those tiles goes to the rank
+ *    that holds the slice (one group of RCCL point-to-point transfers, pnol_lm_jacobian_mpi_d);
+ *  - each rank forms J^T J and -J^T F over its slices; the slice sums are combined by one
+ *    fixed tree (nodes to each tile's owner, then one allgather, pnol_lm_normal_mpi_d).
+ * Other objectives keep column tiles with the rows shared point-to-point and the tile-split
+ * J^T J.  A, -J^T F and the whole trajectory are bitwise independent of the rank count, as in
+ * the reference.  Messages print on rank 0.
  */
 #ifndef PNOL_AMD_LEVENBERGMARQUARDT_MPI_HPP_
 #define PNOL_AMD_LEVENBERGMARQUARDT_MPI_HPP_
