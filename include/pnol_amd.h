@@ -128,6 +128,13 @@ int pnol_bfgs_pass_ident_mpi_d(pnol_ctx* ctx, double* Dsh, int ldd, int n, const
  * free-free block of D handed to the reduced problem, BFGS_with_bnd_linsearch_MPI.cpp:822-843 */
 int pnol_gather_submatrix_d(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub,
                             double* Dsub, int lds);
+/* The same for a row-sharded D (collective; pnol_bfgs_rows shards of n rows in, of nsub rows
+ * out): D = this rank's rows of the source, Dsub = this rank's rows of the block; idx: HOST
+ * ints, ascending, < n, the same on every rank.  Each rank gathers the kept columns of its kept
+ * rows on the device, and those rows go to their new owners point to point (RCCL; the host
+ * backend bounces through host memory) -- D never crosses PCIe whole. */
+int pnol_gather_submatrix_mpi_d(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub,
+                                double* Dsub, int lds);
 
 /* ---- Levenberg-Marquardt -------------------------------------------------------------- */
 /* A = JT JT^T (= J^T J) with A_ii = (1 + lambda) * (J^T J)_ii  (Marquardt scaling).

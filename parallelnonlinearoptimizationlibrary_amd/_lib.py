@@ -80,6 +80,7 @@ _SIGS = {
     "pnol_hg_mpi_d": (_i, [_vp, _vp, _i, _vp, _vp, _i]),
     "pnol_bfgs_pass_mpi_d": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
     "pnol_gather_submatrix_d": (_i, [_vp, _vp, _i, _i, _vp, _i, _vp, _i]),
+    "pnol_gather_submatrix_mpi_d": (_i, [_vp, _vp, _i, _i, _vp, _i, _vp, _i]),
     "pnol_jtj_d": (_i, [_vp, _vp, _i, _i, _i, _d, _vp, _i, _vp]),
     "pnol_jtj_mpi_d": (_i, [_vp, _vp, _i, _i, _i, _d, _vp, _i, _vp]),
     "pnol_lm_sliced_layout": (_i, [_i, _i, C.POINTER(_i), C.POINTER(_sz)]),

@@ -139,6 +139,47 @@ int pnol_set_identity_rows_d(pnol_ctx* ctx, double* Dsh, int ldd, int n, const d
     return launch_set_identity(ctx, Dsh, ldd, n, scale, b, b + c);
 }
 
+int pnol_gather_submatrix_mpi_d(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub,
+                                double* Dsub, int lds) {
+    PNOL_CHECK(set_device(ctx));
+    if (!idx || nsub <= 0 || nsub > n || lds < nsub || ldd < n) return PNOL_ERR_ARG;
+    for (int a = 0; a < nsub; ++a)
+        if (idx[a] < 0 || idx[a] >= n || (a > 0 && idx[a] <= idx[a - 1])) return PNOL_ERR_ARG;
+    const int P = comm_size(), me = comm_rank();
+    // kept rows of old shard q: the new indices [a0[q], a1[q]) (contiguous: idx is ascending)
+    std::vector<int> a0(P), a1(P), nb(P), nc(P);
+    for (int q = 0; q < P; ++q) {
+        int ob = 0, oc = 0;
+        PNOL_CHECK(pnol_bfgs_rows(n, P, q, &ob, &oc));
+        a0[q] = (int)(std::lower_bound(idx, idx + nsub, ob) - idx);
+        a1[q] = (int)(std::lower_bound(idx, idx + nsub, ob + oc) - idx);
+        PNOL_CHECK(pnol_bfgs_rows(nsub, P, q, &nb[q], &nc[q]));
+    }
+    int ob = 0, oc = 0;
+    PNOL_CHECK(pnol_bfgs_rows(n, P, me, &ob, &oc));
+    if (a1[me] > a0[me] && !D) return PNOL_ERR_ARG;
+    if (nc[me] > 0 && !Dsub) return PNOL_ERR_ARG;
+    void *di = nullptr, *pk = nullptr;
+    PNOL_CHECK(ws_get(ctx, "subm_idx", sizeof(int) * (size_t)nsub, &di));
+    PNOL_CHECK(pnol_memcpy_h2d(ctx, di, idx, sizeof(int) * (size_t)nsub));
+    const int mine = a1[me] - a0[me];
+    PNOL_CHECK(ws_get(ctx, "subm_pack", sizeof(double) * (size_t)std::max(mine, 1) * lds, &pk));
+    double* pack = (double*)pk;
+    PNOL_CHECK(launch_gather_rows(ctx, D, ldd, (const int*)di + a0[me], mine, ob, (const int*)di, nsub, pack, lds));
+    // rows this rank keeps for itself
+    const int slo = std::max(a0[me], nb[me]), shi = std::min(a1[me], nb[me] + nc[me]);
+    if (shi > slo)
+        PNOL_HIP(hipMemcpyAsync(Dsub + (size_t)(slo - nb[me]) * lds, pack + (size_t)(slo - a0[me]) * lds,
+                                sizeof(double) * (size_t)(shi - slo) * lds, hipMemcpyDeviceToDevice, ctx->stream));
+    if (P == 1) return PNOL_OK;
+    return comm_exchange(ctx, pack, Dsub, [&](int q, int d, std::vector<XBlock>& bl) {
+        bl.clear();
+        const int lo = std::max(a0[q], nb[d]), hi = std::min(a1[q], nb[d] + nc[d]);
+        if (hi > lo)
+            bl.push_back({(size_t)(lo - a0[q]) * lds, (size_t)(lo - nb[d]) * lds, (size_t)(hi - lo) * lds});
+    });
+}
+
 int pnol_hg_mpi_d(pnol_ctx* ctx, const double* Dsh, int ldd, const double* g, double* p, int n) {
     PNOL_CHECK(set_device(ctx));
     if (!Dsh || !g || !p || n <= 0 || ldd < n) return PNOL_ERR_ARG;

@@ -123,8 +123,21 @@ void DenseInverseHessian::setSubmatrixOf(DenseInverseHessian& src, const std::ve
         }
         return;
     }
+    if (sharded_ && src.sharded_) {
+        // the boundary recursion of the row-sharded variants: kept rows move to their new
+        // owners device to device
+        src.materialize();
+        src.ensureDevice();
+        check(pnol_gather_submatrix_mpi_d(ctx_, src.Dp_, src.ld_, src.n_, idx.data(), n_, Dp_, ld_),
+              "gather_submatrix_mpi");
+        pending_ = false;
+        ident_ = false;
+        dev_ok_ = true;
+        clobbered_ = false;
+        return;
+    }
     if (sharded_ || src.sharded_) {
-        // rare (boundary recursion): through the host, every rank holding the whole source
+        // mixed sharding (not used by the drop-ins): through the host
         std::vector<std::vector<double>> full, sub(n_, std::vector<double>(n_));
         src.getMatrix(full);
         for (int a = 0; a < n_; ++a)

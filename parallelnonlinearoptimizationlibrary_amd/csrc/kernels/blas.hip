@@ -544,11 +544,12 @@ __global__ void k_set_identity(double* __restrict__ D, long ldd, int nrows, int 
 
 // Dsub[a][b] = D[idx[a]][idx[b]]: one workgroup per destination row (idx ascending, so the
 // source reads of a row stay within one row of D and mostly coalesce)
-__global__ void k_gather_sub(const double* __restrict__ D, long ldd, const int* __restrict__ idx, int nsub,
-                             double* __restrict__ Dsub, long lds) {
-    for (int a = blockIdx.x; a < nsub; a += gridDim.x) {
-        const double* row = D + (long)idx[a] * ldd;
-        for (int b = threadIdx.x; b < nsub; b += blockDim.x) Dsub[(long)a * lds + b] = row[idx[b]];
+// Dsub[a][b] = D[ridx[a] - rbase][cidx[b]], a < nrows, b < ncols
+__global__ void k_gather_sub(const double* __restrict__ D, long ldd, const int* __restrict__ ridx, int nrows,
+                             int rbase, const int* __restrict__ cidx, int ncols, double* __restrict__ Dsub, long lds) {
+    for (int a = blockIdx.x; a < nrows; a += gridDim.x) {
+        const double* row = D + (long)(ridx[a] - rbase) * ldd;
+        for (int b = threadIdx.x; b < ncols; b += blockDim.x) Dsub[(long)a * lds + b] = row[cidx[b]];
     }
 }
 
@@ -743,8 +744,17 @@ int launch_gather_sub(pnol_ctx* ctx, const double* D, int ldd, int n, const int*
                       int lds) {
     if (!D || !idx || !Dsub || nsub < 0 || nsub > n || ldd < n || lds < nsub) return PNOL_ERR_ARG;
     if (nsub == 0) return PNOL_OK;
-    hipLaunchKernelGGL(k_gather_sub, dim3(std::min(nsub, 8192)), dim3(256), 0, ctx->stream, D, (long)ldd, idx, nsub,
-                       Dsub, (long)lds);
+    hipLaunchKernelGGL(k_gather_sub, dim3(std::min(nsub, 8192)), dim3(256), 0, ctx->stream, D, (long)ldd, idx, nsub, 0,
+                       idx, nsub, Dsub, (long)lds);
+    return launch_check();
+}
+
+int launch_gather_rows(pnol_ctx* ctx, const double* D, int ldd, const int* ridx, int nrows, int rbase, const int* cidx,
+                       int ncols, double* Dsub, int lds) {
+    if (nrows <= 0 || ncols <= 0) return PNOL_OK;
+    if (!D || !ridx || !cidx || !Dsub || lds < ncols) return PNOL_ERR_ARG;
+    hipLaunchKernelGGL(k_gather_sub, dim3(std::min(nrows, 8192)), dim3(256), 0, ctx->stream, D, (long)ldd, ridx, nrows,
+                       rbase, cidx, ncols, Dsub, (long)lds);
     return launch_check();
 }
 

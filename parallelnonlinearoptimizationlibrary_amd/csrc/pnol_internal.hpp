@@ -161,6 +161,9 @@ int launch_set_identity(pnol_ctx* ctx, double* D, int ldd, int n, const double* 
 int launch_add(pnol_ctx* ctx, const double* x, const double* y, double* z, int n);
 int launch_gather_sub(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub, double* Dsub,
                       int lds);
+// Dsub[a][b] = D[ridx[a] - rbase][cidx[b]] (rows of a shard starting at global row rbase)
+int launch_gather_rows(pnol_ctx* ctx, const double* D, int ldd, const int* ridx, int nrows, int rbase, const int* cidx,
+                       int ncols, double* Dsub, int lds);
 
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                double* jtj_diag);

@@ -76,14 +76,31 @@ def main():
                                          dy.data_ptr(), dg.data_ptr(), u.data_ptr(), w.data_ptr(), v.data_ptr()),
             "pass_mpi")
     ctx.synchronize()
+    # the boundary recursion's free-free block of the row-sharded D (pnol_gather_submatrix_mpi_d):
+    # kept rows to their new owners, device to device
+    keep = np.sort(np.random.default_rng(4).choice(nD, 411, replace=False)).astype(np.int32)
+    Dsh2 = ctx.tensor(Dfull[rb:rb + rc] if rc > 0 else np.zeros((1, nD)))
+    sb, sc = C.c_int(), C.c_int()
+    L.check(L.lib().pnol_bfgs_rows(len(keep), world, rank, C.byref(sb), C.byref(sc)), "bfgs_rows")
+    sb, sc = sb.value, sc.value
+    Dsub = ctx.empty(max(sc, 1), len(keep))
+    L.check(L.lib().pnol_gather_submatrix_mpi_d(ctx.h, Dsh2.data_ptr(), nD, nD,
+                                                keep.ctypes.data_as(C.POINTER(C.c_int)), len(keep),
+                                                Dsub.data_ptr(), len(keep)), "gather_submatrix_mpi")
+    ctx.synchronize()
     # BFGS_MPI, fast mode (fused passes) on the synthetic quadratic with D row-sharded; pool 4
     nq = 300
     Pq = [1e-4, 0.9, 4, 1, 1000, 1e-6, 1e-3, 40, 1e-9, 1e-6, 0, 0, 4, 1, 2]
     Xq, resq = run_bfgs(DeviceObjective.synthetic(ctx, L.OBJ_QUADRATIC, nq), np.zeros(nq), Pq, which=1)
-    np.savez(os.path.join(out, f"rank{rank}.npz"), **res, Xb=Xb,
+    # BFGSBnd_MPI in fast mode at n = 600 (D row-sharded over the ranks; active bounds, so the
+    # reduced problems start from the sharded free-free block)
+    Pf = [1e-4, 0.1, 1e-16, 4, 1, 200, 1e-6, 1e-3, 100, 1e-9, 1e-6, 1e-9, 0, 0, 4]
+    Xf, resf = run_bfgs(DeviceObjective.synthetic(ctx, L.OBJ_QUADRATIC, 600, 0, bscale=4.0), np.zeros(600), Pf,
+                        which=3, lb=np.full(600, -0.25), ub=np.full(600, 0.25))
+    np.savez(os.path.join(out, f"rank{rank}.npz"), **res, Xb=Xb, Xf=Xf, ff=np.array([resf.fopt]),
              fb=np.array([resb.fopt]), Xs=Xs, fs=np.array([ress.fopt]), hg=p.cpu().numpy(), u=u.cpu().numpy(),
              w=w.cpu().numpy(), v=v.cpu().numpy(), Drows=Dsh.cpu().numpy()[:rc], rows=np.array([rb, rc]), Xq=Xq,
-             fq=np.array([resq.fopt]))
+             fq=np.array([resq.fopt]), Dsub=Dsub.cpu().numpy()[:sc], subrows=np.array([sb, sc]), keep=keep)
     comm.close()
     dist.barrier()
     dist.destroy_process_group()

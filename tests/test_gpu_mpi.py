@@ -126,7 +126,27 @@ def test_levmarq_mpi_ranks_bitwise_equal_single(tmp_path, world, oracle):
         assert np.array_equal(z["Drows"], Dafter[rb:rb + rc]), r
         covered += rc
     assert covered == nD
+    # the sharded free-free block: every rank's new rows equal the whole-matrix gather
+    covered = 0
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        keep = z["keep"]
+        sub = Dfull[np.ix_(keep, keep)]
+        sb, sc = z["subrows"]
+        assert np.array_equal(z["Dsub"], sub[sb:sb + sc]), r
+        covered += sc
+    assert covered == len(keep)
     from parallelnonlinearoptimizationlibrary_amd.device import run_bfgs
+    # BFGSBnd_MPI fast mode with the sharded D and its sharded boundary recursion: the ranks'
+    # trajectory equals the single-rank one bitwise
+    Pf = [1e-4, 0.1, 1e-16, 4, 1, 200, 1e-6, 1e-3, 100, 1e-9, 1e-6, 1e-9, 0, 0, 4]
+    Xf1, resf1 = run_bfgs(DeviceObjective.synthetic(ctx, L.OBJ_QUADRATIC, 600, 0, bscale=4.0), np.zeros(600), Pf,
+                          which=3, lb=np.full(600, -0.25), ub=np.full(600, 0.25))
+    assert np.any(np.abs(Xf1) == 0.25)   # bounds active: the recursion ran
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        assert np.array_equal(z["Xf"], Xf1), r
+        assert z["ff"][0] == resf1.fopt, r
     Pq = [1e-4, 0.9, 4, 1, 1000, 1e-6, 1e-3, 40, 1e-9, 1e-6, 0, 0, 4, 1, 2]
     Xq1, resq1 = run_bfgs(DeviceObjective.synthetic(ctx, L.OBJ_QUADRATIC, 300), np.zeros(300), Pq, which=1)
     for r in range(world):
