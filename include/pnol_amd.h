@@ -297,6 +297,14 @@ int pnol_run_bfgs(int which, pnol_dobj* obj, int host_eval, const double* params
 int pnol_run_bfgs_ex(int which, pnol_dobj* obj, int host_eval, const double* params, int nparams, double* X, int n,
                      const double* Xlb, const double* Xub, pnol_result* res, double* ftrace, int trace_cap,
                      int* ntrace, double* profile);
+/* which: 0 = GeneticAlgorithm, 1 = GeneticAlgorithmMPI (10 params, the setGAParams order without
+ * graph: Npop, maxGenerations, eliteFrac, crossFrac, eliteMutationFrac, mutationSize,
+ * eliteMutationSize, initialPopScaling, NstaticGenerations, verbose); seed: the selection /
+ * mutation stream (GeneticAlgorithm::setSeed); res->iters = generations.  Each generation's
+ * population is one device batch for device objectives (GeneticAlgorithm.cpp:301-310,
+ * GeneticAlgorithmMPI.cpp:283-414). */
+int pnol_run_ga(int which, pnol_dobj* obj, int host_eval, const double* params, int nparams, unsigned long long seed,
+                double* X, int n, const double* Xlb, const double* Xub, pnol_result* res);
 /* which: 0 = LevMarq, 1 = LevMarqMPI (6 params). F0/FOpt host arrays of m. */
 int pnol_run_levmarq(int which, pnol_dobj* obj, int host_eval, const double* params, double* X, int n,
                      double* F0, double* FOpt, int m, pnol_result* res);

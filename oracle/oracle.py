@@ -351,6 +351,17 @@ def bfgs_bnd_mpi_sw_findmin(o: Obj, x0, lb, ub, params, procs):  # BFGS_Bnd_MPI_
     return X, res
 
 
+def ga_findmin(o: Obj, x0, lb, ub, params, seed, nprocs=0):  # GeneticAlgorithm{,MPI}::findMinBnd
+    """params: the first 9 setGAParams values (Npop ... NstaticGenerations); nprocs 0 = serial."""
+    X = np.array(x0, dtype=np.float64)
+    lb = np.ascontiguousarray(lb, dtype=np.float64); ub = np.ascontiguousarray(ub, dtype=np.float64)
+    prm = np.ascontiguousarray(params[:9], dtype=np.float64)
+    res = Result()
+    st = lib().orc_ga_findmin(o.ref(), ptr(prm), C.c_ulonglong(seed), nprocs, ptr(X), ptr(lb), ptr(ub), len(X),
+                              C.byref(res))
+    return X, res, st
+
+
 def check_alpha_pool_bnd(pool, x, lb, ub, p):  # checkAlphaPoolBnd, BFGS_with_bnd_linsearch_MPI.cpp:711-743
     ap = np.array(pool, dtype=np.float64)
     arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (x, lb, ub, p)]

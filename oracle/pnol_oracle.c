@@ -1521,3 +1521,174 @@ void orc_make_cubic_data(int m, double* xData, double* yData) {
         yData[k] = 0.3 * pow(x, 3.0) + 1.1 * (x * x) - 4.3 * x + 7.3;
     }
 }
+
+/* ------------------------------------------------------------------------------------ */
+/* genetic algorithm                                                  */
+/* ------------------------------------------------------------------------------------ */
+/* GeneticAlgorithm::findMinBnd (GeneticAlgorithm.cpp:12-297) and GeneticAlgorithmMPI
+ * (GeneticAlgorithmMPI.cpp:12-414).  timeRand() (UtilityFunctionLibrary, absent) is restated
+ * as a uniform double in [0, 1) from a splitmix64 stream; the three documented repairs of the
+ * product (include/GeneticAlgorithm.hpp: clamped selection index, uniform selection when every
+ * fitness is 0, first-minimum sort) are applied the same way here.  nprocs > 1: the population
+ * evaluation is dealt round-robin over nprocs ranks and every value comes back as v + 0.0 (the
+ * reference's zero-padded MPI_Allreduce); nprocs == 0: the serial class. */
+typedef struct {
+    unsigned long long state;
+} ga_rng;
+
+static double ga_next(ga_rng* r) {
+    unsigned long long z = (r->state += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (double)(z >> 11) * 0x1.0p-53;
+}
+
+/* GeneticAlgorithm.cpp:312-340 */
+static void ga_identical(double* Xp, int Npop, int n, const double* lb, const double* ub, int* ind, ga_rng* r) {
+    for (int i = 0; i < Npop; i++)
+        for (int k = i + 1; k < Npop; k++) {
+            int same = 0;
+            for (int j = 0; j < n; j++)
+                if (Xp[i * n + j] == Xp[k * n + j]) same++;
+            if (same == n) {
+                for (int j = 0; j < n; j++) Xp[i * n + j] = lb[j] + (ub[j] - lb[j]) * ga_next(r);
+                ind[i] = 1;
+            }
+        }
+}
+
+/* GeneticAlgorithm.cpp:343-362 */
+static void ga_bounds(double* Xp, int Npop, int n, const double* lb, const double* ub, int* ind, ga_rng* r) {
+    for (int i = 0; i < Npop; i++)
+        for (int j = 0; j < n; j++)
+            if (Xp[i * n + j] > ub[j] || Xp[i * n + j] < lb[j]) {
+                Xp[i * n + j] = lb[j] + (ub[j] - lb[j]) * ga_next(r);
+                ind[i] = 1;
+            }
+}
+
+/* GeneticAlgorithm.cpp:367-406: repeated first minimum among the members not yet placed */
+static void ga_sort(double* Xp, double* F, int Npop, int n, double* Xt, double* Ft, int* taken) {
+    for (int i = 0; i < Npop; i++) taken[i] = 0;
+    for (int k = 0; k < Npop; k++) {
+        int best = -1;
+        for (int i = 0; i < Npop; i++)
+            if (!taken[i] && (best < 0 || F[i] < F[best])) best = i;
+        taken[best] = 1;
+        memcpy(Xt + (size_t)k * n, Xp + (size_t)best * n, sizeof(double) * n);
+        Ft[k] = F[best];
+    }
+    memcpy(Xp, Xt, sizeof(double) * (size_t)Npop * n);
+    memcpy(F, Ft, sizeof(double) * Npop);
+}
+
+/* GeneticAlgorithm::evaluatePopulation (:301-310) / evaluatePopulationParallel (MPI :283-414) */
+static void ga_pad(double* Xp, double* F, int Npop, int n) {   /* the zero-padded sums, P > 1 */
+    for (int i = 0; i < Npop; i++) {
+        F[i] = F[i] + 0.0;
+        for (int j = 0; j < n; j++) Xp[(size_t)i * n + j] = Xp[(size_t)i * n + j] + 0.0;
+    }
+}
+
+/* which rank evaluates a member changes no value: only the padding of the two exchanges shows */
+static void ga_evaluate(orc_objective* o, double* Xp, double* F, const int* ind, int Npop, int n, int nprocs) {
+    if (nprocs > 1) ga_pad(Xp, F, Npop, n);   /* the root's population to every rank */
+    for (int i = 0; i < Npop; i++)
+        if (ind[i]) F[i] = orc_obj_eval(o, Xp + (size_t)i * n);
+    if (nprocs > 1) ga_pad(Xp, F, Npop, n);   /* the values back */
+}
+
+static int ga_select(ga_rng* r, const double* fitness, double maxFitness, int Npop) {
+    int index = 0;
+    while (index == 0) {
+        int k = (int)round(ga_next(r) * Npop);
+        if (k > Npop - 1) k = Npop - 1;
+        const double u = ga_next(r);
+        if (maxFitness == 0.0 || u <= fitness[k] / maxFitness) index = k;
+    }
+    return index;
+}
+
+/* params: Npop, maxGenerations, eliteFrac, crossFrac, eliteMutationFrac, mutationSize,
+ * eliteMutationSize, initialPopScaling, NstaticGenerations; res->iters = generations */
+int orc_ga_findmin(orc_objective* o, const double* prm, unsigned long long seed, int nprocs, double* X,
+                   const double* lb, const double* ub, int n, orc_result* res) {
+    const int Npop = (int)prm[0], maxGen = (int)prm[1];
+    const double eliteFrac = prm[2], crossFrac = prm[3], eliteMutFrac = prm[4], mutSize = prm[5], eliteMutSize = prm[6];
+    const double Nstatic_max = prm[8];
+    const int Nelite = (int)ceil(eliteFrac * Npop), NeliteMut = (int)ceil(eliteMutFrac * Npop),
+              Ncross = (int)ceil(crossFrac * Npop), Nrand = Npop - Nelite - NeliteMut - Ncross;
+    if (Nrand <= 0 || Npop < 2) return -1;
+    const size_t pn = (size_t)Npop * n;
+    double* Xp = calloc(pn, sizeof(double));
+    double* Xn = calloc(pn, sizeof(double));
+    double* Xt = calloc(pn, sizeof(double));
+    double* F = calloc(Npop, sizeof(double));
+    double* Fn = calloc(Npop, sizeof(double));
+    double* Ft = calloc(Npop, sizeof(double));
+    double* fit = calloc(Npop, sizeof(double));
+    int* ind = calloc(Npop, sizeof(int));
+    int* taken = calloc(Npop, sizeof(int));
+    int* idx = calloc(n, sizeof(int));
+    ga_rng r = {seed};
+    o->evals = 0;
+    for (int i = 0; i < Npop; i++) ind[i] = 1;
+    for (int j = 0; j < n; j++) Xp[j] = X[j];
+    for (int i = 1; i < Npop; i++)
+        for (int j = 0; j < n; j++) Xp[(size_t)i * n + j] = Xp[j] + ((ub[j] - lb[j]) * ga_next(&r) + lb[j]);
+    ga_identical(Xn, Npop, n, lb, ub, ind, &r);   /* the reference checks XpopNew (zeros) here */
+    ga_bounds(Xp, Npop, n, lb, ub, ind, &r);
+    ga_evaluate(o, Xp, F, ind, Npop, n, nprocs);
+    res->f0 = F[0];
+    ga_sort(Xp, F, Npop, n, Xt, Ft, taken);
+    double FbestPrev = F[0];
+    int Nstatic = 0, iter = 0;
+    while (iter < maxGen) {
+        for (int k = 0; k < Npop; k++) fit[k] = pow(F[Npop - 1] - F[k], 2);
+        const double maxFit = fit[0];
+        for (int k = 0; k < Npop; k++) ind[k] = 1;
+        int p = 0;
+        for (int k = 0; k < Nelite; k++, p++) {
+            memcpy(Xn + (size_t)p * n, Xp + (size_t)p * n, sizeof(double) * n);
+            Fn[p] = F[p];
+            ind[p] = 0;
+        }
+        for (int k = 0; k < Ncross; k++, p++) {
+            for (int i = 0; i < n; i++) idx[i] = ga_select(&r, fit, maxFit, Npop);
+            for (int i = 0; i < n; i++) Xn[(size_t)p * n + i] = Xp[(size_t)idx[i] * n + i];
+        }
+        const double spread = mutSize * (maxGen - iter) / maxGen;
+        for (int k = 0; k < Nrand; k++, p++) {
+            const int s = ga_select(&r, fit, maxFit, Npop);
+            for (int j = 0; j < n; j++) {
+                const double mut = spread * (ub[j] - lb[j]) * ga_next(&r);
+                Xn[(size_t)p * n + j] = Xp[(size_t)s * n + j] + mut;
+            }
+        }
+        for (int k = 0; k < NeliteMut; k++, p++)
+            for (int j = 0; j < n; j++) {
+                int e = (int)round(ga_next(&r) * Nelite);
+                if (e > Npop - 1) e = Npop - 1;
+                const double mut = eliteMutSize * (ub[j] - lb[j]) * ga_next(&r);
+                Xn[(size_t)p * n + j] = Xp[(size_t)e * n + j] + mut;
+            }
+        ga_identical(Xn, Npop, n, lb, ub, ind, &r);
+        ga_bounds(Xn, Npop, n, lb, ub, ind, &r);
+        ga_evaluate(o, Xn, Fn, ind, Npop, n, nprocs);
+        ga_sort(Xn, Fn, Npop, n, Xt, Ft, taken);
+        memcpy(F, Fn, sizeof(double) * Npop);
+        memcpy(Xp, Xn, sizeof(double) * pn);
+        const double Fbest = F[0];
+        Nstatic = (Fbest == FbestPrev) ? Nstatic + 1 : 0;
+        if (Nstatic > Nstatic_max) break;
+        FbestPrev = Fbest;
+        iter++;
+    }
+    res->iters = iter;
+    res->evals = o->evals;
+    res->fopt = F[0];
+    for (int j = 0; j < n; j++) X[j] = Xp[j];
+    free(Xp); free(Xn); free(Xt); free(F); free(Fn); free(Ft); free(fit); free(ind); free(taken); free(idx);
+    return 0;
+}

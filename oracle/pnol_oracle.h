@@ -151,4 +151,10 @@ void orc_make_cubic_data(int m, double* xData, double* yData);
 #ifdef __cplusplus
 }
 #endif
+/* GeneticAlgorithm / GeneticAlgorithmMPI (GeneticAlgorithm.cpp:12-436, GeneticAlgorithmMPI.cpp:12-414):
+ * prm = Npop, maxGenerations, eliteFrac, crossFrac, eliteMutationFrac, mutationSize,
+ * eliteMutationSize, initialPopScaling, NstaticGenerations; nprocs 0 = the serial class. */
+int orc_ga_findmin(orc_objective* o, const double* prm, unsigned long long seed, int nprocs, double* X,
+                   const double* lb, const double* ub, int n, orc_result* res);
+
 #endif

@@ -12,6 +12,8 @@
 #include "BFGS_with_bnd_linesearch_MPI.hpp"
 #include "BFGS_with_linesearch.hpp"
 #include "BFGS_with_linesearch_MPI.hpp"
+#include "GeneticAlgorithm.hpp"
+#include "GeneticAlgorithmMPI.hpp"
 #include "LevenbergMarquardt.hpp"
 #include "LevenbergMarquardtMPI.hpp"
 #include "device_util.hpp"
@@ -247,6 +249,39 @@ int pnol_run_bfgs_ex(int which, pnol_dobj* obj, int host_eval, const double* p, 
         res->fopt = fopt;
         for (int k = 0; k < (int)trace.size() && k < trace_cap; ++k) ftrace[k] = trace[k];
         if (ntrace) *ntrace = (int)trace.size();
+    });
+}
+
+int pnol_run_ga(int which, pnol_dobj* obj, int host_eval, const double* p, int np, unsigned long long seed, double* X,
+                int n, const double* Xlb, const double* Xub, pnol_result* res) {
+    if (!obj || !p || np < 10 || !X || n <= 0 || !Xlb || !Xub || !res) return PNOL_ERR_ARG;
+    return guarded([&] {
+        DriverScalar o(obj, host_eval != 0);
+        std::vector<double> x(X, X + n), lb(Xlb, Xlb + n), ub(Xub, Xub + n);
+        double f0 = 0, fopt = 0;
+        int gens = 0;
+        if (which == 0) {
+            GeneticAlgorithm g;
+            g.setGAParams((int)p[0], (int)p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8], p[9] != 0, false);
+            g.setSeed(seed);
+            g.setObjPtr(o);
+            g.findMinBnd(x, lb, ub, f0, fopt);
+            gens = g.getGenerations();
+        } else if (which == 1) {
+            GeneticAlgorithmMPI g;
+            g.setGAParams((int)p[0], (int)p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8], p[9] != 0);
+            g.setSeed(seed);
+            g.setObjPtr(o);
+            g.findMinBnd(x, lb, ub, f0, fopt);
+            gens = g.getGenerations();
+        } else {
+            throw std::runtime_error("unknown GA variant");
+        }
+        for (int i = 0; i < n; ++i) X[i] = x[i];
+        res->iters = gens;
+        res->evals = o.evals;
+        res->f0 = f0;
+        res->fopt = fopt;
     });
 }
 

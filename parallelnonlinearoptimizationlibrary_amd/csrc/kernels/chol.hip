@@ -715,7 +715,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
     const int b = blockIdx.x;
 
     if (b == 0) {   // ---------------- diagonal tile d = k + 1
-        const int d = k + 1, d0 = d * NB;
+        const int d = k + 1;
         const DiagLds L = diag_lds(smem);
         if (t < 6) cnt[t] = 0;
         if (k >= 0) {

@@ -281,6 +281,20 @@ def run_bfgs(obj: DeviceObjective, x0, params, which=0, host_eval=False, lb=None
     return X, res
 
 
+def run_ga(obj: DeviceObjective, x0, lb, ub, params, seed, which=0, host_eval=False):
+    """Run the C++ drop-in GeneticAlgorithm (0) or GeneticAlgorithmMPI (1) on a scalar device
+    objective with a fixed selection / mutation stream; params = setGAParams without graph (10
+    values).  Returns (X, result); result.iters = generations."""
+    X = np.array(x0, dtype=np.float64)
+    p = np.array(params, dtype=np.float64)
+    lba = np.ascontiguousarray(lb, dtype=np.float64)
+    uba = np.ascontiguousarray(ub, dtype=np.float64)
+    res = L.Result()
+    L.check(L.lib().pnol_run_ga(which, obj.h, int(host_eval), _dptr(p), p.size, seed, _dptr(X), X.size, _dptr(lba),
+                                _dptr(uba), C.byref(res)), "pnol_run_ga")
+    return X, res
+
+
 def run_levmarq(obj: DeviceObjective, x0, params, which=0, host_eval=False):
     """Run the C++ drop-in LevMarq (0) or LevMarqMPI (1); returns (X, F0, FOpt, result)."""
     X = np.array(x0, dtype=np.float64)

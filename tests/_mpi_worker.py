@@ -92,12 +92,18 @@ def main():
     nq = 300
     Pq = [1e-4, 0.9, 4, 1, 1000, 1e-6, 1e-3, 40, 1e-9, 1e-6, 0, 0, 4, 1, 2]
     Xq, resq = run_bfgs(DeviceObjective.synthetic(ctx, L.OBJ_QUADRATIC, nq), np.zeros(nq), Pq, which=1)
+    # GeneticAlgorithmMPI: the population dealt round-robin over the ranks, one device batch each
+    from parallelnonlinearoptimizationlibrary_amd.device import run_ga
+    Pga = [40, 200, 0.1, 0.3, 0.2, 0.5, 0.01, 0.5, 20, 0]
+    Xga, resga = run_ga(DeviceObjective(ctx, L.OBJ_ROSENBROCK, 4), np.full(4, -1.0), np.full(4, -2.0),
+                        np.full(4, 2.0), Pga, 12345, which=1)
     # BFGSBnd_MPI in fast mode at n = 600 (D row-sharded over the ranks; active bounds, so the
     # reduced problems start from the sharded free-free block)
     Pf = [1e-4, 0.1, 1e-16, 4, 1, 200, 1e-6, 1e-3, 100, 1e-9, 1e-6, 1e-9, 0, 0, 4]
     Xf, resf = run_bfgs(DeviceObjective.synthetic(ctx, L.OBJ_QUADRATIC, 600, 0, bscale=4.0), np.zeros(600), Pf,
                         which=3, lb=np.full(600, -0.25), ub=np.full(600, 0.25))
-    np.savez(os.path.join(out, f"rank{rank}.npz"), **res, Xb=Xb, Xf=Xf, ff=np.array([resf.fopt]),
+    np.savez(os.path.join(out, f"rank{rank}.npz"), **res, Xb=Xb, Xf=Xf, ff=np.array([resf.fopt]), Xga=Xga,
+             ga=np.array([resga.f0, resga.fopt, resga.iters, resga.evals]),
              fb=np.array([resb.fopt]), Xs=Xs, fs=np.array([ress.fopt]), hg=p.cpu().numpy(), u=u.cpu().numpy(),
              w=w.cpu().numpy(), v=v.cpu().numpy(), Drows=Dsh.cpu().numpy()[:rc], rows=np.array([rb, rc]), Xq=Xq,
              fq=np.array([resq.fopt]), Dsub=Dsub.cpu().numpy()[:sc], subrows=np.array([sb, sc]), keep=keep)

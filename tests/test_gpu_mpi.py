@@ -104,6 +104,18 @@ def test_levmarq_mpi_ranks_bitwise_equal_single(tmp_path, world, oracle):
         z = np.load(tmp_path / f"rank{r}.npz")
         assert np.array_equal(z["Xs"], Xo), r
         assert z["fs"][0] == reso.fopt, r
+    # GeneticAlgorithmMPI across the ranks equals the restatement at np = world (row f4); the
+    # evaluation count is the whole job's, split over the ranks
+    Xgo, rgo, st = oracle.ga_findmin(oracle.rosenbrock(4), np.full(4, -1.0), np.full(4, -2.0), np.full(4, 2.0),
+                                     [40, 200, 0.1, 0.3, 0.2, 0.5, 0.01, 0.5, 20], 12345, world)
+    assert st == 0
+    evals = 0
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        assert np.array_equal(z["Xga"], Xgo), r
+        assert z["ga"][0] == rgo.f0 and z["ga"][1] == rgo.fopt and z["ga"][2] == rgo.iters, r
+        evals += int(z["ga"][3])
+    assert evals == rgo.evals
     # BFGS D row-sharded: the collective H.g / fused pass equal the whole-matrix kernels bitwise,
     # and BFGS_MPI in fast mode gives the single-rank trajectory bitwise
     import torch

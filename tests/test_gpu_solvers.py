@@ -538,3 +538,32 @@ def test_user_program_own_multiobjective_levmarq(ctx, oracle, tmp_path, m, n):
     assert rel(X1, xs) <= 1e-8
     assert ev1 == reso.evals, (ev1, reso.evals)
     assert b1 >= 6   # one batch (or more) of FD points per Jacobian, plus the trial points
+
+
+GA_P = [40, 200, 0.1, 0.3, 0.2, 0.5, 0.01, 0.5, 20, 0]   # setGAParams without graph
+
+
+@pytest.mark.parametrize("which,host_eval", [(0, False), (1, False), (0, True)])
+def test_ga_matches_oracle(ctx, oracle, which, host_eval):
+    """GeneticAlgorithm (0) / GeneticAlgorithmMPI on one rank (1) equal the restatement bitwise --
+    X, f0, fOpt, generations, evaluations -- with every generation's population evaluated as
+    one device batch (host_eval: through objEvalBatch on the host formula, the same bits).
+    Rosenbrock n = 4 in [-2, 2]^4 and the cfg-2 quadratic at n = 100 (row f4)."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective, run_ga
+    for kind, n, seed in ((L.OBJ_ROSENBROCK, 4, 12345), (L.OBJ_QUADRATIC, 100, 7)):
+        lb, ub = np.full(n, -2.0), np.full(n, 2.0)
+        x0 = np.full(n, -1.0)
+        if kind == L.OBJ_ROSENBROCK:
+            dobj, oobj = DeviceObjective(ctx, kind, n), oracle.rosenbrock(n)
+        else:
+            dd, bb = oracle.quadratic_data(n)
+            dobj, oobj = DeviceObjective(ctx, kind, n, 0, dd, bb), oracle.Obj(oracle.QUADRATIC, n, 0, dd, bb)
+        X, res = run_ga(dobj, x0, lb, ub, GA_P, seed, which=which, host_eval=host_eval)
+        Xo, reso, st = oracle.ga_findmin(oobj, x0, lb, ub, GA_P[:9], seed, 0)
+        assert st == 0
+        assert np.array_equal(X, Xo), (kind, np.max(np.abs(X - Xo)))
+        assert res.f0 == reso.f0 and res.fopt == reso.fopt, kind
+        assert res.iters == reso.iters and res.evals == reso.evals, (kind, res.iters, reso.iters, res.evals, reso.evals)
+        assert res.fopt < res.f0
+

@@ -221,3 +221,32 @@ def test_oracle_asan_ubsan_clean():
     r = subprocess.run([os.path.join(here, "_asan", "oracle_asan_check")], capture_output=True, timeout=300,
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1"))
     assert r.returncode == 0 and b"clean" in r.stdout, r.stderr.decode(errors="replace")[-3000:]
+
+
+GA_P = [40, 200, 0.1, 0.3, 0.2, 0.5, 0.01, 0.5, 20]   # Npop, maxGen, fractions, sizes, Nstatic
+
+
+def test_ga_oracle_properties(oracle):
+    """The GA restatement (GeneticAlgorithm.cpp:12-436; row f4, parity unpinned: timeRand is
+    restated, the reference is time-seeded): the optimum stays in the box, improves on the
+    start, the stream is reproducible from the seed, and the MPI form's values differ from the
+    serial ones only through the zero-padded sums (none here: no -0.0 appears)."""
+    n = 4
+    lb, ub = np.full(n, -2.0), np.full(n, 2.0)
+    X, r, st = oracle.ga_findmin(oracle.rosenbrock(n), np.full(n, -1.0), lb, ub, GA_P, 12345)
+    assert st == 0
+    assert np.all(X >= lb) and np.all(X <= ub)
+    assert r.fopt < r.f0 and r.fopt < 0.5
+    X2, r2, _ = oracle.ga_findmin(oracle.rosenbrock(n), np.full(n, -1.0), lb, ub, GA_P, 12345)
+    assert np.array_equal(X, X2) and r.fopt == r2.fopt and r.evals == r2.evals and r.iters == r2.iters
+    X3, r3, _ = oracle.ga_findmin(oracle.rosenbrock(n), np.full(n, -1.0), lb, ub, GA_P, 12345, 3)
+    assert np.array_equal(X, X3) and r.fopt == r3.fopt and r.evals == r3.evals
+    X4, r4, _ = oracle.ga_findmin(oracle.rosenbrock(n), np.full(n, -1.0), lb, ub, GA_P, 999)
+    assert not np.array_equal(X, X4)
+    # evaluations: the initial population plus every non-elite member of each generation
+    nelite = int(np.ceil(GA_P[2] * GA_P[0]))
+    assert r.evals <= GA_P[0] + r.iters * (GA_P[0] - nelite) + (GA_P[0] - nelite)
+    _, _, bad = oracle.ga_findmin(oracle.rosenbrock(n), np.full(n, -1.0), lb, ub,
+                                  [10, 5, 0.5, 0.3, 0.3, 0.5, 0.01, 0.5, 5], 1)
+    assert bad == -1   # fractions leave no random members (the reference exits)
+
