@@ -94,6 +94,18 @@ int main(void) {
         orc_objective o = obj(ORC_ROSENBROCK, n, 0, NULL, NULL, 2);
         orc_fd_hessian(&o, X, h, B, n);
     }
+    /* genetic algorithm (row f4), serial and at 1..4 ranks */
+    {
+        const int n = 4;
+        double lb[4] = {-2, -2, -2, -2}, ub[4] = {2, 2, 2, 2};
+        const double prm[9] = {30, 40, 0.1, 0.3, 0.2, 0.5, 0.01, 0.5, 10};
+        orc_objective o = obj(ORC_ROSENBROCK, n, 0, NULL, NULL, 2);
+        orc_result r;
+        for (int np = 0; np <= 4; ++np) {
+            double X[4] = {-1, -1, -1, -1};
+            orc_ga_findmin(&o, prm, 12345ull + np, np, X, lb, ub, n, &r);
+        }
+    }
     printf("asan_check: clean\n");
     return 0;
 }
