@@ -68,23 +68,13 @@ __device__ __forceinline__ void load_stage(StageRegs<TILE, NT>& s, const double*
     }
 }
 
-// LDS image of a stage: row r's K column c at r * kPad + (c ^ swz(r)), swz(r) = (r >> 3) & 1.
-// A fragment read has 16 lanes on rows f = 0..15 at one column; ds_read2_b64 banks are
-// (byte / 4) mod 32, and with the 36-dword row stride rows f and f + 8 would share banks
-// (2-way: SQ_LDS_BANK_CONFLICT was 43% of the LDS cycles); the column swap on rows 8..15 of
-// every 16 puts them on the other half of the banks.  A 16-byte slot holds the pair (c, c+1)
-// swapped on those rows, so the stores stay 16-byte aligned.
-__device__ __forceinline__ int lds_swz(int row) { return (row >> 3) & 1; }
-
 template <int TILE, int NT = 256>
 __device__ __forceinline__ void store_stage(const StageRegs<TILE, NT>& s, double* __restrict__ lds) {
     constexpr int TPR = NT / TILE, CPT = 16 / TPR, NV = CPT / 2;
-    const int t = threadIdx.x, row = t / TPR;
-    double* dst = lds + row * kPad + (t % TPR) * CPT;
-    const bool sw = lds_swz(row);
+    const int t = threadIdx.x;
+    double* dst = lds + (t / TPR) * kPad + (t % TPR) * CPT;
 #pragma unroll
-    for (int q = 0; q < NV; ++q)
-        *reinterpret_cast<double2*>(dst + 2 * q) = sw ? make_double2(s.v[q].y, s.v[q].x) : s.v[q];
+    for (int q = 0; q < NV; ++q) *reinterpret_cast<double2*>(dst + 2 * q) = s.v[q];
 }
 
 #ifdef PNOL_SYRK_TIMELINE
@@ -172,10 +162,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
     }
     const int frow = lane & 15;
     const int fk = lane >> 4;
-    // a wave whose sub-tile of a diagonal tile lies wholly above the diagonal computes nothing
-    // (only the lower triangle and the diagonal are ever read from a diagonal tile); it still
-    // stages its share of every K slice for the other waves
-    const bool idle = diag && wc * WTN >= wr * WTM + WTM;
     for (int st = 0; st < nstages; ++st) {
         const int buf = st & 1;
         double* P = lds[buf][0];
@@ -189,15 +175,13 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
             load_stage<TILE, NT>(ps, X, ldx, nr, prow0, k0, kend, full);
             if (!diag) load_stage<TILE, NT>(qs, X, ldx, nr, qrow0, k0, kend, full);
         }
-        if (idle) continue;   // wave-uniform
 #pragma unroll
         for (int kk = 0; kk < kTK / 4; ++kk) {
             double a[NBM], b[NBN];
-            const int kc = (kk * 4 + fk) ^ lds_swz(frow);   // rows wr*WTM + mi*16 + frow: swz(frow)
 #pragma unroll
-            for (int mi = 0; mi < NBM; ++mi) a[mi] = P[(wr * WTM + mi * 16 + frow) * kPad + kc];
+            for (int mi = 0; mi < NBM; ++mi) a[mi] = P[(wr * WTM + mi * 16 + frow) * kPad + kk * 4 + fk];
 #pragma unroll
-            for (int ni = 0; ni < NBN; ++ni) b[ni] = Q[(wc * WTN + ni * 16 + frow) * kPad + kc];
+            for (int ni = 0; ni < NBN; ++ni) b[ni] = Q[(wc * WTN + ni * 16 + frow) * kPad + kk * 4 + fk];
 #pragma unroll
             for (int mi = 0; mi < NBM; ++mi)
 #pragma unroll
