@@ -656,17 +656,24 @@ __global__ __launch_bounds__(256) void k_linres_fdP(const double* __restrict__ A
     };
     auto bcast = [&](int kb, int ke) {
         int k = kb;
-        if (k + 8 <= ke) {
+        const int nblk = (ke - k) / 8;   // whole blocks of 8
+        if (nblk > 0) {
+            // pairs of blocks with one loop exit: the accumulators keep their registers across
+            // the back edge (a loop with an exit after each block made the compiler copy all 32
+            // of them once per pair).  The load of the block after the pair is clamped to the
+            // last block, so it is always in bounds and unused when past the end.
+            const int klast = kb + (nblk - 1) * 8;
             double p0[8], p1[8];
             load8(p0, k);
-            while (true) {
-                if (k + 16 > ke) { step8(p0, k); k += 8; break; }
+            for (int b = 0; b + 2 <= nblk; b += 2) {
                 load8(p1, k + 8);
                 step8(p0, k);
-                k += 8;
-                if (k + 16 > ke) { step8(p1, k); k += 8; break; }
-                load8(p0, k + 8);
-                step8(p1, k);
+                load8(p0, min(k + 16, klast));
+                step8(p1, k + 8);
+                k += 16;
+            }
+            if (nblk & 1) {
+                step8(p0, k);
                 k += 8;
             }
         }
