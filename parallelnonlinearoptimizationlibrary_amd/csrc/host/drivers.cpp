@@ -1,10 +1,12 @@
 // drivers.cpp -- C ABI entry points that run the C++ drop-in classes end to end on a
 // built-in device objective (used by the parity tests and bench.py through ctypes), plus a
 // callback-objective FD entry point for the host path of the FD engine.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <exception>
+#include <stdexcept>
 #include <vector>
 
 #include "BFGS_bnd_linesearch.hpp"
@@ -29,8 +31,50 @@ std::vector<double> download_param(pnol_dobj* d, const double* p, size_t len) {
     return h;
 }
 
-// scalar objective around a pnol_dobj: FD batches on the device; single points evaluated with
-// the objective's host formula (identical arithmetic to the device batch)
+// The term i of a built-in scalar objective at the point X (the objective's own expression,
+// ExampleObjectives.hpp); Rosenbrock sums i < n - 1, the others i < n.
+struct ScalarTerms {
+    int kind, n;
+    double power;
+    const double *p0, *p1;
+};
+
+template <int KIND>
+inline double scalar_term(const ScalarTerms& st, const double* X, int i) {
+    if (KIND == PNOL_OBJ_ROSENBROCK) {
+        const double t = X[i + 1] - X[i] * X[i], u = 1.0 - X[i];
+        return 100.0 * (t * t) + u * u;
+    } else if (KIND == PNOL_OBJ_POWER) {
+        return st.power == 2.0 ? X[i] * X[i] : std::pow(X[i], st.power);
+    } else {
+        double t = (0.5 * st.p0[i] * X[i]) * X[i] - st.p1[i] * X[i];
+        if (i + 1 < st.n) t = t + (0.25 * X[i]) * X[i + 1];
+        return t;
+    }
+}
+
+// f(X_c) for C points at once.  Each point is the objective's sequential sum f = f + t_i in
+// index order (the host objEval's bits); a lone chain is bound by one dependent add per term,
+// C interleaved chains let the core overlap their add latencies.
+template <int KIND, int C>
+void scalar_chains_k(const ScalarTerms& st, const double* const* X, double* out) {
+    double f[C];
+    for (int c = 0; c < C; ++c) f[c] = 0.0;
+    const int nt = KIND == PNOL_OBJ_ROSENBROCK ? std::max(st.n - 1, 0) : st.n;
+    for (int i = 0; i < nt; ++i)
+        for (int c = 0; c < C; ++c) f[c] = f[c] + scalar_term<KIND>(st, X[c], i);
+    for (int c = 0; c < C; ++c) out[c] = f[c];
+}
+
+template <int C>
+void scalar_chains(const ScalarTerms& st, const double* const* X, double* out) {
+    if (st.kind == PNOL_OBJ_ROSENBROCK) scalar_chains_k<PNOL_OBJ_ROSENBROCK, C>(st, X, out);
+    else if (st.kind == PNOL_OBJ_POWER) scalar_chains_k<PNOL_OBJ_POWER, C>(st, X, out);
+    else scalar_chains_k<PNOL_OBJ_QUADRATIC, C>(st, X, out);
+}
+
+// scalar objective around a pnol_dobj: FD batches on the device; single points and line-search
+// batches evaluated with the objective's host formula (identical arithmetic to the device batch)
 class DriverScalar : public Objective {
   public:
     DriverScalar(pnol_dobj* d, bool host_only) : d_(d), host_only_(host_only) {
@@ -39,42 +83,52 @@ class DriverScalar : public Objective {
     }
     double objEval(vector<double>& X) override {
         evals++;
-        const size_t n = X.size();
-        double f = 0.0;
-        switch (d_->kind) {
-            case PNOL_OBJ_ROSENBROCK:
-                for (size_t k = 0; k + 1 < n; ++k) {
-                    const double t = X[k + 1] - X[k] * X[k], u = 1.0 - X[k];
-                    f = f + (100.0 * (t * t) + u * u);
-                }
-                return f;
-            case PNOL_OBJ_POWER:
-                for (size_t k = 0; k < n; ++k) f = f + (d_->power == 2.0 ? X[k] * X[k] : std::pow(X[k], d_->power));
-                return f;
-            case PNOL_OBJ_QUADRATIC:
-                for (size_t i = 0; i < n; ++i) {
-                    double t = (0.5 * p0_[i] * X[i]) * X[i] - p1_[i] * X[i];
-                    if (i + 1 < n) t = t + (0.25 * X[i]) * X[i + 1];
-                    f = f + t;
-                }
-                return f;
-            default:
-                throw std::runtime_error("DriverScalar: not a scalar objective");
-        }
+        const double* xp = X.data();
+        double f;
+        scalar_chains<1>(terms((int)X.size()), &xp, &f);
+        return f;
     }
-    // Trial points / pools: the host formula by default (an O(n) objective costs less on the
-    // host than a PCIe round trip); PNOL_DEVICE_POINTS=1 sends every batch to the device
-    // (pnol_dobj_eval_batch, the same bits) -- how the tests exercise the device batch path.
+    // Trial points / pools: the host formula by default -- an O(n) sequential sum is a chain of n
+    // dependent adds, which a host core runs faster than a GPU lane (tools/eval_probe.py: 36-44 us
+    // per point at n = 4096 on the device plus the PCIe round trip, vs ~3.5 us on the host), and
+    // the points of a batch run as interleaved chains.  PNOL_DEVICE_POINTS=1 sends every batch to
+    // the device (pnol_dobj_eval_batch, the same bits) -- how the tests exercise that path.
     void objEvalBatch(const double* Xs, int nPts, int n, double* f) override {
-        if (host_only_ || !device_points() || n != d_->n) return Objective::objEvalBatch(Xs, nPts, n, f);
+        if (!host_only_ && device_points() && n == d_->n) {
+            evals += nPts;
+            check(pnol_dobj_eval_batch(d_->ctx, d_, Xs, nPts, f), "dobj_eval_batch");
+            return;
+        }
         evals += nPts;
-        check(pnol_dobj_eval_batch(d_->ctx, d_, Xs, nPts, f), "dobj_eval_batch");
+        const ScalarTerms st = terms(n);
+        int k = 0;
+        for (; k + 4 <= nPts; k += 4) {
+            const double* xp[4] = {Xs + (size_t)k * n, Xs + (size_t)(k + 1) * n, Xs + (size_t)(k + 2) * n,
+                                   Xs + (size_t)(k + 3) * n};
+            scalar_chains<4>(st, xp, f + k);
+        }
+        if (nPts - k >= 2) {
+            const double* xp[2] = {Xs + (size_t)k * n, Xs + (size_t)(k + 1) * n};
+            scalar_chains<2>(st, xp, f + k);
+            k += 2;
+        }
+        if (k < nPts) {
+            const double* xp = Xs + (size_t)k * n;
+            scalar_chains<1>(st, &xp, f + k);
+        }
     }
     pnol_dobj* deviceObjective(int n) override { return (host_only_ || n != d_->n) ? nullptr : d_; }
     void countEvals(long k) override { evals += k; }
     long evals = 0;
 
   private:
+    ScalarTerms terms(int n) const {
+        if (d_->kind != PNOL_OBJ_ROSENBROCK && d_->kind != PNOL_OBJ_POWER && d_->kind != PNOL_OBJ_QUADRATIC)
+            throw std::runtime_error("DriverScalar: not a scalar objective");
+        if (d_->kind == PNOL_OBJ_QUADRATIC && (p0_.size() < (size_t)n || p1_.size() < (size_t)n))
+            throw std::runtime_error("DriverScalar: point longer than the objective's data");
+        return ScalarTerms{d_->kind, n, d_->power, p0_.data(), p1_.data()};
+    }
     static bool device_points() {
         const char* e = std::getenv("PNOL_DEVICE_POINTS");   // read per call (tests flip it)
         return e && std::atoi(e) != 0;

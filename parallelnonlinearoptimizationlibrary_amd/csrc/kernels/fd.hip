@@ -180,48 +180,90 @@ __global__ __launch_bounds__(256) void k_scalar_terms(const double* __restrict__
 }
 
 // Points q in [0, cnt] (q == cnt: the base point): vals[q] = f(x + h_j e_j), j = i0 + q.
-// T streams through LDS in chunks (cooperative coalesced loads); the uniform addends are LDS
-// broadcast reads, which -- unlike scalar loads, whose completion order is not fixed -- stay
-// in flight eight at a time ahead of the dependent add chain.
-constexpr int kTermChunk = 2048;   // 16 KB of terms per LDS stage
+// T streams through LDS in double-buffered chunks (cooperative coalesced loads of chunk c + 1
+// in flight while chunk c is summed); the uniform addends are LDS broadcast reads, which --
+// unlike scalar loads, whose completion order is not fixed -- stay in flight sixteen at a time
+// ahead of the dependent add chain.  Each lane forms its two perturbed terms (t_{j-1}, t_j at
+// x + h_j e_j) before the chain, so inside the window the substitution is two selects.
+// Measured chain step (tools/microbench/add_chain.hip, one wave): 5.3 cycles with the addends in
+// VGPRs (the dependent v_add_f64 latency), 9.7 from LDS 16 ahead, 12.7 from LDS 8 ahead, ~21
+// from scalar loads.
+constexpr int kTermChunk = 2048;   // 16 KB of terms per LDS stage (two stages)
+constexpr int kChainAhead = 16;
 
-// f + Tc[k0] + Tc[k0 + 1] + ... + Tc[k1 - 1], left to right: the next eight LDS reads are in
-// flight while the current eight are added (register double buffer)
+// f + Tc[k0] + Tc[k0 + 1] + ... + Tc[k1 - 1], left to right.  Three register blocks of
+// kChainAhead addends rotate (no copies): the LDS reads of block b + 2 are issued before the adds
+// of block b, so two blocks of reads are in flight across each block of the dependent chain.
+// The sched_barriers keep the compiler from sinking the reads behind the adds (which left one
+// block's latency exposed per iteration).
+__device__ __forceinline__ void chain_ld(double (&v)[kChainAhead], const double* __restrict__ Tc, int k) {
+#pragma unroll
+    for (int q = 0; q < kChainAhead; q += 2) {
+        const double2 w = *reinterpret_cast<const double2*>(Tc + k + q);
+        v[q] = w.x;
+        v[q + 1] = w.y;
+    }
+}
+__device__ __forceinline__ double chain_add(double f, const double (&v)[kChainAhead]) {
+#pragma unroll
+    for (int q = 0; q < kChainAhead; ++q) f = f + v[q];
+    return f;
+}
 __device__ __forceinline__ double chain_sum(double f, const double* __restrict__ Tc, int k0, int k1) {
+    constexpr int D = kChainAhead;
     int k = k0;
-    if (k1 - k >= 16) {
-        double cur[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) cur[q] = Tc[k + q];
-        for (; k + 16 <= k1; k += 8) {
-            double nxt[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) nxt[q] = Tc[k + 8 + q];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) f = f + cur[q];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
+    // scalar head up to a 16-byte boundary of the LDS chunk (Tc + k even)
+    if ((k & 1) && k < k1) f = f + Tc[k++];
+    if (k1 - k >= 3 * D) {
+        double A[D], B[D], C[D];
+        chain_ld(A, Tc, k);
+        chain_ld(B, Tc, k + D);
+        for (; k + 6 * D <= k1; k += 3 * D) {
+            __builtin_amdgcn_sched_barrier(0);
+            chain_ld(C, Tc, k + 2 * D);
+            __builtin_amdgcn_sched_barrier(0);
+            f = chain_add(f, A);
+            __builtin_amdgcn_sched_barrier(0);
+            chain_ld(A, Tc, k + 3 * D);
+            __builtin_amdgcn_sched_barrier(0);
+            f = chain_add(f, B);
+            __builtin_amdgcn_sched_barrier(0);
+            chain_ld(B, Tc, k + 4 * D);
+            __builtin_amdgcn_sched_barrier(0);
+            f = chain_add(f, C);
         }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) f = f + cur[q];
-        k += 8;
+        // A, B hold [k, k + 2D); k + 3D <= k1 < k + 6D
+        __builtin_amdgcn_sched_barrier(0);
+        chain_ld(C, Tc, k + 2 * D);
+        f = chain_add(f, A);
+        f = chain_add(f, B);
+        f = chain_add(f, C);
+        k += 3 * D;
     }
     for (; k < k1; ++k) f = f + Tc[k];
     return f;
 }
+
 template <int KIND>
 __global__ __launch_bounds__(256) void k_scalar_fd_chain(const double* __restrict__ x, const double* __restrict__ h,
                                                          int n, int i0, int cnt, const double* __restrict__ p0,
                                                          const double* __restrict__ p1, double power,
                                                          const double* __restrict__ T, double* __restrict__ vals) {
-    __shared__ double Ts[kTermChunk];
+    __shared__ __attribute__((aligned(16))) double Ts[2][kTermChunk];
+    constexpr int kPer = kTermChunk / 2 / 256;   // double2 loads per thread per chunk
     const int lane = threadIdx.x & 63;
     const int q0 = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 64);
     const int q = q0 + lane;
     const bool active = q <= cnt;
     const int j = (active && q < cnt) ? i0 + q : -1;            // perturbed coordinate, -1: base
-    const double xj = j >= 0 ? x[j] + h[j] : 0.0;                 // XdX[j] = X[j] + dX[j]
     const int nt = scalar_nterms<KIND>(n);
+    // this lane's perturbed terms at XdX[j] = X[j] + dX[j]: t_j and (not for power) t_{j-1}
+    double tj = 0.0, tjm1 = 0.0;
+    if (j >= 0) {
+        const double xj = x[j] + h[j];
+        if (j < nt) tj = scalar_term<KIND>(j, n, xj, j + 1 < n ? x[j + 1] : 0.0, p0, p1, power);
+        if (KIND != PNOL_OBJ_POWER && j >= 1 && j - 1 < nt) tjm1 = scalar_term<KIND>(j - 1, n, x[j - 1], xj, p0, p1, power);
+    }
     // terms some lane of the wave perturbs: [w0, w1) (empty for a wave of base / idle lanes)
     const int jlo = i0 + q0, jhi = i0 + min(q0 + 63, cnt - 1);
     int w0 = nt, w1 = nt;
@@ -229,29 +271,40 @@ __global__ __launch_bounds__(256) void k_scalar_fd_chain(const double* __restric
         w0 = max(0, min(KIND == PNOL_OBJ_POWER ? jlo : jlo - 1, nt));
         w1 = max(w0, min(jhi + 1, nt));
     }
+    // chunk c of T into registers (zero past nt; only [c0, c1) is ever read)
+    double2 pre[kPer];
+    auto fetch = [&](int c0) {
+#pragma unroll
+        for (int r = 0; r < kPer; ++r) {
+            const int e = c0 + 2 * (threadIdx.x + 256 * r);
+            pre[r] = make_double2(e < nt ? T[e] : 0.0, e + 1 < nt ? T[e + 1] : 0.0);
+        }
+    };
+    auto stash = [&](double* dst) {
+#pragma unroll
+        for (int r = 0; r < kPer; ++r) reinterpret_cast<double2*>(dst)[threadIdx.x + 256 * r] = pre[r];
+    };
     double f = 0.0;
-    for (int c0 = 0; c0 < nt; c0 += kTermChunk) {
+    fetch(0);
+    stash(Ts[0]);
+    __syncthreads();
+    for (int c0 = 0, cb = 0; c0 < nt; c0 += kTermChunk, cb ^= 1) {
         const int c1 = min(c0 + kTermChunk, nt);
-        __syncthreads();
-        for (int e = threadIdx.x; e < c1 - c0; e += blockDim.x) Ts[e] = T[c0 + e];
-        __syncthreads();
-        const double* __restrict__ Tc = Ts - c0;   // Tc[k] = T[k] for k in [c0, c1)
-        int k = c0;
+        const bool more = c1 < nt;
+        if (more) fetch(c1);                       // in flight during this chunk's chain
+        const double* __restrict__ Tc = Ts[cb] - c0;   // Tc[k] = T[k] for k in [c0, c1)
         const int e0 = min(max(w0, c0), c1);
-        f = chain_sum(f, Tc, k, e0);
-        k = e0;
+        f = chain_sum(f, Tc, c0, e0);
         const int e1 = min(max(w1, c0), c1);
-        for (; k < e1; ++k) {
+        for (int k = e0; k < e1; ++k) {
             double t = Tc[k];
-            const bool touch = j >= 0 && (k == j || (KIND != PNOL_OBJ_POWER && k + 1 == j));
-            if (touch) {
-                const double xk = k == j ? xj : x[k];
-                const double xk1 = k + 1 < n ? (k + 1 == j ? xj : x[k + 1]) : 0.0;
-                t = scalar_term<KIND>(k, n, xk, xk1, p0, p1, power);
-            }
+            t = k == j ? tj : t;
+            if (KIND != PNOL_OBJ_POWER) t = k + 1 == j ? tjm1 : t;
             f = f + t;
         }
-        f = chain_sum(f, Tc, k, c1);
+        f = chain_sum(f, Tc, e1, c1);
+        if (more) stash(Ts[cb ^ 1]);
+        __syncthreads();
     }
     if (active) vals[q] = f;
 }
