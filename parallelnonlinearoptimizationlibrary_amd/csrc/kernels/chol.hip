@@ -196,6 +196,30 @@ __device__ __forceinline__ bool spin_ge(const int* f, int target, int* info) {
     return true;
 }
 
+// Every *f[q] >= tg[q]: all N words are loaded in each round (one memory round trip for the set
+// instead of one per word when they are already there); the same cap and info checks.
+template <int N>
+__device__ __forceinline__ bool spin_all(const int* const (&f)[N], const int (&tg)[N], int* info) {
+    int it = 0;
+    for (;;) {
+        int v[N];
+#pragma unroll
+        for (int q = 0; q < N; ++q) v[q] = __hip_atomic_load(f[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < N; ++q) ok = ok && v[q] >= tg[q];
+        if (ok) return true;
+        __builtin_amdgcn_s_sleep(1);
+        if ((++it & 63) == 0) {
+            if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+            if (it > kSpin) {
+                atomicExch(info, kInfoTimeout);
+                return false;
+            }
+        }
+    }
+}
+
 // ---- the diagonal tile: blocked Cholesky + inverse ---------------------------------------
 // The 64 x 64 tile is factored as two 32-wide panels:
 //   P1  wave 0: the 64 x 32 panel [S11; S21] (lane t = row t, 32 entries in registers) gives
@@ -453,11 +477,19 @@ __device__ __forceinline__ void diag_put(const DiagLds& L, int row, int col, dou
     else if (row >= kHalf) L.S22[(row - kHalf) * kS + col - kHalf] = v;
 }
 
+struct NoEarly {
+    __device__ void operator()(int, int) const {}
+};
+
 // Factor the tile held in L.Sl / L.S22 and write W_d = L_dd^{-1} (64 x 64 row-major) to Wd.
-// STAMP: s_memtime stamps of the phases into st[0..31] (tools/microbench/diag_timing.hip only)
-template <bool STAMP = false, bool SC1 = false>
+// STAMP: s_memtime stamps of the phases into st[0..31] (tools/microbench/diag_timing.hip only).
+// early(wave, lane): run by waves 2 and 3 once T is formed, while waves 0 / 1 finish the second
+// panel (the persistent chain's look-ahead for the next tile, EarlyNext).  Wst != nullptr: rows
+// 32..63 of W_d also go to Wst in the substage layout (the next tile's L = A W^T operand).
+template <bool STAMP = false, bool SC1 = false, class EARLY = NoEarly>
 __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict__ rinv, int* cnt,
-                                            double* __restrict__ Wd, int d, int* info, long long* st = nullptr) {
+                                            double* __restrict__ Wd, int d, int* info, long long* st = nullptr,
+                                            const EARLY& early = EARLY(), double* __restrict__ Wst = nullptr) {
     const int t = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
     // The phases are chained by LDS words instead of workgroup barriers, so the inverse wave
     // finishing W11 overlaps the S22 update:  cnt[0] = final panel columns, cnt[1] = W11 done,
@@ -534,18 +566,17 @@ __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict
 #pragma unroll
             for (int r = 0; r < 4; ++r) L.Tl[(ti * 16 + (lane >> 4) + 4 * r) * kHalf + tj * 16 + (lane & 15)] = tacc[r];
         }
+        early(wave, lane);
     }
     __syncthreads();
     if constexpr (STAMP) if (wave == 0) st[15] = __builtin_amdgcn_s_memtime();
     // P4: W21 = -W22 T
-    {
-        const int qi = wave >> 1, qj = wave & 1;
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
-        acc = mfma_blk<kHalf>(acc, [&](int i, int k) { return -L.W22[(qi * 16 + i) * kS + k]; },
-                              [&](int j, int k) { return L.Tl[k * kHalf + qj * 16 + j]; }, lane);
+    const int qi = wave >> 1, qj = wave & 1;
+    d4 w21 = {0.0, 0.0, 0.0, 0.0};
+    w21 = mfma_blk<kHalf>(w21, [&](int i, int k) { return -L.W22[(qi * 16 + i) * kS + k]; },
+                          [&](int j, int k) { return L.Tl[k * kHalf + qj * 16 + j]; }, lane);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) stg<SC1>(Wd + (kHalf + qi * 16 + (lane >> 4) + 4 * r) * NB + qj * 16 + (lane & 15), acc[r]);
-    }
+    for (int r = 0; r < 4; ++r) stg<SC1>(Wd + (kHalf + qi * 16 + (lane >> 4) + 4 * r) * NB + qj * 16 + (lane & 15), w21[r]);
     if constexpr (STAMP) if (wave == 0) st[16] = __builtin_amdgcn_s_memtime();
     // W11, W22 and the zero upper-right block: thread t writes columns (t & 31) of rows t >> 5 + 8 q
     {
@@ -556,6 +587,20 @@ __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict
             stg<SC1>(Wd + r * NB + c, L.W11[r * kS + c]);
             stg<SC1>(Wd + r * NB + kHalf + c, 0.0);
             stg<SC1>(Wd + (kHalf + r) * NB + kHalf + c, L.W22[r * kS + c]);
+        }
+    }
+    if (Wst) {
+        // rows 32..63 of W_d ([W21 | W22]) in the substage layout; Wst overlaps Lc1 / Lc2 / W11,
+        // whose last reads (the W11 stores above) end at this barrier; W22 lives in the Sl space
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            Wst[qj * kSub + (kHalf + qi * 16 + (lane >> 4) + 4 * r) * kPad + (lane & 15)] = w21[r];
+        const int c = t & 31, r0 = t >> 5;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = r0 + 8 * q;
+            Wst[(2 + (c >> 4)) * kSub + (kHalf + r) * kPad + (c & 15)] = L.W22[r * kS + c];
         }
     }
 }
@@ -604,6 +649,12 @@ __device__ __forceinline__ int diag_blk(int w, int s) {   // (ib << 2) | jb, or 
 // 1 panel, 2 update): first start, last end (100 MHz realtime)
 __device__ unsigned long long g_chol_tl[64 * 3 * 2];
 __device__ unsigned long long g_chol_clk[64 * 8];   // the diagonal workgroup's shader-clock stamps
+// persistent form, per step k (100 MHz realtime): [0] W_k published, panel (k+2, k) [1] claimed
+// [2] flags ok [3] stored; update (k+2, k+1, k) [4] claimed [5] flags ok [6] stored; [7] panel
+// (k+1, k) stored
+__device__ unsigned long long g_chol_crit[64 * 8];
+#define PNOL_CRIT(k, i) \
+    if (threadIdx.x == 0 && (k) >= 0 && (k) < 64) g_chol_crit[8 * (k) + (i)] = __builtin_amdgcn_s_memrealtime();
 #define PNOL_CHOL_STAMP(k, i) \
     if (threadIdx.x == 0 && (k) + 1 < 64) g_chol_clk[8 * ((k) + 1) + (i)] = __builtin_amdgcn_s_memtime();
 __device__ __forceinline__ void chol_tl_mark(int k, int cls, unsigned long long t0) {
@@ -615,6 +666,7 @@ __device__ __forceinline__ void chol_tl_mark(int k, int cls, unsigned long long 
 }
 #else
 #define PNOL_CHOL_STAMP(k, i)
+#define PNOL_CRIT(k, i)
 #endif
 
 // The diagonal tile d = k + 1 (k >= 0) ready for factor_diag: L = A_{d,k} W_k^T (recomputed
@@ -667,6 +719,190 @@ __device__ __forceinline__ void diag_prepare(const double* __restrict__ P, long 
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             diag_put(L, ib * 16 + (lane >> 4) + 4 * r, jb * 16 + (lane & 15), cdd[sb][r]);
+    }
+}
+
+// ---- the persistent chain's look-ahead --------------------------------------------------------
+// While tile d is factored, waves 2 and 3 (idle once T is formed) start the next tile's products:
+// once tiles (d+1, d) and (d+1, d+1) carry the updates of columns < d (their version words), they
+// stage A_{d+1,d} and the lower 16 x 16 blocks of A_{d+1,d+1}, form the left half of
+// L = A_{d+1,d} W_d^T (block columns 0, 1 need only W11, which wave 1 has finished) and apply
+// its part of A_dd - L L^T (K blocks 0, 1).  After the factor, late_prepare forms the right half
+// of L (K blocks up to 3, W_d's rows 32..63 from the LDS copy Wst) and the rest of L L^T.  Every
+// accumulator receives the same MFMAs in the same order as diag_prepare's, so the factor is
+// bitwise method 4's.  Waves 2 / 3 wait for the tiles inside the factor (their dependencies are
+// tasks of step d-1, which never wait on W_d); with a finite cutoff (PNOL_CHOL_LOOKAHEAD = c)
+// they give up once wave 0 has c columns of the tile final, and the next step stages as before.
+constexpr int kLowerBlks = 10;   // lower 16 x 16 blocks of a 64 x 64 tile, index ib (ib + 1) / 2 + jb
+
+__device__ __forceinline__ void blk_ij(int b, int& ib, int& jb) {
+    ib = b >= 6 ? 3 : (b >= 3 ? 2 : (b >= 1 ? 1 : 0));
+    jb = b - ib * (ib + 1) / 2;
+}
+
+__device__ __forceinline__ int lds_peek(const int* w) {
+    const __attribute__((address_space(3))) int* p = (const __attribute__((address_space(3))) int*)w;
+    int v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+
+struct EarlyLds {
+    double* pfx;   // A_{d+1,d} in the substage layout (then L's right half, substages 2, 3)
+    double* pll;   // L's left half, substages 0, 1
+    double* pfc;   // the lower blocks of A_{d+1,d+1} (16 x 16 row-major each), then minus L_left L_left^T
+    int* w;        // [0] decision (1 go, 2 skip), [1] / [2] wave 2 / 3's L_left stored
+};
+
+struct EarlyNext {
+    const double* P;
+    long ldp;
+    int T, d;
+    const int* ver;
+    const double* W11;   // L.W11 of the tile being factored (row stride kS)
+    const int* cnt;      // factor_diag's column counter (wave 0's progress)
+    int cutoff;          // give up once cnt reaches this (> 64: wait for the tiles)
+    EarlyLds E;
+    __device__ void operator()(int wave, int lane) const {
+        const int dn = d + 1;
+        if (dn >= T) return;
+        if (wave == 2) {
+            int ready = 0;
+            for (int it = 0;; ++it) {
+                ready = __hip_atomic_load(ver + dn * T + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= d &&
+                        __hip_atomic_load(ver + dn * T + dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= d;
+                ready = __builtin_amdgcn_readfirstlane(ready);
+                if (ready || it > 4096 || lds_peek(cnt) >= cutoff) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            lds_signal(E.w, ready ? 1 : 2);
+        } else {
+            wait_lds_ge(E.w, 1);
+        }
+        if (__builtin_amdgcn_readfirstlane(lds_peek(E.w)) != 1) return;
+        const int h = wave - 2;   // wave 2: rows 0..31 and blocks 0..4; wave 3: rows 32..63, blocks 5..9
+        {
+            // an opaque copy of the lane id: keeps the (loop-invariant) load offsets from being
+            // hoisted out of the chain loop and held in registers across the factor
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            // the 26 16-byte sc1 loads per lane in one round
+            const double* base = P + (long)(dn * NB + 32 * h) * ldp + d * NB;   // wave-uniform
+            const double* cb = P + (long)(dn * NB) * ldp + dn * NB;
+            double2 v[16], u[10];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int id = q * 64 + ln, row = id >> 5, col = (id & 31) * 2;
+                v[q] = ld16_sc1(base, (unsigned)((row * ldp + col) * 8));
+            }
+#pragma unroll
+            for (int q = 0; q < 10; ++q) {
+                int ib, jb;
+                blk_ij(5 * h + (q >> 1), ib, jb);
+                const int id = (q & 1) * 64 + ln, row = id >> 3, col = (id & 7) * 2;
+                u[q] = ld16_sc1(cb, (unsigned)(((ib * 16 + row) * ldp + jb * 16 + col) * 8));
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int id = q * 64 + ln, row = 32 * h + (id >> 5), col = (id & 31) * 2;
+                *reinterpret_cast<double2*>(E.pfx + (col >> 4) * kSub + row * kPad + (col & 15)) = v[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 10; ++q) {
+                const int id = (q & 1) * 64 + ln, row = id >> 3, col = (id & 7) * 2;
+                *reinterpret_cast<double2*>(E.pfc + (5 * h + (q >> 1)) * 256 + row * 16 + col) = u[q];
+            }
+        }
+        const int frow = lane & 15, fk = lane >> 4;
+        // L's left half for this wave's strips (block columns jb = 0, 1: K blocks kb <= jb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int strip = 2 * h + s;
+            d4 acc[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const double a = E.pfx[kb * kSub + (strip * 16 + frow) * kPad + kk * 4 + fk];
+#pragma unroll
+                    for (int jb = kb; jb < 2; ++jb) {
+                        const double b = W11[(jb * 16 + frow) * kS + kb * 16 + kk * 4 + fk];
+                        acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[jb], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+            for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    E.pll[jb * kSub + (strip * 16 + (lane >> 4) + 4 * r) * kPad + (lane & 15)] = acc[jb][r];
+        }
+        lds_signal(E.w + 1 + h, 1);
+        wait_lds_ge(E.w + 2 - h, 1);
+        // this wave's five blocks of A_dd - L_left L_left^T (K blocks 0, 1)
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const int b = 5 * h + q;
+            int ib, jb;
+            blk_ij(b, ib, jb);
+            d4 c;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c[r] = E.pfc[b * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15)];
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const double a = -E.pll[kb * kSub + (ib * 16 + frow) * kPad + kk * 4 + fk];
+                    const double bb = E.pll[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
+                    c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, c, 0, 0, 0);
+                }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) E.pfc[b * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15)] = c[r];
+        }
+    }
+};
+
+// The rest of diag_prepare after a look-ahead: L's right half (block columns 2, 3) from the staged
+// A_{d,k} (E.pfx) and W_k's rows 32..63 (Wst), then K blocks 2, 3 of A_dd - L L^T on the partial
+// blocks in E.pfc, into the split LDS copy L.
+__device__ __forceinline__ void late_prepare(const EarlyLds& E, const double* __restrict__ Wst, const DiagLds& L,
+                                             int wave, int lane) {
+    const int frow = lane & 15, fk = lane >> 4;
+    d4 lr[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const double a = E.pfx[kb * kSub + (wave * 16 + frow) * kPad + kk * 4 + fk];
+#pragma unroll
+            for (int jb = (kb > 2 ? kb : 2); jb < 4; ++jb) {
+                const double b = Wst[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
+                lr[jb - 2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, lr[jb - 2], 0, 0, 0);
+            }
+        }
+    // this wave's own rows of substages 2, 3 (only it reads them above)
+#pragma unroll
+    for (int jb = 2; jb < 4; ++jb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) E.pfx[jb * kSub + (wave * 16 + (lane >> 4) + 4 * r) * kPad + (lane & 15)] = lr[jb - 2][r];
+    __syncthreads();
+#pragma unroll
+    for (int sb = 0; sb < 3; ++sb) {
+        const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
+        if (bl < 0) continue;   // wave-uniform
+        const int b = ib * (ib + 1) / 2 + jb;
+        d4 c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c[r] = E.pfc[b * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15)];
+#pragma unroll
+        for (int kb = 2; kb < 4; ++kb)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const double a = -E.pfx[kb * kSub + (ib * 16 + frow) * kPad + kk * 4 + fk];
+                const double bb = E.pfx[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
+                c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, c, 0, 0, 0);
+            }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) diag_put(L, ib * 16 + (lane >> 4) + 4 * r, jb * 16 + (lane & 15), c[r]);
     }
 }
 
@@ -847,11 +1083,16 @@ __device__ __forceinline__ void publish(int* w, int v) {
 __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P, double* __restrict__ Lm, long ldp,
                                                       int T, double* __restrict__ W, double* __restrict__ bv,
                                                       double* __restrict__ zv, int* __restrict__ flags, int ntasks,
-                                                      int* __restrict__ info) {
+                                                      int* __restrict__ info, int lookahead) {
     __shared__ __attribute__((aligned(16))) double smem[2 * kStage];   // 73.7 KB
+    // the chain's look-ahead areas (EarlyNext / late_prepare): 75.8 KB
+    __shared__ __attribute__((aligned(16))) double pfx[kStage];
+    __shared__ __attribute__((aligned(16))) double pll[2 * kSub];
+    __shared__ __attribute__((aligned(16))) double pfc[kLowerBlks * 256];
     __shared__ double rinv[NB];
     __shared__ double zsh[NB];
     __shared__ int cnt[6];
+    __shared__ int ew[4];
     __shared__ int task_sh, ok_sh;
     const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), wr = wave >> 1, wc = wave & 1;
     const PersistWords pw = persist_words(flags, T);
@@ -859,6 +1100,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
     double* Y = smem + kStage;
 
     if (blockIdx.x == 0) {   // ---------------- the diagonal chain
+        const EarlyLds E{pfx, pll, pfc, ew};
+        if (t < 4) ew[t] = 0;
         for (int d = 1; d < T; ++d) {
             const int k = d - 1;
 #ifdef PNOL_CHOL_TIMELINE
@@ -866,20 +1109,32 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
 #endif
             if (t == 0) {
                 const bool ok = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-                                spin_ge(pw.ver + d * T + k, k, info) && spin_ge(pw.ver + d * T + d, k, info);
+                                spin_all<2>({pw.ver + d * T + k, pw.ver + d * T + d}, {k, k}, info);
                 ok_sh = ok;
             }
             __syncthreads();
             if (!ok_sh) return;
             PNOL_CHOL_STAMP(k, 5)
             const DiagLds L = diag_lds(smem);
-            if (t < 6) cnt[t] = 0;
-            diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane);
+            // the previous factor's waves 2 / 3 staged this tile and did half of its products
+            const bool pre = lookahead && ew[0] == 1;
+#ifdef PNOL_CHOL_TIMELINE
+            if (t == 0 && k + 1 < 64) g_chol_clk[8 * (k + 1) + 6] = pre ? 1 : 0;
+#endif
+            if (pre) late_prepare(E, Y, L, wave, lane);
+            else diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane);
+            if (t < 6) cnt[t] = 0;   // every read of cnt / ew above is behind a barrier inside
+            if (t < 4) ew[t] = 0;    // either prepare
             __syncthreads();
             PNOL_CHOL_STAMP(k, 3)
-            factor_diag<false, true>(L, rinv, cnt, W + (long)d * NB * NB, d, info);
+            if (lookahead)
+                factor_diag<false, true, EarlyNext>(L, rinv, cnt, W + (long)d * NB * NB, d, info, nullptr,
+                                                    EarlyNext{P, ldp, T, d, pw.ver, L.W11, cnt, lookahead, E}, Y);
+            else
+                factor_diag<false, true>(L, rinv, cnt, W + (long)d * NB * NB, d, info);
             PNOL_CHOL_STAMP(k, 4)
             publish(pw.wdone + d, 1);   // its barrier also ends every read of this step's LDS
+            PNOL_CRIT(d, 0)
 #ifdef PNOL_CHOL_TIMELINE
             chol_tl_mark(k, 0, tl0);
             if (threadIdx.x == 0 && k + 1 < 64) g_chol_clk[8 * (k + 1)] = ck0;
@@ -908,13 +1163,17 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             const int i = k + 1 + g, i0 = i * NB;
 #ifdef PNOL_CHOL_TIMELINE
             const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
+            if (i == k + 2) PNOL_CRIT(k, 1)
 #endif
             if (t == 0) {
                 // W_k (tile 0 comes from the prep launch), A_ik through column k-1, b_k complete,
                 // and b_i's earlier updates
-                const bool ok = (k == 0 || spin_ge(pw.wdone + k, 1, info)) && spin_ge(pw.ver + i * T + k, k, info) &&
-                                spin_ge(pw.bcnt + k, k, info) && spin_ge(pw.bcnt + i, k, info);
+                const bool ok = spin_all<4>({pw.wdone + k, pw.ver + i * T + k, pw.bcnt + k, pw.bcnt + i},
+                                            {k == 0 ? 0 : 1, k, k, k}, info);
                 ok_sh = ok;
+#ifdef PNOL_CHOL_TIMELINE
+                if (i == k + 2) PNOL_CRIT(k, 2)
+#endif
             }
             __syncthreads();
             if (!ok_sh) return;
@@ -926,6 +1185,10 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             mfma_xyt<false>(acc, X, Y, wr, wc, lane);
             acc_store<true>(acc, Lm, ldp, i0, k0, wr, wc, lane);
             publish(pw.lcnt + i, k + 1);
+#ifdef PNOL_CHOL_TIMELINE
+            if (i == k + 2) PNOL_CRIT(k, 3)
+            if (i == k + 1) PNOL_CRIT(k, 7)
+#endif
             acc_to_rows(acc, X, wr, wc, lane);   // X is free (the MFMA finished before the barrier)
             if (t < NB) {
                 double s = 0.0;
@@ -961,11 +1224,15 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         const int i = j + u;
 #ifdef PNOL_CHOL_TIMELINE
         const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
+        const bool crit = i == k + 2 && j == k + 1;
+        if (crit) PNOL_CRIT(k, 4)
 #endif
         if (t == 0) {
-            const bool ok = spin_ge(pw.lcnt + i, k + 1, info) && spin_ge(pw.lcnt + j, k + 1, info) &&
-                            spin_ge(pw.ver + i * T + j, k, info);
+            const bool ok = spin_all<3>({pw.lcnt + i, pw.lcnt + j, pw.ver + i * T + j}, {k + 1, k + 1, k}, info);
             ok_sh = ok;
+#ifdef PNOL_CHOL_TIMELINE
+            if (crit) PNOL_CRIT(k, 5)
+#endif
         }
         __syncthreads();
         if (!ok_sh) return;
@@ -978,6 +1245,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         acc_store<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
         publish(pw.ver + i * T + j, k + 1);
 #ifdef PNOL_CHOL_TIMELINE
+        if (crit) PNOL_CRIT(k, 6)
         chol_tl_mark(k, 2, tl0);
 #endif
     }
@@ -1114,16 +1382,23 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
     if (persist) {
         int ntasks = 0;
         for (int R = T - 1; R >= 1; --R) ntasks += R + R * (R + 1) / 2 - 1;
-        // tuning knobs (read per call): PNOL_CHOL5_WORKERS = worker workgroups, PNOL_CHOL5_SOLO = 1:
-        // a dynamic LDS pad so no two workgroups share a CU (the diagonal chain runs alone)
+        // tuning knob (read per call): PNOL_CHOL5_WORKERS = worker workgroups; one per CU
+        // (the look-ahead areas already hold the static LDS to one workgroup per CU).
+        // PNOL_CHOL_LOOKAHEAD = 0 turns the diagonal chain's look-ahead off (read per call).
         const char* ew = std::getenv("PNOL_CHOL5_WORKERS");
-        const char* es = std::getenv("PNOL_CHOL5_SOLO");
-        const bool solo = es && std::atoi(es) != 0;
-        const int slots = (solo ? 1 : 2) * std::max(ctx->num_cu, 1) - 1;
+        const char* el = std::getenv("PNOL_CHOL_LOOKAHEAD");
+        // > 0: the look-ahead gives up once wave 0 has finished that many columns of the tile
+        // (0 off; above 64: the factor waits for the next tiles).  Measured at n = 2048
+        // (tools/microbench/chol_timeline.hip): 0: 0.645 ms, 52: 0.625, 64: 0.621 (default; half
+        // the steps find their tiles ready), 1000: 0.705 -- the next tiles wait on a panel and an
+        // update task (~6 us each after W_{d-1}), so waiting for them inside the factor costs more
+        // than the prepare it saves.
+        const int lookahead = el ? std::max(0, std::atoi(el)) : 64;
+        const int slots = std::max(ctx->num_cu, 1) - 1;
         const int want = ew ? std::atoi(ew) : slots;
         const int workers = std::max(1, std::min(ntasks, want));
-        hipLaunchKernelGGL(k_chol_persist, dim3(1 + workers), dim3(256), solo ? 16384 : 0, ctx->stream, (double*)P,
-                           (double*)Lm, ldp, T, (double*)W, (double*)bv, (double*)zv, (int*)pf, ntasks, dinfo);
+        hipLaunchKernelGGL(k_chol_persist, dim3(1 + workers), dim3(256), 0, ctx->stream, (double*)P, (double*)Lm, ldp,
+                           T, (double*)W, (double*)bv, (double*)zv, (int*)pf, ntasks, dinfo, lookahead);
     }
     const int epoch = ++ctx->chol4_epoch;
     hipLaunchKernelGGL(k_chol_bwd, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n, (const double*)W,

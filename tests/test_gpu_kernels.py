@@ -346,6 +346,30 @@ def test_cholesky_persistent_equals_per_step_launches(ctx, n):
     assert np.linalg.norm(_np(s5) - x) <= 1e-10 * np.linalg.norm(x) * np.linalg.cond(A)
 
 
+@pytest.mark.parametrize("n", [130, 700, 2048, 2111])
+def test_cholesky_lookahead_equals_plain_chain(ctx, monkeypatch, n):
+    """Method 5's diagonal chain starts the next tile's products inside the current factor
+    (waves 2 / 3: the left half of L and K blocks 0, 1 of A_dd - L L^T), the rest after it.
+    Every accumulator takes the same MFMAs in the same order: sigma is bitwise the chain without
+    the look-ahead (PNOL_CHOL_LOOKAHEAD=0) and method 4's."""
+    rng = np.random.default_rng(n + 7)
+    J = rng.standard_normal((n + 64, n))
+    A = J.T @ J + 0.25 * np.eye(n)
+    b = rng.standard_normal(n)
+    At, bt = ctx.tensor(A), ctx.tensor(b)
+    monkeypatch.setenv("PNOL_CHOL_LOOKAHEAD", "0")
+    s_off, i_off = ctx.solve(At, bt, method=5)
+    monkeypatch.setenv("PNOL_CHOL_LOOKAHEAD", "52")   # gives up when late: mixed steps
+    s_mix, i_mix = ctx.solve(At, bt, method=5)
+    monkeypatch.delenv("PNOL_CHOL_LOOKAHEAD")           # default: every step
+    s_on, i_on = ctx.solve(At, bt, method=5)
+    s4, i4 = ctx.solve(At, bt, method=4)
+    assert i_off == i_mix == i_on == i4 == 1
+    assert np.array_equal(_np(s_on), _np(s_off))
+    assert np.array_equal(_np(s_mix), _np(s_off))
+    assert np.array_equal(_np(s_on), _np(s4))
+
+
 @pytest.mark.parametrize("n", [200, 1000])
 def test_cholesky_falls_back_to_lu_on_indefinite(ctx, oracle, n):
     rng = np.random.default_rng(9)

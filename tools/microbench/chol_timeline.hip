@@ -57,6 +57,7 @@ int main(int argc, char** argv) {
         hipStreamSynchronize(ctx->stream);
         hipMemcpyToSymbol(HIP_SYMBOL(g_chol_clk), zero.data(), sizeof(unsigned long long) * zero.size());
         hipMemcpyToSymbol(HIP_SYMBOL(g_chol_tl), init.data(), sizeof(unsigned long long) * init.size());
+        hipMemcpyToSymbol(HIP_SYMBOL(g_chol_crit), zero.data(), sizeof(unsigned long long) * zero.size());
         hipEventRecord(e0, ctx->stream);
         if (launch_chol_solve(ctx, A, n, b, x, n, info) != PNOL_OK) return 1;
         hipEventRecord(e1, ctx->stream);
@@ -83,7 +84,7 @@ int main(int argc, char** argv) {
         sum_gap += gap;
         std::printf("%s{\"k\": %d, \"diag\": [%.2f, %.2f], \"panel\": [%.2f, %.2f], \"update\": [%.2f, %.2f], "
                     "\"gap_to_next_diag\": %.2f, \"diag_cycles\": %llu, \"diag_clock_ghz\": %.3f, "
-                    "\"stamps\": [%lld, %lld, %lld, %lld, %lld, %lld]}",
+                    "\"stamps\": [%lld, %lld, %lld, %lld, %lld, %lld], \"lookahead_used\": %llu}",
                     s ? ", " : "", s - 1, ds, de, hp ? (at(s, 1, 0) - base) * 0.01 : -1.0,
                     hp ? (at(s, 1, 1) - base) * 0.01 : -1.0, hu ? (at(s, 2, 0) - base) * 0.01 : -1.0,
                     hu ? (at(s, 2, 1) - base) * 0.01 : -1.0, gap, ck[8 * s + 7] - ck[8 * s],
@@ -93,11 +94,20 @@ int main(int argc, char** argv) {
                     (long long)(ck[8 * s + 3] - ck[8 * s]), (long long)(ck[8 * s + 4] - ck[8 * s]),
                     (long long)(ck[8 * s + 7] - ck[8 * s]),
                     // persistent form: the end of the wait for the two tiles (0 in method 4)
-                    ck[8 * s + 5] ? (long long)(ck[8 * s + 5] - ck[8 * s]) : 0LL);
+                    ck[8 * s + 5] ? (long long)(ck[8 * s + 5] - ck[8 * s]) : 0LL, ck[8 * s + 6]);
+    }
+    std::vector<unsigned long long> cr(64 * 8);
+    hipMemcpyFromSymbol(cr.data(), HIP_SYMBOL(g_chol_crit), sizeof(unsigned long long) * cr.size());
+    std::printf("], \"critical_us_after_W\": [");
+    for (int k = 1; k + 2 < T && k < 64; ++k) {
+        auto dt = [&](int i) { return cr[8 * k + i] ? ((long long)cr[8 * k + i] - (long long)cr[8 * k]) * 0.01 : -1.0; };
+        std::printf("%s[%d, %.2f, %.2f, %.2f, %.2f, %.2f, %.2f, %.2f]", k > 1 ? ", " : "", k, dt(1), dt(2), dt(3), dt(4),
+                    dt(5), dt(6), dt(7));
     }
     std::printf("], \"sum_diag_us\": %.1f, \"sum_gap_us\": %.1f, \"workers\": \"%s\", \"solo\": \"%s\", "
-                "\"persist\": \"%s\"}\n", sum_diag, sum_gap, std::getenv("PNOL_CHOL5_WORKERS") ? std::getenv("PNOL_CHOL5_WORKERS") : "",
+                "\"persist\": \"%s\", \"lookahead\": \"%s\"}\n", sum_diag, sum_gap, std::getenv("PNOL_CHOL5_WORKERS") ? std::getenv("PNOL_CHOL5_WORKERS") : "",
                 std::getenv("PNOL_CHOL5_SOLO") ? std::getenv("PNOL_CHOL5_SOLO") : "",
-                std::getenv("PNOL_CHOL_PERSIST") ? std::getenv("PNOL_CHOL_PERSIST") : "");
+                std::getenv("PNOL_CHOL_PERSIST") ? std::getenv("PNOL_CHOL_PERSIST") : "",
+                std::getenv("PNOL_CHOL_LOOKAHEAD") ? std::getenv("PNOL_CHOL_LOOKAHEAD") : "");
     return 0;
 }
