@@ -404,15 +404,24 @@ int pnol_fd_gradient(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const doubl
     PNOL_CHECK(set_device(ctx));
     if (!obj || !x || !h || !f0 || (cnt > 0 && !g) || cnt < 0 || i0 < 0 || i0 + cnt > obj->n) return PNOL_ERR_ARG;
     const size_t n = (size_t)obj->n, io = 2 * n + (size_t)cnt + 1;
-    void* dv = nullptr;
+    void *dv = nullptr, *dhv = nullptr;
     PNOL_CHECK(ws_get(ctx, "fdg_io", sizeof(double) * io, &dv));
+    PNOL_CHECK(ws_get(ctx, "fdg_h", sizeof(double) * n, &dhv));
     double* dx = (double*)dv;
-    double *dh = dx + n, *dg = dh + n, *df = dg + cnt;
+    double *dg = dx + 2 * n, *df = dg + cnt, *dh = (double*)dhv;
     double* st = (double*)pinned_stage(ctx, sizeof(double) * io);
     if (!st) return PNOL_ERR_NOMEM;
     std::memcpy(st, x, sizeof(double) * n);
-    std::memcpy(st + n, h, sizeof(double) * n);
-    PNOL_HIP(hipMemcpyAsync(dx, st, sizeof(double) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+    PNOL_HIP(hipMemcpyAsync(dx, st, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
+    // the step vector rarely changes between calls (a solver's dX): re-upload it only when its
+    // content differs from the copy on the device (the workspace buffer is the one it went to)
+    if (ctx->fdg_h_dev != dh || ctx->fdg_h_host.size() != n ||
+        std::memcmp(ctx->fdg_h_host.data(), h, sizeof(double) * n) != 0) {
+        std::memcpy(st + n, h, sizeof(double) * n);
+        PNOL_HIP(hipMemcpyAsync(dh, st + n, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
+        ctx->fdg_h_host.assign(h, h + n);
+        ctx->fdg_h_dev = dh;
+    }
     {
         ScopedTimer tm(ctx, "fd_gradient");
         PNOL_CHECK(launch_fd_gradient(ctx, obj, dx, dh, i0, cnt, df, dg));

@@ -21,7 +21,8 @@ inline void eval_line_points(Objective* o, const std::vector<double>& X, const s
                              const double* alphas, int na, double* f) {
     if (na <= 0) return;
     const int n = (int)X.size();
-    std::vector<double> pts((size_t)na * n);
+    thread_local std::vector<double> pts;   // kept across calls (one batch per line-search step)
+    pts.resize((size_t)na * n);
     for (int k = 0; k < na; ++k) {
         double* row = pts.data() + (size_t)k * n;
         const double a = alphas[k];
@@ -37,15 +38,20 @@ inline void eval_line_points_recur(Objective* o, const std::vector<double>& X, c
                                    const std::vector<bool>& cI, double* f) {
     if (na <= 0) return;
     const int nf = (int)cX.size();
-    std::vector<int> map;
-    for (int i = 0; i < nf; ++i)
-        if (!cI[i]) map.push_back(i);
-    std::vector<double> pts((size_t)na * nf);
+    thread_local std::vector<double> pts;   // kept across calls (two per bounded BFGS iteration)
+    pts.resize((size_t)na * nf);
     for (int k = 0; k < na; ++k) {
         double* row = pts.data() + (size_t)k * nf;
-        for (int i = 0; i < nf; ++i) row[i] = cX[i];
         const double a = alphas[k];
-        for (size_t r = 0; r < map.size(); ++r) row[map[r]] = X[r] + a * p[r];
+        size_t r = 0;
+        for (int i = 0; i < nf; ++i) {
+            if (cI[i]) {
+                row[i] = cX[i];
+            } else {
+                row[i] = X[r] + a * p[r];
+                ++r;
+            }
+        }
     }
     o->objEvalBatch(pts.data(), na, nf, f);
 }

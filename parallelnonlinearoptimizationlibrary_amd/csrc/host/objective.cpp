@@ -201,17 +201,32 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
     const int N = (int)X.size();
     dFdX.resize(N);
     if (pnol_dobj* d = deviceObjective((int)constantX.size())) {
-        // full-length point and step: the free coordinate i maps to full index map[i]; the
-        // perturbed point equals the reference's scatter(X + dX_i e_i) bit for bit
-        std::vector<double> Xf = scatter_full(X, constantX, constantIndicator);
-        std::vector<double> hf(Xf.size(), 1.0);
-        const std::vector<int> map = free_map(constantIndicator);
-        for (int i = 0; i < N; ++i) hf[map[i]] = dX[i];
-        std::vector<double> gf(Xf.size());
+        // full-length point and step: the free coordinate i maps to full index i_f; the
+        // perturbed point equals the reference's scatter(X + dX_i e_i) bit for bit.  One pass
+        // builds both (frozen coordinates: their constant and a dummy step 1.0), in buffers kept
+        // across calls (the bounded solvers call this twice per iteration at full length).
+        const size_t nf = constantX.size();
+        thread_local std::vector<double> Xf, hf, gf;
+        Xf.resize(nf);
+        hf.resize(nf);
+        gf.resize(nf);
+        size_t ir = 0;
+        for (size_t i = 0; i < nf; ++i) {
+            if (constantIndicator[i]) {
+                Xf[i] = constantX[i];
+                hf[i] = 1.0;
+            } else {
+                Xf[i] = X[ir];
+                hf[i] = dX[ir];
+                ++ir;
+            }
+        }
         double F = 0;
-        device_gradient(d, Xf, hf, 0, (int)Xf.size(), &F, gf.data());
+        device_gradient(d, Xf, hf, 0, (int)nf, &F, gf.data());
         countEvals(N + 1);
-        for (int i = 0; i < N; ++i) dFdX[i] = gf[map[i]];
+        ir = 0;
+        for (size_t i = 0; i < nf; ++i)
+            if (!constantIndicator[i]) dFdX[ir++] = gf[i];
         return;
     }
     std::vector<double> v(N + 1);

@@ -45,6 +45,9 @@ struct pnol_ctx {
     pnol::Workspace ws;
     void* pinned = nullptr;         // pinned host staging for pnol_memcpy_* (grown on demand)
     size_t pinned_bytes = 0;
+    // pnol_fd_gradient's step vector as last uploaded (host copy) and where it went
+    std::vector<double> fdg_h_host;
+    const double* fdg_h_dev = nullptr;
     // two slots of linear-residual prefix checkpoints ("linres_ckpt0/1"), each tagged with the
     // objective and the device x it was computed at; use = last-use stamp (least recent is reused)
     unsigned long long ckpt_oid[2] = {0, 0};   // pnol_dobj::id (0: untagged)
