@@ -771,7 +771,7 @@ __global__ __launch_bounds__(256) void k_linres_fdP(const double* __restrict__ A
         for (int j = 0; j < kPW; ++j)
             if (j < np) {
                 const int col = c0 + j;
-                out[(long)(col - tl.jbase) * ldjt] = ((acc[j] - yr) - f0) / h[col];
+                __builtin_nontemporal_store(((acc[j] - yr) - f0) / h[col], out + (long)(col - tl.jbase) * ldjt);
             }
     }
 }

@@ -216,7 +216,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                 for (int r = 0; r < 4; ++r) {
                     int row = wr * WTM + mi * 16 + orow + 4 * r;
                     int col = wc * WTN + ni * 16 + ocol;
-                    out[row * ld + col] = acc[mi][ni][r];
+                    __builtin_nontemporal_store(acc[mi][ni][r], out + row * ld + col);
                 }
     } else {
 #pragma unroll
