@@ -636,6 +636,24 @@ __device__ __forceinline__ void diag_strip_to_stage(const d4 (&acc)[4], double* 
         for (int r = 0; r < 4; ++r) X[jb * kSub + (w * 16 + (lane >> 4) + 4 * r) * kPad + (lane & 15)] = acc[jb][r];
 }
 
+// a panel's L strip (this wave's 16 rows of L_ik, from diag_l_strip) to the factor matrix, and
+// into LDS row-major 64 x 65 (the forward substitution's copy)
+template <bool SC1 = false>
+__device__ __forceinline__ void strip_store(const d4 (&acc)[4], double* __restrict__ Lm, long ldp, int r0, int c0, int w,
+                                            int lane) {
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            stg<SC1>(Lm + (long)(r0 + w * 16 + (lane >> 4) + 4 * r) * ldp + c0 + jb * 16 + (lane & 15), acc[jb][r]);
+}
+__device__ __forceinline__ void strip_to_rows(const d4 (&acc)[4], double* __restrict__ S, int w, int lane) {
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) S[(w * 16 + (lane >> 4) + 4 * r) * (NB + 1) + jb * 16 + (lane & 15)] = acc[jb][r];
+}
+
 // A_dd - L L^T on the 10 lower 16 x 16 blocks (ib >= jb) only -- the factor never reads the
 // upper ones -- 3 / 3 / 2 / 2 blocks per wave (48 MFMAs on the busiest wave instead of 64)
 __device__ __forceinline__ int diag_blk(int w, int s) {   // (ib << 2) | jb, or -1
@@ -985,10 +1003,12 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
         stage_tile(X, P, ldp, i0, k0);
         stage_tile(Y, W + (long)k * NB * NB, NB, 0, 0);
         __syncthreads();
-        d4 acc[2][2];
-        acc_zero(acc);
-        mfma_xyt<false>(acc, X, Y, wr, wc, lane);
-        acc_store(acc, Lm, ldp, i0, k0, wr, wc, lane);
+        // W_k is lower triangular: each wave forms a 16-row strip of L_ik over the nonzero K
+        // blocks only (40 MFMAs instead of 64; the diagonal workgroup's own L uses the same
+        // products, so both copies of L_{k+1,k} carry the same bits)
+        d4 acc[4];
+        diag_l_strip(acc, X, Y, wave, lane);
+        strip_store(acc, Lm, ldp, i0, k0, wave, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();                                 // every wave's stores have drained
         if (t == 0) {
@@ -997,7 +1017,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
             __hip_atomic_store(rowflag + i, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         // forward substitution carried by the panel: z_k = W_k b_k, b_i -= L_ik z_k
-        acc_to_rows(acc, X, wr, wc, lane);   // X is free (the MFMA finished before the barrier)
+        strip_to_rows(acc, X, wave, lane);   // X is free (the MFMA finished before the barrier)
         if (t < NB) {
             double s = 0.0;
 #pragma unroll 16
@@ -1165,31 +1185,31 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
             if (i == k + 2) PNOL_CRIT(k, 1)
 #endif
-            if (t == 0) {
-                // W_k (tile 0 comes from the prep launch), A_ik through column k-1, b_k complete,
-                // and b_i's earlier updates
-                const bool ok = spin_all<4>({pw.wdone + k, pw.ver + i * T + k, pw.bcnt + k, pw.bcnt + i},
-                                            {k == 0 ? 0 : 1, k, k, k}, info);
-                ok_sh = ok;
+            // A_ik through column k-1, b_k complete and b_i's earlier updates: usually long
+            // before W_k, so A_ik is staged while the workgroup waits for the diagonal chain
+            if (t == 0) ok_sh = spin_all<3>({pw.ver + i * T + k, pw.bcnt + k, pw.bcnt + i}, {k, k, k}, info);
+            __syncthreads();
+            if (!ok_sh) return;
+            stage_tile<true>(X, P, ldp, i0, k0);
+            if (t == 0) {   // W_k (tile 0 comes from the prep launch)
+                ok_sh = k == 0 || spin_ge(pw.wdone + k, 1, info);
 #ifdef PNOL_CHOL_TIMELINE
                 if (i == k + 2) PNOL_CRIT(k, 2)
 #endif
             }
             __syncthreads();
             if (!ok_sh) return;
-            stage_tile<true>(X, P, ldp, i0, k0);
             stage_tile<true>(Y, W + (long)k * NB * NB, NB, 0, 0);
             __syncthreads();
-            d4 acc[2][2];
-            acc_zero(acc);
-            mfma_xyt<false>(acc, X, Y, wr, wc, lane);
-            acc_store<true>(acc, Lm, ldp, i0, k0, wr, wc, lane);
+            d4 acc[4];   // this wave's 16-row strip of L_ik (nonzero K blocks of W_k^T only)
+            diag_l_strip(acc, X, Y, wave, lane);
+            strip_store<true>(acc, Lm, ldp, i0, k0, wave, lane);
             publish(pw.lcnt + i, k + 1);
 #ifdef PNOL_CHOL_TIMELINE
             if (i == k + 2) PNOL_CRIT(k, 3)
             if (i == k + 1) PNOL_CRIT(k, 7)
 #endif
-            acc_to_rows(acc, X, wr, wc, lane);   // X is free (the MFMA finished before the barrier)
+            strip_to_rows(acc, X, wave, lane);   // X is free (the MFMA finished before the barrier)
             if (t < NB) {
                 double s = 0.0;
 #pragma unroll 16
@@ -1227,9 +1247,15 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         const bool crit = i == k + 2 && j == k + 1;
         if (crit) PNOL_CRIT(k, 4)
 #endif
+        // the tile's earlier updates first: its loads stay in flight while the workgroup waits
+        // for the two panels
+        if (t == 0) ok_sh = spin_ge(pw.ver + i * T + j, k, info);
+        __syncthreads();
+        if (!ok_sh) return;
+        d4 acc[2][2];
+        acc_load<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
         if (t == 0) {
-            const bool ok = spin_all<3>({pw.lcnt + i, pw.lcnt + j, pw.ver + i * T + j}, {k + 1, k + 1, k}, info);
-            ok_sh = ok;
+            ok_sh = spin_all<2>({pw.lcnt + i, pw.lcnt + j}, {k + 1, k + 1}, info);
 #ifdef PNOL_CHOL_TIMELINE
             if (crit) PNOL_CRIT(k, 5)
 #endif
@@ -1238,8 +1264,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         if (!ok_sh) return;
         stage_tile<true>(X, Lm, ldp, i * NB, k0);
         if (i != j) stage_tile<true>(Y, Lm, ldp, j * NB, k0);
-        d4 acc[2][2];
-        acc_load<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
         __syncthreads();
         mfma_xyt<true>(acc, X, i != j ? Y : X, wr, wc, lane);
         acc_store<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
