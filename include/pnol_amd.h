@@ -254,6 +254,13 @@ int pnol_fd_jacobian_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const dou
  * nchunks <= 1 runs them back to back. */
 int pnol_fd_jtj_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0, int compute_f0,
                   double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, int nchunks);
+/* pnol_fd_jtj_d (nchunks = 1) + pnol_jtr_d(JT, F0, rhs) in one queue (LevenbergMarquardt.cpp:55-80):
+ * the FD Jacobian, A = J^T J with the Marquardt diagonal, and rhs = -(J^T F0), where F0 = F(x)
+ * as computed or reused per compute_f0.  The -J^T F GEMV is launched behind the J^T J partial
+ * tiles without a stream barrier, so it runs on the CUs the J^T J frees in its last dispatch
+ * round.  Bitwise the same JT, A and rhs as the separate calls. */
+int pnol_fd_normal_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0, int compute_f0,
+                     double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, double* rhs);
 /* The FD Jacobian rows of a tile list (columns [start[t], start[t] + count[t]), count <=
  * PNOL_FD_TILE), column c written to JT + c * ldjt; one base-chain pass for all tiles. */
 int pnol_fd_jacobian_tiles_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, const int* start,

@@ -229,10 +229,10 @@ class LMAsync {
                                        nullptr),
                   "normal equations");
         } else {
-            check(pnol_fd_jtj_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 3 : 1, JT_.get(), ldjt_, lambda,
-                                A_.get(), lda_, nullptr, 1),
-                  "fd_jtj");
-            check(pnol_jtr_d(ctx_, JT_.get(), ldjt_, m_, n_, F(s), rhs_.get()), "jtr");
+            // FD Jacobian, A and -J^T F in one queue (the GEMV in the J^T J's tail)
+            check(pnol_fd_normal_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 3 : 1, JT_.get(), ldjt_, lambda,
+                                   A_.get(), lda_, nullptr, rhs_.get()),
+                  "fd_normal");
         }
         check(pnol_solve_async_d(ctx_, A_.get(), lda_, rhs_.get(), sig(s), n_, info(s)), "solve");
         finish(s);

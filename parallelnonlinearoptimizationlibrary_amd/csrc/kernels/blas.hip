@@ -616,7 +616,8 @@ int launch_gemv_neg(pnol_ctx* ctx, const double* A, int lda, int rows, int cols,
 }
 
 int launch_gemv_neg_slices(pnol_ctx* ctx, const double* A, int lda, long sstride, int rows, int m, int mS, int s0,
-                           int nsl, const double* x, double* y) {
+                           int nsl, const double* x, double* y, hipStream_t stream) {
+    if (!stream) stream = ctx->stream;
     if (!A || !x || !y || rows <= 0 || nsl <= 0 || (mS & 1) || !aligned16(x)) return PNOL_ERR_ARG;
     // rows per workgroup (PNOL_JTR_ROWS = 1, 2 or 4; tuning -- each row's sum is the same for all)
     static const int R = [] {
@@ -628,7 +629,7 @@ int launch_gemv_neg_slices(pnol_ctx* ctx, const double* A, int lda, long sstride
     const bool vec = !((lda & 1) || (sstride & 1) || !aligned16(A));
     const dim3 grid((rows + R - 1) / R, nsl);
 #define PNOL_SLICES(RR, V) \
-    hipLaunchKernelGGL((k_gemv_neg_slices<RR, V>), grid, dim3(256), 0, ctx->stream, A, (long)lda, sstride, rows, m, mS, s0, x, y)
+    hipLaunchKernelGGL((k_gemv_neg_slices<RR, V>), grid, dim3(256), 0, stream, A, (long)lda, sstride, rows, m, mS, s0, x, y)
     if (vec) {
         if (R == 1) PNOL_SLICES(1, true); else if (R == 4) PNOL_SLICES(4, true); else PNOL_SLICES(2, true);
     } else {

@@ -31,6 +31,12 @@ constexpr int kTile = 128;
 constexpr int kTK = 16;
 constexpr int kPad = 18;   // LDS row stride in doubles
 
+// MFMA fragments read from LDS 16 bytes at a time (two K-groups per read); 0: 8-byte reads,
+// one K-group each (the summation order differs between the two builds)
+#ifndef PNOL_SYRK_B128
+#define PNOL_SYRK_B128 1
+#endif
+
 __device__ __forceinline__ void tile_of(int t, int& ti, int& tj) {
     int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
     while ((r + 1) * (r + 2) / 2 <= t) ++r;
@@ -95,13 +101,19 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                                                       int split_k, int kfirst, int kchunk, int sub, int slice0,
                                                       int mS, long sstride, int umajor, double* __restrict__ part,
                                                       double* __restrict__ C, long ldc, double alpha,
-                                                      double beta, int tile0) {
+                                                      double beta, int tile0, unsigned* __restrict__ tail_flag,
+                                                      unsigned tail_val) {
     constexpr int NT = 64 * NW, WC = NW / 2;
     constexpr int WTM = TILE / 2, WTN = TILE / WC, NBM = WTM / 16, NBN = WTN / 16;
     __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
 #ifdef PNOL_SYRK_TIMELINE
     const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
 #endif
+    // the last-dispatched workgroup announces the launch's tail (jtr_tail): a system-scope
+    // vector store the command processor's wait on this word sees; speed only, nothing in the
+    // data path depends on it
+    if (tail_flag && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+        __hip_atomic_store(tail_flag, tail_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 
     // XMAP (split_k a multiple of 8): the K slices s = xcd, xcd + 8, ... go to the XCD that
     // dispatch slot blockIdx % 8 lands on, all tiles of one slice before the next, so the
@@ -175,6 +187,33 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
             load_stage<TILE, NT>(ps, X, ldx, nr, prow0, k0, kend, full);
             if (!diag) load_stage<TILE, NT>(qs, X, ldx, nr, qrow0, k0, kend, full);
         }
+#if PNOL_SYRK_B128
+        // one 16-byte fragment read per operand block covers two MFMA K-groups: lane l holds
+        // k = 8 kk + 2 (l >> 4) + {0, 1}; the first MFMA takes the even k of the 8-block, the
+        // second the odd ones (half the ds_read instructions; the 144-byte row stride keeps the
+        // 16 rows of a 16-lane group on distinct bank quads).  Every element's MFMA chain is
+        // the same in every mode and tile size, so all paths still sum it identically.
+#pragma unroll
+        for (int kk = 0; kk < kTK / 8; ++kk) {
+            double2 a[NBM], b[NBN];
+#pragma unroll
+            for (int mi = 0; mi < NBM; ++mi)
+                a[mi] = *reinterpret_cast<const double2*>(P + (wr * WTM + mi * 16 + frow) * kPad + kk * 8 + 2 * fk);
+#pragma unroll
+            for (int ni = 0; ni < NBN; ++ni)
+                b[ni] = *reinterpret_cast<const double2*>(Q + (wc * WTN + ni * 16 + frow) * kPad + kk * 8 + 2 * fk);
+#pragma unroll
+            for (int mi = 0; mi < NBM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < NBN; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].x, b[ni].x, acc[mi][ni], 0, 0, 0);
+#pragma unroll
+            for (int mi = 0; mi < NBM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < NBN; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].y, b[ni].y, acc[mi][ni], 0, 0, 0);
+        }
+#else
 #pragma unroll
         for (int kk = 0; kk < kTK / 4; ++kk) {
             double a[NBM], b[NBN];
@@ -188,6 +227,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                 for (int ni = 0; ni < NBN; ++ni)
                     acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
         }
+#endif
     }
 
     // f64 MFMA C/D layout: lane l, register r -> row (l >> 4) + 4 r, column l & 15
@@ -564,7 +604,7 @@ static bool syrk_xmap() {
 // part[((t - tile0) * nsl * sub + (s - slice0) * sub + u) * 128^2].
 static void syrk_partials(pnol_ctx* ctx, hipStream_t stream, bool rows_variant, const double* X, long ldx,
                           long sstride, int nr, int K, const SliceCfg& sc, int slice0, int nsl, int tile0, int ntl,
-                          double* part, bool t64 = false) {
+                          double* part, bool t64 = false, unsigned* tail_flag = nullptr, unsigned tail_val = 0) {
     const int split = nsl * sc.sub;
     const dim3 grid(ntl * split);
     LaunchTimer tm(ctx, rows_variant ? "syrk_rows" : "syrk");
@@ -572,41 +612,107 @@ static void syrk_partials(pnol_ctx* ctx, hipStream_t stream, bool rows_variant, 
         const int nt64 = (nr + 63) / 64;
         hipExtLaunchKernelGGL((k_syrk_tile<4, 64>), dim3(nt64 * (nt64 + 1) / 2 * split), dim3(256), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr,
                            K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part,
-                           (double*)nullptr, 0L, 1.0, 0.0, 0);
+                           (double*)nullptr, 0L, 1.0, 0.0, 0, tail_flag, tail_val);
     } else if (rows_variant)
         hipExtLaunchKernelGGL((k_syrk_tile<2, kTile, false, 8>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr, K, split,
-                           sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
+                           sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0, tail_flag, tail_val);
     else if (syrk_nw() == 8)
         hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, false, 8>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr, K, split,
-                           sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
+                           sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0, tail_flag, tail_val);
     else if (syrk_xmap() && split % kNumXcd == 0)
         hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, true>), grid, dim3(256), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr, K, split, sc.kfirst,
-                           sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
+                           sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0, tail_flag, tail_val);
     else
         hipExtLaunchKernelGGL((k_syrk_tile<0, kTile>), grid, dim3(256), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr, K, split, sc.kfirst,
-                           sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0);
+                           sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0, tail_flag, tail_val);
+}
+
+// -J^T F in the J^T J's tail (PNOL_JTR_TAIL=1; off by default: measured slower, below).  The GEMV reads only J^T and F, both
+// complete before the SYRK starts, so it need not wait for the SYRK to drain: the SYRK's
+// last-dispatched workgroup stores the launch's epoch into the context's tail word when it
+// starts, a second stream waits for that value (hipStreamWaitValue32: the command processor
+// polls, no CU is held) and runs the GEMV on the CUs the SYRK frees as its last round drains;
+// the context stream waits for the GEMV's event only before the -J^T F tree.  (A launch without
+// the AQL barrier bit -- hipExtAnyOrderLaunch -- does not start early on gfx950:
+// profiles/r02_anyorder_probe.json.)  The same kernels and bits as the plain order.  Measured
+// (tools/jtr_tail_ab.sh, same box, alternating 30-trip benches): 305-311 LM iters/s with the
+// GEMV in the tail vs 314-317 in stream order -- the GEMV's HBM stream slows the SYRK's last
+// workgroups more than it saves, so stream order stays the default.
+static bool jtr_tail_on(pnol_ctx* ctx) {
+    const char* e = std::getenv("PNOL_JTR_TAIL");   // read per call: tests switch it
+    if (!e || std::atoi(e) == 0) return false;
+    static int supported = -1;
+    if (supported < 0) {
+        int v = 0;
+        supported = hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, ctx->device) == hipSuccess && v;
+    }
+    return supported;
+}
+
+static int tail_prepare(pnol_ctx* ctx, unsigned** flag, unsigned* val) {
+    if (!ctx->aux_stream) PNOL_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
+    if (!ctx->tail_ev) PNOL_HIP(hipEventCreateWithFlags(&ctx->tail_ev, hipEventDisableTiming));
+    if (!ctx->tail_flag) {
+        // one 8-byte signal word; plain device memory where signal memory is refused
+        if (hipExtMallocWithFlags((void**)&ctx->tail_flag, 8, hipMallocSignalMemory) != hipSuccess) {
+            (void)hipGetLastError();
+            ctx->tail_flag = nullptr;
+            PNOL_HIP(hipMalloc((void**)&ctx->tail_flag, 64));
+        }
+        PNOL_HIP(hipMemset(ctx->tail_flag, 0, 8));
+        ctx->tail_epoch = 0;
+    }
+    *flag = ctx->tail_flag;
+    *val = ++ctx->tail_epoch;
+    return PNOL_OK;
+}
+
+static int jtr_gemv(pnol_ctx* ctx, const double* JT, int ldjt, long sstride, int m, int n, int mS, int s0, int nsl,
+                    const double* F, hipStream_t stream = nullptr);
+static int jtr_tree(pnol_ctx* ctx, int n, int s0, int nsl, double* out);
+
+// after the SYRK launch that carried (tf, tv): the GEMV on the aux stream gated by the tail word
+static int jtr_gemv_tail(pnol_ctx* ctx, unsigned* tf, unsigned tv, const double* JT, int ldjt, long sstride, int m,
+                         int n, int mS, int s0, int nsl, const double* F) {
+    PNOL_HIP(hipStreamWaitValue32(ctx->aux_stream, tf, tv, hipStreamWaitValueGte, 0xffffffffu));
+    PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sstride, m, n, mS, s0, nsl, F, ctx->aux_stream));
+    PNOL_HIP(hipEventRecord(ctx->tail_ev, ctx->aux_stream));
+    return PNOL_OK;
 }
 
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
-               double* jtj_diag) {
+               double* jtj_diag, const double* F, double* rhs) {
     if (!JT || !A || m <= 0 || n <= 0 || ldjt < m || lda < n) return PNOL_ERR_ARG;
     if (n <= PNOL_SEQ_MAX && m <= 4096) {
         dim3 blk(16, 16), grd((n + 15) / 16, (n + 15) / 16);
         hipLaunchKernelGGL(k_jtj_seq, grd, blk, 0, ctx->stream, JT, (long)ldjt, m, n, lambda, A, (long)lda, jtj_diag);
-        return launch_check();
+        PNOL_CHECK(launch_check());
+        return rhs ? launch_jtr(ctx, JT, ldjt, m, n, F, rhs) : PNOL_OK;
     }
     const int nt = (n + kTile - 1) / kTile;
     const int ntiles = nt * (nt + 1) / 2;
     const SliceCfg sc = slice_cfg(m, ntiles);
     void* part = nullptr;
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * kS * sc.sub * kTile * kTile, &part));
+    const bool tail = rhs && jtr_tail_on(ctx);
+    unsigned* tf = nullptr;
+    unsigned tv = 0;
+    if (tail) PNOL_CHECK(tail_prepare(ctx, &tf, &tv));
     syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
-                  syrk_t64(false));
+                  syrk_t64(false), tf, tv);
     PNOL_CHECK(launch_check());
-    ScopedTimer tm(ctx, "syrk_reduce");
-    launch_reduce(dim3(kTile / 32, ntiles), dim3(256), 0, ctx->stream, (const double*)part, ntiles,
-                       sc.sub, n, lambda, A, (long)lda, jtj_diag, 0);
-    return launch_check();
+    if (tail)
+        PNOL_CHECK(jtr_gemv_tail(ctx, tf, tv, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F));
+    else if (rhs)
+        PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F));
+    {
+        ScopedTimer tm(ctx, "syrk_reduce");
+        launch_reduce(dim3(kTile / 32, ntiles), dim3(256), 0, ctx->stream, (const double*)part, ntiles,
+                      sc.sub, n, lambda, A, (long)lda, jtj_diag, 0);
+        PNOL_CHECK(launch_check());
+    }
+    if (tail) PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->tail_ev, 0));
+    return rhs ? jtr_tree(ctx, n, 0, kS, rhs) : PNOL_OK;
 }
 
 int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldjt, int m, int n, double lambda,
@@ -635,13 +741,14 @@ int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldj
 // index (prefix sharing) while J^T J rows grow, so chunk boundaries are placed at equal FD cost.
 // JT and A are bitwise those of launch_fd_jacobian + launch_jtj.
 int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
-                  double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, int nchunks) {
+                  double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, int nchunks,
+                  double* rhs) {
     if (!o || !JT || !A) return PNOL_ERR_ARG;
     const int n = o->n, m = o->m;
     const int nt = (n + kTile - 1) / kTile;
     if (o->kind != PNOL_OBJ_LINRES || nchunks <= 1 || nt < 2 || (n <= PNOL_SEQ_MAX && m <= 4096)) {
         PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
-        return launch_jtj(ctx, JT, ldjt, m, n, lambda, A, lda, jtj_diag);   // times "syrk" itself
+        return launch_jtj(ctx, JT, ldjt, m, n, lambda, A, lda, jtj_diag, F0, rhs);   // times "syrk" itself
     }
     nchunks = std::min(nchunks, nt);
     if (!ctx->aux_stream) PNOL_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
@@ -682,7 +789,7 @@ int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h,
     }
     PNOL_HIP(hipEventRecord(ctx->aux_events[nchunks], ctx->aux_stream));
     PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->aux_events[nchunks], 0));
-    return PNOL_OK;
+    return rhs ? launch_jtr(ctx, JT, ldjt, m, n, F0, rhs) : PNOL_OK;
 }
 
 int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, double alpha, double* C, int ldc,
@@ -695,7 +802,7 @@ int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, do
     const int nt = (nr + kT - 1) / kT;
     const int ntiles = nt * (nt + 1) / 2;
     hipLaunchKernelGGL((k_syrk_tile<1, kT>), dim3(ntiles), dim3(256), 0, ctx->stream, X, (long)ldx, nr, K, 1, K, K, 1,
-                       0, K, (long)K, 0, (double*)nullptr, C, (long)ldc, alpha, 1.0, 0);
+                       0, K, (long)K, 0, (double*)nullptr, C, (long)ldc, alpha, 1.0, 0, (unsigned*)nullptr, 0u);
     return launch_check();
 }
 
@@ -747,14 +854,26 @@ static void dyadic_nodes(int a, int b, std::vector<std::pair<int, int>>& out) {
 // -J^T F on the m-slices [s0, s0 + nsl): jp[(s - s0) * n + j] = -sum_{k in slice s} JT_jk F_k
 // (JT slice s at JT + s * sstride, row stride ldjt), then the slice nodes of that range into
 // out[c * n + j] (one node = -J^T F itself when the range is all kLmSlices slices).
-static int jtr_slices(pnol_ctx* ctx, const double* JT, int ldjt, long sstride, int m, int n, int mS, int s0, int nsl,
-                      const double* F, double* out) {
+static int jtr_gemv(pnol_ctx* ctx, const double* JT, int ldjt, long sstride, int m, int n, int mS, int s0, int nsl,
+                    const double* F, hipStream_t stream) {
+    if (!F) return PNOL_ERR_ARG;
     void* jp = nullptr;
     PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
-    PNOL_CHECK(launch_gemv_neg_slices(ctx, JT, ldjt, sstride, n, m, mS, s0, nsl, F, (double*)jp));
+    return launch_gemv_neg_slices(ctx, JT, ldjt, sstride, n, m, mS, s0, nsl, F, (double*)jp, stream);
+}
+
+static int jtr_tree(pnol_ctx* ctx, int n, int s0, int nsl, double* out) {
+    void* jp = nullptr;
+    PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
     hipLaunchKernelGGL(k_tree_nodes, dim3((n + 255) / 256, 1), dim3(256), 0, ctx->stream, (const double*)jp, 0L,
                        (long)n, 1, s0, s0 + nsl, n, out, (long)n, 0L);
     return launch_check();
+}
+
+static int jtr_slices(pnol_ctx* ctx, const double* JT, int ldjt, long sstride, int m, int n, int mS, int s0, int nsl,
+                      const double* F, double* out) {
+    PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sstride, m, n, mS, s0, nsl, F));
+    return jtr_tree(ctx, n, s0, nsl, out);
 }
 
 int launch_jtr(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs) {
@@ -790,9 +909,20 @@ int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lamb
     void* part = nullptr;
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * std::max(nsl, 1) * sc.sub * E, &part));
     const bool t64 = syrk_t64(true);
-    if (nsl > 0)
-        syrk_partials(ctx, ctx->stream, false, JTs, sc.mS, sstr, n, m, sc, s0, nsl, 0, ntiles, (double*)part, t64);
-    PNOL_CHECK(launch_check());
+    // -J^T F's slice partials in the SYRK's tail (jtr_tail_on)
+    const bool tail = nsl > 0 && jtr_tail_on(ctx);
+    if (nsl > 0) {
+        unsigned* tf = nullptr;
+        unsigned tv = 0;
+        if (tail) PNOL_CHECK(tail_prepare(ctx, &tf, &tv));
+        syrk_partials(ctx, ctx->stream, false, JTs, sc.mS, sstr, n, m, sc, s0, nsl, 0, ntiles, (double*)part, t64,
+                      tf, tv);
+        PNOL_CHECK(launch_check());
+        if (tail)
+            PNOL_CHECK(jtr_gemv_tail(ctx, tf, tv, JTs, sc.mS, sstr, m, n, sc.mS, s0, nsl, F));
+        else
+            PNOL_CHECK(jtr_gemv(ctx, JTs, sc.mS, sstr, m, n, sc.mS, s0, nsl, F));
+    }
     if (P == 1) {
         {
             ScopedTimer tm(ctx, "syrk_reduce");
@@ -800,8 +930,8 @@ int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lamb
                                ntiles, sc.sub, n, lambda, A, (long)lda, jtj_diag, 0);
         }
         PNOL_CHECK(launch_check());
-        ScopedTimer tm(ctx, "jtr");
-        return jtr_slices(ctx, JTs, sc.mS, sstr, m, n, sc.mS, 0, kS, F, rhs);
+        if (tail) PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->tail_ev, 0));
+        return jtr_tree(ctx, n, 0, kS, rhs);
     }
     // the global node list: rank q's nodes in slice order, ranks in order
     std::vector<std::pair<int, int>> nodes;
@@ -837,10 +967,8 @@ int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lamb
     }
     PNOL_CHECK(launch_check());
     // -J^T F nodes of my slices into the tail of my allgather slot
-    if (nsl > 0) {
-        ScopedTimer tm(ctx, "jtr");
-        PNOL_CHECK(jtr_slices(ctx, JTs, sc.mS, sstr, m, n, sc.mS, s0, nsl, F, mine + (long)tpr * E));
-    }
+    if (tail) PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->tail_ev, 0));
+    if (nsl > 0) PNOL_CHECK(jtr_tree(ctx, n, s0, nsl, mine + (long)tpr * E));
     // reduce-scatter in tree order: rank q's nodes of owner d's tiles -> d
     {
         ScopedTimer tm(ctx, "exchange_A");

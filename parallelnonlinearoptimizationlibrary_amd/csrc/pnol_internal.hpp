@@ -64,6 +64,12 @@ struct pnol_ctx {
     int chol4_epoch = 0;            // last flag value handed out (monotonic; flags reset on regrow)
     hipStream_t aux_stream = nullptr;   // second stream (J^T J rows beside the FD chunks), lazily created
     std::vector<hipEvent_t> aux_events; // chunk-done events between the two streams
+    // J^T J tail word (syrk.hip, jtr_tail): the SYRK's last-dispatched workgroup stores
+    // tail_epoch into *tail_flag when it starts; the aux stream waits for that value
+    // (hipStreamWaitValue32) and then runs the -J^T F GEMV on the CUs the SYRK's tail frees
+    unsigned* tail_flag = nullptr;
+    unsigned tail_epoch = 0;
+    hipEvent_t tail_ev = nullptr;       // the GEMV done (aux stream), waited for by the main stream
 };
 
 struct pnol_dobj {
@@ -153,8 +159,9 @@ inline int launch_check() {
 int launch_gemv_neg(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y);
 int launch_gemv_neg_seq(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y);
 // y[(s - s0) * rows + j] = -sum_{k in m-slice s} A_s[j][k] x[s mS + k], s in [s0, s0 + nsl)
+// stream: nullptr = the context stream
 int launch_gemv_neg_slices(pnol_ctx* ctx, const double* A, int lda, long sstride, int rows, int m, int mS, int s0,
-                           int nsl, const double* x, double* y);
+                           int nsl, const double* x, double* y, hipStream_t stream = nullptr);
 int launch_bfgs_update_exact(pnol_ctx* ctx, double* D, int ldd, const double* y, const double* s, int n);
 int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p, const double* a_p,
                      const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
@@ -168,8 +175,9 @@ int launch_gather_sub(pnol_ctx* ctx, const double* D, int ldd, int n, const int*
 int launch_gather_rows(pnol_ctx* ctx, const double* D, int ldd, const int* ridx, int nrows, int rbase, const int* cidx,
                        int ncols, double* Dsub, int lds);
 
+// rhs (nullable): also rhs = -J^T F, its GEMV in the SYRK's tail (bitwise launch_jtr)
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
-               double* jtj_diag);
+               double* jtj_diag, const double* F = nullptr, double* rhs = nullptr);
 int launch_jtj_sharded(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                        double* jtj_diag);
 int launch_jtr(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
@@ -207,8 +215,10 @@ int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldj
                     double* A, int lda, double* jtj_diag, int row_begin, int row_end);
 // FD Jacobian of all columns + A = J^T J (+ Marquardt diagonal), pipelined: FD column chunks on
 // the context stream, the J^T J tile rows they complete on a second stream
+// rhs (nullable): also rhs = -J^T F0 (pnol_fd_normal_d)
 int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
-                  double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, int nchunks);
+                  double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, int nchunks,
+                  double* rhs = nullptr);
 int launch_fd_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int j0, int cnt,
                        double* F0, int compute_f0, double* JT, int ldjt);
 int launch_synthetic_quadratic(pnol_ctx* ctx, unsigned long long seed, int n, double bscale, double* d, double* b);

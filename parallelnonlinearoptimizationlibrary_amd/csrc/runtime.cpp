@@ -439,6 +439,8 @@ int pnol_ctx_destroy(pnol_ctx* ctx) {
         (void)hipStreamDestroy(ctx->aux_stream);
     }
     for (hipEvent_t e : ctx->aux_events) (void)hipEventDestroy(e);
+    if (ctx->tail_ev) (void)hipEventDestroy(ctx->tail_ev);
+    if (ctx->tail_flag) (void)hipFree(ctx->tail_flag);
     for (auto& kv : ctx->timers.pending)
         for (auto& ev : kv.second) {
             (void)hipEventDestroy(ev.first);

@@ -212,6 +212,14 @@ class DeviceObjective:
                 "pnol_fd_jtj_d")
         return (F0, JT, A, diag) if want_diag else (F0, JT, A)
 
+    def fd_normal(self, x, h, lam, JT, A, rhs, F0=None, compute_f0=True):
+        """FD Jacobian + A (Marquardt diagonal) + rhs = -J^T F0 in one queue (pnol_fd_normal_d)."""
+        F0 = self.ctx.empty(self.m) if F0 is None else F0
+        L.check(L.lib().pnol_fd_normal_d(self.ctx.h, self.h, _ptr(x), _ptr(h), _ptr(F0), int(compute_f0), _ptr(JT),
+                                         JT.stride(0), C.c_double(lam), _ptr(A), A.stride(0), None, _ptr(rhs)),
+                "pnol_fd_normal_d")
+        return F0, JT, A, rhs
+
     def lm_jacobian_mpi(self, x, h, JTs=None, F0=None, compute_f0=True):
         """This rank's FD tiles for all rows into the m-sliced J^T, then each slice to its rank."""
         if JTs is None:

@@ -632,6 +632,32 @@ def test_fd_jtj_pipelined_bitwise(ctx, m, n, chunks):
     assert np.array_equal(_np(db), _np(da))
 
 
+@pytest.mark.parametrize("m,n,tail", [(16384, 2048, "1"), (16384, 2048, "0"), (5000, 1000, "1"),
+                                      (777, 129, "1"), (300, 40, "1")])
+def test_fd_normal_bitwise(ctx, m, n, tail, monkeypatch):
+    """pnol_fd_normal_d (FD Jacobian + A + -J^T F in one queue, the -J^T F GEMV on a second stream
+    released by the J^T J's last-dispatched workgroup) equals pnol_fd_jacobian_d + pnol_jtj_d +
+    pnol_jtr_d bitwise, over repeated calls (the GEMV must never read a stale J^T: the second
+    call's JT is a new point's).  tail = "0": the same kernels in stream order."""
+    monkeypatch.setenv("PNOL_JTR_TAIL", tail)
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    d = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+    h = ctx.tensor(np.full(n, 1e-7))
+    JTb, Ab, rb = ctx.empty(n, m), ctx.empty(n, n), ctx.empty(n)
+    for rep, lo in enumerate((-0.5, -0.25)):
+        x = ctx.tensor(np.linspace(lo, 0.5, n))
+        F0a, JTa = d.fd_jacobian(x, h, 0, n)
+        Aa = ctx.jtj(JTa, 0.37)
+        ra = ctx.jtr(JTa, F0a)
+        F0b, JTb, Ab, rb = d.fd_normal(x, h, 0.37, JTb, Ab, rb)
+        ctx.synchronize()
+        assert np.array_equal(_np(JTb), _np(JTa)), rep
+        assert np.array_equal(_np(F0b), _np(F0a)), rep
+        assert np.array_equal(_np(Ab), _np(Aa)), rep
+        assert np.array_equal(_np(rb), _np(ra)), rep
+
+
 def test_synthetic_data_matches_oracle_stream(ctx, oracle):
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective

@@ -3,7 +3,9 @@
 // has finished?  Kernel A: G workgroups, 2 per CU (64 KB LDS each), each busy for D realtime
 // ticks (100 MHz) -- several dispatch rounds.  Kernel B: 256 small workgroups that stamp their
 // start.  Printed (microseconds, relative to A's first start): A's last workgroup start (its
-// last dispatch), A's last end, B's first start -- for B launched plainly and with the flag.
+// last dispatch), A's last end, B's first start -- for B launched plainly and with the flag,
+// and for B on a second stream gated by hipStreamWaitValue32 on a word that A's last
+// workgroup stores (system scope) when it starts ("wait_value").
 //   hipcc --offload-arch=gfx950 -O3 anyorder_probe.hip -o anyorder_probe
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
@@ -22,9 +24,11 @@
     } while (0)
 
 __global__ __launch_bounds__(256) void k_busy(unsigned long long* st, unsigned long long* en, long ticks,
-                                             double* sink) {
+                                             double* sink, unsigned* flag, unsigned epoch) {
     __shared__ double pad[8192];   // 64 KB: two workgroups per CU
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    if (flag && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+        __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     pad[threadIdx.x] = (double)threadIdx.x;
     __syncthreads();
     double a = pad[(threadIdx.x + 1) & 255];
@@ -50,17 +54,37 @@ int main() {
     CK(hipMalloc(&en, G * 8));
     CK(hipMalloc(&bst, GB * 8));
     CK(hipMalloc(&sink, 8));
-    hipStream_t s;
+    hipStream_t s, s2;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    unsigned* flag = nullptr;
+    // signal memory is one 8-byte word; plain device memory as a fallback
+    bool sig = hipExtMallocWithFlags((void**)&flag, 8, hipMallocSignalMemory) == hipSuccess;
+    if (!sig) {
+        (void)hipGetLastError();
+        CK(hipMalloc((void**)&flag, 64));
+    }
+    CK(hipMemset(flag, 0, 8));
+    std::fprintf(stderr, "flag memory: %s\n", sig ? "signal" : "device");
+    unsigned epoch = 0;
     std::vector<unsigned long long> hs(G), he(G), hb(GB);
     std::printf("{");
-    for (int flag = 0; flag < 2; ++flag) {
+    const char* names[3] = {"plain", "any_order", "wait_value"};
+    for (int mode = 0; mode < 3; ++mode) {
         for (int rep = 0; rep < 4; ++rep) {
-            hipExtLaunchKernelGGL(k_busy, dim3(G), dim3(256), 0, s, nullptr, nullptr, 0, st, en, ticks, sink);
-            hipExtLaunchKernelGGL(k_stamp, dim3(GB), dim3(256), 0, s, nullptr, nullptr, flag ? hipExtAnyOrderLaunch : 0,
-                                  bst);
+            ++epoch;
+            hipExtLaunchKernelGGL(k_busy, dim3(G), dim3(256), 0, s, nullptr, nullptr, 0, st, en, ticks, sink,
+                                  mode == 2 ? flag : (unsigned*)nullptr, epoch);
+            if (mode == 2) {
+                CK(hipStreamWaitValue32(s2, flag, epoch, hipStreamWaitValueGte, 0xffffffffu));
+                hipLaunchKernelGGL(k_stamp, dim3(GB), dim3(256), 0, s2, bst);
+            } else {
+                hipExtLaunchKernelGGL(k_stamp, dim3(GB), dim3(256), 0, s, nullptr, nullptr,
+                                      mode ? hipExtAnyOrderLaunch : 0, bst);
+            }
             CK(hipGetLastError());
             CK(hipStreamSynchronize(s));
+            CK(hipStreamSynchronize(s2));
         }
         CK(hipMemcpy(hs.data(), st, G * 8, hipMemcpyDeviceToHost));
         CK(hipMemcpy(he.data(), en, G * 8, hipMemcpyDeviceToHost));
@@ -70,7 +94,7 @@ int main() {
         const unsigned long long aend = *std::max_element(he.begin(), he.end());
         const unsigned long long b0 = *std::min_element(hb.begin(), hb.end());
         std::printf("%s\"%s\": {\"a_last_start_us\": %.2f, \"a_end_us\": %.2f, \"b_first_start_us\": %.2f}",
-                    flag ? ", " : "", flag ? "any_order" : "plain", (alast - a0) / 100.0, (aend - a0) / 100.0,
+                    mode ? ", " : "", names[mode], (alast - a0) / 100.0, (aend - a0) / 100.0,
                     ((double)b0 - (double)a0) / 100.0);
     }
     std::printf("}\n");
