@@ -37,6 +37,7 @@ constexpr int kPad = 18;   // LDS row stride in doubles
 #define PNOL_SYRK_B128 1
 #endif
 
+
 __device__ __forceinline__ void tile_of(int t, int& ti, int& tj) {
     int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
     while ((r + 1) * (r + 2) / 2 <= t) ++r;
