@@ -1,0 +1,14 @@
+#!/bin/bash
+# Same-box A/B of env settings on short LM benches: alternating runs of each setting, LM iters/s,
+# ms per trip and the warmup breakdown of one kernel timer.
+#   VAR=PNOL_EVAL_RPW VALS="64 32 16" KEY=linres_eval tools/env_ab.sh
+set -u
+mkdir -p gpurun_out
+for rep in 1 2 3; do
+  for v in $VALS; do
+    env $VAR=$v timeout -k 10 180 python bench.py --no-cpu-baseline --no-hg --no-bfgs --steps 30 --warmup 3 \
+        > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err
+    rc=$?; [ "$rc" -eq 0 ] || { echo "bench rc=$rc"; tail -5 gpurun_out/ab_$v.err; exit $rc; }
+    python3 -c "import json; d=json.loads(open('gpurun_out/ab_$v.json').readline()); print('$VAR=$v', round(d['value'],2), round(d['ms_per_step'],4), '${KEY:-linres_eval}', round(d['kernel_ms_per_call_warmup_breakdown'].get('${KEY:-linres_eval}',0),4))"
+  done
+done
