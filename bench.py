@@ -360,13 +360,27 @@ def main():
     dctx = C.c_void_p()
     L.check(L.lib().pnol_default_ctx(C.byref(dctx)), "pnol_default_ctx")
     host_comm = None
+    comm_backend = "none"
     if world > 1 and args.host_comm:
         from parallelnonlinearoptimizationlibrary_amd.dist import HostComm
         host_comm = HostComm(rank, world)
+        comm_backend = "host-gloo"
     elif world > 1:
         class _Ctx:  # RCCL communicator on the solver's context
             h = dctx
         init_rccl(_Ctx, rank, world)
+        comm_backend = "rccl"
+        # the RCCL transport first runs here: a small LevMarqMPI must reproduce the one-process
+        # LevMarq bit for bit, or the measurement falls back to the host communicator over a
+        # gloo group (labelled as such in "comm")
+        from parallelnonlinearoptimizationlibrary_amd.dist import HostComm, rccl_selfcheck
+        ok, why = rccl_selfcheck(ctx, world)
+        if rank == 0:
+            print(f"[bench] RCCL self-check: {why}", file=sys.stderr, flush=True)
+        if not ok:
+            L.lib().pnol_comm_finalize()
+            host_comm = HostComm(rank, world, group=dist.new_group(backend="gloo"))
+            comm_backend = f"host-gloo (RCCL self-check failed: {why[:160]})"
 
     obj = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)   # A, y generated in HBM
     x0 = np.zeros(n)
@@ -509,7 +523,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (splitmix64 seed 0x5EED2018, r(x)=Ax-y generated in HBM)",
             "config": {"workload": f"LevenbergMarquardt{'MPI' if world > 1 else ''} m={m} n={n}, "
-                                   f"FD columns {'in cost-balanced tiles over ' + str(world) + ' GPUs, J rows exchanged by m-slice (' + ('host communicator over gloo: one-GPU rehearsal' if args.host_comm else 'RCCL p2p') + '), J^T J + J^T F by m-slice + reduce-scatter/allgather' if world > 1 else 'on 1 GPU'}",
+                                   f"FD columns {'in cost-balanced tiles over ' + str(world) + ' GPUs, J rows exchanged by m-slice (' + ('host communicator over gloo: one-GPU rehearsal' if args.host_comm else ('RCCL p2p' if comm_backend == 'rccl' else comm_backend)) + '), J^T J + J^T F by m-slice + reduce-scatter/allgather' if world > 1 else 'on 1 GPU'}",
                        "m": m, "n": n, "parallelism": f"fd-columns+m-slices x{world}" if world > 1 else "single"},
             "roofline": roofline,
             "rooflines": rooflines,
@@ -524,7 +538,7 @@ def main():
             "bfgs_hg": hg, "bfgs_hg_n4096": hg4096 if hg else None, "bfgs_hg_n16384": hg16384 if hg else None,
             "bfgs_hg_row_sharded": hg_sharded,
             "bfgs_cfg2_solve": bfgs2, "bfgs_bnd_cfg5_solve": bnd5,
-            "comm": {"backend": ("host-gloo" if args.host_comm else "rccl") if world > 1 else "none", "ranks": world},
+            "comm": {"backend": comm_backend, "ranks": world},
             "cpu_baseline": cpu,
         }
         sys.stdout.flush()

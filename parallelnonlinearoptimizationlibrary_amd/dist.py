@@ -39,10 +39,37 @@ def init_rccl(ctx, rank: int, world: int):
     return n.value
 
 
-class HostComm:
-    """Host-backend communicator: allgather of raw bytes through torch.distributed (gloo)."""
+def rccl_selfcheck(ctx, world: int):
+    """Before an N > 1 measurement: one small LevMarqMPI run through the library's RCCL
+    communicator (m-slice exchange, tree-order reduce-scatter, allgather) must give bitwise the
+    single-process LevMarq's X on every rank.  Returns (ok, reason), agreed by all ranks."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from .device import DeviceObjective, run_levmarq
+    ok, why = True, "ok"
+    try:
+        m, n = 1500, 300
+        obj = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+        params = (0.001, 10.0, 1e-7, 6, 0.0, -1)
+        x_mpi, *_ = run_levmarq(obj, np.zeros(n), params, which=1)
+        x_one, *_ = run_levmarq(obj, np.zeros(n), params, which=0)
+        if not np.array_equal(x_mpi, x_one):
+            ok, why = False, f"LevMarqMPI X differs from LevMarq (max |dx| {np.abs(x_mpi - x_one).max():.3e})"
+    except Exception as e:  # noqa: BLE001 -- any failure of the RCCL path means: do not measure on it
+        ok, why = False, f"{type(e).__name__}: {e}"
+    flag = torch.tensor([0.0 if ok else 1.0], device="cuda")
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    if flag.item() != 0.0 and ok:
+        ok, why = False, "the self-check failed on another rank"
+    return ok, why
 
-    def __init__(self, rank: int, world: int):
+
+class HostComm:
+    """Host-backend communicator: allgather of raw bytes through torch.distributed (gloo);
+    `group`: a gloo process group when the default group is NCCL."""
+
+    def __init__(self, rank: int, world: int, group=None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.world = torch, dist, world
@@ -52,7 +79,7 @@ class HostComm:
                 src = (C.c_uint8 * nbytes).from_address(send)
                 t = torch.frombuffer(bytearray(src), dtype=torch.uint8)
                 outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
-                dist.all_gather(outs, t)
+                dist.all_gather(outs, t, group=group)
                 C.memmove(recv, bytes(torch.cat(outs).numpy()), nbytes * world)
                 return 0
             except Exception:  # pragma: no cover - surfaces as PNOL_ERR_COMM
