@@ -195,3 +195,16 @@ def test_bench_multi_rank_line_is_valid(tmp_path, world):
     assert line["comm"] == {"backend": "host-gloo", "ranks": world} and line["n_gpus"] == world
     assert line["fd_jacobian_ms_max_over_ranks"] > 0
     assert "host communicator" in line["config"]["workload"]
+
+
+def test_rccl_selfcheck_world1():
+    """The bench's N > 1 guard (dist.rccl_selfcheck): the library's RCCL communicator (one rank on
+    the box's one GPU -- RCCL refuses two ranks on one device) carries a small LevMarqMPI whose X
+    must equal the one-process LevMarq bit for bit; the probe exits 0 only when it does."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", f"--master-port={port}", os.path.join(os.path.dirname(HERE), "tools", "rccl_selfcheck_probe.py")]
+    r = subprocess.run(cmd, capture_output=True, timeout=240)
+    out = r.stdout.decode(errors="replace") + r.stderr.decode(errors="replace")
+    assert r.returncode == 0, out[-3000:]
+    assert "RCCL self-check ok=True" in out
