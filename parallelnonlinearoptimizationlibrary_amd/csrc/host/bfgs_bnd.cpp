@@ -172,14 +172,19 @@ void BFGS_Bnd::boundaryAssessment(double& F, vector<double>& X, vector<double>& 
     std::vector<int> frozen;
     bool bndFlag = false;
     int icur = 0;
-    for (int i = 0; i < Ndim; ++i) {
-        if (cI[i]) continue;
-        if ((std::fabs(X[icur] - Xlb[icur]) < bndTol) && ((p[icur] < 0) || (dFdX[icur] > 0))) {
-            bndFlag = true; cI[i] = true; cX[i] = X[icur]; cIcur[icur] = true; frozen.push_back(i);
-        } else if ((std::fabs(X[icur] - Xub[icur]) < bndTol) && ((p[icur] > 0) || (dFdX[icur] < 0))) {
-            bndFlag = true; cI[i] = true; cX[i] = X[icur]; cIcur[icur] = true; frozen.push_back(i);
+    // the same tests, evaluated without short-circuit branches (the frozen pattern is
+    // unpredictable); only a coordinate that hits a bound takes a branch
+    const int klast = ncur > 0 ? ncur - 1 : 0;
+    for (int i = 0; i < Ndim && ncur > 0; ++i) {
+        const bool c = cI[i];
+        const int k = icur < klast ? icur : klast;
+        const double xk = X[k], pk = p[k], gk = dFdX[k];
+        const bool lo = (std::fabs(xk - Xlb[k]) < bndTol) & ((pk < 0) | (gk > 0));
+        const bool hi = (std::fabs(xk - Xub[k]) < bndTol) & ((pk > 0) | (gk < 0));
+        if (!c & (lo | hi)) {
+            bndFlag = true; cI[i] = true; cX[i] = xk; cIcur[icur] = true; frozen.push_back(i);
         }
-        icur++;
+        icur += !c;
     }
     int Nconst = 0;
     for (int i = 0; i < Ndim; ++i) Nconst += cI[i];
@@ -190,12 +195,16 @@ void BFGS_Bnd::boundaryAssessment(double& F, vector<double>& X, vector<double>& 
     const int nr = Ndim - Nconst;
     if (bndFlag && nr > 0) {
         double FR = F;
-        std::vector<double> XR, gR, lbR, ubR, dXR;
-        for (icur = 0; icur < ncur; ++icur)
-            if (!cIcur[icur]) {
-                XR.push_back(X[icur]); gR.push_back(dFdX[icur]); lbR.push_back(Xlb[icur]);
-                ubR.push_back(Xub[icur]); dXR.push_back(dX[icur]);
-            }
+        std::vector<double> XR(nr), gR(nr), lbR(nr), ubR(nr), dXR(nr);
+        {
+            int ir = 0;
+            for (icur = 0; icur < ncur; ++icur)
+                if (!cIcur[icur]) {
+                    XR[ir] = X[icur]; gR[ir] = dFdX[icur]; lbR[ir] = Xlb[icur];
+                    ubR[ir] = Xub[icur]; dXR[ir] = dX[icur];
+                    ++ir;
+                }
+        }
         // the outer D is discarded while the reduced problem runs (reset below), so the
         // reduced D takes over its device buffer: one n x n matrix for the whole recursion
         DenseInverseHessian DR(D, nr, updateMode);
@@ -282,7 +291,11 @@ void BFGS_Bnd::mainBFGSLoop(double& F, vector<double>& X, vector<double>& dFdX, 
         for (int i = 0; i < n; ++i) { Xprev[i] = X[i]; X[i] = X[i] + alpha * p[i]; }
         F = Fopt;
         {
-            std::vector<double> gprev = dFdX, s(n), y(n);
+            // per-iteration scratch (not live across the recursion below, so one set per thread)
+            thread_local std::vector<double> gprev, s, y;
+            gprev.assign(dFdX.begin(), dFdX.end());
+            s.resize(n);
+            y.resize(n);
             {
                 PhaseClock t(prof_slot(profile, kProfGrad));
                 objPtr->gradientApproximationRecur(X, dX, dFdX, cX, cI);
@@ -291,15 +304,21 @@ void BFGS_Bnd::mainBFGSLoop(double& F, vector<double>& X, vector<double>& dFdX, 
             for (int i = 0; i < n; ++i) { s[i] = alpha * p[i]; y[i] = dFdX[i] - gprev[i]; }
             PhaseClock t(prof_slot(profile, kProfUpdate));
             D.update(y, s, &dFdX, &pnext);
-        }   // s, y, gprev freed before a possible recursion (one level per frozen coordinate)
+        }
         assessRecursed = false;
         boundaryAssessment(F, X, p, dFdX, D, Xlb, Xub, dX, cX, cI, optimFlag, recurFlag);
         // a recursion reset D to I and recomputed the gradient: the fused direction is stale
         have_next = !assessRecursed;
         if (!have_next) std::vector<double>().swap(pnext);
+        // the step's sum |X - Xprev| and the gradient's sum of squares: two independent
+        // sequential chains (each in the reference's order), one loop
         xdiff = 0;
-        for (int i = 0; i < n; ++i) xdiff += std::fabs(X[i] - Xprev[i]);
-        gnorm = std::sqrt(seq_dot(dFdX, dFdX));
+        double gg = 0.0;
+        for (int i = 0; i < n; ++i) {
+            xdiff += std::fabs(X[i] - Xprev[i]);
+            gg = gg + dFdX[i] * dFdX[i];
+        }
+        gnorm = std::sqrt(gg);
         if (fTrace) fTrace->push_back(F);
         if (verbose > 1 && comm_rank() == ROOT_ID) {
             std::cout << "  Step completed with F = " << F << " and mean abs xdiff is " << xdiff

@@ -220,6 +220,19 @@ void DenseInverseHessian::getMatrix(std::vector<std::vector<double>>& D) {
 
 void DenseInverseHessian::direction(const std::vector<double>& g, std::vector<double>& p) {
     p.resize(n_);
+    if (ident_ && !pending_ && identFinite(nullptr, nullptr)) {
+        // a stored diagonal, nothing pending: p_i = -(0.0 + d_i g_i) in one pass (a non-finite
+        // g_i sends the whole direction to the device path below, which rewrites p)
+        const double* gp = g.data();
+        const double* scp = hscale_.empty() ? nullptr : hscale_.data();
+        double* pp = p.data();
+        bool fin = true;
+        for (int i = 0; i < n_; ++i) {
+            fin = fin && std::isfinite(gp[i]);
+            pp[i] = -(0.0 + (scp ? scp[i] : 1.0) * gp[i]);
+        }
+        if (fin) return;
+    }
     if (ident_ && identFinite(&g, nullptr)) {
         // D g for a stored diagonal: the one nonzero term of each row sum, 0.0 + d_i g_i (the
         // device sums start from +0, so an exact zero product comes out +0)
@@ -229,7 +242,8 @@ void DenseInverseHessian::direction(const std::vector<double>& g, std::vector<do
             for (int i = 0; i < n_; ++i) p[i] = -v[i];
             return;
         }
-        const double ag = seq_dot(ha_, g), sg = seq_dot(hs_, g);
+        double ag, sg;
+        seq_dot2(ha_, g, hs_, g, ag, sg);
         for (int i = 0; i < n_; ++i) p[i] = -(v[i] + hs_[i] * ag + hb_[i] * sg);
         return;
     }
@@ -247,7 +261,8 @@ void DenseInverseHessian::direction(const std::vector<double>& g, std::vector<do
           "bfgs_pass(direction)");
     std::vector<double> v(n_);
     down(kV, v.data(), (size_t)n_);
-    const double ag = seq_dot(ha_, g), sg = seq_dot(hs_, g);
+    double ag, sg;
+    seq_dot2(ha_, g, hs_, g, ag, sg);
     for (int i = 0; i < n_; ++i) p[i] = -(v[i] + hs_[i] * ag + hb_[i] * sg);
 }
 
@@ -264,6 +279,7 @@ void DenseInverseHessian::update(const std::vector<double>& y, const std::vector
         if (gnext && pnext) direction(*gnext, *pnext);
         return;
     }
+    if (ident_ && !pending_ && updateIdentFused(y, s, gnext, pnext)) return;
     std::vector<double> u(n_), w(n_), v;
     if (gnext) v.resize(n_);
     if (ident_ && !pending_ && identFinite(&y, gnext)) {
@@ -290,8 +306,9 @@ void DenseInverseHessian::update(const std::vector<double>& y, const std::vector
         std::copy(uwv.begin() + n_, uwv.begin() + 2 * n_, w.begin());
         if (gnext) std::copy(uwv.begin() + 2 * n_, uwv.end(), v.begin());
     }
-    const double rho = 1 / seq_dot(y, s);
-    const double beta = seq_dot(y, u);
+    double ys, beta;
+    seq_dot2(y, s, y, u, ys, beta);
+    const double rho = 1 / ys;
     const double c = rho * rho * beta + rho;
     hs_ = s;
     ha_.resize(n_);
@@ -301,10 +318,72 @@ void DenseInverseHessian::update(const std::vector<double>& y, const std::vector
     pending_ = true;
     pend_dev_ = false;
     if (gnext && pnext) {
-        const double ag = seq_dot(ha_, *gnext), sg = seq_dot(hs_, *gnext);
+        double ag, sg;
+        seq_dot2(ha_, *gnext, hs_, *gnext, ag, sg);
         pnext->resize(n_);
         for (int i = 0; i < n_; ++i) (*pnext)[i] = -(v[i] + hs_[i] * ag + hb_[i] * sg);
     }
+}
+
+// update() from a stored diagonal with no pending correction, in three passes over the
+// vectors instead of one per quantity: (1) u = w = D y and v = D g_next (0.0 + d_i y_i, as the
+// device sums give them) with the chains y.s and y.u; (2) the new pending correction
+// (s, a = c s - rho w, b = -rho u) with the chains a.g and s.g; (3) p_next.  Every chain adds
+// in index order from 0.0 exactly as seq_dot, so the bits are update()'s general path's.
+// false (nothing changed) on a non-finite operand: the device path handles those.
+bool DenseInverseHessian::updateIdentFused(const std::vector<double>& y, const std::vector<double>& s,
+                                           const std::vector<double>* gnext, std::vector<double>* pnext) {
+    const int n = n_;
+    for (double x : hscale_)
+        if (!std::isfinite(x)) return false;
+    thread_local std::vector<double> ub, vb;
+    if ((int)ub.size() < n) ub.resize(n);
+    if (gnext && (int)vb.size() < n) vb.resize(n);
+    double* u = ub.data();
+    double* v = vb.data();
+    const double* yp = y.data();
+    const double* sp = s.data();
+    const double* gp = gnext ? gnext->data() : nullptr;
+    const double* scp = hscale_.empty() ? nullptr : hscale_.data();
+    bool fin = true;
+    double ys = 0.0, beta = 0.0;
+    for (int i = 0; i < n; ++i) {
+        const double di = scp ? scp[i] : 1.0, yi = yp[i];
+        const double ui = 0.0 + di * yi;
+        u[i] = ui;
+        fin = fin && std::isfinite(yi);
+        if (gp) {
+            v[i] = 0.0 + di * gp[i];
+            fin = fin && std::isfinite(gp[i]);
+        }
+        ys = ys + yi * sp[i];
+        beta = beta + yi * ui;
+    }
+    if (!fin) return false;
+    const double rho = 1 / ys;
+    const double c = rho * rho * beta + rho;
+    hs_.resize(n);
+    ha_.resize(n);
+    hb_.resize(n);
+    double ag = 0.0, sg = 0.0;
+    for (int i = 0; i < n; ++i) {
+        const double si = sp[i], ai = c * si - rho * u[i];   // w = u for a diagonal D
+        hs_[i] = si;
+        ha_[i] = ai;
+        hb_[i] = -rho * u[i];
+        if (gp) {
+            ag = ag + ai * gp[i];
+            sg = sg + si * gp[i];
+        }
+    }
+    pending_ = true;
+    pend_dev_ = false;
+    if (gnext && pnext) {
+        pnext->resize(n);
+        double* pn = pnext->data();
+        for (int i = 0; i < n; ++i) pn[i] = -(v[i] + hs_[i] * ag + hb_[i] * sg);
+    }
+    return true;
 }
 
 void DenseInverseHessian::setInverseOf(const std::vector<std::vector<double>>& B) {

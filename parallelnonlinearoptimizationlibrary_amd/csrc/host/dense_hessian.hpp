@@ -68,6 +68,8 @@ class DenseInverseHessian {
     void ensureDevice();  // the stored D really in device memory (writes a lazy identity)
     const double* deviceScale();
     bool identFinite(const std::vector<double>* a, const std::vector<double>* b) const;
+    bool updateIdentFused(const std::vector<double>& y, const std::vector<double>& s,
+                          const std::vector<double>* gnext, std::vector<double>* pnext);
     double sc(int i) const { return hscale_.empty() ? 1.0 : hscale_[i]; }
     int pass(const double* sp, const double* ap, const double* bp, int wb, const double* y, const double* g, double* u,
              double* w, double* v);

@@ -102,5 +102,19 @@ inline double seq_dot(const double* a, const double* b, size_t n) {
 inline double seq_dot(const std::vector<double>& a, const std::vector<double>& b) {
     return seq_dot(a.data(), b.data(), a.size());
 }
+// two independent sequential dot products in one loop: each chain is exactly seq_dot's, the two
+// dependent add chains just overlap (a host core's add latency, not its throughput, bounds one)
+inline void seq_dot2(const std::vector<double>& a1, const std::vector<double>& b1, const std::vector<double>& a2,
+                     const std::vector<double>& b2, double& s1, double& s2) {
+    const size_t n = a1.size();
+    const double *p1 = a1.data(), *q1 = b1.data(), *p2 = a2.data(), *q2 = b2.data();
+    double x = 0.0, y = 0.0;
+    for (size_t i = 0; i < n; ++i) {
+        x = x + p1[i] * q1[i];
+        y = y + p2[i] * q2[i];
+    }
+    s1 = x;
+    s2 = y;
+}
 
 }  // namespace pnol

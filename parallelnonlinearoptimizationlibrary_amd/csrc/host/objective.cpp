@@ -205,28 +205,35 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
         // perturbed point equals the reference's scatter(X + dX_i e_i) bit for bit.  One pass
         // builds both (frozen coordinates: their constant and a dummy step 1.0), in buffers kept
         // across calls (the bounded solvers call this twice per iteration at full length).
+        // Branch-free: which coordinates are frozen follows the active set, which looks random
+        // to a branch predictor (a mispredicted branch per few coordinates was ~30 us per pass
+        // at n = 16384); the reduced index advances by !frozen (X, dX read one past their end
+        // at most through the clamp, never used).
         const size_t nf = constantX.size();
-        thread_local std::vector<double> Xf, hf, gf;
+        thread_local std::vector<double> Xf, hf, gf, gr;
         Xf.resize(nf);
         hf.resize(nf);
         gf.resize(nf);
+        gr.resize(nf + 1);
+        const size_t last = N > 0 ? (size_t)N - 1 : 0;
         size_t ir = 0;
         for (size_t i = 0; i < nf; ++i) {
-            if (constantIndicator[i]) {
-                Xf[i] = constantX[i];
-                hf[i] = 1.0;
-            } else {
-                Xf[i] = X[ir];
-                hf[i] = dX[ir];
-                ++ir;
-            }
+            const bool c = constantIndicator[i];
+            const size_t k = ir < last ? ir : last;
+            const double xr = N > 0 ? X[k] : 0.0, hr = N > 0 ? dX[k] : 1.0;
+            Xf[i] = c ? constantX[i] : xr;
+            hf[i] = c ? 1.0 : hr;
+            ir += !c;
         }
         double F = 0;
         device_gradient(d, Xf, hf, 0, (int)nf, &F, gf.data());
         countEvals(N + 1);
         ir = 0;
-        for (size_t i = 0; i < nf; ++i)
-            if (!constantIndicator[i]) dFdX[ir++] = gf[i];
+        for (size_t i = 0; i < nf; ++i) {
+            gr[ir] = gf[i];
+            ir += !constantIndicator[i];
+        }
+        std::copy(gr.begin(), gr.begin() + N, dFdX.begin());
         return;
     }
     std::vector<double> v(N + 1);
