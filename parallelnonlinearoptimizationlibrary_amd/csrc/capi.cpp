@@ -403,22 +403,35 @@ int pnol_fd_gradient(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const doubl
                      double* g) {
     PNOL_CHECK(set_device(ctx));
     if (!obj || !x || !h || !f0 || (cnt > 0 && !g) || cnt < 0 || i0 < 0 || i0 + cnt > obj->n) return PNOL_ERR_ARG;
+    // device block [x | h | g | f0] and its pinned image: x (and h, when it changed) go up in ONE
+    // copy, g and f0 come down in one
     const size_t n = (size_t)obj->n, io = 2 * n + (size_t)cnt + 1;
-    void *dv = nullptr, *dhv = nullptr;
+    void* dv = nullptr;
     PNOL_CHECK(ws_get(ctx, "fdg_io", sizeof(double) * io, &dv));
-    PNOL_CHECK(ws_get(ctx, "fdg_h", sizeof(double) * n, &dhv));
     double* dx = (double*)dv;
-    double *dg = dx + 2 * n, *df = dg + cnt, *dh = (double*)dhv;
+    double *dh = dx + n, *dg = dx + 2 * n, *df = dg + cnt;
     double* st = (double*)pinned_stage(ctx, sizeof(double) * io);
     if (!st) return PNOL_ERR_NOMEM;
     std::memcpy(st, x, sizeof(double) * n);
-    PNOL_HIP(hipMemcpyAsync(dx, st, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
-    // the step vector rarely changes between calls (a solver's dX): re-upload it only when its
-    // content differs from the copy on the device (the workspace buffer is the one it went to)
-    if (ctx->fdg_h_dev != dh || ctx->fdg_h_host.size() != n ||
-        std::memcmp(ctx->fdg_h_host.data(), h, sizeof(double) * n) != 0) {
-        std::memcpy(st + n, h, sizeof(double) * n);
-        PNOL_HIP(hipMemcpyAsync(dh, st + n, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
+    // the step vector rarely changes between calls (a solver's dX): it is staged and sent only
+    // when its content differs from the copy on the device (compared while it is staged)
+    bool same = ctx->fdg_h_dev == dh && ctx->fdg_h_host.size() == n;
+    {
+        double* sh = st + n;
+        const double* prev = ctx->fdg_h_host.data();
+        if (same) {
+            bool diff = false;
+            for (size_t i = 0; i < n; ++i) {
+                sh[i] = h[i];
+                diff |= std::memcmp(&h[i], &prev[i], sizeof(double)) != 0;
+            }
+            same = !diff;
+        } else {
+            std::memcpy(sh, h, sizeof(double) * n);
+        }
+    }
+    PNOL_HIP(hipMemcpyAsync(dx, st, sizeof(double) * (same ? n : 2 * n), hipMemcpyHostToDevice, ctx->stream));
+    if (!same) {
         ctx->fdg_h_host.assign(h, h + n);
         ctx->fdg_h_dev = dh;
     }
