@@ -175,8 +175,11 @@ void BFGS_Bnd::boundaryAssessment(double& F, vector<double>& X, vector<double>& 
     // the same tests, evaluated without short-circuit branches (the frozen pattern is
     // unpredictable); only a coordinate that hits a bound takes a branch
     const int klast = ncur > 0 ? ncur - 1 : 0;
-    for (int i = 0; i < Ndim && ncur > 0; ++i) {
+    int Nconst = 0;   // coordinates frozen before this assessment (the loop reads every cI[i])
+    for (int i = 0; i < Ndim; ++i) {
         const bool c = cI[i];
+        Nconst += c;
+        if (ncur == 0) continue;
         const int k = icur < klast ? icur : klast;
         const double xk = X[k], pk = p[k], gk = dFdX[k];
         const bool lo = (std::fabs(xk - Xlb[k]) < bndTol) & ((pk < 0) | (gk > 0));
@@ -186,8 +189,7 @@ void BFGS_Bnd::boundaryAssessment(double& F, vector<double>& X, vector<double>& 
         }
         icur += !c;
     }
-    int Nconst = 0;
-    for (int i = 0; i < Ndim; ++i) Nconst += cI[i];
+    Nconst += (int)frozen.size();   // == the count of cI after the freezes
     if (bndFlag && verbose && comm_rank() == ROOT_ID) {
         std::cout << std::endl << "Optimizer reached box boundary; steepest descent points outside the box at "
                   << frozen.size() << " coordinate(s); recursing on the remaining ones." << std::endl;
