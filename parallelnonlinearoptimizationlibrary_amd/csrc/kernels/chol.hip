@@ -73,6 +73,12 @@ __device__ __forceinline__ double2 ld16_sc1(const double* base, unsigned off) {
     return __builtin_bit_cast(double2, v);
 }
 
+// 16-byte sc1 store at byte offset `off` from a wave-uniform base (buffer_store_dwordx4 ... sc1)
+__device__ __forceinline__ void st16_sc1(double* base, unsigned off, double2 v) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), r, off, 0, 16);
+}
+
 // Stage the 64 x 64 tile at (r0, c0) of P into four 64 x 16 substages (row stride kPad):
 // thread t owns row t >> 2 and the 16 columns of substage t & 3 (eight 16-byte loads; SC1:
 // sixteen 8-byte sc1 loads).
@@ -1284,6 +1290,12 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
 // wait, then lane 0's sc1 flag store; the consumer's lane 0 polls with sc1 loads, the block
 // barrier follows, and every load of x_c is an sc1 load.  No release / acquire fence (each
 // costs ~1.7 us) sits on the 32-step chain.
+// GRAN (the default): x_w goes out as 16-byte granules (x_w[t], epoch) -- one sc1 store per
+// lane, no vmcnt wait, no flag -- and each consumer wave polls the 16 granules it needs itself
+// (MI355X_MICROARCH.md "Valid forms": R2's granule needs no ordering), so a hop costs one
+// memory round trip instead of store-drain + flag + poll + load.  xg holds 2 T*64 doubles,
+// zeroed whenever the epoch restarts.  The arithmetic is the same either way.
+template <bool GRAN>
 __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm, long ldp, int T, int n,
                                                   const double* __restrict__ W, const double* __restrict__ bv,
                                                   const double* __restrict__ zv, double* xw, double* __restrict__ x,
@@ -1316,15 +1328,40 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm,
     double wr[16];   // W_w's column j, rows q*16 .. +16: requested before the chain, not after it
 #pragma unroll
     for (int r = 0; r < 16; ++r) wr[r] = Ww[(q * 16 + r) * NB + j];
+    const double ep = (double)epoch;
     for (int c = T - 1; c > w; --c) {
         if (c - 1 > w) load_blk(Ln, c - 1);
-        if (t == 0) ok_sh = spin_ge(flags + c, epoch, info);
-        __syncthreads();
-        if (!ok_sh) return;
-        const double* xc = xw + c * NB + q * 16;
         double xr[16];
+        if constexpr (GRAN) {
+            // lanes 0..15 of wave q poll the granules of x_c[q*16 .. q*16+15]
+            double* g = xw + 2 * ((long)c * NB + q * 16);   // wave-uniform
+            double v = 0.0;
+            int it = 0;
+            for (;;) {
+                const double2 gv = j < 16 ? ld16_sc1(g, (unsigned)(j * 16)) : make_double2(0.0, ep);
+                if (__all(gv.y == ep)) {
+                    v = gv.x;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                if ((++it & 63) == 0) {
+                    if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+                    if (it > kSpin) {
+                        atomicExch(info, kInfoTimeout);
+                        return;   // every wave leaves (waves that ended no longer hold the barrier)
+                    }
+                }
+            }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) xr[r] = __hip_atomic_load(xc + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int r = 0; r < 16; ++r) xr[r] = readlane_d(v, r);
+        } else {
+            if (t == 0) ok_sh = spin_ge(flags + c, epoch, info);
+            __syncthreads();
+            if (!ok_sh) return;
+            const double* xc = xw + c * NB + q * 16;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) xr[r] = __hip_atomic_load(xc + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         double s = 0.0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) s = fma(Lv[r], xr[r], s);
@@ -1343,10 +1380,15 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm,
     __syncthreads();
     if (t < NB) {   // wave 0 alone stores x_w
         const double xv = (part[0][t] + part[1][t]) + (part[2][t] + part[3][t]);
-        __hip_atomic_store(xw + w0 + t, xv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (w0 + t < n) x[w0 + t] = xv;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (t == 0) __hip_atomic_store(flags + w, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (GRAN) {
+            st16_sc1(xw + 2 * (long)w0, (unsigned)(t * 16), make_double2(xv, ep));
+            if (w0 + t < n) x[w0 + t] = xv;
+        } else {
+            __hip_atomic_store(xw + w0 + t, xv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (w0 + t < n) x[w0 + t] = xv;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (t == 0) __hip_atomic_store(flags + w, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -1365,6 +1407,12 @@ static bool chol_persistent(int variant) {
     return e ? std::atoi(e) != 0 : true;
 }
 
+// PNOL_BWD_GRANULE = 0: the backward solve's flag hand-off instead of granules (read per call)
+static bool bwd_granules() {
+    const char* e = std::getenv("PNOL_BWD_GRANULE");
+    return !e || std::atoi(e) != 0;
+}
+
 int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo) {
     return launch_chol_solve_v(ctx, A, lda, rhs, sigma, n, dinfo, 0);
 }
@@ -1379,12 +1427,24 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
     PNOL_CHECK(ws_get(ctx, "chol4_W", sizeof(double) * (size_t)T * NB * NB, &W));
     PNOL_CHECK(ws_get(ctx, "chol4_b", sizeof(double) * (size_t)N, &bv));
     PNOL_CHECK(ws_get(ctx, "chol4_z", sizeof(double) * (size_t)N, &zv));
-    PNOL_CHECK(ws_get(ctx, "chol4_x", sizeof(double) * (size_t)N, &xw));
+    // the backward solve's hand-off words: x granules (x, epoch) -- 2 N doubles, zeroed when
+    // allocated and whenever the epoch restarts (a stale granule must never match)
+    // (the flag form keeps its own buffer, so the two layouts never share memory)
+    const bool gran = bwd_granules();
+    if (gran) {
+        auto it = ctx->ws.bufs.find("chol4_xg");
+        const void* before = it == ctx->ws.bufs.end() ? nullptr : it->second.first;
+        PNOL_CHECK(ws_get(ctx, "chol4_xg", sizeof(double) * 2 * (size_t)N, &xw));
+        if (xw != before) PNOL_HIP(hipMemsetAsync(xw, 0, sizeof(double) * 2 * (size_t)N, ctx->stream));
+    } else {
+        PNOL_CHECK(ws_get(ctx, "chol4_x", sizeof(double) * (size_t)N, &xw));
+    }
     if (T > ctx->chol4_cap || ctx->chol4_epoch > (1 << 29)) {
         void* f = nullptr;
         const int cap = std::max(T, ctx->chol4_cap);
         PNOL_CHECK(ws_get(ctx, "chol4_flags", sizeof(int) * (size_t)2 * cap, &f));
         PNOL_HIP(hipMemsetAsync(f, 0, sizeof(int) * (size_t)2 * cap, ctx->stream));
+        if (gran) PNOL_HIP(hipMemsetAsync(xw, 0, sizeof(double) * 2 * (size_t)N, ctx->stream));   // epoch restarts
         ctx->chol4_flags = (int*)f;
         ctx->chol4_cap = cap;
         ctx->chol4_epoch = 0;
@@ -1425,8 +1485,14 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
                            T, (double*)W, (double*)bv, (double*)zv, (int*)pf, ntasks, dinfo, lookahead);
     }
     const int epoch = ++ctx->chol4_epoch;
-    hipLaunchKernelGGL(k_chol_bwd, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n, (const double*)W,
-                       (const double*)bv, (const double*)zv, (double*)xw, sigma, bwdflag, epoch, dinfo);
+    if (gran)
+        hipLaunchKernelGGL(k_chol_bwd<true>, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n,
+                           (const double*)W, (const double*)bv, (const double*)zv, (double*)xw, sigma, bwdflag, epoch,
+                           dinfo);
+    else
+        hipLaunchKernelGGL(k_chol_bwd<false>, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n,
+                           (const double*)W, (const double*)bv, (const double*)zv, (double*)xw, sigma, bwdflag, epoch,
+                           dinfo);
     PNOL_CHECK(launch_check());
     // test hook (tests/test_gpu_solvers.py): report a non-positive pivot so the callers' LU
     // fallback paths run on an SPD system (read per call: the tests flip it)
