@@ -953,10 +953,33 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
 #endif
     if (k < 0 && blockIdx.x > 0) {   // prep: rows b-1, b-1+G, ... of P
         const int N = T * NB, G = gridDim.x - 1;
+        // 16-byte loads and stores, all of a row's loads issued before its stores (N is a multiple
+        // of 64; the pairs past n -- the padding -- are formed per element)
+        const bool vec = ((lda & 1) == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
         for (int r = blockIdx.x - 1; r < N; r += G) {
             double* pr = P + (long)r * ldp;
             const double* ar = A + (long)r * lda;
-            for (int c = t; c < N; c += 256) pr[c] = (r < n && c < n) ? ar[c] : (r == c ? 1.0 : 0.0);
+            if (vec && r < n) {
+                double2 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int c = 2 * (t + 256 * u);
+                    v[u] = c + 1 < n ? *reinterpret_cast<const double2*>(ar + c)
+                                     : make_double2(c < n ? ar[c] : (r == c ? 1.0 : 0.0), r == c + 1 ? 1.0 : 0.0);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int c = 2 * (t + 256 * u);
+                    if (c < N) *reinterpret_cast<double2*>(pr + c) = v[u];
+                }
+                for (int c = 2 * (t + 1024); c < N; c += 512) {   // rows past 2048 columns
+                    const double2 w = c + 1 < n ? *reinterpret_cast<const double2*>(ar + c)
+                                                : make_double2(c < n ? ar[c] : (r == c ? 1.0 : 0.0), r == c + 1 ? 1.0 : 0.0);
+                    *reinterpret_cast<double2*>(pr + c) = w;
+                }
+            } else {
+                for (int c = t; c < N; c += 256) pr[c] = (r < n && c < n) ? ar[c] : (r == c ? 1.0 : 0.0);
+            }
         }
         if (blockIdx.x == 1)
             for (int r = t; r < N; r += 256) bv[r] = r < n ? rhs[r] : 0.0;
