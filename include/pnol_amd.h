@@ -190,6 +190,11 @@ int pnol_solve_d(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
  * falls back to pnol_solve_d with method 2; A is left intact).  Lets the LM loop keep the
  * device busy while the host checks the previous trial point. */
 int pnol_solve_async_d(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo);
+/* pnol_solve_async_d + pnol_add_d(x, sigma, xnext): the LM trial point X + sigma
+ * (LevenbergMarquardt.cpp:83-90) written by the solve's last launch.  xnext is undefined, like
+ * sigma, when *dinfo ends nonzero. */
+int pnol_solve_step_d(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo,
+                      const double* x, double* xnext);
 /* Binv = B^{-1} (n x n, row-major, device), bitwise the reference's matrixInverse: luSolve(B, e_c)
  * for every column c (UtilityFunctionLibrary restatement) as ONE partial-pivoting
  * elimination of [B | I] followed by per-column back substitution (the initHessFD inverse,

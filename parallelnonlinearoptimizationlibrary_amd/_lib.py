@@ -89,6 +89,7 @@ _SIGS = {
     "pnol_jtr_d": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
     "pnol_solve_d": (_i, [_vp, _vp, _i, _vp, _vp, _i, _i, C.POINTER(_i)]),
     "pnol_solve_async_d": (_i, [_vp, _vp, _i, _vp, _vp, _i, _vp]),
+    "pnol_solve_step_d": (_i, [_vp, _vp, _i, _vp, _vp, _i, _vp, _vp, _vp]),
     "pnol_matrix_inverse_d": (_i, [_vp, _vp, _i, _i, _vp, _i, C.POINTER(_i)]),
     "pnol_add_d": (_i, [_vp, _vp, _vp, _vp, _i]),
     "pnol_dobj_create": (_i, [_vp, _i, _i, _i, _dp, _sz, _dp, _sz, _d, C.POINTER(_vp)]),

@@ -80,6 +80,14 @@ int pnol_solve_async_d(pnol_ctx* ctx, const double* A, int lda, const double* rh
     return launch_chol_solve(ctx, A, lda, rhs, sigma, n, dinfo);
 }
 
+int pnol_solve_step_d(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo,
+                      const double* x, double* xnext) {
+    PNOL_CHECK(set_device(ctx));
+    if (!A || !rhs || !sigma || !dinfo || !x || !xnext || n <= 0 || lda < n) return PNOL_ERR_ARG;
+    ScopedTimer tm(ctx, "solve");
+    return launch_chol_solve(ctx, A, lda, rhs, sigma, n, dinfo, x, xnext);
+}
+
 int pnol_gather_submatrix_d(pnol_ctx* ctx, const double* D, int ldd, int n, const int* idx, int nsub,
                             double* Dsub, int lds) {
     PNOL_CHECK(set_device(ctx));

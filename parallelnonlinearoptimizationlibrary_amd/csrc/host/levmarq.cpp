@@ -234,12 +234,15 @@ class LMAsync {
                                    A_.get(), lda_, nullptr, rhs_.get()),
                   "fd_normal");
         }
-        check(pnol_solve_async_d(ctx_, A_.get(), lda_, rhs_.get(), sig(s), n_, info(s)), "solve");
-        finish(s);
+        // the solve's last launch also forms the trial point x_[s] + sigma
+        check(pnol_solve_step_d(ctx_, A_.get(), lda_, rhs_.get(), sig(s), n_, info(s), x_[s].get(), x_[s ^ 1].get()),
+              "solve");
+        finish(s, false);
     }
-    // the rest of a trip once sigma_[s] is known: trial point, its residuals, copies back
-    void finish(int s) {
-        check(pnol_add_d(ctx_, x_[s].get(), sig(s), x_[s ^ 1].get(), n_), "add");
+    // the rest of a trip once sigma_[s] is known: trial point (unless the solve formed it), its
+    // residuals, copies back
+    void finish(int s, bool add = true) {
+        if (add) check(pnol_add_d(ctx_, x_[s].get(), sig(s), x_[s ^ 1].get(), n_), "add");
         check(pnol_dobj_eval_ckpt_d(ctx_, d_, x_[s ^ 1].get(), F(s ^ 1)), "objective eval");
         check(pnol_memcpy_d2h_async(ctx_, pin_[s], trip_[s].get(), sizeof(double) * ((size_t)np_ + mp_ + 1)), "d2h");
         check(pnol_event_record(ctx_, ev_[s]), "event");

@@ -1322,7 +1322,9 @@ template <bool GRAN>
 __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm, long ldp, int T, int n,
                                                   const double* __restrict__ W, const double* __restrict__ bv,
                                                   const double* __restrict__ zv, double* xw, double* __restrict__ x,
-                                                  int* flags, int epoch, int* info) {
+                                                  int* flags, int epoch, int* info,
+                                                  const double* __restrict__ xbase = nullptr,
+                                                  double* __restrict__ xnext = nullptr) {
     __shared__ double part[4][NB];
     __shared__ double vsh[NB];
     __shared__ int ok_sh;
@@ -1405,10 +1407,15 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm,
         const double xv = (part[0][t] + part[1][t]) + (part[2][t] + part[3][t]);
         if constexpr (GRAN) {
             st16_sc1(xw + 2 * (long)w0, (unsigned)(t * 16), make_double2(xv, ep));
-            if (w0 + t < n) x[w0 + t] = xv;
         } else {
             __hip_atomic_store(xw + w0 + t, xv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (w0 + t < n) x[w0 + t] = xv;
+        }
+        if (w0 + t < n) {
+            x[w0 + t] = xv;
+            // the LM trial point X + sigma (LevenbergMarquardt.cpp:87-90), the add of pnol_add_d
+            if (xnext) xnext[w0 + t] = xbase[w0 + t] + xv;
+        }
+        if constexpr (!GRAN) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (t == 0) __hip_atomic_store(flags + w, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1436,12 +1443,13 @@ static bool bwd_granules() {
     return !e || std::atoi(e) != 0;
 }
 
-int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo) {
-    return launch_chol_solve_v(ctx, A, lda, rhs, sigma, n, dinfo, 0);
+int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo,
+                      const double* xbase, double* xnext) {
+    return launch_chol_solve_v(ctx, A, lda, rhs, sigma, n, dinfo, 0, xbase, xnext);
 }
 
 int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo,
-                        int variant) {
+                        int variant, const double* xbase, double* xnext) {
     const int T = (n + NB - 1) / NB, N = T * NB;
     const long ldp = N;
     void *P = nullptr, *Lm = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr;
@@ -1511,11 +1519,11 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
     if (gran)
         hipLaunchKernelGGL(k_chol_bwd<true>, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n,
                            (const double*)W, (const double*)bv, (const double*)zv, (double*)xw, sigma, bwdflag, epoch,
-                           dinfo);
+                           dinfo, xbase, xnext);
     else
         hipLaunchKernelGGL(k_chol_bwd<false>, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n,
                            (const double*)W, (const double*)bv, (const double*)zv, (double*)xw, sigma, bwdflag, epoch,
-                           dinfo);
+                           dinfo, xbase, xnext);
     PNOL_CHECK(launch_check());
     // test hook (tests/test_gpu_solvers.py): report a non-positive pivot so the callers' LU
     // fallback paths run on an SPD system (read per call: the tests flip it)

@@ -188,11 +188,13 @@ int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, do
 // Binv = B^{-1} as the reference's matrixInverse (per-column luSolve), bitwise: one elimination
 // of [B | I], per-column back substitution; *info_host = -1 on a zero pivot (inf / NaN entries)
 int launch_matrix_inverse(pnol_ctx* ctx, const double* B, int ldb, int n, double* Binv, int ldi, int* info_host);
-int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo);
+// xnext (nullable): also xnext = xbase + sigma (the LM trial point), written by the final launch
+int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo,
+                      const double* xbase = nullptr, double* xnext = nullptr);
 // variant 0: auto (PNOL_CHOL_PERSIST, default the persistent form), 4: per-step launches,
 // 5: one persistent launch for the panel steps (bitwise the same result)
 int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo,
-                        int variant);
+                        int variant, const double* xbase = nullptr, double* xnext = nullptr);
 int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n, int method,
                  int* info);
 
