@@ -208,3 +208,4 @@ def test_rccl_selfcheck_world1():
     out = r.stdout.decode(errors="replace") + r.stderr.decode(errors="replace")
     assert r.returncode == 0, out[-3000:]
     assert "RCCL self-check ok=True" in out
+    assert "host-communicator fallback ok=True" in out

@@ -26,11 +26,25 @@ def main():
     class _Ctx:
         h = dctx
     init_rccl(_Ctx, rank, world)
-    ok, why = rccl_selfcheck(Context(local), world)
+    ctx = Context(local)
+    ok, why = rccl_selfcheck(ctx, world)
     print(f"rank {rank}/{world}: RCCL self-check ok={ok} ({why})", flush=True)
+    # the bench's fallback after a failed check: the RCCL communicator dropped, the host
+    # communicator over a gloo group beside the NCCL default group, LevMarqMPI through it
+    import numpy as np
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective, run_levmarq
+    from parallelnonlinearoptimizationlibrary_amd.dist import HostComm
     L.lib().pnol_comm_finalize()
+    hc = HostComm(rank, world, group=dist.new_group(backend="gloo"))
+    obj = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, 300, 1500)
+    params = (0.001, 10.0, 1e-7, 6, 0.0, -1)
+    x_mpi, *_ = run_levmarq(obj, np.zeros(300), params, which=1)
+    x_one, *_ = run_levmarq(obj, np.zeros(300), params, which=0)
+    fb = bool(np.array_equal(x_mpi, x_one))
+    print(f"rank {rank}/{world}: host-communicator fallback ok={fb}", flush=True)
+    hc.close()
     dist.destroy_process_group()
-    sys.exit(0 if ok else 1)
+    sys.exit(0 if (ok and fb) else 1)
 
 
 if __name__ == "__main__":
