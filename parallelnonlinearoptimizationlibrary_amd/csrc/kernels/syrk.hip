@@ -415,10 +415,24 @@ __global__ void k_syrk_unpack(const double* __restrict__ packed, int ntiles, int
 // row-wise, and writes the mirror from an LDS transpose so those stores are row-wise too.
 // SUB > 0: the sub-chunk count at compile time (all kS * SUB loads of an element in flight at
 // once); SUB = 0: runtime `sub`.
+// jp / rhs (nullable): one more row of blocks (blockIdx.y == ntiles) forms rhs = the slice
+// tree of the 8 -J^T F slice partials jp[s * n + e], exactly as k_tree_nodes over all slices does
+// (leaf = 0.0 + partial, then tree8): the tree rides in this launch instead of its own.
 template <int SUB, int SR = 32>
 __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ part, int ntiles, int sub_rt, int n,
                                                      double lambda, double* __restrict__ A, long lda,
-                                                     double* __restrict__ diag_out, int tile0) {
+                                                     double* __restrict__ diag_out, int tile0,
+                                                     const double* __restrict__ jp = nullptr,
+                                                     double* __restrict__ rhs = nullptr) {
+    if (jp && (int)blockIdx.y == ntiles) {
+        for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+            double l[kS];
+#pragma unroll
+            for (int s = 0; s < kS; ++s) l[s] = 0.0 + jp[(long)s * n + e];
+            rhs[e] = tree8(l);
+        }
+        return;
+    }
     const int sub = SUB > 0 ? SUB : sub_rt;                // SR: strip rows
     __shared__ double st[SR][kTile + 1];
     const int t = tile0 + blockIdx.y;                      // part holds this launch's tiles from tile0 on
@@ -706,12 +720,19 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
         PNOL_CHECK(jtr_gemv_tail(ctx, tf, tv, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F));
     else if (rhs)
         PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F));
+    // -J^T F's slice tree rides in the reduce launch (an extra row of blocks), except when the
+    // GEMV ran on the tail stream (the tree then waits for its event)
+    const bool fold = rhs && !tail;
+    void* jp = nullptr;
+    if (fold) PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
     {
         ScopedTimer tm(ctx, "syrk_reduce");
-        launch_reduce(dim3(kTile / 32, ntiles), dim3(256), 0, ctx->stream, (const double*)part, ntiles,
-                      sc.sub, n, lambda, A, (long)lda, jtj_diag, 0);
+        launch_reduce(dim3(kTile / 32, ntiles + (fold ? 1 : 0)), dim3(256), 0, ctx->stream, (const double*)part,
+                      ntiles, sc.sub, n, lambda, A, (long)lda, jtj_diag, 0, (const double*)jp,
+                      fold ? rhs : (double*)nullptr);
         PNOL_CHECK(launch_check());
     }
+    if (fold) return PNOL_OK;
     if (tail) PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->tail_ev, 0));
     return rhs ? jtr_tree(ctx, n, 0, kS, rhs) : PNOL_OK;
 }
@@ -925,13 +946,18 @@ int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lamb
             PNOL_CHECK(jtr_gemv(ctx, JTs, sc.mS, sstr, m, n, sc.mS, s0, nsl, F));
     }
     if (P == 1) {
+        // the -J^T F tree rides in the reduce launch unless the GEMV ran on the tail stream
+        void* jp = nullptr;
+        if (!tail) PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
         {
             ScopedTimer tm(ctx, "syrk_reduce");
-            launch_reduce(dim3(kTile / 32, ntiles), dim3(256), 0, ctx->stream, (const double*)part,
-                               ntiles, sc.sub, n, lambda, A, (long)lda, jtj_diag, 0);
+            launch_reduce(dim3(kTile / 32, ntiles + (tail ? 0 : 1)), dim3(256), 0, ctx->stream, (const double*)part,
+                          ntiles, sc.sub, n, lambda, A, (long)lda, jtj_diag, 0, (const double*)jp,
+                          tail ? (double*)nullptr : rhs);
         }
         PNOL_CHECK(launch_check());
-        if (tail) PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->tail_ev, 0));
+        if (!tail) return PNOL_OK;
+        PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->tail_ev, 0));
         return jtr_tree(ctx, n, 0, kS, rhs);
     }
     // the global node list: rank q's nodes in slice order, ranks in order
