@@ -505,7 +505,10 @@ def main():
                                "achieved": hg["hg_GBps"],
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hg["hg_frac_of_hbm"],
                                "algorithmic_bytes": 8.0 * HG_N * HG_N + 16.0 * HG_N,
-                               "traffic": pmc.get("k_gemv_neg_wg<2, true>", {}).get("traffic_bytes_per_launch"),
+                               # the launch at this n: (n / 2) workgroups of 256 lanes (launch_gemv_neg);
+                               # the bench also runs H.g at n = 4096 and 16384, so key by grid
+                               "traffic": pmc.get(f"k_gemv_neg_wg<2, true>@grid{HG_N // 2 * 256}",
+                                                  {}).get("traffic_bytes_per_launch"),
                                "n": HG_N}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
