@@ -290,6 +290,9 @@ struct ColBuf {
 #ifndef PNOL_CHOL_HELP_COLS
 #define PNOL_CHOL_HELP_COLS 16
 #endif
+#ifndef PNOL_CHOL_LOCAL_PIV
+#define PNOL_CHOL_LOCAL_PIV 1
+#endif
 constexpr int kSplit = 16, kHelpK = kSplit + 2, kHelpCols = PNOL_CHOL_HELP_COLS;
 // the hand-off step: before column kHelpCols's tail reaches the helpers' entries, and before
 // step kHelpK - 2's immediate update of entry kHelpK
@@ -307,10 +310,17 @@ __device__ __forceinline__ void panel_step(double (&a)[kHalf], double& piv, doub
     const double l = a[J] * r, rJ = r;
     a[J] = l;
     if constexpr (J + 1 < kHalf) {
-        // the critical chain: only l_{J+1,J} (a readlane) feeds the next pivot
         const double l1 = readlane_d(l, J + 1);
+#if PNOL_CHOL_LOCAL_PIV
+        // the critical chain: lane J+1 holds both l_{J+1,J} (its own l) and the entry (J+1, J+1),
+        // so it forms the next pivot without the broadcast -- fma(-l, l, .) there is the same
+        // operation on the same operands as fma(-l, l1, .) -- and one readlane remains on the chain
+        piv = readlane_d(fma(-l, l, a[J + 1]), J + 1);
+        a[J + 1] = fma(-l, l1, a[J + 1]);
+#else
         a[J + 1] = fma(-l, l1, a[J + 1]);
         piv = readlane_d(a[J + 1], J + 1);
+#endif
         bad |= !(piv > 0.0);
         r = rsqrt_nr(piv);
     }

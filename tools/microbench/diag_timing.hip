@@ -6,6 +6,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 namespace pnol {
@@ -63,7 +64,9 @@ int main() {
             err = std::fmax(err, std::fabs(acc - (i == j)));
         }
     const long long b = st[31];
-    printf("{\"info\": %d, \"max|W A W^T - I|\": %.3e, \"cycles\": {", info, err);
+    unsigned long long h = 1469598103934665603ULL;   // FNV-1a of W's bits (A/B builds must agree)
+    for (double v : W) { unsigned long long u; memcpy(&u, &v, 8); h = (h ^ u) * 1099511628211ULL; }
+    printf("{\"info\": %d, \"max|W A W^T - I|\": %.3e, \"w_hash\": \"%016llx\", \"cycles\": {", info, err, h);
     const char* names[] = {"p1_j0", "p1_j8", "p1_j16", "p1_j24", "p1_end", "w11_end", "p2_q00_end", "-", "p3_start",
                            "p3_j0", "p3_j8", "p3_j16", "p3_j24", "p3_end", "w22_end", "b3", "p4_end"};
     for (int i = 0; i < 17; ++i)
