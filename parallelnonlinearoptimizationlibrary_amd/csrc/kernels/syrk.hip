@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 namespace pnol {
@@ -37,6 +38,39 @@ constexpr int kPad = 18;   // LDS row stride in doubles
 #define PNOL_SYRK_B128 1
 #endif
 
+// Diagonal tiles (ti == tj) of the 8-wave 128-row kernel compute only their 36 lower 16 x 16
+// blocks (bi >= bj) of the 64, 5 or 4 per wave so that the two waves of each SIMD (waves w and
+// w + 4) hold 9 together -- the busiest SIMD issues 36 MFMAs per stage instead of 64 -- and
+// zero the 28 upper blocks (no reader uses them; the partials stay fully defined).  Each block
+// runs the same MFMA chain as in the 2 x 4 wave layout, so the partials are bitwise the same.
+#ifndef PNOL_SYRK_DIAG_BAL
+#define PNOL_SYRK_DIAG_BAL 1
+#endif
+// wave w's blocks as bi * 8 + bj, 6 bits each (blocks of one block row together: they share
+// the A fragment); bits 30..31: 4 or 5 blocks.  Words, not bytes: a scalar load.
+__device__ __forceinline__ unsigned diag_blocks(int w) {
+    constexpr unsigned T[8] = {
+        56u | 57u << 6 | 58u << 12 | 59u << 18 | 60u << 24 | 1u << 30,
+        48u | 49u << 6 | 50u << 12 | 51u << 18 | 52u << 24 | 1u << 30,
+        40u | 41u << 6 | 42u << 12 | 43u << 18 | 44u << 24 | 1u << 30,
+        32u | 33u << 6 | 34u << 12 | 35u << 18 | 36u << 24 | 1u << 30,
+        61u | 62u << 6 | 63u << 12 | 0u << 18,
+        53u | 54u << 6 | 8u << 12 | 9u << 18,
+        45u | 16u << 6 | 17u << 12 | 18u << 18,
+        24u | 25u << 6 | 26u << 12 | 27u << 18};
+    unsigned v = T[0];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) v = w == q ? T[q] : v;   // w is wave-uniform: scalar selects
+    return v;
+}
+// the first kDiagSplit[w] blocks share one block row, the rest another (two A fragments)
+__device__ __forceinline__ int diag_split(int w) {
+    constexpr int S[8] = {5, 5, 5, 5, 3, 2, 1, 4};
+    int v = S[0];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) v = w == q ? S[q] : v;
+    return v;
+}
 
 __device__ __forceinline__ void tile_of(int t, int& ti, int& tj) {
     int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
@@ -167,69 +201,114 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
 #pragma unroll
         for (int j = 0; j < NBN; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
 
-    StageRegs<TILE, NT> ps, qs;
-    if (nstages > 0) {
-        bool full = ldx_even && (kbeg + kTK <= kend);
-        load_stage<TILE, NT>(ps, X, ldx, nr, prow0, kbeg, kend, full);
-        if (!diag) load_stage<TILE, NT>(qs, X, ldx, nr, qrow0, kbeg, kend, full);
+    constexpr bool kBal = PNOL_SYRK_DIAG_BAL && NW == 8 && TILE == 128 && MODE != 1 && !XMAP;
+    const bool bal = kBal && diag;
+    int dbi[5], dbj[5], dcnt = 0, dsplit = 0;
+    {
+        const int wv = __builtin_amdgcn_readfirstlane(wave);
+        const unsigned code = bal ? diag_blocks(wv) : 0u;
+        dcnt = 4 + (int)(code >> 30);
+        dsplit = diag_split(wv);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            dbi[q] = (code >> (6 * q + 3)) & 7;
+            dbj[q] = (code >> (6 * q)) & 7;
+        }
     }
-    const int frow = lane & 15;
-    const int fk = lane >> 4;
-    for (int st = 0; st < nstages; ++st) {
-        const int buf = st & 1;
-        double* P = lds[buf][0];
-        double* Q = diag ? lds[buf][0] : lds[buf][1];
-        store_stage<TILE, NT>(ps, P);
-        if (!diag) store_stage<TILE, NT>(qs, Q);
-        __syncthreads();
-        if (st + 1 < nstages) {
-            const int k0 = kbeg + (st + 1) * kTK;
-            bool full = ldx_even && (k0 + kTK <= kend);
-            load_stage<TILE, NT>(ps, X, ldx, nr, prow0, k0, kend, full);
-            if (!diag) load_stage<TILE, NT>(qs, X, ldx, nr, qrow0, k0, kend, full);
+    const int drow0 = dbi[0], drow1 = dsplit >= 4 ? dbi[4] : dsplit == 3 ? dbi[3] : dsplit == 2 ? dbi[2] : dbi[1];
+
+    // the stage loop, instantiated once per path (diagonal-balanced or 2 x 4 waves) so each copy
+    // holds only its own fragments live
+    auto stage_loop = [&](auto BAL) {
+        StageRegs<TILE, NT> ps, qs;
+        if (nstages > 0) {
+            bool full = ldx_even && (kbeg + kTK <= kend);
+            load_stage<TILE, NT>(ps, X, ldx, nr, prow0, kbeg, kend, full);
+            if (!diag) load_stage<TILE, NT>(qs, X, ldx, nr, qrow0, kbeg, kend, full);
         }
+        const int frow = lane & 15;
+        const int fk = lane >> 4;
+        for (int st = 0; st < nstages; ++st) {
+            const int buf = st & 1;
+            double* P = lds[buf][0];
+            double* Q = diag ? lds[buf][0] : lds[buf][1];
+            store_stage<TILE, NT>(ps, P);
+            if (!diag) store_stage<TILE, NT>(qs, Q);
+            __syncthreads();
+            if (st + 1 < nstages) {
+                const int k0 = kbeg + (st + 1) * kTK;
+                bool full = ldx_even && (k0 + kTK <= kend);
+                load_stage<TILE, NT>(ps, X, ldx, nr, prow0, k0, kend, full);
+                if (!diag) load_stage<TILE, NT>(qs, X, ldx, nr, qrow0, k0, kend, full);
+            }
 #if PNOL_SYRK_B128
-        // one 16-byte fragment read per operand block covers two MFMA K-groups: lane l holds
-        // k = 8 kk + 2 (l >> 4) + {0, 1}; the first MFMA takes the even k of the 8-block, the
-        // second the odd ones (half the ds_read instructions; the 144-byte row stride keeps the
-        // 16 rows of a 16-lane group on distinct bank quads).  Every element's MFMA chain is
-        // the same in every mode and tile size, so all paths still sum it identically.
+            // one 16-byte fragment read per operand block covers two MFMA K-groups: lane l holds
+            // k = 8 kk + 2 (l >> 4) + {0, 1}; the first MFMA takes the even k of the 8-block, the
+            // second the odd ones (half the ds_read instructions; the 144-byte row stride keeps the
+            // 16 rows of a 16-lane group on distinct bank quads).  Every element's MFMA chain is
+            // the same in every mode and tile size, so all paths still sum it identically.
+            if constexpr (decltype(BAL)::value) {
 #pragma unroll
-        for (int kk = 0; kk < kTK / 8; ++kk) {
-            double2 a[NBM], b[NBN];
+                for (int kk = 0; kk < kTK / 8; ++kk) {
+                    const double2 a0 = *reinterpret_cast<const double2*>(P + (drow0 * 16 + frow) * kPad + kk * 8 + 2 * fk);
+                    const double2 a1 = *reinterpret_cast<const double2*>(P + (drow1 * 16 + frow) * kPad + kk * 8 + 2 * fk);
+                    double2 b[5];
 #pragma unroll
-            for (int mi = 0; mi < NBM; ++mi)
-                a[mi] = *reinterpret_cast<const double2*>(P + (wr * WTM + mi * 16 + frow) * kPad + kk * 8 + 2 * fk);
+                    for (int q = 0; q < 5; ++q)
+                        if (q < 4 || dcnt == 5)
+                            b[q] = *reinterpret_cast<const double2*>(P + (dbj[q] * 16 + frow) * kPad + kk * 8 + 2 * fk);
 #pragma unroll
-            for (int ni = 0; ni < NBN; ++ni)
-                b[ni] = *reinterpret_cast<const double2*>(Q + (wc * WTN + ni * 16 + frow) * kPad + kk * 8 + 2 * fk);
+                    for (int q = 0; q < 5; ++q)
+                        if (q < 4 || dcnt == 5)
+                            acc[q >> 1][q & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(q < dsplit ? a0.x : a1.x, b[q].x,
+                                                                                      acc[q >> 1][q & 1], 0, 0, 0);
 #pragma unroll
-            for (int mi = 0; mi < NBM; ++mi)
+                    for (int q = 0; q < 5; ++q)
+                        if (q < 4 || dcnt == 5)
+                            acc[q >> 1][q & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(q < dsplit ? a0.y : a1.y, b[q].y,
+                                                                                      acc[q >> 1][q & 1], 0, 0, 0);
+                }
+            } else {
+#pragma unroll
+            for (int kk = 0; kk < kTK / 8; ++kk) {
+                double2 a[NBM], b[NBN];
+#pragma unroll
+                for (int mi = 0; mi < NBM; ++mi)
+                    a[mi] = *reinterpret_cast<const double2*>(P + (wr * WTM + mi * 16 + frow) * kPad + kk * 8 + 2 * fk);
 #pragma unroll
                 for (int ni = 0; ni < NBN; ++ni)
-                    acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].x, b[ni].x, acc[mi][ni], 0, 0, 0);
+                    b[ni] = *reinterpret_cast<const double2*>(Q + (wc * WTN + ni * 16 + frow) * kPad + kk * 8 + 2 * fk);
 #pragma unroll
-            for (int mi = 0; mi < NBM; ++mi)
+                for (int mi = 0; mi < NBM; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < NBN; ++ni)
-                    acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].y, b[ni].y, acc[mi][ni], 0, 0, 0);
-        }
+                    for (int ni = 0; ni < NBN; ++ni)
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].x, b[ni].x, acc[mi][ni], 0, 0, 0);
+#pragma unroll
+                for (int mi = 0; mi < NBM; ++mi)
+#pragma unroll
+                    for (int ni = 0; ni < NBN; ++ni)
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].y, b[ni].y, acc[mi][ni], 0, 0, 0);
+            }
+            }
 #else
 #pragma unroll
-        for (int kk = 0; kk < kTK / 4; ++kk) {
-            double a[NBM], b[NBN];
+            for (int kk = 0; kk < kTK / 4; ++kk) {
+                double a[NBM], b[NBN];
 #pragma unroll
-            for (int mi = 0; mi < NBM; ++mi) a[mi] = P[(wr * WTM + mi * 16 + frow) * kPad + kk * 4 + fk];
+                for (int mi = 0; mi < NBM; ++mi) a[mi] = P[(wr * WTM + mi * 16 + frow) * kPad + kk * 4 + fk];
 #pragma unroll
-            for (int ni = 0; ni < NBN; ++ni) b[ni] = Q[(wc * WTN + ni * 16 + frow) * kPad + kk * 4 + fk];
+                for (int ni = 0; ni < NBN; ++ni) b[ni] = Q[(wc * WTN + ni * 16 + frow) * kPad + kk * 4 + fk];
 #pragma unroll
-            for (int mi = 0; mi < NBM; ++mi)
+                for (int mi = 0; mi < NBM; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < NBN; ++ni)
-                    acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
-        }
+                    for (int ni = 0; ni < NBN; ++ni)
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+            }
 #endif
-    }
+        }
+    };
+    if (kBal && bal) stage_loop(std::true_type{});
+    else stage_loop(std::false_type{});
 
     // f64 MFMA C/D layout: lane l, register r -> row (l >> 4) + 4 r, column l & 15
     const int ocol = lane & 15;
@@ -249,16 +328,35 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
             out = part + (long)blk * TILE * TILE;
             ld = TILE;
         }
+        if (kBal && bal) {
 #pragma unroll
-        for (int mi = 0; mi < NBM; ++mi)
+            for (int q = 0; q < 5; ++q)
+                if (q < 4 || dcnt == 5)
 #pragma unroll
-            for (int ni = 0; ni < NBN; ++ni)
+                    for (int r = 0; r < 4; ++r)
+                        __builtin_nontemporal_store(acc[q >> 1][q & 1][r],
+                                                    out + (dbi[q] * 16 + orow + 4 * r) * ld + dbj[q] * 16 + ocol);
+            // upper block u = bj (bj - 1) / 2 + bi (bi < bj): blocks wave, wave + 8, ... of the 28
+            for (int u = __builtin_amdgcn_readfirstlane(wave); u < 28; u += NW) {
+                int bj = 1;
+                while ((bj + 1) * bj / 2 <= u) ++bj;
+                const int bi = u - bj * (bj - 1) / 2;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    int row = wr * WTM + mi * 16 + orow + 4 * r;
-                    int col = wc * WTN + ni * 16 + ocol;
-                    __builtin_nontemporal_store(acc[mi][ni][r], out + row * ld + col);
-                }
+                for (int r = 0; r < 4; ++r)
+                    __builtin_nontemporal_store(0.0, out + (bi * 16 + orow + 4 * r) * ld + bj * 16 + ocol);
+            }
+        } else {
+#pragma unroll
+            for (int mi = 0; mi < NBM; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < NBN; ++ni)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        int row = wr * WTM + mi * 16 + orow + 4 * r;
+                        int col = wc * WTN + ni * 16 + ocol;
+                        __builtin_nontemporal_store(acc[mi][ni][r], out + row * ld + col);
+                    }
+        }
     } else {
 #pragma unroll
         for (int mi = 0; mi < NBM; ++mi)
