@@ -162,7 +162,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
         const int tl = local % ntl;
         blk = tl * split_k + sidx;           // partial slot: the same layout as below
         t = tile0 + tl;
-    } else if (umajor) {
+    } else if (umajor & 1) {
         // every (tile, slice)'s chunk 0 first, then chunk 1, ...: with a long chunk 0 the short
         // chunks fill the last dispatch round instead of leaving it part-empty
         const int ntl = gridDim.x / split_k, nsl = split_k / sub;
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
         for (int j = 0; j < NBN; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
 
     constexpr bool kBal = PNOL_SYRK_DIAG_BAL && NW == 8 && TILE == 128 && MODE != 1 && !XMAP;
-    const bool bal = kBal && diag;
+    const bool bal = kBal && diag && !(umajor & 2);
     int dbi[5], dbj[5], dcnt = 0, dsplit = 0;
     {
         const int wv = __builtin_amdgcn_readfirstlane(wave);
@@ -685,10 +685,13 @@ static int syrk_nw() {
     return nw;
 }
 
+// bit 0: umajor dispatch (PNOL_SYRK_UMAJOR, default on); bit 1: the diagonal tiles in the 2 x 4
+// wave layout instead of the balanced block sets (PNOL_SYRK_DIAG_BAL=0; A/B switch)
 static int syrk_umajor() {
     static const int v = [] {
         const char* e = std::getenv("PNOL_SYRK_UMAJOR");
-        return e ? std::atoi(e) : 1;
+        const char* d = std::getenv("PNOL_SYRK_DIAG_BAL");
+        return (e ? (std::atoi(e) != 0) : 1) | (d && std::atoi(d) == 0 ? 2 : 0);
     }();
     return v;
 }

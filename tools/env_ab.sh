@@ -1,6 +1,7 @@
 #!/bin/bash
 # Same-box A/B of env settings on short LM benches: alternating runs of each setting, LM iters/s,
-# ms per trip and the warmup breakdown of one kernel timer.
+# ms per trip, the warmup breakdown of one kernel timer and the in-step SYRK / FD times (the FD
+# time shows the box's drift between runs).
 #   VAR=PNOL_EVAL_RPW VALS="64 32 16" KEY=linres_eval tools/env_ab.sh
 set -u
 mkdir -p gpurun_out
@@ -9,6 +10,6 @@ for rep in 1 2 3; do
     env $VAR=$v timeout -k 10 180 python bench.py --no-cpu-baseline --no-hg --no-bfgs --steps 30 --warmup 3 \
         > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err
     rc=$?; [ "$rc" -eq 0 ] || { echo "bench rc=$rc"; tail -5 gpurun_out/ab_$v.err; exit $rc; }
-    python3 -c "import json; d=json.loads(open('gpurun_out/ab_$v.json').readline()); print('$VAR=$v', round(d['value'],2), round(d['ms_per_step'],4), '${KEY:-linres_eval}', round(d['kernel_ms_per_call_warmup_breakdown'].get('${KEY:-linres_eval}',0),4))"
+    python3 -c "import json; d=json.loads(open('gpurun_out/ab_$v.json').readline()); k=d['kernel_ms_per_step_max_over_ranks']; print('$VAR=$v', round(d['value'],2), round(d['ms_per_step'],4), '${KEY:-linres_eval}', round(d['kernel_ms_per_call_warmup_breakdown'].get('${KEY:-linres_eval}',0),4), 'in-step syrk', round(k['syrk'],4), 'fd', round(k['fd_jacobian'],4))"
   done
 done
