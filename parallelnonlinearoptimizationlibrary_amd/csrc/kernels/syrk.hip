@@ -633,14 +633,15 @@ static void launch_reduce(dim3 grid, dim3 block, size_t shm, hipStream_t st, con
                           Args... args) {
     static const int sr = [] {
         const char* e = std::getenv("PNOL_REDUCE_SR");
-        return e ? std::atoi(e) : 8;
+        return e ? std::atoi(e) : 16;
     }();
     if (sr == 32)
         launch_reduce_sr<32>(grid, block, shm, st, part, ntiles, sub, args...);
-    else if (sr == 16)   // 70 us vs 77 us for 32-row strips at n = 2048, sub = 2
-        launch_reduce_sr<16>(grid, block, shm, st, part, ntiles, sub, args...);
-    else   // 8-row strips (default): 72-73 us vs 75.5-78 us for 16 (same-box pairs, tools/env_ab.sh)
+    else if (sr == 8)   // the reduce itself 72-74 vs 75.5-78 us, but the trips of those runs were
+                        // not faster (4 of 6 same-box pairs slower, tools/env_ab.sh): kept optional
         launch_reduce_sr<8>(grid, block, shm, st, part, ntiles, sub, args...);
+    else   // 16-row strips (default): 70 us vs 77 us for 32-row strips at n = 2048, sub = 2
+        launch_reduce_sr<16>(grid, block, shm, st, part, ntiles, sub, args...);
 }
 
 static SliceCfg slice_cfg(int m, int ntiles) {
