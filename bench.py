@@ -329,8 +329,83 @@ def cpu_baseline(m, n, budget_s=20.0):
     }
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n, base_env, port):
+    """The environment of each of the n ranks bench.py starts itself (one process per GPU, as
+    torch.distributed.run would set it up on one node, rendezvous on 127.0.0.1)."""
+    envs = []
+    for r in range(n):
+        e = dict(base_env)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                  "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(argv, n, timeout_s=None, python=None, script=None):
+    """`bench.py --gpus N` without a launcher: start N child processes of this script, one per
+    GPU, each with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set; relay rank 0's
+    stdout (its one JSON line) and return non-zero if any rank fails.  This process never touches
+    the GPU (it runs before `import torch`).  When one rank fails the others are stopped (they
+    would wait in a collective for it)."""
+    import subprocess
+    py = python or sys.executable
+    envs = rank_envs(n, os.environ, _free_port())
+    procs = []
+    for r in range(n):
+        procs.append(subprocess.Popen([py, script or os.path.abspath(__file__)] + list(argv), env=envs[r],
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out0 = []
+    import threading
+    rd = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
+    rd.start()
+    t0 = time.monotonic()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad or (timeout_s is not None and time.monotonic() - t0 > timeout_s):
+            rc = bad[0] if bad else 124
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(0.05)
+    rd.join(timeout=30)
+    data = out0[0] if out0 else b""
+    if data:
+        sys.stdout.buffer.write(data)
+        sys.stdout.flush()
+    if rc:
+        print(f"[bench] a rank exited with status {rc}; {n} ranks stopped", file=sys.stderr, flush=True)
+    return rc
+
+
 def main():
     args = _args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher: start the ranks here, before anything touches the GPU
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={env_world}: refusing to measure a different "
+              f"job size than the one asked for", file=sys.stderr, flush=True)
+        sys.exit(2)
     # the ONE JSON line goes to the real stdout; everything else written to fd 1 -- the drop-in
     # solvers' console messages (BFGS_Bnd prints one per boundary recursion, as the reference
     # does), library logs -- goes to stderr

@@ -329,6 +329,12 @@ typedef double (*pnol_host_scalar_fn)(const double* x, int n, void* user);
 int pnol_host_fd_hessian(pnol_host_scalar_fn fn, void* user, const double* x, const double* h, int n, double* B);
 int pnol_host_fd_jacobian(pnol_host_multi_fn fn, void* user, const double* x, const double* h, int n, int m,
                           int sharded, double* J_rowmajor);
+/* GeneticAlgorithm (which 0) / GeneticAlgorithmMPI (1) findMinBnd (GeneticAlgorithm.cpp:12-297) on a C
+ * callback objective, each generation handed to objEvalBatch on the host; params / seed / res as
+ * pnol_run_ga.  Needs no device. */
+int pnol_host_run_ga(int which, pnol_host_scalar_fn fn, void* user, const double* params, int nparams,
+                     unsigned long long seed, double* X, int n, const double* Xlb, const double* Xub,
+                     pnol_result* res);
 
 #ifdef __cplusplus
 }

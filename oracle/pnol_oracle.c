@@ -1600,12 +1600,17 @@ static void ga_evaluate(orc_objective* o, double* Xp, double* F, const int* ind,
 }
 
 static int ga_select(ga_rng* r, const double* fitness, double maxFitness, int Npop) {
+    /* repair: uniform over 1..Npop-1 when no member past the best has positive fitness (all
+     * tie with the worst; the weighted draw would accept only u == 0 and loop forever) */
+    int flat = 1;
+    for (int k = 1; k < Npop; k++)
+        if (fitness[k] > 0.0) { flat = 0; break; }
     int index = 0;
     while (index == 0) {
         int k = (int)round(ga_next(r) * Npop);
         if (k > Npop - 1) k = Npop - 1;
         const double u = ga_next(r);
-        if (maxFitness == 0.0 || u <= fitness[k] / maxFitness) index = k;
+        if (flat || maxFitness == 0.0 || u <= fitness[k] / maxFitness) index = k;
     }
     return index;
 }

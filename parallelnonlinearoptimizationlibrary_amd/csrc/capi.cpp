@@ -413,13 +413,29 @@ int pnol_fd_gradient(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const doubl
     if (!obj || !x || !h || !f0 || (cnt > 0 && !g) || cnt < 0 || i0 < 0 || i0 + cnt > obj->n) return PNOL_ERR_ARG;
     // device block [x | h | g | f0] and its pinned image: x (and h, when it changed) go up in ONE
     // copy, g and f0 come down in one
-    const size_t n = (size_t)obj->n, io = 2 * n + (size_t)cnt + 1;
+    // sized by n alone (cnt <= n), so a span that changes between calls does not regrow it
+    const size_t n = (size_t)obj->n, io = 3 * n + 1;
     void* dv = nullptr;
-    PNOL_CHECK(ws_get(ctx, "fdg_io", sizeof(double) * io, &dv));
+    bool fresh = false;
+    PNOL_CHECK(ws_get(ctx, "fdg_io", sizeof(double) * io, &dv, &fresh));
+    if (fresh) ctx->fdg_h_dev = nullptr;   // the device copy of h is gone
     double* dx = (double*)dv;
     double *dh = dx + n, *dg = dx + 2 * n, *df = dg + cnt;
     double* st = (double*)pinned_stage(ctx, sizeof(double) * io);
-    if (!st) return PNOL_ERR_NOMEM;
+    if (!st) {
+        // larger than the pinned staging block: pageable copies straight from / to the caller
+        ctx->fdg_h_dev = nullptr;
+        PNOL_HIP(hipMemcpyAsync(dx, x, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
+        PNOL_HIP(hipMemcpyAsync(dh, h, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
+        {
+            ScopedTimer tm(ctx, "fd_gradient");
+            PNOL_CHECK(launch_fd_gradient(ctx, obj, dx, dh, i0, cnt, df, dg));
+        }
+        if (cnt > 0) PNOL_HIP(hipMemcpyAsync(g, dg, sizeof(double) * cnt, hipMemcpyDeviceToHost, ctx->stream));
+        PNOL_HIP(hipMemcpyAsync(f0, df, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+        PNOL_HIP(hipStreamSynchronize(ctx->stream));
+        return PNOL_OK;
+    }
     std::memcpy(st, x, sizeof(double) * n);
     // the step vector rarely changes between calls (a solver's dX): it is staged and sent only
     // when its content differs from the copy on the device (compared while it is staged)

@@ -203,7 +203,11 @@ class CallbackMulti : public MultiObjective {
 class CallbackScalar : public Objective {
   public:
     CallbackScalar(pnol_host_scalar_fn fn, void* user) : fn_(fn), user_(user) {}
-    double objEval(vector<double>& X) override { return fn_(X.data(), (int)X.size(), user_); }
+    double objEval(vector<double>& X) override {
+        evals++;
+        return fn_(X.data(), (int)X.size(), user_);
+    }
+    long evals = 0;
 
   private:
     pnol_host_scalar_fn fn_;
@@ -306,36 +310,58 @@ int pnol_run_bfgs_ex(int which, pnol_dobj* obj, int host_eval, const double* p, 
     });
 }
 
+}  // extern "C"
+
+namespace {
+// GeneticAlgorithm / GeneticAlgorithmMPI on any Objective; evals: the objective's count
+template <class Obj>
+void run_ga_on(Obj& o, int which, const double* p, unsigned long long seed, double* X, int n, const double* Xlb,
+           const double* Xub, pnol_result* res) {
+    std::vector<double> x(X, X + n), lb(Xlb, Xlb + n), ub(Xub, Xub + n);
+    double f0 = 0, fopt = 0;
+    int gens = 0;
+    if (which == 0) {
+        GeneticAlgorithm g;
+        g.setGAParams((int)p[0], (int)p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8], p[9] != 0, false);
+        g.setSeed(seed);
+        g.setObjPtr(o);
+        g.findMinBnd(x, lb, ub, f0, fopt);
+        gens = g.getGenerations();
+    } else if (which == 1) {
+        GeneticAlgorithmMPI g;
+        g.setGAParams((int)p[0], (int)p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8], p[9] != 0);
+        g.setSeed(seed);
+        g.setObjPtr(o);
+        g.findMinBnd(x, lb, ub, f0, fopt);
+        gens = g.getGenerations();
+    } else {
+        throw std::runtime_error("unknown GA variant");
+    }
+    for (int i = 0; i < n; ++i) X[i] = x[i];
+    res->iters = gens;
+    res->evals = o.evals;
+    res->f0 = f0;
+    res->fopt = fopt;
+}
+}  // namespace
+
+extern "C" {
+
 int pnol_run_ga(int which, pnol_dobj* obj, int host_eval, const double* p, int np, unsigned long long seed, double* X,
                 int n, const double* Xlb, const double* Xub, pnol_result* res) {
     if (!obj || !p || np < 10 || !X || n <= 0 || !Xlb || !Xub || !res) return PNOL_ERR_ARG;
     return guarded([&] {
         DriverScalar o(obj, host_eval != 0);
-        std::vector<double> x(X, X + n), lb(Xlb, Xlb + n), ub(Xub, Xub + n);
-        double f0 = 0, fopt = 0;
-        int gens = 0;
-        if (which == 0) {
-            GeneticAlgorithm g;
-            g.setGAParams((int)p[0], (int)p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8], p[9] != 0, false);
-            g.setSeed(seed);
-            g.setObjPtr(o);
-            g.findMinBnd(x, lb, ub, f0, fopt);
-            gens = g.getGenerations();
-        } else if (which == 1) {
-            GeneticAlgorithmMPI g;
-            g.setGAParams((int)p[0], (int)p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8], p[9] != 0);
-            g.setSeed(seed);
-            g.setObjPtr(o);
-            g.findMinBnd(x, lb, ub, f0, fopt);
-            gens = g.getGenerations();
-        } else {
-            throw std::runtime_error("unknown GA variant");
-        }
-        for (int i = 0; i < n; ++i) X[i] = x[i];
-        res->iters = gens;
-        res->evals = o.evals;
-        res->f0 = f0;
-        res->fopt = fopt;
+        run_ga_on(o, which, p, seed, X, n, Xlb, Xub, res);
+    });
+}
+
+int pnol_host_run_ga(int which, pnol_host_scalar_fn fn, void* user, const double* p, int np, unsigned long long seed,
+                     double* X, int n, const double* Xlb, const double* Xub, pnol_result* res) {
+    if (!fn || !p || np < 10 || !X || n <= 0 || !Xlb || !Xub || !res) return PNOL_ERR_ARG;
+    return guarded([&] {
+        CallbackScalar o(fn, user);
+        run_ga_on(o, which, p, seed, X, n, Xlb, Xub, res);
     });
 }
 

@@ -93,13 +93,17 @@ void eval_points(Objective* o, const vector<double>& Xs, int npts, int n, double
 
 // selection index of the crossover and mutation steps (GeneticAlgorithmMPI.cpp:134-146):
 // round(u * Npop), clamped to the population (the reference reads one past it), accepted with
-// probability fitness / maxFitness (uniform when every fitness is 0), never 0
+// probability fitness / maxFitness, never 0; uniform when no member past index 0 has positive
+// fitness (every fitness 0, or all but the best tie with the worst -- a plateau objective --
+// where the weighted draw would accept only u == 0 and never end)
 int select_member(GARandom& rng, const vector<double>& fitness, double maxFitness, int Npop) {
+    const bool flat = maxFitness == 0.0 ||
+                      std::none_of(fitness.begin() + 1, fitness.begin() + Npop, [](double f) { return f > 0.0; });
     int index = 0;
     while (index == 0) {
         const int r = std::min((int)std::round(rng.next() * Npop), Npop - 1);
         const double u = rng.next();
-        if (maxFitness == 0.0 ? true : u <= fitness[r] / maxFitness) index = r;
+        if (flat || u <= fitness[r] / maxFitness) index = r;
     }
     return index;
 }

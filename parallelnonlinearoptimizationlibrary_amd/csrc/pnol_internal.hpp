@@ -114,7 +114,9 @@ namespace pnol {
 void* pinned_stage(pnol_ctx* ctx, size_t bytes);
 
 // Returns a device scratch buffer of at least `bytes` for `key` (grows, keeps contents undefined).
-int ws_get(pnol_ctx* ctx, const char* key, size_t bytes, void** out);
+// fresh (optional): set when the buffer was (re)allocated, i.e. its contents are undefined --
+// compare this, not the pointer (hipFree + hipMalloc may return the same address)
+int ws_get(pnol_ctx* ctx, const char* key, size_t bytes, void** out, bool* fresh = nullptr);
 int ws_get_zeroed(pnol_ctx* ctx, const char* key, size_t bytes, void** out);
 
 // Scoped timer: records a start event now and a stop event at scope exit (when enabled).

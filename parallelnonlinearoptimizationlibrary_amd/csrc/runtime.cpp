@@ -15,10 +15,12 @@
 
 namespace pnol {
 
-int ws_get(pnol_ctx* ctx, const char* key, size_t bytes, void** out) {
+int ws_get(pnol_ctx* ctx, const char* key, size_t bytes, void** out, bool* fresh) {
     if (!ctx || !out) return PNOL_ERR_ARG;
     auto& slot = ctx->ws.bufs[key];
+    if (fresh) *fresh = false;
     if (slot.second < bytes) {
+        if (fresh) *fresh = true;   // new contents, even when the allocator hands back the old address
         if (slot.first) {
             PNOL_HIP(hipStreamSynchronize(ctx->stream));
             PNOL_HIP(hipFree(slot.first));
@@ -39,10 +41,9 @@ int ws_get(pnol_ctx* ctx, const char* key, size_t bytes, void** out) {
 // ws_get whose buffer reads as zero when (re)allocated (flag / counter arrays)
 int ws_get_zeroed(pnol_ctx* ctx, const char* key, size_t bytes, void** out) {
     if (!ctx || !out) return PNOL_ERR_ARG;
-    auto it = ctx->ws.bufs.find(key);
-    const void* before = it == ctx->ws.bufs.end() ? nullptr : it->second.first;
-    PNOL_CHECK(ws_get(ctx, key, bytes, out));
-    if (*out != before) PNOL_HIP(hipMemsetAsync(*out, 0, ctx->ws.bufs[key].second, ctx->stream));
+    bool fresh = false;
+    PNOL_CHECK(ws_get(ctx, key, bytes, out, &fresh));
+    if (fresh) PNOL_HIP(hipMemsetAsync(*out, 0, ctx->ws.bufs[key].second, ctx->stream));
     return PNOL_OK;
 }
 

@@ -39,14 +39,30 @@ def init_rccl(ctx, rank: int, world: int):
     return n.value
 
 
-def rccl_selfcheck(ctx, world: int):
+def rccl_selfcheck(ctx, world: int, timeout_s: float = 300.0):
     """Before an N > 1 measurement: one small LevMarqMPI run through the library's RCCL
     communicator (m-slice exchange, tree-order reduce-scatter, allgather) must give bitwise the
-    single-process LevMarq's X on every rank.  Returns (ok, reason), agreed by all ranks."""
+    single-process LevMarq's X on every rank.  Returns (ok, reason), agreed by all ranks.
+
+    A rank whose run raises may leave the others blocked inside an RCCL collective, where no
+    agreement all_reduce can reach them: such a rank exits the process (status 3) so the launcher
+    stops the job, and a watchdog exits any rank still inside the check after `timeout_s`
+    (status 124).  Only a completed run whose X differs is reported as (False, reason)."""
+    import sys
+    import threading
     import numpy as np
     import torch
     import torch.distributed as dist
     from .device import DeviceObjective, run_levmarq
+
+    def _expire():
+        print(f"[pnol_amd] RCCL self-check still running after {timeout_s:.0f} s: exiting", file=sys.stderr,
+              flush=True)
+        os._exit(124)
+
+    dog = threading.Timer(timeout_s, _expire)
+    dog.daemon = True
+    dog.start()
     ok, why = True, "ok"
     try:
         m, n = 1500, 300
@@ -56,10 +72,12 @@ def rccl_selfcheck(ctx, world: int):
         x_one, *_ = run_levmarq(obj, np.zeros(n), params, which=0)
         if not np.array_equal(x_mpi, x_one):
             ok, why = False, f"LevMarqMPI X differs from LevMarq (max |dx| {np.abs(x_mpi - x_one).max():.3e})"
-    except Exception as e:  # noqa: BLE001 -- any failure of the RCCL path means: do not measure on it
-        ok, why = False, f"{type(e).__name__}: {e}"
+    except Exception as e:  # noqa: BLE001 -- the other ranks may be stuck in a collective
+        print(f"[pnol_amd] RCCL self-check raised {type(e).__name__}: {e}; exiting", file=sys.stderr, flush=True)
+        os._exit(3)
     flag = torch.tensor([0.0 if ok else 1.0], device="cuda")
     dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    dog.cancel()
     if flag.item() != 0.0 and ok:
         ok, why = False, "the self-check failed on another rank"
     return ok, why

@@ -370,6 +370,28 @@ def test_cholesky_lookahead_equals_plain_chain(ctx, monkeypatch, n):
     assert np.array_equal(_np(s_on), _np(s4))
 
 
+def test_cholesky_bwd_granules_equal_flag_form(ctx, monkeypatch):
+    """The backward solve's granule hand-off (x_w[t] with its epoch in one 16-byte sc1 store,
+    polled by the consumers) assumes an aligned 16-byte store is seen whole.  A torn read (new
+    epoch, old x) would pass the epoch test and corrupt sigma.  Many solves of varying size,
+    back to back (epochs advancing, the granule buffer reused), each bitwise the flag form's
+    (PNOL_BWD_GRANULE=0)."""
+    rng = np.random.default_rng(1234)
+    for k in range(40):
+        n = int(rng.integers(65, 1400))
+        J = rng.standard_normal((n + 16, n))
+        A = J.T @ J + 0.5 * np.eye(n)
+        b = rng.standard_normal(n)
+        At, bt = ctx.tensor(A), ctx.tensor(b)
+        monkeypatch.setenv("PNOL_BWD_GRANULE", "0")
+        s_flag, i_flag = ctx.solve(At, bt, method=5)
+        monkeypatch.delenv("PNOL_BWD_GRANULE")
+        outs = [ctx.solve(At, bt, method=5) for _ in range(3)]
+        assert i_flag == 1 and all(i == 1 for _, i in outs)
+        for s, _ in outs:
+            assert np.array_equal(_np(s), _np(s_flag)), (k, n)
+
+
 @pytest.mark.parametrize("n", [200, 1000])
 def test_cholesky_falls_back_to_lu_on_indefinite(ctx, oracle, n):
     rng = np.random.default_rng(9)

@@ -197,6 +197,26 @@ def test_bench_multi_rank_line_is_valid(tmp_path, world):
     assert "host communicator" in line["config"]["workload"]
 
 
+def test_bench_gpus_flag_launches_ranks():
+    """`python bench.py --gpus 2` without a launcher starts its own two ranks (one process per
+    GPU; here both share the box's GPU over the host communicator) and the relayed line reports
+    the job it measured: n_gpus = communicator size = 2."""
+    import json
+    m, n = 4096, 512
+    cmd = [sys.executable, os.path.join(os.path.dirname(HERE), "bench.py"), "--gpus", "2", "--host-comm",
+           "--steps", "2", "--warmup", "1", "--residuals", str(m), "--params", str(n),
+           "--no-bfgs", "--no-hg", "--no-cpu-baseline"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr.decode(errors="replace")[-3000:]
+    lines = [l for l in r.stdout.decode().splitlines() if l.strip()]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["comm"] == {"backend": "host-gloo", "ranks": 2}
+    assert 0 < line["roofline"]["frac"] <= 1.0
+    assert line["value"] > 0
+
+
 def test_rccl_selfcheck_world1():
     """The bench's N > 1 guard (dist.rccl_selfcheck): the library's RCCL communicator (one rank on
     the box's one GPU -- RCCL refuses two ranks on one device) carries a small LevMarqMPI whose X

@@ -55,3 +55,65 @@ def test_host_fd_hessian_bitwise(oracle, factory, n):
                                          B.ctypes.data_as(dp)), "host fd hessian")
     assert np.array_equal(B, oracle.fd_hessian(obj, x, h))
     assert len(calls) == 1 + 3 * n * (n + 1) // 2
+
+
+GA_P = [40, 200, 0.1, 0.3, 0.2, 0.5, 0.01, 0.5, 20, 0]   # setGAParams without graph
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_host_ga_bitwise(oracle, which):
+    """GeneticAlgorithm / GeneticAlgorithmMPI (one rank) on a host callback objective, each
+    generation through objEvalBatch: X, f0, fOpt, generations and evaluations bitwise the
+    oracle's restatement (GeneticAlgorithm.cpp:12-297) -- no GPU needed."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    n = 4
+    obj = oracle.rosenbrock(n)
+    cb = L.HOST_SCALAR_FN(lambda x, nn, user: oracle.obj_eval(obj, np.ctypeslib.as_array(x, shape=(nn,)).copy()))
+    lb, ub, x0 = np.full(n, -2.0), np.full(n, 2.0), np.full(n, -1.0)
+    X = x0.copy()
+    p = np.array(GA_P, dtype=np.float64)
+    res = L.Result()
+    dp = C.POINTER(C.c_double)
+    L.check(L.lib().pnol_host_run_ga(which, cb, None, p.ctypes.data_as(dp), p.size, 12345, X.ctypes.data_as(dp), n,
+                                     lb.ctypes.data_as(dp), ub.ctypes.data_as(dp), C.byref(res)), "host ga")
+    Xo, reso, st = oracle.ga_findmin(oracle.rosenbrock(n), x0, lb, ub, GA_P[:9], 12345, 0)
+    assert st == 0 and np.array_equal(X, Xo)
+    assert (res.f0, res.fopt, res.iters, res.evals) == (reso.f0, reso.fopt, reso.iters, reso.evals)
+
+
+PLATEAU = r'''
+import ctypes as C, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from parallelnonlinearoptimizationlibrary_amd import _lib as L
+n = 3
+x0 = np.full(n, 0.25)
+# one better point (x0); every other point ties with the worst -- a penalty-style plateau
+cb = L.HOST_SCALAR_FN(lambda x, nn, u: 0.0 if np.array_equal(np.ctypeslib.as_array(x, shape=(nn,)), x0) else 1.0)
+lb, ub = np.full(n, -1.0), np.full(n, 1.0)
+X = x0.copy()
+p = np.array([20, 100, 0.1, 0.3, 0.2, 0.5, 0.01, 0.5, 5, 0], dtype=np.float64)
+res = L.Result()
+dp = C.POINTER(C.c_double)
+L.check(L.lib().pnol_host_run_ga(int(sys.argv[2]), cb, None, p.ctypes.data_as(dp), p.size, 99, X.ctypes.data_as(dp),
+                                 n, lb.ctypes.data_as(dp), ub.ctypes.data_as(dp), C.byref(res)), "ga")
+assert np.array_equal(X, x0) and res.fopt == 0.0, (X, res.fopt)
+print("generations", res.iters, "evals", res.evals)
+'''
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_host_ga_plateau_terminates(tmp_path, which):
+    """A plateau objective (one strictly better member, every other one tied with the worst) gives
+    fitness 0 to every member the weighted selection may pick; selection then falls back to
+    uniform over members 1..Npop-1 instead of waiting for a draw u == 0 (the reference's loop,
+    GeneticAlgorithmMPI.cpp:134-146).  Run in a child with a time limit: a regression hangs."""
+    import subprocess
+    import sys
+    import os
+    s = tmp_path / "plateau.py"
+    s.write_text(PLATEAU)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, str(s), root, str(which)], capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode(errors="replace")[-2000:]
+    assert b"generations" in r.stdout
