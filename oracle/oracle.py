@@ -279,12 +279,13 @@ def lm_step(J, F, lam):  # LevenbergMarquardt.cpp:59-83
     return JTJ, A, rhs, sigma
 
 
-def bfgs_findmin(o: Obj, x0, params, trace_cap=0):  # BFGS::findMin
+def bfgs_findmin(o: Obj, x0, params, trace_cap=0, rank2=False):  # BFGS::findMin
+    """rank2: updateHessianInv in the O(n^2) rank-2 form (large n)."""
     X = np.array(x0, dtype=np.float64)
     prm = BFGSParams(*params)
     res = Result()
     tr = np.zeros((max(trace_cap, 1), len(X)))
-    lib().orc_bfgs_findmin(o.ref(), C.byref(prm), ptr(X), len(X), C.byref(res), ptr(tr), trace_cap)
+    lib().orc_bfgs_findmin_ex(o.ref(), C.byref(prm), ptr(X), len(X), C.byref(res), ptr(tr), trace_cap, int(rank2))
     return X, res, tr[: min(res.iters, trace_cap)]
 
 
@@ -306,6 +307,35 @@ def lm_findmin(o: Obj, x0, params, trace_cap=0):  # LevMarq::findMin
     lib().orc_lm_findmin(o.ref(), C.byref(prm), ptr(X), len(X), ptr(F0), ptr(FOpt), m, C.byref(res),
                          ptr(tr), trace_cap)
     return X, res, F0, FOpt, tr[: min(res.iters + 1, trace_cap)]
+
+
+_par = None
+
+
+def lm_findmin_par(o: Obj, x0, params, trace_cap=0, threads=None):
+    """LevMarq::findMin as lm_findmin, its FD columns, J^T J tiles and J^T F rows spread over
+    OpenMP threads (pnol_oracle_par.c, liboracle_par.so): bitwise lm_findmin's results, plus X,
+    chi^2 and lambda after every trip.  Returns (X, res, F0, FOpt, trace_x, trace_chi, trace_lambda)."""
+    global _par
+    if threads:
+        os.environ["OMP_NUM_THREADS"] = str(threads)
+    if _par is None:
+        path = os.path.join(HERE, "liboracle_par.so")
+        if not os.path.exists(path):
+            build()
+        _par = C.CDLL(path)
+    X = np.array(x0, dtype=np.float64)
+    m = o.s.m
+    F0 = np.zeros(m); FOpt = np.zeros(m)
+    prm = LMParams(*params)
+    res = Result()
+    cap = max(trace_cap, 1)
+    tx, tc, tl = np.zeros((cap, len(X))), np.zeros(cap), np.zeros(cap)
+    rc = _par.orc_lm_findmin_par(o.ref(), C.byref(prm), ptr(X), len(X), ptr(F0), ptr(FOpt), m, C.byref(res),
+                                 ptr(tx), ptr(tc), ptr(tl), trace_cap)
+    assert rc == 0
+    k = min(res.iters + 1, trace_cap)
+    return X, res, F0, FOpt, tx[:k], tc[:k], tl[:k]
 
 
 def bfgs_bnd_findmin(o: Obj, x0, lb, ub, params):  # BFGS_Bnd::findMinBnd

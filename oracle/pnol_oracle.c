@@ -466,6 +466,13 @@ static void set_identity(double* D, int n) {
 /* BFGS::findMin, BFGS_with_linesearch.cpp:12-139 */
 int orc_bfgs_findmin(orc_objective* o, const orc_bfgs_params* prm, double* X, int n, orc_result* res,
                      double* trace, int trace_cap) {
+    return orc_bfgs_findmin_ex(o, prm, X, n, res, trace, trace_cap, 0);
+}
+
+/* rank2 = 1: updateHessianInv in its O(n^2) rank-2 form (orc_update_hessian_inv_rank2), so the
+ * large-n configs (cfg 2, n = 4096) run in seconds; everything else as orc_bfgs_findmin */
+int orc_bfgs_findmin_ex(orc_objective* o, const orc_bfgs_params* prm, double* X, int n, orc_result* res,
+                        double* trace, int trace_cap, int rank2) {
     int maxIter = (int)prm->maxIter; /* int member set from a double (hpp:62,72) */
     double* D = (double*)malloc(sizeof(double) * (size_t)n * n);
     double* dX = (double*)malloc(sizeof(double) * (size_t)n);
@@ -504,7 +511,8 @@ int orc_bfgs_findmin(orc_objective* o, const orc_bfgs_params* prm, double* X, in
         F = Fopt;
         orc_fd_gradient(o, X, dX, g, n);
         for (int i = 0; i < n; ++i) { s[i] = alpha * p[i]; y[i] = g[i] - gprev[i]; }
-        orc_update_hessian_inv(D, y, s, n);
+        if (rank2) orc_update_hessian_inv_rank2(D, y, s, n);
+        else orc_update_hessian_inv(D, y, s, n);
         xdiff = 0;
         for (int i = 0; i < n; ++i) xdiff += fabs(X[i] - Xprev[i]);
         gnorm = orc_util_norm2(g, n);

@@ -90,6 +90,8 @@ typedef struct {
 /* BFGS::findMin, BFGS_with_linesearch.cpp:12-139 ; trace (optional) gets X after every iteration */
 int orc_bfgs_findmin(orc_objective* o, const orc_bfgs_params* prm, double* X, int n, orc_result* res,
                      double* trace, int trace_cap);
+int orc_bfgs_findmin_ex(orc_objective* o, const orc_bfgs_params* prm, double* X, int n, orc_result* res,
+                        double* trace, int trace_cap, int rank2);   /* rank2: O(n^2) update form */
 
 typedef struct {   /* BFGS_MPI::setParams, BFGS_with_linesearch_MPI.hpp:64 */
     double c1, c2, maxAlphaMult, alphaGuess; int maxIterLineSearch;
@@ -105,6 +107,10 @@ typedef struct {   /* LevMarq::setParams, LevenbergMarquardt.hpp:41 */
 /* LevMarq::findMin, LevenbergMarquardt.cpp:11-167 (LevMarqMPI is identical up to the FD sharding) */
 int orc_lm_findmin(orc_objective* o, const orc_lm_params* prm, double* X, int n, double* F0, double* FOpt,
                    int m, orc_result* res, double* trace, int trace_cap);
+/* orc_lm_findmin with its independent work over OpenMP threads (pnol_oracle_par.c, liboracle_par.so
+ * only): bitwise the same results; X / chiSq / lambda recorded after every trip */
+int orc_lm_findmin_par(orc_objective* o, const orc_lm_params* prm, double* X, int n, double* F0, double* FOpt, int m,
+                       orc_result* res, double* trace_x, double* trace_chi, double* trace_lambda, int trace_cap);
 /* one LM loop trip's linear algebra, LevenbergMarquardt.cpp:55-83: J -> JTJ, A, rhs, sigma */
 int orc_lm_step(const double* J, const double* F, double lambda, int m, int n,
                 double* JTJ, double* A, double* rhs, double* sigma);

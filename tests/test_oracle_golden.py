@@ -250,3 +250,18 @@ def test_ga_oracle_properties(oracle):
                                   [10, 5, 0.5, 0.3, 0.3, 0.5, 0.01, 0.5, 5], 1)
     assert bad == -1   # fractions leave no random members (the reference exits)
 
+
+
+@pytest.mark.parametrize("m,n,iters,lam0", [(300, 70, 5, 0.001), (700, 300, 4, 1e3), (37, 9, 6, 0.5)])
+def test_lm_par_oracle_equals_sequential(oracle, m, n, iters, lam0):
+    """The threaded composition of the oracle's LM (pnol_oracle_par.c: FD columns, J^T J tiles and
+    J^T F rows over OpenMP threads), which makes the full-size cfg-3 golden trips, forms every
+    value with the oracle's operations in its order: X, F0, FOpt, chi^2 and evaluations are
+    bitwise orc_lm_findmin's, trip by trip, through accepted and rejected steps."""
+    params = (lam0, 10.0, 1e-7, iters, 0.0, -1)
+    Xs, rs, F0s, FOs, trs = oracle.lm_findmin(oracle.linres(m, n), np.zeros(n), params, trace_cap=iters)
+    Xp, rp, F0p, FOp, tx, tc, tl = oracle.lm_findmin_par(oracle.linres(m, n), np.zeros(n), params,
+                                                         trace_cap=iters, threads=4)
+    assert np.array_equal(Xs, Xp) and np.array_equal(F0s, F0p) and np.array_equal(FOs, FOp)
+    assert (rs.f0, rs.fopt, rs.iters, rs.evals) == (rp.f0, rp.fopt, rp.iters, rp.evals)
+    assert np.array_equal(trs, tx)
