@@ -251,18 +251,30 @@ def bench_bfgs_solve(ctx, which, n, bscale, params, bounds=None):
     return blk
 
 
+def _median_time(fn, reps):
+    """Median wall time of `reps` calls of fn() (and every sample, for the spread)."""
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), ts
+
+
 def cpu_baseline(m, n, budget_s=20.0):
     """The reference path on the host cores: the oracle (the CPU restatement of the reference,
     loop for loop) built -O3 -march=x86-64-v3 -ffp-contract=off (liboracle_fast.so), timed on a
-    bounded sample of one LM loop trip at (m, n) and extrapolated to the whole trip:
+    bounded sample of one LM loop trip at (m, n) and extrapolated to the whole trip.  Every leg
+    is the median of >= 3 timings (the samples are reported beside it):
       - residual evaluations (the n + 2 of a trip), 1 thread and P threads -- the reference's
         MPI FD sharding (PNOL_Objective.cpp:202-299) as P concurrent evaluators;
       - rows of J^T J with the reference's matrixMultiply, 1 and P threads;
       - the reference LU (luSolve) at n = 1024, scaled by (n / 1024)^3.
     value = LM trips per second with P threads (P = the host cores this process may use, at
-    most 16, the box's per-GPU CPU share).  Also the BFGS kernels' CPU counterparts: p = -D g at
-    n = 8192 (GB/s), the rank-2 update at n = 4096 and the reference's O(n^3) update form at
-    n = 512 (extrapolated by n^3 to 4096)."""
+    most 16, the box's per-GPU CPU share).  Also, single-threaded: cfg 1 (BFGS on the 2-D
+    Rosenbrock, the whole solve), cfg 2 (BFGS at n = 4096: whole solve with the rank-2 update
+    form, and per iteration with the reference's O(n^3) update extrapolated from n = 512), and
+    the BFGS kernels' CPU counterparts (p = -D g at n = 8192, the rank-2 update at n = 4096)."""
     from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -272,59 +284,74 @@ def cpu_baseline(m, n, budget_s=20.0):
     A, xs, y = O.linres_data(m, n)
     o = O.Obj(O.LINRES, n, m, A, y)
     x = np.zeros(n)
-    t0 = time.perf_counter(); k_eval = 0
-    while k_eval < 4 or (time.perf_counter() - t0 < budget_s * 0.15 and k_eval < 32):
-        O.obj_eval_multi(o, x); k_eval += 1
-    t_eval = (time.perf_counter() - t0) / k_eval
-    # P concurrent evaluators (ctypes releases the GIL inside the C call)
+    O.obj_eval_multi(o, x)                                                  # warm
+    t_eval, s_eval = _median_time(lambda: O.obj_eval_multi(o, x), 5)
+    # P concurrent evaluators (ctypes releases the GIL inside the C call): per evaluation, amortised
     objs = [O.Obj(O.LINRES, n, m, A, y) for _ in range(P)]
     with ThreadPoolExecutor(P) as ex:
         list(ex.map(lambda q: O.obj_eval_multi(objs[q], x), range(P)))   # warm
-        t0 = time.perf_counter()
-        list(ex.map(lambda q: O.obj_eval_multi(objs[q % P], x), range(2 * P)))
-        t_eval_par = (time.perf_counter() - t0) / (2 * P)                  # per evaluation, amortised
+        t_ep, s_ep = _median_time(lambda: list(ex.map(lambda q: O.obj_eval_multi(objs[q % P], x), range(2 * P))), 3)
+        t_eval_par = t_ep / (2 * P)
     J = np.ascontiguousarray(A)                    # any m x n data: cost is data-independent
     JT = np.ascontiguousarray(J.T)
-    t0 = time.perf_counter(); k_rows = 0
-    while k_rows < 2 or (time.perf_counter() - t0 < budget_s * 0.15 and k_rows < 32):
-        O.matmul(JT[k_rows:k_rows + 1], J); k_rows += 1
-    t_row = (time.perf_counter() - t0) / k_rows
+    t_row, s_row = _median_time(lambda: O.matmul(JT[0:1], J), 3)
     with ThreadPoolExecutor(P) as ex:
-        t0 = time.perf_counter()
-        list(ex.map(lambda q: O.matmul(JT[q:q + 1], J), range(P)))
-        t_row_par = (time.perf_counter() - t0) / P
+        t_rp, s_rp = _median_time(lambda: list(ex.map(lambda q: O.matmul(JT[q:q + 1], J), range(P))), 3)
+        t_row_par = t_rp / P
     nl = min(n, 1024)
     Al = JT[:nl, :nl] @ JT[:nl, :nl].T + np.eye(nl)
-    t0 = time.perf_counter(); O.lusolve(Al, np.ones(nl)); t_lu = (time.perf_counter() - t0) * (n / nl) ** 3
+    t_lu_s, s_lu = _median_time(lambda: O.lusolve(Al, np.ones(nl)), 3)
+    t_lu = t_lu_s * (n / nl) ** 3
     t_trip1 = t_eval * (n + 2) + t_row * n + t_lu
     t_tripP = t_eval_par * (n + 2) + t_row_par * n + t_lu
+    # cfg 1: the whole BFGS solve on the 2-D Rosenbrock (the reference's CPU example)
+    g1 = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_survey.json")))["bfgs_rosenbrock2_m12_1"]
+    t_cfg1, _ = _median_time(lambda: O.bfgs_findmin(O.rosenbrock(2), g1["x0"], g1["params"]), 5)
+    # cfg 2: BFGS n = 4096 (the bench's own parameters): whole solve with the rank-2 update form
+    dd, bb = O.quadratic_data(4096)
+    runs = []
+
+    def cfg2():
+        runs.append(O.bfgs_findmin(O.Obj(O.QUADRATIC, 4096, 0, dd, bb), np.zeros(4096), CFG2_P, rank2=True))
+    t_cfg2, s_cfg2 = _median_time(cfg2, 3)
+    it2 = max(runs[-1][1].iters, 1)
     # BFGS counterparts (single thread, the reference's sequential loops)
     rng = np.random.default_rng(0)
     nh = 8192
     D = rng.standard_normal((nh, nh)); g = rng.standard_normal(nh)
-    t0 = time.perf_counter(); O.matvec(D, g); t_hg = time.perf_counter() - t0
+    t_hg, s_hg = _median_time(lambda: O.matvec(D, g), 3)
     del D
     nu = 4096
     D = np.eye(nu) + 1e-3 * rng.standard_normal((nu, nu)); yv = rng.standard_normal(nu); sv = yv + 0.1
-    t0 = time.perf_counter(); O.update_hessian_inv_rank2(D, yv, sv); t_r2 = time.perf_counter() - t0
+    t_r2, s_r2 = _median_time(lambda: O.update_hessian_inv_rank2(D, yv, sv), 3)
     del D
     n3 = 512
     D = np.eye(n3); y3 = rng.standard_normal(n3); s3 = y3 + 0.1
-    t0 = time.perf_counter(); O.update_hessian_inv(D, y3, s3); t_n3 = time.perf_counter() - t0
+    t_n3, s_n3 = _median_time(lambda: O.update_hessian_inv(D, y3, s3), 3)
+    scale3 = (4096 / n3) ** 3
+    ref_iter = t_cfg2 / it2 - t_r2 + t_n3 * scale3
     return {
         "value": 1.0 / t_tripP, "unit": "LM iters/sec", "cores": P, "kind": "port",
-        "sample": (f"oracle (C restatement, gcc -O3 -march=x86-64-v3 -ffp-contract=off) at m={m}, n={n}: "
-                   f"{k_eval} residual evals on 1 thread ({t_eval*1e3:.1f} ms each) and {2 * P} on {P} threads "
-                   f"({t_eval_par*1e3:.1f} ms each amortised), x{n + 2} per trip; {k_rows} rows of J^T J on 1 thread "
-                   f"({t_row*1e3:.1f} ms each) and {P} on {P} threads ({t_row_par*1e3:.1f} ms each amortised), x{n}; "
-                   f"LU at n={nl} scaled by (n/{nl})^3 ({t_lu:.1f} s); extrapolated {t_tripP:.1f} s per LM trip on "
-                   f"{P} threads, {t_trip1:.1f} s on 1"),
+        "sample": (f"oracle (C restatement, gcc -O3 -march=x86-64-v3 -ffp-contract=off) at m={m}, n={n}, medians of "
+                   f"timings: residual eval {t_eval*1e3:.1f} ms on 1 thread, {t_eval_par*1e3:.1f} ms amortised over "
+                   f"{P} threads, x{n + 2} per trip; a J^T J row (reference matrixMultiply) {t_row*1e3:.1f} ms on 1 "
+                   f"thread, {t_row_par*1e3:.1f} ms amortised over {P}, x{n}; LU at n={nl} {t_lu_s:.2f} s scaled by "
+                   f"(n/{nl})^3; extrapolated {t_tripP:.1f} s per LM trip on {P} threads, {t_trip1:.1f} s on 1"),
         "seconds_per_trip": t_tripP, "seconds_per_trip_1_thread": t_trip1, "iters_per_s_1_thread": 1.0 / t_trip1,
         "threads": P,
+        "samples_s": {"eval_1t": s_eval, "eval_Pt_2P_evals": s_ep, "jtj_row_1t": s_row, "jtj_rows_Pt_P_rows": s_rp,
+                      "lu_n1024": s_lu},
+        "cfg1_bfgs_rosenbrock2_solve_s": t_cfg1,
+        "cfg2_bfgs_n4096": {"solve_s_rank2_update": t_cfg2, "solve_samples_s": s_cfg2, "iterations": it2,
+                            "s_per_iteration_rank2_update": t_cfg2 / it2,
+                            "s_per_iteration_reference_update_extrapolated": ref_iter,
+                            "note": "reference O(n^3) updateHessianInv per iteration = its n=512 time x (4096/512)^3"},
         "bfgs_cpu_1_thread": {
-            "hg_n8192_s": t_hg, "hg_n8192_GBps": 8.0 * nh * nh / t_hg / 1e9,
-            "rank2_update_n4096_s": t_r2,
-            "reference_update_n512_s": t_n3, "reference_update_n4096_s_extrapolated": t_n3 * (4096 / n3) ** 3,
+            "hg_n8192_s": t_hg, "hg_n8192_GBps": 8.0 * nh * nh / t_hg / 1e9, "hg_samples_s": s_hg,
+            "rank2_update_n4096_s": t_r2, "rank2_samples_s": s_r2,
+            "reference_update_n512_s": t_n3, "reference_update_n512_samples_s": s_n3,
+            "reference_update_n4096_s_extrapolated": t_n3 * scale3,
+            "reference_update_n4096_s_extrapolated_range": [min(s_n3) * scale3, max(s_n3) * scale3],
         },
     }
 
@@ -461,15 +488,19 @@ def main():
     x0 = np.zeros(n)
     which = 1 if world > 1 else 0
 
+    trips = [0, 0]
+
     def run(iters):
         X = x0.copy()
         p = np.array([0.001, 10.0, 1e-7, float(iters), 0.0, -1.0])  # xMinDiff 0: every trip runs
         F0, FO = np.zeros(m), np.zeros(m)
         res = L.Result()
+        steps = (C.c_int * 2)()
         dp = C.POINTER(C.c_double)
-        L.check(L.lib().pnol_run_levmarq(which, obj.h, 0, p.ctypes.data_as(dp), X.ctypes.data_as(dp), n,
-                                         F0.ctypes.data_as(dp), FO.ctypes.data_as(dp), m, C.byref(res)),
+        L.check(L.lib().pnol_run_levmarq_ex(which, obj.h, 0, p.ctypes.data_as(dp), X.ctypes.data_as(dp), n,
+                                            F0.ctypes.data_as(dp), FO.ctypes.data_as(dp), m, C.byref(res), steps),
                 "pnol_run_levmarq")
+        trips[:] = [steps[0], steps[1]]
         return X
 
     # warmup with every per-kernel timer on: the full breakdown (untimed); the timed region
@@ -613,6 +644,8 @@ def main():
             "fd_jacobian_ms_max_over_ranks": per_max["fd_jacobian"] + per_max["fd_ckpt_per_step"] + (
                 per_max["exchange_J"] if per_max["exchange_J"] > 0 else per_max["allgather"]),
             "converged_rel_err_vs_xstar": err,
+            # the timed trips' outcomes: every trip recomputes J, J^T J and the solve either way
+            "trips_accepted": trips[0], "trips_rejected": trips[1],
             "bfgs_hg": hg, "bfgs_hg_n4096": hg4096 if hg else None, "bfgs_hg_n16384": hg16384 if hg else None,
             "bfgs_hg_row_sharded": hg_sharded,
             "bfgs_cfg2_solve": bfgs2, "bfgs_bnd_cfg5_solve": bnd5,

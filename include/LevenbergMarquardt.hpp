@@ -24,6 +24,7 @@ class LevMarq : public MultiAlgorithm {
     int maxIter;
     double lambdaFactor;   // > 1
     int verbose;
+    int stepCounts[2] = {0, 0};   // accepted, rejected loop trips of the last findMin
 
   public:
     void findMin(vector<double>& X, vector<double>& f0, vector<double>& fOpt);
@@ -33,6 +34,9 @@ class LevMarq : public MultiAlgorithm {
         maxIter = (int)maxIterIn; xMinDiff = xMinDiffIn; verbose = verboseIn; dXGrad = dXGradIn;
         lambda0 = lambda0In; lambdaFactor = lambdaFactorIn;
     }
+    // additive: how many loop trips of the last findMin were accepted / rejected steps
+    int getAcceptedSteps() const { return stepCounts[0]; }
+    int getRejectedSteps() const { return stepCounts[1]; }
 
     LevMarq() : lambda0(0.001), dXGrad(1e-7), xMinDiff(1e-7), maxIter(10000), lambdaFactor(10), verbose(1) {}
     ~LevMarq() {}

@@ -320,6 +320,9 @@ int pnol_run_ga(int which, pnol_dobj* obj, int host_eval, const double* params, 
 /* which: 0 = LevMarq, 1 = LevMarqMPI (6 params). F0/FOpt host arrays of m. */
 int pnol_run_levmarq(int which, pnol_dobj* obj, int host_eval, const double* params, double* X, int n,
                      double* F0, double* FOpt, int m, pnol_result* res);
+/* pnol_run_levmarq + steps[2] = accepted / rejected loop trips (LevMarq::getAcceptedSteps) */
+int pnol_run_levmarq_ex(int which, pnol_dobj* obj, int host_eval, const double* params, double* X, int n,
+                        double* F0, double* FOpt, int m, pnol_result* res, int* steps);
 /* Host-objective FD through the C++ MultiObjective with a C callback objective
  * (gradientApproximation / gradientApproximationMPI on the active communicator). */
 typedef void (*pnol_host_multi_fn)(const double* x, int n, double* F, int m, void* user);

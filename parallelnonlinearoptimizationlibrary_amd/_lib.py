@@ -118,6 +118,7 @@ _SIGS = {
     "pnol_run_bfgs_ex": (_i, [_i, _vp, _i, _dp, _i, _dp, _i, _dp, _dp, C.POINTER(Result), _dp, _i, C.POINTER(_i),
                               _dp]),
     "pnol_run_levmarq": (_i, [_i, _vp, _i, _dp, _dp, _i, _dp, _dp, _i, C.POINTER(Result)]),
+    "pnol_run_levmarq_ex": (_i, [_i, _vp, _i, _dp, _dp, _i, _dp, _dp, _i, C.POINTER(Result), C.POINTER(_i)]),
     "pnol_run_ga": (_i, [_i, _vp, _i, _dp, _i, C.c_ulonglong, _dp, _i, _dp, _dp, C.POINTER(Result)]),
     "pnol_host_fd_hessian": (_i, [HOST_SCALAR_FN, _vp, _dp, _dp, _i, _dp]),
     "pnol_host_fd_jacobian": (_i, [HOST_MULTI_FN, _vp, _dp, _dp, _i, _i, _i, _dp]),

@@ -367,6 +367,11 @@ int pnol_host_run_ga(int which, pnol_host_scalar_fn fn, void* user, const double
 
 int pnol_run_levmarq(int which, pnol_dobj* obj, int host_eval, const double* p, double* X, int n, double* F0,
                      double* FOpt, int m, pnol_result* res) {
+    return pnol_run_levmarq_ex(which, obj, host_eval, p, X, n, F0, FOpt, m, res, nullptr);
+}
+
+int pnol_run_levmarq_ex(int which, pnol_dobj* obj, int host_eval, const double* p, double* X, int n, double* F0,
+                        double* FOpt, int m, pnol_result* res, int* steps) {
     if (!obj || !p || !X || !F0 || !FOpt || n <= 0 || m <= 0 || !res) return PNOL_ERR_ARG;
     return guarded([&] {
         DriverMulti o(obj, host_eval != 0);
@@ -376,11 +381,13 @@ int pnol_run_levmarq(int which, pnol_dobj* obj, int host_eval, const double* p, 
             lm.setParams(p[0], p[1], p[2], p[3], p[4], (int)p[5]);
             lm.setObjPtr(o);
             lm.findMin(x, f0, fopt);
+            if (steps) { steps[0] = lm.getAcceptedSteps(); steps[1] = lm.getRejectedSteps(); }
         } else {
             LevMarqMPI lm;
             lm.setParams(p[0], p[1], p[2], p[3], p[4], (int)p[5]);
             lm.setObjPtr(o);
             lm.findMin(x, f0, fopt);
+            if (steps) { steps[0] = lm.getAcceptedSteps(); steps[1] = lm.getRejectedSteps(); }
         }
         for (int i = 0; i < n; ++i) X[i] = x[i];
         for (int i = 0; i < m; ++i) { F0[i] = f0[i]; FOpt[i] = fopt[i]; }

@@ -21,6 +21,7 @@ namespace {
 struct LMParams {
     double lambda0, lambdaFactor, dXGrad, xMinDiff;
     int maxIter, verbose;
+    int* steps;   // optional: [accepted, rejected] loop trips (LevMarq::getStepCounts)
 };
 
 double norm2(const std::vector<double>& v) { return std::sqrt(seq_dot(v, v)); }
@@ -331,10 +332,12 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool s
                           << ",  increasing lambda: " << lambda / P.lambdaFactor << " --> " << lambda << std::endl;
             chiSq = chiSqPrev;
             lambda = lambda * P.lambdaFactor;
+            if (P.steps) P.steps[1]++;
             ckpt = true;               // x_[s], F_[s] stand, and so do x_[s]'s checkpoints (the
                                        // trial point's went to the other slot)
         } else {
             lambda = lambda / P.lambdaFactor;
+            if (P.steps) P.steps[0]++;
             for (int i = 0; i < n; ++i) X[i] = X[i] + sig_h[i];   // == x_[s^1] (same IEEE add)
             s ^= 1;
             ckpt = true;
@@ -408,8 +411,10 @@ void lm_solve(MultiObjective* obj, const LMParams& P, bool sharded, std::vector<
             F = Fprev;
             dev.restoreF();
             lambda = lambda * P.lambdaFactor;
+            if (P.steps) P.steps[1]++;
         } else {
             lambda = lambda / P.lambdaFactor;
+            if (P.steps) P.steps[0]++;
             xdiff2Norm = norm2(sigma);
             if (xdiff2Norm < P.xMinDiff) break;
         }
@@ -435,11 +440,13 @@ void lm_solve(MultiObjective* obj, const LMParams& P, bool sharded, std::vector<
 }  // namespace
 
 void LevMarq::findMin(vector<double>& X, vector<double>& F0, vector<double>& FOpt) {
-    LMParams P{lambda0, lambdaFactor, dXGrad, xMinDiff, maxIter, verbose};
+    stepCounts[0] = stepCounts[1] = 0;
+    LMParams P{lambda0, lambdaFactor, dXGrad, xMinDiff, maxIter, verbose, stepCounts};
     lm_solve(mObjPtr, P, false, X, F0, FOpt);
 }
 
 void LevMarqMPI::findMin(vector<double>& X, vector<double>& F0, vector<double>& FOpt) {
-    LMParams P{lambda0, lambdaFactor, dXGrad, xMinDiff, maxIter, verbose};
+    stepCounts[0] = stepCounts[1] = 0;
+    LMParams P{lambda0, lambdaFactor, dXGrad, xMinDiff, maxIter, verbose, stepCounts};
     lm_solve(mObjPtr, P, true, X, F0, FOpt);
 }
