@@ -14,6 +14,7 @@
 #include <cstring>
 
 #include "../pnol_comm.hpp"
+#include "../pnol_internal.hpp"
 #include "PNOL_Objective.hpp"
 #include "device_util.hpp"
 
@@ -91,6 +92,20 @@ void host_points_recur(Objective* o, const std::vector<double>& X, const std::ve
         row[map[i]] = X[i] + dX[i];
     }, out);
 }
+
+// the last device Recur gradient: its full point, steps, per-coordinate values and F(x)
+struct RecurCache {
+    unsigned long long oid = 0;   // pnol_dobj::id (never reused)
+    std::vector<double> Xf, hf, gf, pts, fv;
+    std::vector<int> redo;
+    double F = 0.0;
+};
+RecurCache& recur_cache() {
+    thread_local RecurCache c;
+    return c;
+}
+// above this many changed steps the whole gradient goes to the device again
+constexpr size_t kRecurRedoMax = 32;
 
 // what the reference's zero-padded MPI_Allreduce(SUM) returns for a value one rank owns:
 // v + 0.0 + ... + 0.0 = v, except -0.0 -> +0.0 (PNOL_Objective.cpp:147-148, 279-286); one rank: v
@@ -225,9 +240,59 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
             hf[i] = c ? 1.0 : hr;
             ir += !c;
         }
-        double F = 0;
-        device_gradient(d, Xf, hf, 0, (int)nf, &F, gf.data());
-        countEvals(N + 1);
+        // Same-point reuse: the bounded solvers' recursion unwinds through one level per frozen
+        // coordinate, and every level asks for the gradient at the SAME full point (its free
+        // coordinates are a superset of the level below's; BFGS_bnd_linesearch.cpp:620-650).
+        // Every value f(x + h_i e_i) is a pure function of the full point and h_i, so a value
+        // computed for the same full point and the same h_i by the previous call is the one this
+        // call would compute, bit for bit; only coordinates whose step changed (those that were
+        // frozen, with the dummy step, in the previous call) are evaluated, on the host by the
+        // objective's own formula (objEvalBatch: the device kernel's bits).  Built-in scalar
+        // device objectives only (pure); the evaluation count is the reference's N + 1.
+        RecurCache& rc = recur_cache();
+        const bool pure = d->kind == PNOL_OBJ_ROSENBROCK || d->kind == PNOL_OBJ_POWER || d->kind == PNOL_OBJ_QUADRATIC;
+        std::vector<int>& redo = rc.redo;
+        redo.clear();
+        bool reuse = pure && rc.oid == d->id && rc.Xf.size() == nf &&
+                     std::memcmp(rc.Xf.data(), Xf.data(), sizeof(double) * nf) == 0;
+        if (reuse) {
+            for (size_t i = 0; i < nf && redo.size() <= kRecurRedoMax; ++i)
+                if (!constantIndicator[i] && std::memcmp(&rc.hf[i], &hf[i], sizeof(double)) != 0) redo.push_back((int)i);
+            reuse = redo.size() <= kRecurRedoMax;
+        }
+        if (reuse) {
+            const int k = (int)redo.size();
+            if (k > 0) {
+                std::vector<double>& pts = rc.pts;
+                pts.resize((size_t)k * nf);
+                for (int q = 0; q < k; ++q) {
+                    double* row = pts.data() + (size_t)q * nf;
+                    std::memcpy(row, Xf.data(), sizeof(double) * nf);
+                    const int i = redo[q];
+                    row[i] = Xf[i] + hf[i];
+                }
+                rc.fv.resize(k);
+                objEvalBatch(pts.data(), k, (int)nf, rc.fv.data());   // counts its k points
+                for (int q = 0; q < k; ++q) {
+                    const int i = redo[q];
+                    rc.gf[i] = (rc.fv[q] - rc.F) / hf[i];
+                    rc.hf[i] = hf[i];
+                }
+            }
+            countEvals(N + 1 - k);
+            gf.assign(rc.gf.begin(), rc.gf.end());
+        } else {
+            double F = 0;
+            device_gradient(d, Xf, hf, 0, (int)nf, &F, gf.data());
+            countEvals(N + 1);
+            if (pure) {
+                rc.oid = d->id;
+                rc.Xf = Xf;
+                rc.hf = hf;
+                rc.gf = gf;
+                rc.F = F;
+            }
+        }
         ir = 0;
         for (size_t i = 0; i < nf; ++i) {
             gr[ir] = gf[i];

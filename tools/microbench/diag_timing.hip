@@ -10,7 +10,7 @@
 #include <vector>
 
 namespace pnol {
-int ws_get(pnol_ctx*, const char*, size_t, void**) { return PNOL_ERR_ARG; }   // unused here
+int ws_get(pnol_ctx*, const char*, size_t, void**, bool*) { return PNOL_ERR_ARG; }   // unused here
 }
 
 __global__ __launch_bounds__(256, 2) void k_diag_time(const double* A, double* W, int* info, long long* st) {
