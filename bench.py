@@ -457,6 +457,10 @@ def main():
                                 device_id=torch.device("cuda", local))
 
     m, n = args.residuals, args.params
+    # LevMarqMPI's Jacobian decomposition (csrc/kernels/fd.hip launch_lm_jacobian): rows mode by
+    # default (every FD column on the rank's own m-slices, no J exchange); PNOL_LM_FD=columns:
+    # cost-balanced FD column tiles + the m-slice exchange
+    rows_mode = os.environ.get("PNOL_LM_FD", "") != "columns"
     ctx = Context(local)
     # the C++ drop-in classes run on the process default context: bind its timers
     dctx = C.c_void_p()
@@ -507,7 +511,7 @@ def main():
     # keeps only the timers of the kernels priced below (each timer adds two event records
     # between launches, ~1.5% of a trip with all of them on)
     names = ("fd_jtj", "fd_jacobian", "fd_ckpt", "linres_eval", "syrk", "syrk_rows", "syrk_reduce", "jtr", "solve",
-             "allgather", "exchange_J", "exchange_A")
+             "allgather", "exchange_J", "exchange_A", "exchange_F")
     L.check(L.lib().pnol_ctx_enable_timers(dctx, 0 if args.no_timers else 1), "timers")
     L.check(L.lib().pnol_ctx_reset_timers(dctx), "timers")
     run(args.warmup)
@@ -574,10 +578,15 @@ def main():
             jtj_rows = m
         jtj_flop = float(jtj_rows) * n * (n + 1)
         from parallelnonlinearoptimizationlibrary_amd import fd_tiles
-        my_tiles = fd_tiles(n, world, rank)                  # this rank's cost-balanced FD tiles
+        if world > 1 and rows_mode:
+            my_tiles = fd_tiles(n, 1, 0)                     # rows mode: every FD column ...
+            fd_rows = jtj_rows                               # ... on this rank's own m-slices
+        else:
+            my_tiles = fd_tiles(n, world, rank)              # this rank's cost-balanced FD tiles, all rows
+            fd_rows = m
         my_cols = sum(c for _, c in my_tiles)
-        fd_flop_nominal = 2.0 * m * n * my_cols              # full-length chains for this rank's points
-        fd_flop = fd_flop_executed(m, n, my_tiles)           # prefix-shared chains actually run
+        fd_flop_nominal = 2.0 * fd_rows * n * my_cols        # full-length chains for this rank's points
+        fd_flop = fd_flop_executed(fd_rows, n, my_tiles)     # prefix-shared chains actually run
         pmc = pmc_traffic()
         one_gpu = world == 1
         roofline = {
@@ -599,7 +608,7 @@ def main():
                             "bound": "valu_fp64", "ms": fd_ms,
                             "achieved": fd_flop / (fd_ms * 1e-3) / 1e12 if fd_ms else None,
                             "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "flop_executed": fd_flop,
-                            "flop_minimal": fd_flop_minimal(m, my_tiles, n),
+                            "flop_minimal": fd_flop_minimal(fd_rows, my_tiles, n), "rows": fd_rows,
                             "flop_nominal_full_chains": fd_flop_nominal,
                             "valu_busy_pmc": next((v.get("valu_busy_frac") for k, v in pmc_valu().items()
                                                    if "k_linres_fdP" in k), None),
@@ -632,7 +641,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (splitmix64 seed 0x5EED2018, r(x)=Ax-y generated in HBM)",
             "config": {"workload": f"LevenbergMarquardt{'MPI' if world > 1 else ''} m={m} n={n}, "
-                                   f"FD columns {'in cost-balanced tiles over ' + str(world) + ' GPUs, J rows exchanged by m-slice (' + ('host communicator over gloo: one-GPU rehearsal' if args.host_comm else ('RCCL p2p' if comm_backend == 'rccl' else comm_backend)) + '), J^T J + J^T F by m-slice + reduce-scatter/allgather' if world > 1 else 'on 1 GPU'}",
+                                   f"FD columns {((('all of them on each rank' + chr(39) + 's own m-slices of residual rows over ' + str(world) + ' GPUs (no J exchange; trial residuals shared p2p)') if rows_mode else ('in cost-balanced tiles over ' + str(world) + ' GPUs, J rows exchanged by m-slice')) + ' (' + ('host communicator over gloo: one-GPU rehearsal' if args.host_comm else ('RCCL p2p' if comm_backend == 'rccl' else comm_backend)) + '), J^T J + J^T F by m-slice + reduce-scatter/allgather') if world > 1 else 'on 1 GPU'}",
                        "m": m, "n": n, "parallelism": f"fd-columns+m-slices x{world}" if world > 1 else "single"},
             "roofline": roofline,
             "rooflines": rooflines,
@@ -641,8 +650,10 @@ def main():
             "kernel_ms_per_step_max_over_ranks": per_max,
             # the north star's strong-scaling quantity: the sharded FD Jacobian + its exchange
             # (m-slice point-to-point exchange; the column-row allgather with PNOL_LM_SLICED=0)
+            # (rows mode: no J exchange; the trial residuals' exchange is reported as exchange_F)
             "fd_jacobian_ms_max_over_ranks": per_max["fd_jacobian"] + per_max["fd_ckpt_per_step"] + (
                 per_max["exchange_J"] if per_max["exchange_J"] > 0 else per_max["allgather"]),
+            "lm_fd_mode": ("rows" if rows_mode else "columns") if world > 1 else "single",
             "converged_rel_err_vs_xstar": err,
             # the timed trips' outcomes: every trip recomputes J, J^T J and the solve either way
             "trips_accepted": trips[0], "trips_rejected": trips[1],

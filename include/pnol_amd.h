@@ -158,12 +158,19 @@ int pnol_jtj_mpi_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, doub
 #define PNOL_LM_SLICES 8
 int pnol_lm_sliced_layout(int m, int n, int* slice_rows, size_t* jt_elems);
 /* LevenbergMarquardtMPI.cpp:60 + PNOL_Objective.cpp:202-299 (gradientApproximationMPI's column
- * loop and its MPI_Allreduce): this rank's cost-balanced FD tiles (pnol_fd_tiles) for all
- * residual rows into JTs, then each m-slice of them to the rank holding that slice (one group of
- * RCCL point-to-point transfers).  Linear-residual device objectives; compute_f0 as for
- * pnol_fd_jacobian_tiles_d. */
+ * loop and its MPI_Allreduce), the J^T slices this rank's normal-equation share needs.  Rows mode
+ * (default): every FD column evaluated on this rank's own m-slices of residual rows (each row of
+ * the residual is its own chain, so these are the same bits) -- no Jacobian exchange; F0 (when
+ * computed) holds this rank's rows.  Columns mode (environment PNOL_LM_FD=columns): this rank's
+ * cost-balanced FD tiles (pnol_fd_tiles) for all residual rows, then each m-slice of them to the
+ * rank holding that slice (one group of RCCL point-to-point transfers).  Linear-residual device
+ * objectives; compute_f0 as for pnol_fd_jacobian_tiles_d. */
 int pnol_lm_jacobian_mpi_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0,
                            int compute_f0, double* JTs);
+/* The LevMarqMPI trial point F(x) (LevenbergMarquardtMPI.cpp:92) with its prefix checkpoints:
+ * rows mode: this rank's rows, then every rank's rows to all ranks (point-to-point), so F holds
+ * all m residuals everywhere; columns mode or one rank: pnol_dobj_eval_ckpt_d. */
+int pnol_lm_eval_mpi_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, double* F);
 /* LevenbergMarquardtMPI.cpp:64-80 from this rank's slices of pnol_lm_jacobian_mpi_d: A = J^T J
  * with A_ii = (1 + lambda) (J^T J)_ii and rhs = -(J^T F) on every rank.  Partial tiles of the
  * rank's slices, their tree nodes to each tile's owner (point-to-point), the owners merge, one

@@ -85,6 +85,7 @@ _SIGS = {
     "pnol_jtj_mpi_d": (_i, [_vp, _vp, _i, _i, _i, _d, _vp, _i, _vp]),
     "pnol_lm_sliced_layout": (_i, [_i, _i, C.POINTER(_i), C.POINTER(_sz)]),
     "pnol_lm_jacobian_mpi_d": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp]),
+    "pnol_lm_eval_mpi_d": (_i, [_vp, _vp, _vp, _vp]),
     "pnol_lm_normal_mpi_d": (_i, [_vp, _vp, _i, _i, _d, _vp, _vp, _i, _vp, _vp]),
     "pnol_jtr_d": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
     "pnol_solve_d": (_i, [_vp, _vp, _i, _vp, _vp, _i, _i, C.POINTER(_i)]),

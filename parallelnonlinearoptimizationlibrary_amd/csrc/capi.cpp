@@ -263,6 +263,12 @@ int pnol_lm_jacobian_mpi_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const
     return launch_lm_jacobian(ctx, obj, x, h, F0, compute_f0, JTs);
 }
 
+int pnol_lm_eval_mpi_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, double* F) {
+    PNOL_CHECK(set_device(ctx));
+    if (!obj || !x || !F) return PNOL_ERR_ARG;
+    return launch_lm_eval(ctx, obj, x, F);
+}
+
 int pnol_lm_normal_mpi_d(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F, double* A,
                          int lda, double* rhs, double* jtj_diag) {
     PNOL_CHECK(set_device(ctx));

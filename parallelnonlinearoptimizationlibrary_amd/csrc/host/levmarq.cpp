@@ -179,8 +179,10 @@ class LMDevice {
 // wasted trip, and the post-convergence steps of the bench are mostly rejections.)
 //
 // LevMarqMPI (sliced = true) runs the same loop with the Jacobian split by residual-row
-// slices: each rank evaluates its FD column tiles for all rows and sends every m-slice of them
-// to the slice's rank (pnol_lm_jacobian_mpi_d); each rank forms its slices' share of J^T J and
+// slices: each rank evaluates every FD column on its own m-slices of residual rows (rows mode;
+// PNOL_LM_FD=columns: its FD column tiles for all rows, every m-slice of them then sent to the
+// slice's rank) (pnol_lm_jacobian_mpi_d), and the trial point likewise on its own rows, shared
+// point-to-point (pnol_lm_eval_mpi_d); each rank forms its slices' share of J^T J and
 // J^T F and one reduce-scatter + allgather assemble A and -J^T F on every rank
 // (pnol_lm_normal_mpi_d).  The collectives are queued on the same stream, so the trip still
 // has one host wait; A, rhs and hence the trajectory are bitwise the single-GPU ones.
@@ -244,7 +246,9 @@ class LMAsync {
     // residuals, copies back
     void finish(int s, bool add = true) {
         if (add) check(pnol_add_d(ctx_, x_[s].get(), sig(s), x_[s ^ 1].get(), n_), "add");
-        check(pnol_dobj_eval_ckpt_d(ctx_, d_, x_[s ^ 1].get(), F(s ^ 1)), "objective eval");
+        // LevMarqMPI: each rank's rows, then all rows everywhere (rows mode)
+        if (sliced_) check(pnol_lm_eval_mpi_d(ctx_, d_, x_[s ^ 1].get(), F(s ^ 1)), "objective eval");
+        else check(pnol_dobj_eval_ckpt_d(ctx_, d_, x_[s ^ 1].get(), F(s ^ 1)), "objective eval");
         check(pnol_memcpy_d2h_async(ctx_, pin_[s], trip_[s].get(), sizeof(double) * ((size_t)np_ + mp_ + 1)), "d2h");
         check(pnol_event_record(ctx_, ev_[s]), "event");
     }

@@ -22,6 +22,7 @@
 #include "../pnol_comm.hpp"
 
 #include <algorithm>
+#include <cstring>
 #include <memory>
 #include <cstdlib>
 #include <vector>
@@ -610,8 +611,10 @@ __global__ __launch_bounds__(64) void k_linres_evalP(const double* __restrict__ 
                                                      const double* __restrict__ y, int m, int n,
                                                      double* __restrict__ F, double* __restrict__ C,
                                                      double* __restrict__ xsave = nullptr,
-                                                     const double* __restrict__ xcheck = nullptr) {
-    const int rb = blockIdx.x, row = rb * kPanel + threadIdx.x;
+                                                     const double* __restrict__ xcheck = nullptr, int rb0 = 0) {
+    // rb0: the first row panel of this launch (a row-sharded LevMarqMPI rank evaluates its
+    // m-slices only; the grid covers its panels)
+    const int rb = rb0 + blockIdx.x, row = rb * kPanel + threadIdx.x;
     if (xcheck) {
         bool diff = false;
         const unsigned long long* xa = reinterpret_cast<const unsigned long long*>(x);
@@ -619,7 +622,7 @@ __global__ __launch_bounds__(64) void k_linres_evalP(const double* __restrict__ 
         for (int k = threadIdx.x; k < n; k += 64) diff |= xa[k] != xb[k];
         if (!__any(diff)) return;   // one wave per block: uniform
     }
-    if (xsave && rb == 0)
+    if (xsave && blockIdx.x == 0)
         for (int k = threadIdx.x; k < n; k += 64) xsave[k] = x[k];
     const double* a = panel_col(AP, n, rb, 0) + threadIdx.x;
     constexpr int U = kCkpt;
@@ -670,12 +673,12 @@ __global__ __launch_bounds__(256) void k_linres_fdP(const double* __restrict__ A
                                                     const double* __restrict__ x, const double* __restrict__ h, int m,
                                                     int n, const FdTiles tl, const double* __restrict__ F0,
                                                     const double* __restrict__ C, double* __restrict__ JT, long ldjt,
-                                                    int mS, long sstride) {
+                                                    int mS, long sstride, int mt0, int nmt) {
     // Longest work first: the host sorts the tiles by first column (the chains of tile t run
     // k = ks_t .. n-1), and blockIdx walks all panels of tile 0, then of tile 1, ..., so the
     // short tiles fill the tail.  Panel mt lands on XCD mt % 8 for every tile (L2 reuse).
-    const int nmt = (m + kPanel - 1) / kPanel;
-    const int nt = blockIdx.x / nmt, mt = blockIdx.x % nmt;
+    // Panels [mt0, mt0 + nmt): the launch's rows (all of them, or a row-sharded rank's slices).
+    const int nt = blockIdx.x / nmt, mt = mt0 + blockIdx.x % nmt;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int j0 = tl.start[nt], cnt = tl.count[nt];
     const int pw0 = w * kPW;
@@ -867,9 +870,10 @@ static int ensure_panels(pnol_ctx* ctx, pnol_dobj* o) {
 // id (never reused, unlike its address) and the device x pointer, and keeps a copy of x's
 // content (written by the kernel that makes the checkpoints), so a compute_f0 = 2 caller that
 // changed x in place gets a recomputation instead of stale checkpoints.
-static int ckpt_find(pnol_ctx* ctx, const pnol_dobj* o, const double* x) {
+static int ckpt_find(pnol_ctx* ctx, const pnol_dobj* o, const double* x, int r0, int r1) {
     for (int s = 0; s < 2; ++s)
-        if (o && ctx->ckpt_oid[s] == o->id && ctx->ckpt_x[s] == x) return s;
+        if (o && ctx->ckpt_oid[s] == o->id && ctx->ckpt_x[s] == x && ctx->ckpt_r0[s] <= r0 && ctx->ckpt_r1[s] >= r1)
+            return s;
     return -1;
 }
 static int ckpt_buf(pnol_ctx* ctx, const pnol_dobj* o, int slot, void** C, void** xcopy) {
@@ -878,13 +882,16 @@ static int ckpt_buf(pnol_ctx* ctx, const pnol_dobj* o, int slot, void** C, void*
     PNOL_CHECK(ws_get(ctx, slot ? "linres_ckx1" : "linres_ckx0", sizeof(double) * (size_t)o->n, xcopy));
     return ws_get(ctx, slot ? "linres_ckpt1" : "linres_ckpt0", sizeof(double) * (size_t)o->m * (ncp > 1 ? ncp : 1), C);
 }
-// the slot the checkpoints of (o, x) are written to: its own if tagged, else the least recent;
-// tagged (o, x) (reusable false: written but never reused)
-static int ckpt_claim(pnol_ctx* ctx, const pnol_dobj* o, const double* x, bool reusable, void** C, void** xcopy) {
-    int s = ckpt_find(ctx, o, x);
+// the slot the checkpoints of (o, x) on rows [r0, r1) are written to: its own if tagged, else
+// the least recent; tagged (o, x, rows) (reusable false: written but never reused)
+static int ckpt_claim(pnol_ctx* ctx, const pnol_dobj* o, const double* x, bool reusable, void** C, void** xcopy,
+                      int r0, int r1) {
+    int s = ckpt_find(ctx, o, x, r0, r1);
     if (s < 0) s = ctx->ckpt_use[0] <= ctx->ckpt_use[1] ? 0 : 1;
     ctx->ckpt_oid[s] = reusable ? o->id : 0;
     ctx->ckpt_x[s] = x;
+    ctx->ckpt_r0[s] = r0;
+    ctx->ckpt_r1[s] = r1;
     ctx->ckpt_last = s;
     return ckpt_buf(ctx, o, s, C, xcopy);
 }
@@ -892,17 +899,22 @@ static int ckpt_claim(pnol_ctx* ctx, const pnol_dobj* o, const double* x, bool r
 // F = F(x), and for a linear residual also the prefix checkpoints of x, kept in the context
 // for the next FD call on (o, x) with compute_f0 == 2 (the LM trial point becomes the next
 // Jacobian point when the step is accepted).
-int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out) {
+int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out, int r0, int r1) {
     if (!o || !x || !out) return PNOL_ERR_ARG;
     if (o->kind != PNOL_OBJ_LINRES) return launch_dobj_eval(ctx, o, x, out);
+    if (r1 < 0) {
+        r0 = 0;
+        r1 = o->m;
+    }
+    if (r0 < 0 || r0 % kPanel || r1 > o->m || r0 > r1 || (r1 % kPanel && r1 != o->m)) return PNOL_ERR_ARG;
     PNOL_CHECK(ensure_panels(ctx, o));
     void *C = nullptr, *xc = nullptr;
-    PNOL_CHECK(ckpt_claim(ctx, o, x, true, &C, &xc));
-    {
+    PNOL_CHECK(ckpt_claim(ctx, o, x, true, &C, &xc, r0, r1));
+    const int nb = (r1 - r0 + kPanel - 1) / kPanel;
+    if (nb > 0) {
         ScopedTimer tm(ctx, "linres_eval");
-        hipLaunchKernelGGL((k_linres_evalP<true>), dim3((o->m + kPanel - 1) / kPanel), dim3(64), 0, ctx->stream,
-                           (const double*)o->at, x, o->p1, o->m, o->n, out, (double*)C, (double*)xc,
-                           (const double*)nullptr);
+        hipLaunchKernelGGL((k_linres_evalP<true>), dim3(nb), dim3(64), 0, ctx->stream, (const double*)o->at, x, o->p1,
+                           o->m, o->n, out, (double*)C, (double*)xc, (const double*)nullptr, r0 / kPanel);
     }
     return launch_check();
 }
@@ -961,8 +973,16 @@ int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
 // prefix checkpoints), then the FD GEMM over all tiles in launches of <= kFdMaxTiles tiles.
 int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, const int* start,
                              const int* count, int ntiles, double* F0, int compute_f0, double* JT, int jbase,
-                             int ldjt, int ckpt, int mS, long sstride) {
+                             int ldjt, int ckpt, int mS, long sstride, int r0, int r1) {
     const bool sliced = mS > 0;
+    const bool rows_all = r1 < 0;
+    if (!o) return PNOL_ERR_ARG;
+    if (rows_all) {
+        r0 = 0;
+        r1 = o->m;
+    }
+    if (!rows_all && (!sliced || r0 < 0 || r0 % kPanel || r1 > o->m || r0 > r1 || (r1 % kPanel && r1 != o->m)))
+        return PNOL_ERR_ARG;
     if (!o || !x || !h || !F0 || is_scalar_kind(o->kind) || ntiles < 0 || ldjt < (sliced ? mS : o->m))
         return PNOL_ERR_ARG;
     if (sliced && (o->kind != PNOL_OBJ_LINRES || mS % kPanel != 0 || sstride < (long)o->n * ldjt))
@@ -1004,23 +1024,24 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
     void *C = nullptr, *xc = nullptr;
     double* f0_out = (compute_f0 == 1 || compute_f0 == 2) ? F0 : nullptr;
     const double* xcheck = nullptr;
-    const int have = (compute_f0 >= 2 && kmajor) ? ckpt_find(ctx, o, x) : -1;
+    const int have = (compute_f0 >= 2 && kmajor) ? ckpt_find(ctx, o, x, r0, r1) : -1;
     if (have >= 0) {
         ctx->ckpt_last = have;
         PNOL_CHECK(ckpt_buf(ctx, o, have, &C, &xc));
         if (compute_f0 == 3 || !ckpt) ckpt = 0;
         else xcheck = (const double*)xc;   // verify, recompute on a mismatch
     } else if (ckpt) {
-        PNOL_CHECK(ckpt_claim(ctx, o, x, kmajor, &C, &xc));
+        PNOL_CHECK(ckpt_claim(ctx, o, x, kmajor, &C, &xc, r0, r1));
         if (compute_f0 == 3) f0_out = nullptr;
     } else {   // the caller's previous call on (o, x) wrote them (chunked FD: chunks after the first)
         PNOL_CHECK(ckpt_buf(ctx, o, ctx->ckpt_last, &C, &xc));
     }
-    if (ckpt && kmajor) {
+    const int mt0 = r0 / kPanel, nmt = (r1 - r0 + kPanel - 1) / kPanel;   // this call's row panels
+    if (ckpt && kmajor && nmt > 0) {
         LaunchTimer tm(ctx, "fd_ckpt");
-        hipExtLaunchKernelGGL((k_linres_evalP<true>), dim3((o->m + kPanel - 1) / kPanel), dim3(64), 0, ctx->stream,
-                              tm.start(), tm.stop(), 0, (const double*)o->at, x, (const double*)o->p1, o->m, o->n,
-                              f0_out, (double*)C, xcheck ? (double*)nullptr : (double*)xc, xcheck);
+        hipExtLaunchKernelGGL((k_linres_evalP<true>), dim3(nmt), dim3(64), 0, ctx->stream, tm.start(), tm.stop(), 0,
+                              (const double*)o->at, x, (const double*)o->p1, o->m, o->n, f0_out, (double*)C,
+                              xcheck ? (double*)nullptr : (double*)xc, xcheck, mt0);
     } else if (ckpt) {
         ScopedTimer tm(ctx, "fd_ckpt");
         if ((o->n % 2) == 0)
@@ -1031,6 +1052,7 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
                                ctx->stream, o->p0, x, o->p1, o->m, o->n, f0_out, (double*)C);
     }
     if (ckpt) PNOL_CHECK(launch_check());
+    if (nmt == 0) return PNOL_OK;   // a rank without rows
     const bool even = (o->n % 2) == 0;
     // the row-panel kernels carry their timer events in the dispatch (LaunchTimer); the tuning
     // variants keep a ScopedTimer
@@ -1051,7 +1073,7 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
             tl.start[t] = start[ord[t0 + t]];
             tl.count[t] = count[ord[t0 + t]];
         }
-        const dim3 g1(((o->m + 127) / 128) * tl.ntiles), g2(((o->m + 63) / 64) * tl.ntiles);
+        const dim3 g1(((o->m + 127) / 128) * tl.ntiles), g2(nmt * tl.ntiles);
         hipEvent_t ea = nullptr, eb = nullptr;
         if (lt) {
             ea = t0 == 0 ? lt->start() : nullptr;
@@ -1060,11 +1082,11 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
         if (fdk == 5 && !sliced) {
             hipExtLaunchKernelGGL((k_linres_fdP<false>), g2, dim3(256), 0, ctx->stream, ea, eb, 0, (const double*)o->at,
                                   (const double*)o->p1, x, h, o->m, o->n, tl, (const double*)F0, Cc, JT, (long)ldjt,
-                                  mS, sstride);
+                                  mS, sstride, mt0, nmt);
         } else if (fdk == 6 || kmajor) {
             hipExtLaunchKernelGGL((k_linres_fdP<true>), g2, dim3(256), 0, ctx->stream, ea, eb, 0, (const double*)o->at,
                                   (const double*)o->p1, x, h, o->m, o->n, tl, (const double*)F0, Cc, JT, (long)ldjt,
-                                  mS, sstride);
+                                  mS, sstride, mt0, nmt);
         } else if (fdk == 2) {
             if (even)
                 hipLaunchKernelGGL((k_linres_fd2<true, 8, 8>), g1, dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
@@ -1148,6 +1170,20 @@ int launch_synthetic_linres(pnol_ctx* ctx, unsigned long long seed, int m, int n
 // them to the rank that holds the slice (lm_rank_slices) -- one group of point-to-point
 // transfers, 1/P of the J^T an allgather would move.  Each rank ends with every FD column of
 // its own slices, which is all launch_lm_normal reads.
+bool lm_rows_mode() {
+    const char* e = std::getenv("PNOL_LM_FD");   // read per call: tests compare both modes
+    return !(e && std::strcmp(e, "columns") == 0);
+}
+
+// this rank's residual rows [r0, r1) in rows mode: its m-slices
+static void lm_my_rows(int m, int* r0, int* r1) {
+    const int P = comm_size(), me = comm_rank(), mS = lm_slice_rows(m);
+    int s0 = 0, s1 = 0;
+    lm_rank_slices(P, me, &s0, &s1);
+    *r0 = std::min(m, s0 * mS);
+    *r1 = std::min(m, s1 * mS);
+}
+
 int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
                        double* JTs) {
     if (!o || !JTs || o->kind != PNOL_OBJ_LINRES) return PNOL_ERR_UNSUPPORTED;
@@ -1156,6 +1192,17 @@ int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
     const int mS = lm_slice_rows(o->m);
     const long sstr = (long)n * mS;
     std::vector<int> st, ct;
+    if (lm_rows_mode()) {
+        // Every residual row of the linear residual is its own fma chain over x, so the FD
+        // column j on rows [r0, r1) is exactly the rows [r0, r1) of the whole column: each rank
+        // evaluates all n FD columns on its m-slices -- 1/P of the FD work, balanced, and the
+        // sliced J^T it needs (launch_lm_normal) is complete with no exchange.
+        int r0 = 0, r1 = 0;
+        lm_my_rows(o->m, &r0, &r1);
+        fd_tiles_of(n, 1, 0, st, ct);
+        return launch_fd_jacobian_tiles(ctx, o, x, h, st.data(), ct.data(), (int)st.size(), F0, compute_f0, JTs, 0, mS,
+                                        1, mS, sstr, r0, r1);
+    }
     fd_tiles_of(n, P, me, st, ct);
     PNOL_CHECK(launch_fd_jacobian_tiles(ctx, o, x, h, st.data(), ct.data(), (int)st.size(), F0, compute_f0, JTs, 0, mS,
                                         1, mS, sstr));
@@ -1183,6 +1230,28 @@ int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
                 bl.push_back({off, off, (size_t)r.second * mS});
             }
         }
+    });
+}
+
+// The LevMarqMPI trial point: F(x) and its checkpoints on this rank's rows, then each rank's
+// rows to every other rank (the host's chi^2 sums all m residuals on every rank).  Columns mode:
+// every rank evaluates all rows, as the one-GPU loop does.
+int launch_lm_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* F) {
+    if (!o || !x || !F) return PNOL_ERR_ARG;
+    const int P = comm_size();
+    if (P == 1 || !lm_rows_mode() || o->kind != PNOL_OBJ_LINRES) return launch_dobj_eval_ckpt(ctx, o, x, F);
+    int r0 = 0, r1 = 0;
+    lm_my_rows(o->m, &r0, &r1);
+    PNOL_CHECK(launch_dobj_eval_ckpt(ctx, o, x, F, r0, r1));
+    ScopedTimer tm(ctx, "exchange_F");
+    return comm_exchange(ctx, F, F, [&](int q, int d, std::vector<XBlock>& bl) {
+        (void)d;
+        bl.clear();
+        const int m = o->m, mS = lm_slice_rows(m);
+        int s0 = 0, s1 = 0;
+        lm_rank_slices(comm_size(), q, &s0, &s1);
+        const int a = std::min(m, s0 * mS), b = std::min(m, s1 * mS);
+        if (b > a) bl.push_back({(size_t)a, (size_t)a, (size_t)(b - a)});
     });
 }
 

@@ -52,6 +52,7 @@ struct pnol_ctx {
     // objective and the device x it was computed at; use = last-use stamp (least recent is reused)
     unsigned long long ckpt_oid[2] = {0, 0};   // pnol_dobj::id (0: untagged)
     const double* ckpt_x[2] = {nullptr, nullptr};
+    int ckpt_r0[2] = {0, 0}, ckpt_r1[2] = {0, 0};   // the residual rows the slot's checkpoints cover
     unsigned long ckpt_use[2] = {0, 0};
     unsigned long ckpt_clock = 0;
     int ckpt_last = 0;   // the slot written last
@@ -201,7 +202,8 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
                  int* info);
 
 int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
-int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
+// rows [r0, r1) only (multiples of 64 but r1 = m; r1 < 0: all): a row-sharded LevMarqMPI rank
+int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out, int r0 = 0, int r1 = -1);
 // out[k] = f(Xs row k) (scalar kinds) or out rows = F(Xs row k) (residual kinds), k < npts
 int launch_eval_batch(pnol_ctx* ctx, pnol_dobj* o, const double* Xs, int npts, double* out);
 int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt,
@@ -212,7 +214,7 @@ int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
 // stride ldjt >= mS); linear residuals on the row-panel kernels only
 int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, const int* start,
                              const int* count, int ntiles, double* F0, int compute_f0, double* JT, int jbase,
-                             int ldjt, int ckpt = 1, int mS = 0, long sstride = 0);
+                             int ldjt, int ckpt = 1, int mS = 0, long sstride = 0, int r0 = 0, int r1 = -1);
 // J^T J tiles of tile rows [row_begin, row_end) (128 x 128 tiles, split_k of the whole matrix so
 // every tile is summed exactly as by launch_jtj), partials + reduce on `stream`
 int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldjt, int m, int n, double lambda,
@@ -245,9 +247,16 @@ inline void lm_rank_slices(int P, int r, int* s0, int* s1) {
 // diagonal) and rhs = -J^T F on every rank (syrk.hip)
 int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F, double* A,
                      int lda, double* rhs, double* jtj_diag);
-// this rank's FD tiles into the sliced J^T, then each slice's rows to the slice's rank (fd.hip)
+// the sliced J^T of this rank's m-slices (fd.hip).  Rows mode (default): every FD column on
+// the rank's own residual rows -- no Jacobian exchange.  Columns mode (PNOL_LM_FD=columns): the
+// rank's cost-balanced FD tiles for every row, then each slice's rows to the slice's rank.
 int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
                        double* JTs);
+// LevMarqMPI trial point: F(x) (+ checkpoints) on this rank's rows in rows mode, then every
+// rank's rows to all ranks; columns mode: all rows on every rank (fd.hip)
+int launch_lm_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* F);
+// rows mode on (PNOL_LM_FD != columns)
+bool lm_rows_mode();
 
 // Row-tile height of the fused BFGS pass (w = D^T y partials are per row tile): 256 rows when
 // that still gives >= 512 workgroups (n >= 8192), else 128 (n = 4096: 256 workgroups instead of

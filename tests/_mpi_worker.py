@@ -39,8 +39,8 @@ def main():
     Fr = ctx.tensor(np.random.default_rng(12).standard_normal(m))
     As, rs, ds = ctx.lm_normal_mpi(JTs, m, n, 0.25, Fr, want_diag=True)
     ctx.synchronize()
-    res = dict(X=X, A=A.cpu().numpy(), diag=diag.cpu().numpy(), As=As.cpu().numpy(), rs=rs.cpu().numpy(),
-               ds=ds.cpu().numpy())
+    res = dict(X=X, F0=F0, FO=FO, A=A.cpu().numpy(), diag=diag.cpu().numpy(), As=As.cpu().numpy(),
+               rs=rs.cpu().numpy(), ds=ds.cpu().numpy())
     if lm_only:
         np.savez(os.path.join(out, f"rank{rank}.npz"), **res)
         comm.close()

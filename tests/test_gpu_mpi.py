@@ -77,6 +77,31 @@ def test_levmarq_mpi_m_sliced_more_ranks(tmp_path, world, m, n):
     _check_levmarq_and_normal(tmp_path, world, m, n)
 
 
+@pytest.mark.parametrize("mode", ["rows", "columns"])
+@pytest.mark.parametrize("world,m,n", [(2, 1500, 200), (4, 2000, 300), (8, 600, 130)])
+def test_levmarq_mpi_fd_modes_bitwise(tmp_path, monkeypatch, mode, world, m, n):
+    """LevMarqMPI's two Jacobian decompositions: rows mode (default; every FD column on the
+    rank's own m-slices, trial residuals shared point-to-point -- no Jacobian exchange) and
+    columns mode (PNOL_LM_FD=columns: cost-balanced FD column tiles, then the m-slice exchange).
+    X, F0 and FOpt on every rank are bitwise the single-GPU LevMarq's either way (m = 600 at 8
+    ranks: three ranks own no rows)."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_levmarq
+    if mode == "columns":
+        monkeypatch.setenv("PNOL_LM_FD", "columns")
+    else:
+        monkeypatch.delenv("PNOL_LM_FD", raising=False)
+    _run_workers(tmp_path, world, m, n, "lm")
+    monkeypatch.delenv("PNOL_LM_FD", raising=False)
+    ctx = Context(0)
+    obj = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+    X1, F01, FO1, _ = run_levmarq(obj, np.zeros(n), (0.001, 10.0, 1e-7, 5, 0.0, -1), which=0)
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        assert np.array_equal(z["X"], X1), (mode, r)
+        assert np.array_equal(z["F0"], F01) and np.array_equal(z["FO"], FO1), (mode, r)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_levmarq_mpi_ranks_bitwise_equal_single(tmp_path, world, oracle):
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
