@@ -906,7 +906,9 @@ int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* 
         r0 = 0;
         r1 = o->m;
     }
-    if (r0 < 0 || r0 % kPanel || r1 > o->m || r0 > r1 || (r1 % kPanel && r1 != o->m)) return PNOL_ERR_ARG;
+    if (r0 == r1) r0 = r1 = o->m;   // no rows
+    if (r0 < 0 || (r0 % kPanel && r0 != o->m) || r1 > o->m || r0 > r1 || (r1 % kPanel && r1 != o->m))
+        return PNOL_ERR_ARG;
     PNOL_CHECK(ensure_panels(ctx, o));
     void *C = nullptr, *xc = nullptr;
     PNOL_CHECK(ckpt_claim(ctx, o, x, true, &C, &xc, r0, r1));
@@ -981,7 +983,9 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
         r0 = 0;
         r1 = o->m;
     }
-    if (!rows_all && (!sliced || r0 < 0 || r0 % kPanel || r1 > o->m || r0 > r1 || (r1 % kPanel && r1 != o->m)))
+    if (!rows_all && r0 == r1) r0 = r1 = o->m;   // no rows (a rank past the last residual)
+    if (!rows_all && (!sliced || r0 < 0 || (r0 % kPanel && r0 != o->m) || r1 > o->m || r0 > r1 ||
+                      (r1 % kPanel && r1 != o->m)))
         return PNOL_ERR_ARG;
     if (!o || !x || !h || !F0 || is_scalar_kind(o->kind) || ntiles < 0 || ldjt < (sliced ? mS : o->m))
         return PNOL_ERR_ARG;
