@@ -42,6 +42,12 @@ class BFGS_Bnd : public AlgorithmBnd {
     vector<double>* fTrace = nullptr;     // extension: F after every iteration (any recursion level)
     double* profile = nullptr;            // extension: per-phase seconds and counts
     int depth = 0;
+    // host bookkeeping of the active-set recursion (no reference counterpart): freeIdx[k] is the
+    // full-space index of the current level's coordinate k while freeIdxLive, and the caller's
+    // pending next direction is released while a reduced problem runs
+    vector<int> freeIdx;
+    bool freeIdxLive = false;
+    vector<double>* pnextHeld = nullptr;
 
   public:
     void findMinBnd(vector<double>& X, vector<double>& Xlb, vector<double>& Xub, double& f0, double& fOpt);

@@ -1,8 +1,10 @@
 // bfgs_bnd.cpp -- bounded BFGS with active-set recursion (drop-in for
 // Source/BFGS_bnd_linesearch.cpp) plus the box helpers (Box_boundary_functions.cpp:11-40,
 // BFGS_with_bnd_linsearch_MPI.cpp:665-708).
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <iostream>
 
 #include "../pnol_comm.hpp"
@@ -15,6 +17,37 @@ using namespace pnol;
 
 namespace {
 double sign_of(double x) { return x > 0 ? 1.0 : (x < 0 ? -1.0 : 0.0); }
+// PNOL_BND_DETAIL=1: where the host time of the "other" phase goes (diagnostics, stderr)
+enum { kDetFreeze, kDetGather, kDetCopyBack, kDetIterLoops, kDetCount };
+thread_local double g_det[kDetCount];
+double* det_slot(int k) {
+    static const bool on = [] {
+        const char* e = std::getenv("PNOL_BND_DETAIL");
+        return e && std::atoi(e) != 0;
+    }();
+    return on ? &g_det[k] : nullptr;
+}
+// drop positions fk (ascending) of v[0, n): the kept entries slide down run by run
+template <class T>
+void drop_positions(std::vector<T>& v, const std::vector<int>& fk, int n) {
+    if (fk.empty()) return;
+    int dst = fk[0];
+    for (size_t f = 0; f < fk.size(); ++f) {
+        const int b = fk[f] + 1, e = f + 1 < fk.size() ? fk[f + 1] : n;
+        std::copy(v.begin() + b, v.begin() + e, v.begin() + dst);
+        dst += e - b;
+    }
+}
+// the inverse: reopen the gaps at positions fk of v[0, n) (their contents are the caller's)
+template <class T>
+void reopen_positions(std::vector<T>& v, const std::vector<int>& fk, int n) {
+    int hi = n;
+    for (int f = (int)fk.size() - 1; f >= 0; --f) {
+        const int b = fk[f] + 1;
+        std::copy_backward(v.begin() + (b - f - 1), v.begin() + (hi - f - 1), v.begin() + hi);
+        hi = fk[f];
+    }
+}
 void print_vec(const std::vector<double>& v) {
     for (double x : v) std::printf("%.17g ", x);
     std::printf("\n");
@@ -168,90 +201,152 @@ void BFGS_Bnd::boundaryAssessment(double& F, vector<double>& X, vector<double>& 
     // BFGS_bnd_linesearch.cpp:503-728
     const int ncur = (int)X.size();
     const int Ndim = (int)cX.size();
-    std::vector<bool> cIcur(ncur, false);
-    std::vector<int> frozen;
+    PhaseClock tf(det_slot(kDetFreeze));
+    std::vector<int> fk, fi;   // positions in X frozen by this assessment (ascending), their full indices
     bool bndFlag = false;
-    int icur = 0;
-    // the same tests, evaluated without short-circuit branches (the frozen pattern is
-    // unpredictable); only a coordinate that hits a bound takes a branch
-    const int klast = ncur > 0 ? ncur - 1 : 0;
-    int Nconst = 0;   // coordinates frozen before this assessment (the loop reads every cI[i])
-    for (int i = 0; i < Ndim; ++i) {
-        const bool c = cI[i];
-        Nconst += c;
-        if (ncur == 0) continue;
-        const int k = icur < klast ? icur : klast;
-        const double xk = X[k], pk = p[k], gk = dFdX[k];
-        const bool lo = (std::fabs(xk - Xlb[k]) < bndTol) & ((pk < 0) | (gk > 0));
-        const bool hi = (std::fabs(xk - Xub[k]) < bndTol) & ((pk > 0) | (gk < 0));
-        if (!c & (lo | hi)) {
-            bndFlag = true; cI[i] = true; cX[i] = xk; cIcur[icur] = true; frozen.push_back(i);
+    int Nconst = 0;            // coordinates frozen after the tests
+    if (freeIdxLive && (int)freeIdx.size() == ncur) {
+        // the level's coordinates are the free ones of cI in order (freeIdx): the reference's
+        // walk over all Ndim indicators reduces to the tests over X's own positions
+        for (int k = 0; k < ncur; ++k) {
+            const double xk = X[k], pk = p[k], gk = dFdX[k];
+            const bool lo = (std::fabs(xk - Xlb[k]) < bndTol) & ((pk < 0) | (gk > 0));
+            const bool hi = (std::fabs(xk - Xub[k]) < bndTol) & ((pk > 0) | (gk < 0));
+            if (lo | hi) fk.push_back(k);
         }
-        icur += !c;
+        for (int k : fk) {
+            const int i = freeIdx[k];
+            cI[i] = true; cX[i] = X[k]; fi.push_back(i);
+        }
+        bndFlag = !fk.empty();
+        Nconst = Ndim - ncur + (int)fk.size();
+    } else {
+        // any constantIndicator: the reference's walk, evaluated without short-circuit
+        // branches (only a coordinate that hits a bound takes one)
+        freeIdxLive = false;
+        const int klast = ncur > 0 ? ncur - 1 : 0;
+        int icur = 0;
+        for (int i = 0; i < Ndim; ++i) {
+            const bool c = cI[i];
+            Nconst += c;
+            if (ncur == 0) continue;
+            const int k = icur < klast ? icur : klast;
+            const double xk = X[k], pk = p[k], gk = dFdX[k];
+            const bool lo = (std::fabs(xk - Xlb[k]) < bndTol) & ((pk < 0) | (gk > 0));
+            const bool hi = (std::fabs(xk - Xub[k]) < bndTol) & ((pk > 0) | (gk < 0));
+            if (!c & (lo | hi)) {
+                bndFlag = true; cI[i] = true; cX[i] = xk; fi.push_back(i);
+                if (icur < ncur) fk.push_back(icur);
+            }
+            icur += !c;
+        }
+        Nconst += (int)fi.size();   // == the count of cI after the freezes
     }
-    Nconst += (int)frozen.size();   // == the count of cI after the freezes
     if (bndFlag && verbose && comm_rank() == ROOT_ID) {
         std::cout << std::endl << "Optimizer reached box boundary; steepest descent points outside the box at "
-                  << frozen.size() << " coordinate(s); recursing on the remaining ones." << std::endl;
+                  << fi.size() << " coordinate(s); recursing on the remaining ones." << std::endl;
     }
     const int nr = Ndim - Nconst;
+    tf.stop();
     if (bndFlag && nr > 0) {
-        double FR = F;
-        std::vector<double> XR(nr), gR(nr), lbR(nr), ubR(nr), dXR(nr);
-        {
-            int ir = 0;
-            for (icur = 0; icur < ncur; ++icur)
-                if (!cIcur[icur]) {
-                    XR[ir] = X[icur]; gR[ir] = dFdX[icur]; lbR[ir] = Xlb[icur];
-                    ubR[ir] = Xub[icur]; dXR[ir] = dX[icur];
-                    ++ir;
-                }
+        PhaseClock tg(det_slot(kDetGather));
+        // The reduced problem runs on these same vectors: the frozen entries are set aside and
+        // the others slide down in place (the reference gathers them into fresh vectors at every
+        // level), so one set of n-vectors serves the whole recursion -- about 11k levels at
+        // n = 16384 -- instead of five new ones per level.
+        const int nf = (int)fk.size(), nk = ncur - nf;
+        std::vector<double> held((size_t)nf * 5);
+        for (int f = 0; f < nf; ++f) {
+            const int k = fk[f];
+            double* h = &held[(size_t)f * 5];
+            h[0] = X[k]; h[1] = dFdX[k]; h[2] = Xlb[k]; h[3] = Xub[k]; h[4] = dX[k];
         }
+        const bool idx = freeIdxLive;
+        for (vector<double>* v : {&X, &dFdX, &Xlb, &Xub, &dX}) {
+            drop_positions(*v, fk, ncur);
+            v->resize(nr);
+        }
+        if (idx) {
+            drop_positions(freeIdx, fk, ncur);
+            freeIdx.resize(nr);
+        }
+        const double FR = F;
+        double Fr = F;
         // the outer D is discarded while the reduced problem runs (reset below), so the
         // reduced D takes over its device buffer: one n x n matrix for the whole recursion
         DenseInverseHessian DR(D, nr, updateMode);
-        std::vector<double> scaleR;
         if (!initialScalingVec.empty()) {
-            for (int i = 0; i < Ndim; ++i) if (!cI[i]) scaleR.push_back(initialScalingVec[i]);
+            std::vector<double> scaleR;
+            if (idx) {
+                scaleR.resize(nr);
+                for (int k = 0; k < nr; ++k) scaleR[k] = initialScalingVec[freeIdx[k]];
+            } else {
+                for (int i = 0; i < Ndim; ++i) if (!cI[i]) scaleR.push_back(initialScalingVec[i]);
+            }
             DR.setIdentity(&scaleR);
         } else {
             DR.setIdentity();
         }
         recurFlag = true;
+        // the caller's direction (and the next one its update prepared) are recomputed after
+        // the recursion: release them while it runs
+        std::vector<double>().swap(p);
+        if (pnextHeld) std::vector<double>().swap(*pnextHeld);
+        pnextHeld = nullptr;
+        tg.stop();
         ++depth;
         if (profile && depth > profile[kProfDepth]) profile[kProfDepth] = depth;
-        mainBFGSLoop(FR, XR, gR, DR, lbR, ubR, dXR, cX, cI, optimFlag, recurFlag);
+        mainBFGSLoop(Fr, X, dFdX, DR, Xlb, Xub, dX, cX, cI, optimFlag, recurFlag);
         --depth;
         assessRecursed = true;   // after the reduced loop, which clears it for its own levels
-        int ir = 0;
-        for (icur = 0; icur < ncur; ++icur)
-            if (!cIcur[icur]) {
-                F = FR; X[icur] = XR[ir]; dFdX[icur] = gR[ir]; Xlb[icur] = lbR[ir]; Xub[icur] = ubR[ir];
-                dX[icur] = dXR[ir];
-                ir++;
-            }
-        for (int k : frozen) cI[k] = false;
+        PhaseClock tc(det_slot(kDetCopyBack));
+        F = nk > 0 ? Fr : FR;
+        for (vector<double>* v : {&X, &dFdX, &Xlb, &Xub, &dX}) {
+            v->resize(ncur);
+            reopen_positions(*v, fk, ncur);
+        }
+        for (int f = 0; f < nf; ++f) {
+            const int k = fk[f];
+            const double* h = &held[(size_t)f * 5];
+            X[k] = h[0]; dFdX[k] = h[1]; Xlb[k] = h[2]; Xub[k] = h[3]; dX[k] = h[4];
+        }
+        if (idx && freeIdxLive) {   // (a level below may have dropped the index map)
+            freeIdx.resize(ncur);
+            reopen_positions(freeIdx, fk, ncur);
+            for (int f = 0; f < nf; ++f) freeIdx[fk[f]] = fi[f];
+        }
+        for (int i : fi) cI[i] = false;
         if (!initialScalingVec.empty()) {
             std::vector<double> scale;
-            for (int i = 0; i < Ndim; ++i) if (!cI[i]) scale.push_back(initialScalingVec[i]);
-            scale.resize(ncur, 1.0);
+            if (freeIdxLive) {
+                scale.resize(ncur);
+                for (int k = 0; k < ncur; ++k) scale[k] = initialScalingVec[freeIdx[k]];
+            } else {
+                for (int i = 0; i < Ndim; ++i) if (!cI[i]) scale.push_back(initialScalingVec[i]);
+                scale.resize(ncur, 1.0);
+            }
             D.setIdentity(&scale);
         } else {
             D.setIdentity();
         }
+        tc.stop();
         {
             PhaseClock t(prof_slot(profile, kProfGrad));
             objPtr->gradientApproximationRecur(X, dX, dFdX, cX, cI);
             if (profile) profile[kProfGradCalls] += 1;
         }
+        PhaseClock tc2(det_slot(kDetCopyBack));
         bool cont = false;
-        for (icur = 0; icur < ncur; ++icur)
-            if (cIcur[icur]) {
-                if ((std::fabs(X[icur] - Xlb[icur]) < bndTol) && (dFdX[icur] < 0)) cont = true;
-                else if ((std::fabs(X[icur] - Xub[icur]) < bndTol) && (dFdX[icur] > 0)) cont = true;
-            }
-        Nconst = 0;
-        for (int i = 0; i < Ndim; ++i) Nconst += cI[i];
+        for (int k : fk) {
+            if ((std::fabs(X[k] - Xlb[k]) < bndTol) && (dFdX[k] < 0)) cont = true;
+            else if ((std::fabs(X[k] - Xub[k]) < bndTol) && (dFdX[k] > 0)) cont = true;
+        }
+        if (freeIdxLive) {
+            Nconst = Ndim - ncur;
+        } else {
+            Nconst = 0;
+            for (int i = 0; i < Ndim; ++i) Nconst += cI[i];
+        }
         if (Nconst == 0) recurFlag = false;
         optimFlag = cont;
         if (verbose > 0 && comm_rank() == ROOT_ID)
@@ -259,6 +354,9 @@ void BFGS_Bnd::boundaryAssessment(double& F, vector<double>& X, vector<double>& 
                                : "     Optimization exiting after recursive boundary optimization.")
                       << std::endl;
     } else if (nr == 0) {
+        // the coordinates frozen here stay frozen (as in the reference): cI no longer matches
+        // the levels above, so they fall back to the full walk
+        freeIdxLive = false;
         optimFlag = false;
         if (verbose > 0 && comm_rank() == ROOT_ID) std::cout << "      NO VARIABLES LEFT TO OPTIMIZE!!!! " << std::endl;
     }
@@ -290,6 +388,7 @@ void BFGS_Bnd::mainBFGSLoop(double& F, vector<double>& X, vector<double>& dFdX, 
             PhaseClock t(prof_slot(profile, kProfLineSearch));
             cubicInterpolationLineSearchBnd(X, Xlb, Xub, F, dFdX, p, cX, cI, alpha, Fopt);
         }
+        PhaseClock tl(det_slot(kDetIterLoops));
         for (int i = 0; i < n; ++i) { Xprev[i] = X[i]; X[i] = X[i] + alpha * p[i]; }
         F = Fopt;
         {
@@ -298,6 +397,7 @@ void BFGS_Bnd::mainBFGSLoop(double& F, vector<double>& X, vector<double>& dFdX, 
             gprev.assign(dFdX.begin(), dFdX.end());
             s.resize(n);
             y.resize(n);
+            tl.stop();
             {
                 PhaseClock t(prof_slot(profile, kProfGrad));
                 objPtr->gradientApproximationRecur(X, dX, dFdX, cX, cI);
@@ -308,12 +408,15 @@ void BFGS_Bnd::mainBFGSLoop(double& F, vector<double>& X, vector<double>& dFdX, 
             D.update(y, s, &dFdX, &pnext);
         }
         assessRecursed = false;
+        pnextHeld = &pnext;
         boundaryAssessment(F, X, p, dFdX, D, Xlb, Xub, dX, cX, cI, optimFlag, recurFlag);
+        pnextHeld = nullptr;
         // a recursion reset D to I and recomputed the gradient: the fused direction is stale
         have_next = !assessRecursed;
         if (!have_next) std::vector<double>().swap(pnext);
         // the step's sum |X - Xprev| and the gradient's sum of squares: two independent
         // sequential chains (each in the reference's order), one loop
+        PhaseClock tl2(det_slot(kDetIterLoops));
         xdiff = 0;
         double gg = 0.0;
         for (int i = 0; i < n; ++i) {
@@ -337,7 +440,13 @@ void BFGS_Bnd::findMinBnd(vector<double>& X, vector<double>& Xlb, vector<double>
     // at n = 16384, SURVEY 8(d) cfg 5): run it on a thread with a stack sized for that
     PhaseClock total(prof_slot(profile, kProfTotal));
     depth = 0;
-    run_deep([&] { findMinBndBody(X, Xlb, Xub, f0, fOpt); });
+    run_deep([&] {
+        for (double& v : g_det) v = 0.0;
+        findMinBndBody(X, Xlb, Xub, f0, fOpt);
+        if (det_slot(0))
+            std::fprintf(stderr, "[pnol_amd] BFGS_Bnd host detail (s): freeze %.3f gather+alloc %.3f copyback %.3f iter-loops %.3f\n",
+                         g_det[kDetFreeze], g_det[kDetGather], g_det[kDetCopyBack], g_det[kDetIterLoops]);
+    });
     if (profile) profile[kProfIters] = totalIter;
 }
 
@@ -375,7 +484,17 @@ void BFGS_Bnd::findMinBndBody(vector<double>& X, vector<double>& Xlb, vector<dou
     f0 = F;
     bool optimFlag = true;
     int recurFlag = 0;
-    mainBFGSLoop(F, X, dFdX, D, Xlb, Xub, dX, cX, cI, optimFlag, recurFlag);
+    freeIdx.resize(n);
+    for (int i = 0; i < n; ++i) freeIdx[i] = i;
+    freeIdxLive = true;
+    try {
+        mainBFGSLoop(F, X, dFdX, D, Xlb, Xub, dX, cX, cI, optimFlag, recurFlag);
+    } catch (...) {
+        freeIdxLive = false;
+        throw;
+    }
+    freeIdxLive = false;
+    std::vector<int>().swap(freeIdx);
     fOpt = F;
     if (verbose >= 0 && comm_rank() == ROOT_ID) {
         std::cout << std::endl << "  Completed bounded BFGS." << std::endl << "  X0 = ";

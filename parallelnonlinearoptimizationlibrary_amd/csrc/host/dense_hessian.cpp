@@ -55,6 +55,13 @@ DenseInverseHessian::DenseInverseHessian(DenseInverseHessian& parent, int n, int
         iop_ = io_.get();
     }
     dev_ok_ = false;
+    // the parent's host state is forfeit too: release its pending correction while the
+    // reduced problem runs (each recursion level would otherwise hold three n-vectors)
+    parent.clobbered_ = true;
+    parent.pending_ = parent.pend_dev_ = false;
+    parent.ident_ = parent.dev_ok_ = false;
+    for (std::vector<double>* v : {&parent.hs_, &parent.ha_, &parent.hb_, &parent.hscale_})
+        std::vector<double>().swap(*v);
 }
 
 const double* DenseInverseHessian::deviceScale() {

@@ -78,8 +78,11 @@ class PhaseClock {
     explicit PhaseClock(double* acc) : acc_(acc) {
         if (acc_) t0_ = std::chrono::steady_clock::now();
     }
-    ~PhaseClock() {
+    ~PhaseClock() { stop(); }
+    // end the phase early (the destructor then adds nothing)
+    void stop() {
         if (acc_) *acc_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0_).count();
+        acc_ = nullptr;
     }
 
   private:

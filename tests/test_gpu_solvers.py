@@ -180,6 +180,10 @@ def test_bfgs_mpi_pool_matches_oracle(ctx, oracle):
     ("testBFGSBnd", 5, [2.0] * 5, [-5.0] * 5, [5.0] * 5),
     ("lower-active", 3, [-1.0, 2.0, 2.0], [-1.0] * 3, [5.0] * 3),
     ("upper-active", 3, [0.0, 0.0, 0.0], [-2.0] * 3, [0.5] * 3),
+    # frozen sets at interior and several positions at once (the in-place reduced vectors)
+    ("alternating", 12, [0.2, -0.2] * 6, [-0.3] * 12, [0.6] * 12),
+    ("upper-ramp", 16, list(np.linspace(-0.9, 0.9, 16)), [-1.0] * 16, [0.35] * 16),
+    ("interior-lower", 9, [1.5] * 9, [0.2, 1.2, 0.2, 1.3, 0.2, 1.1, 0.2, 1.4, 0.2], [2.0] * 9),
 ])
 def test_bfgs_bnd_matches_oracle(ctx, oracle, case):
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
