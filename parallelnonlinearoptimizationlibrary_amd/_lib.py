@@ -11,7 +11,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpnol_amd.so")
+# PNOL_AMD_LIB: an A/B build of the same library (tools/ab_lib.sh); default the in-tree build
+LIB_PATH = os.environ.get("PNOL_AMD_LIB") or os.path.join(HERE, "libpnol_amd.so")
 
 PNOL_OK, PNOL_ERR_ARG, PNOL_ERR_HIP, PNOL_ERR_NOMEM, PNOL_ERR_NODEVICE = 0, 1, 2, 3, 4
 PNOL_ERR_SINGULAR, PNOL_ERR_COMM, PNOL_ERR_UNSUPPORTED = 5, 6, 7

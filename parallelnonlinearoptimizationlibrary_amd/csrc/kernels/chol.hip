@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace pnol {
 namespace {
@@ -513,7 +514,7 @@ struct NoEarly {
 // panel (the persistent chain's look-ahead for the next tile, EarlyNext).  Wst != nullptr: rows
 // 32..63 of W_d also go to Wst in the substage layout (the next tile's L = A W^T operand).
 template <bool STAMP = false, bool SC1 = false, class EARLY = NoEarly>
-__device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict__ rinv, int* cnt,
+__device__ __forceinline__ void factor_diag32(const DiagLds& L, double* __restrict__ rinv, int* cnt,
                                             double* __restrict__ Wd, int d, int* info, long long* st = nullptr,
                                             const EARLY& early = EARLY(), double* __restrict__ Wst = nullptr) {
     const int t = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
@@ -631,6 +632,418 @@ __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict
     }
 }
 
+// ---- the diagonal tile in 16-wide micro-panels (PNOL_CHOL_MP, the default) --------------------
+// factor_diag32's chain wave issues every rank-1 update of a 32-wide panel itself (~290 cycles
+// per pivot, 23k cycles per tile).  Here the tile is four 64 x 16 micro-panels:
+//   wave 0      the pivot chain of micro-panel p (rows 16p .. 63, one row per lane, 16 entries in
+//               registers): per pivot at most 14 rank-1 fmas, software-pipelined as panel_step;
+//               column c and 1 / L_cc go to LDS, every 2 columns a counter in LDS
+//   waves 2, 3  the trailing update by micro-panels 0 and 1 as fp64 MFMA: each owns some lower
+//               16 x 16 blocks (ib, q), q >= 1, kept in registers, and applies -L_{ib,p} L_{q,p}^T
+//               four columns at a time as wave 0 publishes them (one v_mfma_f64_16x16x4_f64 per
+//               block and group); the blocks of micro-panel p+1 go to LDS when panel p is
+//               complete.  Micro-panel 2's one block update (3,3) is wave 0's, so waves 2 / 3 are
+//               free for the chain's look-ahead (EARLY) from the end of micro-panel 1
+//   wave 1      V_p = L_pp^{-1} (16 x 16, lane = column) one column pair behind the chain, then
+//               the off-diagonal blocks of W = L^{-1} by block rows, W_ij = -V_i X_ij with
+//               X_ij = sum_{k=j}^{i-1} L_ik W_kj accumulated as soon as its operands exist, so only
+//               W_3j = -V_3 X_3j (three products, waves 0 and 1) follow the last pivot.
+// Every accumulator receives its MFMAs in a fixed order, so W is deterministic; it is not bitwise
+// factor_diag32's (other summation order), and methods 4 and 5 both use this factor.
+// LDS (doubles, from L.Sl): the tile (Sl / S22, 3168), the panels' columns (2560), the W blocks
+// (10 x 288), a 64-double discard row; the X hand-off blocks reuse Sl rows 0 .. 26, dead once
+// micro-panel 1 is in registers.  Words: cnt[0] final columns, cnt[1] W rows 0..31 done,
+// cnt[2] / cnt[3] waves 2 / 3 have stored micro-panel cnt's blocks, cnt[4] V_3 and X_3j in LDS.
+#ifndef PNOL_CHOL_MP
+#define PNOL_CHOL_MP 0
+#endif
+constexpr int kMW = 16;            // micro-panel width
+constexpr int kBP = 18;            // row stride of a 16 x 16 block in LDS (conflict-free fragments)
+constexpr int kBlk = 16 * kBP;     // doubles per block
+__host__ __device__ constexpr int lblk(int ib, int jb) { return ib * (ib + 1) / 2 + jb; }
+__host__ __device__ constexpr int mp_ld(int p) { return NB - kMW * p; }                 // rows of micro-panel p
+__host__ __device__ constexpr int mp_base(int p) { return 1024 * p - 128 * p * (p - 1); }   // sum of kMW * mp_ld(q), q < p
+
+struct MpLds {
+    double* Sl;     // the tile, as diag_put leaves it
+    double* S22;
+    double* Lc;     // micro-panel p's columns at mp_base(p), column-major, rows 16p .. 63 (stride mp_ld(p))
+    double* Wb;     // the 10 lower blocks of W, block (ib, jb) at lblk(ib, jb) * kBlk, row stride kBP
+    double* Xs;     // 3 hand-off blocks (row stride kBP), in Sl rows 0 .. 26
+    double* disc;   // one block (kBlk doubles): stores of lanes outside a micro-panel or a block
+};
+__device__ __forceinline__ MpLds mp_lds(const DiagLds& L) {
+    MpLds M;
+    M.Sl = L.Sl;
+    M.S22 = L.S22;
+    M.Lc = L.S22 + kHalf * kS;
+    M.Wb = M.Lc + mp_base(4);
+    M.disc = M.Wb + 10 * kBlk;
+    M.Xs = L.Sl;
+    return M;
+}
+static_assert(64 * kS + kHalf * kS + mp_base(4) + 11 * kBlk <= 2 * kStage, "micro-panel factor fits the staging LDS");
+static_assert(3 * kBlk <= kHalf * kS, "X hand-off blocks fit Sl rows 0..31");
+
+// the W_d rows 0..31 operand of EarlyNext: element (r, c), c <= r block-wise
+__device__ __forceinline__ double w11_at(const double* W11, int r, int c) {
+#if PNOL_CHOL_MP
+    return W11[lblk(r >> 4, c >> 4) * kBlk + (r & 15) * kBP + (c & 15)];
+#else
+    return W11[r * kS + c];
+#endif
+}
+__device__ __forceinline__ const double* diag_w11(const DiagLds& L) {
+#if PNOL_CHOL_MP
+    return mp_lds(L).Wb;
+#else
+    return L.W11;
+#endif
+}
+
+// tile entry (row, col), lower triangle, in the diag_put layout
+__device__ __forceinline__ double* mp_s(const MpLds& M, int row, int col) {
+    return col < kHalf ? M.Sl + row * kS + col : M.S22 + (row - kHalf) * kS + (col - kHalf);
+}
+
+// Column J's values as wave 0 reads them back for the deferred part of its rank-1 update:
+// entries k >= J + 4 (in pairs from the even K0).
+template <int J>
+struct ColBuf16 {
+    static constexpr int K0 = (J + 4) & ~1, NR = K0 < kMW ? (kMW - K0) / 2 : 0;
+    double2 v[NR > 0 ? NR : 1];
+};
+
+// column c-2's deferred update (entries k >= J + 2), the pairs q with q % 4 == G
+template <int J, int G>
+__device__ __forceinline__ void mp_def(double (&a)[kMW], double lp2, const ColBuf16<J - 2>& cp2) {
+    if constexpr (J >= 2) {
+#pragma unroll
+        for (int q = G; q < ColBuf16<J - 2>::NR; q += 4) {
+            const int k = ColBuf16<J - 2>::K0 + 2 * q;
+            if (k >= J + 2) {
+                a[k] = fma(-lp2, cp2.v[q].x, a[k]);
+                asm volatile("" : "+v"(a[k]));
+            }
+            if (k + 1 >= J + 2) {
+                a[k + 1] = fma(-lp2, cp2.v[q].y, a[k + 1]);
+                asm volatile("" : "+v"(a[k + 1]));
+            }
+        }
+    }
+}
+
+// a value defined here: volatile asm statements keep their order, so the IR passes cannot sink
+// the computation past this point (sched_barrier alone orders only the machine scheduler)
+#define PNOL_PIN(x) asm volatile("" : "+v"(x))
+#define PNOL_SB __builtin_amdgcn_sched_barrier(0)
+
+// One pivot of micro-panel P (wave 0): column c = 16P + J from its reciprocal square root r.
+// The rank-1 update of column c is split: entries J+1 .. J+3 at once, with the column's values
+// from their lanes (v_readlane; entry J+1 is the next pivot, formed in its own lane first), and
+// entries k >= J+4 two steps later, with the values read back from the column's LDS copy
+// (issued here, consumed at step J+2, so the LDS round trip is off the chain).  Entry k still
+// receives every column's update before it is used (columns <= k-4 by step k-2); the order of
+// the updates on one entry is fixed by the code, so W is deterministic.
+// Issue order is pinned by scheduling barriers: each dependent op of the pivot chain (~12
+// cycles of latency each, tools/microbench/piv_chain.hip: 124 cycles per pivot for the bare
+// chain) is followed by a group of independent updates that fill its latency; left to itself
+// the scheduler issues the chain ops back to back (~280 cycles per pivot).
+template <int J, int P, bool STAMP>
+__device__ __forceinline__ void mp_step(double (&a)[kMW], double r, double lp1, const ColBuf16<J - 1>& cp1, double lp2,
+                                        const ColBuf16<J - 2>& cp2, double* __restrict__ Lp, double* __restrict__ disc,
+                                        double* __restrict__ rinv, int* cnt, int lane, bool& bad, long long* st) {
+    constexpr int c = kMW * P + J, LD = mp_ld(P);
+    if constexpr (STAMP && (J & 7) == 0) st[2 * P + (J >> 3)] = __builtin_amdgcn_s_memtime();
+    const double l = a[J] * r;
+    a[J] = l;
+    double rn = 0.0;
+    if constexpr (J + 1 < kMW) {
+        const double piv = readlane_d(fma(-l, l, a[J + 1]), c + 1);   // lane c+1's own update
+        double r0 = __builtin_amdgcn_rsq(piv);
+        PNOL_PIN(r0);
+        PNOL_SB;
+        a[J + 1] = fma(-l, readlane_d(l, c + 1), a[J + 1]);
+        PNOL_PIN(a[J + 1]);
+        mp_def<J, 0>(a, lp2, cp2);
+        PNOL_SB;
+        double r2 = r0 * r0;
+        PNOL_PIN(r2);
+        PNOL_SB;
+        if constexpr (J + 2 < kMW) {
+            a[J + 2] = fma(-l, readlane_d(l, c + 2), a[J + 2]);
+            PNOL_PIN(a[J + 2]);
+        }
+        mp_def<J, 1>(a, lp2, cp2);
+        PNOL_SB;
+        double e = fma(-piv, r2, 1.0);
+        PNOL_PIN(e);
+        PNOL_SB;
+        if constexpr (J + 3 < kMW) {
+            a[J + 3] = fma(-l, readlane_d(l, c + 3), a[J + 3]);
+            PNOL_PIN(a[J + 3]);
+        }
+        mp_def<J, 2>(a, lp2, cp2);
+        PNOL_SB;
+        double pp = fma(e, 0.375, 0.5), re = r0 * e;
+        PNOL_PIN(pp);
+        PNOL_PIN(re);
+        PNOL_SB;
+        mp_def<J, 3>(a, lp2, cp2);
+        bad |= !(piv > 0.0);
+        PNOL_SB;
+        rn = fma(re, pp, r0);   // = rsqrt_nr(piv), the same operations
+        PNOL_SB;
+    }
+    // lanes above the micro-panel store into the discard row (a select, not a branch)
+    double* dst = (P == 0 || lane >= kMW * P) ? Lp + J * LD + (lane - kMW * P) : disc + lane;
+    *dst = l;
+    rinv[c] = r;   // every lane stores the same value: no divergent branch in the chain
+    if constexpr ((J & 1) == 1) lds_signal(cnt, c + 1);
+    ColBuf16<J> cv;
+    if constexpr (ColBuf16<J>::NR > 0) {
+#pragma unroll
+        for (int q = 0; q < ColBuf16<J>::NR; ++q)
+            cv.v[q] = *reinterpret_cast<const double2*>(Lp + J * LD + ColBuf16<J>::K0 + 2 * q);
+    }
+    asm volatile("" ::: "memory");   // keep the next steps' LDS reads from being hoisted here
+    PNOL_SB;
+    if constexpr (J + 1 < kMW)
+        mp_step<J + 1, P, STAMP>(a, rn, l, cv, lp1, cp1, Lp, disc, rinv, cnt, lane, bad, st);
+}
+
+template <int P, bool STAMP>
+__device__ __forceinline__ void mp_panel(const MpLds& M, double* __restrict__ rinv, int* cnt, int lane, int d,
+                                         int* info, long long* st) {
+    if constexpr (P == 1 || P == 2) {   // the owners' blocks of this micro-panel are in LDS
+        wait_lds_ge(cnt + 2, P);
+        wait_lds_ge(cnt + 3, P);
+    } else if constexpr (P == 3) {
+        // block (3,3) as wave 2 left it (micro-panels 0, 1 applied); micro-panel 2's update here,
+        // from the columns this wave has just written: waves 2 and 3 are free after micro-panel 1
+        // for the chain's look-ahead
+        wait_lds_ge(cnt + 2, 2);
+        d4 acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = *mp_s(M, 48 + (lane >> 4) + 4 * r, 48 + (lane & 15));
+        const double* Lp = M.Lc + mp_base(2);
+        acc = mfma_blk<16>(acc, [&](int i, int k) { return -Lp[k * mp_ld(2) + 16 + i]; },
+                           [&](int j, int k) { return Lp[k * mp_ld(2) + 16 + j]; }, lane);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) *mp_s(M, 48 + (lane >> 4) + 4 * r, 48 + (lane & 15)) = acc[r];
+    }
+    double a[kMW];
+    const int row = max(lane, kMW * P);
+#pragma unroll
+    for (int k = 0; k < kMW; ++k) a[k] = lane >= kMW * P ? *mp_s(M, row, kMW * P + k) : 0.0;
+    const double piv = readlane_d(a[0], kMW * P);
+    bool bad = !(piv > 0.0);
+    const ColBuf16<-1> n1{};
+    const ColBuf16<-2> n2{};
+    mp_step<0, P, STAMP>(a, rsqrt_nr(piv), 0.0, n1, 0.0, n2, M.Lc + mp_base(P), M.disc, rinv, cnt, lane, bad, st);
+    if (bad && lane == 0) atomicCAS(info, 0, d * NB + kMW * P + 1);
+}
+
+// 16 x 16 block (row stride kBP) <-> MFMA accumulator layout
+__device__ __forceinline__ void blk_put(double* __restrict__ B, const d4& acc, int lane) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) B[((lane >> 4) + 4 * r) * kBP + (lane & 15)] = acc[r];
+}
+
+__host__ __device__ constexpr int own_i(int ow, int b) { return ow == 2 ? (b == 0 ? 1 : (b == 2 ? 2 : 3)) : (b == 0 ? 2 : 3); }
+__host__ __device__ constexpr int own_q(int ow, int b) { return ow == 2 ? (b < 2 ? 1 : b) : b + 1; }
+// The trailing update by micro-panels 0 and 1, owned by wave OW (2 or 3): blocks (ib, q),
+// 1 <= q <= ib <= 3, with (ib - q) & 1 == OW - 2.  Wave 2: (1,1) (3,1) (2,2) (3,3); wave 3:
+// (2,1) (3,2).  Block (3,3) goes to LDS with the blocks of micro-panel 2; wave 0 applies
+// micro-panel 2's update to it (mp_panel<3>).
+template <int OW>
+__device__ __forceinline__ void mp_owner(const MpLds& M, int* cnt, int lane) {
+    constexpr int NBk = OW == 2 ? 4 : 2;
+    const int frow = lane & 15, fk = lane >> 4;
+    d4 acc[NBk];
+#pragma unroll
+    for (int b = 0; b < NBk; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            acc[b][r] = *mp_s(M, 16 * own_i(OW, b) + (lane >> 4) + 4 * r, 16 * own_q(OW, b) + (lane & 15));
+    auto panel = [&](auto pc) {
+        constexpr int P = decltype(pc)::value, LD = mp_ld(P);
+        const double* Lp = M.Lc + mp_base(P);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            wait_lds_ge(cnt, kMW * P + 4 * g + 4);
+#pragma unroll
+            for (int b = 0; b < NBk; ++b) {
+                const int ib = own_i(OW, b), q = own_q(OW, b);
+                if (q <= P) continue;   // compile-time after unrolling
+                const double x = -Lp[(4 * g + fk) * LD + 16 * ib - kMW * P + frow];
+                const double y = Lp[(4 * g + fk) * LD + 16 * q - kMW * P + frow];
+                acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc[b], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < NBk; ++b)
+            if (own_q(OW, b) == P + 1 || (P == 1 && own_q(OW, b) == 3))
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    *mp_s(M, 16 * own_i(OW, b) + (lane >> 4) + 4 * r, 16 * own_q(OW, b) + (lane & 15)) = acc[b][r];
+        lds_signal(cnt + OW, P + 1);   // in order after the block stores (one wave's LDS ops are ordered)
+    };
+    panel(std::integral_constant<int, 0>());
+    panel(std::integral_constant<int, 1>());
+}
+
+// V_P = L_PP^{-1} (wave 1, lane j = column j; lanes >= 16 compute zeros) into W block (P, P)
+template <int P>
+__device__ __forceinline__ void mp_inverse(const MpLds& M, const double* __restrict__ rinv, const int* cnt, int lane) {
+    constexpr int LD = mp_ld(P);
+    const double* Lp = M.Lc + mp_base(P);   // row 16P + k of column 16P + J at Lp[J * LD + k]
+    double y[kMW];
+#pragma unroll
+    for (int k = 0; k < kMW; ++k) y[k] = (k == lane) ? 1.0 : 0.0;
+    auto step = [&](auto jc) {
+        constexpr int J = decltype(jc)::value, K0 = J, NR = (kMW - K0) / 2;
+        wait_lds_ge(cnt, kMW * P + J + 2);
+        double2 c0[NR], c1[NR];
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+            c0[q] = *reinterpret_cast<const double2*>(Lp + J * LD + K0 + 2 * q);
+            c1[q] = *reinterpret_cast<const double2*>(Lp + (J + 1) * LD + K0 + 2 * q);
+        }
+        const double r0 = rinv[kMW * P + J], r1 = rinv[kMW * P + J + 1];
+        __builtin_amdgcn_sched_barrier(0);
+        const double w0 = y[J] * r0;
+        y[J] = w0;
+        y[J + 1] = fma(-c0[0].y, w0, y[J + 1]);
+        const double w1 = y[J + 1] * r1;
+        y[J + 1] = w1;
+#pragma unroll
+        for (int q = 1; q < NR; ++q) {
+            const int k = K0 + 2 * q;
+            y[k] = fma(-c0[q].x, w0, y[k]);
+            y[k + 1] = fma(-c0[q].y, w0, y[k + 1]);
+            y[k] = fma(-c1[q].x, w1, y[k]);
+            y[k + 1] = fma(-c1[q].y, w1, y[k + 1]);
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    step(std::integral_constant<int, 0>());
+    step(std::integral_constant<int, 2>());
+    step(std::integral_constant<int, 4>());
+    step(std::integral_constant<int, 6>());
+    step(std::integral_constant<int, 8>());
+    step(std::integral_constant<int, 10>());
+    step(std::integral_constant<int, 12>());
+    step(std::integral_constant<int, 14>());
+    // lanes >= 16 (zero columns) store into the discard block: one base, immediate offsets
+    double* dst = (lane < kMW ? M.Wb + lblk(P, P) * kBlk : M.disc) + (lane & 15);
+#pragma unroll
+    for (int k = 0; k < kMW; ++k) dst[k * kBP] = y[k];
+}
+
+// acc += L_{I,K} W_{K,J} (K = 16): L from micro-panel K's columns, W from its block
+template <int I, int K, int J>
+__device__ __forceinline__ d4 mp_lw(d4 acc, const MpLds& M, int lane) {
+    const double* Lp = M.Lc + mp_base(K);
+    const double* Wk = M.Wb + lblk(K, J) * kBlk;
+    return mfma_blk<16>(acc, [&](int i, int k) { return Lp[k * mp_ld(K) + 16 * (I - K) + i]; },
+                        [&](int j, int k) { return Wk[k * kBP + j]; }, lane);
+}
+// W_{I,J} = -V_I X (X a block in LDS) into W block (I, J)
+template <int I, int J>
+__device__ __forceinline__ void mp_vx(const MpLds& M, const double* __restrict__ X, int lane) {
+    const double* Vi = M.Wb + lblk(I, I) * kBlk;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    acc = mfma_blk<16>(acc, [&](int i, int k) { return -Vi[i * kBP + k]; }, [&](int j, int k) { return X[k * kBP + j]; },
+                       lane);
+    blk_put(M.Wb + lblk(I, J) * kBlk, acc, lane);
+}
+
+template <bool STAMP = false, bool SC1 = false, class EARLY = NoEarly>
+__device__ __forceinline__ void factor_diag16(const DiagLds& L, double* __restrict__ rinv, int* cnt,
+                                              double* __restrict__ Wd, int d, int* info, long long* st = nullptr,
+                                              const EARLY& early = EARLY(), double* __restrict__ Wst = nullptr) {
+    const int t = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+    const MpLds M = mp_lds(L);
+    if (wave == 0) {
+        mp_panel<0, STAMP>(M, rinv, cnt, lane, d, info, st);
+        mp_panel<1, STAMP>(M, rinv, cnt, lane, d, info, st);
+        mp_panel<2, STAMP>(M, rinv, cnt, lane, d, info, st);
+        mp_panel<3, STAMP>(M, rinv, cnt, lane, d, info, st);
+        if constexpr (STAMP) st[8] = __builtin_amdgcn_s_memtime();
+        wait_lds_ge(cnt + 4, 1);
+        mp_vx<3, 0>(M, M.Xs, lane);
+        mp_vx<3, 1>(M, M.Xs + kBlk, lane);
+        if constexpr (STAMP) st[9] = __builtin_amdgcn_s_memtime();
+    } else if (wave == 1) {
+        const d4 z = {0.0, 0.0, 0.0, 0.0};
+        mp_inverse<0>(M, rinv, cnt, lane);
+        d4 x10 = mp_lw<1, 0, 0>(z, M, lane), x20 = mp_lw<2, 0, 0>(z, M, lane), x30 = mp_lw<3, 0, 0>(z, M, lane);
+        mp_inverse<1>(M, rinv, cnt, lane);
+        if constexpr (STAMP) st[10] = __builtin_amdgcn_s_memtime();
+        blk_put(M.Xs, x10, lane);
+        mp_vx<1, 0>(M, M.Xs, lane);
+        lds_signal(cnt + 1, 1);   // W rows 0 .. 31 (blocks (0,0), (1,0), (1,1)) are final
+        d4 x21 = mp_lw<2, 1, 1>(z, M, lane), x31 = mp_lw<3, 1, 1>(z, M, lane);
+        x20 = mp_lw<2, 1, 0>(x20, M, lane);
+        x30 = mp_lw<3, 1, 0>(x30, M, lane);
+        mp_inverse<2>(M, rinv, cnt, lane);
+        if constexpr (STAMP) st[11] = __builtin_amdgcn_s_memtime();
+        blk_put(M.Xs, x20, lane);
+        blk_put(M.Xs + kBlk, x21, lane);
+        mp_vx<2, 0>(M, M.Xs, lane);
+        mp_vx<2, 1>(M, M.Xs + kBlk, lane);
+        d4 x32 = mp_lw<3, 2, 2>(z, M, lane);
+        x30 = mp_lw<3, 2, 0>(x30, M, lane);
+        x31 = mp_lw<3, 2, 1>(x31, M, lane);
+        blk_put(M.Xs, x30, lane);   // after mp_vx<2, *>'s reads of Xs (one wave's LDS ops are ordered)
+        blk_put(M.Xs + kBlk, x31, lane);
+        blk_put(M.Xs + 2 * kBlk, x32, lane);
+        mp_inverse<3>(M, rinv, cnt, lane);
+        lds_signal(cnt + 4, 1);
+        if constexpr (STAMP) st[12] = __builtin_amdgcn_s_memtime();
+        mp_vx<3, 2>(M, M.Xs + 2 * kBlk, lane);
+    } else {
+        if (wave == 2) mp_owner<2>(M, cnt, lane);
+        else mp_owner<3>(M, cnt, lane);
+        wait_lds_ge(cnt + 1, 1);   // EarlyNext reads W rows 0..31
+        early(wave, lane);
+    }
+    __syncthreads();
+    if constexpr (STAMP) if (wave == 0) st[13] = __builtin_amdgcn_s_memtime();
+    // W_d to HBM: thread t writes row t >> 2, columns 16 (t & 3) .. +16 (zeros above the diagonal
+    // blocks); with Wst, the same values also go to LDS in the substage layout (the next tile's
+    // L = A W^T operand: late_prepare reads rows 32..63, diag_prepare all of it).  Wst overlaps
+    // the column and W areas: every value is read before the barrier.
+    {
+        const int row = t >> 2, jb = t & 3, ib = row >> 4;
+        const double* src = M.Wb + lblk(ib, jb <= ib ? jb : 0) * kBlk + (row & 15) * kBP;
+        double v[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) v[c] = jb <= ib ? src[c] : 0.0;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) stg<SC1>(Wd + row * NB + 16 * jb + c, v[c]);
+        if (Wst) {
+            __syncthreads();
+            double2* dst = reinterpret_cast<double2*>(Wst + jb * kSub + row * kPad);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) dst[c] = make_double2(v[2 * c], v[2 * c + 1]);
+        }
+    }
+}
+
+template <bool STAMP = false, bool SC1 = false, class EARLY = NoEarly>
+__device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict__ rinv, int* cnt,
+                                            double* __restrict__ Wd, int d, int* info, long long* st = nullptr,
+                                            const EARLY& early = EARLY(), double* __restrict__ Wst = nullptr) {
+#if PNOL_CHOL_MP
+    factor_diag16<STAMP, SC1, EARLY>(L, rinv, cnt, Wd, d, info, st, early, Wst);
+#else
+    factor_diag32<STAMP, SC1, EARLY>(L, rinv, cnt, Wd, d, info, st, early, Wst);
+#endif
+}
+
 // ---- the diagonal workgroup's two products, balanced over its 4 waves --------------------
 // L = A_{d,k} W_k^T with W_k lower triangular: wave w forms the 16-row strip w of L; output
 // block column jb needs only K blocks kb <= jb, so every wave issues 4 (1 + 2 + 3 + 4) = 40
@@ -716,14 +1129,16 @@ __device__ __forceinline__ void chol_tl_mark(int k, int cls, unsigned long long 
 // The diagonal tile d = k + 1 (k >= 0) ready for factor_diag: L = A_{d,k} W_k^T (recomputed
 // here rather than waited for), A_dd - L L^T on its 10 lower 16 x 16 blocks, into the split LDS
 // copy L.  X / Y: the two staging areas (smem, smem + kStage).
+// w_in_lds: Y already holds W_k in the substage layout (the previous factor_diag16 of the chain
+// left it there), so only A_{d,k} is staged.
 template <bool SC1 = false>
 __device__ __forceinline__ void diag_prepare(const double* __restrict__ P, long ldp, const double* __restrict__ W,
                                              int k, double* __restrict__ X, double* __restrict__ Y, const DiagLds& L,
-                                             int wave, int lane) {
+                                             int wave, int lane, bool w_in_lds = false) {
     const int d0 = (k + 1) * NB;
     const int k0 = k * NB;
     stage_tile<SC1>(X, P, ldp, d0, k0);
-    stage_tile<SC1>(Y, W + (long)k * NB * NB, NB, 0, 0);
+    if (!w_in_lds) stage_tile<SC1>(Y, W + (long)k * NB * NB, NB, 0, 0);
     d4 cdd[3];   // this wave's lower blocks of A_dd, in flight during the first product
 #pragma unroll
     for (int sb = 0; sb < 3; ++sb) {
@@ -803,7 +1218,7 @@ struct EarlyNext {
     long ldp;
     int T, d;
     const int* ver;
-    const double* W11;   // L.W11 of the tile being factored (row stride kS)
+    const double* W11;   // W_d rows 0..31 of the tile being factored (diag_w11, read by w11_at)
     const int* cnt;      // factor_diag's column counter (wave 0's progress)
     int cutoff;          // give up once cnt reaches this (> 64: wait for the tiles)
     EarlyLds E;
@@ -870,7 +1285,7 @@ struct EarlyNext {
                     const double a = E.pfx[kb * kSub + (strip * 16 + frow) * kPad + kk * 4 + fk];
 #pragma unroll
                     for (int jb = kb; jb < 2; ++jb) {
-                        const double b = W11[(jb * 16 + frow) * kS + kb * 16 + kk * 4 + fk];
+                        const double b = w11_at(W11, jb * 16 + frow, kb * 16 + kk * 4 + fk);
                         acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[jb], 0, 0, 0);
                     }
                 }
@@ -1191,16 +1606,17 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             if (t == 0 && k + 1 < 64) g_chol_clk[8 * (k + 1) + 6] = pre ? 1 : 0;
 #endif
             if (pre) late_prepare(E, Y, L, wave, lane);
-            else diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane);
+            else diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane, PNOL_CHOL_MP && d > 1);
             if (t < 6) cnt[t] = 0;   // every read of cnt / ew above is behind a barrier inside
             if (t < 4) ew[t] = 0;    // either prepare
             __syncthreads();
             PNOL_CHOL_STAMP(k, 3)
             if (lookahead)
                 factor_diag<false, true, EarlyNext>(L, rinv, cnt, W + (long)d * NB * NB, d, info, nullptr,
-                                                    EarlyNext{P, ldp, T, d, pw.ver, L.W11, cnt, lookahead, E}, Y);
-            else
-                factor_diag<false, true>(L, rinv, cnt, W + (long)d * NB * NB, d, info);
+                                                    EarlyNext{P, ldp, T, d, pw.ver, diag_w11(L), cnt, lookahead, E}, Y);
+            else   // micro-panel factor: W_d also stays in Y for the next diag_prepare
+                factor_diag<false, true>(L, rinv, cnt, W + (long)d * NB * NB, d, info, nullptr, NoEarly(),
+                                         PNOL_CHOL_MP ? Y : nullptr);
             PNOL_CHOL_STAMP(k, 4)
             publish(pw.wdone + d, 1);   // its barrier also ends every read of this step's LDS
             PNOL_CRIT(d, 0)

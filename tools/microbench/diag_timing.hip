@@ -67,10 +67,17 @@ int main() {
     unsigned long long h = 1469598103934665603ULL;   // FNV-1a of W's bits (A/B builds must agree)
     for (double v : W) { unsigned long long u; memcpy(&u, &v, 8); h = (h ^ u) * 1099511628211ULL; }
     printf("{\"info\": %d, \"max|W A W^T - I|\": %.3e, \"w_hash\": \"%016llx\", \"cycles\": {", info, err, h);
+#if PNOL_CHOL_MP
+    const char* names[] = {"p0_j0", "p0_j8", "p1_j0", "p1_j8", "p2_j0", "p2_j8", "p3_j0", "p3_j8", "chain_end",
+                           "w30_w31_end", "v1_end", "v2_end", "v3_end", "barrier"};
+    const int nn = 14;
+#else
     const char* names[] = {"p1_j0", "p1_j8", "p1_j16", "p1_j24", "p1_end", "w11_end", "p2_q00_end", "-", "p3_start",
                            "p3_j0", "p3_j8", "p3_j16", "p3_j24", "p3_end", "w22_end", "b3", "p4_end"};
-    for (int i = 0; i < 17; ++i)
-        if (i != 7) printf("%s\"%s\": %lld", i ? ", " : "", names[i], st[i] ? st[i] - b : -1LL);
+    const int nn = 17;
+#endif
+    for (int i = 0; i < nn; ++i)
+        if (names[i][0] != '-') printf("%s\"%s\": %lld", i ? ", " : "", names[i], st[i] ? st[i] - b : -1LL);
     printf("}}\n");
     return (info == 0 && err < 1e-12) ? 0 : 1;
 }
