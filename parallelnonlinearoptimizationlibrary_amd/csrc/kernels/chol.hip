@@ -655,7 +655,7 @@ __device__ __forceinline__ void factor_diag32(const DiagLds& L, double* __restri
 // micro-panel 1 is in registers.  Words: cnt[0] final columns, cnt[1] W rows 0..31 done,
 // cnt[2] / cnt[3] waves 2 / 3 have stored micro-panel cnt's blocks, cnt[4] V_3 and X_3j in LDS.
 #ifndef PNOL_CHOL_MP
-#define PNOL_CHOL_MP 0
+#define PNOL_CHOL_MP 1
 #endif
 constexpr int kMW = 16;            // micro-panel width
 constexpr int kBP = 18;            // row stride of a 16 x 16 block in LDS (conflict-free fragments)
@@ -1012,23 +1012,25 @@ __device__ __forceinline__ void factor_diag16(const DiagLds& L, double* __restri
     }
     __syncthreads();
     if constexpr (STAMP) if (wave == 0) st[13] = __builtin_amdgcn_s_memtime();
-    // W_d to HBM: thread t writes row t >> 2, columns 16 (t & 3) .. +16 (zeros above the diagonal
-    // blocks); with Wst, the same values also go to LDS in the substage layout (the next tile's
-    // L = A W^T operand: late_prepare reads rows 32..63, diag_prepare all of it).  Wst overlaps
-    // the column and W areas: every value is read before the barrier.
+    // W_d to HBM: wave w writes rows 16 w .. 16 w + 15, lane = column (each store one coalesced
+    // 512-byte row; zeros above the diagonal blocks); with Wst, the same values also go to LDS in
+    // the substage layout (the next tile's L = A W^T operand: late_prepare reads rows 32..63,
+    // diag_prepare all of it).  Wst overlaps the column and W areas: every value is read before
+    // the barrier.
     {
-        const int row = t >> 2, jb = t & 3, ib = row >> 4;
-        const double* src = M.Wb + lblk(ib, jb <= ib ? jb : 0) * kBlk + (row & 15) * kBP;
+        const int jb = lane >> 4, c = lane & 15;
         double v[16];
 #pragma unroll
-        for (int c = 0; c < 16; ++c) v[c] = jb <= ib ? src[c] : 0.0;
+        for (int q = 0; q < 16; ++q) {
+            const int ib = wave;
+            v[q] = jb <= ib ? M.Wb[lblk(ib, jb <= ib ? jb : 0) * kBlk + q * kBP + c] : 0.0;
+        }
 #pragma unroll
-        for (int c = 0; c < 16; ++c) stg<SC1>(Wd + row * NB + 16 * jb + c, v[c]);
+        for (int q = 0; q < 16; ++q) stg<SC1>(Wd + (16 * wave + q) * NB + lane, v[q]);
         if (Wst) {
             __syncthreads();
-            double2* dst = reinterpret_cast<double2*>(Wst + jb * kSub + row * kPad);
 #pragma unroll
-            for (int c = 0; c < 8; ++c) dst[c] = make_double2(v[2 * c], v[2 * c + 1]);
+            for (int q = 0; q < 16; ++q) Wst[jb * kSub + (16 * wave + q) * kPad + c] = v[q];
         }
     }
 }
