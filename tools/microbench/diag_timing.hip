@@ -28,6 +28,32 @@ __global__ __launch_bounds__(256, 2) void k_diag_time(const double* A, double* W
     factor_diag<true>(L, rinv, cnt, W, 0, info, st);
 }
 
+#if PNOL_CHOL_MP
+// wave 0's chain alone (waves 1..3 idle, the owners' words preset): the pivot chain's cost
+// without the other waves' LDS polling and MFMA traffic beside it
+__global__ __launch_bounds__(256, 2) void k_chain_solo(const double* A, int* info, long long* st) {
+    using namespace pnol;
+    __shared__ __attribute__((aligned(16))) double smem[2 * kStage];
+    __shared__ double rinv[NB];
+    __shared__ int cnt[6];
+    const int t = threadIdx.x;
+    const DiagLds L = diag_lds(smem);
+    if (t < 6) cnt[t] = t >= 2 ? 99 : 0;
+    const int row = t >> 2, c0 = (t & 3) * 16;
+    for (int q = 0; q < 16; ++q) diag_put(L, row, c0 + q, A[row * 64 + c0 + q]);
+    __syncthreads();
+    if (t >= 64) return;
+    const MpLds M = mp_lds(L);
+    const int lane = t;
+    if (t == 0) st[31] = __builtin_amdgcn_s_memtime();
+    mp_panel<0, true>(M, rinv, cnt, lane, 0, info, st);
+    mp_panel<1, true>(M, rinv, cnt, lane, 0, info, st);
+    mp_panel<2, true>(M, rinv, cnt, lane, 0, info, st);
+    mp_panel<3, true>(M, rinv, cnt, lane, 0, info, st);
+    if (t == 0) st[8] = __builtin_amdgcn_s_memtime();
+}
+#endif
+
 int main() {
     const int n = 64;
     std::vector<double> M(n * n), A(n * n);
@@ -78,6 +104,16 @@ int main() {
 #endif
     for (int i = 0; i < nn; ++i)
         if (names[i][0] != '-') printf("%s\"%s\": %lld", i ? ", " : "", names[i], st[i] ? st[i] - b : -1LL);
-    printf("}}\n");
+    printf("}");
+#if PNOL_CHOL_MP
+    hipMemset(dst, 0, 8 * 32);
+    for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(k_chain_solo, dim3(1), dim3(256), 0, 0, dA, dinfo, dst);
+    hipDeviceSynchronize();
+    hipMemcpy(st.data(), dst, 8 * 32, hipMemcpyDeviceToHost);
+    printf(", \"chain_solo\": {");
+    for (int i = 0; i < 9; ++i) printf("%s\"%s\": %lld", i ? ", " : "", names[i], st[i] - st[31]);
+    printf("}");
+#endif
+    printf("}\n");
     return (info == 0 && err < 1e-12) ? 0 : 1;
 }
