@@ -31,6 +31,11 @@ if [ "${PMC:-1}" = "1" ]; then
       python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-bfgs > /tmp/pmc_fetch.log 2>&1
   step pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d /tmp/pmc_write -o pmc --output-format csv -- \
       python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-bfgs > /tmp/pmc_write.log 2>&1
+  # the sliced SYRK an N > 1 rank runs (k_syrk_tile<4, 64>), in one process over all 8 m-slices
+  step pmc_fetch_sliced 300 rocprofv3 --pmc FETCH_SIZE -d /tmp/pmc_fetch -o probe --output-format csv -- \
+      python tools/syrk_sliced_probe.py 3 > /tmp/pmc_fetch_sliced.log 2>&1
+  step pmc_write_sliced 300 rocprofv3 --pmc WRITE_SIZE -d /tmp/pmc_write -o probe --output-format csv -- \
+      python tools/syrk_sliced_probe.py 3 > /tmp/pmc_write_sliced.log 2>&1
   python3 tools/pmc_traffic.py /tmp/pmc_fetch /tmp/pmc_write gpurun_out/pmc_traffic.json
 fi
 if [ "${MFMA:-1}" = "1" ]; then
