@@ -24,7 +24,7 @@ def main():
     h = ctx.tensor(np.full(n, 1e-7))
     F0, JTs = d.lm_jacobian_mpi(x, h)
     for _ in range(reps):
-        A, r, _ = ctx.lm_normal_mpi(JTs, m, n, 0.37, F0, want_diag=False)
+        A, r = ctx.lm_normal_mpi(JTs, m, n, 0.37, F0)
     ctx.synchronize()
     print(f"sliced J^T J m={m} n={n}: A[0,0]={float(A[0, 0]):.6e}")
 
