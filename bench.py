@@ -596,10 +596,12 @@ def main():
             "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "flop_per_launch": jtj_flop, "rows": jtj_rows,
             # one GPU: the PMC passes of this bench; N > 1: the PMC passes of the sliced kernel over
-            # all 8 m-slices in one process (tools/syrk_sliced_probe.py), times this rank's rows / m
+            # all 8 m-slices in one process (tools/syrk_sliced_probe.py, the metric's m and n), times
+            # this rank's rows / m; other sizes have no committed pass (null)
             "traffic": (pmc.get("k_syrk_tile<0, 128>", {}).get("traffic_bytes_per_launch") if one_gpu else
                         (pmc["k_syrk_tile<4, 64>"]["traffic_bytes_per_launch"] * jtj_rows / m
-                         if "traffic_bytes_per_launch" in pmc.get("k_syrk_tile<4, 64>", {}) else None)),
+                         if (m, n) == (M_RES, N_PAR) and "traffic_bytes_per_launch" in pmc.get("k_syrk_tile<4, 64>", {})
+                         else None)),
             "mfma_busy_pmc": next((v.get("mfma_busy_frac") for k, v in pmc_valu("syrk_mfma").items()
                                    if "k_syrk_tile" in k), None) if one_gpu else None,
         }
