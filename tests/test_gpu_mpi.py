@@ -102,6 +102,28 @@ def test_levmarq_mpi_fd_modes_bitwise(tmp_path, monkeypatch, mode, world, m, n):
         assert np.array_equal(z["F0"], F01) and np.array_equal(z["FO"], FO1), (mode, r)
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_levmarq_mpi_cfg4_full_size_bitwise(tmp_path, monkeypatch, world):
+    """cfg 4's decomposition at the headline size (m = 16384, n = 2048;
+    LevenbergMarquardtMPI.cpp:12-172 with the FD Jacobian of PNOL_Objective.cpp:202-299): rows
+    mode over 2 and 4 ranks (sharing the box's GPU, host communicator) gives X, F0 and FOpt after
+    5 trips bitwise equal to the one-GPU LevMarq, which test_lm_cfg3_full_size_matches_oracle_trips
+    holds to the oracle's trips."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_levmarq
+    m, n = 16384, 2048
+    monkeypatch.delenv("PNOL_LM_FD", raising=False)
+    _run_workers(tmp_path, world, m, n, "lm")
+    ctx = Context(0)
+    obj = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+    X1, F01, FO1, _ = run_levmarq(obj, np.zeros(n), (0.001, 10.0, 1e-7, 5, 0.0, -1), which=0)
+    obj.close()
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        assert np.array_equal(z["X"], X1), r
+        assert np.array_equal(z["F0"], F01) and np.array_equal(z["FO"], FO1), r
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_levmarq_mpi_ranks_bitwise_equal_single(tmp_path, world, oracle):
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
