@@ -657,6 +657,10 @@ __device__ __forceinline__ void factor_diag32(const DiagLds& L, double* __restri
 #ifndef PNOL_CHOL_MP
 #define PNOL_CHOL_MP 1
 #endif
+// k_chol_persist: row k+2's panel task also applies column k to tiles (k+2, k+1) and (k+2, k+2)
+#ifndef PNOL_CHOL_FUSE
+#define PNOL_CHOL_FUSE 0
+#endif
 constexpr int kMW = 16;            // micro-panel width
 constexpr int kBP = 18;            // row stride of a 16 x 16 block in LDS (conflict-free fragments)
 constexpr int kBlk = 16 * kBP;     // doubles per block
@@ -1056,17 +1060,26 @@ __device__ __forceinline__ void diag_l_strip(d4 (&acc)[4], const double* __restr
     const int frow = lane & 15, fk = lane >> 4;
 #pragma unroll
     for (int jb = 0; jb < 4; ++jb) acc[jb] = d4{0.0, 0.0, 0.0, 0.0};
+    // every operand read from LDS before the first MFMA: one wait instead of one LDS round trip
+    // per K step (the MFMAs and their order are unchanged)
+    double a[4][4], b[10][4];   // b: the pairs (kb, jb <= kb .. 3) in order
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
-            const double a = X[kb * kSub + (w * 16 + frow) * kPad + kk * 4 + fk];
+            a[kb][kk] = X[kb * kSub + (w * 16 + frow) * kPad + kk * 4 + fk];
 #pragma unroll
-            for (int jb = kb; jb < 4; ++jb) {
-                const double b = Y[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
-                acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[jb], 0, 0, 0);
-            }
+            for (int jb = kb; jb < 4; ++jb)
+                b[kb * 4 - kb * (kb - 1) / 2 + jb - kb][kk] = Y[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
         }
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+            for (int jb = kb; jb < 4; ++jb)
+                acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kb][kk], b[kb * 4 - kb * (kb - 1) / 2 + jb - kb][kk], acc[jb],
+                                                               0, 0, 0);
 }
 
 // the strip into LDS in the substage layout (L as the operand of the second product)
@@ -1112,6 +1125,11 @@ __device__ unsigned long long g_chol_clk[64 * 8];   // the diagonal workgroup's 
 // [2] flags ok [3] stored; update (k+2, k+1, k) [4] claimed [5] flags ok [6] stored; [7] panel
 // (k+1, k) stored
 __device__ unsigned long long g_chol_crit[64 * 8];
+// the chain's look-ahead inside step d's factor (wave 2, shader clock): [0] polling starts,
+// [1] tiles ready, [2] staged in LDS, [3] its MFMAs done
+__device__ unsigned long long g_chol_la[64 * 4];
+#define PNOL_LA_STAMP(d, i) \
+    if (threadIdx.x == 128 && (d) < 64) g_chol_la[4 * (d) + (i)] = __builtin_amdgcn_s_memtime();
 #define PNOL_CRIT(k, i) \
     if (threadIdx.x == 0 && (k) >= 0 && (k) < 64) g_chol_crit[8 * (k) + (i)] = __builtin_amdgcn_s_memrealtime();
 #define PNOL_CHOL_STAMP(k, i) \
@@ -1126,6 +1144,7 @@ __device__ __forceinline__ void chol_tl_mark(int k, int cls, unsigned long long 
 #else
 #define PNOL_CHOL_STAMP(k, i)
 #define PNOL_CRIT(k, i)
+#define PNOL_LA_STAMP(d, i)
 #endif
 
 // The diagonal tile d = k + 1 (k >= 0) ready for factor_diag: L = A_{d,k} W_k^T (recomputed
@@ -1163,14 +1182,18 @@ __device__ __forceinline__ void diag_prepare(const double* __restrict__ P, long 
     for (int sb = 0; sb < 3; ++sb) {           // A_dd - L L^T, lower blocks
         const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
         if (bl < 0) continue;                   // wave-uniform
+        double fa[4][4], fb[4][4];              // the block's operands, read before its MFMAs
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
-                const double a = -X[kb * kSub + (ib * 16 + frow) * kPad + kk * 4 + fk];
-                const double b = X[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
-                cdd[sb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, cdd[sb], 0, 0, 0);
+                fa[kb][kk] = -X[kb * kSub + (ib * 16 + frow) * kPad + kk * 4 + fk];
+                fb[kb][kk] = X[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
             }
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) cdd[sb] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[kb][kk], fb[kb][kk], cdd[sb], 0, 0, 0);
     }
     __syncthreads();                            // X / Y are rewritten below
 #pragma unroll
@@ -1228,6 +1251,7 @@ struct EarlyNext {
         const int dn = d + 1;
         if (dn >= T) return;
         if (wave == 2) {
+            PNOL_LA_STAMP(d, 0)
             int ready = 0;
             for (int it = 0;; ++it) {
                 ready = __hip_atomic_load(ver + dn * T + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= d &&
@@ -1236,6 +1260,7 @@ struct EarlyNext {
                 if (ready || it > 4096 || lds_peek(cnt) >= cutoff) break;
                 __builtin_amdgcn_s_sleep(1);
             }
+            PNOL_LA_STAMP(d, 1)
             lds_signal(E.w, ready ? 1 : 2);
         } else {
             wait_lds_ge(E.w, 1);
@@ -1274,51 +1299,79 @@ struct EarlyNext {
                 *reinterpret_cast<double2*>(E.pfc + (5 * h + (q >> 1)) * 256 + row * 16 + col) = u[q];
             }
         }
+        PNOL_LA_STAMP(d, 2)
         const int frow = lane & 15, fk = lane >> 4;
+        // Every MFMA operand of a phase is read from LDS before its first MFMA (one wait, not one
+        // LDS round trip per K step); each accumulator takes the same MFMAs in the same order.
         // L's left half for this wave's strips (block columns jb = 0, 1: K blocks kb <= jb)
+        {
+            double av[2][2][4], bw[3][4];   // av[s][kb][kk]; bw: (kb, jb) = (0, 0), (0, 1), (1, 1)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int strip = 2 * h + s;
-            d4 acc[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+            for (int kk = 0; kk < 4; ++kk) {
+                bw[0][kk] = w11_at(W11, frow, kk * 4 + fk);
+                bw[1][kk] = w11_at(W11, 16 + frow, kk * 4 + fk);
+                bw[2][kk] = w11_at(W11, 16 + frow, 16 + kk * 4 + fk);
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
+                for (int s = 0; s < 2; ++s)
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) {
-                    const double a = E.pfx[kb * kSub + (strip * 16 + frow) * kPad + kk * 4 + fk];
+                    for (int kb = 0; kb < 2; ++kb)
+                        av[s][kb][kk] = E.pfx[kb * kSub + ((2 * h + s) * 16 + frow) * kPad + kk * 4 + fk];
+            }
 #pragma unroll
-                    for (int jb = kb; jb < 2; ++jb) {
-                        const double b = w11_at(W11, jb * 16 + frow, kb * 16 + kk * 4 + fk);
-                        acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[jb], 0, 0, 0);
-                    }
-                }
+            for (int s = 0; s < 2; ++s) {
+                const int strip = 2 * h + s;
+                d4 acc[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
 #pragma unroll
-            for (int jb = 0; jb < 2; ++jb)
+                for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    E.pll[jb * kSub + (strip * 16 + (lane >> 4) + 4 * r) * kPad + (lane & 15)] = acc[jb][r];
+                    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                        for (int jb = kb; jb < 2; ++jb)
+                            acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s][kb][kk], bw[kb + jb][kk], acc[jb], 0, 0, 0);
+#pragma unroll
+                for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        E.pll[jb * kSub + (strip * 16 + (lane >> 4) + 4 * r) * kPad + (lane & 15)] = acc[jb][r];
+            }
         }
         lds_signal(E.w + 1 + h, 1);
         wait_lds_ge(E.w + 2 - h, 1);
-        // this wave's five blocks of A_dd - L_left L_left^T (K blocks 0, 1)
+        // this wave's five blocks of A_dd - L_left L_left^T (K blocks 0, 1): the fragments of the
+        // row blocks they touch, then the blocks
+        auto llt = [&](auto hc) {
+            constexpr int H = decltype(hc)::value, RB = H == 0 ? 3 : 4;
+            double fr[RB][2][4];
+            d4 c[5];
 #pragma unroll
-        for (int q = 0; q < 5; ++q) {
-            const int b = 5 * h + q;
-            int ib, jb;
-            blk_ij(b, ib, jb);
-            d4 c;
+            for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) c[r] = E.pfc[b * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15)];
+                for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
+                    for (int kk = 0; kk < 4; ++kk) fr[rb][kb][kk] = E.pll[kb * kSub + (rb * 16 + frow) * kPad + kk * 4 + fk];
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) {
-                    const double a = -E.pll[kb * kSub + (ib * 16 + frow) * kPad + kk * 4 + fk];
-                    const double bb = E.pll[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
-                    c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, c, 0, 0, 0);
-                }
+            for (int q = 0; q < 5; ++q)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) E.pfc[b * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15)] = c[r];
-        }
+                for (int r = 0; r < 4; ++r) c[q][r] = E.pfc[(5 * H + q) * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15)];
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                constexpr int b0 = 5 * H;
+                const int b = b0 + q;
+                const int ib = b >= 6 ? 3 : (b >= 3 ? 2 : (b >= 1 ? 1 : 0)), jb = b - ib * (ib + 1) / 2;
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk)
+                        c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-fr[ib][kb][kk], fr[jb][kb][kk], c[q], 0, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) E.pfc[(5 * H + q) * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15)] = c[q][r];
+        };
+        if (h == 0) llt(std::integral_constant<int, 0>());
+        else llt(std::integral_constant<int, 1>());
+        PNOL_LA_STAMP(d, 3)
     }
 };
 
@@ -1328,42 +1381,61 @@ struct EarlyNext {
 __device__ __forceinline__ void late_prepare(const EarlyLds& E, const double* __restrict__ Wst, const DiagLds& L,
                                              int wave, int lane) {
     const int frow = lane & 15, fk = lane >> 4;
-    d4 lr[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+    // each phase's MFMA operands are read from LDS before its first MFMA (as in EarlyNext)
+    {
+        double a[4][4], b[7][4];   // b: (kb, jb) = (0,2) (0,3) (1,2) (1,3) (2,2) (2,3) (3,3)
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
+        for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const double a = E.pfx[kb * kSub + (wave * 16 + frow) * kPad + kk * 4 + fk];
+            for (int kk = 0; kk < 4; ++kk) {
+                a[kb][kk] = E.pfx[kb * kSub + (wave * 16 + frow) * kPad + kk * 4 + fk];
 #pragma unroll
-            for (int jb = (kb > 2 ? kb : 2); jb < 4; ++jb) {
-                const double b = Wst[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
-                lr[jb - 2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, lr[jb - 2], 0, 0, 0);
+                for (int jb = (kb > 2 ? kb : 2); jb < 4; ++jb)
+                    b[kb < 3 ? 2 * kb + jb - 2 : 6][kk] = Wst[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
             }
-        }
-    // this wave's own rows of substages 2, 3 (only it reads them above)
+        d4 lr[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
 #pragma unroll
-    for (int jb = 2; jb < 4; ++jb)
+        for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) E.pfx[jb * kSub + (wave * 16 + (lane >> 4) + 4 * r) * kPad + (lane & 15)] = lr[jb - 2][r];
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int jb = (kb > 2 ? kb : 2); jb < 4; ++jb)
+                    lr[jb - 2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kb][kk], b[kb < 3 ? 2 * kb + jb - 2 : 6][kk], lr[jb - 2], 0, 0, 0);
+        // this wave's own rows of substages 2, 3 (only it reads them above)
+#pragma unroll
+        for (int jb = 2; jb < 4; ++jb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                E.pfx[jb * kSub + (wave * 16 + (lane >> 4) + 4 * r) * kPad + (lane & 15)] = lr[jb - 2][r];
+    }
     __syncthreads();
+    double fa[3][2][4], fb[3][2][4];
+    d4 c[3];
+#pragma unroll
+    for (int sb = 0; sb < 3; ++sb) {
+        const int bl = diag_blk(wave, sb), ib = bl < 0 ? 0 : bl >> 2, jb = bl < 0 ? 0 : bl & 3;
+        const int b = ib * (ib + 1) / 2 + jb;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c[sb][r] = E.pfc[b * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15)];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                fa[sb][kb][kk] = -E.pfx[(kb + 2) * kSub + (ib * 16 + frow) * kPad + kk * 4 + fk];
+                fb[sb][kb][kk] = E.pfx[(kb + 2) * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
+            }
+    }
 #pragma unroll
     for (int sb = 0; sb < 3; ++sb) {
         const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
         if (bl < 0) continue;   // wave-uniform
-        const int b = ib * (ib + 1) / 2 + jb;
-        d4 c;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) c[r] = E.pfc[b * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15)];
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int kb = 2; kb < 4; ++kb)
+            for (int kk = 0; kk < 4; ++kk)
+                c[sb] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[sb][kb][kk], fb[sb][kb][kk], c[sb], 0, 0, 0);
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                const double a = -E.pfx[kb * kSub + (ib * 16 + frow) * kPad + kk * 4 + fk];
-                const double bb = E.pfx[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
-                c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, c, 0, 0, 0);
-            }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) diag_put(L, ib * 16 + (lane >> 4) + 4 * r, jb * 16 + (lane & 15), c[r]);
+        for (int r = 0; r < 4; ++r) diag_put(L, ib * 16 + (lane >> 4) + 4 * r, jb * 16 + (lane & 15), c[sb][r]);
     }
 }
 
@@ -1658,6 +1730,20 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             __syncthreads();
             if (!ok_sh) return;
             stage_tile<true>(X, P, ldp, i0, k0);
+            // row k+2 also applies column k to the two tiles the diagonal chain needs next
+            // (PNOL_CHOL_FUSE): (k+2, k+2) straight from this strip, (k+2, k+1) with panel k+1's
+            // strip -- the update tasks of those tiles are skipped.  Their tiles are loaded now,
+            // while the workgroup waits for W_k; their earlier updates and panel k+1 are tasks
+            // claimed before this one.
+            const bool fuse = PNOL_CHOL_FUSE && i == k + 2;
+            d4 accD[2][2], accO[2][2];
+            if (fuse) {
+                if (t == 0) ok_sh = spin_all<2>({pw.ver + i * T + i, pw.ver + i * T + (k + 1)}, {k, k}, info);
+                __syncthreads();
+                if (!ok_sh) return;
+                acc_load<true>(accD, P, ldp, i0, i0, wr, wc, lane);
+                acc_load<true>(accO, P, ldp, i0, k0 + NB, wr, wc, lane);
+            }
             if (t == 0) {   // W_k (tile 0 comes from the prep launch)
                 ok_sh = k == 0 || spin_ge(pw.wdone + k, 1, info);
 #ifdef PNOL_CHOL_TIMELINE
@@ -1671,11 +1757,52 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             d4 acc[4];   // this wave's 16-row strip of L_ik (nonzero K blocks of W_k^T only)
             diag_l_strip(acc, X, Y, wave, lane);
             strip_store<true>(acc, Lm, ldp, i0, k0, wave, lane);
-            publish(pw.lcnt + i, k + 1);
+            // the strip in the substage layout: the same values stage_tile reads back from Lm
+            if (fuse) diag_strip_to_stage(acc, pfx, wave, lane);
+            publish(pw.lcnt + i, k + 1);   // its barrier also covers the pfx stores
 #ifdef PNOL_CHOL_TIMELINE
             if (i == k + 2) PNOL_CRIT(k, 3)
             if (i == k + 1) PNOL_CRIT(k, 7)
 #endif
+            if (fuse) {   // the update tasks' arithmetic (mfma_xyt, X = L_ik, Y = L_jk)
+#ifdef PNOL_CHOL_TIMELINE
+                PNOL_CRIT(k, 4)
+#endif
+                if (t == 0) ok_sh = spin_ge(pw.lcnt + k + 1, k + 1, info);
+                __syncthreads();
+                if (!ok_sh) return;
+#ifdef PNOL_CHOL_TIMELINE
+                PNOL_CRIT(k, 5)
+#endif
+                // panel k+1's strip: the loads in flight while (k+2, k+2)'s MFMAs run
+                double2 lv[8];
+                {
+                    const double* base = Lm + (long)(k0 + NB) * ldp + k0;   // wave-uniform
+                    const unsigned off = (unsigned)(((t >> 2) * ldp + (t & 3) * 16) * 8);
+#pragma unroll
+                    for (int qq = 0; qq < 8; ++qq) lv[qq] = ld16_sc1(base, off + 16 * qq);
+                }
+                mfma_xyt<true>(accD, pfx, pfx, wr, wc, lane);
+                __builtin_amdgcn_sched_barrier(0);   // the MFMAs issue before the loads are waited on
+                {   // X (A_ik) is dead: every wave passed the barriers since diag_l_strip
+                    double2* dst = reinterpret_cast<double2*>(X + (t & 3) * kSub + (t >> 2) * kPad);
+#pragma unroll
+                    for (int qq = 0; qq < 8; ++qq) dst[qq] = lv[qq];
+                }
+                acc_store<true>(accD, P, ldp, i0, i0, wr, wc, lane);
+                __syncthreads();
+                mfma_xyt<true>(accO, pfx, X, wr, wc, lane);
+                acc_store<true>(accO, P, ldp, i0, k0 + NB, wr, wc, lane);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();   // also ends the reads of X before strip_to_rows
+                if (t == 0) {
+                    __hip_atomic_store(pw.ver + i * T + i, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(pw.ver + i * T + (k + 1), k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+#ifdef PNOL_CHOL_TIMELINE
+                PNOL_CRIT(k, 6)
+#endif
+            }
             strip_to_rows(acc, X, wave, lane);   // X is free (the MFMA finished before the barrier)
             if (t < NB) {
                 double s = 0.0;
@@ -1702,6 +1829,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         // (k+2, k+2) at f = R, and so on.  Step k's first two tasks are the tiles the chain needs
         // next, f = 1 = (k+2, k+1) and f = R = (k+2, k+2); the rest follow in column order.
         const int q = g - R;
+        if (PNOL_CHOL_FUSE && q < 2) continue;   // row k+2's panel task applied them
         int u = q == 0 ? 1 : (q == 1 ? R : (q < R ? q : q + 1));
         int j = k + 1;
         while (u >= T - j) {

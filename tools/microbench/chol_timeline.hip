@@ -58,6 +58,7 @@ int main(int argc, char** argv) {
         hipMemcpyToSymbol(HIP_SYMBOL(g_chol_clk), zero.data(), sizeof(unsigned long long) * zero.size());
         hipMemcpyToSymbol(HIP_SYMBOL(g_chol_tl), init.data(), sizeof(unsigned long long) * init.size());
         hipMemcpyToSymbol(HIP_SYMBOL(g_chol_crit), zero.data(), sizeof(unsigned long long) * zero.size());
+        hipMemcpyToSymbol(HIP_SYMBOL(g_chol_la), zero.data(), sizeof(unsigned long long) * 64 * 4);
         hipEventRecord(e0, ctx->stream);
         if (launch_chol_solve(ctx, A, n, b, x, n, info) != PNOL_OK) return 1;
         hipEventRecord(e1, ctx->stream);
@@ -95,6 +96,15 @@ int main(int argc, char** argv) {
                     (long long)(ck[8 * s + 7] - ck[8 * s]),
                     // persistent form: the end of the wait for the two tiles (0 in method 4)
                     ck[8 * s + 5] ? (long long)(ck[8 * s + 5] - ck[8 * s]) : 0LL, ck[8 * s + 6]);
+    }
+    std::vector<unsigned long long> la(64 * 4);
+    hipMemcpyFromSymbol(la.data(), HIP_SYMBOL(g_chol_la), sizeof(unsigned long long) * la.size());
+    // the look-ahead inside step s's factor, cycles from the factor's start: polling starts,
+    // tiles ready, staged, MFMAs done (-1: not run)
+    std::printf("], \"lookahead_cycles\": [");
+    for (int s = 1; s < T && s < 64; ++s) {
+        auto dc = [&](int i) { return la[4 * s + i] ? (long long)la[4 * s + i] - (long long)ck[8 * s + 3] : -1LL; };
+        std::printf("%s[%d, %lld, %lld, %lld, %lld]", s > 1 ? ", " : "", s, dc(0), dc(1), dc(2), dc(3));
     }
     std::vector<unsigned long long> cr(64 * 8);
     hipMemcpyFromSymbol(cr.data(), HIP_SYMBOL(g_chol_crit), sizeof(unsigned long long) * cr.size());
