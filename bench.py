@@ -457,10 +457,12 @@ def main():
                                 device_id=torch.device("cuda", local))
 
     m, n = args.residuals, args.params
-    # LevMarqMPI's Jacobian decomposition (csrc/kernels/fd.hip launch_lm_jacobian): rows mode by
-    # default (every FD column on the rank's own m-slices, no J exchange); PNOL_LM_FD=columns:
-    # cost-balanced FD column tiles + the m-slice exchange
-    rows_mode = os.environ.get("PNOL_LM_FD", "") != "columns"
+    # LevMarqMPI's Jacobian decomposition (csrc/kernels/fd.hip launch_lm_jacobian): columns mode,
+    # the reference's (cost-balanced FD column tiles per rank, each tile's m-slices exchanged
+    # while the next computes), is the headline; rows mode (every FD column on the rank's own
+    # m-slices, no J exchange; linear residuals only) is timed beside it at N > 1 as an extra
+    os.environ.pop("PNOL_LM_FD", None)
+    rows_mode = False
     ctx = Context(local)
     # the C++ drop-in classes run on the process default context: bind its timers
     dctx = C.c_void_p()
@@ -511,44 +513,68 @@ def main():
     # keeps only the timers of the kernels priced below (each timer adds two event records
     # between launches, ~1.5% of a trip with all of them on)
     names = ("fd_jtj", "fd_jacobian", "fd_ckpt", "linres_eval", "syrk", "syrk_rows", "syrk_reduce", "jtr", "solve",
-             "allgather", "exchange_J", "exchange_A", "exchange_F")
-    L.check(L.lib().pnol_ctx_enable_timers(dctx, 0 if args.no_timers else 1), "timers")
-    L.check(L.lib().pnol_ctx_reset_timers(dctx), "timers")
-    run(args.warmup)
-    torch.cuda.synchronize()
-    breakdown = {k: _timer(L, dctx, k) for k in names}
-    breakdown = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in breakdown.items()}
-    L.check(L.lib().pnol_ctx_enable_timers(dctx, 0 if args.no_timers else 2), "timers")
-    L.check(L.lib().pnol_ctx_reset_timers(dctx), "timers")
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    X = run(args.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=_red_dev())
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    timers = {k: _timer(L, dctx, k) for k in names}
-    # per-step kernel times, max over ranks (the slowest rank sets the pace)
-    per_local = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timers.items()}
-    # the checkpoint pass runs only when no slot holds x's checkpoints (the first trip; the
-    # trial-point evaluation and the two slots cover accepted and rejected steps): per trip
-    per_local["fd_ckpt_per_step"] = timers["fd_ckpt"][0] / max(args.steps, 1)
-    if world > 1:
-        keys = sorted(per_local)
-        tv = torch.tensor([per_local[k] for k in keys], dtype=torch.float64, device=_red_dev())
-        dist.all_reduce(tv, op=dist.ReduceOp.MAX)
-        per_max = dict(zip(keys, tv.tolist()))
-    else:
-        per_max = dict(per_local)
-    L.check(L.lib().pnol_ctx_enable_timers(dctx, 0), "timers")
+             "allgather", "exchange_J", "exchange_J_busy", "exchange_A", "exchange_F")
+
+    def timed_lm():
+        """W warmup trips (all timers: the breakdown), then K timed trips between barriers +
+        synchronize, max over ranks; per-step kernel times of this rank and max over ranks."""
+        L.check(L.lib().pnol_ctx_enable_timers(dctx, 0 if args.no_timers else 1), "timers")
+        L.check(L.lib().pnol_ctx_reset_timers(dctx), "timers")
+        run(args.warmup)
+        torch.cuda.synchronize()
+        bd = {k: _timer(L, dctx, k) for k in names}
+        bd = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in bd.items()}
+        L.check(L.lib().pnol_ctx_enable_timers(dctx, 0 if args.no_timers else 2), "timers")
+        L.check(L.lib().pnol_ctx_reset_timers(dctx), "timers")
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        Xr = run(args.steps)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64, device=_red_dev())
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        timers = {k: _timer(L, dctx, k) for k in names}
+        # per-step kernel times, max over ranks (the slowest rank sets the pace)
+        pl = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in timers.items()}
+        # the checkpoint pass runs only when no slot holds x's checkpoints (the first trip; the
+        # trial-point evaluation and the two slots cover accepted and rejected steps): per trip
+        pl["fd_ckpt_per_step"] = timers["fd_ckpt"][0] / max(args.steps, 1)
+        if world > 1:
+            keys = sorted(pl)
+            tv = torch.tensor([pl[k] for k in keys], dtype=torch.float64, device=_red_dev())
+            dist.all_reduce(tv, op=dist.ReduceOp.MAX)
+            pm = dict(zip(keys, tv.tolist()))
+        else:
+            pm = dict(pl)
+        L.check(L.lib().pnol_ctx_enable_timers(dctx, 0), "timers")
+        return el, Xr, bd, pl, pm, list(trips)
+
+    elapsed, X, breakdown, per_local, per_max, trips_main = timed_lm()
     err = float(np.max(np.abs(X - obj.xstar)) / np.max(np.abs(obj.xstar)))
+    rows_extra = None
+    if world > 1:
+        # rows mode beside the headline (labelled extra; linear residuals only): every rank the
+        # same environment, LevMarqMPI reads it once per solve and checks that the ranks agree
+        os.environ["PNOL_LM_FD"] = "rows"
+        el_r, X_r, _, pl_r, pm_r, tr_r = timed_lm()
+        os.environ.pop("PNOL_LM_FD", None)
+        rows_extra = {
+            "value": args.steps / el_r, "unit": "iters/s", "ms_per_step": el_r / args.steps * 1e3,
+            "fd_jacobian_ms_max_over_ranks": pm_r["fd_jacobian"] + pm_r["fd_ckpt_per_step"],
+            "exchange_F_ms_max_over_ranks": pm_r["exchange_F"],
+            "kernel_ms_per_step_max_over_ranks": pm_r, "trips_accepted": tr_r[0], "trips_rejected": tr_r[1],
+            "X_bitwise_equal_columns_mode": bool(np.array_equal(X_r, X)),
+            "note": ("LevMarqMPI rows mode (PNOL_LM_FD=rows): every FD column on the rank's own m-slices of "
+                     "residual rows, no J exchange; valid for the linear residual only (not the reference's "
+                     "decomposition) -- an extra, not the headline"),
+        }
+    trips[:] = trips_main
 
     hg_sharded = None
     if world > 1 and not args.no_hg:
@@ -634,6 +660,14 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(m, n)
         ms_per_step = elapsed / args.steps * 1e3
+        if world > 1:
+            transport = ("host communicator over gloo: one-GPU rehearsal" if args.host_comm else
+                         "RCCL p2p" if comm_backend == "rccl" else comm_backend)
+            workload = (f"LevenbergMarquardtMPI m={m} n={n}, FD columns in cost-balanced tiles over {world} GPUs, "
+                        f"each tile's J rows exchanged by m-slice behind its launch ({transport}), "
+                        f"J^T J + J^T F by m-slice + reduce-scatter/allgather")
+        else:
+            workload = f"LevenbergMarquardt m={m} n={n}, FD columns on 1 GPU"
         line = {
             "metric": f"LM iters/sec at m={m},n={n}",
             "value": args.steps / elapsed,
@@ -645,20 +679,21 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (splitmix64 seed 0x5EED2018, r(x)=Ax-y generated in HBM)",
-            "config": {"workload": f"LevenbergMarquardt{'MPI' if world > 1 else ''} m={m} n={n}, "
-                                   f"FD columns {((('all of them on each rank' + chr(39) + 's own m-slices of residual rows over ' + str(world) + ' GPUs (no J exchange; trial residuals shared p2p)') if rows_mode else ('in cost-balanced tiles over ' + str(world) + ' GPUs, J rows exchanged by m-slice')) + ' (' + ('host communicator over gloo: one-GPU rehearsal' if args.host_comm else ('RCCL p2p' if comm_backend == 'rccl' else comm_backend)) + '), J^T J + J^T F by m-slice + reduce-scatter/allgather') if world > 1 else 'on 1 GPU'}",
-                       "m": m, "n": n, "parallelism": f"fd-columns+m-slices x{world}" if world > 1 else "single"},
+            "config": {"workload": workload, "m": m, "n": n, "parallelism": f"fd-columns+m-slices x{world}" if world > 1 else "single"},
             "roofline": roofline,
             "rooflines": rooflines,
             "kernel_ms_per_step": per,   # timed region: the priced kernels only
             "kernel_ms_per_call_warmup_breakdown": breakdown,   # every timer, warmup trips (untimed)
             "kernel_ms_per_step_max_over_ranks": per_max,
             # the north star's strong-scaling quantity: the sharded FD Jacobian + its exchange
-            # (m-slice point-to-point exchange; the column-row allgather with PNOL_LM_SLICED=0)
-            # (rows mode: no J exchange; the trial residuals' exchange is reported as exchange_F)
+            # (columns mode: the m-slice point-to-point exchange left after the FD launches end --
+            # exchange_J, the exposed part; exchange_J_busy is its whole span on the comm stream)
             "fd_jacobian_ms_max_over_ranks": per_max["fd_jacobian"] + per_max["fd_ckpt_per_step"] + (
-                per_max["exchange_J"] if per_max["exchange_J"] > 0 else per_max["allgather"]),
+                per_max["exchange_J"] if per_max["exchange_J_busy"] > 0 else per_max["allgather"]),
+            "exchange_J_ms_max_over_ranks": {"exposed": per_max["exchange_J"], "busy": per_max["exchange_J_busy"]}
+            if world > 1 else None,
             "lm_fd_mode": ("rows" if rows_mode else "columns") if world > 1 else "single",
+            "rows_mode_extra": rows_extra,
             "converged_rel_err_vs_xstar": err,
             # the timed trips' outcomes: every trip recomputes J, J^T J and the solve either way
             "trips_accepted": trips[0], "trips_rejected": trips[1],

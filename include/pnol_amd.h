@@ -56,6 +56,8 @@ int pnol_default_ctx(pnol_ctx** out);
  * since the last reset.  on = 2 times only "fd_jacobian", "fd_ckpt", "syrk", "exchange_J",
  * "allgather", "hg" and "bfgs_pass" (fewer event records between launches). */
 int pnol_ctx_enable_timers(pnol_ctx* ctx, int on);
+/* (also "exchange_J_busy": the columns-mode exchange's span on its own stream; "exchange_J" is
+ * then the part of it left after the FD launches end -- the exposed exchange) */
 int pnol_ctx_reset_timers(pnol_ctx* ctx);
 int pnol_ctx_timer(pnol_ctx* ctx, const char* name, double* total_ms, int* count);
 
@@ -158,18 +160,29 @@ int pnol_jtj_mpi_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, doub
 #define PNOL_LM_SLICES 8
 int pnol_lm_sliced_layout(int m, int n, int* slice_rows, size_t* jt_elems);
 /* LevenbergMarquardtMPI.cpp:60 + PNOL_Objective.cpp:202-299 (gradientApproximationMPI's column
- * loop and its MPI_Allreduce), the J^T slices this rank's normal-equation share needs.  Rows mode
- * (default): every FD column evaluated on this rank's own m-slices of residual rows (each row of
+ * loop and its MPI_Allreduce), the J^T slices this rank's normal-equation share needs.  Columns
+ * mode (the default, the reference's decomposition): this rank's cost-balanced FD tiles
+ * (pnol_fd_tiles) for all residual rows, one launch per tile (cheapest first), each tile's
+ * m-slices sent to the ranks holding them (RCCL point-to-point on a second stream, gated by an
+ * event behind that tile's launch, so all but the last tile's transfer overlap the FD); F0 (when
+ * computed) holds all m rows.  Rows mode (pnol_lm_set_fd_mode 1, or PNOL_LM_FD=rows; linear
+ * residuals): every FD column evaluated on this rank's own m-slices of residual rows (each row of
  * the residual is its own chain, so these are the same bits) -- no Jacobian exchange; F0 (when
- * computed) holds this rank's rows.  Columns mode (environment PNOL_LM_FD=columns): this rank's
- * cost-balanced FD tiles (pnol_fd_tiles) for all residual rows, then each m-slice of them to the
- * rank holding that slice (one group of RCCL point-to-point transfers).  Linear-residual device
- * objectives; compute_f0 as for pnol_fd_jacobian_tiles_d. */
+ * computed) then holds only this rank's rows [r0, r1) of pnol_lm_rank_rows, the rest untouched.
+ * Linear-residual device objectives; compute_f0 as for pnol_fd_jacobian_tiles_d. */
 int pnol_lm_jacobian_mpi_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0,
                            int compute_f0, double* JTs);
+/* LevMarqMPI's FD decomposition on this context: 0 = columns (default), 1 = rows, -1 = read the
+ * environment again (PNOL_LM_FD=rows -> 1, else 0).  Every rank must use the same mode (the
+ * LevMarqMPI drop-in re-reads the environment once per findMin and checks that all ranks agree);
+ * pnol_lm_jacobian_mpi_d and pnol_lm_eval_mpi_d follow it. */
+int pnol_lm_set_fd_mode(pnol_ctx* ctx, int mode);
+int pnol_lm_fd_mode(pnol_ctx* ctx, int* mode);
+/* Residual rows [r0, r1) held by `rank` of `nranks` (<= PNOL_LM_SLICES): its m-slices. */
+int pnol_lm_rank_rows(int m, int nranks, int rank, int* r0, int* r1);
 /* The LevMarqMPI trial point F(x) (LevenbergMarquardtMPI.cpp:92) with its prefix checkpoints:
  * rows mode: this rank's rows, then every rank's rows to all ranks (point-to-point), so F holds
- * all m residuals everywhere; columns mode or one rank: pnol_dobj_eval_ckpt_d. */
+ * all m residuals everywhere; columns mode (default) or one rank: pnol_dobj_eval_ckpt_d. */
 int pnol_lm_eval_mpi_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, double* F);
 /* LevenbergMarquardtMPI.cpp:64-80 from this rank's slices of pnol_lm_jacobian_mpi_d: A = J^T J
  * with A_ii = (1 + lambda) (J^T J)_ii and rhs = -(J^T F) on every rank.  Partial tiles of the

@@ -263,6 +263,28 @@ int pnol_lm_jacobian_mpi_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const
     return launch_lm_jacobian(ctx, obj, x, h, F0, compute_f0, JTs);
 }
 
+int pnol_lm_set_fd_mode(pnol_ctx* ctx, int mode) {
+    if (!ctx || mode < -1 || mode > 1) return PNOL_ERR_ARG;
+    ctx->lm_fd_mode = mode < 0 ? lm_fd_mode_env() : mode;
+    return PNOL_OK;
+}
+
+int pnol_lm_fd_mode(pnol_ctx* ctx, int* mode) {
+    if (!ctx || !mode) return PNOL_ERR_ARG;
+    *mode = lm_rows_mode(ctx) ? 1 : 0;
+    return PNOL_OK;
+}
+
+int pnol_lm_rank_rows(int m, int nranks, int rank, int* r0, int* r1) {
+    if (m <= 0 || nranks < 1 || nranks > kLmSlices || rank < 0 || rank >= nranks || !r0 || !r1) return PNOL_ERR_ARG;
+    const int mS = lm_slice_rows(m);
+    int s0 = 0, s1 = 0;
+    lm_rank_slices(nranks, rank, &s0, &s1);
+    *r0 = std::min(m, s0 * mS);
+    *r1 = std::min(m, s1 * mS);
+    return PNOL_OK;
+}
+
 int pnol_lm_eval_mpi_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, double* F) {
     PNOL_CHECK(set_device(ctx));
     if (!obj || !x || !F) return PNOL_ERR_ARG;

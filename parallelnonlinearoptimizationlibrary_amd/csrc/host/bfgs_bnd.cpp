@@ -265,6 +265,10 @@ void BFGS_Bnd::boundaryAssessment(double& F, vector<double>& X, vector<double>& 
         for (vector<double>* v : {&X, &dFdX, &Xlb, &Xub, &dX}) {
             drop_positions(*v, fk, ncur);
             v->resize(nr);
+            // the fallback walk (freeIdxLive off, e.g. below a level that froze every coordinate)
+            // can leave nr != nk: entries past the nk kept ones read 0.0, as the reference's
+            // fresh XR(nr) would hold them (never stale values from the compaction)
+            if (nr > nk) std::fill(v->begin() + nk, v->end(), 0.0);
         }
         if (idx) {
             drop_positions(freeIdx, fk, ncur);

@@ -19,6 +19,7 @@
 #include "LevenbergMarquardt.hpp"
 #include "LevenbergMarquardtMPI.hpp"
 #include "device_util.hpp"
+#include "scalar_host.hpp"
 #include "../pnol_internal.hpp"
 
 using namespace pnol;
@@ -29,48 +30,6 @@ std::vector<double> download_param(pnol_dobj* d, const double* p, size_t len) {
     std::vector<double> h(len);
     if (len && p) check(pnol_memcpy_d2h(d->ctx, h.data(), p, sizeof(double) * len), "d2h(params)");
     return h;
-}
-
-// The term i of a built-in scalar objective at the point X (the objective's own expression,
-// ExampleObjectives.hpp); Rosenbrock sums i < n - 1, the others i < n.
-struct ScalarTerms {
-    int kind, n;
-    double power;
-    const double *p0, *p1;
-};
-
-template <int KIND>
-inline double scalar_term(const ScalarTerms& st, const double* X, int i) {
-    if (KIND == PNOL_OBJ_ROSENBROCK) {
-        const double t = X[i + 1] - X[i] * X[i], u = 1.0 - X[i];
-        return 100.0 * (t * t) + u * u;
-    } else if (KIND == PNOL_OBJ_POWER) {
-        return st.power == 2.0 ? X[i] * X[i] : std::pow(X[i], st.power);
-    } else {
-        double t = (0.5 * st.p0[i] * X[i]) * X[i] - st.p1[i] * X[i];
-        if (i + 1 < st.n) t = t + (0.25 * X[i]) * X[i + 1];
-        return t;
-    }
-}
-
-// f(X_c) for C points at once.  Each point is the objective's sequential sum f = f + t_i in
-// index order (the host objEval's bits); a lone chain is bound by one dependent add per term,
-// C interleaved chains let the core overlap their add latencies.
-template <int KIND, int C>
-void scalar_chains_k(const ScalarTerms& st, const double* const* X, double* out) {
-    double f[C];
-    for (int c = 0; c < C; ++c) f[c] = 0.0;
-    const int nt = KIND == PNOL_OBJ_ROSENBROCK ? std::max(st.n - 1, 0) : st.n;
-    for (int i = 0; i < nt; ++i)
-        for (int c = 0; c < C; ++c) f[c] = f[c] + scalar_term<KIND>(st, X[c], i);
-    for (int c = 0; c < C; ++c) out[c] = f[c];
-}
-
-template <int C>
-void scalar_chains(const ScalarTerms& st, const double* const* X, double* out) {
-    if (st.kind == PNOL_OBJ_ROSENBROCK) scalar_chains_k<PNOL_OBJ_ROSENBROCK, C>(st, X, out);
-    else if (st.kind == PNOL_OBJ_POWER) scalar_chains_k<PNOL_OBJ_POWER, C>(st, X, out);
-    else scalar_chains_k<PNOL_OBJ_QUADRATIC, C>(st, X, out);
 }
 
 // scalar objective around a pnol_dobj: FD batches on the device; single points and line-search
@@ -100,22 +59,7 @@ class DriverScalar : public Objective {
             return;
         }
         evals += nPts;
-        const ScalarTerms st = terms(n);
-        int k = 0;
-        for (; k + 4 <= nPts; k += 4) {
-            const double* xp[4] = {Xs + (size_t)k * n, Xs + (size_t)(k + 1) * n, Xs + (size_t)(k + 2) * n,
-                                   Xs + (size_t)(k + 3) * n};
-            scalar_chains<4>(st, xp, f + k);
-        }
-        if (nPts - k >= 2) {
-            const double* xp[2] = {Xs + (size_t)k * n, Xs + (size_t)(k + 1) * n};
-            scalar_chains<2>(st, xp, f + k);
-            k += 2;
-        }
-        if (k < nPts) {
-            const double* xp = Xs + (size_t)k * n;
-            scalar_chains<1>(st, &xp, f + k);
-        }
+        scalar_batch(terms(n), Xs, nPts, n, f);
     }
     pnol_dobj* deviceObjective(int n) override { return (host_only_ || n != d_->n) ? nullptr : d_; }
     void countEvals(long k) override { evals += k; }

@@ -7,9 +7,11 @@
 #include <cstring>
 #include <cstdio>
 #include <iostream>
+#include <stdexcept>
 #include <utility>
 
 #include "../pnol_comm.hpp"
+#include "../pnol_internal.hpp"
 #include "LevenbergMarquardt.hpp"
 #include "LevenbergMarquardtMPI.hpp"
 #include "device_util.hpp"
@@ -178,11 +180,11 @@ class LMDevice {
 // (Queueing trip i+1 before deciding step i was measured: a rejected step then costs a whole
 // wasted trip, and the post-convergence steps of the bench are mostly rejections.)
 //
-// LevMarqMPI (sliced = true) runs the same loop with the Jacobian split by residual-row
-// slices: each rank evaluates every FD column on its own m-slices of residual rows (rows mode;
-// PNOL_LM_FD=columns: its FD column tiles for all rows, every m-slice of them then sent to the
-// slice's rank) (pnol_lm_jacobian_mpi_d), and the trial point likewise on its own rows, shared
-// point-to-point (pnol_lm_eval_mpi_d); each rank forms its slices' share of J^T J and
+// LevMarqMPI (sliced = true) runs the same loop with the Jacobian split over the ranks
+// (pnol_lm_jacobian_mpi_d): each rank evaluates its FD column tiles for all rows, every m-slice
+// of them sent to the slice's rank while its next tile computes (columns mode, the default), or
+// every FD column on its own m-slices of residual rows with the trial point likewise on its own
+// rows, shared point-to-point (rows mode, PNOL_LM_FD=rows; pnol_lm_eval_mpi_d); each rank forms its slices' share of J^T J and
 // J^T F and one reduce-scatter + allgather assemble A and -J^T F on every rank
 // (pnol_lm_normal_mpi_d).  The collectives are queued on the same stream, so the trip still
 // has one host wait; A, rhs and hence the trajectory are bitwise the single-GPU ones.
@@ -191,7 +193,16 @@ class LMAsync {
     LMAsync(pnol_ctx* ctx, pnol_dobj* d, int n, int m, bool sliced)
         : ctx_(ctx), d_(d), n_(n), m_(m), ldjt_(even_ld(m)), lda_(even_ld(n)), sliced_(sliced) {
         size_t jt = (size_t)n * ldjt_;
-        if (sliced) check(pnol_lm_sliced_layout(m, n, nullptr, &jt), "sliced layout");
+        if (sliced) {
+            check(pnol_lm_sliced_layout(m, n, nullptr, &jt), "sliced layout");
+            // the FD decomposition, read once per solve (PNOL_LM_FD) and the same on every rank:
+            // the two modes pair different transfers, so ranks that disagreed would mismatch them
+            ctx->lm_fd_mode = lm_fd_mode_env();
+            std::vector<int> all;
+            check(comm_allgather_int(ctx, ctx->lm_fd_mode, all), "allgather(fd mode)");
+            for (int v : all)
+                if (v != ctx->lm_fd_mode) throw std::runtime_error("LevMarqMPI: ranks disagree on PNOL_LM_FD");
+        }
         JT_.reset(ctx, jt);
         A_.reset(ctx, (size_t)n * lda_);
         rhs_.reset(ctx, n);

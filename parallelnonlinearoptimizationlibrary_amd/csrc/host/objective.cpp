@@ -17,6 +17,7 @@
 #include "../pnol_internal.hpp"
 #include "PNOL_Objective.hpp"
 #include "device_util.hpp"
+#include "scalar_host.hpp"
 
 using namespace pnol;
 
@@ -97,6 +98,7 @@ void host_points_recur(Objective* o, const std::vector<double>& X, const std::ve
 struct RecurCache {
     unsigned long long oid = 0;   // pnol_dobj::id (never reused)
     std::vector<double> Xf, hf, gf, pts, fv;
+    std::vector<double> p0h, p1h;   // host copies of the objective's data (oid's)
     std::vector<int> redo;
     double F = 0.0;
 };
@@ -246,11 +248,15 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
         // Every value f(x + h_i e_i) is a pure function of the full point and h_i, so a value
         // computed for the same full point and the same h_i by the previous call is the one this
         // call would compute, bit for bit; only coordinates whose step changed (those that were
-        // frozen, with the dummy step, in the previous call) are evaluated, on the host by the
-        // objective's own formula (objEvalBatch: the device kernel's bits).  Built-in scalar
-        // device objectives only (pure); the evaluation count is the reference's N + 1.
+        // frozen, with the dummy step, in the previous call) are evaluated -- on the host by the
+        // library's own copy of the device formula (scalar_host.hpp, the device kernel's bits),
+        // never through the overridable objEvalBatch (a user override, or a header objective
+        // built with contraction on, could differ in the last place, and 1/h amplifies that).
+        // Only kinds whose host formula is bitwise the device's (host_bitwise_kind: PowerObject
+        // with power != 2 calls pow, which may not be); the evaluation count is the reference's
+        // N + 1.
         RecurCache& rc = recur_cache();
-        const bool pure = d->kind == PNOL_OBJ_ROSENBROCK || d->kind == PNOL_OBJ_POWER || d->kind == PNOL_OBJ_QUADRATIC;
+        const bool pure = host_bitwise_kind(d->kind, d->power);
         std::vector<int>& redo = rc.redo;
         redo.clear();
         bool reuse = pure && rc.oid == d->id && rc.Xf.size() == nf &&
@@ -272,25 +278,35 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
                     row[i] = Xf[i] + hf[i];
                 }
                 rc.fv.resize(k);
-                objEvalBatch(pts.data(), k, (int)nf, rc.fv.data());   // counts its k points
+                const ScalarTerms st{d->kind, (int)nf, d->power, rc.p0h.data(), rc.p1h.data()};
+                scalar_batch(st, pts.data(), k, (int)nf, rc.fv.data());
                 for (int q = 0; q < k; ++q) {
                     const int i = redo[q];
                     rc.gf[i] = (rc.fv[q] - rc.F) / hf[i];
                     rc.hf[i] = hf[i];
                 }
             }
-            countEvals(N + 1 - k);
+            countEvals(N + 1);
             gf.assign(rc.gf.begin(), rc.gf.end());
         } else {
             double F = 0;
             device_gradient(d, Xf, hf, 0, (int)nf, &F, gf.data());
             countEvals(N + 1);
             if (pure) {
+                if (rc.oid != d->id) {   // the objective's data, once per objective
+                    rc.p0h.assign(d->len0, 0.0);
+                    rc.p1h.assign(d->len1, 0.0);
+                    pnol_ctx* c = d->ctx;
+                    if (d->len0) check(pnol_memcpy_d2h(c, rc.p0h.data(), d->p0, sizeof(double) * d->len0), "d2h(p0)");
+                    if (d->len1) check(pnol_memcpy_d2h(c, rc.p1h.data(), d->p1, sizeof(double) * d->len1), "d2h(p1)");
+                }
                 rc.oid = d->id;
                 rc.Xf = Xf;
                 rc.hf = hf;
                 rc.gf = gf;
                 rc.F = F;
+                // the quadratic's formula reads d[i], b[i] for every i < n
+                if (d->kind == PNOL_OBJ_QUADRATIC && (rc.p0h.size() < nf || rc.p1h.size() < nf)) rc.oid = 0;
             }
         }
         ir = 0;

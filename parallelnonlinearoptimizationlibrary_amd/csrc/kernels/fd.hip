@@ -13,16 +13,18 @@
 //   k_scalar_fd_values   scalar objectives: one thread per point, x staged through LDS
 //   k_multi_fd           ExpCurve / Cubic (tiny n): one thread per (point, residual)
 //   k_linres_eval        r = A x - y: one thread per residual row, A tiles staged in LDS
-//   k_linres_fd2         all points of a block at once: a register-tiled fp64 VALU GEMM
-//                        R = A [x + h_j e_j]_j, epilogue J = ((R - y) - F0) / h  (no MFMA:
-//                        this is the objective, evaluated like user code would be); tiles
+//   k_linres_fdP         all points of a tile list at once on the row-panel copy of A: one
+//                        residual row per lane, each point's fma chain in a register
+//                        (R = A [x + h_j e_j]_j, epilogue J = ((R - y) - F0) / h; no MFMA:
+//                        this is the objective, evaluated like user code would be); waves
 //                        resume from base-chain checkpoints and broadcast x outside the
-//                        perturbation window (k_linres_fd: the full-B-tile form)
+//                        perturbation window
 #include "../pnol_internal.hpp"
 #include "../pnol_comm.hpp"
 
 #include <algorithm>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <cstdlib>
 #include <vector>
@@ -435,11 +437,6 @@ __global__ __launch_bounds__(256) void k_linres_eval(const double* __restrict__ 
 constexpr int kBK = 16;
 constexpr int kFdTile = PNOL_FD_TILE;   // columns per point tile (BN of every launched variant)
 
-__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
-    const int xcd = orig % kNumXcd, q = nwg / kNumXcd, r = nwg % kNumXcd;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / kNumXcd;
-}
-
 // Point tiles of one FD GEMM launch (kernel argument): columns [start[t], start[t] + count[t]).
 constexpr int kFdMaxTiles = 64;
 struct FdTiles {
@@ -448,130 +445,6 @@ struct FdTiles {
     int start[kFdMaxTiles];
     int count[kFdMaxTiles];
 };
-
-// Batched FD GEMM, x-broadcast form.  Thread (ty, tx) = (t >> 4, t & 15) owns RM rows and
-// PN points (RM * PN accumulators); workgroup tile (16 RM) rows x (16 PN) points.  The B
-// operand of this GEMM is x with ONE perturbed entry per point, and with prefix sharing all
-// of a tile's perturbed columns lie in its first few K stages.  Those stages ("window"
-// stages) build the full 16 x BN B tile in LDS; every later stage multiplies by x[k]
-// broadcast to all points, so per k a thread reads RM A values and one x value for RM * PN
-// fmas.  Each accumulator is still the objective's sequential fma chain: bit-identical to
-// k_linres_fd and to the host evaluation.
-template <bool EVEN, int RM, int PN, int OCC = 1, int KB = kBK>
-__global__ __launch_bounds__(256, OCC) void k_linres_fd2(const double* __restrict__ A, const double* __restrict__ y,
-                                                    const double* __restrict__ x, const double* __restrict__ h, int m,
-                                                    int n, const FdTiles tl, const double* __restrict__ F0,
-                                                    const double* __restrict__ C, double* __restrict__ JT, long ldjt) {
-    constexpr int BM = 16 * RM, BN = 16 * PN;
-    constexpr int TPR = 256 / BM;      // threads staging one A row
-    constexpr int KPT = KB / TPR;      // consecutive k per staging thread
-    __shared__ __attribute__((aligned(16))) double As[KB][BM];
-    __shared__ __attribute__((aligned(16))) double Bs[KB][BN];
-    __shared__ __attribute__((aligned(16))) double xs[KB];
-    const int nmt = (m + BM - 1) / BM, nnt = tl.ntiles;
-    const int v = xcd_remap(blockIdx.x, nmt * nnt);
-    const int mt = v / nnt, nt = v % nnt;
-    const int m0 = mt * BM;
-    const int j0 = tl.start[nt], cnt = tl.count[nt], pbase = 0;   // this tile's columns
-    const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
-    const int jfirst = j0 + pbase, jlast = j0 + min(pbase + BN, cnt) - 1;   // perturbed columns of the tile
-    const int ks = (jfirst / kBK) * kBK;
-
-    double acc[RM][PN];
-#pragma unroll
-    for (int i = 0; i < RM; ++i) {
-        const int row = min(m0 + ty * RM + i, m - 1);
-        const double c0 = ks > 0 ? C[(long)(ks / kCkpt) * m + row] : 0.0;
-#pragma unroll
-        for (int j = 0; j < PN; ++j) acc[i][j] = c0;
-    }
-
-    const int lrow = t / TPR, lk = (t % TPR) * KPT;
-    const long arow = (long)min(m0 + lrow, m - 1) * n;
-    const bool rowok = m0 + lrow < m;
-    double areg[KPT];
-    auto load_a = [&](int k0) {
-        if (EVEN && rowok && k0 + KB <= n) {
-            const double2* p = reinterpret_cast<const double2*>(A + arow + k0 + lk);
-#pragma unroll
-            for (int q = 0; q < KPT / 2; ++q) { double2 w = p[q]; areg[2 * q] = w.x; areg[2 * q + 1] = w.y; }
-        } else {
-#pragma unroll
-            for (int q = 0; q < KPT; ++q) {
-                const int k = k0 + lk + q;
-                areg[q] = (rowok && k < n) ? A[arow + k] : 0.0;
-            }
-        }
-    };
-    load_a(ks);
-    for (int k0 = ks; k0 < n; k0 += KB) {
-        const bool window = k0 <= jlast && k0 + KB > jfirst;   // uniform over the workgroup
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < KPT; ++q) As[lk + q][lrow] = areg[q];
-        if (t < KB) xs[t] = k0 + t < n ? x[k0 + t] : 0.0;
-        if (window) {
-#pragma unroll
-            for (int q = 0; q < KB * BN / 256; ++q) {
-                const int e = t + 256 * q;
-                const int k = e / BN, jj = e % BN;
-                const int kk = k0 + k;
-                const int p = pbase + jj;
-                const int jcol = j0 + p;
-                double val = kk < n ? x[kk] : 0.0;
-                if (p < cnt && kk == jcol) val = x[kk] + h[jcol];
-                Bs[k][jj] = val;
-            }
-        }
-        __syncthreads();
-        if (k0 + KB < n) load_a(k0 + KB);
-        if (window) {
-#pragma unroll
-            for (int k = 0; k < KB; ++k) {
-                double a[RM], b[PN];
-                const double2* ap = reinterpret_cast<const double2*>(&As[k][ty * RM]);
-#pragma unroll
-                for (int q = 0; q < RM / 2; ++q) { double2 w = ap[q]; a[2 * q] = w.x; a[2 * q + 1] = w.y; }
-                const double2* bp = reinterpret_cast<const double2*>(&Bs[k][tx * PN]);
-#pragma unroll
-                for (int q = 0; q < PN / 2; ++q) { double2 w = bp[q]; b[2 * q] = w.x; b[2 * q + 1] = w.y; }
-#pragma unroll
-                for (int i = 0; i < RM; ++i)
-#pragma unroll
-                    for (int j = 0; j < PN; ++j) acc[i][j] = fma(a[i], b[j], acc[i][j]);
-                if (k & 1) __builtin_amdgcn_sched_barrier(0);
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < KB; ++k) {
-                double a[RM];
-                const double2* ap = reinterpret_cast<const double2*>(&As[k][ty * RM]);
-#pragma unroll
-                for (int q = 0; q < RM / 2; ++q) { double2 w = ap[q]; a[2 * q] = w.x; a[2 * q + 1] = w.y; }
-                const double xk = xs[k];
-#pragma unroll
-                for (int i = 0; i < RM; ++i)
-#pragma unroll
-                    for (int j = 0; j < PN; ++j) acc[i][j] = fma(a[i], xk, acc[i][j]);
-                // bound the loads the scheduler hoists ahead (registers, not latency, limit us)
-                if (k & 1) __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-    }
-    // epilogue: F = acc - y; J = (F - F0) / h
-#pragma unroll
-    for (int j = 0; j < PN; ++j) {
-        const int p = pbase + tx * PN + j;
-        if (p >= cnt) continue;
-        const double hj = h[j0 + p];
-        double* out = JT + (long)(j0 + p - tl.jbase) * ldjt;
-#pragma unroll
-        for (int i = 0; i < RM; ++i) {
-            const int row = m0 + ty * RM + i;
-            if (row < m) out[row] = ((acc[i][j] - y[row]) - F0[row]) / hj;
-        }
-    }
-}
 
 // ---- row-panel k-major forms: one residual row per lane, no LDS --------------------------
 // AP holds A in 64-row panels, k-major inside a panel: AP[(rb * n + k) * 64 + r] = A[64 rb + r][k]
@@ -662,18 +535,22 @@ __global__ __launch_bounds__(64) void k_linres_evalP(const double* __restrict__ 
 
 // FD GEMM from AP.  Workgroup = 4 waves on the same 64-row panel (one row per lane), wave w
 // owning points [32w, 32w + 32) of the tile and starting from the base-chain checkpoint at
-// the tile's first column (WAVE_KS: at its own first column).  Per k a lane does 32 fmas:
+// its own first column.  Per k a lane does 32 fmas:
 // x_k for every point except the one whose column is k, which gets x_k + h_k
 // (XdX[j] = X[j] + dX[j]).  The next 8 k of the panel are in flight while the current 8 are
-// consumed.  Bit-identical to the host evaluation, like k_linres_fd2.
-constexpr int kPW = 32;   // points per wave
+// consumed.  Bit-identical to the host evaluation.
+// PW points per wave: 32 (the tile's 128 columns over 4 waves), or 16 (8 waves) for launches
+// too small to fill the chip -- a LevMarqMPI rank's share at P >= 8, or one tile of the phased
+// columns-mode launch: there the makespan is the longest chain's single-wave latency (a wave
+// starting at column 0 runs ~n k-steps of PW fmas each), and 16 points per wave halve it while
+// the chip still holds >= 2 waves per SIMD.  Every point's chain is the same either way.
+constexpr int kPW = 32;
 
-template <bool WAVE_KS>
-__global__ __launch_bounds__(256) void k_linres_fdP(const double* __restrict__ AP, const double* __restrict__ y,
-                                                    const double* __restrict__ x, const double* __restrict__ h, int m,
-                                                    int n, const FdTiles tl, const double* __restrict__ F0,
-                                                    const double* __restrict__ C, double* __restrict__ JT, long ldjt,
-                                                    int mS, long sstride, int mt0, int nmt) {
+template <int PW = kPW>
+__global__ __launch_bounds__(64 * (PNOL_FD_TILE / PW)) void k_linres_fdP(
+    const double* __restrict__ AP, const double* __restrict__ y, const double* __restrict__ x,
+    const double* __restrict__ h, int m, int n, const FdTiles tl, const double* __restrict__ F0,
+    const double* __restrict__ C, double* __restrict__ JT, long ldjt, int mS, long sstride, int mt0, int nmt) {
     // Longest work first: the host sorts the tiles by first column (the chains of tile t run
     // k = ks_t .. n-1), and blockIdx walks all panels of tile 0, then of tile 1, ..., so the
     // short tiles fill the tail.  Panel mt lands on XCD mt % 8 for every tile (L2 reuse).
@@ -681,19 +558,19 @@ __global__ __launch_bounds__(256) void k_linres_fdP(const double* __restrict__ A
     const int nt = blockIdx.x / nmt, mt = mt0 + blockIdx.x % nmt;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int j0 = tl.start[nt], cnt = tl.count[nt];
-    const int pw0 = w * kPW;
+    const int pw0 = w * PW;
     if (pw0 >= cnt) return;                 // wave-uniform; the kernel has no barriers
-    const int np = min(kPW, cnt - pw0);
+    const int np = min(PW, cnt - pw0);
     const int c0 = j0 + pw0;                // first column of this wave
-    const int ks = WAVE_KS ? (c0 / kBK) * kBK : (j0 / kBK) * kBK;
+    const int ks = (c0 / kBK) * kBK;
     const int row = mt * kPanel + lane, rowc = min(row, m - 1);
     const double* a = panel_col(AP, n, mt, 0) + lane;
 
-    double acc[kPW];
+    double acc[PW];
     {
         const double c = ks > 0 ? C[(long)(ks / kCkpt) * m + rowc] : 0.0;
 #pragma unroll
-        for (int j = 0; j < kPW; ++j) acc[j] = c;
+        for (int j = 0; j < PW; ++j) acc[j] = c;
     }
     // k in [kb, ke): every point multiplies by x_k; blocks of 8, ping-pong prefetch of the
     // next block (no register copies)
@@ -702,7 +579,7 @@ __global__ __launch_bounds__(256) void k_linres_fdP(const double* __restrict__ A
         for (int q = 0; q < 8; ++q) {
             const double xk = x[k + q];
 #pragma unroll
-            for (int j = 0; j < kPW; ++j) acc[j] = fma(av[q], xk, acc[j]);
+            for (int j = 0; j < PW; ++j) acc[j] = fma(av[q], xk, acc[j]);
         }
     };
     auto load8 = [&](double (&av)[8], int k) {
@@ -736,15 +613,15 @@ __global__ __launch_bounds__(256) void k_linres_fdP(const double* __restrict__ A
         for (; k < ke; ++k) {
             const double av = a[(long)k * kPanel], xk = x[k];
 #pragma unroll
-            for (int j = 0; j < kPW; ++j) acc[j] = fma(av, xk, acc[j]);
+            for (int j = 0; j < PW; ++j) acc[j] = fma(av, xk, acc[j]);
         }
     };
     bcast(ks, c0);
     // the window: point kk is perturbed at k = c0 + kk
-    const int klen = min(kPW, n - c0);
-    if (klen == kPW) {
+    const int klen = min(PW, n - c0);
+    if (klen == PW) {
 #pragma unroll
-        for (int q0 = 0; q0 < kPW; q0 += 8) {
+        for (int q0 = 0; q0 < PW; q0 += 8) {
             double av[8];
             load8(av, c0 + q0);
 #pragma unroll
@@ -752,7 +629,7 @@ __global__ __launch_bounds__(256) void k_linres_fdP(const double* __restrict__ A
                 const int kk = q0 + q;
                 const double xk = x[c0 + kk], xp = xk + h[c0 + kk];
 #pragma unroll
-                for (int j = 0; j < kPW; ++j) acc[j] = fma(av[q], j == kk ? xp : xk, acc[j]);
+                for (int j = 0; j < PW; ++j) acc[j] = fma(av[q], j == kk ? xp : xk, acc[j]);
             }
         }
     } else {
@@ -760,7 +637,7 @@ __global__ __launch_bounds__(256) void k_linres_fdP(const double* __restrict__ A
             const double av = a[(long)(c0 + kk) * kPanel];
             const double xk = x[c0 + kk], xp = xk + h[c0 + kk];
 #pragma unroll
-            for (int j = 0; j < kPW; ++j) acc[j] = fma(av, j == kk ? xp : xk, acc[j]);
+            for (int j = 0; j < PW; ++j) acc[j] = fma(av, j == kk ? xp : xk, acc[j]);
         }
     }
     bcast(c0 + klen, n);
@@ -771,7 +648,7 @@ __global__ __launch_bounds__(256) void k_linres_fdP(const double* __restrict__ A
         const int sl = (mt * kPanel) / mS;
         double* out = JT + (long)sl * sstride + (row - sl * mS);
 #pragma unroll
-        for (int j = 0; j < kPW; ++j)
+        for (int j = 0; j < PW; ++j)
             if (j < np) {
                 const int col = c0 + j;
                 __builtin_nontemporal_store(((acc[j] - yr) - f0) / h[col], out + (long)(col - tl.jbase) * ldjt);
@@ -975,7 +852,8 @@ int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
 // prefix checkpoints), then the FD GEMM over all tiles in launches of <= kFdMaxTiles tiles.
 int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, const int* start,
                              const int* count, int ntiles, double* F0, int compute_f0, double* JT, int jbase,
-                             int ldjt, int ckpt, int mS, long sstride, int r0, int r1) {
+                             int ldjt, int ckpt, int mS, long sstride, int r0, int r1,
+                             const std::function<int(int)>* after_tile) {
     const bool sliced = mS > 0;
     const bool rows_all = r1 < 0;
     if (!o) return PNOL_ERR_ARG;
@@ -1009,17 +887,7 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
                                               JT + (size_t)(start[t] - jbase) * ldjt, ldjt));
         return PNOL_OK;
     }
-    // PNOL_FD_KERNEL selects the FD GEMM (tuning; all variants are bitwise equal):
-    // 2 = x-broadcast 128 x 128 tiles (8 x 8 per thread), 3 = 64 x 128 (4 x 8) with 16-deep K
-    // stages, 4 = 64 x 128 with 32-deep K stages, 5 = lane-per-row form on the row-panel copy
-    // of A (tile-aligned starts), 6 (default) = the same with per-wave starts.
-    static const int fdk = [] {
-        const char* e = std::getenv("PNOL_FD_KERNEL");
-        const int v = e ? std::atoi(e) : 6;
-        return (v >= 2 && v <= 6) ? v : 6;
-    }();
-    const bool kmajor = fdk >= 5 || sliced;   // the sliced layout is written by the row-panel kernel
-    if (kmajor) PNOL_CHECK(ensure_panels(ctx, o));
+    PNOL_CHECK(ensure_panels(ctx, o));
     // one pass of the base chain: F0 (when asked) and the prefix checkpoints.  compute_f0 == 3
     // (the library's own LM loop: x untouched since pnol_dobj_eval_ckpt_d) reuses a tagged
     // slot outright; compute_f0 == 2 (ABI callers) reuses it only if x's content still matches
@@ -1028,92 +896,66 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
     void *C = nullptr, *xc = nullptr;
     double* f0_out = (compute_f0 == 1 || compute_f0 == 2) ? F0 : nullptr;
     const double* xcheck = nullptr;
-    const int have = (compute_f0 >= 2 && kmajor) ? ckpt_find(ctx, o, x, r0, r1) : -1;
+    const int have = compute_f0 >= 2 ? ckpt_find(ctx, o, x, r0, r1) : -1;
     if (have >= 0) {
         ctx->ckpt_last = have;
         PNOL_CHECK(ckpt_buf(ctx, o, have, &C, &xc));
         if (compute_f0 == 3 || !ckpt) ckpt = 0;
         else xcheck = (const double*)xc;   // verify, recompute on a mismatch
     } else if (ckpt) {
-        PNOL_CHECK(ckpt_claim(ctx, o, x, kmajor, &C, &xc, r0, r1));
+        PNOL_CHECK(ckpt_claim(ctx, o, x, true, &C, &xc, r0, r1));
         if (compute_f0 == 3) f0_out = nullptr;
     } else {   // the caller's previous call on (o, x) wrote them (chunked FD: chunks after the first)
         PNOL_CHECK(ckpt_buf(ctx, o, ctx->ckpt_last, &C, &xc));
     }
     const int mt0 = r0 / kPanel, nmt = (r1 - r0 + kPanel - 1) / kPanel;   // this call's row panels
-    if (ckpt && kmajor && nmt > 0) {
+    if (ckpt && nmt > 0) {
         LaunchTimer tm(ctx, "fd_ckpt");
         hipExtLaunchKernelGGL((k_linres_evalP<true>), dim3(nmt), dim3(64), 0, ctx->stream, tm.start(), tm.stop(), 0,
                               (const double*)o->at, x, (const double*)o->p1, o->m, o->n, f0_out, (double*)C,
                               xcheck ? (double*)nullptr : (double*)xc, xcheck, mt0);
-    } else if (ckpt) {
-        ScopedTimer tm(ctx, "fd_ckpt");
-        if ((o->n % 2) == 0)
-            hipLaunchKernelGGL((k_linres_eval<true, true>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0,
-                               ctx->stream, o->p0, x, o->p1, o->m, o->n, f0_out, (double*)C);
-        else
-            hipLaunchKernelGGL((k_linres_eval<false, true>), dim3((o->m + kEvRows - 1) / kEvRows), dim3(256), 0,
-                               ctx->stream, o->p0, x, o->p1, o->m, o->n, f0_out, (double*)C);
+        PNOL_CHECK(launch_check());
     }
-    if (ckpt) PNOL_CHECK(launch_check());
     if (nmt == 0) return PNOL_OK;   // a rank without rows
-    const bool even = (o->n % 2) == 0;
-    // the row-panel kernels carry their timer events in the dispatch (LaunchTimer); the tuning
-    // variants keep a ScopedTimer
-    std::unique_ptr<LaunchTimer> lt;
-    std::unique_ptr<ScopedTimer> stm;
-    if (kmajor) lt.reset(new LaunchTimer(ctx, "fd_jacobian"));
-    else stm.reset(new ScopedTimer(ctx, "fd_jacobian"));
     const double* Cc = (const double*)C;
-    // tiles in order of first column (longest chains first; outputs go by column)
+    // Launch order: batched (after_tile == nullptr) -- the tiles sorted by first column (longest
+    // chains first), up to kFdMaxTiles per launch; phased -- one launch per tile in the caller's
+    // order, after_tile(t) called behind each (the columns-mode exchange of that tile's rows).
     std::vector<int> ord(ntiles);
     for (int t = 0; t < ntiles; ++t) ord[t] = t;
-    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return start[a] < start[b]; });
-    for (int t0 = 0; t0 < ntiles; t0 += kFdMaxTiles) {
+    if (!after_tile)
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return start[a] < start[b]; });
+    const int per_launch = after_tile ? 1 : kFdMaxTiles;
+    // 16 points per wave when a launch would hold <= 2 waves per SIMD at 32 (k_linres_fdP);
+    // PNOL_FD_PW = 16 / 32 forces either (A/B measurement)
+    static const int force_pw = [] {
+        const char* e = std::getenv("PNOL_FD_PW");
+        return e ? std::atoi(e) : 0;
+    }();
+    LaunchTimer lt(ctx, "fd_jacobian");
+    for (int t0 = 0; t0 < ntiles; t0 += per_launch) {
         FdTiles tl;
-        tl.ntiles = std::min(kFdMaxTiles, ntiles - t0);
+        tl.ntiles = std::min(per_launch, ntiles - t0);
         tl.jbase = jbase;
         for (int t = 0; t < tl.ntiles; ++t) {
             tl.start[t] = start[ord[t0 + t]];
             tl.count[t] = count[ord[t0 + t]];
         }
-        const dim3 g1(((o->m + 127) / 128) * tl.ntiles), g2(nmt * tl.ntiles);
-        hipEvent_t ea = nullptr, eb = nullptr;
-        if (lt) {
-            ea = t0 == 0 ? lt->start() : nullptr;
-            eb = t0 + kFdMaxTiles >= ntiles ? lt->stop() : nullptr;
-        }
-        if (fdk == 5 && !sliced) {
-            hipExtLaunchKernelGGL((k_linres_fdP<false>), g2, dim3(256), 0, ctx->stream, ea, eb, 0, (const double*)o->at,
-                                  (const double*)o->p1, x, h, o->m, o->n, tl, (const double*)F0, Cc, JT, (long)ldjt,
-                                  mS, sstride, mt0, nmt);
-        } else if (fdk == 6 || kmajor) {
-            hipExtLaunchKernelGGL((k_linres_fdP<true>), g2, dim3(256), 0, ctx->stream, ea, eb, 0, (const double*)o->at,
-                                  (const double*)o->p1, x, h, o->m, o->n, tl, (const double*)F0, Cc, JT, (long)ldjt,
-                                  mS, sstride, mt0, nmt);
-        } else if (fdk == 2) {
-            if (even)
-                hipLaunchKernelGGL((k_linres_fd2<true, 8, 8>), g1, dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
-                                   o->n, tl, F0, Cc, JT, (long)ldjt);
-            else
-                hipLaunchKernelGGL((k_linres_fd2<false, 8, 8>), g1, dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
-                                   o->n, tl, F0, Cc, JT, (long)ldjt);
-        } else if (fdk == 3) {
-            if (even)
-                hipLaunchKernelGGL((k_linres_fd2<true, 4, 8>), g2, dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
-                                   o->n, tl, F0, Cc, JT, (long)ldjt);
-            else
-                hipLaunchKernelGGL((k_linres_fd2<false, 4, 8>), g2, dim3(256), 0, ctx->stream, o->p0, o->p1, x, h, o->m,
-                                   o->n, tl, F0, Cc, JT, (long)ldjt);
-        } else {
-            if (even)
-                hipLaunchKernelGGL((k_linres_fd2<true, 4, 8, 1, 32>), g2, dim3(256), 0, ctx->stream, o->p0, o->p1, x, h,
-                                   o->m, o->n, tl, F0, Cc, JT, (long)ldjt);
-            else
-                hipLaunchKernelGGL((k_linres_fd2<false, 4, 8, 1, 32>), g2, dim3(256), 0, ctx->stream, o->p0, o->p1, x,
-                                   h, o->m, o->n, tl, F0, Cc, JT, (long)ldjt);
-        }
+        const dim3 grid(nmt * tl.ntiles);
+        const hipEvent_t ea = t0 == 0 ? lt.start() : nullptr;
+        const hipEvent_t eb = t0 + per_launch >= ntiles ? lt.stop() : nullptr;
+        const long waves32 = (long)nmt * tl.ntiles * (kFdTile / kPW);
+        const bool pw16 = force_pw ? force_pw == 16 : waves32 <= 8L * std::max(ctx->num_cu, 1);
+        if (pw16)
+            hipExtLaunchKernelGGL((k_linres_fdP<16>), grid, dim3(64 * (kFdTile / 16)), 0, ctx->stream, ea, eb, 0,
+                                  (const double*)o->at, (const double*)o->p1, x, h, o->m, o->n, tl, (const double*)F0,
+                                  Cc, JT, (long)ldjt, mS, sstride, mt0, nmt);
+        else
+            hipExtLaunchKernelGGL((k_linres_fdP<kPW>), grid, dim3(64 * (kFdTile / kPW)), 0, ctx->stream, ea, eb, 0,
+                                  (const double*)o->at, (const double*)o->p1, x, h, o->m, o->n, tl, (const double*)F0,
+                                  Cc, JT, (long)ldjt, mS, sstride, mt0, nmt);
         PNOL_CHECK(launch_check());
+        if (after_tile) PNOL_CHECK((*after_tile)(ord[t0]));
     }
     return PNOL_OK;
 }
@@ -1169,14 +1011,14 @@ int launch_synthetic_linres(pnol_ctx* ctx, unsigned long long seed, int m, int n
     return launch_check();
 }
 
-// LevMarqMPI Jacobian on the sliced J^T layout (pnol_lm_sliced_layout): this rank evaluates its
-// cost-balanced FD tiles (fd_tiles_of) for every residual row, then sends each m-slice of
-// them to the rank that holds the slice (lm_rank_slices) -- one group of point-to-point
-// transfers, 1/P of the J^T an allgather would move.  Each rank ends with every FD column of
-// its own slices, which is all launch_lm_normal reads.
-bool lm_rows_mode() {
-    const char* e = std::getenv("PNOL_LM_FD");   // read per call: tests compare both modes
-    return !(e && std::strcmp(e, "columns") == 0);
+int lm_fd_mode_env() {
+    const char* e = std::getenv("PNOL_LM_FD");
+    return (e && std::strcmp(e, "rows") == 0) ? 1 : 0;
+}
+
+bool lm_rows_mode(pnol_ctx* ctx) {
+    if (ctx->lm_fd_mode < 0) ctx->lm_fd_mode = lm_fd_mode_env();
+    return ctx->lm_fd_mode == 1;
 }
 
 // this rank's residual rows [r0, r1) in rows mode: its m-slices
@@ -1188,6 +1030,36 @@ static void lm_my_rows(int m, int* r0, int* r1) {
     *r1 = std::min(m, s1 * mS);
 }
 
+// Rank q's FD tiles in phase order: cheapest first (the latest first column: the shortest
+// prefix-shared chains), so the exchange of the early tiles runs while the expensive ones compute
+// and only the last tile's exchange is left after the FD.
+static void lm_phase_tiles(int n, int P, int q, std::vector<int>& st, std::vector<int>& ct) {
+    fd_tiles_of(n, P, q, st, ct);   // ascending first column
+    std::reverse(st.begin(), st.end());
+    std::reverse(ct.begin(), ct.end());
+}
+
+static int lm_comm_stream(pnol_ctx* ctx, int nphase) {
+    if (!ctx->comm_stream) PNOL_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
+    while ((int)ctx->phase_events.size() < nphase) {
+        hipEvent_t e;
+        PNOL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->phase_events.push_back(e);
+    }
+    if (!ctx->comm_done) PNOL_HIP(hipEventCreateWithFlags(&ctx->comm_done, hipEventDisableTiming));
+    return PNOL_OK;
+}
+
+// LevMarqMPI Jacobian on the sliced J^T layout (pnol_lm_sliced_layout), LevenbergMarquardtMPI.cpp:60
+// -> PNOL_Objective.cpp:202-299.
+// Columns mode (default; the reference's decomposition, its round-robin columns dealt as
+// cost-balanced tiles): this rank evaluates its FD tiles for every residual row, one launch per
+// tile, cheapest first; behind each launch an event, and on the communication stream, gated by
+// it, that tile's m-slices go to the ranks holding them (one group of point-to-point transfers
+// per tile: phase k carries every rank's k-th tile).  Each rank ends with every FD column of its
+// own slices -- all launch_lm_normal reads -- having moved 1/P of the J^T an allgather would,
+// and all but the last tile's transfer overlapped with the FD launches.  Rows mode (linear
+// residuals): every FD column on this rank's own m-slices, no Jacobian exchange at all.
 int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
                        double* JTs) {
     if (!o || !JTs || o->kind != PNOL_OBJ_LINRES) return PNOL_ERR_UNSUPPORTED;
@@ -1196,7 +1068,7 @@ int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
     const int mS = lm_slice_rows(o->m);
     const long sstr = (long)n * mS;
     std::vector<int> st, ct;
-    if (lm_rows_mode()) {
+    if (lm_rows_mode(ctx)) {
         // Every residual row of the linear residual is its own fma chain over x, so the FD
         // column j on rows [r0, r1) is exactly the rows [r0, r1) of the whole column: each rank
         // evaluates all n FD columns on its m-slices -- 1/P of the FD work, balanced, and the
@@ -1207,34 +1079,53 @@ int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
         return launch_fd_jacobian_tiles(ctx, o, x, h, st.data(), ct.data(), (int)st.size(), F0, compute_f0, JTs, 0, mS,
                                         1, mS, sstr, r0, r1);
     }
-    fd_tiles_of(n, P, me, st, ct);
-    PNOL_CHECK(launch_fd_jacobian_tiles(ctx, o, x, h, st.data(), ct.data(), (int)st.size(), F0, compute_f0, JTs, 0, mS,
-                                        1, mS, sstr));
-    if (P == 1) return PNOL_OK;
-    // runs of consecutive tiles per rank: one transfer per (run, slice)
-    std::vector<std::vector<std::pair<int, int>>> runs(P);
-    for (int q = 0; q < P; ++q) {
-        fd_tiles_of(n, P, q, st, ct);
-        for (size_t i = 0; i < st.size(); ++i) {
-            if (!runs[q].empty() && runs[q].back().first + runs[q].back().second == st[i])
-                runs[q].back().second += ct[i];
-            else
-                runs[q].push_back({st[i], ct[i]});
-        }
+    if (P == 1) {
+        fd_tiles_of(n, 1, 0, st, ct);
+        return launch_fd_jacobian_tiles(ctx, o, x, h, st.data(), ct.data(), (int)st.size(), F0, compute_f0, JTs, 0,
+                                        mS, 1, mS, sstr);
     }
-    ScopedTimer tm(ctx, "exchange_J");
-    return comm_exchange(ctx, JTs, JTs, [&](int q, int d, std::vector<XBlock>& bl) {
-        bl.clear();
-        int s0, s1;
-        lm_rank_slices(P, d, &s0, &s1);
-        for (int s = s0; s < s1; ++s) {
-            if ((long)s * mS >= o->m) break;
-            for (auto& r : runs[q]) {
-                const size_t off = (size_t)s * sstr + (size_t)r.first * mS;
-                bl.push_back({off, off, (size_t)r.second * mS});
+    std::vector<std::vector<int>> pst(P), pct(P);
+    int nphase = 0;
+    for (int q = 0; q < P; ++q) {
+        lm_phase_tiles(n, P, q, pst[q], pct[q]);
+        nphase = std::max(nphase, (int)pst[q].size());
+    }
+    PNOL_CHECK(lm_comm_stream(ctx, nphase + 1));
+    const int mine = (int)pst[me].size();
+    // phase k is gated by the event behind this rank's k-th tile; phases past its last tile
+    // (and every phase of a rank without tiles) by the event behind its last launch
+    int launched = 0;
+    const std::function<int(int)> after = [&](int) {
+        PNOL_HIP(hipEventRecord(ctx->phase_events[launched++], ctx->stream));
+        return PNOL_OK;
+    };
+    PNOL_CHECK(launch_fd_jacobian_tiles(ctx, o, x, h, pst[me].data(), pct[me].data(), mine, F0, compute_f0, JTs, 0,
+                                        mS, 1, mS, sstr, 0, -1, &after));
+    if (launched < mine) return PNOL_ERR_UNSUPPORTED;   // (linear residuals launch per tile)
+    if (mine == 0) PNOL_HIP(hipEventRecord(ctx->phase_events[0], ctx->stream));
+    const hipEvent_t fd_end = timer_event(ctx, "exchange_J", ctx->stream);
+    hipEvent_t busy0 = nullptr;
+    for (int k = 0; k < nphase; ++k) {
+        PNOL_HIP(hipStreamWaitEvent(ctx->comm_stream, ctx->phase_events[std::min(k, std::max(mine - 1, 0))], 0));
+        if (k == 0) busy0 = timer_event(ctx, "exchange_J_busy", ctx->comm_stream);
+        PNOL_CHECK(comm_exchange(ctx, JTs, JTs, [&](int q, int d, std::vector<XBlock>& bl) {
+            bl.clear();
+            if (k >= (int)pst[q].size()) return;
+            const size_t c0 = (size_t)pst[q][k], cc = (size_t)pct[q][k];
+            int s0, s1;
+            lm_rank_slices(P, d, &s0, &s1);
+            for (int s = s0; s < s1; ++s) {
+                if ((long)s * mS >= o->m) break;
+                const size_t off = (size_t)s * sstr + c0 * mS;
+                bl.push_back({off, off, cc * mS});
             }
-        }
-    });
+        }, ctx->comm_stream));
+    }
+    timer_pair(ctx, "exchange_J_busy", busy0, timer_event(ctx, "exchange_J_busy", ctx->comm_stream));
+    timer_pair(ctx, "exchange_J", fd_end, timer_event(ctx, "exchange_J", ctx->comm_stream));
+    PNOL_HIP(hipEventRecord(ctx->comm_done, ctx->comm_stream));
+    PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->comm_done, 0));
+    return PNOL_OK;
 }
 
 // The LevMarqMPI trial point: F(x) and its checkpoints on this rank's rows, then each rank's
@@ -1243,7 +1134,7 @@ int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
 int launch_lm_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* F) {
     if (!o || !x || !F) return PNOL_ERR_ARG;
     const int P = comm_size();
-    if (P == 1 || !lm_rows_mode() || o->kind != PNOL_OBJ_LINRES) return launch_dobj_eval_ckpt(ctx, o, x, F);
+    if (P == 1 || !lm_rows_mode(ctx) || o->kind != PNOL_OBJ_LINRES) return launch_dobj_eval_ckpt(ctx, o, x, F);
     int r0 = 0, r1 = 0;
     lm_my_rows(o->m, &r0, &r1);
     PNOL_CHECK(launch_dobj_eval_ckpt(ctx, o, x, F, r0, r1));

@@ -21,17 +21,21 @@ void fd_tiles_of(int ncols, int nranks, int rank, std::vector<int>& start, std::
 int comm_share_rows(pnol_ctx* ctx, double* buf, size_t ld, int ncols);
 // recv[r*count + i] = send_r[i]; host buffers (any backend)
 int comm_allgather_host(pnol_ctx* ctx, const double* send, double* recv, size_t count);
-// device buffers (RCCL backend native; host backend bounces through host memory)
-int comm_allgather_device(pnol_ctx* ctx, const double* send, double* recv, size_t count);
+// device buffers (RCCL backend native; host backend bounces through host memory); stream:
+// nullptr = the context stream
+int comm_allgather_device(pnol_ctx* ctx, const double* send, double* recv, size_t count, void* stream = nullptr);
+// one int per rank, gathered on every rank (host memory; setup-time agreement checks)
+int comm_allgather_int(pnol_ctx* ctx, int mine, std::vector<int>& all);
 // Point-to-point exchange of device blocks: blocks(src, dst, out) lists what rank src sends to
 // rank dst (src != dst) -- soff into the sender's sbase, roff into the receiver's rbase, count
 // doubles -- and must give the same list on every rank.  RCCL: one group of sends / receives
-// on the context stream; host backend: packed through one allgather.
+// on `stream` (nullptr: the context stream); host backend: packed through one allgather, the
+// copies on `stream` (the host waits for that stream only).
 struct XBlock {
     size_t soff, roff, count;
 };
 int comm_exchange(pnol_ctx* ctx, const double* sbase, double* rbase,
-                  const std::function<void(int, int, std::vector<XBlock>&)>& blocks);
+                  const std::function<void(int, int, std::vector<XBlock>&)>& blocks, void* stream = nullptr);
 // process default GPU context (nullptr when no gfx950 device is visible)
 pnol_ctx* default_ctx_or_null();
 

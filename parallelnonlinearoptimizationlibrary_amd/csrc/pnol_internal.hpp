@@ -8,6 +8,7 @@
 #include <atomic>
 #include <cstddef>
 #include <cstdio>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <string>
@@ -71,6 +72,14 @@ struct pnol_ctx {
     unsigned* tail_flag = nullptr;
     unsigned tail_epoch = 0;
     hipEvent_t tail_ev = nullptr;       // the GEMV done (aux stream), waited for by the main stream
+    // LevMarqMPI's FD decomposition (fd.hip): -1 = not chosen yet (PNOL_LM_FD at first use),
+    // 0 = columns (the reference's: FD column tiles per rank + the m-slice exchange), 1 = rows
+    int lm_fd_mode = -1;
+    // columns mode: the m-slice exchange of each FD tile runs on comm_stream, gated by the
+    // event recorded behind that tile's FD launch on the context stream
+    hipStream_t comm_stream = nullptr;
+    std::vector<hipEvent_t> phase_events;
+    hipEvent_t comm_done = nullptr;
 };
 
 struct pnol_dobj {
@@ -212,9 +221,12 @@ int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
 // checkpoints of the previous call at the same x (chunked launches of one Jacobian)
 // mS > 0: the sliced J^T layout (row r of J in slice r / mS at JT + (r / mS) * sstride, row
 // stride ldjt >= mS); linear residuals on the row-panel kernels only
+// after_tile (nullable): one launch per tile in the given order (no sorting), after_tile(t)
+// called behind the launch of tile t -- the phased columns-mode exchange (linear residuals)
 int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, const int* start,
                              const int* count, int ntiles, double* F0, int compute_f0, double* JT, int jbase,
-                             int ldjt, int ckpt = 1, int mS = 0, long sstride = 0, int r0 = 0, int r1 = -1);
+                             int ldjt, int ckpt = 1, int mS = 0, long sstride = 0, int r0 = 0, int r1 = -1,
+                             const std::function<int(int)>* after_tile = nullptr);
 // J^T J tiles of tile rows [row_begin, row_end) (128 x 128 tiles, split_k of the whole matrix so
 // every tile is summed exactly as by launch_jtj), partials + reduce on `stream`
 int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldjt, int m, int n, double lambda,
@@ -247,16 +259,26 @@ inline void lm_rank_slices(int P, int r, int* s0, int* s1) {
 // diagonal) and rhs = -J^T F on every rank (syrk.hip)
 int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F, double* A,
                      int lda, double* rhs, double* jtj_diag);
-// the sliced J^T of this rank's m-slices (fd.hip).  Rows mode (default): every FD column on
-// the rank's own residual rows -- no Jacobian exchange.  Columns mode (PNOL_LM_FD=columns): the
-// rank's cost-balanced FD tiles for every row, then each slice's rows to the slice's rank.
+// the sliced J^T of this rank's m-slices (fd.hip).  Columns mode (default, the reference's
+// decomposition): the rank's cost-balanced FD tiles for every row, each tile's m-slices sent to
+// the slices' ranks while the next tile computes.  Rows mode (PNOL_LM_FD=rows, linear residuals):
+// every FD column on the rank's own residual rows -- no Jacobian exchange.
 int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
                        double* JTs);
 // LevMarqMPI trial point: F(x) (+ checkpoints) on this rank's rows in rows mode, then every
 // rank's rows to all ranks; columns mode: all rows on every rank (fd.hip)
 int launch_lm_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* F);
-// rows mode on (PNOL_LM_FD != columns)
-bool lm_rows_mode();
+// LevMarqMPI's decomposition on this context: rows mode (1) or columns mode (0); the first call
+// reads PNOL_LM_FD ("rows" -> 1, anything else -> 0), later calls keep it (lm_fd_mode_reset
+// re-reads it: once per LevMarqMPI solve, checked equal on every rank)
+bool lm_rows_mode(pnol_ctx* ctx);
+int lm_fd_mode_env();
+
+// Timer events that do not bracket one stream: timer_event records an event on `stream` when
+// the timer `name` is on (nullptr otherwise); timer_pair books (a, b) under `name` -- elapsed
+// b - a, floored at 0 (a pair across two streams: b may complete before a).
+hipEvent_t timer_event(pnol_ctx* ctx, const char* name, hipStream_t stream);
+void timer_pair(pnol_ctx* ctx, const char* name, hipEvent_t a, hipEvent_t b);
 
 // Row-tile height of the fused BFGS pass (w = D^T y partials are per row tile): 256 rows when
 // that still gives >= 512 workgroups (n >= 8192), else 128 (n = 4096: 256 workgroups instead of

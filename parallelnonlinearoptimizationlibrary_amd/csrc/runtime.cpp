@@ -153,9 +153,10 @@ int comm_share_rows(pnol_ctx* ctx, double* buf, size_t ld, int ncols) {
 }
 
 int comm_exchange(pnol_ctx* ctx, const double* sbase, double* rbase,
-                  const std::function<void(int, int, std::vector<XBlock>&)>& blocks) {
+                  const std::function<void(int, int, std::vector<XBlock>&)>& blocks, void* stream_) {
     const int P = g_comm.nranks, me = g_comm.rank;
     if (g_comm.kind == 0 || P == 1) return PNOL_OK;
+    const hipStream_t st = stream_ ? (hipStream_t)stream_ : ctx->stream;
     std::vector<XBlock> bl;
     if (g_comm.kind == 1) {
         if (ncclGroupStart() != ncclSuccess) return PNOL_ERR_COMM;
@@ -164,21 +165,24 @@ int comm_exchange(pnol_ctx* ctx, const double* sbase, double* rbase,
             if (d == me) continue;
             blocks(me, d, bl);
             for (const XBlock& b : bl)
-                if (b.count && ncclSend(sbase + b.soff, b.count, ncclDouble, d, g_comm.nccl, ctx->stream) != ncclSuccess)
+                if (b.count && ncclSend(sbase + b.soff, b.count, ncclDouble, d, g_comm.nccl, st) != ncclSuccess)
                     ok = false;
         }
         for (int q = 0; q < P && ok; ++q) {
             if (q == me) continue;
             blocks(q, me, bl);
             for (const XBlock& b : bl)
-                if (b.count && ncclRecv(rbase + b.roff, b.count, ncclDouble, q, g_comm.nccl, ctx->stream) != ncclSuccess)
+                if (b.count && ncclRecv(rbase + b.roff, b.count, ncclDouble, q, g_comm.nccl, st) != ncclSuccess)
                     ok = false;
         }
         if (ncclGroupEnd() != ncclSuccess || !ok) return PNOL_ERR_COMM;
         return PNOL_OK;
     }
     // host backend: every rank packs all its outgoing blocks (destinations in order) into one
-    // slot of the largest rank's size; one allgather; receivers pick their blocks out
+    // slot of the largest rank's size; one allgather; receivers pick their blocks out.  The
+    // host waits for `st` anyway (the allgather below): first for its earlier copies, so a
+    // scratch regrow cannot free a buffer they still read.
+    PNOL_HIP(hipStreamSynchronize(st));
     auto out_size = [&](int q) {
         size_t t = 0;
         for (int d = 0; d < P; ++d) {
@@ -191,6 +195,7 @@ int comm_exchange(pnol_ctx* ctx, const double* sbase, double* rbase,
     size_t slot = 1;
     for (int q = 0; q < P; ++q) slot = std::max(slot, out_size(q));
     void *sv = nullptr, *rv = nullptr;
+    // (a buffer regrow synchronises the context stream: sizes settle on the first trip)
     PNOL_CHECK(ws_get(ctx, "xchg_send", sizeof(double) * slot, &sv));
     PNOL_CHECK(ws_get(ctx, "xchg_recv", sizeof(double) * slot * P, &rv));
     double *send = (double*)sv, *recv = (double*)rv;
@@ -201,11 +206,11 @@ int comm_exchange(pnol_ctx* ctx, const double* sbase, double* rbase,
         for (const XBlock& b : bl) {
             if (b.count)
                 PNOL_HIP(hipMemcpyAsync(send + off, sbase + b.soff, sizeof(double) * b.count, hipMemcpyDeviceToDevice,
-                                        ctx->stream));
+                                        st));
             off += b.count;
         }
     }
-    PNOL_CHECK(comm_allgather_device(ctx, send, recv, slot));
+    PNOL_CHECK(comm_allgather_device(ctx, send, recv, slot, st));
     for (int q = 0; q < P; ++q) {
         if (q == me) continue;
         off = 0;
@@ -215,11 +220,22 @@ int comm_exchange(pnol_ctx* ctx, const double* sbase, double* rbase,
             for (const XBlock& b : bl) {
                 if (d == me && b.count)
                     PNOL_HIP(hipMemcpyAsync(rbase + b.roff, recv + (size_t)q * slot + off, sizeof(double) * b.count,
-                                            hipMemcpyDeviceToDevice, ctx->stream));
+                                            hipMemcpyDeviceToDevice, st));
                 off += b.count;
             }
         }
     }
+    return PNOL_OK;
+}
+
+int comm_allgather_int(pnol_ctx* ctx, int mine, std::vector<int>& all) {
+    const int P = g_comm.nranks;
+    all.assign(P, mine);
+    if (g_comm.kind == 0 || P == 1) return PNOL_OK;
+    std::vector<double> v(P);
+    const double m = mine;
+    PNOL_CHECK(comm_allgather_host(ctx, &m, v.data(), 1));
+    for (int r = 0; r < P; ++r) all[r] = (int)v[r];
     return PNOL_OK;
 }
 
@@ -241,24 +257,24 @@ int comm_allgather_host(pnol_ctx* ctx, const double* send, double* recv, size_t 
     return PNOL_OK;
 }
 
-int comm_allgather_device(pnol_ctx* ctx, const double* send, double* recv, size_t count) {
+int comm_allgather_device(pnol_ctx* ctx, const double* send, double* recv, size_t count, void* stream_) {
+    const hipStream_t st = stream_ ? (hipStream_t)stream_ : ctx->stream;
     if (g_comm.kind == 0) {
-        if (send != recv)
-            PNOL_HIP(hipMemcpyAsync(recv, send, sizeof(double) * count, hipMemcpyDeviceToDevice, ctx->stream));
+        if (send != recv) PNOL_HIP(hipMemcpyAsync(recv, send, sizeof(double) * count, hipMemcpyDeviceToDevice, st));
         return PNOL_OK;
     }
     if (g_comm.kind == 1) {
-        ScopedTimer tm(ctx, "allgather");
-        if (ncclAllGather(send, recv, count, ncclDouble, g_comm.nccl, ctx->stream) != ncclSuccess) return PNOL_ERR_COMM;
+        ScopedTimer tm(ctx, "allgather", st);
+        if (ncclAllGather(send, recv, count, ncclDouble, g_comm.nccl, st) != ncclSuccess) return PNOL_ERR_COMM;
         return PNOL_OK;
     }
     // host backend with device buffers: bounce through host memory
     std::vector<double> hs(count), hr(count * (size_t)g_comm.nranks);
-    PNOL_HIP(hipMemcpyAsync(hs.data(), send, sizeof(double) * count, hipMemcpyDeviceToHost, ctx->stream));
-    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    PNOL_HIP(hipMemcpyAsync(hs.data(), send, sizeof(double) * count, hipMemcpyDeviceToHost, st));
+    PNOL_HIP(hipStreamSynchronize(st));
     if (g_comm.fn(hs.data(), hr.data(), sizeof(double) * count, g_comm.user) != 0) return PNOL_ERR_COMM;
-    PNOL_HIP(hipMemcpyAsync(recv, hr.data(), sizeof(double) * hr.size(), hipMemcpyHostToDevice, ctx->stream));
-    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    PNOL_HIP(hipMemcpyAsync(recv, hr.data(), sizeof(double) * hr.size(), hipMemcpyHostToDevice, st));
+    PNOL_HIP(hipStreamSynchronize(st));
     return PNOL_OK;
 }
 
@@ -268,7 +284,8 @@ int comm_allgather_device(pnol_ctx* ctx, const double* send, double* recv, size_
 // mode 2: the kernels bench.py prices against a roofline or a scaling target; each timer
 // costs two event records between launches (~5 us of dispatch gap each)
 static bool hot_timer(const char* name) {
-    for (const char* h : {"fd_jacobian", "fd_ckpt", "syrk", "exchange_J", "allgather", "hg", "bfgs_pass"})
+    for (const char* h : {"fd_jacobian", "fd_ckpt", "syrk", "exchange_J", "exchange_J_busy", "allgather", "hg",
+                          "bfgs_pass"})
         if (std::strcmp(name, h) == 0) return true;
     return false;
 }
@@ -316,14 +333,43 @@ ScopedTimer::~ScopedTimer() {
     ctx_->timers.pending[name_].push_back({a_, b_});
 }
 
+static bool timer_take(pnol_ctx* ctx, hipEvent_t* e) {
+    auto& pool = ctx->timers.free_events;
+    if (!pool.empty()) {
+        *e = pool.back();
+        pool.pop_back();
+        return true;
+    }
+    return hipEventCreate(e) == hipSuccess;
+}
+
+hipEvent_t timer_event(pnol_ctx* ctx, const char* name, hipStream_t stream) {
+    if (!ctx || !ctx->timers.on || (ctx->timers.on == 2 && !hot_timer(name))) return nullptr;
+    hipEvent_t e = nullptr;
+    if (!timer_take(ctx, &e)) return nullptr;
+    (void)hipEventRecord(e, stream ? stream : ctx->stream);
+    return e;
+}
+
+void timer_pair(pnol_ctx* ctx, const char* name, hipEvent_t a, hipEvent_t b) {
+    if (!ctx) return;
+    if (a && b) {
+        ctx->timers.pending[name].push_back({a, b});
+        return;
+    }
+    for (hipEvent_t e : {a, b})
+        if (e) ctx->timers.free_events.push_back(e);
+}
+
 static void resolve_timers(pnol_ctx* ctx) {
     for (auto& kv : ctx->timers.pending) {
         auto& acc = ctx->timers.done[kv.first];
         for (auto& ev : kv.second) {
             float ms = 0.f;
             (void)hipEventSynchronize(ev.second);
+            (void)hipEventSynchronize(ev.first);
             if (hipEventElapsedTime(&ms, ev.first, ev.second) == hipSuccess) {
-                acc.first += ms;
+                acc.first += ms > 0.f ? ms : 0.f;   // a cross-stream pair may end before it starts
                 acc.second += 1;
             }
             ctx->timers.free_events.push_back(ev.first);
@@ -440,6 +486,12 @@ int pnol_ctx_destroy(pnol_ctx* ctx) {
         (void)hipStreamDestroy(ctx->aux_stream);
     }
     for (hipEvent_t e : ctx->aux_events) (void)hipEventDestroy(e);
+    if (ctx->comm_stream) {
+        (void)hipStreamSynchronize(ctx->comm_stream);
+        (void)hipStreamDestroy(ctx->comm_stream);
+    }
+    for (hipEvent_t e : ctx->phase_events) (void)hipEventDestroy(e);
+    if (ctx->comm_done) (void)hipEventDestroy(ctx->comm_done);
     if (ctx->tail_ev) (void)hipEventDestroy(ctx->tail_ev);
     if (ctx->tail_flag) (void)hipFree(ctx->tail_flag);
     for (auto& kv : ctx->timers.pending)

@@ -126,6 +126,15 @@ class Context:
                                              _ptr(rhs), _ptr(diag)), "pnol_lm_normal_mpi_d")
         return (A, rhs, diag) if want_diag else (A, rhs)
 
+    def set_lm_fd_mode(self, mode):
+        """LevMarqMPI's FD decomposition on this context: 0 columns (default), 1 rows, -1 env."""
+        L.check(L.lib().pnol_lm_set_fd_mode(self.h, int(mode)), "pnol_lm_set_fd_mode")
+
+    def lm_fd_mode(self):
+        v = C.c_int()
+        L.check(L.lib().pnol_lm_fd_mode(self.h, C.byref(v)), "pnol_lm_fd_mode")
+        return v.value
+
     def solve(self, A, rhs, method=0):
         """sigma = A^{-1} rhs; A is overwritten.  Returns (sigma, info)."""
         n = rhs.numel()
@@ -221,10 +230,15 @@ class DeviceObjective:
         return F0, JT, A, rhs
 
     def lm_jacobian_mpi(self, x, h, JTs=None, F0=None, compute_f0=True):
-        """This rank's FD tiles for all rows into the m-sliced J^T, then each slice to its rank."""
+        """The m-sliced J^T this rank's share of the normal equations reads (pnol_lm_jacobian_mpi_d).
+        Columns mode (default): this rank's FD tiles for all rows, each tile's m-slices sent to
+        the slices' ranks; F0 (when computed) holds all m residuals.  Rows mode
+        (Context.set_lm_fd_mode(1)): every FD column on this rank's own m-slices, no exchange;
+        F0 then holds only this rank's rows (lm_rank_rows), the other rows read as zero."""
         if JTs is None:
             JTs = self.ctx.empty(lm_sliced_layout(self.m, self.n)[1])
-        F0 = self.ctx.empty(self.m) if F0 is None else F0
+        F0 = self.ctx.torch.zeros(self.m, dtype=self.ctx.torch.float64, device=f"cuda:{self.ctx.device}") \
+            if F0 is None else F0
         L.check(L.lib().pnol_lm_jacobian_mpi_d(self.ctx.h, self.h, _ptr(x), _ptr(h), _ptr(F0), int(compute_f0),
                                                _ptr(JTs)), "pnol_lm_jacobian_mpi_d")
         return F0, JTs
@@ -239,6 +253,13 @@ class DeviceObjective:
                                                  int(compute_f0), _ptr(JT), JT.stride(0)),
                 "pnol_fd_jacobian_tiles_d")
         return F0, JT
+
+
+def lm_rank_rows(m, nranks, rank):
+    """Residual rows [r0, r1) held by `rank` of `nranks` (its m-slices; rows mode's F0 rows)."""
+    r0, r1 = C.c_int(), C.c_int()
+    L.check(L.lib().pnol_lm_rank_rows(m, nranks, rank, C.byref(r0), C.byref(r1)), "pnol_lm_rank_rows")
+    return r0.value, r1.value
 
 
 def lm_sliced_layout(m, n):

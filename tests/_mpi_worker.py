@@ -1,6 +1,7 @@
 """Worker for tests/test_gpu_mpi.py: one rank of LevMarqMPI on the (shared) GPU with the
 host communicator backend (torch.distributed gloo allgather).  Writes its results to
 <out>/rank<r>.npz.  Started as a child process by the test (never exec'd in place)."""
+import ctypes as C
 import os
 import sys
 
@@ -12,7 +13,8 @@ sys.path.insert(0, ROOT)
 
 def main():
     out, m, n = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
-    lm_only = len(sys.argv) > 4 and sys.argv[4] == "lm"
+    what = sys.argv[4] if len(sys.argv) > 4 else ""
+    lm_only = what in ("lm", "lmonly")
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
@@ -23,6 +25,16 @@ def main():
     ctx = Context(0)
     obj = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
     X, F0, FO, res = run_levmarq(obj, np.zeros(n), (0.001, 10.0, 1e-7, 5, 0.0, -1), which=1)
+    if what == "lmonly":   # the LevMarqMPI solve alone (full-size cfg 4), with the mode it ran in
+        dctx = C.c_void_p()
+        L.check(L.lib().pnol_default_ctx(C.byref(dctx)), "pnol_default_ctx")
+        mode = C.c_int()
+        L.check(L.lib().pnol_lm_fd_mode(dctx, C.byref(mode)), "pnol_lm_fd_mode")
+        np.savez(os.path.join(out, f"rank{rank}.npz"), X=X, F0=F0, FO=FO, mode=np.array([mode.value]))
+        comm.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     # the sharded J^T J kernel on its own, on a random JT
     rng = np.random.default_rng(11)
     JT = ctx.tensor(rng.standard_normal((n, m)))
@@ -59,7 +71,6 @@ def main():
     Xs, ress = run_bfgs(DeviceObjective(ctx, L.OBJ_ROSENBROCK, 3), [-1.0, 2.0, 2.0], Psw, which=4, lb=[-1.0] * 3,
                         ub=[5.0] * 3)
     # BFGS D row-sharded: this rank's rows through the collective pass / H.g
-    import ctypes as C
     nD = 700
     rng = np.random.default_rng(3)
     Dfull = rng.standard_normal((nD, nD))

@@ -77,20 +77,25 @@ def test_levmarq_mpi_m_sliced_more_ranks(tmp_path, world, m, n):
     _check_levmarq_and_normal(tmp_path, world, m, n)
 
 
-@pytest.mark.parametrize("mode", ["rows", "columns"])
-@pytest.mark.parametrize("world,m,n", [(2, 1500, 200), (4, 2000, 300), (8, 600, 130)])
-def test_levmarq_mpi_fd_modes_bitwise(tmp_path, monkeypatch, mode, world, m, n):
-    """LevMarqMPI's two Jacobian decompositions: rows mode (default; every FD column on the
-    rank's own m-slices, trial residuals shared point-to-point -- no Jacobian exchange) and
-    columns mode (PNOL_LM_FD=columns: cost-balanced FD column tiles, then the m-slice exchange).
-    X, F0 and FOpt on every rank are bitwise the single-GPU LevMarq's either way (m = 600 at 8
-    ranks: three ranks own no rows)."""
-    from parallelnonlinearoptimizationlibrary_amd import _lib as L
-    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_levmarq
-    if mode == "columns":
-        monkeypatch.setenv("PNOL_LM_FD", "columns")
+def _set_mode(monkeypatch, mode):
+    if mode == "rows":
+        monkeypatch.setenv("PNOL_LM_FD", "rows")
     else:
         monkeypatch.delenv("PNOL_LM_FD", raising=False)
+
+
+@pytest.mark.parametrize("mode", ["rows", "columns"])
+@pytest.mark.parametrize("world,m,n", [(2, 1500, 200), (4, 2000, 300), (8, 600, 130), (3, 1000, 700)])
+def test_levmarq_mpi_fd_modes_bitwise(tmp_path, monkeypatch, mode, world, m, n):
+    """LevMarqMPI's two Jacobian decompositions: columns mode (default, the reference's:
+    cost-balanced FD column tiles per rank, each tile's m-slices exchanged behind its launch) and
+    rows mode (PNOL_LM_FD=rows: every FD column on the rank's own m-slices, trial residuals
+    shared point-to-point -- no Jacobian exchange).  X, F0 and FOpt on every rank are bitwise the
+    single-GPU LevMarq's either way (m = 600 at 8 ranks: three ranks own no rows; n = 700 at 3
+    ranks: unequal tile counts, so rank 2 sits out the last exchange phase)."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_levmarq
+    _set_mode(monkeypatch, mode)
     _run_workers(tmp_path, world, m, n, "lm")
     monkeypatch.delenv("PNOL_LM_FD", raising=False)
     ctx = Context(0)
@@ -102,26 +107,58 @@ def test_levmarq_mpi_fd_modes_bitwise(tmp_path, monkeypatch, mode, world, m, n):
         assert np.array_equal(z["F0"], F01) and np.array_equal(z["FO"], FO1), (mode, r)
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_levmarq_mpi_cfg4_full_size_bitwise(tmp_path, monkeypatch, world):
-    """cfg 4's decomposition at the headline size (m = 16384, n = 2048;
-    LevenbergMarquardtMPI.cpp:12-172 with the FD Jacobian of PNOL_Objective.cpp:202-299): rows
-    mode over 2 and 4 ranks (sharing the box's GPU, host communicator) gives X, F0 and FOpt after
-    5 trips bitwise equal to the one-GPU LevMarq, which test_lm_cfg3_full_size_matches_oracle_trips
-    holds to the oracle's trips."""
+@pytest.mark.parametrize("mode", ["columns", "rows"])
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_levmarq_mpi_cfg4_full_size_bitwise(tmp_path, monkeypatch, mode, world):
+    """cfg 4 at the headline size (m = 16384, n = 2048; LevenbergMarquardtMPI.cpp:12-172 with the
+    FD Jacobian of PNOL_Objective.cpp:202-299): columns mode (the reference's decomposition, the
+    bench's headline: FD column tiles per rank + the phased m-slice exchange) and rows mode over
+    2, 4 and 8 ranks (sharing the box's GPU, host communicator) give X, F0 and FOpt after 5 trips
+    bitwise equal to the one-GPU LevMarq, which test_lm_cfg3_full_size_matches_oracle_trips holds
+    to the oracle's trips."""
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_levmarq
     m, n = 16384, 2048
+    _set_mode(monkeypatch, mode)
+    _run_workers(tmp_path, world, m, n, "lmonly")
     monkeypatch.delenv("PNOL_LM_FD", raising=False)
-    _run_workers(tmp_path, world, m, n, "lm")
     ctx = Context(0)
     obj = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
     X1, F01, FO1, _ = run_levmarq(obj, np.zeros(n), (0.001, 10.0, 1e-7, 5, 0.0, -1), which=0)
     obj.close()
     for r in range(world):
         z = np.load(tmp_path / f"rank{r}.npz")
+        assert int(z["mode"][0]) == (1 if mode == "rows" else 0), r
         assert np.array_equal(z["X"], X1), r
         assert np.array_equal(z["F0"], F01) and np.array_equal(z["FO"], FO1), r
+
+
+def test_levmarq_mpi_mode_disagreement_is_refused(tmp_path):
+    """The FD decomposition is read once per LevMarqMPI solve and must be the same on every rank
+    (the two modes pair different transfers): ranks started with different PNOL_LM_FD stop with
+    an error instead of mismatching their exchanges."""
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", PNOL_DEVICE="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.pop("PNOL_LM_FD", None)
+        if r == 1:
+            env["PNOL_LM_FD"] = "rows"
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_mpi_worker.py"), str(tmp_path),
+                                       "600", "130", "lmonly"], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT))
+    outs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=120)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(o.decode(errors="replace"))
+    assert all(p.returncode != 0 for p in procs), "\n".join(o[-2000:] for o in outs)
+    assert any("disagree on PNOL_LM_FD" in o for o in outs)
 
 
 @pytest.mark.parametrize("world", [2, 3])
