@@ -194,15 +194,15 @@ int pnol_lm_normal_mpi_d(pnol_ctx* ctx, const double* JTs, int m, int n, double 
 /* rhs = -(J^T F), LevenbergMarquardt.cpp:78-80 */
 int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
 /* sigma = A^{-1} rhs, replacing luSolve(A, rhs, sigma), LevenbergMarquardt.cpp:83.
- * method 0 = auto (n <= PNOL_SEQ_MAX: reference LU; else method 4, LU on a non-positive
- * pivot), 1 = Cholesky (per-panel launches), 2 = LU with partial pivoting (reference operation
- * order), 3 = Cholesky as one persistent tile-DAG launch (experimental), 4 = lookahead tile
- * Cholesky with diagonal-tile inverses, one launch per panel, forward solve folded in, 5 = the
- * same factorisation (bitwise) as one persistent launch: one workgroup runs the diagonal chain,
- * the others take the panel / update tiles from an ordered queue (the default of method 0;
- * PNOL_CHOL_PERSIST=0 makes method 0 use 4).  Methods 1 and 3 consume A (overwritten by its
- * factor); methods 4 and 5 factor a padded copy and leave A intact.  info (host, nullable) gets the method family used (1 = Cholesky, 2 = LU)
- * or -1 on a singular matrix. */
+ * method 0 = auto (n <= PNOL_SEQ_MAX: reference LU; else the tile Cholesky, LU on a non-positive
+ * pivot), 2 = LU with partial pivoting (reference operation order), 4 = lookahead tile Cholesky
+ * with diagonal-tile inverses, one launch per panel step, forward solve folded in, 5 = the same
+ * factorisation (bitwise) as one persistent launch: one workgroup runs the diagonal chain, the
+ * others take the panel / update tiles from an ordered queue (the default of method 0;
+ * PNOL_CHOL_PERSIST=0 makes method 0 use 4).  Methods 4 and 5 factor a padded copy and leave A
+ * intact.  (Methods 1 and 3, the per-panel-launch and tile-DAG Cholesky forms, were removed:
+ * PNOL_ERR_UNSUPPORTED.)  info (host, nullable) gets the method family used (1 = Cholesky,
+ * 2 = LU) or -1 on a singular matrix. */
 int pnol_solve_d(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n,
                  int method, int* info);
 /* The method-4 Cholesky solve queued without any host wait: *dinfo (a device int) ends 0 on
@@ -281,9 +281,8 @@ int pnol_fd_jtj_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* 
                   double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, int nchunks);
 /* pnol_fd_jtj_d (nchunks = 1) + pnol_jtr_d(JT, F0, rhs) in one queue (LevenbergMarquardt.cpp:55-80):
  * the FD Jacobian, A = J^T J with the Marquardt diagonal, and rhs = -(J^T F0), where F0 = F(x)
- * as computed or reused per compute_f0.  The -J^T F GEMV is launched behind the J^T J partial
- * tiles without a stream barrier, so it runs on the CUs the J^T J frees in its last dispatch
- * round.  Bitwise the same JT, A and rhs as the separate calls. */
+ * as computed or reused per compute_f0.  The -J^T F slice tree rides in the J^T J reduce launch.
+ * Bitwise the same JT, A and rhs as the separate calls. */
 int pnol_fd_normal_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0, int compute_f0,
                      double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, double* rhs);
 /* The FD Jacobian rows of a tile list (columns [start[t], start[t] + count[t]), count <=

@@ -123,22 +123,18 @@ class LMDevice {
     }
 
     // Single process, device objective: the FD Jacobian and A = J^T J + lambda diag(J^T J) in
-    // one call (PNOL_FD_CHUNKS > 1 pipelines FD column chunks beside the J^T J rows they
-    // complete; at cfg 3 that measured slower than back to back, so the default is 1);
-    // bitwise the same J and A as jacobian() + the J^T J of step().
+    // one call, back to back (pnol_fd_jtj_d can also pipeline FD column chunks beside the J^T J
+    // rows they complete; at cfg 3 that measured slower, so the loop does not use it); bitwise the
+    // same J and A as jacobian() + the J^T J of step().
     bool jacobianAndNormal(MultiObjective* obj, std::vector<double>& X, std::vector<double>& dX, double lambda) {
         pnol_dobj* d = obj->deviceObjective();
         if (!d) return false;
-        static const int chunks = [] {
-            const char* e = std::getenv("PNOL_FD_CHUNKS");
-            return e ? std::atoi(e) : 1;   // measured: chunked overlap is slower at cfg 3
-        }();
         uploadX(X);
         uploadH(dX);
         // x_ still holds the point F_ was evaluated at: reuse F_ and its checkpoints
         const bool reuse = ckpt_valid_;
         check(pnol_fd_jtj_d(ctx_, d, x_.get(), h_.get(), reuse ? F_.get() : F0_.get(), reuse ? 3 : 1, JT_.get(),
-                            ldjt_, lambda, A_.get(), lda_, nullptr, chunks),
+                            ldjt_, lambda, A_.get(), lda_, nullptr, 1),
               "fd_jtj");
         obj->countEvals(n_ + 1);
         return true;

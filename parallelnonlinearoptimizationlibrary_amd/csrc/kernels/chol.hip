@@ -237,19 +237,7 @@ __device__ __forceinline__ bool spin_all(const int* const (&f)[N], const int (&t
     }
 }
 
-// ---- the diagonal tile: blocked Cholesky + inverse ---------------------------------------
-// The 64 x 64 tile is factored as two 32-wide panels:
-//   P1  wave 0: the 64 x 32 panel [S11; S21] (lane t = row t, 32 entries in registers) gives
-//       L11 and L21 together; wave 1 forms W11 = L11^{-1} one column step behind
-//   P2  S22 -= L21 L21^T (fp64 MFMA, three 16 x 16 quadrants)
-//   P3  wave 0: the 32 x 32 panel S22 -> L22; wave 1: W22 = L22^{-1}; waves 2, 3 meanwhile
-//       form T = L21 W11 (MFMA)
-//   P4  W21 = -W22 T (MFMA)
-// Panel steps are software-pipelined: after column J is formed, lane J+1 alone needs the
-// broadcast l_{J+1,J} to update its diagonal entry, so the next pivot (readlane + rsqrt +
-// two Newton steps) is issued before the rest of the rank-1 update, whose LDS broadcasts
-// and FMAs then overlap that latency chain.  Column J and 1/L_JJ go to LDS (Lc, rinv); every
-// 2 steps an LDS counter tells wave 1 how many columns are final.
+// ---- the diagonal tile: LDS words and copies ------------------------------------------------
 constexpr int kHalf = 32;
 constexpr int kS = kHalf + 1;   // row stride of the LDS copies of the tile halves
 
@@ -277,185 +265,6 @@ __device__ __forceinline__ void wait_lds_ge(const int* cnt, int target) {
         : "vcc", "memory");
 }
 
-// Column J's broadcast as wave 0 holds it for the rank-1 update: entries k = K0 .. 31 in pairs.
-template <int J>
-struct ColBuf {
-    static constexpr int K0 = (J + 2) & ~1, NR = (kHalf - K0) / 2;
-    double2 v[NR > 0 ? NR : 1];
-};
-
-// One step of a 32-wide panel (wave 0).  On entry piv / r are the pivot of column J and its
-// reciprocal square root; on exit those of column J + 1.  Lc is column-major with stride LDC.
-// Software-pipelined one step deep: step J's region holds its own pivot chain for column J + 1
-// (readlane, rsqrt) beside the tail of step J-1's rank-1 update (k >= J + 2, with the previous
-// column lp / cp still in registers), and only the entry k = J + 2 of its own update, which
-// the next pivot needs.  Each entry still receives its updates in column order.
-// SPLIT > 0 (the first panel): the updates of entries k >= SPLIT + 2 by columns < SPLIT are
-// the helper wave's (panel_helper); wave 0 takes those entries over from LDS at step SPLIT,
-// after its pivot chain.  Every entry still receives the same fmas in column order.
-// kHelpCols: the columns whose updates of entries >= kHelpK the helpers apply; wave 0 takes
-// the entries over at step kHandoff.  Measured
-// (tools/microbench/diag_timing.hip): the first panel 10.5k -> 9.3k cycles with 16 columns and
-// two helper waves (12 or 14 columns: no better -- the helpers trail wave 0 by ~800 cycles of
-// LDS signal and read latency at the hand-off either way).
-#ifndef PNOL_CHOL_HELP_COLS
-#define PNOL_CHOL_HELP_COLS 16
-#endif
-#ifndef PNOL_CHOL_LOCAL_PIV
-#define PNOL_CHOL_LOCAL_PIV 1
-#endif
-constexpr int kSplit = 16, kHelpK = kSplit + 2, kHelpCols = PNOL_CHOL_HELP_COLS;
-// the hand-off step: before column kHelpCols's tail reaches the helpers' entries, and before
-// step kHelpK - 2's immediate update of entry kHelpK
-constexpr int kHandoff = kHelpCols + 1 < kHelpK - 2 ? kHelpCols + 1 : kHelpK - 2;
-static_assert(kHelpCols <= kSplit, "helpers apply at most the first kSplit columns");
-
-template <int J, int LDC, bool STAMP = false, int SPLIT = 0>
-__device__ __forceinline__ void panel_step(double (&a)[kHalf], double& piv, double& r, double lp,
-                                           const ColBuf<J - 1>& cp, double* __restrict__ Lc,
-                                           double* __restrict__ rinv, int* cnt, int cbase, int t, bool& bad,
-                                           long long* st = nullptr, const double* hs = nullptr) {
-    if constexpr (STAMP && (J & 7) == 0) st[J >> 3] = __builtin_amdgcn_s_memtime();   // microbenchmark only
-    // lane J: a[J] * r = piv / sqrt(piv), the diagonal; lanes t < J scale upper-triangle
-    // entries nobody reads (column J above the diagonal is never consumed)
-    const double l = a[J] * r, rJ = r;
-    a[J] = l;
-    if constexpr (J + 1 < kHalf) {
-        const double l1 = readlane_d(l, J + 1);
-#if PNOL_CHOL_LOCAL_PIV
-        // the critical chain: lane J+1 holds both l_{J+1,J} (its own l) and the entry (J+1, J+1),
-        // so it forms the next pivot without the broadcast -- fma(-l, l, .) there is the same
-        // operation on the same operands as fma(-l, l1, .) -- and one readlane remains on the chain
-        piv = readlane_d(fma(-l, l, a[J + 1]), J + 1);
-        a[J + 1] = fma(-l, l1, a[J + 1]);
-#else
-        a[J + 1] = fma(-l, l1, a[J + 1]);
-        piv = readlane_d(a[J + 1], J + 1);
-#endif
-        bad |= !(piv > 0.0);
-        r = rsqrt_nr(piv);
-    }
-    if constexpr (SPLIT > 0 && J == kHandoff) {
-        // take over entries k >= SPLIT + 2, updated by the helper wave with columns 0 .. SPLIT-1
-        wait_lds_ge(cnt + 4, 1);
-        wait_lds_ge(cnt + 5, 1);
-#pragma unroll
-        for (int k = SPLIT + 2; k < kHalf; ++k) a[k] = hs[t * (kHalf - SPLIT - 2) + k - SPLIT - 2];
-    }
-    // beside it: the tail of step J-1's update (k >= J + 2) ...
-    if constexpr (J >= 1) {
-        constexpr int KLIM = (SPLIT > 0 && J - 1 < kHelpCols) ? kHelpK : kHalf;   // helpers' entries excluded
-#pragma unroll
-        for (int q = 0; q < ColBuf<J - 1>::NR; ++q) {
-            const int k = ColBuf<J - 1>::K0 + 2 * q;
-            if (k >= J + 2 && k < KLIM) a[k] = fma(-lp, cp.v[q].x, a[k]);
-            if (k + 1 >= J + 2 && k + 1 < KLIM) a[k + 1] = fma(-lp, cp.v[q].y, a[k + 1]);
-        }
-    }
-    // ... and the one entry of step J's update the next step's chain needs (l_{J+2,J} by readlane)
-    if constexpr (J + 2 < kHalf) a[J + 2] = fma(-l, readlane_d(l, J + 2), a[J + 2]);
-    // column J to LDS (wave 1 and the rest of step J's update, applied in step J+1's region)
-    Lc[J * LDC + t] = l;
-    rinv[cbase + J] = rJ;   // every lane stores the same value: no divergent branch in the chain
-    if constexpr ((J & 1) == 1) lds_signal(cnt, cbase + J + 1);
-    ColBuf<J> cv;
-    if constexpr (J + 1 < kHalf) {
-#pragma unroll
-        for (int q = 0; q < ColBuf<J>::NR; ++q)
-            cv.v[q] = *reinterpret_cast<const double2*>(Lc + J * LDC + ColBuf<J>::K0 + 2 * q);
-    }
-    asm volatile("" ::: "memory");   // keep the next steps' LDS reads from being hoisted here
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (J + 1 < kHalf)
-        panel_step<J + 1, LDC, STAMP, SPLIT>(a, piv, r, l, cv, Lc, rinv, cnt, cbase, t, bad, st, hs);
-}
-
-// The helper waves of the first panel: entries k in [K0, K1) (K0 >= kHelpK) of every row take
-// the updates of columns 0 .. kSplit-1 here (the same fma(-l_row, l_k, entry) in column
-// order), then go to LDS for wave 0 (its flag).  Columns are read in pairs once wave 0 has signalled them.
-template <int LDC, int K0, int K1>
-__device__ __forceinline__ void panel_helper(const double* __restrict__ Sl, const double* __restrict__ Lc, int* cnt,
-                                             double* __restrict__ hs, int* flag, int lane) {
-    constexpr int NB_ = K1 - K0, NH = kHalf - kHelpK;
-    static_assert(NB_ % 2 == 0 && K0 % 2 == 0, "pairs of entries");
-    double b[NB_];
-#pragma unroll
-    for (int i = 0; i < NB_; ++i) b[i] = Sl[lane * kS + K0 + i];
-#pragma unroll 1
-    for (int c = 0; c < kHelpCols; c += 2) {   // two columns per signal, all their reads in flight at once
-        wait_lds_ge(cnt, c + 2);
-        const double lt0 = Lc[c * LDC + lane], lt1 = Lc[(c + 1) * LDC + lane];
-        double2 k0[NB_ / 2], k1[NB_ / 2];
-#pragma unroll
-        for (int i = 0; i < NB_ / 2; ++i) {
-            k0[i] = *reinterpret_cast<const double2*>(Lc + c * LDC + K0 + 2 * i);
-            k1[i] = *reinterpret_cast<const double2*>(Lc + (c + 1) * LDC + K0 + 2 * i);
-        }
-#pragma unroll
-        for (int i = 0; i < NB_ / 2; ++i) {
-            b[2 * i] = fma(-lt0, k0[i].x, b[2 * i]);
-            b[2 * i + 1] = fma(-lt0, k0[i].y, b[2 * i + 1]);
-            b[2 * i] = fma(-lt1, k1[i].x, b[2 * i]);
-            b[2 * i + 1] = fma(-lt1, k1[i].y, b[2 * i + 1]);
-        }
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int i = 0; i < NB_; ++i) hs[lane * NH + K0 - kHelpK + i] = b[i];
-    lds_signal(flag, 1);   // in order after the data writes (one wave's LDS ops are ordered)
-}
-
-// One step of the inverse of a 32 x 32 lower factor (wave 1, lane c = column c of W):
-// w_J = y_J / L_JJ, then y_k -= L_kJ w_J for k > J.
-template <int J, int LDC>
-__device__ __forceinline__ void inv_step(double (&y)[kHalf], const double* __restrict__ Lc,
-                                         const double* __restrict__ rinv, const int* cnt, int cbase) {
-    // two columns per region (the signal granularity): both broadcasts and both reciprocals
-    // are requested at once, then the two substitution steps
-    static_assert((J & 1) == 0, "two steps per call");
-    wait_lds_ge(cnt, cbase + J + 2);
-    constexpr int K0 = (J + 1) & ~1, NR = (kHalf - K0) / 2;   // column J: entries from K0 (= J)
-    double2 c0[NR > 0 ? NR : 1], c1[NR > 0 ? NR : 1];
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-        c0[q] = *reinterpret_cast<const double2*>(Lc + J * LDC + K0 + 2 * q);
-        c1[q] = *reinterpret_cast<const double2*>(Lc + (J + 1) * LDC + K0 + 2 * q);
-    }
-    const double r0 = rinv[cbase + J], r1 = rinv[cbase + J + 1];
-    __builtin_amdgcn_sched_barrier(0);
-    const double w0 = y[J] * r0;
-    y[J] = w0;
-    y[J + 1] = fma(-c0[0].y, w0, y[J + 1]);   // K0 == J: c0[0] = (L_JJ, L_J+1,J)
-    const double w1 = y[J + 1] * r1;
-    y[J + 1] = w1;
-#pragma unroll
-    for (int q = 1; q < NR; ++q) {
-        const int k = K0 + 2 * q;
-        y[k] = fma(-c0[q].x, w0, y[k]);
-        y[k + 1] = fma(-c0[q].y, w0, y[k + 1]);
-        y[k] = fma(-c1[q].x, w1, y[k]);
-        y[k + 1] = fma(-c1[q].y, w1, y[k + 1]);
-    }
-    asm volatile("" ::: "memory");   // keep the next steps' LDS reads from being hoisted here
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (J + 2 < kHalf) inv_step<J + 2, LDC>(y, Lc, rinv, cnt, cbase);
-}
-
-// Wave 1's part of a panel: W = L^{-1} of the 32 x 32 factor whose columns appear in Lc, stored
-// row-major into Wl.  Lanes >= 32 (all-zero columns) store into the 32 doubles after Wl
-// instead of branching: a divergent branch after the register chain makes it spill.
-template <int LDC>
-__device__ __forceinline__ void panel_inverse(const double* __restrict__ Lc, const double* __restrict__ rinv,
-                                                         const int* cnt, int cbase, double* __restrict__ Wl, int lane) {
-    double y[kHalf];
-#pragma unroll
-    for (int k = 0; k < kHalf; ++k) y[k] = (k == lane) ? 1.0 : 0.0;
-    inv_step<0, LDC>(y, Lc, rinv, cnt, cbase);
-#pragma unroll
-    for (int k = 0; k < kHalf; ++k) Wl[lane < kHalf ? k * kS + lane : kHalf * kS + (lane - kHalf)] = y[k];
-}
-
 // 16 x 16 block of C = sum_k A(i, k) B(j, k) over K (v_mfma_f64_16x16x4_f64), accumulated into acc.
 template <int K, class FA, class FB>
 __device__ __forceinline__ d4 mfma_blk(d4 acc, FA fa, FB fb, int lane) {
@@ -477,24 +286,14 @@ __device__ __forceinline__ d4 mfma_blk(d4 acc, FA fa, FB fb, int lane) {
 }
 
 struct DiagLds {
-    double* Sl;    // 64 x 32 left half of the tile, stride kS (dead after P1 starts)
+    double* Sl;    // 64 x 32 left half of the tile, stride kS
     double* S22;   // 32 x 32 bottom-right quarter, stride kS
-    double* Lc1;   // P1 columns, column-major, stride 64
-    double* Lc2;   // P3 columns, column-major, stride 64 (lanes >= 32 fill rows 32..63 with zeros)
-    double* W11;   // 32 x 32 row-major, row stride kS (conflict-free fragment reads), + 32 discard
-    double* W22;   // the same (in the Sl space)
-    double* Tl;    // 32 x 32 row-major (in the Sl space)
 };
 
 __device__ __forceinline__ DiagLds diag_lds(double* smem) {
     DiagLds L;
     L.Sl = smem;
-    L.Tl = smem;
-    L.W22 = smem + 1024;
     L.S22 = smem + 64 * kS;
-    L.Lc1 = L.S22 + kHalf * kS;
-    L.Lc2 = L.Lc1 + 64 * kHalf;
-    L.W11 = L.Lc2 + 64 * kHalf;
     return L;
 }
 
@@ -508,133 +307,11 @@ struct NoEarly {
     __device__ void operator()(int, int) const {}
 };
 
+// ---- the diagonal tile: Cholesky + inverse in 16-wide micro-panels -------------------------
 // Factor the tile held in L.Sl / L.S22 and write W_d = L_dd^{-1} (64 x 64 row-major) to Wd.
-// STAMP: s_memtime stamps of the phases into st[0..31] (tools/microbench/diag_timing.hip only).
-// early(wave, lane): run by waves 2 and 3 once T is formed, while waves 0 / 1 finish the second
-// panel (the persistent chain's look-ahead for the next tile, EarlyNext).  Wst != nullptr: rows
-// 32..63 of W_d also go to Wst in the substage layout (the next tile's L = A W^T operand).
-template <bool STAMP = false, bool SC1 = false, class EARLY = NoEarly>
-__device__ __forceinline__ void factor_diag32(const DiagLds& L, double* __restrict__ rinv, int* cnt,
-                                            double* __restrict__ Wd, int d, int* info, long long* st = nullptr,
-                                            const EARLY& early = EARLY(), double* __restrict__ Wst = nullptr) {
-    const int t = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
-    // The phases are chained by LDS words instead of workgroup barriers, so the inverse wave
-    // finishing W11 overlaps the S22 update:  cnt[0] = final panel columns, cnt[1] = W11 done,
-    // cnt[2] / cnt[3] = S22 quadrants (1,0) / (1,1) done, cnt[4] / cnt[5] = the helpers' entries
-    // are in LDS.  All are zero on entry.
-    int* flags = cnt + 1;
-    const double* L21 = L.Lc1 + kHalf;
-    if (wave == 0) {
-        {   // P1
-            double a[kHalf];
-#pragma unroll
-            for (int k = 0; k < kHalf; ++k) a[k] = L.Sl[lane * kS + k];
-            double piv = readlane_d(a[0], 0);
-            bool bad = !(piv > 0.0);
-            double r = rsqrt_nr(piv);
-            const ColBuf<-1> none{};
-            panel_step<0, 64, STAMP, kSplit>(a, piv, r, 0.0, none, L.Lc1, rinv, cnt, 0, lane, bad, st, L.Lc2);
-            if constexpr (STAMP) st[4] = __builtin_amdgcn_s_memtime();
-            if (bad && lane == 0) atomicCAS(info, 0, d * NB + 1);
-        }
-        {   // P2, quadrant (0,0): S22 -= L21 L21^T
-            d4 acc;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) acc[r] = L.S22[((lane >> 4) + 4 * r) * kS + (lane & 15)];
-            acc = mfma_blk<kHalf>(acc, [&](int i, int k) { return -L21[k * 64 + i]; },
-                                  [&](int j, int k) { return L21[k * 64 + j]; }, lane);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) L.S22[((lane >> 4) + 4 * r) * kS + (lane & 15)] = acc[r];
-        }
-        if constexpr (STAMP) st[6] = __builtin_amdgcn_s_memtime();
-        wait_lds_ge(flags + 1, 1);
-        wait_lds_ge(flags + 2, 1);
-        {   // P3
-            double a[kHalf];
-#pragma unroll
-            for (int k = 0; k < kHalf; ++k) a[k] = lane < kHalf ? L.S22[lane * kS + k] : 0.0;
-            double piv = readlane_d(a[0], 0);
-            bool bad = !(piv > 0.0);
-            double r = rsqrt_nr(piv);
-            if constexpr (STAMP) st[8] = __builtin_amdgcn_s_memtime();
-            const ColBuf<-1> none{};
-            panel_step<0, 64, STAMP>(a, piv, r, 0.0, none, L.Lc2, rinv, cnt, kHalf, lane, bad, st + 9);
-            if constexpr (STAMP) st[13] = __builtin_amdgcn_s_memtime();
-            if (bad && lane == 0) atomicCAS(info, 0, d * NB + kHalf + 1);
-        }
-    } else if (wave == 1) {
-        panel_inverse<64>(L.Lc1, rinv, cnt, 0, L.W11, lane);
-        lds_signal(flags, 1);
-        if constexpr (STAMP) st[5] = __builtin_amdgcn_s_memtime();
-        panel_inverse<64>(L.Lc2, rinv, cnt, kHalf, L.W22, lane);
-        if constexpr (STAMP) st[14] = __builtin_amdgcn_s_memtime();
-    } else {
-        const int qi = 1, qj = wave - 2;   // P2 quadrants (1,0) and (1,1)
-        // the first panel's helpers (entries 18..23 / 24..31); Lc2 is free until P3
-        if (wave == 2) panel_helper<64, kHelpK, 24>(L.Sl, L.Lc1, cnt, L.Lc2, cnt + 4, lane);
-        else panel_helper<64, 24, kHalf>(L.Sl, L.Lc1, cnt, L.Lc2, cnt + 5, lane);
-        wait_lds_ge(cnt, kHalf);
-        d4 acc;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = L.S22[(qi * 16 + (lane >> 4) + 4 * r) * kS + qj * 16 + (lane & 15)];
-        acc = mfma_blk<kHalf>(acc, [&](int i, int k) { return -L21[k * 64 + qi * 16 + i]; },
-                              [&](int j, int k) { return L21[k * 64 + qj * 16 + j]; }, lane);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) L.S22[(qi * 16 + (lane >> 4) + 4 * r) * kS + qj * 16 + (lane & 15)] = acc[r];
-        lds_signal(flags + wave - 1, 1);
-        // T = L21 W11, rows 16 (wave - 2) .. +16, once W11 is in LDS
-        wait_lds_ge(flags, 1);
-        const int ti = wave - 2;
-#pragma unroll
-        for (int tj = 0; tj < 2; ++tj) {
-            d4 tacc = {0.0, 0.0, 0.0, 0.0};
-            tacc = mfma_blk<kHalf>(tacc, [&](int i, int k) { return L21[k * 64 + ti * 16 + i]; },
-                                   [&](int j, int k) { return L.W11[k * kS + tj * 16 + j]; }, lane);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) L.Tl[(ti * 16 + (lane >> 4) + 4 * r) * kHalf + tj * 16 + (lane & 15)] = tacc[r];
-        }
-        early(wave, lane);
-    }
-    __syncthreads();
-    if constexpr (STAMP) if (wave == 0) st[15] = __builtin_amdgcn_s_memtime();
-    // P4: W21 = -W22 T
-    const int qi = wave >> 1, qj = wave & 1;
-    d4 w21 = {0.0, 0.0, 0.0, 0.0};
-    w21 = mfma_blk<kHalf>(w21, [&](int i, int k) { return -L.W22[(qi * 16 + i) * kS + k]; },
-                          [&](int j, int k) { return L.Tl[k * kHalf + qj * 16 + j]; }, lane);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) stg<SC1>(Wd + (kHalf + qi * 16 + (lane >> 4) + 4 * r) * NB + qj * 16 + (lane & 15), w21[r]);
-    if constexpr (STAMP) if (wave == 0) st[16] = __builtin_amdgcn_s_memtime();
-    // W11, W22 and the zero upper-right block: thread t writes columns (t & 31) of rows t >> 5 + 8 q
-    {
-        const int c = t & 31, r0 = t >> 5;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int r = r0 + 8 * q;
-            stg<SC1>(Wd + r * NB + c, L.W11[r * kS + c]);
-            stg<SC1>(Wd + r * NB + kHalf + c, 0.0);
-            stg<SC1>(Wd + (kHalf + r) * NB + kHalf + c, L.W22[r * kS + c]);
-        }
-    }
-    if (Wst) {
-        // rows 32..63 of W_d ([W21 | W22]) in the substage layout; Wst overlaps Lc1 / Lc2 / W11,
-        // whose last reads (the W11 stores above) end at this barrier; W22 lives in the Sl space
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            Wst[qj * kSub + (kHalf + qi * 16 + (lane >> 4) + 4 * r) * kPad + (lane & 15)] = w21[r];
-        const int c = t & 31, r0 = t >> 5;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int r = r0 + 8 * q;
-            Wst[(2 + (c >> 4)) * kSub + (kHalf + r) * kPad + (c & 15)] = L.W22[r * kS + c];
-        }
-    }
-}
-
-// ---- the diagonal tile in 16-wide micro-panels (PNOL_CHOL_MP, the default) --------------------
-// factor_diag32's chain wave issues every rank-1 update of a 32-wide panel itself (~290 cycles
-// per pivot, 23k cycles per tile).  Here the tile is four 64 x 16 micro-panels:
+// (A 32-wide two-panel form, whose chain wave issued every rank-1 update of its panel itself,
+// ran ~290 cycles per pivot, 23k cycles per tile; removed in round 4.)  The tile is four 64 x 16
+// micro-panels:
 //   wave 0      the pivot chain of micro-panel p (rows 16p .. 63, one row per lane, 16 entries in
 //               registers): per pivot at most 14 rank-1 fmas, software-pipelined as panel_step;
 //               column c and 1 / L_cc go to LDS, every 2 columns a counter in LDS
@@ -648,19 +325,12 @@ __device__ __forceinline__ void factor_diag32(const DiagLds& L, double* __restri
 //               the off-diagonal blocks of W = L^{-1} by block rows, W_ij = -V_i X_ij with
 //               X_ij = sum_{k=j}^{i-1} L_ik W_kj accumulated as soon as its operands exist, so only
 //               W_3j = -V_3 X_3j (three products, waves 0 and 1) follow the last pivot.
-// Every accumulator receives its MFMAs in a fixed order, so W is deterministic; it is not bitwise
-// factor_diag32's (other summation order), and methods 4 and 5 both use this factor.
+// Every accumulator receives its MFMAs in a fixed order, so W is deterministic; methods 4 and 5
+// both use this factor.
 // LDS (doubles, from L.Sl): the tile (Sl / S22, 3168), the panels' columns (2560), the W blocks
 // (10 x 288), a 64-double discard row; the X hand-off blocks reuse Sl rows 0 .. 26, dead once
 // micro-panel 1 is in registers.  Words: cnt[0] final columns, cnt[1] W rows 0..31 done,
 // cnt[2] / cnt[3] waves 2 / 3 have stored micro-panel cnt's blocks, cnt[4] V_3 and X_3j in LDS.
-#ifndef PNOL_CHOL_MP
-#define PNOL_CHOL_MP 1
-#endif
-// k_chol_persist: row k+2's panel task also applies column k to tiles (k+2, k+1) and (k+2, k+2)
-#ifndef PNOL_CHOL_FUSE
-#define PNOL_CHOL_FUSE 0
-#endif
 constexpr int kMW = 16;            // micro-panel width
 constexpr int kBP = 18;            // row stride of a 16 x 16 block in LDS (conflict-free fragments)
 constexpr int kBlk = 16 * kBP;     // doubles per block
@@ -691,19 +361,9 @@ static_assert(3 * kBlk <= kHalf * kS, "X hand-off blocks fit Sl rows 0..31");
 
 // the W_d rows 0..31 operand of EarlyNext: element (r, c), c <= r block-wise
 __device__ __forceinline__ double w11_at(const double* W11, int r, int c) {
-#if PNOL_CHOL_MP
     return W11[lblk(r >> 4, c >> 4) * kBlk + (r & 15) * kBP + (c & 15)];
-#else
-    return W11[r * kS + c];
-#endif
 }
-__device__ __forceinline__ const double* diag_w11(const DiagLds& L) {
-#if PNOL_CHOL_MP
-    return mp_lds(L).Wb;
-#else
-    return L.W11;
-#endif
-}
+__device__ __forceinline__ const double* diag_w11(const DiagLds& L) { return mp_lds(L).Wb; }
 
 // tile entry (row, col), lower triangle, in the diag_put layout
 __device__ __forceinline__ double* mp_s(const MpLds& M, int row, int col) {
@@ -1043,11 +703,7 @@ template <bool STAMP = false, bool SC1 = false, class EARLY = NoEarly>
 __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict__ rinv, int* cnt,
                                             double* __restrict__ Wd, int d, int* info, long long* st = nullptr,
                                             const EARLY& early = EARLY(), double* __restrict__ Wst = nullptr) {
-#if PNOL_CHOL_MP
     factor_diag16<STAMP, SC1, EARLY>(L, rinv, cnt, Wd, d, info, st, early, Wst);
-#else
-    factor_diag32<STAMP, SC1, EARLY>(L, rinv, cnt, Wd, d, info, st, early, Wst);
-#endif
 }
 
 // ---- the diagonal workgroup's two products, balanced over its 4 waves --------------------
@@ -1680,7 +1336,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             if (t == 0 && k + 1 < 64) g_chol_clk[8 * (k + 1) + 6] = pre ? 1 : 0;
 #endif
             if (pre) late_prepare(E, Y, L, wave, lane);
-            else diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane, PNOL_CHOL_MP && d > 1);
+            else diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane, d > 1);
             if (t < 6) cnt[t] = 0;   // every read of cnt / ew above is behind a barrier inside
             if (t < 4) ew[t] = 0;    // either prepare
             __syncthreads();
@@ -1689,8 +1345,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
                 factor_diag<false, true, EarlyNext>(L, rinv, cnt, W + (long)d * NB * NB, d, info, nullptr,
                                                     EarlyNext{P, ldp, T, d, pw.ver, diag_w11(L), cnt, lookahead, E}, Y);
             else   // micro-panel factor: W_d also stays in Y for the next diag_prepare
-                factor_diag<false, true>(L, rinv, cnt, W + (long)d * NB * NB, d, info, nullptr, NoEarly(),
-                                         PNOL_CHOL_MP ? Y : nullptr);
+                factor_diag<false, true>(L, rinv, cnt, W + (long)d * NB * NB, d, info, nullptr, NoEarly(), Y);
             PNOL_CHOL_STAMP(k, 4)
             publish(pw.wdone + d, 1);   // its barrier also ends every read of this step's LDS
             PNOL_CRIT(d, 0)
@@ -1730,20 +1385,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             __syncthreads();
             if (!ok_sh) return;
             stage_tile<true>(X, P, ldp, i0, k0);
-            // row k+2 also applies column k to the two tiles the diagonal chain needs next
-            // (PNOL_CHOL_FUSE): (k+2, k+2) straight from this strip, (k+2, k+1) with panel k+1's
-            // strip -- the update tasks of those tiles are skipped.  Their tiles are loaded now,
-            // while the workgroup waits for W_k; their earlier updates and panel k+1 are tasks
-            // claimed before this one.
-            const bool fuse = PNOL_CHOL_FUSE && i == k + 2;
-            d4 accD[2][2], accO[2][2];
-            if (fuse) {
-                if (t == 0) ok_sh = spin_all<2>({pw.ver + i * T + i, pw.ver + i * T + (k + 1)}, {k, k}, info);
-                __syncthreads();
-                if (!ok_sh) return;
-                acc_load<true>(accD, P, ldp, i0, i0, wr, wc, lane);
-                acc_load<true>(accO, P, ldp, i0, k0 + NB, wr, wc, lane);
-            }
             if (t == 0) {   // W_k (tile 0 comes from the prep launch)
                 ok_sh = k == 0 || spin_ge(pw.wdone + k, 1, info);
 #ifdef PNOL_CHOL_TIMELINE
@@ -1757,53 +1398,12 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             d4 acc[4];   // this wave's 16-row strip of L_ik (nonzero K blocks of W_k^T only)
             diag_l_strip(acc, X, Y, wave, lane);
             strip_store<true>(acc, Lm, ldp, i0, k0, wave, lane);
-            // the strip in the substage layout: the same values stage_tile reads back from Lm
-            if (fuse) diag_strip_to_stage(acc, pfx, wave, lane);
-            publish(pw.lcnt + i, k + 1);   // its barrier also covers the pfx stores
+            publish(pw.lcnt + i, k + 1);
 #ifdef PNOL_CHOL_TIMELINE
             if (i == k + 2) PNOL_CRIT(k, 3)
             if (i == k + 1) PNOL_CRIT(k, 7)
 #endif
-            if (fuse) {   // the update tasks' arithmetic (mfma_xyt, X = L_ik, Y = L_jk)
-#ifdef PNOL_CHOL_TIMELINE
-                PNOL_CRIT(k, 4)
-#endif
-                if (t == 0) ok_sh = spin_ge(pw.lcnt + k + 1, k + 1, info);
-                __syncthreads();
-                if (!ok_sh) return;
-#ifdef PNOL_CHOL_TIMELINE
-                PNOL_CRIT(k, 5)
-#endif
-                // panel k+1's strip: the loads in flight while (k+2, k+2)'s MFMAs run
-                double2 lv[8];
-                {
-                    const double* base = Lm + (long)(k0 + NB) * ldp + k0;   // wave-uniform
-                    const unsigned off = (unsigned)(((t >> 2) * ldp + (t & 3) * 16) * 8);
-#pragma unroll
-                    for (int qq = 0; qq < 8; ++qq) lv[qq] = ld16_sc1(base, off + 16 * qq);
-                }
-                mfma_xyt<true>(accD, pfx, pfx, wr, wc, lane);
-                __builtin_amdgcn_sched_barrier(0);   // the MFMAs issue before the loads are waited on
-                {   // X (A_ik) is dead: every wave passed the barriers since diag_l_strip
-                    double2* dst = reinterpret_cast<double2*>(X + (t & 3) * kSub + (t >> 2) * kPad);
-#pragma unroll
-                    for (int qq = 0; qq < 8; ++qq) dst[qq] = lv[qq];
-                }
-                acc_store<true>(accD, P, ldp, i0, i0, wr, wc, lane);
-                __syncthreads();
-                mfma_xyt<true>(accO, pfx, X, wr, wc, lane);
-                acc_store<true>(accO, P, ldp, i0, k0 + NB, wr, wc, lane);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();   // also ends the reads of X before strip_to_rows
-                if (t == 0) {
-                    __hip_atomic_store(pw.ver + i * T + i, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(pw.ver + i * T + (k + 1), k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-#ifdef PNOL_CHOL_TIMELINE
-                PNOL_CRIT(k, 6)
-#endif
-            }
-            strip_to_rows(acc, X, wave, lane);   // X is free (the MFMA finished before the barrier)
+            strip_to_rows(acc, X, wave, lane);   // X is free (the products finished before the barrier)
             if (t < NB) {
                 double s = 0.0;
 #pragma unroll 16
@@ -1829,7 +1429,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         // (k+2, k+2) at f = R, and so on.  Step k's first two tasks are the tiles the chain needs
         // next, f = 1 = (k+2, k+1) and f = R = (k+2, k+2); the rest follow in column order.
         const int q = g - R;
-        if (PNOL_CHOL_FUSE && q < 2) continue;   // row k+2's panel task applied them
         int u = q == 0 ? 1 : (q == 1 ? R : (q < R ? q : q + 1));
         int j = k + 1;
         while (u >= T - j) {

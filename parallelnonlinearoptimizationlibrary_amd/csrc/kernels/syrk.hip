@@ -13,8 +13,6 @@
 //   k_syrk_reduce   sums the split-K partial tiles in a fixed order (deterministic), applies
 //                   A_ii = (1 + lambda) * JTJ_ii, writes the lower triangle and its mirror.
 //   k_jtj_seq       n <= PNOL_SEQ_MAX: the reference's summation order, bitwise.
-// The same tile kernel in "direct" mode (C = beta C + alpha X X^T on the lower tiles) is the
-// trailing update of the blocked Cholesky in solve.hip.
 #include "../pnol_internal.hpp"
 #include "../pnol_comm.hpp"
 
@@ -32,20 +30,11 @@ constexpr int kTile = 128;
 constexpr int kTK = 16;
 constexpr int kPad = 18;   // LDS row stride in doubles
 
-// MFMA fragments read from LDS 16 bytes at a time (two K-groups per read); 0: 8-byte reads,
-// one K-group each (the summation order differs between the two builds)
-#ifndef PNOL_SYRK_B128
-#define PNOL_SYRK_B128 1
-#endif
-
 // Diagonal tiles (ti == tj) of the 8-wave 128-row kernel compute only their 36 lower 16 x 16
 // blocks (bi >= bj) of the 64, 5 or 4 per wave so that the two waves of each SIMD (waves w and
 // w + 4) hold 9 together -- the busiest SIMD issues 36 MFMAs per stage instead of 64 -- and
 // zero the 28 upper blocks (no reader uses them; the partials stay fully defined).  Each block
 // runs the same MFMA chain as in the 2 x 4 wave layout, so the partials are bitwise the same.
-#ifndef PNOL_SYRK_DIAG_BAL
-#define PNOL_SYRK_DIAG_BAL 1
-#endif
 // wave w's blocks as bi * 8 + bj, 6 bits each (blocks of one block row together: they share
 // the A fragment); bits 30..31: 4 or 5 blocks.  Words, not bytes: a scalar load.
 __device__ __forceinline__ unsigned diag_blocks(int w) {
@@ -124,57 +113,33 @@ __device__ __forceinline__ void store_stage(const StageRegs<TILE, NT>& s, double
 __device__ unsigned long long g_syrk_tl[3 * 65536];
 #endif
 
-// MODE 0: write split-K partial tile to part; MODE 1: C = beta*C + alpha*acc (lower tiles);
-// MODE 4: 64 x 64 tiles into the 128 x 128 partial layout of MODE 0 (see the store below);
-// MODE 2: as MODE 0, instantiated separately for the chunked launches of launch_fd_jtj (so a
-// kernel trace tells the whole-matrix launches and the pipelined row chunks apart).
+// MODE 0: write split-K partial tile to part; MODE 4: 64 x 64 tiles into the 128 x 128 partial
+// layout of MODE 0 (see the store below); MODE 2: as MODE 0, instantiated separately for the
+// chunked launches of launch_fd_jtj (so a kernel trace tells the whole-matrix launches and the
+// pipelined row chunks apart).
 // TILE 128: waves 2 x 2 of 64 x 64 (4 x 4 MFMA blocks each); TILE 64: 2 x 2 of 32 x 32.
 // NW = 4: waves 2 x 2, each (TILE/2)^2; NW = 8: waves 2 x 4, each TILE/2 x TILE/4 (half the
 // accumulators per wave, so twice the waves per SIMD hide the stage boundaries).
-template <int MODE, int TILE, bool XMAP = false, int NW = 4>
+template <int MODE, int TILE, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
                                                       int split_k, int kfirst, int kchunk, int sub, int slice0,
-                                                      int mS, long sstride, int umajor, double* __restrict__ part,
-                                                      double* __restrict__ C, long ldc, double alpha,
-                                                      double beta, int tile0, unsigned* __restrict__ tail_flag,
-                                                      unsigned tail_val) {
+                                                      int mS, long sstride, double* __restrict__ part, int tile0) {
     constexpr int NT = 64 * NW, WC = NW / 2;
     constexpr int WTM = TILE / 2, WTN = TILE / WC, NBM = WTM / 16, NBN = WTN / 16;
     __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
 #ifdef PNOL_SYRK_TIMELINE
     const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    // the last-dispatched workgroup announces the launch's tail (jtr_tail): a system-scope
-    // vector store the command processor's wait on this word sees; speed only, nothing in the
-    // data path depends on it
-    if (tail_flag && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
-        __hip_atomic_store(tail_flag, tail_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-
-    // XMAP (split_k a multiple of 8): the K slices s = xcd, xcd + 8, ... go to the XCD that
-    // dispatch slot blockIdx % 8 lands on, all tiles of one slice before the next, so the
-    // workgroups resident on an XCD stream the same JT columns and share them in its L2.
-    // Otherwise consecutive workgroups are the slices of one tile.
+    // every (tile, slice)'s chunk 0 first, then chunk 1, ...: with a long chunk 0 the short
+    // chunks fill the last dispatch round instead of leaving it part-empty
     int blk, t, sidx;
-    if (XMAP) {
-        const int xcd = blockIdx.x % kNumXcd, local = blockIdx.x / kNumXcd;
-        const int ntl = gridDim.x / split_k;
-        sidx = xcd + kNumXcd * (local / ntl);
-        const int tl = local % ntl;
-        blk = tl * split_k + sidx;           // partial slot: the same layout as below
-        t = tile0 + tl;
-    } else if (umajor & 1) {
-        // every (tile, slice)'s chunk 0 first, then chunk 1, ...: with a long chunk 0 the short
-        // chunks fill the last dispatch round instead of leaving it part-empty
+    {
         const int ntl = gridDim.x / split_k, nsl = split_k / sub;
         const int u0 = blockIdx.x / (ntl * nsl), rest = blockIdx.x % (ntl * nsl);
         const int tl = rest / nsl;
         sidx = (rest % nsl) * sub + u0;
-        blk = tl * split_k + sidx;
-        t = tile0 + tl;
-    } else {
-        blk = blockIdx.x;                    // partial slot (local to this launch)
-        t = tile0 + blk / split_k;           // lower-triangle tile index
-        sidx = blk % split_k;
+        blk = tl * split_k + sidx;           // partial slot (local to this launch)
+        t = tile0 + tl;                      // lower-triangle tile index
     }
     int ti, tj;
     tile_of(t, ti, tj);
@@ -201,8 +166,8 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
 #pragma unroll
         for (int j = 0; j < NBN; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
 
-    constexpr bool kBal = PNOL_SYRK_DIAG_BAL && NW == 8 && TILE == 128 && MODE != 1 && !XMAP;
-    const bool bal = kBal && diag && !(umajor & 2);
+    constexpr bool kBal = NW == 8 && TILE == 128;
+    const bool bal = kBal && diag;
     int dbi[5], dbj[5], dcnt = 0, dsplit = 0;
     {
         const int wv = __builtin_amdgcn_readfirstlane(wave);
@@ -241,7 +206,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                 load_stage<TILE, NT>(ps, X, ldx, nr, prow0, k0, kend, full);
                 if (!diag) load_stage<TILE, NT>(qs, X, ldx, nr, qrow0, k0, kend, full);
             }
-#if PNOL_SYRK_B128
             // one 16-byte fragment read per operand block covers two MFMA K-groups: lane l holds
             // k = 8 kk + 2 (l >> 4) + {0, 1}; the first MFMA takes the even k of the 8-block, the
             // second the odd ones (half the ds_read instructions; the 144-byte row stride keeps the
@@ -290,21 +254,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                         acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi].y, b[ni].y, acc[mi][ni], 0, 0, 0);
             }
             }
-#else
-#pragma unroll
-            for (int kk = 0; kk < kTK / 4; ++kk) {
-                double a[NBM], b[NBN];
-#pragma unroll
-                for (int mi = 0; mi < NBM; ++mi) a[mi] = P[(wr * WTM + mi * 16 + frow) * kPad + kk * 4 + fk];
-#pragma unroll
-                for (int ni = 0; ni < NBN; ++ni) b[ni] = Q[(wc * WTN + ni * 16 + frow) * kPad + kk * 4 + fk];
-#pragma unroll
-                for (int mi = 0; mi < NBM; ++mi)
-#pragma unroll
-                    for (int ni = 0; ni < NBN; ++ni)
-                        acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
-            }
-#endif
         }
     };
     if (kBal && bal) stage_loop(std::true_type{});
@@ -313,7 +262,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
     // f64 MFMA C/D layout: lane l, register r -> row (l >> 4) + 4 r, column l & 15
     const int ocol = lane & 15;
     const int orow = lane >> 4;
-    if (MODE == 0 || MODE == 2 || MODE == 4) {
+    {
         // MODE 4 (TILE 64, tile0 = 0): the quadrant (ti & 1, tj & 1) of the 128 x 128 partial
         // tile (ti / 2, tj / 2) -- the same partial layout, and every element summed in the same
         // order as by the 128-row kernel (one MFMA accumulator chain over the same K range)
@@ -357,20 +306,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                         __builtin_nontemporal_store(acc[mi][ni][r], out + row * ld + col);
                     }
         }
-    } else {
-#pragma unroll
-        for (int mi = 0; mi < NBM; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < NBN; ++ni)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    int i = prow0 + wr * WTM + mi * 16 + orow + 4 * r;
-                    int j = qrow0 + wc * WTN + ni * 16 + ocol;
-                    if (i < nr && j < nr && j <= i) {
-                        double* c = C + (long)i * ldc + j;
-                        *c = beta * (*c) + alpha * acc[mi][ni][r];
-                    }
-                }
     }
 #ifdef PNOL_SYRK_TIMELINE
     if (threadIdx.x == 0) {
@@ -628,20 +563,11 @@ static void launch_reduce_sr(dim3 grid, dim3 block, size_t shm, hipStream_t st, 
         hipLaunchKernelGGL((k_syrk_reduce<0, SR>), grid, block, shm, st, part, ntiles, sub, args...);
 }
 
+// 16-row strips: 70 us vs 77 us for 32-row strips at n = 2048, sub = 2
 template <typename... Args>
 static void launch_reduce(dim3 grid, dim3 block, size_t shm, hipStream_t st, const double* part, int ntiles, int sub,
                           Args... args) {
-    static const int sr = [] {
-        const char* e = std::getenv("PNOL_REDUCE_SR");
-        return e ? std::atoi(e) : 16;
-    }();
-    if (sr == 32)
-        launch_reduce_sr<32>(grid, block, shm, st, part, ntiles, sub, args...);
-    else if (sr == 8)   // the reduce itself 72-74 vs 75.5-78 us, but the trips of those runs were
-                        // not faster (4 of 6 same-box pairs slower, tools/env_ab.sh): kept optional
-        launch_reduce_sr<8>(grid, block, shm, st, part, ntiles, sub, args...);
-    else   // 16-row strips (default): 70 us vs 77 us for 32-row strips at n = 2048, sub = 2
-        launch_reduce_sr<16>(grid, block, shm, st, part, ntiles, sub, args...);
+    launch_reduce_sr<16>(grid, block, shm, st, part, ntiles, sub, args...);
 }
 
 static SliceCfg slice_cfg(int m, int ntiles) {
@@ -661,7 +587,7 @@ static SliceCfg slice_cfg(int m, int ntiles) {
     c.kchunk = ((c.mS + c.sub - 1) / c.sub + kTK - 1) / kTK * kTK;
     c.kfirst = c.kchunk;
     // Chunk 0 takes 75% of the slice (PNOL_SYRK_FIRST = percent; the rest split evenly over
-    // chunks 1..sub-1) and is dispatched first (PNOL_SYRK_UMAJOR): 1088 long workgroups, then
+    // chunks 1..sub-1) and is dispatched first (k_syrk_tile's order): 1088 long workgroups, then
     // 1088 short ones that fill the tail of the last dispatch round.  Measured at m = 16384,
     // n = 2048: 1.265 ms vs 1.326 ms for two equal chunks (tools/syrk_sweep.py).
     static const int first_pct = [] {
@@ -675,29 +601,10 @@ static SliceCfg slice_cfg(int m, int ntiles) {
     return c;
 }
 
-// J^T J variant (tuning; every variant sums each element in the same order):
-// PNOL_SYRK_NW = 8 (default) or 4 waves per 128 x 128 tile.  Measured at m = 16384, n = 2048:
-// 8 waves 1.35 ms vs 4 waves 1.40 ms.  (A split-K reduce fused into the tile kernel by the last
-// arriving workgroup measured 1.51 ms vs 1.35 + 0.06: every tile's last slice finishes in the
-// final round, so the reduces all land in the tail; removed.)
-static int syrk_nw() {
-    static const int nw = [] {
-        const char* e = std::getenv("PNOL_SYRK_NW");
-        return (e && std::atoi(e) == 4) ? 4 : 8;
-    }();
-    return nw;
-}
-
-// bit 0: umajor dispatch (PNOL_SYRK_UMAJOR, default on); bit 1: the diagonal tiles in the 2 x 4
-// wave layout instead of the balanced block sets (PNOL_SYRK_DIAG_BAL=0; A/B switch)
-static int syrk_umajor() {
-    static const int v = [] {
-        const char* e = std::getenv("PNOL_SYRK_UMAJOR");
-        const char* d = std::getenv("PNOL_SYRK_DIAG_BAL");
-        return (e ? (std::atoi(e) != 0) : 1) | (d && std::atoi(d) == 0 ? 2 : 0);
-    }();
-    return v;
-}
+// 8 waves per 128 x 128 tile (1.35 ms vs 1.40 ms with 4 at m = 16384, n = 2048).  (A split-K
+// reduce fused into the tile kernel by the last arriving workgroup measured 1.51 ms vs 1.35 +
+// 0.06: every tile's last slice finishes in the final round, so the reduces all land in the
+// tail; an XCD-sliced dispatch and 8-byte fragment reads were no faster either; removed.)
 
 // 64 x 64 output tiles (MODE 4) instead of 128 x 128 for the whole-matrix launches: 4x the
 // workgroups (4 per CU), the same per-element sums.  Measured at m = 16384, n = 2048 on the
@@ -710,94 +617,32 @@ static bool syrk_t64(bool sliced) {
     return e ? std::atoi(e) != 0 : sliced;
 }
 
-static bool syrk_xmap() {
-    static const bool on = [] {
-        const char* e = std::getenv("PNOL_SYRK_XMAP");
-        return e && std::atoi(e) != 0;
-    }();
-    return on;
-}
-
 // Partial tiles [tile0, tile0 + ntl) x slices [slice0, slice0 + nsl) x sub-chunks of
 // X (nr rows, K columns; slice s at X + s * sstride, row stride ldx) into
 // part[((t - tile0) * nsl * sub + (s - slice0) * sub + u) * 128^2].
 static void syrk_partials(pnol_ctx* ctx, hipStream_t stream, bool rows_variant, const double* X, long ldx,
                           long sstride, int nr, int K, const SliceCfg& sc, int slice0, int nsl, int tile0, int ntl,
-                          double* part, bool t64 = false, unsigned* tail_flag = nullptr, unsigned tail_val = 0) {
+                          double* part, bool t64 = false) {
     const int split = nsl * sc.sub;
     const dim3 grid(ntl * split);
     LaunchTimer tm(ctx, rows_variant ? "syrk_rows" : "syrk");
     if (t64) {   // all tiles (tile0 = 0): ntl counts the 64 x 64 lower tiles
         const int nt64 = (nr + 63) / 64;
-        hipExtLaunchKernelGGL((k_syrk_tile<4, 64>), dim3(nt64 * (nt64 + 1) / 2 * split), dim3(256), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr,
-                           K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part,
-                           (double*)nullptr, 0L, 1.0, 0.0, 0, tail_flag, tail_val);
-    } else if (rows_variant)
-        hipExtLaunchKernelGGL((k_syrk_tile<2, kTile, false, 8>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr, K, split,
-                           sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0, tail_flag, tail_val);
-    else if (syrk_nw() == 8)
-        hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, false, 8>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr, K, split,
-                           sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0, tail_flag, tail_val);
-    else if (syrk_xmap() && split % kNumXcd == 0)
-        hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, true>), grid, dim3(256), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr, K, split, sc.kfirst,
-                           sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0, tail_flag, tail_val);
-    else
-        hipExtLaunchKernelGGL((k_syrk_tile<0, kTile>), grid, dim3(256), 0, stream, tm.start(), tm.stop(), 0, X, ldx, nr, K, split, sc.kfirst,
-                           sc.kchunk, sc.sub, slice0, sc.mS, sstride, syrk_umajor(), part, (double*)nullptr, 0L, 1.0, 0.0, tile0, tail_flag, tail_val);
-}
-
-// -J^T F in the J^T J's tail (PNOL_JTR_TAIL=1; off by default: measured slower, below).  The GEMV reads only J^T and F, both
-// complete before the SYRK starts, so it need not wait for the SYRK to drain: the SYRK's
-// last-dispatched workgroup stores the launch's epoch into the context's tail word when it
-// starts, a second stream waits for that value (hipStreamWaitValue32: the command processor
-// polls, no CU is held) and runs the GEMV on the CUs the SYRK frees as its last round drains;
-// the context stream waits for the GEMV's event only before the -J^T F tree.  (A launch without
-// the AQL barrier bit -- hipExtAnyOrderLaunch -- does not start early on gfx950:
-// profiles/r02_anyorder_probe.json.)  The same kernels and bits as the plain order.  Measured
-// (tools/jtr_tail_ab.sh, same box, alternating 30-trip benches): 305-311 LM iters/s with the
-// GEMV in the tail vs 314-317 in stream order -- the GEMV's HBM stream slows the SYRK's last
-// workgroups more than it saves, so stream order stays the default.
-static bool jtr_tail_on(pnol_ctx* ctx) {
-    const char* e = std::getenv("PNOL_JTR_TAIL");   // read per call: tests switch it
-    if (!e || std::atoi(e) == 0) return false;
-    static int supported = -1;
-    if (supported < 0) {
-        int v = 0;
-        supported = hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, ctx->device) == hipSuccess && v;
+        hipExtLaunchKernelGGL((k_syrk_tile<4, 64>), dim3(nt64 * (nt64 + 1) / 2 * split), dim3(256), 0, stream,
+                              tm.start(), tm.stop(), 0, X, ldx, nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0,
+                              sc.mS, sstride, part, 0);
+    } else if (rows_variant) {
+        hipExtLaunchKernelGGL((k_syrk_tile<2, kTile, 8>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0, X, ldx,
+                              nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, tile0);
+    } else {
+        hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, 8>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0, X, ldx,
+                              nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, tile0);
     }
-    return supported;
-}
-
-static int tail_prepare(pnol_ctx* ctx, unsigned** flag, unsigned* val) {
-    if (!ctx->aux_stream) PNOL_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
-    if (!ctx->tail_ev) PNOL_HIP(hipEventCreateWithFlags(&ctx->tail_ev, hipEventDisableTiming));
-    if (!ctx->tail_flag) {
-        // one 8-byte signal word; plain device memory where signal memory is refused
-        if (hipExtMallocWithFlags((void**)&ctx->tail_flag, 8, hipMallocSignalMemory) != hipSuccess) {
-            (void)hipGetLastError();
-            ctx->tail_flag = nullptr;
-            PNOL_HIP(hipMalloc((void**)&ctx->tail_flag, 64));
-        }
-        PNOL_HIP(hipMemset(ctx->tail_flag, 0, 8));
-        ctx->tail_epoch = 0;
-    }
-    *flag = ctx->tail_flag;
-    *val = ++ctx->tail_epoch;
-    return PNOL_OK;
 }
 
 static int jtr_gemv(pnol_ctx* ctx, const double* JT, int ldjt, long sstride, int m, int n, int mS, int s0, int nsl,
                     const double* F, hipStream_t stream = nullptr);
 static int jtr_tree(pnol_ctx* ctx, int n, int s0, int nsl, double* out);
-
-// after the SYRK launch that carried (tf, tv): the GEMV on the aux stream gated by the tail word
-static int jtr_gemv_tail(pnol_ctx* ctx, unsigned* tf, unsigned tv, const double* JT, int ldjt, long sstride, int m,
-                         int n, int mS, int s0, int nsl, const double* F) {
-    PNOL_HIP(hipStreamWaitValue32(ctx->aux_stream, tf, tv, hipStreamWaitValueGte, 0xffffffffu));
-    PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sstride, m, n, mS, s0, nsl, F, ctx->aux_stream));
-    PNOL_HIP(hipEventRecord(ctx->tail_ev, ctx->aux_stream));
-    return PNOL_OK;
-}
 
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                double* jtj_diag, const double* F, double* rhs) {
@@ -813,20 +658,15 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     const SliceCfg sc = slice_cfg(m, ntiles);
     void* part = nullptr;
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * kS * sc.sub * kTile * kTile, &part));
-    const bool tail = rhs && jtr_tail_on(ctx);
-    unsigned* tf = nullptr;
-    unsigned tv = 0;
-    if (tail) PNOL_CHECK(tail_prepare(ctx, &tf, &tv));
     syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
-                  syrk_t64(false), tf, tv);
+                  syrk_t64(false));
     PNOL_CHECK(launch_check());
-    if (tail)
-        PNOL_CHECK(jtr_gemv_tail(ctx, tf, tv, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F));
-    else if (rhs)
-        PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F));
-    // -J^T F's slice tree rides in the reduce launch (an extra row of blocks), except when the
-    // GEMV ran on the tail stream (the tree then waits for its event)
-    const bool fold = rhs && !tail;
+    if (rhs) PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F));
+    // -J^T F's slice tree rides in the reduce launch (an extra row of blocks).  (The GEMV on a
+    // second stream released by the SYRK's last-dispatched workgroup -- hipStreamWaitValue32 on a
+    // tail word -- measured slower, 305-311 vs 314-317 LM iters/s: its HBM stream slowed the
+    // SYRK's last workgroups more than it hid; removed.)
+    const bool fold = rhs != nullptr;
     void* jp = nullptr;
     if (fold) PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
     {
@@ -836,9 +676,7 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
                       fold ? rhs : (double*)nullptr);
         PNOL_CHECK(launch_check());
     }
-    if (fold) return PNOL_OK;
-    if (tail) PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->tail_ev, 0));
-    return rhs ? jtr_tree(ctx, n, 0, kS, rhs) : PNOL_OK;
+    return PNOL_OK;
 }
 
 int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldjt, int m, int n, double lambda,
@@ -916,20 +754,6 @@ int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h,
     PNOL_HIP(hipEventRecord(ctx->aux_events[nchunks], ctx->aux_stream));
     PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->aux_events[nchunks], 0));
     return rhs ? launch_jtr(ctx, JT, ldjt, m, n, F0, rhs) : PNOL_OK;
-}
-
-int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, double alpha, double* C, int ldc,
-                      int split_k) {
-    (void)split_k;
-    if (!X || !C || nr <= 0 || K <= 0) return PNOL_ERR_ARG;
-    // 64 x 64 tiles: the Cholesky trailing update has K = 64, so per-workgroup work is small
-    // and the launch is latency-bound; 4x more workgroups than 128 x 128 tiles fill the chip.
-    constexpr int kT = 64;
-    const int nt = (nr + kT - 1) / kT;
-    const int ntiles = nt * (nt + 1) / 2;
-    hipLaunchKernelGGL((k_syrk_tile<1, kT>), dim3(ntiles), dim3(256), 0, ctx->stream, X, (long)ldx, nr, K, 1, K, K, 1,
-                       0, K, (long)K, 0, (double*)nullptr, C, (long)ldc, alpha, 1.0, 0, (unsigned*)nullptr, 0u);
-    return launch_check();
 }
 
 // J^T J with the 128 x 128 tiles split over the communicator's ranks (contiguous ranges of
@@ -1035,34 +859,21 @@ int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lamb
     void* part = nullptr;
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * std::max(nsl, 1) * sc.sub * E, &part));
     const bool t64 = syrk_t64(true);
-    // -J^T F's slice partials in the SYRK's tail (jtr_tail_on)
-    const bool tail = nsl > 0 && jtr_tail_on(ctx);
     if (nsl > 0) {
-        unsigned* tf = nullptr;
-        unsigned tv = 0;
-        if (tail) PNOL_CHECK(tail_prepare(ctx, &tf, &tv));
-        syrk_partials(ctx, ctx->stream, false, JTs, sc.mS, sstr, n, m, sc, s0, nsl, 0, ntiles, (double*)part, t64,
-                      tf, tv);
+        syrk_partials(ctx, ctx->stream, false, JTs, sc.mS, sstr, n, m, sc, s0, nsl, 0, ntiles, (double*)part, t64);
         PNOL_CHECK(launch_check());
-        if (tail)
-            PNOL_CHECK(jtr_gemv_tail(ctx, tf, tv, JTs, sc.mS, sstr, m, n, sc.mS, s0, nsl, F));
-        else
-            PNOL_CHECK(jtr_gemv(ctx, JTs, sc.mS, sstr, m, n, sc.mS, s0, nsl, F));
+        PNOL_CHECK(jtr_gemv(ctx, JTs, sc.mS, sstr, m, n, sc.mS, s0, nsl, F));
     }
     if (P == 1) {
-        // the -J^T F tree rides in the reduce launch unless the GEMV ran on the tail stream
+        // the -J^T F tree rides in the reduce launch
         void* jp = nullptr;
-        if (!tail) PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
+        PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
         {
             ScopedTimer tm(ctx, "syrk_reduce");
-            launch_reduce(dim3(kTile / 32, ntiles + (tail ? 0 : 1)), dim3(256), 0, ctx->stream, (const double*)part,
-                          ntiles, sc.sub, n, lambda, A, (long)lda, jtj_diag, 0, (const double*)jp,
-                          tail ? (double*)nullptr : rhs);
+            launch_reduce(dim3(kTile / 32, ntiles + 1), dim3(256), 0, ctx->stream, (const double*)part, ntiles,
+                          sc.sub, n, lambda, A, (long)lda, jtj_diag, 0, (const double*)jp, rhs);
         }
-        PNOL_CHECK(launch_check());
-        if (!tail) return PNOL_OK;
-        PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->tail_ev, 0));
-        return jtr_tree(ctx, n, 0, kS, rhs);
+        return launch_check();
     }
     // the global node list: rank q's nodes in slice order, ranks in order
     std::vector<std::pair<int, int>> nodes;
@@ -1098,7 +909,6 @@ int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lamb
     }
     PNOL_CHECK(launch_check());
     // -J^T F nodes of my slices into the tail of my allgather slot
-    if (tail) PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->tail_ev, 0));
     if (nsl > 0) PNOL_CHECK(jtr_tree(ctx, n, s0, nsl, mine + (long)tpr * E));
     // reduce-scatter in tree order: rank q's nodes of owner d's tiles -> d
     {

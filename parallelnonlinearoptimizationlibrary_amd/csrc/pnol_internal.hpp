@@ -66,12 +66,6 @@ struct pnol_ctx {
     int chol4_epoch = 0;            // last flag value handed out (monotonic; flags reset on regrow)
     hipStream_t aux_stream = nullptr;   // second stream (J^T J rows beside the FD chunks), lazily created
     std::vector<hipEvent_t> aux_events; // chunk-done events between the two streams
-    // J^T J tail word (syrk.hip, jtr_tail): the SYRK's last-dispatched workgroup stores
-    // tail_epoch into *tail_flag when it starts; the aux stream waits for that value
-    // (hipStreamWaitValue32) and then runs the -J^T F GEMV on the CUs the SYRK's tail frees
-    unsigned* tail_flag = nullptr;
-    unsigned tail_epoch = 0;
-    hipEvent_t tail_ev = nullptr;       // the GEMV done (aux stream), waited for by the main stream
     // LevMarqMPI's FD decomposition (fd.hip): -1 = not chosen yet (PNOL_LM_FD at first use),
     // 0 = columns (the reference's: FD column tiles per rank + the m-slice exchange), 1 = rows
     int lm_fd_mode = -1;
@@ -187,15 +181,12 @@ int launch_gather_sub(pnol_ctx* ctx, const double* D, int ldd, int n, const int*
 int launch_gather_rows(pnol_ctx* ctx, const double* D, int ldd, const int* ridx, int nrows, int rbase, const int* cidx,
                        int ncols, double* Dsub, int lds);
 
-// rhs (nullable): also rhs = -J^T F, its GEMV in the SYRK's tail (bitwise launch_jtr)
+// rhs (nullable): also rhs = -J^T F (bitwise launch_jtr), its slice tree in the reduce launch
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                double* jtj_diag, const double* F = nullptr, double* rhs = nullptr);
 int launch_jtj_sharded(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                        double* jtj_diag);
 int launch_jtr(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
-// C(lower tiles of rows [r0, r0+nr)) = beta*C + alpha * X X^T  over K columns (MFMA)
-int launch_syrk_lower(pnol_ctx* ctx, const double* X, int ldx, int nr, int K, double alpha, double* C,
-                      int ldc, int split_k);
 
 // Binv = B^{-1} as the reference's matrixInverse (per-column luSolve), bitwise: one elimination
 // of [B | I], per-column back substitution; *info_host = -1 on a zero pivot (inf / NaN entries)

@@ -492,8 +492,6 @@ int pnol_ctx_destroy(pnol_ctx* ctx) {
     }
     for (hipEvent_t e : ctx->phase_events) (void)hipEventDestroy(e);
     if (ctx->comm_done) (void)hipEventDestroy(ctx->comm_done);
-    if (ctx->tail_ev) (void)hipEventDestroy(ctx->tail_ev);
-    if (ctx->tail_flag) (void)hipFree(ctx->tail_flag);
     for (auto& kv : ctx->timers.pending)
         for (auto& ev : kv.second) {
             (void)hipEventDestroy(ev.first);

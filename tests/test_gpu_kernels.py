@@ -216,11 +216,11 @@ def test_jtj_mfma_layout_asymmetric(ctx):
     assert np.array_equal(A, J.T @ J)
 
 
-@pytest.mark.parametrize("method", [1, 3, 4])
+@pytest.mark.parametrize("method", [4, 5])
 @pytest.mark.parametrize("n", [65, 100, 129, 777, 1000, 2048, 3001])
 def test_cholesky_solve(ctx, n, method):
-    """method 1: per-panel launches; method 3: one persistent tile-DAG launch; method 4 (the
-    default): lookahead tile Cholesky with diagonal-tile inverses and the forward solve folded in."""
+    """method 4: lookahead tile Cholesky with diagonal-tile inverses and the forward solve folded
+    in, one launch per panel step; method 5 (the default): the same as one persistent launch."""
     rng = np.random.default_rng(n)
     J = rng.standard_normal((2 * n, n))
     A = J.T @ J + np.eye(n)
@@ -231,7 +231,7 @@ def test_cholesky_solve(ctx, n, method):
     assert np.linalg.norm(_np(sigma) - x) <= 1e-10 * np.linalg.norm(x) * np.linalg.cond(A)
 
 
-@pytest.mark.parametrize("method", [1, 3, 4, 5])
+@pytest.mark.parametrize("method", [4, 5])
 def test_cholesky_odd_leading_dimension(ctx, method):
     """Odd lda: scalar staging paths (no 16-byte loads)."""
     rng = np.random.default_rng(77)
@@ -247,7 +247,7 @@ def test_cholesky_odd_leading_dimension(ctx, method):
     assert np.linalg.norm(_np(sigma) - x) <= 1e-10 * np.linalg.norm(x) * np.linalg.cond(A)
 
 
-@pytest.mark.parametrize("method", [1, 4, 5])
+@pytest.mark.parametrize("method", [4, 5])
 def test_cholesky_repeated_solves_reuse_ready_flags(ctx, method):
     """The flag-chained solves tag each call with a new epoch; sizes that grow and shrink (the
     flag buffer is reallocated) and back-to-back calls must all be exact."""
@@ -279,8 +279,10 @@ def test_lu_multi_launch_bitwise(ctx, oracle):
     assert np.array_equal(_np(sigma), oracle.lusolve(A, b))
 
 
-def test_cholesky_m4_keeps_A_and_matches_per_panel(ctx):
-    """Method 4 factors a padded copy (A is left intact) and agrees with the per-panel form."""
+def test_cholesky_m4_keeps_A_and_matches_lu(ctx):
+    """Method 4 factors a padded copy (A is left intact) and agrees with the reference-order LU;
+    the removed methods 1 and 3 are refused."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
     rng = np.random.default_rng(3)
     n = 1000
     J = rng.standard_normal((1200, n))
@@ -290,11 +292,15 @@ def test_cholesky_m4_keeps_A_and_matches_per_panel(ctx):
     s4, i4 = ctx.solve(At, ctx.tensor(b), method=4)
     assert i4 == 1
     assert np.array_equal(_np(At), A)
-    s1, i1 = ctx.solve(ctx.tensor(A), ctx.tensor(b), method=1)
+    s2, i2 = ctx.solve(ctx.tensor(A), ctx.tensor(b), method=2)
+    assert i2 == 2
     x = np.linalg.solve(A, b)
     c = np.linalg.cond(A)
-    for s in (s4, s1):
+    for s in (s4, s2):
         assert np.linalg.norm(_np(s) - x) <= 1e-12 * np.linalg.norm(x) * c
+    for m in (1, 3):
+        with pytest.raises(RuntimeError):
+            ctx.solve(ctx.tensor(A), ctx.tensor(b), method=m)
 
 
 @pytest.mark.parametrize("method", [4, 5])
@@ -654,14 +660,11 @@ def test_fd_jtj_pipelined_bitwise(ctx, m, n, chunks):
     assert np.array_equal(_np(db), _np(da))
 
 
-@pytest.mark.parametrize("m,n,tail", [(16384, 2048, "1"), (16384, 2048, "0"), (5000, 1000, "1"),
-                                      (777, 129, "1"), (300, 40, "1")])
-def test_fd_normal_bitwise(ctx, m, n, tail, monkeypatch):
-    """pnol_fd_normal_d (FD Jacobian + A + -J^T F in one queue, the -J^T F GEMV on a second stream
-    released by the J^T J's last-dispatched workgroup) equals pnol_fd_jacobian_d + pnol_jtj_d +
-    pnol_jtr_d bitwise, over repeated calls (the GEMV must never read a stale J^T: the second
-    call's JT is a new point's).  tail = "0": the same kernels in stream order."""
-    monkeypatch.setenv("PNOL_JTR_TAIL", tail)
+@pytest.mark.parametrize("m,n", [(16384, 2048), (5000, 1000), (777, 129), (300, 40)])
+def test_fd_normal_bitwise(ctx, m, n):
+    """pnol_fd_normal_d (FD Jacobian + A + -J^T F in one queue, the -J^T F tree in the J^T J reduce
+    launch) equals pnol_fd_jacobian_d + pnol_jtj_d + pnol_jtr_d bitwise, over repeated calls (the
+    second call's JT is a new point's)."""
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
     d = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)

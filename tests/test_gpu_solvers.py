@@ -196,6 +196,33 @@ def test_bfgs_bnd_matches_oracle(ctx, oracle, case):
     assert res.fopt == reso.fopt
 
 
+@pytest.mark.parametrize("power", [2.0, 3.0])
+def test_bfgs_bnd_power_recur(ctx, oracle, power):
+    """BFGS_Bnd on PowerObject (ExampleObjectives.hpp:206-234) with every coordinate driven to its
+    lower bound one recursion level at a time, so the Recur FD gradient (PNOL_Objective.cpp:337-360)
+    runs at every level with frozen coordinates.  power = 2 takes the same-point reuse (values
+    formed by the library's own host formula, the device kernel's bits); power = 3 calls pow,
+    whose host and device results may differ in the last place, so its Recur gradients stay on
+    the device.  Either way the run equals the oracle's (bitwise for power 2; power 3 within 1e-12,
+    the oracle's glibc pow against the device's)."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_bfgs
+    n = 8
+    x0 = list(np.linspace(-0.9, -0.2, n)) if power == 3.0 else list(np.linspace(0.9, 0.2, n))
+    lb, ub = [-1.0] * n, [1.0] * n
+    if power == 2.0:
+        lb = list(np.linspace(0.1, 0.45, n))     # the minimiser of sum x^2 outside the box: all bounds active
+    Pb = [1e-4, 0.8, 1e-6, 1, 1e-10, 2, 50, 1e-5, 1e-6, 1e-3, 200, 1e-5, 1e-5, 0, -1]   # Examples.cpp:75
+    X, res = run_bfgs(_obj(ctx, L.OBJ_POWER, n, power=power), x0, Pb, which=2, lb=lb, ub=ub)
+    Xo, reso = oracle.bfgs_bnd_findmin(oracle.power(n, power), x0, lb, ub, Pb)
+    print(f"power {power}: max |X - Xo| = {np.max(np.abs(X - Xo)):.3e}, evals {res.evals} vs {reso.evals}")
+    assert np.allclose(X, lb, atol=1e-5)
+    if power == 2.0:
+        assert np.array_equal(X, Xo) and res.fopt == reso.fopt and res.evals == reso.evals
+    else:
+        assert np.max(np.abs(X - Xo)) <= 1e-12 and abs(res.fopt - reso.fopt) <= 1e-12 * abs(reso.fopt)
+
+
 BND_MPI_P = [1e-4, 0.1, 1e-16, 4, 1, 1000, 1e-7, 1e-3, 200, 1e-5, 1e-5, 1e-5, 0, 0]   # Examples.cpp:112
 
 

@@ -28,10 +28,6 @@ if [ "${SWEEP:-0}" = "1" ]; then
   timeout -k 10 600 python tools/sweep_hg.py > gpurun_out/sweep_hg.log 2>&1
   rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep_hg.log; [ "$rc" -eq 0 ] || exit $rc
 fi
-if [ "${SWEEPFD:-0}" = "1" ]; then
-  timeout -k 10 600 python tools/sweep_fd.py > gpurun_out/sweep_fd.log 2>&1
-  rc=$?; echo "sweep_fd rc=$rc"; cat gpurun_out/sweep_fd.log; [ "$rc" -eq 0 ] || exit $rc
-fi
 if [ "${PMC:-0}" = "1" ]; then
   timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o pmc --output-format csv -- \
       python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_fetch.log 2>&1

@@ -72,9 +72,7 @@ int main(int argc, char** argv) {
     double busy = 0, xbusy[8] = {0};
     int xcnt[8] = {0};
     for (int b = 0; b < grid; ++b) {
-        int u;
-        if (syrk_umajor()) u = b / (ntl * nsl);
-        else u = (b % split) % sc.sub;
+        const int u = b / (ntl * nsl);   // k_syrk_tile's dispatch order: every chunk 0 first
         const int c = u == 0 ? 0 : 1;
         const double d = (double)(tl[3 * b + 1] - tl[3 * b]) * 0.01;   // us
         dur_sum[c] += d;

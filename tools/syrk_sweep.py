@@ -1,6 +1,6 @@
 """Time J^T J (k_syrk_tile + k_syrk_reduce) on the bench shape (m=16384, n=2048, random JT) for
-SYRK variants given as "sub:first:umajor[:nw]" arguments (PNOL_SYRK_SUB / _FIRST / _UMAJOR / _NW,
-read once per process, so one child per variant).  sub 0 = the default choice."""
+K splits given as "sub:first" arguments (PNOL_SYRK_SUB / PNOL_SYRK_FIRST, read once per
+process, so one child per variant).  sub 0 = the default choice."""
 import json
 import os
 import subprocess
@@ -38,9 +38,9 @@ print(json.dumps(out))
 """ % ROOT
 
 if __name__ == "__main__":
-    for v in (sys.argv[1:] or ["0:0:0", "2:75:1"]):
-        f = v.split(":") + ["0", "0", "0", "8"][len(v.split(":")):]
-        env = dict(os.environ, PNOL_SYRK_SUB=f[0], PNOL_SYRK_FIRST=f[1], PNOL_SYRK_UMAJOR=f[2], PNOL_SYRK_NW=f[3])
+    for v in (sys.argv[1:] or ["0:0", "2:75"]):
+        f = v.split(":") + ["0", "0"][len(v.split(":")):]
+        env = dict(os.environ, PNOL_SYRK_SUB=f[0], PNOL_SYRK_FIRST=f[1])
         p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
         if p.returncode != 0:
             print(p.stderr[-2000:])
