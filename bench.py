@@ -261,6 +261,50 @@ def _median_time(fn, reps):
     return float(np.median(ts)), ts
 
 
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo, as lscpu prints it) and its logical CPU count."""
+    name = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                name = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return name, os.cpu_count()
+
+
+def cpu_lm_trip(O, objs, x, h, ex, P):
+    """One whole LevMarq loop trip of the reference CPU path at the oracle's (m, n), timed end to
+    end once on P threads (LevenbergMarquardt.cpp:55-103 at the rank count P of
+    LevenbergMarquardtMPI): F(x); the FD Jacobian with its columns dealt round-robin over the P
+    threads (PNOL_Objective.cpp:228-246); J^T J by the reference's matrixMultiply, its rows split
+    over the threads (the reference replicates the whole product on every rank -- splitting it
+    is generous to the CPU); rhs = -J^T F (matrixVectorMultiply); luSolve; F(x + sigma).  Returns
+    (seconds, sigma)."""
+    o0 = objs[0]
+    m, n = o0.s.m, len(x)
+    t0 = time.perf_counter()
+    F = O.obj_eval_multi(o0, x)
+    J = np.empty((m, n))
+
+    def cols(q):
+        for j in range(q, n, P):                 # owner(j) = j mod P
+            xj = x.copy()
+            xj[j] = xj[j] + h[j]
+            J[:, j] = (O.obj_eval_multi(objs[q], xj) - F) / h[j]
+    list(ex.map(cols, range(P)))
+    JT = np.ascontiguousarray(J.T)
+    blk = (n + P - 1) // P
+    parts = list(ex.map(lambda q: O.matmul(JT[q * blk:min(n, (q + 1) * blk)], J) if q * blk < n else None, range(P)))
+    A = np.vstack([p for p in parts if p is not None])
+    A[np.diag_indices(n)] *= 1.0 + 0.001
+    rhs = -O.matvec(JT, F)
+    sigma = O.lusolve(A, rhs)
+    O.obj_eval_multi(o0, x + sigma)
+    return time.perf_counter() - t0, sigma
+
+
 def cpu_baseline(m, n, budget_s=20.0):
     """The reference path on the host cores: the oracle (the CPU restatement of the reference,
     loop for loop) built -O3 -march=x86-64-v3 -ffp-contract=off (liboracle_fast.so), timed on a
@@ -271,7 +315,9 @@ def cpu_baseline(m, n, budget_s=20.0):
       - rows of J^T J with the reference's matrixMultiply, 1 and P threads;
       - the reference LU (luSolve) at n = 1024, scaled by (n / 1024)^3.
     value = LM trips per second with P threads (P = the host cores this process may use, at
-    most 16, the box's per-GPU CPU share).  Also, single-threaded: cfg 1 (BFGS on the 2-D
+    most 16, the box's per-GPU CPU share), from one whole trip timed end to end (cpu_lm_trip);
+    the sampled legs above extrapolate the 1-thread trip and cross-check it.  Also,
+    single-threaded: cfg 1 (BFGS on the 2-D
     Rosenbrock, the whole solve), cfg 2 (BFGS at n = 4096: whole solve with the rank-2 update
     form, and per iteration with the reference's O(n^3) update extrapolated from n = 512), and
     the BFGS kernels' CPU counterparts (p = -D g at n = 8192, the rank-2 update at n = 4096)."""
@@ -303,7 +349,10 @@ def cpu_baseline(m, n, budget_s=20.0):
     t_lu_s, s_lu = _median_time(lambda: O.lusolve(Al, np.ones(nl)), 3)
     t_lu = t_lu_s * (n / nl) ** 3
     t_trip1 = t_eval * (n + 2) + t_row * n + t_lu
-    t_tripP = t_eval_par * (n + 2) + t_row_par * n + t_lu
+    t_tripP_sampled = t_eval_par * (n + 2) + t_row_par * n + t_lu
+    with ThreadPoolExecutor(P) as ex:
+        t_trip_whole, _ = cpu_lm_trip(O, objs, np.zeros(n), np.full(n, 1e-7), ex, P)
+    t_tripP = t_trip_whole
     # cfg 1: the whole BFGS solve on the 2-D Rosenbrock (the reference's CPU example)
     g1 = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_survey.json")))["bfgs_rosenbrock2_m12_1"]
     t_cfg1, _ = _median_time(lambda: O.bfgs_findmin(O.rosenbrock(2), g1["x0"], g1["params"]), 5)
@@ -317,10 +366,14 @@ def cpu_baseline(m, n, budget_s=20.0):
     it2 = max(runs[-1][1].iters, 1)
     # BFGS counterparts (single thread, the reference's sequential loops)
     rng = np.random.default_rng(0)
-    nh = 8192
-    D = rng.standard_normal((nh, nh)); g = rng.standard_normal(nh)
-    t_hg, s_hg = _median_time(lambda: O.matvec(D, g), 3)
-    del D
+    hg = {}
+    for nh in (4096, 8192, 16384):
+        D = rng.standard_normal((nh, nh)); g = rng.standard_normal(nh)
+        O.matvec(D, g)
+        t, smp = _median_time(lambda: O.matvec(D, g), 5)
+        hg[nh] = (t, smp)
+        del D
+    t_hg, s_hg = hg[8192]
     nu = 4096
     D = np.eye(nu) + 1e-3 * rng.standard_normal((nu, nu)); yv = rng.standard_normal(nu); sv = yv + 0.1
     t_r2, s_r2 = _median_time(lambda: O.update_hessian_inv_rank2(D, yv, sv), 3)
@@ -330,14 +383,20 @@ def cpu_baseline(m, n, budget_s=20.0):
     t_n3, s_n3 = _median_time(lambda: O.update_hessian_inv(D, y3, s3), 3)
     scale3 = (4096 / n3) ** 3
     ref_iter = t_cfg2 / it2 - t_r2 + t_n3 * scale3
+    model, ncpu = cpu_model()
     return {
         "value": 1.0 / t_tripP, "unit": "LM iters/sec", "cores": P, "kind": "port",
-        "sample": (f"oracle (C restatement, gcc -O3 -march=x86-64-v3 -ffp-contract=off) at m={m}, n={n}, medians of "
-                   f"timings: residual eval {t_eval*1e3:.1f} ms on 1 thread, {t_eval_par*1e3:.1f} ms amortised over "
-                   f"{P} threads, x{n + 2} per trip; a J^T J row (reference matrixMultiply) {t_row*1e3:.1f} ms on 1 "
-                   f"thread, {t_row_par*1e3:.1f} ms amortised over {P}, x{n}; LU at n={nl} {t_lu_s:.2f} s scaled by "
-                   f"(n/{nl})^3; extrapolated {t_tripP:.1f} s per LM trip on {P} threads, {t_trip1:.1f} s on 1"),
-        "seconds_per_trip": t_tripP, "seconds_per_trip_1_thread": t_trip1, "iters_per_s_1_thread": 1.0 / t_trip1,
+        "cpu_model": model, "host_logical_cpus": ncpu,
+        "sample": (f"oracle (C restatement, gcc -O3 -march=x86-64-v3 -ffp-contract=off) at m={m}, n={n}: one whole LM "
+                   f"trip timed end to end on {P} threads ({t_trip_whole:.1f} s: F(x), the FD Jacobian's columns "
+                   f"round-robin over the threads, J^T J rows by the reference matrixMultiply split over the threads, "
+                   f"-J^T F, luSolve, F(x + sigma)) on a {model}; the 1-thread trip extrapolated from medians of "
+                   f"sampled legs: residual eval {t_eval*1e3:.1f} ms x{n + 2}, a J^T J row {t_row*1e3:.1f} ms x{n}, LU "
+                   f"at n={nl} {t_lu_s:.2f} s scaled by (n/{nl})^3 = {t_trip1:.1f} s (the same legs on {P} threads: "
+                   f"{t_tripP_sampled:.1f} s)"),
+        "seconds_per_trip": t_tripP, "seconds_per_trip_whole_timed": t_trip_whole,
+        "seconds_per_trip_sampled_P_threads": t_tripP_sampled,
+        "seconds_per_trip_1_thread": t_trip1, "iters_per_s_1_thread": 1.0 / t_trip1,
         "threads": P,
         "samples_s": {"eval_1t": s_eval, "eval_Pt_2P_evals": s_ep, "jtj_row_1t": s_row, "jtj_rows_Pt_P_rows": s_rp,
                       "lu_n1024": s_lu},
@@ -347,7 +406,9 @@ def cpu_baseline(m, n, budget_s=20.0):
                             "s_per_iteration_reference_update_extrapolated": ref_iter,
                             "note": "reference O(n^3) updateHessianInv per iteration = its n=512 time x (4096/512)^3"},
         "bfgs_cpu_1_thread": {
-            "hg_n8192_s": t_hg, "hg_n8192_GBps": 8.0 * nh * nh / t_hg / 1e9, "hg_samples_s": s_hg,
+            "hg_n8192_s": t_hg, "hg_n8192_GBps": 8.0 * 8192 * 8192 / t_hg / 1e9, "hg_samples_s": s_hg,
+            "hg_GBps": {str(k): (8.0 * k * k + 16.0 * k) / v[0] / 1e9 for k, v in hg.items()},
+            "hg_s": {str(k): v[0] for k, v in hg.items()},
             "rank2_update_n4096_s": t_r2, "rank2_samples_s": s_r2,
             "reference_update_n512_s": t_n3, "reference_update_n512_samples_s": s_n3,
             "reference_update_n4096_s_extrapolated": t_n3 * scale3,
