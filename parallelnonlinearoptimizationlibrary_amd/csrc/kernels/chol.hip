@@ -1297,7 +1297,7 @@ __device__ __forceinline__ void publish(int* w, int v) {
 __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P, double* __restrict__ Lm, long ldp,
                                                       int T, double* __restrict__ W, double* __restrict__ bv,
                                                       double* __restrict__ zv, int* __restrict__ flags, int ntasks,
-                                                      int* __restrict__ info, int lookahead) {
+                                                      int* __restrict__ info, int lookahead, int xcd, int smode) {
     __shared__ __attribute__((aligned(16))) double smem[2 * kStage];   // 73.7 KB
     // the chain's look-ahead areas (EarlyNext / late_prepare): 75.8 KB
     __shared__ __attribute__((aligned(16))) double pfx[kStage];
@@ -1307,23 +1307,39 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
     __shared__ double zsh[NB];
     __shared__ int cnt[6];
     __shared__ int ew[4];
-    __shared__ int task_sh, ok_sh;
+    __shared__ int task_sh, ok_sh, role_sh;
     const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), wr = wave >> 1, wc = wave & 1;
     const PersistWords pw = persist_words(flags, T);
     double* X = smem;
     double* Y = smem + kStage;
+    // xcd >= 0: the factorisation stays on that XCD (its workgroups share one L2): workgroups
+    // dispatched to other XCDs leave at once, and the roles go by arrival -- the first to claim
+    // the role word runs the chain, the rest are workers (the grid is dealt round-robin over the
+    // XCDs, so the XCD's share of it is resident, one workgroup per CU)
+    if (xcd >= 0) {
+        if (t == 0) {
+            const int x = (int)(__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) & 15);   // HW_REG_XCC_ID
+            role_sh = x == xcd ? atomicAdd(pw.counter + 1, 1) : -1;
+        }
+        __syncthreads();
+        if (role_sh < 0) return;
+    }
+    const int role = xcd >= 0 ? role_sh : (int)blockIdx.x;
 
-    if (blockIdx.x == 0) {   // ---------------- the diagonal chain
+    if (role == 0) {   // ---------------- the diagonal chain
         const EarlyLds E{pfx, pll, pfc, ew};
         if (t < 4) ew[t] = 0;
-        for (int d = 1; d < T; ++d) {
+        // smode (the streamed solve): no prep launch factored tile 0 -- the chain starts at d = 0,
+        // once the J^T J has published the tile (its version word leaves -1)
+        for (int d = smode ? 0 : 1; d < T; ++d) {
             const int k = d - 1;
 #ifdef PNOL_CHOL_TIMELINE
             const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime(), ck0 = __builtin_amdgcn_s_memtime();
 #endif
             if (t == 0) {
                 const bool ok = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-                                spin_all<2>({pw.ver + d * T + k, pw.ver + d * T + d}, {k, k}, info);
+                                (d == 0 ? spin_ge(pw.ver, 0, info)
+                                        : spin_all<2>({pw.ver + d * T + k, pw.ver + d * T + d}, {k, k}, info));
                 ok_sh = ok;
             }
             __syncthreads();
@@ -1335,8 +1351,18 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
 #ifdef PNOL_CHOL_TIMELINE
             if (t == 0 && k + 1 < 64) g_chol_clk[8 * (k + 1) + 6] = pre ? 1 : 0;
 #endif
-            if (pre) late_prepare(E, Y, L, wave, lane);
-            else diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane, d > 1);
+            if (d == 0) {   // tile 0 as published (sc1 loads; the padding written by the prep)
+                const int row = t >> 2, c0 = (t & 3) * 16;
+                double v[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v[q] = ldg<true>(P + (long)row * ldp + c0 + q);
+#pragma unroll
+                for (int q = 0; q < 16; ++q) diag_put(L, row, c0 + q, v[q]);
+            } else if (pre) {
+                late_prepare(E, Y, L, wave, lane);
+            } else {   // W_{d-1} stays in Y after the chain's own factor
+                diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane, d > 1 || smode);
+            }
             if (t < 6) cnt[t] = 0;   // every read of cnt / ew above is behind a barrier inside
             if (t < 4) ew[t] = 0;    // either prepare
             __syncthreads();
@@ -1386,7 +1412,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             if (!ok_sh) return;
             stage_tile<true>(X, P, ldp, i0, k0);
             if (t == 0) {   // W_k (tile 0 comes from the prep launch)
-                ok_sh = k == 0 || spin_ge(pw.wdone + k, 1, info);
+                ok_sh = (k == 0 && !smode) || spin_ge(pw.wdone + k, 1, info);
 #ifdef PNOL_CHOL_TIMELINE
                 if (i == k + 2) PNOL_CRIT(k, 2)
 #endif
@@ -1589,6 +1615,34 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm,
 
 __global__ void k_flag_info(int* info, int v) { *info = v; }
 
+// The streamed solve's prep (no copy of A: the J^T J writes P itself): the persistent form's
+// progress words -- every tile version at -1 (not yet published by the J^T J), the rest 0 --,
+// b = rhs (zero padded), P's padding (identity on the diagonal past n), info = 0.
+__global__ __launch_bounds__(256) void k_chol_stream_prep(double* __restrict__ P, long ldp, int T, int n,
+                                                          double* __restrict__ bv, const double* __restrict__ rhs,
+                                                          int* __restrict__ pflags, int npflags, int* __restrict__ info) {
+    const int N = T * NB, tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+    const int v0 = 3 * T, v1 = 3 * T + T * T;
+    for (int q = tid; q < npflags; q += nth) pflags[q] = (q >= v0 && q < v1) ? -1 : 0;
+    for (int r = tid; r < N; r += nth) bv[r] = r < n ? rhs[r] : 0.0;
+    if (n < N) {
+        const long pad = (long)(N - n) * N + (long)n * (N - n);   // rows >= n, then columns >= n of rows < n
+        for (long e = tid; e < pad; e += nth) {
+            int r, c;
+            if (e < (long)(N - n) * N) {
+                r = n + (int)(e / N);
+                c = (int)(e % N);
+            } else {
+                const long f = e - (long)(N - n) * N;
+                r = (int)(f / (N - n));
+                c = n + (int)(f % (N - n));
+            }
+            P[(long)r * ldp + c] = r == c ? 1.0 : 0.0;
+        }
+    }
+    if (tid == 0) *info = 0;
+}
+
 }  // namespace
 
 // Solve A sigma = rhs (A SPD, untouched) by the lookahead tile Cholesky; *dinfo (device) != 0
@@ -1613,21 +1667,32 @@ int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs
     return launch_chol_solve_v(ctx, A, lda, rhs, sigma, n, dinfo, 0, xbase, xnext);
 }
 
-int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo,
-                        int variant, const double* xbase, double* xnext) {
-    const int T = (n + NB - 1) / NB, N = T * NB;
-    const long ldp = N;
-    void *P = nullptr, *Lm = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr;
-    PNOL_CHECK(ws_get(ctx, "chol4_P", sizeof(double) * (size_t)N * ldp, &P));
-    PNOL_CHECK(ws_get(ctx, "chol4_L", sizeof(double) * (size_t)N * ldp, &Lm));
+// The tile Cholesky's workspace (method 4 / 5 and the streamed solve share it)
+struct CholWs {
+    int T = 0, N = 0;
+    long ldp = 0;
+    double *P = nullptr, *Lm = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr;
+    int *rowflag = nullptr, *bwdflag = nullptr, *pf = nullptr;
+    int npf = 0;
+    bool gran = false;
+};
+
+static int chol_ws(pnol_ctx* ctx, int n, CholWs& w) {
+    w.T = (n + NB - 1) / NB;
+    w.N = w.T * NB;
+    w.ldp = w.N;
+    const int T = w.T, N = w.N;
+    void *P = nullptr, *Lm = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr, *pf = nullptr;
+    PNOL_CHECK(ws_get(ctx, "chol4_P", sizeof(double) * (size_t)N * w.ldp, &P));
+    PNOL_CHECK(ws_get(ctx, "chol4_L", sizeof(double) * (size_t)N * w.ldp, &Lm));
     PNOL_CHECK(ws_get(ctx, "chol4_W", sizeof(double) * (size_t)T * NB * NB, &W));
     PNOL_CHECK(ws_get(ctx, "chol4_b", sizeof(double) * (size_t)N, &bv));
     PNOL_CHECK(ws_get(ctx, "chol4_z", sizeof(double) * (size_t)N, &zv));
     // the backward solve's hand-off words: x granules (x, epoch) -- 2 N doubles, zeroed when
     // allocated and whenever the epoch restarts (a stale granule must never match)
     // (the flag form keeps its own buffer, so the two layouts never share memory)
-    const bool gran = bwd_granules();
-    if (gran) {
+    w.gran = bwd_granules();
+    if (w.gran) {
         auto it = ctx->ws.bufs.find("chol4_xg");
         const void* before = it == ctx->ws.bufs.end() ? nullptr : it->second.first;
         PNOL_CHECK(ws_get(ctx, "chol4_xg", sizeof(double) * 2 * (size_t)N, &xw));
@@ -1640,65 +1705,119 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
         const int cap = std::max(T, ctx->chol4_cap);
         PNOL_CHECK(ws_get(ctx, "chol4_flags", sizeof(int) * (size_t)2 * cap, &f));
         PNOL_HIP(hipMemsetAsync(f, 0, sizeof(int) * (size_t)2 * cap, ctx->stream));
-        if (gran) PNOL_HIP(hipMemsetAsync(xw, 0, sizeof(double) * 2 * (size_t)N, ctx->stream));   // epoch restarts
+        if (w.gran) PNOL_HIP(hipMemsetAsync(xw, 0, sizeof(double) * 2 * (size_t)N, ctx->stream));   // epoch restarts
         ctx->chol4_flags = (int*)f;
         ctx->chol4_cap = cap;
         ctx->chol4_epoch = 0;
     }
-    int* rowflag = ctx->chol4_flags;
-    int* bwdflag = ctx->chol4_flags + ctx->chol4_cap;
-    const bool persist = chol_persistent(variant) && T >= 2;
-    void* pf = nullptr;
-    const int npf = 3 * T + T * T + 1;
-    if (persist) PNOL_CHECK(ws_get(ctx, "chol5_words", sizeof(int) * (size_t)npf, &pf));
-    for (int k = -1; k <= (persist ? -1 : T - 2); ++k) {
-        const int R = T - 1 - k;
-        const int grid = k < 0 ? 2 + std::min(N, 1024) : R + R * (R + 1) / 2;
-        const int epoch = ++ctx->chol4_epoch;
-        hipLaunchKernelGGL(k_chol_step, dim3(grid), dim3(256), 0, ctx->stream, (double*)P, (double*)Lm, ldp, T, k,
-                           (double*)W, (double*)bv, (double*)zv, rowflag, epoch, dinfo, A, (long)lda, n, rhs,
-                           (int*)pf, persist ? npf : 0);
-    }
-    if (persist) {
-        int ntasks = 0;
-        for (int R = T - 1; R >= 1; --R) ntasks += R + R * (R + 1) / 2 - 1;
-        // tuning knob (read per call): PNOL_CHOL5_WORKERS = worker workgroups; one per CU
-        // (the look-ahead areas already hold the static LDS to one workgroup per CU).
-        // PNOL_CHOL_LOOKAHEAD = 0 turns the diagonal chain's look-ahead off (read per call).
-        const char* ew = std::getenv("PNOL_CHOL5_WORKERS");
-        const char* el = std::getenv("PNOL_CHOL_LOOKAHEAD");
-        // > 0: the look-ahead gives up once wave 0 has finished that many columns of the tile
-        // (0 off; above 64: the factor waits for the next tiles).  Measured at n = 2048
-        // (tools/microbench/chol_timeline.hip): 0: 0.645 ms, 52: 0.625, 64: 0.621 (default; half
-        // the steps find their tiles ready), 1000: 0.705 -- the next tiles wait on a panel and an
-        // update task (~6 us each after W_{d-1}), so waiting for them inside the factor costs more
-        // than the prepare it saves.
-        const int lookahead = el ? std::max(0, std::atoi(el)) : 64;
-        const int slots = std::max(ctx->num_cu, 1) - 1;
-        const int want = ew ? std::atoi(ew) : slots;
-        const int workers = std::max(1, std::min(ntasks, want));
-        hipLaunchKernelGGL(k_chol_persist, dim3(1 + workers), dim3(256), 0, ctx->stream, (double*)P, (double*)Lm, ldp,
-                           T, (double*)W, (double*)bv, (double*)zv, (int*)pf, ntasks, dinfo, lookahead);
-    }
+    w.rowflag = ctx->chol4_flags;
+    w.bwdflag = ctx->chol4_flags + ctx->chol4_cap;
+    w.npf = 3 * T + T * T + 2;   // + the task counter and the role word
+    PNOL_CHECK(ws_get(ctx, "chol5_words", sizeof(int) * (size_t)w.npf, &pf));
+    w.P = (double*)P; w.Lm = (double*)Lm; w.W = (double*)W; w.bv = (double*)bv; w.zv = (double*)zv;
+    w.xw = (double*)xw; w.pf = (int*)pf;
+    return PNOL_OK;
+}
+
+// k_chol_persist on `st`: steps 0 .. T-2 (smode: the chain also factors tile 0, waiting for the
+// streamed J^T J's tiles); xcd >= 0 confines it to that XCD
+static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, int* dinfo, int xcd, int smode) {
+    const int T = w.T;
+    int ntasks = 0;
+    for (int R = T - 1; R >= 1; --R) ntasks += R + R * (R + 1) / 2 - 1;
+    // tuning knob (read per call): PNOL_CHOL5_WORKERS = worker workgroups; one per CU
+    // (the look-ahead areas already hold the static LDS to one workgroup per CU).
+    // PNOL_CHOL_LOOKAHEAD = 0 turns the diagonal chain's look-ahead off (read per call).
+    const char* ew = std::getenv("PNOL_CHOL5_WORKERS");
+    const char* el = std::getenv("PNOL_CHOL_LOOKAHEAD");
+    // > 0: the look-ahead gives up once wave 0 has finished that many columns of the tile
+    // (0 off; above 64: the factor waits for the next tiles).  Measured at n = 2048
+    // (tools/microbench/chol_timeline.hip): 0: 0.645 ms, 52: 0.625, 64: 0.621 (default; half
+    // the steps find their tiles ready), 1000: 0.705 -- the next tiles wait on a panel and an
+    // update task (~6 us each after W_{d-1}), so waiting for them inside the factor costs more
+    // than the prepare it saves.
+    const int lookahead = el ? std::max(0, std::atoi(el)) : 64;
+    const int slots = std::max(ctx->num_cu, 1) - 1;
+    const int want = ew ? std::atoi(ew) : slots;
+    const int workers = std::max(1, std::min(ntasks, want));
+    hipLaunchKernelGGL(k_chol_persist, dim3(1 + workers), dim3(256), 0, st, w.P, w.Lm, w.ldp, T, w.W, w.bv, w.zv, w.pf,
+                       ntasks, dinfo, lookahead, xcd, smode);
+    return launch_check();
+}
+
+// the backward solve (+ the trial point) on `st`
+static int chol_bwd_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, int n, double* sigma, int* dinfo,
+                           const double* xbase, double* xnext) {
     const int epoch = ++ctx->chol4_epoch;
-    if (gran && ((uintptr_t)xw & 15) != 0) return PNOL_ERR_ARG;   // granules need 16-byte alignment
-    if (gran)
-        hipLaunchKernelGGL(k_chol_bwd<true>, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n,
-                           (const double*)W, (const double*)bv, (const double*)zv, (double*)xw, sigma, bwdflag, epoch,
+    if (w.gran && ((uintptr_t)w.xw & 15) != 0) return PNOL_ERR_ARG;   // granules need 16-byte alignment
+    if (w.gran)
+        hipLaunchKernelGGL(k_chol_bwd<true>, dim3(w.T), dim3(256), 0, st, (const double*)w.Lm, w.ldp, w.T, n,
+                           (const double*)w.W, (const double*)w.bv, (const double*)w.zv, w.xw, sigma, w.bwdflag, epoch,
                            dinfo, xbase, xnext);
     else
-        hipLaunchKernelGGL(k_chol_bwd<false>, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n,
-                           (const double*)W, (const double*)bv, (const double*)zv, (double*)xw, sigma, bwdflag, epoch,
+        hipLaunchKernelGGL(k_chol_bwd<false>, dim3(w.T), dim3(256), 0, st, (const double*)w.Lm, w.ldp, w.T, n,
+                           (const double*)w.W, (const double*)w.bv, (const double*)w.zv, w.xw, sigma, w.bwdflag, epoch,
                            dinfo, xbase, xnext);
     PNOL_CHECK(launch_check());
     // test hook (tests/test_gpu_solvers.py): report a non-positive pivot so the callers' LU
     // fallback paths run on an SPD system (read per call: the tests flip it)
     if (const char* e = std::getenv("PNOL_CHOL_FORCE_FALLBACK"))
         if (std::atoi(e) != 0) {
-            hipLaunchKernelGGL(k_flag_info, dim3(1), dim3(1), 0, ctx->stream, dinfo, 1);
+            hipLaunchKernelGGL(k_flag_info, dim3(1), dim3(1), 0, st, dinfo, 1);
             return launch_check();
         }
     return PNOL_OK;
+}
+
+int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo,
+                        int variant, const double* xbase, double* xnext) {
+    CholWs w;
+    PNOL_CHECK(chol_ws(ctx, n, w));
+    const int T = w.T, N = w.N;
+    const bool persist = chol_persistent(variant) && T >= 2;
+    for (int k = -1; k <= (persist ? -1 : T - 2); ++k) {
+        const int R = T - 1 - k;
+        const int grid = k < 0 ? 2 + std::min(N, 1024) : R + R * (R + 1) / 2;
+        const int epoch = ++ctx->chol4_epoch;
+        hipLaunchKernelGGL(k_chol_step, dim3(grid), dim3(256), 0, ctx->stream, w.P, w.Lm, w.ldp, T, k, w.W, w.bv, w.zv,
+                           w.rowflag, epoch, dinfo, A, (long)lda, n, rhs, w.pf, persist ? w.npf : 0);
+    }
+    if (persist) {
+        // PNOL_CHOL_XCD = x: the factorisation confined to XCD x (measurement: what one XCD's
+        // CUs give, the placement a solve beside the J^T J has)
+        static const int xcd = [] {
+            const char* e = std::getenv("PNOL_CHOL_XCD");
+            return e ? std::atoi(e) : -1;
+        }();
+        PNOL_CHECK(chol_persist_launch(ctx, ctx->stream, w, dinfo, xcd, 0));
+    }
+    return chol_bwd_launch(ctx, ctx->stream, w, n, sigma, dinfo, xbase, xnext);
+}
+
+// The streamed solve's prep on the context stream (after rhs is formed): returns where the J^T J
+// writes (P, ldp, T 64-tiles) and the tile version words it publishes
+int launch_chol_stream_prep(pnol_ctx* ctx, int n, const double* rhs, int* dinfo, double** P, long* ldp, int* T,
+                            int** ver) {
+    if (n <= NB || !rhs || !dinfo) return PNOL_ERR_ARG;
+    CholWs w;
+    PNOL_CHECK(chol_ws(ctx, n, w));
+    hipLaunchKernelGGL(k_chol_stream_prep, dim3(std::min(1024, (w.N * w.N / 8 + 255) / 256 + 1)), dim3(256), 0,
+                       ctx->stream, w.P, w.ldp, w.T, n, w.bv, rhs, w.pf, w.npf, dinfo);
+    *P = w.P;
+    *ldp = w.ldp;
+    *T = w.T;
+    *ver = w.pf + 3 * w.T;
+    return launch_check();
+}
+
+// The streamed solve proper on `st` (behind the prep): the persistent factorisation on XCD xcd,
+// consuming the J^T J's tiles as they are published, then the backward solve and the trial point
+int launch_chol_stream_solve(pnol_ctx* ctx, hipStream_t st, int n, double* sigma, int* dinfo, int xcd,
+                             const double* xbase, double* xnext) {
+    CholWs w;
+    PNOL_CHECK(chol_ws(ctx, n, w));
+    PNOL_CHECK(chol_persist_launch(ctx, st, w, dinfo, xcd, 1));
+    return chol_bwd_launch(ctx, st, w, n, sigma, dinfo, xbase, xnext);
 }
 
 }  // namespace pnol

@@ -120,27 +120,27 @@ __device__ unsigned long long g_syrk_tl[3 * 65536];
 // TILE 128: waves 2 x 2 of 64 x 64 (4 x 4 MFMA blocks each); TILE 64: 2 x 2 of 32 x 32.
 // NW = 4: waves 2 x 2, each (TILE/2)^2; NW = 8: waves 2 x 4, each TILE/2 x TILE/4 (half the
 // accumulators per wave, so twice the waves per SIMD hide the stage boundaries).
-template <int MODE, int TILE, int NW = 4>
-__global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
-                                                      int split_k, int kfirst, int kchunk, int sub, int slice0,
-                                                      int mS, long sstride, double* __restrict__ part, int tile0) {
+// A partial-tile store: non-temporal, or (SC1: a consumer in the same launch, possibly on another
+// XCD, reads it after a counter hand-off) write-through sc1 (MI355X_MICROARCH.md "Valid forms")
+template <bool SC1>
+__device__ __forceinline__ void part_store(double* p, double v) {
+    if (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __builtin_nontemporal_store(v, p);
+}
+
+// One split-K unit: the partial of lower-triangle tile t (row-major tile index) over K slice
+// sidx, into partial slot blk.  MODE 0 / 2: 128 x 128 partials part + blk * TILE^2; MODE 4: 64 x 64
+// tiles into the 128 x 128 partial layout (see the store below).
+// TILE 128: waves 2 x 2 of 64 x 64 (4 x 4 MFMA blocks each); TILE 64: 2 x 2 of 32 x 32.
+// NW = 4: waves 2 x 2, each (TILE/2)^2; NW = 8: waves 2 x 4, each TILE/2 x TILE/4 (half the
+// accumulators per wave, so twice the waves per SIMD hide the stage boundaries).
+template <int MODE, int TILE, int NW, bool SC1>
+__device__ __forceinline__ void syrk_unit(const double* __restrict__ X, long ldx, int nr, int K, int split_k,
+                                          int kfirst, int kchunk, int sub, int slice0, int mS, long sstride,
+                                          double* __restrict__ part, int t, int sidx, int blk,
+                                          double (*lds)[2][TILE * kPad]) {
     constexpr int NT = 64 * NW, WC = NW / 2;
     constexpr int WTM = TILE / 2, WTN = TILE / WC, NBM = WTM / 16, NBN = WTN / 16;
-    __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
-#ifdef PNOL_SYRK_TIMELINE
-    const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    // every (tile, slice)'s chunk 0 first, then chunk 1, ...: with a long chunk 0 the short
-    // chunks fill the last dispatch round instead of leaving it part-empty
-    int blk, t, sidx;
-    {
-        const int ntl = gridDim.x / split_k, nsl = split_k / sub;
-        const int u0 = blockIdx.x / (ntl * nsl), rest = blockIdx.x % (ntl * nsl);
-        const int tl = rest / nsl;
-        sidx = (rest % nsl) * sub + u0;
-        blk = tl * split_k + sidx;           // partial slot (local to this launch)
-        t = tile0 + tl;                      // lower-triangle tile index
-    }
     int ti, tj;
     tile_of(t, ti, tj);
     const bool diag = ti == tj;
@@ -283,8 +283,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                 if (q < 4 || dcnt == 5)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        __builtin_nontemporal_store(acc[q >> 1][q & 1][r],
-                                                    out + (dbi[q] * 16 + orow + 4 * r) * ld + dbj[q] * 16 + ocol);
+                        part_store<SC1>(out + (dbi[q] * 16 + orow + 4 * r) * ld + dbj[q] * 16 + ocol, acc[q >> 1][q & 1][r]);
             // upper block u = bj (bj - 1) / 2 + bi (bi < bj): blocks wave, wave + 8, ... of the 28
             for (int u = __builtin_amdgcn_readfirstlane(wave); u < 28; u += NW) {
                 int bj = 1;
@@ -292,7 +291,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                 const int bi = u - bj * (bj - 1) / 2;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    __builtin_nontemporal_store(0.0, out + (bi * 16 + orow + 4 * r) * ld + bj * 16 + ocol);
+                    part_store<SC1>(out + (bi * 16 + orow + 4 * r) * ld + bj * 16 + ocol, 0.0);
             }
         } else {
 #pragma unroll
@@ -303,10 +302,37 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                     for (int r = 0; r < 4; ++r) {
                         int row = wr * WTM + mi * 16 + orow + 4 * r;
                         int col = wc * WTN + ni * 16 + ocol;
-                        __builtin_nontemporal_store(acc[mi][ni][r], out + row * ld + col);
+                        part_store<SC1>(out + row * ld + col, acc[mi][ni][r]);
                     }
         }
     }
+}
+
+// MODE 0: write split-K partial tile to part; MODE 4: 64 x 64 tiles into the 128 x 128 partial
+// layout of MODE 0; MODE 2: as MODE 0, instantiated separately for the chunked launches of
+// launch_fd_jtj (so a kernel trace tells the whole-matrix launches and the pipelined row chunks
+// apart).  One unit per workgroup.
+template <int MODE, int TILE, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
+                                                      int split_k, int kfirst, int kchunk, int sub, int slice0,
+                                                      int mS, long sstride, double* __restrict__ part, int tile0) {
+    __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
+#ifdef PNOL_SYRK_TIMELINE
+    const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    // every (tile, slice)'s chunk 0 first, then chunk 1, ...: with a long chunk 0 the short
+    // chunks fill the last dispatch round instead of leaving it part-empty
+    int blk, t, sidx;
+    {
+        const int ntl = gridDim.x / split_k, nsl = split_k / sub;
+        const int u0 = blockIdx.x / (ntl * nsl), rest = blockIdx.x % (ntl * nsl);
+        const int tl = rest / nsl;
+        sidx = (rest % nsl) * sub + u0;
+        blk = tl * split_k + sidx;           // partial slot (local to this launch)
+        t = tile0 + tl;                      // lower-triangle tile index
+    }
+    syrk_unit<MODE, TILE, NW, false>(X, ldx, nr, K, split_k, kfirst, kchunk, sub, slice0, mS, sstride, part, t, sidx,
+                                     blk, lds);
 #ifdef PNOL_SYRK_TIMELINE
     if (threadIdx.x == 0) {
         const unsigned long long tl1 = __builtin_amdgcn_s_memrealtime();
@@ -317,6 +343,19 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
         g_syrk_tl[3 * blockIdx.x + 2] = ((unsigned long long)xcc << 32) | hw;
     }
 #endif
+}
+
+// ---- J^T J streamed into the Cholesky (launch_jtj_stream) ---------------------------------------
+// 16-byte sc1 load / store at byte offset `off` from a wave-uniform base (buffer_load / _store
+// dwordx4 ... sc1; 0x00020000: the gfx9 raw-buffer descriptor word 3, 32-bit data format)
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ double2 ld16_sc1(const double* base, unsigned off) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+    return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+
+__device__ __forceinline__ int xcc_id() {
+    return (int)(__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) & 15);   // HW_REG_XCC_ID
 }
 
 // ---- the m-slice summation tree ------------------------------------------------------------
@@ -346,6 +385,91 @@ __device__ __forceinline__ void tree_merge(double (&v)[kS], int (&sz)[kS]) {
 
 __device__ __forceinline__ double tree8(const double (&l)[kS]) {
     return ((l[0] + l[1]) + (l[2] + l[3])) + ((l[4] + l[5]) + (l[6] + l[7]));
+}
+
+// Persistent J^T J whose tiles feed the tile Cholesky as they complete (launch_jtj_stream).
+// Workgroups claim split-K units from words[0] in tile-column order (the 128 x 128 tiles of
+// column 0 first: the Cholesky's first steps need them; within a tile the long chunk 0 of every
+// slice first), compute them as k_syrk_tile does (syrk_unit: the same MFMA chains), and store the
+// partial write-through (sc1).  The workgroup whose unit arrives last at a tile (words[1 + t],
+// one agent-scope add per workgroup after every wave's stores drained) sums the tile's partials
+// exactly as k_syrk_reduce does -- leaf s = the sub-chunks from 0.0 in order, then tree8 -- applies
+// the Marquardt diagonal, writes the tile (the diagonal tiles also mirrored) into the Cholesky's
+// padded matrix P with sc1 stores, and publishes version 0 of the tile's 64 x 64 sub-tiles in the
+// Cholesky's words (ver, set to -1 by its prep): every Cholesky task's wait ver >= k then also
+// waits for its tile.  Hand-offs per MI355X_MICROARCH.md "Valid forms" row 1.  skip_xcd >= 0:
+// workgroups dispatched to that XCD leave at once (it runs the Cholesky).  Units are claimed
+// dynamically, so an XCD with fewer workgroups simply takes fewer units.
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 2) void k_syrk_stream(const double* __restrict__ X, long ldx, int nr, int K,
+                                                        int split_k, int kfirst, int kchunk, int sub, int mS,
+                                                        long sstride, double* __restrict__ part, int nt,
+                                                        int skip_xcd, int* __restrict__ words, double lambda,
+                                                        double* __restrict__ P, long ldp, int T,
+                                                        int* __restrict__ ver) {
+    __shared__ __attribute__((aligned(16))) double lds[2][2][kTile * kPad];
+    __shared__ int item_sh, last_sh;
+    if (skip_xcd >= 0 && xcc_id() == skip_xcd) return;
+    constexpr int NT = 64 * NW;
+    const int ntiles = nt * (nt + 1) / 2, nitems = ntiles * split_k, nsl = split_k / sub;
+    const long E = (long)kTile * kTile;
+    for (;;) {
+        if (threadIdx.x == 0) item_sh = __hip_atomic_fetch_add(words, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const int q = item_sh;
+        if (q >= nitems) return;
+        int r = q / split_k, tj = 0;
+        const int w = q % split_k;
+        while (r >= nt - tj) {
+            r -= nt - tj;
+            ++tj;
+        }
+        const int ti = tj + r, t = ti * (ti + 1) / 2 + tj;
+        const int sidx = (w % nsl) * sub + w / nsl;
+        syrk_unit<0, kTile, NW, true>(X, ldx, nr, K, split_k, kfirst, kchunk, sub, 0, mS, sstride, part, t, sidx,
+                                      t * split_k + sidx, lds);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();   // every wave's partial stores drained (also: item_sh and lds free)
+        if (threadIdx.x == 0)
+            last_sh = __hip_atomic_fetch_add(words + 1 + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                      split_k - 1;
+        __syncthreads();
+        if (!last_sh) continue;
+        // ---- the tile's reduce (its last unit's workgroup)
+        const double scale = 1 + lambda;
+        const double* pt = part + (long)t * split_k * E;
+        for (int e = threadIdx.x; e < (int)(E / 2); e += NT) {
+            double lx[kS], ly[kS];
+#pragma unroll
+            for (int sl = 0; sl < kS; ++sl) {
+                double ax = 0.0, ay = 0.0;
+                for (int u = 0; u < sub; ++u) {
+                    const double2 v = ld16_sc1(pt + (long)(sl * sub + u) * E, (unsigned)(e * 16));
+                    ax += v.x;
+                    ay += v.y;
+                }
+                lx[sl] = ax;
+                ly[sl] = ay;
+            }
+            const int rr = (2 * e) / kTile, cc = (2 * e) % kTile;
+            const int i = ti * kTile + rr;
+            for (int h = 0; h < 2; ++h) {
+                const int j = tj * kTile + cc + h;
+                double v = h ? tree8(ly) : tree8(lx);
+                if (i >= nr || j >= nr || (ti == tj && j > i)) continue;
+                if (i == j) v = scale * v;
+                __hip_atomic_store(P + (long)i * ldp + j, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (ti == tj && j < i) __hip_atomic_store(P + (long)j * ldp + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x < 4) {   // the 64 x 64 sub-tiles (2 ti + a, 2 tj + b) on or below the diagonal
+            const int a = threadIdx.x >> 1, b = threadIdx.x & 1;
+            const int I = 2 * ti + a, J = 2 * tj + b;
+            if (I < T && J < T && J <= I) __hip_atomic_store(ver + (long)I * T + J, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 // Leaves of slices [s0, s1) -- leaf s = sum over u < sub of
@@ -679,6 +803,42 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     return PNOL_OK;
 }
 
+// J^T J streamed into the Cholesky's padded matrix P (ld ldp, T 64-tiles; its words ver at -1):
+// k_syrk_stream on `stream`, skip_xcd's workgroups leaving at once.  The split-K partials stay in
+// "syrk_part" (launch_jtj_from_partials forms A from them for the LU fallback).
+int launch_jtj_stream(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldjt, int m, int n, double lambda,
+                      double* P, long ldp, int T, int* ver, int skip_xcd) {
+    if (!JT || !P || !ver || m <= 0 || n <= PNOL_SEQ_MAX || ldjt < m || ldp < (long)T * 64 || T * 64 < n)
+        return PNOL_ERR_ARG;
+    const int nt = (n + kTile - 1) / kTile;
+    const int ntiles = nt * (nt + 1) / 2;
+    const SliceCfg sc = slice_cfg(m, ntiles);
+    const int split = kS * sc.sub;
+    void *part = nullptr, *words = nullptr;
+    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * split * kTile * kTile, &part));
+    PNOL_CHECK(ws_get(ctx, "syrk_stream_words", sizeof(int) * (size_t)(1 + ntiles), &words));
+    PNOL_HIP(hipMemsetAsync(words, 0, sizeof(int) * (size_t)(1 + ntiles), stream));
+    LaunchTimer tm(ctx, "syrk");
+    const int grid = 2 * std::max(ctx->num_cu, 1);   // persistent: two workgroups per CU
+    hipExtLaunchKernelGGL((k_syrk_stream<8>), dim3(grid), dim3(512), 0, stream, tm.start(), tm.stop(), 0, JT,
+                          (long)ldjt, n, m, split, sc.kfirst, sc.kchunk, sc.sub, sc.mS, (long)sc.mS, (double*)part, nt,
+                          skip_xcd, (int*)words, lambda, P, ldp, T, ver);
+    return launch_check();
+}
+
+// A (lower triangle + mirror, the Marquardt diagonal) from the partials of the last launch_jtj_stream
+// (the same reduce as launch_jtj, so the same A)
+int launch_jtj_from_partials(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda) {
+    const int nt = (n + kTile - 1) / kTile;
+    const int ntiles = nt * (nt + 1) / 2;
+    const SliceCfg sc = slice_cfg(m, ntiles);
+    void* part = nullptr;
+    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * kS * sc.sub * kTile * kTile, &part));
+    launch_reduce(dim3(kTile / 32, ntiles), dim3(256), 0, ctx->stream, (const double*)part, ntiles, sc.sub, n, lambda,
+                  A, (long)lda, (double*)nullptr, 0);
+    return launch_check();
+}
+
 int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldjt, int m, int n, double lambda,
                     double* A, int lda, double* jtj_diag, int row_begin, int row_end) {
     const int nt = (n + kTile - 1) / kTile;
@@ -754,6 +914,41 @@ int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h,
     PNOL_HIP(hipEventRecord(ctx->aux_events[nchunks], ctx->aux_stream));
     PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->aux_events[nchunks], 0));
     return rhs ? launch_jtr(ctx, JT, ldjt, m, n, F0, rhs) : PNOL_OK;
+}
+
+// One LM trip's linear algebra with the damped solve streamed behind the J^T J (single process,
+// n > PNOL_SEQ_MAX, LevenbergMarquardt.cpp:59-83): FD Jacobian, rhs = -J^T F, the Cholesky's
+// prep, then at once k_syrk_stream on the context stream (every XCD but xcd) and the persistent
+// Cholesky + backward solve on the aux stream (XCD xcd only), each 64 x 64 tile of A factored
+// as soon as the J^T J publishes it.  A is not formed (launch_jtj_from_partials forms it for the
+// LU fallback); JT, rhs, sigma and xnext are bitwise those of launch_fd_jtj + launch_chol_solve.
+int launch_fd_normal_solve_stream(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0,
+                                  int compute_f0, double* JT, int ldjt, double lambda, double* rhs, double* sigma,
+                                  int* dinfo, double* xnext, int xcd) {
+    if (!o || !x || !h || !F0 || !JT || !rhs || !sigma || !dinfo || !xnext || ldjt < o->m) return PNOL_ERR_ARG;
+    const int n = o->n, m = o->m;
+    if (n <= PNOL_SEQ_MAX || xcd < 0 || xcd > 7) return PNOL_ERR_ARG;
+    PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
+    PNOL_CHECK(launch_jtr(ctx, JT, ldjt, m, n, F0, rhs));
+    double* P = nullptr;
+    long ldp = 0;
+    int T = 0;
+    int* ver = nullptr;
+    PNOL_CHECK(launch_chol_stream_prep(ctx, n, rhs, dinfo, &P, &ldp, &T, &ver));
+    if (!ctx->aux_stream) PNOL_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
+    while (ctx->aux_events.size() < 2) {
+        hipEvent_t e;
+        PNOL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->aux_events.push_back(e);
+    }
+    PNOL_HIP(hipEventRecord(ctx->aux_events[0], ctx->stream));
+    PNOL_HIP(hipStreamWaitEvent(ctx->aux_stream, ctx->aux_events[0], 0));
+    // the Cholesky first: its workgroups off XCD xcd leave at once, before the J^T J fills them
+    PNOL_CHECK(launch_chol_stream_solve(ctx, ctx->aux_stream, n, sigma, dinfo, xcd, x, xnext));
+    PNOL_CHECK(launch_jtj_stream(ctx, ctx->stream, JT, ldjt, m, n, lambda, P, ldp, T, ver, xcd));
+    PNOL_HIP(hipEventRecord(ctx->aux_events[1], ctx->aux_stream));
+    PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->aux_events[1], 0));
+    return PNOL_OK;
 }
 
 // J^T J with the 128 x 128 tiles split over the communicator's ranks (contiguous ranges of

@@ -184,6 +184,14 @@ int launch_gather_rows(pnol_ctx* ctx, const double* D, int ldd, const int* ridx,
 // rhs (nullable): also rhs = -J^T F (bitwise launch_jtr), its slice tree in the reduce launch
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                double* jtj_diag, const double* F = nullptr, double* rhs = nullptr);
+// J^T J streamed into the tile Cholesky (syrk.hip): tiles reduced into its padded P as they
+// complete, each publishing its sub-tiles' Cholesky version words; skip_xcd's workgroups leave
+int launch_jtj_stream(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldjt, int m, int n, double lambda,
+                      double* P, long ldp, int T, int* ver, int skip_xcd);
+int launch_fd_normal_solve_stream(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0,
+                                  int compute_f0, double* JT, int ldjt, double lambda, double* rhs, double* sigma,
+                                  int* dinfo, double* xnext, int xcd);
+int launch_jtj_from_partials(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda);
 int launch_jtj_sharded(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                        double* jtj_diag);
 int launch_jtr(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
@@ -200,6 +208,13 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
                         int variant, const double* xbase = nullptr, double* xnext = nullptr);
 int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n, int method,
                  int* info);
+// The streamed damped solve (chol.hip): the prep on the context stream after rhs is formed
+// (returns where the J^T J writes and the version words it publishes), then the persistent
+// factorisation on XCD xcd + the backward solve (and xnext = xbase + sigma) on stream st
+int launch_chol_stream_prep(pnol_ctx* ctx, int n, const double* rhs, int* dinfo, double** P, long* ldp, int* T,
+                            int** ver);
+int launch_chol_stream_solve(pnol_ctx* ctx, hipStream_t st, int n, double* sigma, int* dinfo, int xcd,
+                             const double* xbase, double* xnext);
 
 int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
 // rows [r0, r1) only (multiples of 64 but r1 = m; r1 < 0: all): a row-sharded LevMarqMPI rank
