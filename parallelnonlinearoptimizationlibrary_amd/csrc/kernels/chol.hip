@@ -1721,7 +1721,8 @@ static int chol_ws(pnol_ctx* ctx, int n, CholWs& w) {
 
 // k_chol_persist on `st`: steps 0 .. T-2 (smode: the chain also factors tile 0, waiting for the
 // streamed J^T J's tiles); xcd >= 0 confines it to that XCD
-static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, int* dinfo, int xcd, int smode) {
+static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, int* dinfo, int xcd, int smode,
+                               int xcd_cus = 0) {
     const int T = w.T;
     int ntasks = 0;
     for (int R = T - 1; R >= 1; --R) ntasks += R + R * (R + 1) / 2 - 1;
@@ -1739,8 +1740,13 @@ static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, i
     const int lookahead = el ? std::max(0, std::atoi(el)) : 64;
     const int slots = std::max(ctx->num_cu, 1) - 1;
     const int want = ew ? std::atoi(ew) : slots;
-    const int workers = std::max(1, std::min(ntasks, want));
-    hipLaunchKernelGGL(k_chol_persist, dim3(1 + workers), dim3(256), 0, st, w.P, w.Lm, w.ldp, T, w.W, w.bv, w.zv, w.pf,
+    int workers = std::max(1, std::min(ntasks, want)), grid = 1 + workers;
+    if (xcd >= 0) {   // workgroup b goes to XCD b % 8: every XCD gets the chain + its workers
+        const int cus = xcd_cus > 0 ? xcd_cus : std::max(ctx->num_cu, 8) / 8;   // the XCD's CUs it may use
+        workers = std::max(1, std::min({ntasks, want, cus - 1}));
+        grid = 8 * (1 + workers);
+    }
+    hipLaunchKernelGGL(k_chol_persist, dim3(grid), dim3(256), 0, st, w.P, w.Lm, w.ldp, T, w.W, w.bv, w.zv, w.pf,
                        ntasks, dinfo, lookahead, xcd, smode);
     return launch_check();
 }
@@ -1810,13 +1816,14 @@ int launch_chol_stream_prep(pnol_ctx* ctx, int n, const double* rhs, int* dinfo,
     return launch_check();
 }
 
-// The streamed solve proper on `st` (behind the prep): the persistent factorisation on XCD xcd,
+// The streamed solve proper on `st` (behind the prep): the persistent factorisation on XCD xcd
+// (xcd_cus of its CUs: the chain + xcd_cus - 1 workers),
 // consuming the J^T J's tiles as they are published, then the backward solve and the trial point
-int launch_chol_stream_solve(pnol_ctx* ctx, hipStream_t st, int n, double* sigma, int* dinfo, int xcd,
+int launch_chol_stream_solve(pnol_ctx* ctx, hipStream_t st, int n, double* sigma, int* dinfo, int xcd, int xcd_cus,
                              const double* xbase, double* xnext) {
     CholWs w;
     PNOL_CHECK(chol_ws(ctx, n, w));
-    PNOL_CHECK(chol_persist_launch(ctx, st, w, dinfo, xcd, 1));
+    PNOL_CHECK(chol_persist_launch(ctx, st, w, dinfo, xcd, 1, xcd_cus));
     return chol_bwd_launch(ctx, st, w, n, sigma, dinfo, xbase, xnext);
 }
 

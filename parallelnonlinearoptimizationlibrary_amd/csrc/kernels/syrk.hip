@@ -916,6 +916,32 @@ int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h,
     return rhs ? launch_jtr(ctx, JT, ldjt, m, n, F0, rhs) : PNOL_OK;
 }
 
+// The streamed solve's two CU-masked streams for XCD xcd (ctx->split_streams).  CU mask bit i
+// is CU i / 8 of XCD i % 8 (tools/microbench/cumask_probe.hip); an XCD left without a bit would
+// be unrestricted, so each stream keeps one CU -- the XCD's last -- of every XCD it does not run
+// on, and the other stream leaves that CU out.
+static int split_streams(pnol_ctx* ctx, int xcd) {
+    if (ctx->split_xcd == xcd && ctx->split_streams[0]) return PNOL_OK;
+    const int ncu = ctx->num_cu, per = ncu / 8;
+    if (ncu < 16 || ncu % 8 != 0) return PNOL_ERR_UNSUPPORTED;
+    for (hipStream_t& st : ctx->split_streams)
+        if (st) {
+            PNOL_HIP(hipStreamSynchronize(st));
+            PNOL_HIP(hipStreamDestroy(st));
+            st = nullptr;
+        }
+    std::vector<uint32_t> mj((ncu + 31) / 32, 0u), mc((ncu + 31) / 32, 0u);
+    for (int i = 0; i < ncu; ++i) {
+        const bool own = i % 8 == xcd, last = i / 8 == per - 1;
+        const bool chol = own ? !last : last;
+        (chol ? mc : mj)[i / 32] |= 1u << (i % 32);
+    }
+    PNOL_HIP(hipExtStreamCreateWithCUMask(&ctx->split_streams[0], (uint32_t)mj.size(), mj.data()));
+    PNOL_HIP(hipExtStreamCreateWithCUMask(&ctx->split_streams[1], (uint32_t)mc.size(), mc.data()));
+    ctx->split_xcd = xcd;
+    return PNOL_OK;
+}
+
 // One LM trip's linear algebra with the damped solve streamed behind the J^T J (single process,
 // n > PNOL_SEQ_MAX, LevenbergMarquardt.cpp:59-83): FD Jacobian, rhs = -J^T F, the Cholesky's
 // prep, then at once k_syrk_stream on the context stream (every XCD but xcd) and the persistent
@@ -935,19 +961,22 @@ int launch_fd_normal_solve_stream(pnol_ctx* ctx, pnol_dobj* o, const double* x, 
     int T = 0;
     int* ver = nullptr;
     PNOL_CHECK(launch_chol_stream_prep(ctx, n, rhs, dinfo, &P, &ldp, &T, &ver));
-    if (!ctx->aux_stream) PNOL_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
-    while (ctx->aux_events.size() < 2) {
+    while (ctx->aux_events.size() < 3) {
         hipEvent_t e;
         PNOL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ctx->aux_events.push_back(e);
     }
     PNOL_HIP(hipEventRecord(ctx->aux_events[0], ctx->stream));
-    PNOL_HIP(hipStreamWaitEvent(ctx->aux_stream, ctx->aux_events[0], 0));
-    // the Cholesky first: its workgroups off XCD xcd leave at once, before the J^T J fills them
-    PNOL_CHECK(launch_chol_stream_solve(ctx, ctx->aux_stream, n, sigma, dinfo, xcd, x, xnext));
-    PNOL_CHECK(launch_jtj_stream(ctx, ctx->stream, JT, ldjt, m, n, lambda, P, ldp, T, ver, xcd));
-    PNOL_HIP(hipEventRecord(ctx->aux_events[1], ctx->aux_stream));
+    PNOL_CHECK(split_streams(ctx, xcd));
+    hipStream_t sj = ctx->split_streams[0], sc = ctx->split_streams[1];
+    PNOL_HIP(hipStreamWaitEvent(sj, ctx->aux_events[0], 0));
+    PNOL_HIP(hipStreamWaitEvent(sc, ctx->aux_events[0], 0));
+    PNOL_CHECK(launch_chol_stream_solve(ctx, sc, n, sigma, dinfo, xcd, std::max(ctx->num_cu, 8) / 8 - 1, x, xnext));
+    PNOL_CHECK(launch_jtj_stream(ctx, sj, JT, ldjt, m, n, lambda, P, ldp, T, ver, xcd));
+    PNOL_HIP(hipEventRecord(ctx->aux_events[1], sc));
     PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->aux_events[1], 0));
+    PNOL_HIP(hipEventRecord(ctx->aux_events[2], sj));
+    PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->aux_events[2], 0));
     return PNOL_OK;
 }
 

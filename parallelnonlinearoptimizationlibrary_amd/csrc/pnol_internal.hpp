@@ -74,6 +74,12 @@ struct pnol_ctx {
     hipStream_t comm_stream = nullptr;
     std::vector<hipEvent_t> phase_events;
     hipEvent_t comm_done = nullptr;
+    // the streamed damped solve (launch_fd_normal_solve_stream): two CU-masked streams that
+    // share no CU -- [0] the J^T J: every CU off XCD split_xcd plus one CU of it; [1] the
+    // Cholesky: the rest of XCD split_xcd plus one CU of every other XCD (a workgroup dispatched
+    // off its XCD leaves at once, so neither launch ever waits for the other's CUs)
+    hipStream_t split_streams[2] = {nullptr, nullptr};
+    int split_xcd = -1;
 };
 
 struct pnol_dobj {
@@ -213,7 +219,7 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
 // factorisation on XCD xcd + the backward solve (and xnext = xbase + sigma) on stream st
 int launch_chol_stream_prep(pnol_ctx* ctx, int n, const double* rhs, int* dinfo, double** P, long* ldp, int* T,
                             int** ver);
-int launch_chol_stream_solve(pnol_ctx* ctx, hipStream_t st, int n, double* sigma, int* dinfo, int xcd,
+int launch_chol_stream_solve(pnol_ctx* ctx, hipStream_t st, int n, double* sigma, int* dinfo, int xcd, int xcd_cus,
                              const double* xbase, double* xnext);
 
 int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);

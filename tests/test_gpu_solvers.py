@@ -576,14 +576,16 @@ def test_lm_streamed_trip_loop_equals_general_loop(ctx, oracle, m, n, force, mon
     params = (0.001, 10, 1e-7, 8, 0.0, -1)
     monkeypatch.setenv("PNOL_CHOL_FORCE_FALLBACK", force)
     out = {}
-    for mode, stream in (("1", "1"), ("0", "0")):
+    for name, mode, stream in (("stream", "1", "1"), ("async", "1", "0"), ("general", "0", "0")):
         monkeypatch.setenv("PNOL_LM_ASYNC", mode)
         monkeypatch.setenv("PNOL_LM_STREAM", stream)
-        out[mode] = run_levmarq(_obj(ctx, L.OBJ_LINRES, n, m, A, y), np.zeros(n), params)
-    (Xa, F0a, FOa, ra), (Xs, F0s, FOs, rs) = out["1"], out["0"]
-    assert np.array_equal(Xa, Xs) and np.array_equal(F0a, F0s) and np.array_equal(FOa, FOs)
-    assert ra.evals == rs.evals
-    assert rel(Xa, xs) <= 1e-8
+        out[name] = run_levmarq(_obj(ctx, L.OBJ_LINRES, n, m, A, y), np.zeros(n), params)
+    for a, b in (("stream", "async"), ("async", "general")):
+        (Xa, F0a, FOa, ra), (Xs, F0s, FOs, rs) = out[a], out[b]
+        assert np.array_equal(Xa, Xs), (a, b, rel(Xa, Xs))
+        assert np.array_equal(F0a, F0s) and np.array_equal(FOa, FOs), (a, b)
+        assert ra.evals == rs.evals, (a, b)
+    assert rel(out["stream"][0], xs) <= 1e-8
 
 
 @pytest.mark.parametrize("n", [1, 7, 100, 300])
