@@ -1280,11 +1280,12 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
 // consumer's lane 0 polls it with sc1 loads before a barrier (MI355X_MICROARCH.md "Valid forms",
 // row 1; one workgroup per CU: __launch_bounds__(256, 1) and the register count).  Every tile, panel and b update is the same arithmetic in the same order as in
 // the per-step launches, so the result is bitwise method 4's.
+// [wdone T][lcnt T][bcnt T][ver T^2][task counter][role word][tile locks T^2 (the streamed form)]
 struct PersistWords {
-    int *wdone, *lcnt, *bcnt, *ver, *counter;
+    int *wdone, *lcnt, *bcnt, *ver, *counter, *lock;
 };
 __device__ __forceinline__ PersistWords persist_words(int* f, int T) {
-    return {f, f + T, f + 2 * T, f + 3 * T, f + 3 * T + T * T};
+    return {f, f + T, f + 2 * T, f + 3 * T, f + 3 * T + T * T, f + 3 * T + T * T + 2};
 }
 
 // publish `v` into *w after every wave's (sc1) stores of this workgroup have completed
@@ -1467,6 +1468,73 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         const bool crit = i == k + 2 && j == k + 1;
         if (crit) PNOL_CRIT(k, 4)
 #endif
+        if (smode) {
+            // The streamed form: the J^T J publishes the tiles in its own (column) order, so a
+            // task must not hold its worker waiting for an unpublished tile.  The tile's updates
+            // are applied under its lock by whichever task gets there, all pending steps at once:
+            // a task that finds the tile unpublished leaves step k to the tile's next task; the
+            // tile's last task (step min(i, j) - 1, the one its consumers wait for) waits for it.
+            // A task that finds the tile already past step k has nothing to do.  The steps are
+            // the same MFMA sequence on one accumulator as the one-task-per-step form, so the
+            // tile's bits are unchanged.
+            // (the diagonal tile's step j - 1 is the chain's own, inside its prepare)
+            const bool last = k == j - 1 - (i == j ? 1 : 0);
+            if (t == 0) {
+                int ok = 1, v = __hip_atomic_load(pw.ver + i * T + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v < 0 && last) {
+                    ok = spin_ge(pw.ver + i * T + j, 0, info);
+                    v = 0;
+                }
+                if (ok && v >= 0 && v <= k) {   // the lock, then the version again under it
+                    int it = 0;
+                    while (atomicCAS(pw.lock + i * T + j, 0, 1) != 0) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if ((++it & 63) == 0 &&
+                            (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 || it > kSpin)) {
+                            if (it > kSpin) atomicExch(info, kInfoTimeout);
+                            ok = 0;
+                            break;
+                        }
+                    }
+                    if (ok) {
+                        v = __hip_atomic_load(pw.ver + i * T + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (v > k) {   // applied while this task waited for the lock
+                            __hip_atomic_store(pw.lock + i * T + j, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            v = -2;
+                        }
+                    }
+                } else if (ok) {
+                    v = -2;   // nothing to do: unpublished (not the last step) or already applied
+                }
+                ok_sh = ok;
+                task_sh = v;
+            }
+            __syncthreads();
+            const int v0 = task_sh;
+            const bool go = ok_sh;
+            __syncthreads();
+            if (!go) return;
+            if (v0 < 0) continue;
+            d4 acc[2][2];
+            acc_load<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
+            for (int kk = v0; kk <= k; ++kk) {
+                if (t == 0) ok_sh = spin_all<2>({pw.lcnt + i, pw.lcnt + j}, {kk + 1, kk + 1}, info);
+                __syncthreads();
+                if (!ok_sh) return;
+                stage_tile<true>(X, Lm, ldp, i * NB, kk * NB);
+                if (i != j) stage_tile<true>(Y, Lm, ldp, j * NB, kk * NB);
+                __syncthreads();
+                mfma_xyt<true>(acc, X, i != j ? Y : X, wr, wc, lane);
+                __syncthreads();   // X / Y are restaged by the next step
+            }
+            acc_store<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
+            publish(pw.ver + i * T + j, k + 1);
+            if (t == 0) {   // the version store completes before the lock is seen free
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(pw.lock + i * T + j, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            continue;
+        }
         // the tile's earlier updates first: its loads stay in flight while the workgroup waits
         // for the two panels
         if (t == 0) ok_sh = spin_ge(pw.ver + i * T + j, k, info);
@@ -1712,7 +1780,7 @@ static int chol_ws(pnol_ctx* ctx, int n, CholWs& w) {
     }
     w.rowflag = ctx->chol4_flags;
     w.bwdflag = ctx->chol4_flags + ctx->chol4_cap;
-    w.npf = 3 * T + T * T + 2;   // + the task counter and the role word
+    w.npf = 3 * T + 2 * T * T + 2;   // + the task counter, the role word and the tile locks
     PNOL_CHECK(ws_get(ctx, "chol5_words", sizeof(int) * (size_t)w.npf, &pf));
     w.P = (double*)P; w.Lm = (double*)Lm; w.W = (double*)W; w.bv = (double*)bv; w.zv = (double*)zv;
     w.xw = (double*)xw; w.pf = (int*)pf;

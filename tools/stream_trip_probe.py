@@ -28,4 +28,10 @@ for t in range(trips):
     out["ms"].append(round((time.perf_counter() - t0) * 1e3, 3))
     out["info"].append(ib)
     out["equal"].append(bool(np.array_equal(sb.cpu().numpy(), ref)))
+for t in range(trips):   # the two-call trip it replaces, same point
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    F0, JT, A, r = d.fd_normal(x, h, 0.37, JT, A, r)
+    ctx.solve_step(A, r, x)
+    out.setdefault("ms_two_call", []).append(round((time.perf_counter() - t0) * 1e3, 3))
 print(json.dumps(out))
