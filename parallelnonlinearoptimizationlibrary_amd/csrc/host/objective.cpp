@@ -266,7 +266,9 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
                 if (!constantIndicator[i] && std::memcmp(&rc.hf[i], &hf[i], sizeof(double)) != 0) redo.push_back((int)i);
             reuse = redo.size() <= kRecurRedoMax;
         }
+        const double* gsrc = gf.data();   // this call's per-coordinate values
         if (reuse) {
+            gsrc = rc.gf.data();
             const int k = (int)redo.size();
             if (k > 0) {
                 std::vector<double>& pts = rc.pts;
@@ -287,7 +289,6 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
                 }
             }
             countEvals(N + 1);
-            gf.assign(rc.gf.begin(), rc.gf.end());
         } else {
             double F = 0;
             device_gradient(d, Xf, hf, 0, (int)nf, &F, gf.data());
@@ -301,9 +302,12 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
                     if (d->len1) check(pnol_memcpy_d2h(c, rc.p1h.data(), d->p1, sizeof(double) * d->len1), "d2h(p1)");
                 }
                 rc.oid = d->id;
-                rc.Xf = Xf;
-                rc.hf = hf;
-                rc.gf = gf;
+                // the cache takes the buffers (no 3 x 8n-byte copies per call); the next call
+                // refills the thread-local ones
+                std::swap(rc.Xf, Xf);
+                std::swap(rc.hf, hf);
+                std::swap(rc.gf, gf);
+                gsrc = rc.gf.data();
                 rc.F = F;
                 // the quadratic's formula reads d[i], b[i] for every i < n
                 if (d->kind == PNOL_OBJ_QUADRATIC && (rc.p0h.size() < nf || rc.p1h.size() < nf)) rc.oid = 0;
@@ -311,7 +315,7 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
         }
         ir = 0;
         for (size_t i = 0; i < nf; ++i) {
-            gr[ir] = gf[i];
+            gr[ir] = gsrc[i];
             ir += !constantIndicator[i];
         }
         std::copy(gr.begin(), gr.begin() + N, dFdX.begin());
