@@ -113,6 +113,22 @@ __device__ __forceinline__ void stage_tile(double* __restrict__ dst, const doubl
     for (int q = 0; q < 8; ++q) d[q] = v[q];
 }
 
+// stage_tile in two halves: the sc1 loads into registers, then the LDS stores (so the next
+// tile's loads fly while the current one is used)
+__device__ __forceinline__ void tile_load_sc1(double2 (&v)[8], const double* __restrict__ P, long ldp, int r0, int c0) {
+    const int t = threadIdx.x, row = t >> 2, sub = t & 3;
+    const double* base = P + (long)r0 * ldp + c0;   // wave-uniform
+    const unsigned off = (unsigned)((row * ldp + sub * 16) * 8);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = ld16_sc1(base, off + 16 * q);
+}
+__device__ __forceinline__ void tile_put(double* __restrict__ dst, const double2 (&v)[8]) {
+    const int t = threadIdx.x, row = t >> 2, sub = t & 3;
+    double2* d = reinterpret_cast<double2*>(dst + sub * kSub + row * kPad);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) d[q] = v[q];
+}
+
 // acc (this wave's 32 x 32 quadrant (wr, wc)) += sign * X Y^T over the 64-wide K of two staged
 // tiles, v_mfma_f64_16x16x4_f64.  Fragment layouts: A/B lane l holds row l & 15, k = l >> 4;
 // C/D lane l, register r -> row (l >> 4) + 4 r, column l & 15.
@@ -1515,17 +1531,47 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             __syncthreads();
             if (!go) return;
             if (v0 < 0) continue;
+            // steps v0 .. k: panel words polled only when the last seen values fall short; the
+            // next step's panel tiles are loaded while the current step's MFMAs run
             d4 acc[2][2];
             acc_load<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
+            double2 ra[8], rb[8];
+            int seen = -1;   // min(lcnt[i], lcnt[j]) last observed (thread 0)
+            auto panels = [&](int need) -> bool {   // thread 0: both panels through column need - 1
+                int it = 0;
+                for (;;) {
+                    const int a = __hip_atomic_load(pw.lcnt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const int b = __hip_atomic_load(pw.lcnt + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    seen = a < b ? a : b;
+                    if (seen >= need) return true;
+                    __builtin_amdgcn_s_sleep(1);
+                    if ((++it & 63) == 0) {
+                        if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+                        if (it > kSpin) {
+                            atomicExch(info, kInfoTimeout);
+                            return false;
+                        }
+                    }
+                }
+            };
+            if (t == 0) ok_sh = panels(v0 + 1);
+            __syncthreads();
+            if (!ok_sh) return;
+            tile_load_sc1(ra, Lm, ldp, i * NB, v0 * NB);
+            if (i != j) tile_load_sc1(rb, Lm, ldp, j * NB, v0 * NB);
             for (int kk = v0; kk <= k; ++kk) {
-                if (t == 0) ok_sh = spin_all<2>({pw.lcnt + i, pw.lcnt + j}, {kk + 1, kk + 1}, info);
+                tile_put(X, ra);
+                if (i != j) tile_put(Y, rb);
                 __syncthreads();
-                if (!ok_sh) return;
-                stage_tile<true>(X, Lm, ldp, i * NB, kk * NB);
-                if (i != j) stage_tile<true>(Y, Lm, ldp, j * NB, kk * NB);
-                __syncthreads();
+                if (kk < k) {   // the next step's panels (known done, or polled now)
+                    if (t == 0) ok_sh = seen >= kk + 2 || panels(kk + 2);
+                    __syncthreads();
+                    if (!ok_sh) return;
+                    tile_load_sc1(ra, Lm, ldp, i * NB, (kk + 1) * NB);
+                    if (i != j) tile_load_sc1(rb, Lm, ldp, j * NB, (kk + 1) * NB);
+                }
                 mfma_xyt<true>(acc, X, i != j ? Y : X, wr, wc, lane);
-                __syncthreads();   // X / Y are restaged by the next step
+                __syncthreads();   // X / Y are rewritten by the next step
             }
             acc_store<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
             publish(pw.ver + i * T + j, k + 1);
