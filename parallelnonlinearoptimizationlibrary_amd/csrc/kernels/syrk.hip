@@ -406,7 +406,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_stream(const double* __rest
                                                         long sstride, double* __restrict__ part, int nt,
                                                         int skip_xcd, int* __restrict__ words, double lambda,
                                                         double* __restrict__ P, long ldp, int T,
-                                                        int* __restrict__ ver) {
+                                                        int* __restrict__ ver, int delay) {
     __shared__ __attribute__((aligned(16))) double lds[2][2][kTile * kPad];
     __shared__ int item_sh, last_sh;
     if (skip_xcd >= 0 && xcc_id() == skip_xcd) return;
@@ -418,14 +418,46 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_stream(const double* __rest
         __syncthreads();
         const int q = item_sh;
         if (q >= nitems) return;
-        int r = q / split_k, tj = 0;
-        const int w = q % split_k;
+        // claim order: every tile's long chunk-0 units (one per slice) run `delay` tiles ahead
+        // of its short units, so the last claims of the launch are short units (a short tail)
+        // while tiles still complete in column order
+        int r, sidx;
+        {
+            const int nl = nsl, ns = split_k - nsl, D = ns > 0 ? delay : 0;
+            int qq = q;
+            if (qq < D * nl) {
+                r = qq / nl;
+                sidx = (qq % nl) * sub;
+            } else {
+                qq -= D * nl;
+                const int full = (ntiles - D) * split_k;
+                int tt, off;
+                if (qq < full) {
+                    tt = qq / split_k;
+                    off = qq % split_k;
+                    if (off < nl) {   // tile tt + D's long unit
+                        r = tt + D;
+                        sidx = off * sub;
+                        off = -1;
+                    }
+                } else {
+                    qq -= full;
+                    tt = ntiles - D + qq / ns;
+                    off = nl + qq % ns;
+                }
+                if (off >= 0) {   // tile tt's short unit b = off - nl: slice b % nl, chunk 1 + b / nl
+                    const int b = off - nl;
+                    r = tt;
+                    sidx = (b % nl) * sub + 1 + b / nl;
+                }
+            }
+        }
+        int tj = 0;
         while (r >= nt - tj) {
             r -= nt - tj;
             ++tj;
         }
         const int ti = tj + r, t = ti * (ti + 1) / 2 + tj;
-        const int sidx = (w % nsl) * sub + w / nsl;
         syrk_unit<0, kTile, NW, true>(X, ldx, nr, K, split_k, kfirst, kchunk, sub, 0, mS, sstride, part, t, sidx,
                                       t * split_k + sidx, lds);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -820,9 +852,14 @@ int launch_jtj_stream(pnol_ctx* ctx, hipStream_t stream, const double* JT, int l
     PNOL_HIP(hipMemsetAsync(words, 0, sizeof(int) * (size_t)(1 + ntiles), stream));
     LaunchTimer tm(ctx, "syrk");
     const int grid = 2 * std::max(ctx->num_cu, 1);   // persistent: two workgroups per CU
+    // the long units' lead over the short ones, in tiles: about one round of the resident
+    // workgroups (PNOL_SYRK_STREAM_DELAY overrides; read per call)
+    const char* ed = std::getenv("PNOL_SYRK_STREAM_DELAY");
+    const int resident = skip_xcd >= 0 ? grid * 7 / 8 : grid;
+    const int delay = std::max(0, std::min(ntiles, ed ? std::atoi(ed) : resident / kS));
     hipExtLaunchKernelGGL((k_syrk_stream<8>), dim3(grid), dim3(512), 0, stream, tm.start(), tm.stop(), 0, JT,
                           (long)ldjt, n, m, split, sc.kfirst, sc.kchunk, sc.sub, sc.mS, (long)sc.mS, (double*)part, nt,
-                          skip_xcd, (int*)words, lambda, P, ldp, T, ver);
+                          skip_xcd, (int*)words, lambda, P, ldp, T, ver, delay);
     return launch_check();
 }
 
