@@ -343,7 +343,11 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool s
     while (iter < P.maxIter) {
         dev.enqueue(s, lambda, ckpt);
         dev.wait(s);
-        if (dev.info_h(s) != 0) dev.redo_lu(s);
+        if (dev.info_h(s) != 0) {
+            if (std::getenv("PNOL_LM_DEBUG"))
+                std::cerr << "[pnol] LM trip " << iter << ": solve status " << dev.info_h(s) << ", LU redo" << std::endl;
+            dev.redo_lu(s);
+        }
         obj->countEvals(own_cols + 1); // the trip's Jacobian
         obj->countEvals(1);            // its trial point
         // chi^2 straight from the pinned copy (no host copy of F: the accepted F stays on the

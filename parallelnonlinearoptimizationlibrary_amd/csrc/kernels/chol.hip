@@ -33,6 +33,10 @@ constexpr int kSub = NB * kPad;      // doubles per substage
 constexpr int kStage = 4 * kSub;     // one 64 x 64 tile as four substages
 constexpr int kSpin = 1 << 24;       // ~1 s of polling
 constexpr int kInfoTimeout = -7;
+// the persistent form's wait sites (the status names the wait that timed out): the chain's
+// tile-0 / tile waits, a panel task's tile / W waits, an update task's publish / lock / panel waits
+constexpr int kToChain0 = -11, kToChain = -12, kToPanelTile = -13, kToPanelW = -14, kToUpdProd = -15,
+              kToUpdLock = -16, kToUpdPanels = -17;
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
@@ -214,14 +218,15 @@ __device__ __forceinline__ void acc_to_rows(const d4 (&acc)[2][2], double* __res
             for (int r = 0; r < 4; ++r) S[acc_row(wr, mi, lane, r) * (NB + 1) + acc_col(wc, ni, lane)] = acc[mi][ni][r];
 }
 
-__device__ __forceinline__ bool spin_ge(const int* f, int target, int* info) {
+// a timed-out wait stores `code` (kInfoTimeout or a site code below it) into info
+__device__ __forceinline__ bool spin_ge(const int* f, int target, int* info, int code = kInfoTimeout) {
     int it = 0;
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
         if ((++it & 63) == 0) {
             if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
             if (it > kSpin) {
-                atomicExch(info, kInfoTimeout);
+                atomicExch(info, code);
                 return false;
             }
         }
@@ -232,7 +237,8 @@ __device__ __forceinline__ bool spin_ge(const int* f, int target, int* info) {
 // Every *f[q] >= tg[q]: all N words are loaded in each round (one memory round trip for the set
 // instead of one per word when they are already there); the same cap and info checks.
 template <int N>
-__device__ __forceinline__ bool spin_all(const int* const (&f)[N], const int (&tg)[N], int* info) {
+__device__ __forceinline__ bool spin_all(const int* const (&f)[N], const int (&tg)[N], int* info,
+                                         int code = kInfoTimeout) {
     int it = 0;
     for (;;) {
         int v[N];
@@ -246,7 +252,7 @@ __device__ __forceinline__ bool spin_all(const int* const (&f)[N], const int (&t
         if ((++it & 63) == 0) {
             if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
             if (it > kSpin) {
-                atomicExch(info, kInfoTimeout);
+                atomicExch(info, code);
                 return false;
             }
         }
@@ -1355,8 +1361,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
 #endif
             if (t == 0) {
                 const bool ok = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-                                (d == 0 ? spin_ge(pw.ver, 0, info)
-                                        : spin_all<2>({pw.ver + d * T + k, pw.ver + d * T + d}, {k, k}, info));
+                                (d == 0 ? spin_ge(pw.ver, 0, info, kToChain0)
+                                        : spin_all<2>({pw.ver + d * T + k, pw.ver + d * T + d}, {k, k}, info, kToChain));
                 ok_sh = ok;
             }
             __syncthreads();
@@ -1424,12 +1430,13 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
 #endif
             // A_ik through column k-1, b_k complete and b_i's earlier updates: usually long
             // before W_k, so A_ik is staged while the workgroup waits for the diagonal chain
-            if (t == 0) ok_sh = spin_all<3>({pw.ver + i * T + k, pw.bcnt + k, pw.bcnt + i}, {k, k, k}, info);
+            if (t == 0)
+                ok_sh = spin_all<3>({pw.ver + i * T + k, pw.bcnt + k, pw.bcnt + i}, {k, k, k}, info, kToPanelTile);
             __syncthreads();
             if (!ok_sh) return;
             stage_tile<true>(X, P, ldp, i0, k0);
             if (t == 0) {   // W_k (tile 0 comes from the prep launch)
-                ok_sh = (k == 0 && !smode) || spin_ge(pw.wdone + k, 1, info);
+                ok_sh = (k == 0 && !smode) || spin_ge(pw.wdone + k, 1, info, kToPanelW);
 #ifdef PNOL_CHOL_TIMELINE
                 if (i == k + 2) PNOL_CRIT(k, 2)
 #endif
@@ -1498,7 +1505,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             if (t == 0) {
                 int ok = 1, v = __hip_atomic_load(pw.ver + i * T + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (v < 0 && last) {
-                    ok = spin_ge(pw.ver + i * T + j, 0, info);
+                    ok = spin_ge(pw.ver + i * T + j, 0, info, kToUpdProd);
                     v = 0;
                 }
                 if (ok && v >= 0 && v <= k) {   // the lock, then the version again under it
@@ -1507,7 +1514,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
                         __builtin_amdgcn_s_sleep(1);
                         if ((++it & 63) == 0 &&
                             (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 || it > kSpin)) {
-                            if (it > kSpin) atomicExch(info, kInfoTimeout);
+                            if (it > kSpin) atomicExch(info, kToUpdLock);
                             ok = 0;
                             break;
                         }
@@ -1548,7 +1555,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
                     if ((++it & 63) == 0) {
                         if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
                         if (it > kSpin) {
-                            atomicExch(info, kInfoTimeout);
+                            atomicExch(info, kToUpdPanels);
                             return false;
                         }
                     }
@@ -1729,16 +1736,17 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm,
 
 __global__ void k_flag_info(int* info, int v) { *info = v; }
 
-// The streamed solve's prep (no copy of A: the J^T J writes P itself): the persistent form's
-// progress words -- every tile version at -1 (not yet published by the J^T J), the rest 0 --,
-// b = rhs (zero padded), P's padding (identity on the diagonal past n), info = 0.
+// The streamed solve's prep (no copy of A: the J^T J's reduce writes P itself): the persistent
+// form's progress words -- every tile version and b's block-row words at -1 (not yet published
+// by the reduce), the rest 0 --, b's padding past n, P's padding (identity on the diagonal past
+// n), info = 0.
 __global__ __launch_bounds__(256) void k_chol_stream_prep(double* __restrict__ P, long ldp, int T, int n,
-                                                          double* __restrict__ bv, const double* __restrict__ rhs,
-                                                          int* __restrict__ pflags, int npflags, int* __restrict__ info) {
+                                                          double* __restrict__ bv, int* __restrict__ pflags,
+                                                          int npflags, int* __restrict__ info) {
     const int N = T * NB, tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
-    const int v0 = 3 * T, v1 = 3 * T + T * T;
-    for (int q = tid; q < npflags; q += nth) pflags[q] = (q >= v0 && q < v1) ? -1 : 0;
-    for (int r = tid; r < N; r += nth) bv[r] = r < n ? rhs[r] : 0.0;
+    const int b0 = 2 * T, v1 = 3 * T + T * T;   // [bcnt | ver]
+    for (int q = tid; q < npflags; q += nth) pflags[q] = (q >= b0 && q < v1) ? -1 : 0;
+    for (int r = n + tid; r < N; r += nth) bv[r] = 0.0;
     if (n < N) {
         const long pad = (long)(N - n) * N + (long)n * (N - n);   // rows >= n, then columns >= n of rows < n
         for (long e = tid; e < pad; e += nth) {
@@ -1914,31 +1922,43 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
     return chol_bwd_launch(ctx, ctx->stream, w, n, sigma, dinfo, xbase, xnext);
 }
 
-// The streamed solve's prep on the context stream (after rhs is formed): returns where the J^T J
-// writes (P, ldp, T 64-tiles) and the tile version words it publishes
-int launch_chol_stream_prep(pnol_ctx* ctx, int n, const double* rhs, int* dinfo, double** P, long* ldp, int* T,
-                            int** ver) {
-    if (n <= NB || !rhs || !dinfo) return PNOL_ERR_ARG;
+// The streamed solve's workspace (allocated before anything of the trip is queued)
+int launch_chol_stream_ws(pnol_ctx* ctx, int n, double** P, long* ldp, int* T, int** ver, int** bcnt, double** bv) {
+    if (n <= NB) return PNOL_ERR_ARG;
     CholWs w;
     PNOL_CHECK(chol_ws(ctx, n, w));
-    hipLaunchKernelGGL(k_chol_stream_prep, dim3(std::min(1024, (w.N * w.N / 8 + 255) / 256 + 1)), dim3(256), 0,
-                       ctx->stream, w.P, w.ldp, w.T, n, w.bv, rhs, w.pf, w.npf, dinfo);
     *P = w.P;
     *ldp = w.ldp;
     *T = w.T;
     *ver = w.pf + 3 * w.T;
+    *bcnt = w.pf + 2 * w.T;
+    *bv = w.bv;
+    return PNOL_OK;
+}
+
+int launch_chol_stream_prep(pnol_ctx* ctx, int n, int* dinfo) {
+    if (n <= NB || !dinfo) return PNOL_ERR_ARG;
+    CholWs w;
+    PNOL_CHECK(chol_ws(ctx, n, w));
+    const long pad = (long)(w.N - n) * w.N + (long)n * (w.N - n), work = std::max<long>(pad, w.npf);
+    hipLaunchKernelGGL(k_chol_stream_prep, dim3((unsigned)std::min<long>(1024, (work + 255) / 256)), dim3(256), 0,
+                       ctx->stream, w.P, w.ldp, w.T, n, w.bv, w.pf, w.npf, dinfo);
     return launch_check();
 }
 
-// The streamed solve proper on `st` (behind the prep): the persistent factorisation on XCD xcd
-// (xcd_cus of its CUs: the chain + xcd_cus - 1 workers),
-// consuming the J^T J's tiles as they are published, then the backward solve and the trial point
-int launch_chol_stream_solve(pnol_ctx* ctx, hipStream_t st, int n, double* sigma, int* dinfo, int xcd, int xcd_cus,
-                             const double* xbase, double* xnext) {
+// The persistent factorisation on `st` behind the prep, on XCD xcd (xcd_cus of its CUs: the
+// chain + xcd_cus - 1 workers), consuming the reduce's tiles as they are published
+int launch_chol_stream_factor(pnol_ctx* ctx, hipStream_t st, int n, int* dinfo, int xcd, int xcd_cus) {
     CholWs w;
     PNOL_CHECK(chol_ws(ctx, n, w));
-    PNOL_CHECK(chol_persist_launch(ctx, st, w, dinfo, xcd, 1, xcd_cus));
-    return chol_bwd_launch(ctx, st, w, n, sigma, dinfo, xbase, xnext);
+    return chol_persist_launch(ctx, st, w, dinfo, xcd, 1, xcd_cus);
+}
+
+// the backward solve and the trial point, on the context stream (the whole chip)
+int launch_chol_stream_bwd(pnol_ctx* ctx, int n, double* sigma, int* dinfo, const double* xbase, double* xnext) {
+    CholWs w;
+    PNOL_CHECK(chol_ws(ctx, n, w));
+    return chol_bwd_launch(ctx, ctx->stream, w, n, sigma, dinfo, xbase, xnext);
 }
 
 }  // namespace pnol

@@ -345,19 +345,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
 #endif
 }
 
-// ---- J^T J streamed into the Cholesky (launch_jtj_stream) ---------------------------------------
-// 16-byte sc1 load / store at byte offset `off` from a wave-uniform base (buffer_load / _store
-// dwordx4 ... sc1; 0x00020000: the gfx9 raw-buffer descriptor word 3, 32-bit data format)
-typedef int v4i_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ double2 ld16_sc1(const double* base, unsigned off) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
-    return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
-}
-
-__device__ __forceinline__ int xcc_id() {
-    return (int)(__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) & 15);   // HW_REG_XCC_ID
-}
-
 // ---- the m-slice summation tree ------------------------------------------------------------
 // J^T J and J^T F are summed over the residual rows in kLmSlices m-slices (slice s: rows
 // [s mS, (s + 1) mS)).  A slice's value ("leaf") is the sequential sum from 0.0 of its
@@ -385,123 +372,6 @@ __device__ __forceinline__ void tree_merge(double (&v)[kS], int (&sz)[kS]) {
 
 __device__ __forceinline__ double tree8(const double (&l)[kS]) {
     return ((l[0] + l[1]) + (l[2] + l[3])) + ((l[4] + l[5]) + (l[6] + l[7]));
-}
-
-// Persistent J^T J whose tiles feed the tile Cholesky as they complete (launch_jtj_stream).
-// Workgroups claim split-K units from words[0] in tile-column order (the 128 x 128 tiles of
-// column 0 first: the Cholesky's first steps need them; within a tile the long chunk 0 of every
-// slice first), compute them as k_syrk_tile does (syrk_unit: the same MFMA chains), and store the
-// partial write-through (sc1).  The workgroup whose unit arrives last at a tile (words[1 + t],
-// one agent-scope add per workgroup after every wave's stores drained) sums the tile's partials
-// exactly as k_syrk_reduce does -- leaf s = the sub-chunks from 0.0 in order, then tree8 -- applies
-// the Marquardt diagonal, writes the tile (the diagonal tiles also mirrored) into the Cholesky's
-// padded matrix P with sc1 stores, and publishes version 0 of the tile's 64 x 64 sub-tiles in the
-// Cholesky's words (ver, set to -1 by its prep): every Cholesky task's wait ver >= k then also
-// waits for its tile.  Hand-offs per MI355X_MICROARCH.md "Valid forms" row 1.  skip_xcd >= 0:
-// workgroups dispatched to that XCD leave at once (it runs the Cholesky).  Units are claimed
-// dynamically, so an XCD with fewer workgroups simply takes fewer units.
-template <int NW>
-__global__ __launch_bounds__(64 * NW, 2) void k_syrk_stream(const double* __restrict__ X, long ldx, int nr, int K,
-                                                        int split_k, int kfirst, int kchunk, int sub, int mS,
-                                                        long sstride, double* __restrict__ part, int nt,
-                                                        int skip_xcd, int* __restrict__ words, double lambda,
-                                                        double* __restrict__ P, long ldp, int T,
-                                                        int* __restrict__ ver, int delay) {
-    __shared__ __attribute__((aligned(16))) double lds[2][2][kTile * kPad];
-    __shared__ int item_sh, last_sh;
-    if (skip_xcd >= 0 && xcc_id() == skip_xcd) return;
-    constexpr int NT = 64 * NW;
-    const int ntiles = nt * (nt + 1) / 2, nitems = ntiles * split_k, nsl = split_k / sub;
-    const long E = (long)kTile * kTile;
-    for (;;) {
-        if (threadIdx.x == 0) item_sh = __hip_atomic_fetch_add(words, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const int q = item_sh;
-        if (q >= nitems) return;
-        // claim order: every tile's long chunk-0 units (one per slice) run `delay` tiles ahead
-        // of its short units, so the last claims of the launch are short units (a short tail)
-        // while tiles still complete in column order
-        int r, sidx;
-        {
-            const int nl = nsl, ns = split_k - nsl, D = ns > 0 ? delay : 0;
-            int qq = q;
-            if (qq < D * nl) {
-                r = qq / nl;
-                sidx = (qq % nl) * sub;
-            } else {
-                qq -= D * nl;
-                const int full = (ntiles - D) * split_k;
-                int tt, off;
-                if (qq < full) {
-                    tt = qq / split_k;
-                    off = qq % split_k;
-                    if (off < nl) {   // tile tt + D's long unit
-                        r = tt + D;
-                        sidx = off * sub;
-                        off = -1;
-                    }
-                } else {
-                    qq -= full;
-                    tt = ntiles - D + qq / ns;
-                    off = nl + qq % ns;
-                }
-                if (off >= 0) {   // tile tt's short unit b = off - nl: slice b % nl, chunk 1 + b / nl
-                    const int b = off - nl;
-                    r = tt;
-                    sidx = (b % nl) * sub + 1 + b / nl;
-                }
-            }
-        }
-        int tj = 0;
-        while (r >= nt - tj) {
-            r -= nt - tj;
-            ++tj;
-        }
-        const int ti = tj + r, t = ti * (ti + 1) / 2 + tj;
-        syrk_unit<0, kTile, NW, true>(X, ldx, nr, K, split_k, kfirst, kchunk, sub, 0, mS, sstride, part, t, sidx,
-                                      t * split_k + sidx, lds);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();   // every wave's partial stores drained (also: item_sh and lds free)
-        if (threadIdx.x == 0)
-            last_sh = __hip_atomic_fetch_add(words + 1 + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                      split_k - 1;
-        __syncthreads();
-        if (!last_sh) continue;
-        // ---- the tile's reduce (its last unit's workgroup)
-        const double scale = 1 + lambda;
-        const double* pt = part + (long)t * split_k * E;
-        for (int e = threadIdx.x; e < (int)(E / 2); e += NT) {
-            double lx[kS], ly[kS];
-#pragma unroll
-            for (int sl = 0; sl < kS; ++sl) {
-                double ax = 0.0, ay = 0.0;
-                for (int u = 0; u < sub; ++u) {
-                    const double2 v = ld16_sc1(pt + (long)(sl * sub + u) * E, (unsigned)(e * 16));
-                    ax += v.x;
-                    ay += v.y;
-                }
-                lx[sl] = ax;
-                ly[sl] = ay;
-            }
-            const int rr = (2 * e) / kTile, cc = (2 * e) % kTile;
-            const int i = ti * kTile + rr;
-            for (int h = 0; h < 2; ++h) {
-                const int j = tj * kTile + cc + h;
-                double v = h ? tree8(ly) : tree8(lx);
-                if (i >= nr || j >= nr || (ti == tj && j > i)) continue;
-                if (i == j) v = scale * v;
-                __hip_atomic_store(P + (long)i * ldp + j, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (ti == tj && j < i) __hip_atomic_store(P + (long)j * ldp + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x < 4) {   // the 64 x 64 sub-tiles (2 ti + a, 2 tj + b) on or below the diagonal
-            const int a = threadIdx.x >> 1, b = threadIdx.x & 1;
-            const int I = 2 * ti + a, J = 2 * tj + b;
-            if (I < T && J < T && J <= I) __hip_atomic_store(ver + (long)I * T + J, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 // Leaves of slices [s0, s1) -- leaf s = sum over u < sub of
@@ -607,6 +477,28 @@ __global__ void k_syrk_unpack(const double* __restrict__ packed, int ntiles, int
 // jp / rhs (nullable): one more row of blocks (blockIdx.y == ntiles) forms rhs = the slice
 // tree of the 8 -J^T F slice partials jp[s * n + e], exactly as k_tree_nodes over all slices does
 // (leaf = 0.0 + partial, then tree8): the tree rides in this launch instead of its own.
+// the reduce's value of element pair q of a strip: per slice the sub-chunk partials from 0.0
+// in order, then tree8 (k_syrk_reduce and k_syrk_reduce_p: the same sums)
+template <int SUB>
+__device__ __forceinline__ void reduce_pair(const double* __restrict__ p, int q, int sub, long E, double& vx,
+                                            double& vy) {
+    double lx[kS], ly[kS];
+#pragma unroll
+    for (int s = 0; s < kS; ++s) {
+        double ax = 0.0, ay = 0.0;
+#pragma unroll
+        for (int u = 0; u < (SUB > 0 ? SUB : sub); ++u) {
+            const double2 w = reinterpret_cast<const double2*>(p + (long)(s * sub + u) * E)[q];
+            ax += w.x;
+            ay += w.y;
+        }
+        lx[s] = ax;
+        ly[s] = ay;
+    }
+    vx = tree8(lx);
+    vy = tree8(ly);
+}
+
 template <int SUB, int SR = 32>
 __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ part, int ntiles, int sub_rt, int n,
                                                      double lambda, double* __restrict__ A, long lda,
@@ -635,20 +527,8 @@ __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ 
 #pragma unroll 2
     for (int q = threadIdx.x; q < SR * kTile / 2; q += 256) {
         const int r = (2 * q) / kTile, c = (2 * q) % kTile;
-        double lx[kS], ly[kS];
-#pragma unroll
-        for (int s = 0; s < kS; ++s) {
-            double ax = 0.0, ay = 0.0;
-#pragma unroll
-            for (int u = 0; u < (SUB > 0 ? SUB : sub); ++u) {
-                const double2 w = reinterpret_cast<const double2*>(p + (long)(s * sub + u) * E)[q];
-                ax += w.x;
-                ay += w.y;
-            }
-            lx[s] = ax;
-            ly[s] = ay;
-        }
-        const double vx = tree8(lx), vy = tree8(ly);
+        double vx, vy;
+        reduce_pair<SUB>(p, q, sub, E, vx, vy);
         st[r][c] = vx;
         st[r][c + 1] = vy;
         const int i = ti * kTile + r0 + r;
@@ -670,6 +550,97 @@ __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ 
         const int c = q / SR, r = q % SR;                  // consecutive threads: consecutive i
         const int i = ti * kTile + r0 + r, j = tj * kTile + c;
         if (i < n && j < n && j < i) A[(long)j * lda + i] = st[r][c];
+    }
+}
+
+// k_syrk_reduce into the tile Cholesky's padded matrix P, streamed to it (the streamed damped
+// solve, launch_fd_normal_solve_stream): blockIdx.y = 0 is the -J^T F slice tree (written to rhs
+// and to the Cholesky's b; its last workgroup then publishes b, the block-row words bcnt = 0),
+// blockIdx.y = 1 + c the c-th 128 x 128 tile in column order (the Cholesky's first steps need the
+// first columns).  Every value is k_syrk_reduce's (reduce_pair); the diagonal tiles are mirrored
+// (the Cholesky reads whole diagonal 64 x 64 tiles), the upper off-diagonal tiles are not
+// written.  All stores sc1; each workgroup adds to its tile's counter after its stores drained
+// and the last of the tile's strips publishes version 0 of its 64 x 64 sub-tiles (the Cholesky
+// waits for version >= k): MI355X_MICROARCH.md "Valid forms" row 1.  Bitwise the A of
+// k_syrk_reduce (lower part, Marquardt diagonal) and its rhs.
+template <int SUB, int SR>
+__global__ __launch_bounds__(256) void k_syrk_reduce_p(const double* __restrict__ part, int ntiles, int sub_rt, int n,
+                                                       double lambda, double* __restrict__ P, long ldp, int T,
+                                                       int* __restrict__ ver, int* __restrict__ bcnt,
+                                                       int* __restrict__ cnt, const double* __restrict__ jp,
+                                                       double* __restrict__ rhs, double* __restrict__ bv) {
+    __shared__ double st[SR][kTile + 1];
+    __shared__ int last_sh;
+    const int nstrip = gridDim.x;
+    if (blockIdx.y == 0) {   // the -J^T F tree: k_syrk_reduce's fold row
+        for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+            double l[kS];
+#pragma unroll
+            for (int s = 0; s < kS; ++s) l[s] = 0.0 + jp[(long)s * n + e];
+            const double v = tree8(l);
+            rhs[e] = v;
+            __hip_atomic_store(bv + e, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            last_sh = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nstrip - 1;
+        __syncthreads();
+        if (last_sh)
+            for (int i = threadIdx.x; i < T; i += blockDim.x)
+                __hip_atomic_store(bcnt + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    const int sub = SUB > 0 ? SUB : sub_rt;
+    // tile c of the column order -> (ti, tj) and its row-major index t (the partials' order)
+    const int nt = (int)((__builtin_sqrt(8.0 * ntiles + 1.0) - 1.0) / 2.0 + 0.5);
+    int r = (int)blockIdx.y - 1, tj = 0;
+    while (r >= nt - tj) {
+        r -= nt - tj;
+        ++tj;
+    }
+    const int ti = tj + r, t = ti * (ti + 1) / 2 + tj;
+    const double scale = 1 + lambda;
+    const int r0 = blockIdx.x * SR;
+    const long E = kTile * kTile;
+    const double* p = part + ((long)t * kS * sub) * E + (long)r0 * kTile;
+    const bool dg = ti == tj;
+#pragma unroll 2
+    for (int q = threadIdx.x; q < SR * kTile / 2; q += 256) {
+        const int rr = (2 * q) / kTile, c = (2 * q) % kTile;
+        double vx, vy;
+        reduce_pair<SUB>(p, q, sub, E, vx, vy);
+        if (dg) {
+            st[rr][c] = vx;
+            st[rr][c + 1] = vy;
+        }
+        const int i = ti * kTile + r0 + rr;
+        for (int h = 0; h < 2; ++h) {
+            const int j = tj * kTile + c + h;
+            const double val = h ? vy : vx;
+            if (i >= n || j >= n || j > i) continue;
+            __hip_atomic_store(P + (long)i * ldp + j, i == j ? scale * val : val, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (dg) {   // the mirror inside the diagonal tile
+        __syncthreads();
+        for (int q = threadIdx.x; q < SR * kTile; q += 256) {
+            const int c = q / SR, rr = q % SR;
+            const int i = ti * kTile + r0 + rr, j = tj * kTile + c;
+            if (i < n && j < n && j < i)
+                __hip_atomic_store(P + (long)j * ldp + i, st[rr][c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last_sh = __hip_atomic_fetch_add(cnt + 1 + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nstrip - 1;
+    __syncthreads();
+    if (last_sh && threadIdx.x < 4) {   // the 64 x 64 sub-tiles (2 ti + a, 2 tj + b) on or below the diagonal
+        const int a = threadIdx.x >> 1, b = threadIdx.x & 1;
+        const int I = 2 * ti + a, J = 2 * tj + b;
+        if (I < T && J < T && J <= I) __hip_atomic_store(ver + (long)I * T + J, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -835,36 +806,8 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     return PNOL_OK;
 }
 
-// J^T J streamed into the Cholesky's padded matrix P (ld ldp, T 64-tiles; its words ver at -1):
-// k_syrk_stream on `stream`, skip_xcd's workgroups leaving at once.  The split-K partials stay in
-// "syrk_part" (launch_jtj_from_partials forms A from them for the LU fallback).
-int launch_jtj_stream(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldjt, int m, int n, double lambda,
-                      double* P, long ldp, int T, int* ver, int skip_xcd) {
-    if (!JT || !P || !ver || m <= 0 || n <= PNOL_SEQ_MAX || ldjt < m || ldp < (long)T * 64 || T * 64 < n)
-        return PNOL_ERR_ARG;
-    const int nt = (n + kTile - 1) / kTile;
-    const int ntiles = nt * (nt + 1) / 2;
-    const SliceCfg sc = slice_cfg(m, ntiles);
-    const int split = kS * sc.sub;
-    void *part = nullptr, *words = nullptr;
-    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * split * kTile * kTile, &part));
-    PNOL_CHECK(ws_get(ctx, "syrk_stream_words", sizeof(int) * (size_t)(1 + ntiles), &words));
-    PNOL_HIP(hipMemsetAsync(words, 0, sizeof(int) * (size_t)(1 + ntiles), stream));
-    LaunchTimer tm(ctx, "syrk");
-    const int grid = 2 * std::max(ctx->num_cu, 1);   // persistent: two workgroups per CU
-    // the long units' lead over the short ones, in tiles: about one round of the resident
-    // workgroups (PNOL_SYRK_STREAM_DELAY overrides; read per call)
-    const char* ed = std::getenv("PNOL_SYRK_STREAM_DELAY");
-    const int resident = skip_xcd >= 0 ? grid * 7 / 8 : grid;
-    const int delay = std::max(0, std::min(ntiles, ed ? std::atoi(ed) : resident / kS));
-    hipExtLaunchKernelGGL((k_syrk_stream<8>), dim3(grid), dim3(512), 0, stream, tm.start(), tm.stop(), 0, JT,
-                          (long)ldjt, n, m, split, sc.kfirst, sc.kchunk, sc.sub, sc.mS, (long)sc.mS, (double*)part, nt,
-                          skip_xcd, (int*)words, lambda, P, ldp, T, ver, delay);
-    return launch_check();
-}
-
-// A (lower triangle + mirror, the Marquardt diagonal) from the partials of the last launch_jtj_stream
-// (the same reduce as launch_jtj, so the same A)
+// A (lower triangle + mirror, the Marquardt diagonal) from the partials of the last streamed trip
+// (launch_fd_normal_solve_stream; the same reduce as launch_jtj, so the same A)
 int launch_jtj_from_partials(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda) {
     const int nt = (n + kTile - 1) / kTile;
     const int ntiles = nt * (nt + 1) / 2;
@@ -979,42 +922,70 @@ static int split_streams(pnol_ctx* ctx, int xcd) {
     return PNOL_OK;
 }
 
-// One LM trip's linear algebra with the damped solve streamed behind the J^T J (single process,
-// n > PNOL_SEQ_MAX, LevenbergMarquardt.cpp:59-83): FD Jacobian, rhs = -J^T F, the Cholesky's
-// prep, then at once k_syrk_stream on the context stream (every XCD but xcd) and the persistent
-// Cholesky + backward solve on the aux stream (XCD xcd only), each 64 x 64 tile of A factored
-// as soon as the J^T J publishes it.  A is not formed (launch_jtj_from_partials forms it for the
-// LU fallback); JT, rhs, sigma and xnext are bitwise those of launch_fd_jtj + launch_chol_solve.
+// One LM trip's linear algebra with the damped solve started under the J^T J's reduce (single
+// process, n > PNOL_SEQ_MAX, LevenbergMarquardt.cpp:59-83): the FD Jacobian, the split-K J^T J
+// partials and the -J^T F slice partials on the whole chip, then at once the reduce on every XCD
+// but xcd (k_syrk_reduce_p: the tiles in column order straight into the Cholesky's padded
+// matrix, b = -J^T F first) and the persistent Cholesky on XCD xcd, which factors each 64 x 64
+// tile as soon as the reduce has published it; the backward solve (and xnext = x + sigma) on the
+// whole chip after both.  The reduce's 2 x 16-byte-per-element HBM stream and the Cholesky's
+// latency-bound chain share the chip instead of following each other, and the copy of A into
+// the Cholesky's matrix is gone.  A is not formed (launch_jtj_from_partials forms it for the LU
+// fallback).  JT, rhs, sigma and xnext are bitwise those of launch_fd_jtj + launch_chol_solve.
 int launch_fd_normal_solve_stream(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0,
                                   int compute_f0, double* JT, int ldjt, double lambda, double* rhs, double* sigma,
                                   int* dinfo, double* xnext, int xcd) {
     if (!o || !x || !h || !F0 || !JT || !rhs || !sigma || !dinfo || !xnext || ldjt < o->m) return PNOL_ERR_ARG;
     const int n = o->n, m = o->m;
     if (n <= PNOL_SEQ_MAX || xcd < 0 || xcd > 7) return PNOL_ERR_ARG;
-    PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
-    PNOL_CHECK(launch_jtr(ctx, JT, ldjt, m, n, F0, rhs));
-    double* P = nullptr;
+    const int nt = (n + kTile - 1) / kTile;
+    const int ntiles = nt * (nt + 1) / 2;
+    const SliceCfg sc = slice_cfg(m, ntiles);
+    // every workspace first: a (re)allocation frees, and a free waits for the device
+    void *part = nullptr, *jp = nullptr, *cnt = nullptr;
+    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * kS * sc.sub * kTile * kTile, &part));
+    PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
+    PNOL_CHECK(ws_get(ctx, "reduce_p_words", sizeof(int) * (size_t)(1 + ntiles), &cnt));
+    double *P = nullptr, *bv = nullptr;
     long ldp = 0;
     int T = 0;
-    int* ver = nullptr;
-    PNOL_CHECK(launch_chol_stream_prep(ctx, n, rhs, dinfo, &P, &ldp, &T, &ver));
+    int *ver = nullptr, *bcnt = nullptr;
+    PNOL_CHECK(launch_chol_stream_ws(ctx, n, &P, &ldp, &T, &ver, &bcnt, &bv));
+    PNOL_CHECK(split_streams(ctx, xcd));
     while (ctx->aux_events.size() < 3) {
         hipEvent_t e;
         PNOL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ctx->aux_events.push_back(e);
     }
+
+    PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
+    syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
+                  syrk_t64(false));
+    PNOL_CHECK(launch_check());
+    PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F0));
+    PNOL_CHECK(launch_chol_stream_prep(ctx, n, dinfo));
+    PNOL_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)(1 + ntiles), ctx->stream));
     PNOL_HIP(hipEventRecord(ctx->aux_events[0], ctx->stream));
-    PNOL_CHECK(split_streams(ctx, xcd));
-    hipStream_t sj = ctx->split_streams[0], sc = ctx->split_streams[1];
-    PNOL_HIP(hipStreamWaitEvent(sj, ctx->aux_events[0], 0));
-    PNOL_HIP(hipStreamWaitEvent(sc, ctx->aux_events[0], 0));
-    PNOL_CHECK(launch_chol_stream_solve(ctx, sc, n, sigma, dinfo, xcd, std::max(ctx->num_cu, 8) / 8 - 1, x, xnext));
-    PNOL_CHECK(launch_jtj_stream(ctx, sj, JT, ldjt, m, n, lambda, P, ldp, T, ver, xcd));
-    PNOL_HIP(hipEventRecord(ctx->aux_events[1], sc));
+    hipStream_t sr = ctx->split_streams[0], sc2 = ctx->split_streams[1];
+    PNOL_HIP(hipStreamWaitEvent(sr, ctx->aux_events[0], 0));
+    PNOL_HIP(hipStreamWaitEvent(sc2, ctx->aux_events[0], 0));
+    {
+        ScopedTimer tm(ctx, "syrk_reduce", sr);
+        const dim3 grid(kTile / 16, 1 + ntiles);   // 16-row strips (launch_reduce's)
+        if (sc.sub == 2)
+            hipLaunchKernelGGL((k_syrk_reduce_p<2, 16>), grid, dim3(256), 0, sr, (const double*)part, ntiles, sc.sub, n,
+                               lambda, P, ldp, T, ver, bcnt, (int*)cnt, (const double*)jp, rhs, bv);
+        else
+            hipLaunchKernelGGL((k_syrk_reduce_p<0, 16>), grid, dim3(256), 0, sr, (const double*)part, ntiles, sc.sub, n,
+                               lambda, P, ldp, T, ver, bcnt, (int*)cnt, (const double*)jp, rhs, bv);
+        PNOL_CHECK(launch_check());
+    }
+    PNOL_CHECK(launch_chol_stream_factor(ctx, sc2, n, dinfo, xcd, std::max(ctx->num_cu, 8) / 8 - 1));
+    PNOL_HIP(hipEventRecord(ctx->aux_events[1], sc2));
+    PNOL_HIP(hipEventRecord(ctx->aux_events[2], sr));
     PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->aux_events[1], 0));
-    PNOL_HIP(hipEventRecord(ctx->aux_events[2], sj));
     PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->aux_events[2], 0));
-    return PNOL_OK;
+    return launch_chol_stream_bwd(ctx, n, sigma, dinfo, x, xnext);
 }
 
 // J^T J with the 128 x 128 tiles split over the communicator's ranks (contiguous ranges of

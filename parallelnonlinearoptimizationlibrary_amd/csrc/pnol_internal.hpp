@@ -190,10 +190,6 @@ int launch_gather_rows(pnol_ctx* ctx, const double* D, int ldd, const int* ridx,
 // rhs (nullable): also rhs = -J^T F (bitwise launch_jtr), its slice tree in the reduce launch
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                double* jtj_diag, const double* F = nullptr, double* rhs = nullptr);
-// J^T J streamed into the tile Cholesky (syrk.hip): tiles reduced into its padded P as they
-// complete, each publishing its sub-tiles' Cholesky version words; skip_xcd's workgroups leave
-int launch_jtj_stream(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldjt, int m, int n, double lambda,
-                      double* P, long ldp, int T, int* ver, int skip_xcd);
 int launch_fd_normal_solve_stream(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0,
                                   int compute_f0, double* JT, int ldjt, double lambda, double* rhs, double* sigma,
                                   int* dinfo, double* xnext, int xcd);
@@ -214,13 +210,16 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
                         int variant, const double* xbase = nullptr, double* xnext = nullptr);
 int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n, int method,
                  int* info);
-// The streamed damped solve (chol.hip): the prep on the context stream after rhs is formed
-// (returns where the J^T J writes and the version words it publishes), then the persistent
-// factorisation on XCD xcd + the backward solve (and xnext = xbase + sigma) on stream st
-int launch_chol_stream_prep(pnol_ctx* ctx, int n, const double* rhs, int* dinfo, double** P, long* ldp, int* T,
-                            int** ver);
-int launch_chol_stream_solve(pnol_ctx* ctx, hipStream_t st, int n, double* sigma, int* dinfo, int xcd, int xcd_cus,
-                             const double* xbase, double* xnext);
+// The streamed damped solve (chol.hip, used by launch_fd_normal_solve_stream): the tile
+// Cholesky's workspace for n -- its padded matrix P (ld ldp, T 64-tiles), the tile version
+// words, the block-row words of b and b itself; the prep on the context stream (tile versions
+// and b's block-row words at -1: not yet published; b's padding, P's padding, info = 0); the
+// persistent factorisation on stream st, confined to XCD xcd (xcd_cus of its CUs); the
+// backward solve (and xnext = xbase + sigma) on the context stream
+int launch_chol_stream_ws(pnol_ctx* ctx, int n, double** P, long* ldp, int* T, int** ver, int** bcnt, double** bv);
+int launch_chol_stream_prep(pnol_ctx* ctx, int n, int* dinfo);
+int launch_chol_stream_factor(pnol_ctx* ctx, hipStream_t st, int n, int* dinfo, int xcd, int xcd_cus);
+int launch_chol_stream_bwd(pnol_ctx* ctx, int n, double* sigma, int* dinfo, const double* xbase, double* xnext);
 
 int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
 // rows [r0, r1) only (multiples of 64 but r1 = m; r1 < 0: all): a row-sharded LevMarqMPI rank
