@@ -285,19 +285,6 @@ int pnol_fd_jtj_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* 
  * Bitwise the same JT, A and rhs as the separate calls. */
 int pnol_fd_normal_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0, int compute_f0,
                      double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, double* rhs);
-/* One LevMarq trip's linear algebra with the damped solve streamed behind the J^T J
- * (LevenbergMarquardt.cpp:55-83; n > 128, single process): the FD Jacobian, rhs = -(J^T F0),
- * then sigma = A^{-1} rhs by the tile Cholesky, each 64 x 64 tile factored as soon as the J^T J
- * has summed it (the J^T J on every XCD but `xcd`, the Cholesky on XCD `xcd`, 0..7), and
- * xnext = x + sigma.  A itself is not formed: *dinfo != 0 (a non-positive pivot) asks for
- * pnol_lm_stream_normal_d + the LU (pnol_solve_d method 2).  JT, rhs, sigma, xnext and *dinfo
- * are bitwise those of pnol_fd_normal_d + pnol_solve_step_d. */
-int pnol_lm_trip_stream_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0,
-                          int compute_f0, double* JT, int ldjt, double lambda, double* rhs, double* sigma, int* dinfo,
-                          double* xnext, int xcd);
-/* A = J^T J with the Marquardt diagonal from the last pnol_lm_trip_stream_d's partial sums
- * (m, n, lambda as passed to it): bitwise pnol_fd_normal_d's A. */
-int pnol_lm_stream_normal_d(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda);
 /* The FD Jacobian rows of a tile list (columns [start[t], start[t] + count[t]), count <=
  * PNOL_FD_TILE), column c written to JT + c * ldjt; one base-chain pass for all tiles. */
 int pnol_fd_jacobian_tiles_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, const int* start,

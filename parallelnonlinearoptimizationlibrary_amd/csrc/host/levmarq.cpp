@@ -199,12 +199,6 @@ class LMAsync {
             for (int v : all)
                 if (v != ctx->lm_fd_mode) throw std::runtime_error("LevMarqMPI: ranks disagree on PNOL_LM_FD");
         }
-        // PNOL_LM_STREAM = 1 (single process; read once per solve): the damped solve streamed
-        // behind the J^T J (pnol_lm_trip_stream_d), the Cholesky on XCD 0
-        if (!sliced) {
-            const char* e = std::getenv("PNOL_LM_STREAM");
-            stream_ = e && std::atoi(e) != 0;
-        }
         JT_.reset(ctx, jt);
         A_.reset(ctx, (size_t)n * lda_);
         rhs_.reset(ctx, n);
@@ -244,15 +238,6 @@ class LMAsync {
             check(pnol_lm_normal_mpi_d(ctx_, JT_.get(), m_, n_, lambda, F(s), A_.get(), lda_, rhs_.get(),
                                        nullptr),
                   "normal equations");
-        } else if (stream_) {
-            // FD Jacobian, -J^T F, then the J^T J and the Cholesky side by side; the solve's
-            // last launch forms the trial point
-            lambda_[s] = lambda;
-            check(pnol_lm_trip_stream_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 3 : 1, JT_.get(), ldjt_, lambda,
-                                        rhs_.get(), sig(s), info(s), x_[s ^ 1].get(), 0),
-                  "lm trip");
-            finish(s, false);
-            return;
         } else {
             // FD Jacobian, A and -J^T F in one queue (the GEMV in the J^T J's tail)
             check(pnol_fd_normal_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 3 : 1, JT_.get(), ldjt_, lambda,
@@ -278,7 +263,6 @@ class LMAsync {
     // the reference-order LU for a trip whose Cholesky reported a non-positive pivot (A intact)
     void redo_lu(int s) {
         check(pnol_ctx_synchronize(ctx_), "sync");
-        if (stream_) check(pnol_lm_stream_normal_d(ctx_, m_, n_, lambda_[s], A_.get(), lda_), "normal equations");
         int info = 0;
         check(pnol_solve_d(ctx_, A_.get(), lda_, rhs_.get(), sig(s), n_, 2, &info), "solve");
         finish(s);
@@ -290,8 +274,6 @@ class LMAsync {
     pnol_dobj* d_;
     int n_, m_, ldjt_, lda_;
     bool sliced_;
-    bool stream_ = false;
-    double lambda_[2] = {0, 0};   // the lambda of trip s (the streamed form's LU fallback forms A)
     int np_ = 0, mp_ = 0;
     DevVec JT_, A_, rhs_, h_, x_[2], trip_[2];
     void* pin_[2] = {nullptr, nullptr};
@@ -344,7 +326,7 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool s
         dev.enqueue(s, lambda, ckpt);
         dev.wait(s);
         if (dev.info_h(s) != 0) {
-            if (std::getenv("PNOL_LM_DEBUG"))
+            if (std::getenv("PNOL_LM_DEBUG"))   // which trips fell back (a timed-out chain: status <= -7)
                 std::cerr << "[pnol] LM trip " << iter << ": solve status " << dev.info_h(s) << ", LU redo" << std::endl;
             dev.redo_lu(s);
         }

@@ -33,10 +33,6 @@ constexpr int kSub = NB * kPad;      // doubles per substage
 constexpr int kStage = 4 * kSub;     // one 64 x 64 tile as four substages
 constexpr int kSpin = 1 << 24;       // ~1 s of polling
 constexpr int kInfoTimeout = -7;
-// the persistent form's wait sites (the status names the wait that timed out): the chain's
-// tile-0 / tile waits, a panel task's tile / W waits, an update task's publish / lock / panel waits
-constexpr int kToChain0 = -11, kToChain = -12, kToPanelTile = -13, kToPanelW = -14, kToUpdProd = -15,
-              kToUpdLock = -16, kToUpdPanels = -17;
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
@@ -112,22 +108,6 @@ __device__ __forceinline__ void stage_tile(double* __restrict__ dst, const doubl
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = src[q];
     }
-    double2* d = reinterpret_cast<double2*>(dst + sub * kSub + row * kPad);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) d[q] = v[q];
-}
-
-// stage_tile in two halves: the sc1 loads into registers, then the LDS stores (so the next
-// tile's loads fly while the current one is used)
-__device__ __forceinline__ void tile_load_sc1(double2 (&v)[8], const double* __restrict__ P, long ldp, int r0, int c0) {
-    const int t = threadIdx.x, row = t >> 2, sub = t & 3;
-    const double* base = P + (long)r0 * ldp + c0;   // wave-uniform
-    const unsigned off = (unsigned)((row * ldp + sub * 16) * 8);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = ld16_sc1(base, off + 16 * q);
-}
-__device__ __forceinline__ void tile_put(double* __restrict__ dst, const double2 (&v)[8]) {
-    const int t = threadIdx.x, row = t >> 2, sub = t & 3;
     double2* d = reinterpret_cast<double2*>(dst + sub * kSub + row * kPad);
 #pragma unroll
     for (int q = 0; q < 8; ++q) d[q] = v[q];
@@ -218,15 +198,14 @@ __device__ __forceinline__ void acc_to_rows(const d4 (&acc)[2][2], double* __res
             for (int r = 0; r < 4; ++r) S[acc_row(wr, mi, lane, r) * (NB + 1) + acc_col(wc, ni, lane)] = acc[mi][ni][r];
 }
 
-// a timed-out wait stores `code` (kInfoTimeout or a site code below it) into info
-__device__ __forceinline__ bool spin_ge(const int* f, int target, int* info, int code = kInfoTimeout) {
+__device__ __forceinline__ bool spin_ge(const int* f, int target, int* info) {
     int it = 0;
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
         if ((++it & 63) == 0) {
             if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
             if (it > kSpin) {
-                atomicExch(info, code);
+                atomicExch(info, kInfoTimeout);
                 return false;
             }
         }
@@ -237,8 +216,7 @@ __device__ __forceinline__ bool spin_ge(const int* f, int target, int* info, int
 // Every *f[q] >= tg[q]: all N words are loaded in each round (one memory round trip for the set
 // instead of one per word when they are already there); the same cap and info checks.
 template <int N>
-__device__ __forceinline__ bool spin_all(const int* const (&f)[N], const int (&tg)[N], int* info,
-                                         int code = kInfoTimeout) {
+__device__ __forceinline__ bool spin_all(const int* const (&f)[N], const int (&tg)[N], int* info) {
     int it = 0;
     for (;;) {
         int v[N];
@@ -252,7 +230,7 @@ __device__ __forceinline__ bool spin_all(const int* const (&f)[N], const int (&t
         if ((++it & 63) == 0) {
             if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
             if (it > kSpin) {
-                atomicExch(info, code);
+                atomicExch(info, kInfoTimeout);
                 return false;
             }
         }
@@ -1302,12 +1280,11 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
 // consumer's lane 0 polls it with sc1 loads before a barrier (MI355X_MICROARCH.md "Valid forms",
 // row 1; one workgroup per CU: __launch_bounds__(256, 1) and the register count).  Every tile, panel and b update is the same arithmetic in the same order as in
 // the per-step launches, so the result is bitwise method 4's.
-// [wdone T][lcnt T][bcnt T][ver T^2][task counter][role word][tile locks T^2 (the streamed form)]
 struct PersistWords {
-    int *wdone, *lcnt, *bcnt, *ver, *counter, *lock;
+    int *wdone, *lcnt, *bcnt, *ver, *counter;
 };
 __device__ __forceinline__ PersistWords persist_words(int* f, int T) {
-    return {f, f + T, f + 2 * T, f + 3 * T, f + 3 * T + T * T, f + 3 * T + T * T + 2};
+    return {f, f + T, f + 2 * T, f + 3 * T, f + 3 * T + T * T};
 }
 
 // publish `v` into *w after every wave's (sc1) stores of this workgroup have completed
@@ -1320,7 +1297,7 @@ __device__ __forceinline__ void publish(int* w, int v) {
 __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P, double* __restrict__ Lm, long ldp,
                                                       int T, double* __restrict__ W, double* __restrict__ bv,
                                                       double* __restrict__ zv, int* __restrict__ flags, int ntasks,
-                                                      int* __restrict__ info, int lookahead, int xcd, int smode) {
+                                                      int* __restrict__ info, int lookahead) {
     __shared__ __attribute__((aligned(16))) double smem[2 * kStage];   // 73.7 KB
     // the chain's look-ahead areas (EarlyNext / late_prepare): 75.8 KB
     __shared__ __attribute__((aligned(16))) double pfx[kStage];
@@ -1330,39 +1307,23 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
     __shared__ double zsh[NB];
     __shared__ int cnt[6];
     __shared__ int ew[4];
-    __shared__ int task_sh, ok_sh, role_sh;
+    __shared__ int task_sh, ok_sh;
     const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6), wr = wave >> 1, wc = wave & 1;
     const PersistWords pw = persist_words(flags, T);
     double* X = smem;
     double* Y = smem + kStage;
-    // xcd >= 0: the factorisation stays on that XCD (its workgroups share one L2): workgroups
-    // dispatched to other XCDs leave at once, and the roles go by arrival -- the first to claim
-    // the role word runs the chain, the rest are workers (the grid is dealt round-robin over the
-    // XCDs, so the XCD's share of it is resident, one workgroup per CU)
-    if (xcd >= 0) {
-        if (t == 0) {
-            const int x = (int)(__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) & 15);   // HW_REG_XCC_ID
-            role_sh = x == xcd ? atomicAdd(pw.counter + 1, 1) : -1;
-        }
-        __syncthreads();
-        if (role_sh < 0) return;
-    }
-    const int role = xcd >= 0 ? role_sh : (int)blockIdx.x;
 
-    if (role == 0) {   // ---------------- the diagonal chain
+    if (blockIdx.x == 0) {   // ---------------- the diagonal chain
         const EarlyLds E{pfx, pll, pfc, ew};
         if (t < 4) ew[t] = 0;
-        // smode (the streamed solve): no prep launch factored tile 0 -- the chain starts at d = 0,
-        // once the J^T J has published the tile (its version word leaves -1)
-        for (int d = smode ? 0 : 1; d < T; ++d) {
+        for (int d = 1; d < T; ++d) {
             const int k = d - 1;
 #ifdef PNOL_CHOL_TIMELINE
             const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime(), ck0 = __builtin_amdgcn_s_memtime();
 #endif
             if (t == 0) {
                 const bool ok = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-                                (d == 0 ? spin_ge(pw.ver, 0, info, kToChain0)
-                                        : spin_all<2>({pw.ver + d * T + k, pw.ver + d * T + d}, {k, k}, info, kToChain));
+                                spin_all<2>({pw.ver + d * T + k, pw.ver + d * T + d}, {k, k}, info);
                 ok_sh = ok;
             }
             __syncthreads();
@@ -1374,18 +1335,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
 #ifdef PNOL_CHOL_TIMELINE
             if (t == 0 && k + 1 < 64) g_chol_clk[8 * (k + 1) + 6] = pre ? 1 : 0;
 #endif
-            if (d == 0) {   // tile 0 as published (sc1 loads; the padding written by the prep)
-                const int row = t >> 2, c0 = (t & 3) * 16;
-                double v[16];
-#pragma unroll
-                for (int q = 0; q < 16; ++q) v[q] = ldg<true>(P + (long)row * ldp + c0 + q);
-#pragma unroll
-                for (int q = 0; q < 16; ++q) diag_put(L, row, c0 + q, v[q]);
-            } else if (pre) {
-                late_prepare(E, Y, L, wave, lane);
-            } else {   // W_{d-1} stays in Y after the chain's own factor
-                diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane, d > 1 || smode);
-            }
+            if (pre) late_prepare(E, Y, L, wave, lane);
+            else diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane, d > 1);
             if (t < 6) cnt[t] = 0;   // every read of cnt / ew above is behind a barrier inside
             if (t < 4) ew[t] = 0;    // either prepare
             __syncthreads();
@@ -1430,13 +1381,12 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
 #endif
             // A_ik through column k-1, b_k complete and b_i's earlier updates: usually long
             // before W_k, so A_ik is staged while the workgroup waits for the diagonal chain
-            if (t == 0)
-                ok_sh = spin_all<3>({pw.ver + i * T + k, pw.bcnt + k, pw.bcnt + i}, {k, k, k}, info, kToPanelTile);
+            if (t == 0) ok_sh = spin_all<3>({pw.ver + i * T + k, pw.bcnt + k, pw.bcnt + i}, {k, k, k}, info);
             __syncthreads();
             if (!ok_sh) return;
             stage_tile<true>(X, P, ldp, i0, k0);
             if (t == 0) {   // W_k (tile 0 comes from the prep launch)
-                ok_sh = (k == 0 && !smode) || spin_ge(pw.wdone + k, 1, info, kToPanelW);
+                ok_sh = k == 0 || spin_ge(pw.wdone + k, 1, info);
 #ifdef PNOL_CHOL_TIMELINE
                 if (i == k + 2) PNOL_CRIT(k, 2)
 #endif
@@ -1491,103 +1441,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         const bool crit = i == k + 2 && j == k + 1;
         if (crit) PNOL_CRIT(k, 4)
 #endif
-        if (smode) {
-            // The streamed form: the J^T J publishes the tiles in its own (column) order, so a
-            // task must not hold its worker waiting for an unpublished tile.  The tile's updates
-            // are applied under its lock by whichever task gets there, all pending steps at once:
-            // a task that finds the tile unpublished leaves step k to the tile's next task; the
-            // tile's last task (step min(i, j) - 1, the one its consumers wait for) waits for it.
-            // A task that finds the tile already past step k has nothing to do.  The steps are
-            // the same MFMA sequence on one accumulator as the one-task-per-step form, so the
-            // tile's bits are unchanged.
-            // (the diagonal tile's step j - 1 is the chain's own, inside its prepare)
-            const bool last = k == j - 1 - (i == j ? 1 : 0);
-            if (t == 0) {
-                int ok = 1, v = __hip_atomic_load(pw.ver + i * T + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (v < 0 && last) {
-                    ok = spin_ge(pw.ver + i * T + j, 0, info, kToUpdProd);
-                    v = 0;
-                }
-                if (ok && v >= 0 && v <= k) {   // the lock, then the version again under it
-                    int it = 0;
-                    while (atomicCAS(pw.lock + i * T + j, 0, 1) != 0) {
-                        __builtin_amdgcn_s_sleep(1);
-                        if ((++it & 63) == 0 &&
-                            (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 || it > kSpin)) {
-                            if (it > kSpin) atomicExch(info, kToUpdLock);
-                            ok = 0;
-                            break;
-                        }
-                    }
-                    if (ok) {
-                        v = __hip_atomic_load(pw.ver + i * T + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (v > k) {   // applied while this task waited for the lock
-                            __hip_atomic_store(pw.lock + i * T + j, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            v = -2;
-                        }
-                    }
-                } else if (ok) {
-                    v = -2;   // nothing to do: unpublished (not the last step) or already applied
-                }
-                ok_sh = ok;
-                task_sh = v;
-            }
-            __syncthreads();
-            const int v0 = task_sh;
-            const bool go = ok_sh;
-            __syncthreads();
-            if (!go) return;
-            if (v0 < 0) continue;
-            // steps v0 .. k: panel words polled only when the last seen values fall short; the
-            // next step's panel tiles are loaded while the current step's MFMAs run
-            d4 acc[2][2];
-            acc_load<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
-            double2 ra[8], rb[8];
-            int seen = -1;   // min(lcnt[i], lcnt[j]) last observed (thread 0)
-            auto panels = [&](int need) -> bool {   // thread 0: both panels through column need - 1
-                int it = 0;
-                for (;;) {
-                    const int a = __hip_atomic_load(pw.lcnt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const int b = __hip_atomic_load(pw.lcnt + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    seen = a < b ? a : b;
-                    if (seen >= need) return true;
-                    __builtin_amdgcn_s_sleep(1);
-                    if ((++it & 63) == 0) {
-                        if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
-                        if (it > kSpin) {
-                            atomicExch(info, kToUpdPanels);
-                            return false;
-                        }
-                    }
-                }
-            };
-            if (t == 0) ok_sh = panels(v0 + 1);
-            __syncthreads();
-            if (!ok_sh) return;
-            tile_load_sc1(ra, Lm, ldp, i * NB, v0 * NB);
-            if (i != j) tile_load_sc1(rb, Lm, ldp, j * NB, v0 * NB);
-            for (int kk = v0; kk <= k; ++kk) {
-                tile_put(X, ra);
-                if (i != j) tile_put(Y, rb);
-                __syncthreads();
-                if (kk < k) {   // the next step's panels (known done, or polled now)
-                    if (t == 0) ok_sh = seen >= kk + 2 || panels(kk + 2);
-                    __syncthreads();
-                    if (!ok_sh) return;
-                    tile_load_sc1(ra, Lm, ldp, i * NB, (kk + 1) * NB);
-                    if (i != j) tile_load_sc1(rb, Lm, ldp, j * NB, (kk + 1) * NB);
-                }
-                mfma_xyt<true>(acc, X, i != j ? Y : X, wr, wc, lane);
-                __syncthreads();   // X / Y are rewritten by the next step
-            }
-            acc_store<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
-            publish(pw.ver + i * T + j, k + 1);
-            if (t == 0) {   // the version store completes before the lock is seen free
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(pw.lock + i * T + j, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            continue;
-        }
         // the tile's earlier updates first: its loads stay in flight while the workgroup waits
         // for the two panels
         if (t == 0) ok_sh = spin_ge(pw.ver + i * T + j, k, info);
@@ -1736,35 +1589,6 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm,
 
 __global__ void k_flag_info(int* info, int v) { *info = v; }
 
-// The streamed solve's prep (no copy of A: the J^T J's reduce writes P itself): the persistent
-// form's progress words -- every tile version and b's block-row words at -1 (not yet published
-// by the reduce), the rest 0 --, b's padding past n, P's padding (identity on the diagonal past
-// n), info = 0.
-__global__ __launch_bounds__(256) void k_chol_stream_prep(double* __restrict__ P, long ldp, int T, int n,
-                                                          double* __restrict__ bv, int* __restrict__ pflags,
-                                                          int npflags, int* __restrict__ info) {
-    const int N = T * NB, tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
-    const int b0 = 2 * T, v1 = 3 * T + T * T;   // [bcnt | ver]
-    for (int q = tid; q < npflags; q += nth) pflags[q] = (q >= b0 && q < v1) ? -1 : 0;
-    for (int r = n + tid; r < N; r += nth) bv[r] = 0.0;
-    if (n < N) {
-        const long pad = (long)(N - n) * N + (long)n * (N - n);   // rows >= n, then columns >= n of rows < n
-        for (long e = tid; e < pad; e += nth) {
-            int r, c;
-            if (e < (long)(N - n) * N) {
-                r = n + (int)(e / N);
-                c = (int)(e % N);
-            } else {
-                const long f = e - (long)(N - n) * N;
-                r = (int)(f / (N - n));
-                c = n + (int)(f % (N - n));
-            }
-            P[(long)r * ldp + c] = r == c ? 1.0 : 0.0;
-        }
-    }
-    if (tid == 0) *info = 0;
-}
-
 }  // namespace
 
 // Solve A sigma = rhs (A SPD, untouched) by the lookahead tile Cholesky; *dinfo (device) != 0
@@ -1789,32 +1613,21 @@ int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs
     return launch_chol_solve_v(ctx, A, lda, rhs, sigma, n, dinfo, 0, xbase, xnext);
 }
 
-// The tile Cholesky's workspace (method 4 / 5 and the streamed solve share it)
-struct CholWs {
-    int T = 0, N = 0;
-    long ldp = 0;
-    double *P = nullptr, *Lm = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr;
-    int *rowflag = nullptr, *bwdflag = nullptr, *pf = nullptr;
-    int npf = 0;
-    bool gran = false;
-};
-
-static int chol_ws(pnol_ctx* ctx, int n, CholWs& w) {
-    w.T = (n + NB - 1) / NB;
-    w.N = w.T * NB;
-    w.ldp = w.N;
-    const int T = w.T, N = w.N;
-    void *P = nullptr, *Lm = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr, *pf = nullptr;
-    PNOL_CHECK(ws_get(ctx, "chol4_P", sizeof(double) * (size_t)N * w.ldp, &P));
-    PNOL_CHECK(ws_get(ctx, "chol4_L", sizeof(double) * (size_t)N * w.ldp, &Lm));
+int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo,
+                        int variant, const double* xbase, double* xnext) {
+    const int T = (n + NB - 1) / NB, N = T * NB;
+    const long ldp = N;
+    void *P = nullptr, *Lm = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr;
+    PNOL_CHECK(ws_get(ctx, "chol4_P", sizeof(double) * (size_t)N * ldp, &P));
+    PNOL_CHECK(ws_get(ctx, "chol4_L", sizeof(double) * (size_t)N * ldp, &Lm));
     PNOL_CHECK(ws_get(ctx, "chol4_W", sizeof(double) * (size_t)T * NB * NB, &W));
     PNOL_CHECK(ws_get(ctx, "chol4_b", sizeof(double) * (size_t)N, &bv));
     PNOL_CHECK(ws_get(ctx, "chol4_z", sizeof(double) * (size_t)N, &zv));
     // the backward solve's hand-off words: x granules (x, epoch) -- 2 N doubles, zeroed when
     // allocated and whenever the epoch restarts (a stale granule must never match)
     // (the flag form keeps its own buffer, so the two layouts never share memory)
-    w.gran = bwd_granules();
-    if (w.gran) {
+    const bool gran = bwd_granules();
+    if (gran) {
         auto it = ctx->ws.bufs.find("chol4_xg");
         const void* before = it == ctx->ws.bufs.end() ? nullptr : it->second.first;
         PNOL_CHECK(ws_get(ctx, "chol4_xg", sizeof(double) * 2 * (size_t)N, &xw));
@@ -1827,138 +1640,65 @@ static int chol_ws(pnol_ctx* ctx, int n, CholWs& w) {
         const int cap = std::max(T, ctx->chol4_cap);
         PNOL_CHECK(ws_get(ctx, "chol4_flags", sizeof(int) * (size_t)2 * cap, &f));
         PNOL_HIP(hipMemsetAsync(f, 0, sizeof(int) * (size_t)2 * cap, ctx->stream));
-        if (w.gran) PNOL_HIP(hipMemsetAsync(xw, 0, sizeof(double) * 2 * (size_t)N, ctx->stream));   // epoch restarts
+        if (gran) PNOL_HIP(hipMemsetAsync(xw, 0, sizeof(double) * 2 * (size_t)N, ctx->stream));   // epoch restarts
         ctx->chol4_flags = (int*)f;
         ctx->chol4_cap = cap;
         ctx->chol4_epoch = 0;
     }
-    w.rowflag = ctx->chol4_flags;
-    w.bwdflag = ctx->chol4_flags + ctx->chol4_cap;
-    w.npf = 3 * T + 2 * T * T + 2;   // + the task counter, the role word and the tile locks
-    PNOL_CHECK(ws_get(ctx, "chol5_words", sizeof(int) * (size_t)w.npf, &pf));
-    w.P = (double*)P; w.Lm = (double*)Lm; w.W = (double*)W; w.bv = (double*)bv; w.zv = (double*)zv;
-    w.xw = (double*)xw; w.pf = (int*)pf;
-    return PNOL_OK;
-}
-
-// k_chol_persist on `st`: steps 0 .. T-2 (smode: the chain also factors tile 0, waiting for the
-// streamed J^T J's tiles); xcd >= 0 confines it to that XCD
-static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, int* dinfo, int xcd, int smode,
-                               int xcd_cus = 0) {
-    const int T = w.T;
-    int ntasks = 0;
-    for (int R = T - 1; R >= 1; --R) ntasks += R + R * (R + 1) / 2 - 1;
-    // tuning knob (read per call): PNOL_CHOL5_WORKERS = worker workgroups; one per CU
-    // (the look-ahead areas already hold the static LDS to one workgroup per CU).
-    // PNOL_CHOL_LOOKAHEAD = 0 turns the diagonal chain's look-ahead off (read per call).
-    const char* ew = std::getenv("PNOL_CHOL5_WORKERS");
-    const char* el = std::getenv("PNOL_CHOL_LOOKAHEAD");
-    // > 0: the look-ahead gives up once wave 0 has finished that many columns of the tile
-    // (0 off; above 64: the factor waits for the next tiles).  Measured at n = 2048
-    // (tools/microbench/chol_timeline.hip): 0: 0.645 ms, 52: 0.625, 64: 0.621 (default; half
-    // the steps find their tiles ready), 1000: 0.705 -- the next tiles wait on a panel and an
-    // update task (~6 us each after W_{d-1}), so waiting for them inside the factor costs more
-    // than the prepare it saves.
-    const int lookahead = el ? std::max(0, std::atoi(el)) : 64;
-    const int slots = std::max(ctx->num_cu, 1) - 1;
-    const int want = ew ? std::atoi(ew) : slots;
-    int workers = std::max(1, std::min(ntasks, want)), grid = 1 + workers;
-    if (xcd >= 0) {   // workgroup b goes to XCD b % 8: every XCD gets the chain + its workers
-        const int cus = xcd_cus > 0 ? xcd_cus : std::max(ctx->num_cu, 8) / 8;   // the XCD's CUs it may use
-        workers = std::max(1, std::min({ntasks, want, cus - 1}));
-        grid = 8 * (1 + workers);
+    int* rowflag = ctx->chol4_flags;
+    int* bwdflag = ctx->chol4_flags + ctx->chol4_cap;
+    const bool persist = chol_persistent(variant) && T >= 2;
+    void* pf = nullptr;
+    const int npf = 3 * T + T * T + 1;
+    if (persist) PNOL_CHECK(ws_get(ctx, "chol5_words", sizeof(int) * (size_t)npf, &pf));
+    for (int k = -1; k <= (persist ? -1 : T - 2); ++k) {
+        const int R = T - 1 - k;
+        const int grid = k < 0 ? 2 + std::min(N, 1024) : R + R * (R + 1) / 2;
+        const int epoch = ++ctx->chol4_epoch;
+        hipLaunchKernelGGL(k_chol_step, dim3(grid), dim3(256), 0, ctx->stream, (double*)P, (double*)Lm, ldp, T, k,
+                           (double*)W, (double*)bv, (double*)zv, rowflag, epoch, dinfo, A, (long)lda, n, rhs,
+                           (int*)pf, persist ? npf : 0);
     }
-    hipLaunchKernelGGL(k_chol_persist, dim3(grid), dim3(256), 0, st, w.P, w.Lm, w.ldp, T, w.W, w.bv, w.zv, w.pf,
-                       ntasks, dinfo, lookahead, xcd, smode);
-    return launch_check();
-}
-
-// the backward solve (+ the trial point) on `st`
-static int chol_bwd_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, int n, double* sigma, int* dinfo,
-                           const double* xbase, double* xnext) {
+    if (persist) {
+        int ntasks = 0;
+        for (int R = T - 1; R >= 1; --R) ntasks += R + R * (R + 1) / 2 - 1;
+        // tuning knob (read per call): PNOL_CHOL5_WORKERS = worker workgroups; one per CU
+        // (the look-ahead areas already hold the static LDS to one workgroup per CU).
+        // PNOL_CHOL_LOOKAHEAD = 0 turns the diagonal chain's look-ahead off (read per call).
+        const char* ew = std::getenv("PNOL_CHOL5_WORKERS");
+        const char* el = std::getenv("PNOL_CHOL_LOOKAHEAD");
+        // > 0: the look-ahead gives up once wave 0 has finished that many columns of the tile
+        // (0 off; above 64: the factor waits for the next tiles).  Measured at n = 2048
+        // (tools/microbench/chol_timeline.hip): 0: 0.645 ms, 52: 0.625, 64: 0.621 (default; half
+        // the steps find their tiles ready), 1000: 0.705 -- the next tiles wait on a panel and an
+        // update task (~6 us each after W_{d-1}), so waiting for them inside the factor costs more
+        // than the prepare it saves.
+        const int lookahead = el ? std::max(0, std::atoi(el)) : 64;
+        const int slots = std::max(ctx->num_cu, 1) - 1;
+        const int want = ew ? std::atoi(ew) : slots;
+        const int workers = std::max(1, std::min(ntasks, want));
+        hipLaunchKernelGGL(k_chol_persist, dim3(1 + workers), dim3(256), 0, ctx->stream, (double*)P, (double*)Lm, ldp,
+                           T, (double*)W, (double*)bv, (double*)zv, (int*)pf, ntasks, dinfo, lookahead);
+    }
     const int epoch = ++ctx->chol4_epoch;
-    if (w.gran && ((uintptr_t)w.xw & 15) != 0) return PNOL_ERR_ARG;   // granules need 16-byte alignment
-    if (w.gran)
-        hipLaunchKernelGGL(k_chol_bwd<true>, dim3(w.T), dim3(256), 0, st, (const double*)w.Lm, w.ldp, w.T, n,
-                           (const double*)w.W, (const double*)w.bv, (const double*)w.zv, w.xw, sigma, w.bwdflag, epoch,
+    if (gran && ((uintptr_t)xw & 15) != 0) return PNOL_ERR_ARG;   // granules need 16-byte alignment
+    if (gran)
+        hipLaunchKernelGGL(k_chol_bwd<true>, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n,
+                           (const double*)W, (const double*)bv, (const double*)zv, (double*)xw, sigma, bwdflag, epoch,
                            dinfo, xbase, xnext);
     else
-        hipLaunchKernelGGL(k_chol_bwd<false>, dim3(w.T), dim3(256), 0, st, (const double*)w.Lm, w.ldp, w.T, n,
-                           (const double*)w.W, (const double*)w.bv, (const double*)w.zv, w.xw, sigma, w.bwdflag, epoch,
+        hipLaunchKernelGGL(k_chol_bwd<false>, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n,
+                           (const double*)W, (const double*)bv, (const double*)zv, (double*)xw, sigma, bwdflag, epoch,
                            dinfo, xbase, xnext);
     PNOL_CHECK(launch_check());
     // test hook (tests/test_gpu_solvers.py): report a non-positive pivot so the callers' LU
     // fallback paths run on an SPD system (read per call: the tests flip it)
     if (const char* e = std::getenv("PNOL_CHOL_FORCE_FALLBACK"))
         if (std::atoi(e) != 0) {
-            hipLaunchKernelGGL(k_flag_info, dim3(1), dim3(1), 0, st, dinfo, 1);
+            hipLaunchKernelGGL(k_flag_info, dim3(1), dim3(1), 0, ctx->stream, dinfo, 1);
             return launch_check();
         }
     return PNOL_OK;
-}
-
-int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo,
-                        int variant, const double* xbase, double* xnext) {
-    CholWs w;
-    PNOL_CHECK(chol_ws(ctx, n, w));
-    const int T = w.T, N = w.N;
-    const bool persist = chol_persistent(variant) && T >= 2;
-    for (int k = -1; k <= (persist ? -1 : T - 2); ++k) {
-        const int R = T - 1 - k;
-        const int grid = k < 0 ? 2 + std::min(N, 1024) : R + R * (R + 1) / 2;
-        const int epoch = ++ctx->chol4_epoch;
-        hipLaunchKernelGGL(k_chol_step, dim3(grid), dim3(256), 0, ctx->stream, w.P, w.Lm, w.ldp, T, k, w.W, w.bv, w.zv,
-                           w.rowflag, epoch, dinfo, A, (long)lda, n, rhs, w.pf, persist ? w.npf : 0);
-    }
-    if (persist) {
-        // PNOL_CHOL_XCD = x: the factorisation confined to XCD x (measurement: what one XCD's
-        // CUs give, the placement a solve beside the J^T J has)
-        static const int xcd = [] {
-            const char* e = std::getenv("PNOL_CHOL_XCD");
-            return e ? std::atoi(e) : -1;
-        }();
-        PNOL_CHECK(chol_persist_launch(ctx, ctx->stream, w, dinfo, xcd, 0));
-    }
-    return chol_bwd_launch(ctx, ctx->stream, w, n, sigma, dinfo, xbase, xnext);
-}
-
-// The streamed solve's workspace (allocated before anything of the trip is queued)
-int launch_chol_stream_ws(pnol_ctx* ctx, int n, double** P, long* ldp, int* T, int** ver, int** bcnt, double** bv) {
-    if (n <= NB) return PNOL_ERR_ARG;
-    CholWs w;
-    PNOL_CHECK(chol_ws(ctx, n, w));
-    *P = w.P;
-    *ldp = w.ldp;
-    *T = w.T;
-    *ver = w.pf + 3 * w.T;
-    *bcnt = w.pf + 2 * w.T;
-    *bv = w.bv;
-    return PNOL_OK;
-}
-
-int launch_chol_stream_prep(pnol_ctx* ctx, int n, int* dinfo) {
-    if (n <= NB || !dinfo) return PNOL_ERR_ARG;
-    CholWs w;
-    PNOL_CHECK(chol_ws(ctx, n, w));
-    const long pad = (long)(w.N - n) * w.N + (long)n * (w.N - n), work = std::max<long>(pad, w.npf);
-    hipLaunchKernelGGL(k_chol_stream_prep, dim3((unsigned)std::min<long>(1024, (work + 255) / 256)), dim3(256), 0,
-                       ctx->stream, w.P, w.ldp, w.T, n, w.bv, w.pf, w.npf, dinfo);
-    return launch_check();
-}
-
-// The persistent factorisation on `st` behind the prep, on XCD xcd (xcd_cus of its CUs: the
-// chain + xcd_cus - 1 workers), consuming the reduce's tiles as they are published
-int launch_chol_stream_factor(pnol_ctx* ctx, hipStream_t st, int n, int* dinfo, int xcd, int xcd_cus) {
-    CholWs w;
-    PNOL_CHECK(chol_ws(ctx, n, w));
-    return chol_persist_launch(ctx, st, w, dinfo, xcd, 1, xcd_cus);
-}
-
-// the backward solve and the trial point, on the context stream (the whole chip)
-int launch_chol_stream_bwd(pnol_ctx* ctx, int n, double* sigma, int* dinfo, const double* xbase, double* xnext) {
-    CholWs w;
-    PNOL_CHECK(chol_ws(ctx, n, w));
-    return chol_bwd_launch(ctx, ctx->stream, w, n, sigma, dinfo, xbase, xnext);
 }
 
 }  // namespace pnol

@@ -120,27 +120,27 @@ __device__ unsigned long long g_syrk_tl[3 * 65536];
 // TILE 128: waves 2 x 2 of 64 x 64 (4 x 4 MFMA blocks each); TILE 64: 2 x 2 of 32 x 32.
 // NW = 4: waves 2 x 2, each (TILE/2)^2; NW = 8: waves 2 x 4, each TILE/2 x TILE/4 (half the
 // accumulators per wave, so twice the waves per SIMD hide the stage boundaries).
-// A partial-tile store: non-temporal, or (SC1: a consumer in the same launch, possibly on another
-// XCD, reads it after a counter hand-off) write-through sc1 (MI355X_MICROARCH.md "Valid forms")
-template <bool SC1>
-__device__ __forceinline__ void part_store(double* p, double v) {
-    if (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else __builtin_nontemporal_store(v, p);
-}
-
-// One split-K unit: the partial of lower-triangle tile t (row-major tile index) over K slice
-// sidx, into partial slot blk.  MODE 0 / 2: 128 x 128 partials part + blk * TILE^2; MODE 4: 64 x 64
-// tiles into the 128 x 128 partial layout (see the store below).
-// TILE 128: waves 2 x 2 of 64 x 64 (4 x 4 MFMA blocks each); TILE 64: 2 x 2 of 32 x 32.
-// NW = 4: waves 2 x 2, each (TILE/2)^2; NW = 8: waves 2 x 4, each TILE/2 x TILE/4 (half the
-// accumulators per wave, so twice the waves per SIMD hide the stage boundaries).
-template <int MODE, int TILE, int NW, bool SC1>
-__device__ __forceinline__ void syrk_unit(const double* __restrict__ X, long ldx, int nr, int K, int split_k,
-                                          int kfirst, int kchunk, int sub, int slice0, int mS, long sstride,
-                                          double* __restrict__ part, int t, int sidx, int blk,
-                                          double (*lds)[2][TILE * kPad]) {
+template <int MODE, int TILE, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
+                                                      int split_k, int kfirst, int kchunk, int sub, int slice0,
+                                                      int mS, long sstride, double* __restrict__ part, int tile0) {
     constexpr int NT = 64 * NW, WC = NW / 2;
     constexpr int WTM = TILE / 2, WTN = TILE / WC, NBM = WTM / 16, NBN = WTN / 16;
+    __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
+#ifdef PNOL_SYRK_TIMELINE
+    const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    // every (tile, slice)'s chunk 0 first, then chunk 1, ...: with a long chunk 0 the short
+    // chunks fill the last dispatch round instead of leaving it part-empty
+    int blk, t, sidx;
+    {
+        const int ntl = gridDim.x / split_k, nsl = split_k / sub;
+        const int u0 = blockIdx.x / (ntl * nsl), rest = blockIdx.x % (ntl * nsl);
+        const int tl = rest / nsl;
+        sidx = (rest % nsl) * sub + u0;
+        blk = tl * split_k + sidx;           // partial slot (local to this launch)
+        t = tile0 + tl;                      // lower-triangle tile index
+    }
     int ti, tj;
     tile_of(t, ti, tj);
     const bool diag = ti == tj;
@@ -283,7 +283,8 @@ __device__ __forceinline__ void syrk_unit(const double* __restrict__ X, long ldx
                 if (q < 4 || dcnt == 5)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        part_store<SC1>(out + (dbi[q] * 16 + orow + 4 * r) * ld + dbj[q] * 16 + ocol, acc[q >> 1][q & 1][r]);
+                        __builtin_nontemporal_store(acc[q >> 1][q & 1][r],
+                                                    out + (dbi[q] * 16 + orow + 4 * r) * ld + dbj[q] * 16 + ocol);
             // upper block u = bj (bj - 1) / 2 + bi (bi < bj): blocks wave, wave + 8, ... of the 28
             for (int u = __builtin_amdgcn_readfirstlane(wave); u < 28; u += NW) {
                 int bj = 1;
@@ -291,7 +292,7 @@ __device__ __forceinline__ void syrk_unit(const double* __restrict__ X, long ldx
                 const int bi = u - bj * (bj - 1) / 2;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    part_store<SC1>(out + (bi * 16 + orow + 4 * r) * ld + bj * 16 + ocol, 0.0);
+                    __builtin_nontemporal_store(0.0, out + (bi * 16 + orow + 4 * r) * ld + bj * 16 + ocol);
             }
         } else {
 #pragma unroll
@@ -302,37 +303,10 @@ __device__ __forceinline__ void syrk_unit(const double* __restrict__ X, long ldx
                     for (int r = 0; r < 4; ++r) {
                         int row = wr * WTM + mi * 16 + orow + 4 * r;
                         int col = wc * WTN + ni * 16 + ocol;
-                        part_store<SC1>(out + row * ld + col, acc[mi][ni][r]);
+                        __builtin_nontemporal_store(acc[mi][ni][r], out + row * ld + col);
                     }
         }
     }
-}
-
-// MODE 0: write split-K partial tile to part; MODE 4: 64 x 64 tiles into the 128 x 128 partial
-// layout of MODE 0; MODE 2: as MODE 0, instantiated separately for the chunked launches of
-// launch_fd_jtj (so a kernel trace tells the whole-matrix launches and the pipelined row chunks
-// apart).  One unit per workgroup.
-template <int MODE, int TILE, int NW = 4>
-__global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
-                                                      int split_k, int kfirst, int kchunk, int sub, int slice0,
-                                                      int mS, long sstride, double* __restrict__ part, int tile0) {
-    __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
-#ifdef PNOL_SYRK_TIMELINE
-    const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    // every (tile, slice)'s chunk 0 first, then chunk 1, ...: with a long chunk 0 the short
-    // chunks fill the last dispatch round instead of leaving it part-empty
-    int blk, t, sidx;
-    {
-        const int ntl = gridDim.x / split_k, nsl = split_k / sub;
-        const int u0 = blockIdx.x / (ntl * nsl), rest = blockIdx.x % (ntl * nsl);
-        const int tl = rest / nsl;
-        sidx = (rest % nsl) * sub + u0;
-        blk = tl * split_k + sidx;           // partial slot (local to this launch)
-        t = tile0 + tl;                      // lower-triangle tile index
-    }
-    syrk_unit<MODE, TILE, NW, false>(X, ldx, nr, K, split_k, kfirst, kchunk, sub, slice0, mS, sstride, part, t, sidx,
-                                     blk, lds);
 #ifdef PNOL_SYRK_TIMELINE
     if (threadIdx.x == 0) {
         const unsigned long long tl1 = __builtin_amdgcn_s_memrealtime();
@@ -477,28 +451,6 @@ __global__ void k_syrk_unpack(const double* __restrict__ packed, int ntiles, int
 // jp / rhs (nullable): one more row of blocks (blockIdx.y == ntiles) forms rhs = the slice
 // tree of the 8 -J^T F slice partials jp[s * n + e], exactly as k_tree_nodes over all slices does
 // (leaf = 0.0 + partial, then tree8): the tree rides in this launch instead of its own.
-// the reduce's value of element pair q of a strip: per slice the sub-chunk partials from 0.0
-// in order, then tree8 (k_syrk_reduce and k_syrk_reduce_p: the same sums)
-template <int SUB>
-__device__ __forceinline__ void reduce_pair(const double* __restrict__ p, int q, int sub, long E, double& vx,
-                                            double& vy) {
-    double lx[kS], ly[kS];
-#pragma unroll
-    for (int s = 0; s < kS; ++s) {
-        double ax = 0.0, ay = 0.0;
-#pragma unroll
-        for (int u = 0; u < (SUB > 0 ? SUB : sub); ++u) {
-            const double2 w = reinterpret_cast<const double2*>(p + (long)(s * sub + u) * E)[q];
-            ax += w.x;
-            ay += w.y;
-        }
-        lx[s] = ax;
-        ly[s] = ay;
-    }
-    vx = tree8(lx);
-    vy = tree8(ly);
-}
-
 template <int SUB, int SR = 32>
 __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ part, int ntiles, int sub_rt, int n,
                                                      double lambda, double* __restrict__ A, long lda,
@@ -527,8 +479,20 @@ __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ 
 #pragma unroll 2
     for (int q = threadIdx.x; q < SR * kTile / 2; q += 256) {
         const int r = (2 * q) / kTile, c = (2 * q) % kTile;
-        double vx, vy;
-        reduce_pair<SUB>(p, q, sub, E, vx, vy);
+        double lx[kS], ly[kS];
+#pragma unroll
+        for (int s = 0; s < kS; ++s) {
+            double ax = 0.0, ay = 0.0;
+#pragma unroll
+            for (int u = 0; u < (SUB > 0 ? SUB : sub); ++u) {
+                const double2 w = reinterpret_cast<const double2*>(p + (long)(s * sub + u) * E)[q];
+                ax += w.x;
+                ay += w.y;
+            }
+            lx[s] = ax;
+            ly[s] = ay;
+        }
+        const double vx = tree8(lx), vy = tree8(ly);
         st[r][c] = vx;
         st[r][c + 1] = vy;
         const int i = ti * kTile + r0 + r;
@@ -550,97 +514,6 @@ __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ 
         const int c = q / SR, r = q % SR;                  // consecutive threads: consecutive i
         const int i = ti * kTile + r0 + r, j = tj * kTile + c;
         if (i < n && j < n && j < i) A[(long)j * lda + i] = st[r][c];
-    }
-}
-
-// k_syrk_reduce into the tile Cholesky's padded matrix P, streamed to it (the streamed damped
-// solve, launch_fd_normal_solve_stream): blockIdx.y = 0 is the -J^T F slice tree (written to rhs
-// and to the Cholesky's b; its last workgroup then publishes b, the block-row words bcnt = 0),
-// blockIdx.y = 1 + c the c-th 128 x 128 tile in column order (the Cholesky's first steps need the
-// first columns).  Every value is k_syrk_reduce's (reduce_pair); the diagonal tiles are mirrored
-// (the Cholesky reads whole diagonal 64 x 64 tiles), the upper off-diagonal tiles are not
-// written.  All stores sc1; each workgroup adds to its tile's counter after its stores drained
-// and the last of the tile's strips publishes version 0 of its 64 x 64 sub-tiles (the Cholesky
-// waits for version >= k): MI355X_MICROARCH.md "Valid forms" row 1.  Bitwise the A of
-// k_syrk_reduce (lower part, Marquardt diagonal) and its rhs.
-template <int SUB, int SR>
-__global__ __launch_bounds__(256) void k_syrk_reduce_p(const double* __restrict__ part, int ntiles, int sub_rt, int n,
-                                                       double lambda, double* __restrict__ P, long ldp, int T,
-                                                       int* __restrict__ ver, int* __restrict__ bcnt,
-                                                       int* __restrict__ cnt, const double* __restrict__ jp,
-                                                       double* __restrict__ rhs, double* __restrict__ bv) {
-    __shared__ double st[SR][kTile + 1];
-    __shared__ int last_sh;
-    const int nstrip = gridDim.x;
-    if (blockIdx.y == 0) {   // the -J^T F tree: k_syrk_reduce's fold row
-        for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-            double l[kS];
-#pragma unroll
-            for (int s = 0; s < kS; ++s) l[s] = 0.0 + jp[(long)s * n + e];
-            const double v = tree8(l);
-            rhs[e] = v;
-            __hip_atomic_store(bv + e, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0)
-            last_sh = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nstrip - 1;
-        __syncthreads();
-        if (last_sh)
-            for (int i = threadIdx.x; i < T; i += blockDim.x)
-                __hip_atomic_store(bcnt + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    const int sub = SUB > 0 ? SUB : sub_rt;
-    // tile c of the column order -> (ti, tj) and its row-major index t (the partials' order)
-    const int nt = (int)((__builtin_sqrt(8.0 * ntiles + 1.0) - 1.0) / 2.0 + 0.5);
-    int r = (int)blockIdx.y - 1, tj = 0;
-    while (r >= nt - tj) {
-        r -= nt - tj;
-        ++tj;
-    }
-    const int ti = tj + r, t = ti * (ti + 1) / 2 + tj;
-    const double scale = 1 + lambda;
-    const int r0 = blockIdx.x * SR;
-    const long E = kTile * kTile;
-    const double* p = part + ((long)t * kS * sub) * E + (long)r0 * kTile;
-    const bool dg = ti == tj;
-#pragma unroll 2
-    for (int q = threadIdx.x; q < SR * kTile / 2; q += 256) {
-        const int rr = (2 * q) / kTile, c = (2 * q) % kTile;
-        double vx, vy;
-        reduce_pair<SUB>(p, q, sub, E, vx, vy);
-        if (dg) {
-            st[rr][c] = vx;
-            st[rr][c + 1] = vy;
-        }
-        const int i = ti * kTile + r0 + rr;
-        for (int h = 0; h < 2; ++h) {
-            const int j = tj * kTile + c + h;
-            const double val = h ? vy : vx;
-            if (i >= n || j >= n || j > i) continue;
-            __hip_atomic_store(P + (long)i * ldp + j, i == j ? scale * val : val, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    if (dg) {   // the mirror inside the diagonal tile
-        __syncthreads();
-        for (int q = threadIdx.x; q < SR * kTile; q += 256) {
-            const int c = q / SR, rr = q % SR;
-            const int i = ti * kTile + r0 + rr, j = tj * kTile + c;
-            if (i < n && j < n && j < i)
-                __hip_atomic_store(P + (long)j * ldp + i, st[rr][c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-        last_sh = __hip_atomic_fetch_add(cnt + 1 + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nstrip - 1;
-    __syncthreads();
-    if (last_sh && threadIdx.x < 4) {   // the 64 x 64 sub-tiles (2 ti + a, 2 tj + b) on or below the diagonal
-        const int a = threadIdx.x >> 1, b = threadIdx.x & 1;
-        const int I = 2 * ti + a, J = 2 * tj + b;
-        if (I < T && J < T && J <= I) __hip_atomic_store(ver + (long)I * T + J, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -806,19 +679,6 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     return PNOL_OK;
 }
 
-// A (lower triangle + mirror, the Marquardt diagonal) from the partials of the last streamed trip
-// (launch_fd_normal_solve_stream; the same reduce as launch_jtj, so the same A)
-int launch_jtj_from_partials(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda) {
-    const int nt = (n + kTile - 1) / kTile;
-    const int ntiles = nt * (nt + 1) / 2;
-    const SliceCfg sc = slice_cfg(m, ntiles);
-    void* part = nullptr;
-    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * kS * sc.sub * kTile * kTile, &part));
-    launch_reduce(dim3(kTile / 32, ntiles), dim3(256), 0, ctx->stream, (const double*)part, ntiles, sc.sub, n, lambda,
-                  A, (long)lda, (double*)nullptr, 0);
-    return launch_check();
-}
-
 int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldjt, int m, int n, double lambda,
                     double* A, int lda, double* jtj_diag, int row_begin, int row_end) {
     const int nt = (n + kTile - 1) / kTile;
@@ -894,98 +754,6 @@ int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h,
     PNOL_HIP(hipEventRecord(ctx->aux_events[nchunks], ctx->aux_stream));
     PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->aux_events[nchunks], 0));
     return rhs ? launch_jtr(ctx, JT, ldjt, m, n, F0, rhs) : PNOL_OK;
-}
-
-// The streamed solve's two CU-masked streams for XCD xcd (ctx->split_streams).  CU mask bit i
-// is CU i / 8 of XCD i % 8 (tools/microbench/cumask_probe.hip); an XCD left without a bit would
-// be unrestricted, so each stream keeps one CU -- the XCD's last -- of every XCD it does not run
-// on, and the other stream leaves that CU out.
-static int split_streams(pnol_ctx* ctx, int xcd) {
-    if (ctx->split_xcd == xcd && ctx->split_streams[0]) return PNOL_OK;
-    const int ncu = ctx->num_cu, per = ncu / 8;
-    if (ncu < 16 || ncu % 8 != 0) return PNOL_ERR_UNSUPPORTED;
-    for (hipStream_t& st : ctx->split_streams)
-        if (st) {
-            PNOL_HIP(hipStreamSynchronize(st));
-            PNOL_HIP(hipStreamDestroy(st));
-            st = nullptr;
-        }
-    std::vector<uint32_t> mj((ncu + 31) / 32, 0u), mc((ncu + 31) / 32, 0u);
-    for (int i = 0; i < ncu; ++i) {
-        const bool own = i % 8 == xcd, last = i / 8 == per - 1;
-        const bool chol = own ? !last : last;
-        (chol ? mc : mj)[i / 32] |= 1u << (i % 32);
-    }
-    PNOL_HIP(hipExtStreamCreateWithCUMask(&ctx->split_streams[0], (uint32_t)mj.size(), mj.data()));
-    PNOL_HIP(hipExtStreamCreateWithCUMask(&ctx->split_streams[1], (uint32_t)mc.size(), mc.data()));
-    ctx->split_xcd = xcd;
-    return PNOL_OK;
-}
-
-// One LM trip's linear algebra with the damped solve started under the J^T J's reduce (single
-// process, n > PNOL_SEQ_MAX, LevenbergMarquardt.cpp:59-83): the FD Jacobian, the split-K J^T J
-// partials and the -J^T F slice partials on the whole chip, then at once the reduce on every XCD
-// but xcd (k_syrk_reduce_p: the tiles in column order straight into the Cholesky's padded
-// matrix, b = -J^T F first) and the persistent Cholesky on XCD xcd, which factors each 64 x 64
-// tile as soon as the reduce has published it; the backward solve (and xnext = x + sigma) on the
-// whole chip after both.  The reduce's 2 x 16-byte-per-element HBM stream and the Cholesky's
-// latency-bound chain share the chip instead of following each other, and the copy of A into
-// the Cholesky's matrix is gone.  A is not formed (launch_jtj_from_partials forms it for the LU
-// fallback).  JT, rhs, sigma and xnext are bitwise those of launch_fd_jtj + launch_chol_solve.
-int launch_fd_normal_solve_stream(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0,
-                                  int compute_f0, double* JT, int ldjt, double lambda, double* rhs, double* sigma,
-                                  int* dinfo, double* xnext, int xcd) {
-    if (!o || !x || !h || !F0 || !JT || !rhs || !sigma || !dinfo || !xnext || ldjt < o->m) return PNOL_ERR_ARG;
-    const int n = o->n, m = o->m;
-    if (n <= PNOL_SEQ_MAX || xcd < 0 || xcd > 7) return PNOL_ERR_ARG;
-    const int nt = (n + kTile - 1) / kTile;
-    const int ntiles = nt * (nt + 1) / 2;
-    const SliceCfg sc = slice_cfg(m, ntiles);
-    // every workspace first: a (re)allocation frees, and a free waits for the device
-    void *part = nullptr, *jp = nullptr, *cnt = nullptr;
-    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * kS * sc.sub * kTile * kTile, &part));
-    PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
-    PNOL_CHECK(ws_get(ctx, "reduce_p_words", sizeof(int) * (size_t)(1 + ntiles), &cnt));
-    double *P = nullptr, *bv = nullptr;
-    long ldp = 0;
-    int T = 0;
-    int *ver = nullptr, *bcnt = nullptr;
-    PNOL_CHECK(launch_chol_stream_ws(ctx, n, &P, &ldp, &T, &ver, &bcnt, &bv));
-    PNOL_CHECK(split_streams(ctx, xcd));
-    while (ctx->aux_events.size() < 3) {
-        hipEvent_t e;
-        PNOL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        ctx->aux_events.push_back(e);
-    }
-
-    PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
-    syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
-                  syrk_t64(false));
-    PNOL_CHECK(launch_check());
-    PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F0));
-    PNOL_CHECK(launch_chol_stream_prep(ctx, n, dinfo));
-    PNOL_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)(1 + ntiles), ctx->stream));
-    PNOL_HIP(hipEventRecord(ctx->aux_events[0], ctx->stream));
-    hipStream_t sr = ctx->split_streams[0], sc2 = ctx->split_streams[1];
-    PNOL_HIP(hipStreamWaitEvent(sr, ctx->aux_events[0], 0));
-    PNOL_HIP(hipStreamWaitEvent(sc2, ctx->aux_events[0], 0));
-    {
-        ScopedTimer tm(ctx, "syrk_reduce", sr);
-        const dim3 grid(kTile / 16, 1 + ntiles);   // 16-row strips (launch_reduce's)
-        if (sc.sub == 2)
-            hipLaunchKernelGGL((k_syrk_reduce_p<2, 16>), grid, dim3(256), 0, sr, (const double*)part, ntiles, sc.sub, n,
-                               lambda, P, ldp, T, ver, bcnt, (int*)cnt, (const double*)jp, rhs, bv);
-        else
-            hipLaunchKernelGGL((k_syrk_reduce_p<0, 16>), grid, dim3(256), 0, sr, (const double*)part, ntiles, sc.sub, n,
-                               lambda, P, ldp, T, ver, bcnt, (int*)cnt, (const double*)jp, rhs, bv);
-        PNOL_CHECK(launch_check());
-    }
-    PNOL_CHECK(launch_chol_stream_factor(ctx, sc2, n, dinfo, xcd, std::max(ctx->num_cu, 8) / 8 - 1));
-    PNOL_HIP(hipEventRecord(ctx->aux_events[1], sc2));
-    PNOL_HIP(hipEventRecord(ctx->aux_events[2], sr));
-    PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->aux_events[1], 0));
-    PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->aux_events[2], 0));
-    return launch_chol_stream_bwd(ctx, n, sigma, dinfo, x, xnext);
 }
 
 // J^T J with the 128 x 128 tiles split over the communicator's ranks (contiguous ranges of

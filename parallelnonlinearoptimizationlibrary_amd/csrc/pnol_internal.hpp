@@ -74,12 +74,6 @@ struct pnol_ctx {
     hipStream_t comm_stream = nullptr;
     std::vector<hipEvent_t> phase_events;
     hipEvent_t comm_done = nullptr;
-    // the streamed damped solve (launch_fd_normal_solve_stream): two CU-masked streams that
-    // share no CU -- [0] the J^T J: every CU off XCD split_xcd plus one CU of it; [1] the
-    // Cholesky: the rest of XCD split_xcd plus one CU of every other XCD (a workgroup dispatched
-    // off its XCD leaves at once, so neither launch ever waits for the other's CUs)
-    hipStream_t split_streams[2] = {nullptr, nullptr};
-    int split_xcd = -1;
 };
 
 struct pnol_dobj {
@@ -190,10 +184,6 @@ int launch_gather_rows(pnol_ctx* ctx, const double* D, int ldd, const int* ridx,
 // rhs (nullable): also rhs = -J^T F (bitwise launch_jtr), its slice tree in the reduce launch
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                double* jtj_diag, const double* F = nullptr, double* rhs = nullptr);
-int launch_fd_normal_solve_stream(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0,
-                                  int compute_f0, double* JT, int ldjt, double lambda, double* rhs, double* sigma,
-                                  int* dinfo, double* xnext, int xcd);
-int launch_jtj_from_partials(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda);
 int launch_jtj_sharded(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                        double* jtj_diag);
 int launch_jtr(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
@@ -210,16 +200,6 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
                         int variant, const double* xbase = nullptr, double* xnext = nullptr);
 int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n, int method,
                  int* info);
-// The streamed damped solve (chol.hip, used by launch_fd_normal_solve_stream): the tile
-// Cholesky's workspace for n -- its padded matrix P (ld ldp, T 64-tiles), the tile version
-// words, the block-row words of b and b itself; the prep on the context stream (tile versions
-// and b's block-row words at -1: not yet published; b's padding, P's padding, info = 0); the
-// persistent factorisation on stream st, confined to XCD xcd (xcd_cus of its CUs); the
-// backward solve (and xnext = xbase + sigma) on the context stream
-int launch_chol_stream_ws(pnol_ctx* ctx, int n, double** P, long* ldp, int* T, int** ver, int** bcnt, double** bv);
-int launch_chol_stream_prep(pnol_ctx* ctx, int n, int* dinfo);
-int launch_chol_stream_factor(pnol_ctx* ctx, hipStream_t st, int n, int* dinfo, int xcd, int xcd_cus);
-int launch_chol_stream_bwd(pnol_ctx* ctx, int n, double* sigma, int* dinfo, const double* xbase, double* xnext);
 
 int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
 // rows [r0, r1) only (multiples of 64 but r1 = m; r1 < 0: all): a row-sharded LevMarqMPI rank

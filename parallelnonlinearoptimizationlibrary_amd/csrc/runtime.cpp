@@ -490,11 +490,6 @@ int pnol_ctx_destroy(pnol_ctx* ctx) {
         (void)hipStreamSynchronize(ctx->comm_stream);
         (void)hipStreamDestroy(ctx->comm_stream);
     }
-    for (hipStream_t& st : ctx->split_streams)
-        if (st) {
-            (void)hipStreamSynchronize(st);
-            (void)hipStreamDestroy(st);
-        }
     for (hipEvent_t e : ctx->phase_events) (void)hipEventDestroy(e);
     if (ctx->comm_done) (void)hipEventDestroy(ctx->comm_done);
     for (auto& kv : ctx->timers.pending)

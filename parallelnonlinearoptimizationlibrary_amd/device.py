@@ -135,23 +135,6 @@ class Context:
         L.check(L.lib().pnol_lm_fd_mode(self.h, C.byref(v)), "pnol_lm_fd_mode")
         return v.value
 
-    def solve_step(self, A, rhs, x):
-        """The LM loop's solve (pnol_solve_step_d): sigma = A^{-1} rhs by the tile Cholesky (A kept)
-        and xnext = x + sigma.  Returns (sigma, xnext, info) -- info read back (synchronises)."""
-        n = rhs.numel()
-        sigma, xnext = self.empty(n), self.empty(n)
-        info = self.torch.zeros(2, dtype=self.torch.int32, device=f"cuda:{self.device}")
-        L.check(L.lib().pnol_solve_step_d(self.h, _ptr(A), A.stride(0), _ptr(rhs), _ptr(sigma), n, _ptr(info),
-                                          _ptr(x), _ptr(xnext)), "pnol_solve_step_d")
-        return sigma, xnext, int(info[0].item())
-
-    def lm_stream_normal(self, m, n, lam, A=None):
-        """A = J^T J + Marquardt diagonal from the last streamed trip's partials (pnol_lm_stream_normal_d)."""
-        A = self.empty(n, n) if A is None else A
-        L.check(L.lib().pnol_lm_stream_normal_d(self.h, m, n, C.c_double(lam), _ptr(A), A.stride(0)),
-                "pnol_lm_stream_normal_d")
-        return A
-
     def solve(self, A, rhs, method=0):
         """sigma = A^{-1} rhs; A is overwritten.  Returns (sigma, info)."""
         n = rhs.numel()
@@ -245,18 +228,6 @@ class DeviceObjective:
                                          JT.stride(0), C.c_double(lam), _ptr(A), A.stride(0), None, _ptr(rhs)),
                 "pnol_fd_normal_d")
         return F0, JT, A, rhs
-
-    def lm_trip_stream(self, x, h, lam, JT, F0=None, compute_f0=True, xcd=0):
-        """One LM trip's linear algebra with the Cholesky streamed behind the J^T J
-        (pnol_lm_trip_stream_d).  Returns (F0, JT, rhs, sigma, xnext, info) -- info read back."""
-        t = self.ctx.torch
-        F0 = self.ctx.empty(self.m) if F0 is None else F0
-        rhs, sigma, xnext = self.ctx.empty(self.n), self.ctx.empty(self.n), self.ctx.empty(self.n)
-        info = t.zeros(2, dtype=t.int32, device=f"cuda:{self.ctx.device}")
-        L.check(L.lib().pnol_lm_trip_stream_d(self.ctx.h, self.h, _ptr(x), _ptr(h), _ptr(F0), int(compute_f0),
-                                              _ptr(JT), JT.stride(0), C.c_double(lam), _ptr(rhs), _ptr(sigma),
-                                              _ptr(info), _ptr(xnext), int(xcd)), "pnol_lm_trip_stream_d")
-        return F0, JT, rhs, sigma, xnext, int(info[0].item())
 
     def lm_jacobian_mpi(self, x, h, JTs=None, F0=None, compute_f0=True):
         """The m-sliced J^T this rank's share of the normal equations reads (pnol_lm_jacobian_mpi_d).

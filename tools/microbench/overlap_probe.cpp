@@ -109,21 +109,12 @@ int main() {
         {"b16_spread", 1, ncu - 16, 1, 0, 16, 16},
         {"b32_low", 32, ncu - 32, 1, 0, 32, 1},
         {"b8_low", 8, ncu - 8, 1, 0, 8, 1},
-        {"b32_every8", 0, 0, 0, 0, 32, 8},   // B = CUs 0, 8, 16, ... (one XCD if CU ids interleave)
     };
     for (const Split& s : splits) {
         hipStream_t sa, sb;
         if (s.b_stride == 1) {
             sa = masked(ncu, s.a_first, s.a_count, 1);
             sb = masked(ncu, s.b_first, s.b_count, 1);
-        } else if (s.b_stride == 8) {   // B = CUs c % 8 == 0, A = the others
-            std::vector<uint32_t> ma((ncu + 31) / 32, 0u), mb((ncu + 31) / 32, 0u);
-            for (int c = 0; c < ncu; ++c) {
-                if (c % 8 == 0) mb[c / 32] |= 1u << (c % 32);
-                else ma[c / 32] |= 1u << (c % 32);
-            }
-            hipExtStreamCreateWithCUMask(&sa, (uint32_t)ma.size(), ma.data());
-            hipExtStreamCreateWithCUMask(&sb, (uint32_t)mb.size(), mb.data());
         } else {   // B = every stride-th CU from 0, A = the others
             std::vector<uint32_t> ma((ncu + 31) / 32, 0u), mb((ncu + 31) / 32, 0u);
             for (int c = 0; c < ncu; ++c) {
