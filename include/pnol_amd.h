@@ -285,6 +285,18 @@ int pnol_fd_jtj_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* 
  * Bitwise the same JT, A and rhs as the separate calls. */
 int pnol_fd_normal_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0, int compute_f0,
                      double* JT, int ldjt, double lambda, double* A, int lda, double* jtj_diag, double* rhs);
+/* One LevMarq trip's linear algebra with A never formed (LevenbergMarquardt.cpp:55-90; n > 64,
+ * single process): the FD Jacobian into JT (compute_f0 as pnol_fd_jacobian_d), rhs = -(J^T F0),
+ * sigma = (J^T J + lambda diag(J^T J))^{-1} rhs by the persistent tile Cholesky -- whose first
+ * tasks sum the J^T J split-K partials straight into its own matrix -- and xnext = x + sigma.
+ * *dinfo (device int) != 0: a non-positive pivot; form A with pnol_lm_trip_normal_d and solve
+ * with the LU (pnol_solve_d method 2).  JT, rhs, sigma, xnext and *dinfo are bitwise those of
+ * pnol_fd_normal_d + pnol_solve_step_d. */
+int pnol_lm_trip_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0, int compute_f0,
+                   double* JT, int ldjt, double lambda, double* rhs, double* sigma, int* dinfo, double* xnext);
+/* A = J^T J + lambda diag(J^T J) from the last pnol_lm_trip_d's partial sums (its m, n, lambda):
+ * bitwise pnol_fd_normal_d's A. */
+int pnol_lm_trip_normal_d(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda);
 /* The FD Jacobian rows of a tile list (columns [start[t], start[t] + count[t]), count <=
  * PNOL_FD_TILE), column c written to JT + c * ldjt; one base-chain pass for all tiles. */
 int pnol_fd_jacobian_tiles_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, const int* start,

@@ -109,6 +109,8 @@ _SIGS = {
     "pnol_fd_jacobian_d": (_i, [_vp, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _i]),
     "pnol_fd_jtj_d": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp, _i, _d, _vp, _i, _vp, _i]),
     "pnol_fd_normal_d": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp, _i, _d, _vp, _i, _vp, _vp]),
+    "pnol_lm_trip_d": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp, _i, _d, _vp, _vp, _vp, _vp]),
+    "pnol_lm_trip_normal_d": (_i, [_vp, _i, _i, _d, _vp, _i]),
     "pnol_fd_jacobian_tiles_d": (_i, [_vp, _vp, _vp, _vp, C.POINTER(_i), C.POINTER(_i), _i, _vp, _i, _vp, _i]),
     "pnol_comm_unique_id": (_i, [C.c_char_p]),
     "pnol_comm_init_rccl": (_i, [_vp, _i, _i, C.c_char_p]),

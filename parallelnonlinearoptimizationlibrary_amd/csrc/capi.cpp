@@ -543,6 +543,18 @@ int pnol_fd_normal_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const doubl
     return launch_fd_jtj(ctx, obj, x, h, F0, compute_f0, JT, ldjt, lambda, A, lda, jtj_diag, 1, rhs);
 }
 
+int pnol_lm_trip_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, double* F0, int compute_f0,
+                   double* JT, int ldjt, double lambda, double* rhs, double* sigma, int* dinfo, double* xnext) {
+    PNOL_CHECK(set_device(ctx));
+    if (compute_f0 < 0 || compute_f0 > 3) return PNOL_ERR_ARG;
+    return launch_fd_normal_solve(ctx, obj, x, h, F0, compute_f0, JT, ldjt, lambda, rhs, sigma, dinfo, xnext);
+}
+
+int pnol_lm_trip_normal_d(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda) {
+    PNOL_CHECK(set_device(ctx));
+    return launch_jtj_from_partials(ctx, m, n, lambda, A, lda);
+}
+
 int pnol_fd_jacobian_tiles_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const double* h, const int* start,
                              const int* count, int ntiles, double* F0, int compute_f0, double* JT, int ldjt) {
     PNOL_CHECK(set_device(ctx));

@@ -199,6 +199,12 @@ class LMAsync {
             for (int v : all)
                 if (v != ctx->lm_fd_mode) throw std::runtime_error("LevMarqMPI: ranks disagree on PNOL_LM_FD");
         }
+        // one trip without forming A (pnol_lm_trip_d; PNOL_LM_TRIP=0 keeps the two calls below;
+        // read once per solve)
+        if (!sliced) {
+            const char* e = std::getenv("PNOL_LM_TRIP");
+            trip_fused_ = !e || std::atoi(e) != 0;
+        }
         JT_.reset(ctx, jt);
         A_.reset(ctx, (size_t)n * lda_);
         rhs_.reset(ctx, n);
@@ -238,6 +244,15 @@ class LMAsync {
             check(pnol_lm_normal_mpi_d(ctx_, JT_.get(), m_, n_, lambda, F(s), A_.get(), lda_, rhs_.get(),
                                        nullptr),
                   "normal equations");
+        } else if (trip_fused_) {
+            // FD Jacobian, the J^T J / -J^T F partials, the Cholesky that reduces them itself,
+            // the backward solve forming the trial point
+            lambda_[s] = lambda;
+            check(pnol_lm_trip_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 3 : 1, JT_.get(), ldjt_, lambda,
+                                 rhs_.get(), sig(s), info(s), x_[s ^ 1].get()),
+                  "lm trip");
+            finish(s, false);
+            return;
         } else {
             // FD Jacobian, A and -J^T F in one queue (the GEMV in the J^T J's tail)
             check(pnol_fd_normal_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 3 : 1, JT_.get(), ldjt_, lambda,
@@ -263,6 +278,7 @@ class LMAsync {
     // the reference-order LU for a trip whose Cholesky reported a non-positive pivot (A intact)
     void redo_lu(int s) {
         check(pnol_ctx_synchronize(ctx_), "sync");
+        if (trip_fused_) check(pnol_lm_trip_normal_d(ctx_, m_, n_, lambda_[s], A_.get(), lda_), "normal equations");
         int info = 0;
         check(pnol_solve_d(ctx_, A_.get(), lda_, rhs_.get(), sig(s), n_, 2, &info), "solve");
         finish(s);
@@ -274,6 +290,8 @@ class LMAsync {
     pnol_dobj* d_;
     int n_, m_, ldjt_, lda_;
     bool sliced_;
+    bool trip_fused_ = false;
+    double lambda_[2] = {0, 0};   // trip s's lambda (the fused trip's LU fallback forms A)
     int np_ = 0, mp_ = 0;
     DevVec JT_, A_, rhs_, h_, x_[2], trip_[2];
     void* pin_[2] = {nullptr, nullptr};

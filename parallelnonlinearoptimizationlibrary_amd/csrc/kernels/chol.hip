@@ -1294,10 +1294,90 @@ __device__ __forceinline__ void publish(int* w, int v) {
     if (threadIdx.x == 0) __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The reducing form (launch_chol_reducing, the LM trip): A is not formed -- the persistent
+// launch's first tasks sum the J^T J split-K partials of k_syrk_tile into the padded matrix P
+// themselves, one 64 x 64 tile each in column order (its version word leaves -1 when it is
+// stored: every step task's wait ver >= k also waits for it), after one task forming
+// b = -J^T F from the slice partials (b's block-row words leave -1).  The chain factors tile 0
+// itself.  Every value is the sum of k_syrk_reduce and k_tree_nodes (leaf = the sub-chunks from
+// 0.0 in order, then tree8; the Marquardt diagonal), and P's upper half inside the diagonal
+// tiles is the mirror, as the copy of A in the prep launch gives -- so the factorisation is
+// bitwise the one of A.
+struct RedArgs {
+    const double* part = nullptr;   // nullptr: not the reducing form
+    int sub = 0, n = 0;
+    double lambda = 0.0;
+    const double* jp = nullptr;     // the 8 -J^T F slice partials (jp[s n + e])
+    double* rhs = nullptr;          // rhs = -J^T F, for the LU fallback
+};
+
+__device__ __forceinline__ void red_pair(const double* __restrict__ p, long off, int sub, double& vx, double& vy) {
+    constexpr long E = 128L * 128L;
+    double lx[8], ly[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        double ax = 0.0, ay = 0.0;
+        for (int u = 0; u < sub; ++u) {
+            const double2 w = *reinterpret_cast<const double2*>(p + (long)(s * sub + u) * E + off);
+            ax += w.x;
+            ay += w.y;
+        }
+        lx[s] = ax;
+        ly[s] = ay;
+    }
+    vx = ((lx[0] + lx[1]) + (lx[2] + lx[3])) + ((lx[4] + lx[5]) + (lx[6] + lx[7]));
+    vy = ((ly[0] + ly[1]) + (ly[2] + ly[3])) + ((ly[4] + ly[5]) + (ly[6] + ly[7]));
+}
+
+// reduce task u of the reducing form: u = 0 b, u >= 1 the (u-1)-th lower 64 x 64 tile in column order
+__device__ void red_task(int u, const RedArgs& red, double* __restrict__ P, long ldp, int T, double* __restrict__ bv,
+                         const PersistWords& pw) {
+    const int t = threadIdx.x;
+    if (u == 0) {
+        for (int e = t; e < red.n; e += 256) {
+            double l[8];
+#pragma unroll
+            for (int s = 0; s < 8; ++s) l[s] = 0.0 + red.jp[(long)s * red.n + e];
+            const double v = ((l[0] + l[1]) + (l[2] + l[3])) + ((l[4] + l[5]) + (l[6] + l[7]));
+            red.rhs[e] = v;
+            stg<true>(bv + e, v);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int i = t; i < T; i += 256) __hip_atomic_store(pw.bcnt + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    int r = u - 1, J = 0;
+    while (r >= T - J) {
+        r -= T - J;
+        ++J;
+    }
+    const int I = J + r, ti = I >> 1, tj = J >> 1;
+    const long tt = (long)ti * (ti + 1) / 2 + tj;
+    const double* p = red.part + tt * 8 * red.sub * (128L * 128L);
+    const double scale = 1 + red.lambda;
+    for (int q = t; q < NB * NB / 2; q += 256) {   // element pairs (r, c), (r, c + 1)
+        const int rr = q >> 5, c = 2 * (q & 31);
+        double v2[2];
+        red_pair(p, (long)(64 * (I & 1) + rr) * 128 + 64 * (J & 1) + c, red.sub, v2[0], v2[1]);
+        const int i = I * NB + rr;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int j = J * NB + c + h;
+            if (i >= red.n || j >= red.n || j > i) continue;
+            stg<true>(P + (long)i * ldp + j, i == j ? scale * v2[h] : v2[h]);
+            if (j < i && I == J) stg<true>(P + (long)j * ldp + i, v2[h]);   // the mirror inside the diagonal tile
+        }
+    }
+    publish(pw.ver + I * T + J, 0);
+}
+
+
 __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P, double* __restrict__ Lm, long ldp,
                                                       int T, double* __restrict__ W, double* __restrict__ bv,
                                                       double* __restrict__ zv, int* __restrict__ flags, int ntasks,
-                                                      int* __restrict__ info, int lookahead) {
+                                                      int* __restrict__ info, int lookahead,
+                                                      const RedArgs red) {
     __shared__ __attribute__((aligned(16))) double smem[2 * kStage];   // 73.7 KB
     // the chain's look-ahead areas (EarlyNext / late_prepare): 75.8 KB
     __shared__ __attribute__((aligned(16))) double pfx[kStage];
@@ -1316,14 +1396,16 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
     if (blockIdx.x == 0) {   // ---------------- the diagonal chain
         const EarlyLds E{pfx, pll, pfc, ew};
         if (t < 4) ew[t] = 0;
-        for (int d = 1; d < T; ++d) {
+        const bool smode = red.part != nullptr;   // the reducing form: the chain also factors tile 0
+        for (int d = smode ? 0 : 1; d < T; ++d) {
             const int k = d - 1;
 #ifdef PNOL_CHOL_TIMELINE
             const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime(), ck0 = __builtin_amdgcn_s_memtime();
 #endif
             if (t == 0) {
                 const bool ok = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-                                spin_all<2>({pw.ver + d * T + k, pw.ver + d * T + d}, {k, k}, info);
+                                (d == 0 ? spin_ge(pw.ver, 0, info)
+                                        : spin_all<2>({pw.ver + d * T + k, pw.ver + d * T + d}, {k, k}, info));
                 ok_sh = ok;
             }
             __syncthreads();
@@ -1335,8 +1417,18 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
 #ifdef PNOL_CHOL_TIMELINE
             if (t == 0 && k + 1 < 64) g_chol_clk[8 * (k + 1) + 6] = pre ? 1 : 0;
 #endif
-            if (pre) late_prepare(E, Y, L, wave, lane);
-            else diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane, d > 1);
+            if (d == 0) {   // tile 0 as the reduce tasks stored it (sc1 loads)
+                const int row = t >> 2, c0 = (t & 3) * 16;
+                double v[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v[q] = ldg<true>(P + (long)row * ldp + c0 + q);
+#pragma unroll
+                for (int q = 0; q < 16; ++q) diag_put(L, row, c0 + q, v[q]);
+            } else if (pre) {
+                late_prepare(E, Y, L, wave, lane);
+            } else {   // W_{d-1} stays in Y after the chain's own factor
+                diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane, d > 1 || smode);
+            }
             if (t < 6) cnt[t] = 0;   // every read of cnt / ew above is behind a barrier inside
             if (t < 4) ew[t] = 0;    // either prepare
             __syncthreads();
@@ -1358,12 +1450,18 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         return;
     }
 
+    const int nred = red.part ? 1 + T * (T + 1) / 2 : 0;   // the reducing form's first tasks
     for (;;) {   // ---------------- workers
         if (t == 0) task_sh = atomicAdd(pw.counter, 1);
         __syncthreads();
         int g = task_sh;
         __syncthreads();   // task_sh is rewritten by the next claim
-        if (g >= ntasks) return;
+        if (g >= nred + ntasks) return;
+        if (g < nred) {
+            red_task(g, red, P, ldp, T, bv, pw);
+            continue;
+        }
+        g -= nred;
         int k = 0, R = T - 1;
         for (;;) {   // step k holds R panel rows and R (R + 1) / 2 - 1 update tiles
             const int S = R + R * (R + 1) / 2 - 1;
@@ -1386,7 +1484,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             if (!ok_sh) return;
             stage_tile<true>(X, P, ldp, i0, k0);
             if (t == 0) {   // W_k (tile 0 comes from the prep launch)
-                ok_sh = k == 0 || spin_ge(pw.wdone + k, 1, info);
+                ok_sh = (k == 0 && !red.part) || spin_ge(pw.wdone + k, 1, info);
 #ifdef PNOL_CHOL_TIMELINE
                 if (i == k + 2) PNOL_CRIT(k, 2)
 #endif
@@ -1613,21 +1711,32 @@ int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs
     return launch_chol_solve_v(ctx, A, lda, rhs, sigma, n, dinfo, 0, xbase, xnext);
 }
 
-int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo,
-                        int variant, const double* xbase, double* xnext) {
-    const int T = (n + NB - 1) / NB, N = T * NB;
-    const long ldp = N;
-    void *P = nullptr, *Lm = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr;
-    PNOL_CHECK(ws_get(ctx, "chol4_P", sizeof(double) * (size_t)N * ldp, &P));
-    PNOL_CHECK(ws_get(ctx, "chol4_L", sizeof(double) * (size_t)N * ldp, &Lm));
+// The tile Cholesky's workspace (the per-step / persistent forms and the reducing form)
+struct CholWs {
+    int T = 0, N = 0;
+    long ldp = 0;
+    double *P = nullptr, *Lm = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr;
+    int *rowflag = nullptr, *bwdflag = nullptr, *pf = nullptr;
+    int npf = 0;
+    bool gran = false;
+};
+
+static int chol_ws(pnol_ctx* ctx, int n, bool persist, CholWs& w) {
+    w.T = (n + NB - 1) / NB;
+    w.N = w.T * NB;
+    w.ldp = w.N;
+    const int T = w.T, N = w.N;
+    void *P = nullptr, *Lm = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr, *pf = nullptr;
+    PNOL_CHECK(ws_get(ctx, "chol4_P", sizeof(double) * (size_t)N * w.ldp, &P));
+    PNOL_CHECK(ws_get(ctx, "chol4_L", sizeof(double) * (size_t)N * w.ldp, &Lm));
     PNOL_CHECK(ws_get(ctx, "chol4_W", sizeof(double) * (size_t)T * NB * NB, &W));
     PNOL_CHECK(ws_get(ctx, "chol4_b", sizeof(double) * (size_t)N, &bv));
     PNOL_CHECK(ws_get(ctx, "chol4_z", sizeof(double) * (size_t)N, &zv));
     // the backward solve's hand-off words: x granules (x, epoch) -- 2 N doubles, zeroed when
     // allocated and whenever the epoch restarts (a stale granule must never match)
     // (the flag form keeps its own buffer, so the two layouts never share memory)
-    const bool gran = bwd_granules();
-    if (gran) {
+    w.gran = bwd_granules();
+    if (w.gran) {
         auto it = ctx->ws.bufs.find("chol4_xg");
         const void* before = it == ctx->ws.bufs.end() ? nullptr : it->second.first;
         PNOL_CHECK(ws_get(ctx, "chol4_xg", sizeof(double) * 2 * (size_t)N, &xw));
@@ -1640,55 +1749,58 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
         const int cap = std::max(T, ctx->chol4_cap);
         PNOL_CHECK(ws_get(ctx, "chol4_flags", sizeof(int) * (size_t)2 * cap, &f));
         PNOL_HIP(hipMemsetAsync(f, 0, sizeof(int) * (size_t)2 * cap, ctx->stream));
-        if (gran) PNOL_HIP(hipMemsetAsync(xw, 0, sizeof(double) * 2 * (size_t)N, ctx->stream));   // epoch restarts
+        if (w.gran) PNOL_HIP(hipMemsetAsync(xw, 0, sizeof(double) * 2 * (size_t)N, ctx->stream));   // epoch restarts
         ctx->chol4_flags = (int*)f;
         ctx->chol4_cap = cap;
         ctx->chol4_epoch = 0;
     }
-    int* rowflag = ctx->chol4_flags;
-    int* bwdflag = ctx->chol4_flags + ctx->chol4_cap;
-    const bool persist = chol_persistent(variant) && T >= 2;
-    void* pf = nullptr;
-    const int npf = 3 * T + T * T + 1;
-    if (persist) PNOL_CHECK(ws_get(ctx, "chol5_words", sizeof(int) * (size_t)npf, &pf));
-    for (int k = -1; k <= (persist ? -1 : T - 2); ++k) {
-        const int R = T - 1 - k;
-        const int grid = k < 0 ? 2 + std::min(N, 1024) : R + R * (R + 1) / 2;
-        const int epoch = ++ctx->chol4_epoch;
-        hipLaunchKernelGGL(k_chol_step, dim3(grid), dim3(256), 0, ctx->stream, (double*)P, (double*)Lm, ldp, T, k,
-                           (double*)W, (double*)bv, (double*)zv, rowflag, epoch, dinfo, A, (long)lda, n, rhs,
-                           (int*)pf, persist ? npf : 0);
-    }
-    if (persist) {
-        int ntasks = 0;
-        for (int R = T - 1; R >= 1; --R) ntasks += R + R * (R + 1) / 2 - 1;
-        // tuning knob (read per call): PNOL_CHOL5_WORKERS = worker workgroups; one per CU
-        // (the look-ahead areas already hold the static LDS to one workgroup per CU).
-        // PNOL_CHOL_LOOKAHEAD = 0 turns the diagonal chain's look-ahead off (read per call).
-        const char* ew = std::getenv("PNOL_CHOL5_WORKERS");
-        const char* el = std::getenv("PNOL_CHOL_LOOKAHEAD");
-        // > 0: the look-ahead gives up once wave 0 has finished that many columns of the tile
-        // (0 off; above 64: the factor waits for the next tiles).  Measured at n = 2048
-        // (tools/microbench/chol_timeline.hip): 0: 0.645 ms, 52: 0.625, 64: 0.621 (default; half
-        // the steps find their tiles ready), 1000: 0.705 -- the next tiles wait on a panel and an
-        // update task (~6 us each after W_{d-1}), so waiting for them inside the factor costs more
-        // than the prepare it saves.
-        const int lookahead = el ? std::max(0, std::atoi(el)) : 64;
-        const int slots = std::max(ctx->num_cu, 1) - 1;
-        const int want = ew ? std::atoi(ew) : slots;
-        const int workers = std::max(1, std::min(ntasks, want));
-        hipLaunchKernelGGL(k_chol_persist, dim3(1 + workers), dim3(256), 0, ctx->stream, (double*)P, (double*)Lm, ldp,
-                           T, (double*)W, (double*)bv, (double*)zv, (int*)pf, ntasks, dinfo, lookahead);
-    }
+    w.rowflag = ctx->chol4_flags;
+    w.bwdflag = ctx->chol4_flags + ctx->chol4_cap;
+    w.npf = 3 * T + T * T + 1;
+    if (persist) PNOL_CHECK(ws_get(ctx, "chol5_words", sizeof(int) * (size_t)w.npf, &pf));
+    w.P = (double*)P; w.Lm = (double*)Lm; w.W = (double*)W; w.bv = (double*)bv; w.zv = (double*)zv;
+    w.xw = (double*)xw; w.pf = (int*)pf;
+    return PNOL_OK;
+}
+
+// k_chol_persist: steps 0 .. T-2 (the reducing form: the reduce tasks first, and tile 0 too)
+static int chol_persist_launch(pnol_ctx* ctx, const CholWs& w, int* dinfo, const RedArgs& red) {
+    const int T = w.T;
+    int ntasks = 0;
+    for (int R = T - 1; R >= 1; --R) ntasks += R + R * (R + 1) / 2 - 1;
+    // tuning knob (read per call): PNOL_CHOL5_WORKERS = worker workgroups; one per CU
+    // (the look-ahead areas already hold the static LDS to one workgroup per CU).
+    // PNOL_CHOL_LOOKAHEAD = 0 turns the diagonal chain's look-ahead off (read per call).
+    const char* ew = std::getenv("PNOL_CHOL5_WORKERS");
+    const char* el = std::getenv("PNOL_CHOL_LOOKAHEAD");
+    // > 0: the look-ahead gives up once wave 0 has finished that many columns of the tile
+    // (0 off; above 64: the factor waits for the next tiles).  Measured at n = 2048
+    // (tools/microbench/chol_timeline.hip): 0: 0.645 ms, 52: 0.625, 64: 0.621 (default; half
+    // the steps find their tiles ready), 1000: 0.705 -- the next tiles wait on a panel and an
+    // update task (~6 us each after W_{d-1}), so waiting for them inside the factor costs more
+    // than the prepare it saves.
+    const int lookahead = el ? std::max(0, std::atoi(el)) : 64;
+    const int slots = std::max(ctx->num_cu, 1) - 1;
+    const int want = ew ? std::atoi(ew) : slots;
+    const int nred = red.part ? 1 + T * (T + 1) / 2 : 0;
+    const int workers = std::max(1, std::min(ntasks + nred, want));
+    hipLaunchKernelGGL(k_chol_persist, dim3(1 + workers), dim3(256), 0, ctx->stream, w.P, w.Lm, w.ldp, T, w.W, w.bv,
+                       w.zv, w.pf, ntasks, dinfo, lookahead, red);
+    return launch_check();
+}
+
+// the backward solve (+ the trial point)
+static int chol_bwd_launch(pnol_ctx* ctx, const CholWs& w, int n, double* sigma, int* dinfo, const double* xbase,
+                           double* xnext) {
     const int epoch = ++ctx->chol4_epoch;
-    if (gran && ((uintptr_t)xw & 15) != 0) return PNOL_ERR_ARG;   // granules need 16-byte alignment
-    if (gran)
-        hipLaunchKernelGGL(k_chol_bwd<true>, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n,
-                           (const double*)W, (const double*)bv, (const double*)zv, (double*)xw, sigma, bwdflag, epoch,
+    if (w.gran && ((uintptr_t)w.xw & 15) != 0) return PNOL_ERR_ARG;   // granules need 16-byte alignment
+    if (w.gran)
+        hipLaunchKernelGGL(k_chol_bwd<true>, dim3(w.T), dim3(256), 0, ctx->stream, (const double*)w.Lm, w.ldp, w.T, n,
+                           (const double*)w.W, (const double*)w.bv, (const double*)w.zv, w.xw, sigma, w.bwdflag, epoch,
                            dinfo, xbase, xnext);
     else
-        hipLaunchKernelGGL(k_chol_bwd<false>, dim3(T), dim3(256), 0, ctx->stream, (const double*)Lm, ldp, T, n,
-                           (const double*)W, (const double*)bv, (const double*)zv, (double*)xw, sigma, bwdflag, epoch,
+        hipLaunchKernelGGL(k_chol_bwd<false>, dim3(w.T), dim3(256), 0, ctx->stream, (const double*)w.Lm, w.ldp, w.T, n,
+                           (const double*)w.W, (const double*)w.bv, (const double*)w.zv, w.xw, sigma, w.bwdflag, epoch,
                            dinfo, xbase, xnext);
     PNOL_CHECK(launch_check());
     // test hook (tests/test_gpu_solvers.py): report a non-positive pivot so the callers' LU
@@ -1699,6 +1811,71 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
             return launch_check();
         }
     return PNOL_OK;
+}
+
+int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo,
+                        int variant, const double* xbase, double* xnext) {
+    CholWs w;
+    const bool persist = chol_persistent(variant) && (n + NB - 1) / NB >= 2;
+    PNOL_CHECK(chol_ws(ctx, n, persist, w));
+    const int T = w.T, N = w.N;
+    for (int k = -1; k <= (persist ? -1 : T - 2); ++k) {
+        const int R = T - 1 - k;
+        const int grid = k < 0 ? 2 + std::min(N, 1024) : R + R * (R + 1) / 2;
+        const int epoch = ++ctx->chol4_epoch;
+        hipLaunchKernelGGL(k_chol_step, dim3(grid), dim3(256), 0, ctx->stream, w.P, w.Lm, w.ldp, T, k, w.W, w.bv, w.zv,
+                           w.rowflag, epoch, dinfo, A, (long)lda, n, rhs, w.pf, persist ? w.npf : 0);
+    }
+    if (persist) PNOL_CHECK(chol_persist_launch(ctx, w, dinfo, RedArgs{}));
+    return chol_bwd_launch(ctx, w, n, sigma, dinfo, xbase, xnext);
+}
+
+// The reducing form's prep: the persistent form's progress words -- the tile versions and b's
+// block-row words at -1 (not yet stored by the reduce tasks), the rest 0 --, b's padding past n,
+// P's padding (identity on the diagonal past n, as the copy of A gives), info = 0.
+__global__ __launch_bounds__(256) void k_chol_reducing_prep(double* __restrict__ P, long ldp, int T, int n,
+                                                            double* __restrict__ bv, int* __restrict__ pflags,
+                                                            int npflags, int* __restrict__ info) {
+    const int N = T * NB, tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+    const int b0 = 2 * T, v1 = 3 * T + T * T;   // [bcnt | ver]
+    for (int q = tid; q < npflags; q += nth) pflags[q] = (q >= b0 && q < v1) ? -1 : 0;
+    for (int r = n + tid; r < N; r += nth) bv[r] = 0.0;
+    if (n < N) {
+        const long pad = (long)(N - n) * N + (long)n * (N - n);   // rows >= n, then columns >= n of rows < n
+        for (long e = tid; e < pad; e += nth) {
+            int r, c;
+            if (e < (long)(N - n) * N) {
+                r = n + (int)(e / N);
+                c = (int)(e % N);
+            } else {
+                const long f = e - (long)(N - n) * N;
+                r = (int)(f / (N - n));
+                c = n + (int)(f % (N - n));
+            }
+            P[(long)r * ldp + c] = r == c ? 1.0 : 0.0;
+        }
+    }
+    if (tid == 0) *info = 0;
+}
+
+int launch_chol_reducing(pnol_ctx* ctx, const double* part, int sub, const double* jp, int n, double lambda,
+                         double* rhs, double* sigma, int* dinfo, const double* xbase, double* xnext) {
+    if (!part || !jp || !rhs || !sigma || !dinfo || n <= NB || sub < 1) return PNOL_ERR_ARG;
+    CholWs w;
+    PNOL_CHECK(chol_ws(ctx, n, true, w));
+    const long pad = (long)(w.N - n) * w.N + (long)n * (w.N - n), work = std::max<long>(pad, w.npf);
+    hipLaunchKernelGGL(k_chol_reducing_prep, dim3((unsigned)std::max<long>(1, std::min<long>(1024, (work + 255) / 256))),
+                       dim3(256), 0, ctx->stream, w.P, w.ldp, w.T, n, w.bv, w.pf, w.npf, dinfo);
+    PNOL_CHECK(launch_check());
+    RedArgs red;
+    red.part = part;
+    red.sub = sub;
+    red.n = n;
+    red.lambda = lambda;
+    red.jp = jp;
+    red.rhs = rhs;
+    PNOL_CHECK(chol_persist_launch(ctx, w, dinfo, red));
+    return chol_bwd_launch(ctx, w, n, sigma, dinfo, xbase, xnext);
 }
 
 }  // namespace pnol

@@ -756,6 +756,49 @@ int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h,
     return rhs ? launch_jtr(ctx, JT, ldjt, m, n, F0, rhs) : PNOL_OK;
 }
 
+// One LM trip's linear algebra with A never formed (single process, n > PNOL_SEQ_MAX,
+// LevenbergMarquardt.cpp:55-90): the FD Jacobian, the J^T J split-K partials (k_syrk_tile) and
+// the -J^T F slice partials on the context stream, then the persistent tile Cholesky whose first
+// tasks sum both into its padded matrix and b (launch_chol_reducing) -- the reduce launch and the
+// copy of A into the Cholesky's matrix are gone, and the reduce's HBM stream runs beside the
+// chain's first steps -- the backward solve and xnext = x + sigma.  JT, rhs, sigma, xnext and the
+// solve status are bitwise those of launch_fd_jtj (+ rhs) and launch_chol_solve; for the LU
+// fallback launch_jtj_from_partials forms A from the trip's partials.
+int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
+                           double* JT, int ldjt, double lambda, double* rhs, double* sigma, int* dinfo, double* xnext) {
+    if (!o || !x || !h || !F0 || !JT || !rhs || !sigma || !dinfo || !xnext || ldjt < o->m) return PNOL_ERR_ARG;
+    const int n = o->n, m = o->m;
+    if (n <= PNOL_SEQ_MAX) return PNOL_ERR_ARG;
+    const int nt = (n + kTile - 1) / kTile;
+    const int ntiles = nt * (nt + 1) / 2;
+    const SliceCfg sc = slice_cfg(m, ntiles);
+    void *part = nullptr, *jp = nullptr;
+    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * kS * sc.sub * kTile * kTile, &part));
+    PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
+    PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
+    syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
+                  syrk_t64(false));
+    PNOL_CHECK(launch_check());
+    PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F0));
+    ScopedTimer tm(ctx, "solve");
+    return launch_chol_reducing(ctx, (const double*)part, sc.sub, (const double*)jp, n, lambda, rhs, sigma, dinfo, x,
+                                xnext);
+}
+
+// A (lower triangle + mirror, the Marquardt diagonal) from the split-K partials of the last
+// launch_fd_normal_solve (the same reduce as launch_jtj, so the same A)
+int launch_jtj_from_partials(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda) {
+    if (!A || m <= 0 || n <= PNOL_SEQ_MAX || lda < n) return PNOL_ERR_ARG;
+    const int nt = (n + kTile - 1) / kTile;
+    const int ntiles = nt * (nt + 1) / 2;
+    const SliceCfg sc = slice_cfg(m, ntiles);
+    void* part = nullptr;
+    PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * kS * sc.sub * kTile * kTile, &part));
+    launch_reduce(dim3(kTile / 32, ntiles), dim3(256), 0, ctx->stream, (const double*)part, ntiles, sc.sub, n, lambda,
+                  A, (long)lda, (double*)nullptr, 0);
+    return launch_check();
+}
+
 // J^T J with the 128 x 128 tiles split over the communicator's ranks (contiguous ranges of
 // tpr = ceil(ntiles / P) tiles), then one allgather of the packed tiles (P * tpr * 128 KB).
 // Each tile is summed exactly as on one GPU (same K split, same slice tree): A is bitwise

@@ -184,6 +184,12 @@ int launch_gather_rows(pnol_ctx* ctx, const double* D, int ldd, const int* ridx,
 // rhs (nullable): also rhs = -J^T F (bitwise launch_jtr), its slice tree in the reduce launch
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                double* jtj_diag, const double* F = nullptr, double* rhs = nullptr);
+// One LM trip's linear algebra without forming A (syrk.hip): FD Jacobian, J^T J split-K
+// partials, -J^T F slice partials, then launch_chol_reducing; A only on request from the
+// partials of the last trip (the LU fallback)
+int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
+                           double* JT, int ldjt, double lambda, double* rhs, double* sigma, int* dinfo, double* xnext);
+int launch_jtj_from_partials(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda);
 int launch_jtj_sharded(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                        double* jtj_diag);
 int launch_jtr(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
@@ -200,6 +206,13 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
                         int variant, const double* xbase = nullptr, double* xnext = nullptr);
 int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n, int method,
                  int* info);
+// The LM trip's damped solve from the J^T J split-K partials (chol.hip): the persistent tile
+// Cholesky whose first tasks reduce the partials (part: k_syrk_tile's 128 x 128 layout, `sub`
+// chunks per m-slice) and the -J^T F slice partials jp into its padded matrix and b (rhs gets
+// -J^T F too), then the factorisation, the backward solve and xnext = xbase + sigma; bitwise the
+// reduce into A + launch_chol_solve
+int launch_chol_reducing(pnol_ctx* ctx, const double* part, int sub, const double* jp, int n, double lambda,
+                         double* rhs, double* sigma, int* dinfo, const double* xbase, double* xnext);
 
 int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
 // rows [r0, r1) only (multiples of 64 but r1 = m; r1 < 0: all): a row-sharded LevMarqMPI rank

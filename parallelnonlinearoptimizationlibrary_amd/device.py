@@ -135,6 +135,23 @@ class Context:
         L.check(L.lib().pnol_lm_fd_mode(self.h, C.byref(v)), "pnol_lm_fd_mode")
         return v.value
 
+    def solve_step(self, A, rhs, x):
+        """The LM loop's solve (pnol_solve_step_d): sigma = A^{-1} rhs by the tile Cholesky (A kept)
+        and xnext = x + sigma.  Returns (sigma, xnext, info) -- info read back (synchronises)."""
+        n = rhs.numel()
+        sigma, xnext = self.empty(n), self.empty(n)
+        info = self.torch.zeros(2, dtype=self.torch.int32, device=f"cuda:{self.device}")
+        L.check(L.lib().pnol_solve_step_d(self.h, _ptr(A), A.stride(0), _ptr(rhs), _ptr(sigma), n, _ptr(info),
+                                          _ptr(x), _ptr(xnext)), "pnol_solve_step_d")
+        return sigma, xnext, int(info[0].item())
+
+    def lm_trip_normal(self, m, n, lam, A=None):
+        """A = J^T J + Marquardt diagonal from the last LM trip's partials (pnol_lm_trip_normal_d)."""
+        A = self.empty(n, n) if A is None else A
+        L.check(L.lib().pnol_lm_trip_normal_d(self.h, m, n, C.c_double(lam), _ptr(A), A.stride(0)),
+                "pnol_lm_trip_normal_d")
+        return A
+
     def solve(self, A, rhs, method=0):
         """sigma = A^{-1} rhs; A is overwritten.  Returns (sigma, info)."""
         n = rhs.numel()
@@ -228,6 +245,18 @@ class DeviceObjective:
                                          JT.stride(0), C.c_double(lam), _ptr(A), A.stride(0), None, _ptr(rhs)),
                 "pnol_fd_normal_d")
         return F0, JT, A, rhs
+
+    def lm_trip(self, x, h, lam, JT, F0=None, compute_f0=True):
+        """One LM trip's linear algebra without forming A (pnol_lm_trip_d).
+        Returns (F0, JT, rhs, sigma, xnext, info) -- info read back (synchronises)."""
+        t = self.ctx.torch
+        F0 = self.ctx.empty(self.m) if F0 is None else F0
+        rhs, sigma, xnext = self.ctx.empty(self.n), self.ctx.empty(self.n), self.ctx.empty(self.n)
+        info = t.zeros(2, dtype=t.int32, device=f"cuda:{self.ctx.device}")
+        L.check(L.lib().pnol_lm_trip_d(self.ctx.h, self.h, _ptr(x), _ptr(h), _ptr(F0), int(compute_f0), _ptr(JT),
+                                       JT.stride(0), C.c_double(lam), _ptr(rhs), _ptr(sigma), _ptr(info), _ptr(xnext)),
+                "pnol_lm_trip_d")
+        return F0, JT, rhs, sigma, xnext, int(info[0].item())
 
     def lm_jacobian_mpi(self, x, h, JTs=None, F0=None, compute_f0=True):
         """The m-sliced J^T this rank's share of the normal equations reads (pnol_lm_jacobian_mpi_d).

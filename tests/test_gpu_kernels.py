@@ -683,6 +683,55 @@ def test_fd_normal_bitwise(ctx, m, n):
         assert np.array_equal(_np(rb), _np(ra)), rep
 
 
+@pytest.mark.parametrize("m,n", [(16384, 2048), (5000, 1000), (777, 129), (3000, 257), (2000, 700)])
+def test_lm_trip_bitwise(ctx, m, n):
+    """The LM trip without A (pnol_lm_trip_d: the persistent Cholesky's first tasks sum the J^T J
+    split-K partials and the -J^T F slice partials into its own matrix and b) gives JT, F0, rhs,
+    sigma, x + sigma and the solve status bitwise those of pnol_fd_normal_d + pnol_solve_step_d,
+    over repeated trips at new points and lambdas; the A the LU fallback forms from the trip's
+    partials (pnol_lm_trip_normal_d) is bitwise pnol_fd_normal_d's A."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    d = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+    h = ctx.tensor(np.full(n, 1e-7))
+    JTa, Aa, ra, JTb = ctx.empty(n, m), ctx.empty(n, n), ctx.empty(n), ctx.empty(n, m)
+    for rep, (lo, lam) in enumerate(((-0.5, 0.37), (-0.25, 1e-3), (0.1, 20.0))):
+        x = ctx.tensor(np.linspace(lo, 0.5, n))
+        F0a, JTa, Aa, ra = d.fd_normal(x, h, lam, JTa, Aa, ra)
+        sa, xa, ia = ctx.solve_step(Aa, ra, x)
+        F0b, JTb, rb, sb, xb, ib = d.lm_trip(x, h, lam, JTb)
+        ctx.synchronize()
+        assert ia == 0 and ib == 0, (rep, ia, ib)
+        assert np.array_equal(_np(JTb), _np(JTa)), rep
+        assert np.array_equal(_np(F0b), _np(F0a)), rep
+        assert np.array_equal(_np(rb), _np(ra)), rep
+        assert np.array_equal(_np(sb), _np(sa)), rep
+        assert np.array_equal(_np(xb), _np(xa)), rep
+        Ab = ctx.lm_trip_normal(m, n, lam)
+        ctx.synchronize()
+        assert np.array_equal(_np(Ab), _np(Aa)), rep
+
+
+def test_lm_trip_reports_non_spd(ctx):
+    """A non-positive pivot met by the fused trip's Cholesky is reported in the status word (the
+    LM loop then forms A from the partials and redoes the solve with the LU), and the next trip
+    on the same context is sound again."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    n = 300
+    d = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, 200)   # 200 residuals: J^T J singular
+    x, h = ctx.tensor(np.linspace(-0.5, 0.5, n)), ctx.tensor(np.full(n, 1e-7))
+    *_, info = d.lm_trip(x, h, 0.0, ctx.empty(n, 200))
+    assert info != 0
+    d2 = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, 1000)
+    JTa, Aa, ra = ctx.empty(n, 1000), ctx.empty(n, n), ctx.empty(n)
+    F0a, JTa, Aa, ra = d2.fd_normal(x, h, 0.5, JTa, Aa, ra)
+    sa, _, ia = ctx.solve_step(Aa, ra, x)
+    *_, sb, _, ib = d2.lm_trip(x, h, 0.5, ctx.empty(n, 1000))
+    assert ia == 0 and ib == 0
+    assert np.array_equal(_np(sb), _np(sa))
+
+
 def test_synthetic_data_matches_oracle_stream(ctx, oracle):
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective

@@ -564,6 +564,30 @@ def test_lm_one_wait_loop_lu_fallback_equals_general_loop(ctx, oracle, m, n, mon
     assert rel(Xa, Xo) <= 1e-10
 
 
+@pytest.mark.parametrize("m,n,force", [(3000, 257, "0"), (2000, 700, "0"), (3000, 257, "1")])
+def test_lm_fused_trip_loop_equals_general_loop(ctx, oracle, m, n, force, monkeypatch):
+    """The one-wait LM loop with the fused trip (pnol_lm_trip_d, the default) replays the
+    one-wait loop with the two calls (PNOL_LM_TRIP=0) and the general loop (PNOL_LM_ASYNC=0)
+    bitwise -- X, F0, FOpt, evaluation count -- also with the LU fallback forced on every trip
+    (force = 1: A formed from the trip's partials, pnol_lm_trip_normal_d)."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_levmarq
+    A, xs, y = oracle.linres_data(m, n)
+    params = (0.001, 10, 1e-7, 8, 0.0, -1)
+    monkeypatch.setenv("PNOL_CHOL_FORCE_FALLBACK", force)
+    out = {}
+    for name, mode, trip in (("fused", "1", "1"), ("two_call", "1", "0"), ("general", "0", "0")):
+        monkeypatch.setenv("PNOL_LM_ASYNC", mode)
+        monkeypatch.setenv("PNOL_LM_TRIP", trip)
+        out[name] = run_levmarq(_obj(ctx, L.OBJ_LINRES, n, m, A, y), np.zeros(n), params)
+    for a, b in (("fused", "two_call"), ("two_call", "general")):
+        (Xa, F0a, FOa, ra), (Xs, F0s, FOs, rs) = out[a], out[b]
+        assert np.array_equal(Xa, Xs), (a, b, rel(Xa, Xs))
+        assert np.array_equal(F0a, F0s) and np.array_equal(FOa, FOs), (a, b)
+        assert ra.evals == rs.evals, (a, b)
+    assert rel(out["fused"][0], xs) <= 1e-8
+
+
 @pytest.mark.parametrize("n", [1, 7, 100, 300])
 def test_matrix_inverse_bitwise(ctx, oracle, n):
     """pnol_matrix_inverse_d (one elimination of [B | I], per-column back substitution) equals
