@@ -1311,13 +1311,15 @@ struct RedArgs {
     double* rhs = nullptr;          // rhs = -J^T F, for the LU fallback
 };
 
+template <int SUB>
 __device__ __forceinline__ void red_pair(const double* __restrict__ p, long off, int sub, double& vx, double& vy) {
     constexpr long E = 128L * 128L;
     double lx[8], ly[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
         double ax = 0.0, ay = 0.0;
-        for (int u = 0; u < sub; ++u) {
+#pragma unroll
+        for (int u = 0; u < (SUB > 0 ? SUB : sub); ++u) {
             const double2 w = *reinterpret_cast<const double2*>(p + (long)(s * sub + u) * E + off);
             ax += w.x;
             ay += w.y;
@@ -1356,19 +1358,32 @@ __device__ void red_task(int u, const RedArgs& red, double* __restrict__ P, long
     const long tt = (long)ti * (ti + 1) / 2 + tj;
     const double* p = red.part + tt * 8 * red.sub * (128L * 128L);
     const double scale = 1 + red.lambda;
-    for (int q = t; q < NB * NB / 2; q += 256) {   // element pairs (r, c), (r, c + 1)
-        const int rr = q >> 5, c = 2 * (q & 31);
-        double v2[2];
-        red_pair(p, (long)(64 * (I & 1) + rr) * 128 + 64 * (J & 1) + c, red.sub, v2[0], v2[1]);
-        const int i = I * NB + rr;
+    // two element pairs per step (the loads of both in flight; 2 x 8 x sub 16-byte loads)
+    auto pairs = [&](auto SUBC) {
+        constexpr int S = decltype(SUBC)::value;
+        for (int q0 = t; q0 < NB * NB / 2; q0 += 512) {   // element pairs (r, c), (r, c + 1)
+            double v[2][2];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int j = J * NB + c + h;
-            if (i >= red.n || j >= red.n || j > i) continue;
-            stg<true>(P + (long)i * ldp + j, i == j ? scale * v2[h] : v2[h]);
-            if (j < i && I == J) stg<true>(P + (long)j * ldp + i, v2[h]);   // the mirror inside the diagonal tile
+            for (int w = 0; w < 2; ++w) {
+                const int q = q0 + 256 * w, rr = q >> 5, c = 2 * (q & 31);
+                red_pair<S>(p, (long)(64 * (I & 1) + rr) * 128 + 64 * (J & 1) + c, red.sub, v[w][0], v[w][1]);
+            }
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                const int q = q0 + 256 * w, rr = q >> 5, c = 2 * (q & 31);
+                const int i = I * NB + rr;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int j = J * NB + c + h;
+                    if (i >= red.n || j >= red.n || j > i) continue;
+                    stg<true>(P + (long)i * ldp + j, i == j ? scale * v[w][h] : v[w][h]);
+                    if (j < i && I == J) stg<true>(P + (long)j * ldp + i, v[w][h]);   // the mirror inside the diagonal tile
+                }
+            }
         }
-    }
+    };
+    if (red.sub == 2) pairs(std::integral_constant<int, 2>{});
+    else pairs(std::integral_constant<int, 0>{});
     publish(pw.ver + I * T + J, 0);
 }
 
