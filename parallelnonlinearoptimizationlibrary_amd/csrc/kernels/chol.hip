@@ -1305,12 +1305,16 @@ __device__ __forceinline__ void publish(int* w, int v) {
 // bitwise the one of A.
 struct RedArgs {
     const double* part = nullptr;   // nullptr: not the reducing form
+    const int* cnt = nullptr;       // tile t's partials are complete once cnt[t] == split (nullptr: all are)
+    int split = 0;
     int sub = 0, n = 0;
     double lambda = 0.0;
     const double* jp = nullptr;     // the 8 -J^T F slice partials (jp[s n + e])
     double* rhs = nullptr;          // rhs = -J^T F, for the LU fallback
 };
 
+// (the partials are read with sc1 loads: in the gated LM trip they were stored write-through by
+// the J^T J running beside this launch, handed off by the tile counter)
 template <int SUB>
 __device__ __forceinline__ void red_pair(const double* __restrict__ p, long off, int sub, double& vx, double& vy) {
     constexpr long E = 128L * 128L;
@@ -1320,7 +1324,7 @@ __device__ __forceinline__ void red_pair(const double* __restrict__ p, long off,
         double ax = 0.0, ay = 0.0;
 #pragma unroll
         for (int u = 0; u < (SUB > 0 ? SUB : sub); ++u) {
-            const double2 w = *reinterpret_cast<const double2*>(p + (long)(s * sub + u) * E + off);
+            const double2 w = ld16_sc1(p + (long)(s * sub + u) * E, (unsigned)(off * 8));
             ax += w.x;
             ay += w.y;
         }
@@ -1333,7 +1337,7 @@ __device__ __forceinline__ void red_pair(const double* __restrict__ p, long off,
 
 // reduce task u of the reducing form: u = 0 b, u >= 1 the (u-1)-th lower 64 x 64 tile in column order
 __device__ void red_task(int u, const RedArgs& red, double* __restrict__ P, long ldp, int T, double* __restrict__ bv,
-                         const PersistWords& pw) {
+                         const PersistWords& pw, int* __restrict__ info) {
     const int t = threadIdx.x;
     if (u == 0) {
         for (int e = t; e < red.n; e += 256) {
@@ -1356,6 +1360,12 @@ __device__ void red_task(int u, const RedArgs& red, double* __restrict__ P, long
     }
     const int I = J + r, ti = I >> 1, tj = J >> 1;
     const long tt = (long)ti * (ti + 1) / 2 + tj;
+    if (red.cnt) {   // the tile's partials: every split-K unit's counter add, after its stores drained
+        __shared__ int ok_red;
+        if (t == 0) ok_red = spin_ge(red.cnt + tt, red.split, info);
+        __syncthreads();
+        if (!ok_red) return;
+    }
     const double* p = red.part + tt * 8 * red.sub * (128L * 128L);
     const double scale = 1 + red.lambda;
     // two element pairs per step (the loads of both in flight; 2 x 8 x sub 16-byte loads)
@@ -1473,7 +1483,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         __syncthreads();   // task_sh is rewritten by the next claim
         if (g >= nred + ntasks) return;
         if (g < nred) {
-            red_task(g, red, P, ldp, T, bv, pw);
+            red_task(g, red, P, ldp, T, bv, pw, info);
             continue;
         }
         g -= nred;
@@ -1726,15 +1736,8 @@ int launch_chol_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs
     return launch_chol_solve_v(ctx, A, lda, rhs, sigma, n, dinfo, 0, xbase, xnext);
 }
 
-// The tile Cholesky's workspace (the per-step / persistent forms and the reducing form)
-struct CholWs {
-    int T = 0, N = 0;
-    long ldp = 0;
-    double *P = nullptr, *Lm = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr;
-    int *rowflag = nullptr, *bwdflag = nullptr, *pf = nullptr;
-    int npf = 0;
-    bool gran = false;
-};
+// The tile Cholesky's workspace (CholWs, pnol_internal.hpp): the per-step / persistent forms and
+// the reducing form
 
 static int chol_ws(pnol_ctx* ctx, int n, bool persist, CholWs& w) {
     w.T = (n + NB - 1) / NB;
@@ -1779,7 +1782,7 @@ static int chol_ws(pnol_ctx* ctx, int n, bool persist, CholWs& w) {
 }
 
 // k_chol_persist: steps 0 .. T-2 (the reducing form: the reduce tasks first, and tile 0 too)
-static int chol_persist_launch(pnol_ctx* ctx, const CholWs& w, int* dinfo, const RedArgs& red) {
+static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, int* dinfo, const RedArgs& red) {
     const int T = w.T;
     int ntasks = 0;
     for (int R = T - 1; R >= 1; --R) ntasks += R + R * (R + 1) / 2 - 1;
@@ -1799,22 +1802,22 @@ static int chol_persist_launch(pnol_ctx* ctx, const CholWs& w, int* dinfo, const
     const int want = ew ? std::atoi(ew) : slots;
     const int nred = red.part ? 1 + T * (T + 1) / 2 : 0;
     const int workers = std::max(1, std::min(ntasks + nred, want));
-    hipLaunchKernelGGL(k_chol_persist, dim3(1 + workers), dim3(256), 0, ctx->stream, w.P, w.Lm, w.ldp, T, w.W, w.bv,
-                       w.zv, w.pf, ntasks, dinfo, lookahead, red);
+    hipLaunchKernelGGL(k_chol_persist, dim3(1 + workers), dim3(256), 0, st, w.P, w.Lm, w.ldp, T, w.W, w.bv, w.zv, w.pf,
+                       ntasks, dinfo, lookahead, red);
     return launch_check();
 }
 
 // the backward solve (+ the trial point)
-static int chol_bwd_launch(pnol_ctx* ctx, const CholWs& w, int n, double* sigma, int* dinfo, const double* xbase,
-                           double* xnext) {
+static int chol_bwd_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, int n, double* sigma, int* dinfo,
+                           const double* xbase, double* xnext) {
     const int epoch = ++ctx->chol4_epoch;
     if (w.gran && ((uintptr_t)w.xw & 15) != 0) return PNOL_ERR_ARG;   // granules need 16-byte alignment
     if (w.gran)
-        hipLaunchKernelGGL(k_chol_bwd<true>, dim3(w.T), dim3(256), 0, ctx->stream, (const double*)w.Lm, w.ldp, w.T, n,
+        hipLaunchKernelGGL(k_chol_bwd<true>, dim3(w.T), dim3(256), 0, st, (const double*)w.Lm, w.ldp, w.T, n,
                            (const double*)w.W, (const double*)w.bv, (const double*)w.zv, w.xw, sigma, w.bwdflag, epoch,
                            dinfo, xbase, xnext);
     else
-        hipLaunchKernelGGL(k_chol_bwd<false>, dim3(w.T), dim3(256), 0, ctx->stream, (const double*)w.Lm, w.ldp, w.T, n,
+        hipLaunchKernelGGL(k_chol_bwd<false>, dim3(w.T), dim3(256), 0, st, (const double*)w.Lm, w.ldp, w.T, n,
                            (const double*)w.W, (const double*)w.bv, (const double*)w.zv, w.xw, sigma, w.bwdflag, epoch,
                            dinfo, xbase, xnext);
     PNOL_CHECK(launch_check());
@@ -1822,7 +1825,7 @@ static int chol_bwd_launch(pnol_ctx* ctx, const CholWs& w, int n, double* sigma,
     // fallback paths run on an SPD system (read per call: the tests flip it)
     if (const char* e = std::getenv("PNOL_CHOL_FORCE_FALLBACK"))
         if (std::atoi(e) != 0) {
-            hipLaunchKernelGGL(k_flag_info, dim3(1), dim3(1), 0, ctx->stream, dinfo, 1);
+            hipLaunchKernelGGL(k_flag_info, dim3(1), dim3(1), 0, st, dinfo, 1);
             return launch_check();
         }
     return PNOL_OK;
@@ -1841,8 +1844,8 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
         hipLaunchKernelGGL(k_chol_step, dim3(grid), dim3(256), 0, ctx->stream, w.P, w.Lm, w.ldp, T, k, w.W, w.bv, w.zv,
                            w.rowflag, epoch, dinfo, A, (long)lda, n, rhs, w.pf, persist ? w.npf : 0);
     }
-    if (persist) PNOL_CHECK(chol_persist_launch(ctx, w, dinfo, RedArgs{}));
-    return chol_bwd_launch(ctx, w, n, sigma, dinfo, xbase, xnext);
+    if (persist) PNOL_CHECK(chol_persist_launch(ctx, ctx->stream, w, dinfo, RedArgs{}));
+    return chol_bwd_launch(ctx, ctx->stream, w, n, sigma, dinfo, xbase, xnext);
 }
 
 // The reducing form's prep: the persistent form's progress words -- the tile versions and b's
@@ -1873,24 +1876,37 @@ __global__ __launch_bounds__(256) void k_chol_reducing_prep(double* __restrict__
     if (tid == 0) *info = 0;
 }
 
-int launch_chol_reducing(pnol_ctx* ctx, const double* part, int sub, const double* jp, int n, double lambda,
-                         double* rhs, double* sigma, int* dinfo, const double* xbase, double* xnext) {
-    if (!part || !jp || !rhs || !sigma || !dinfo || n <= NB || sub < 1) return PNOL_ERR_ARG;
-    CholWs w;
-    PNOL_CHECK(chol_ws(ctx, n, true, w));
+int launch_chol_reducing_prep(pnol_ctx* ctx, int n, int* dinfo, CholRed& cr) {
+    if (!dinfo || n <= NB) return PNOL_ERR_ARG;
+    cr.n = n;
+    cr.dinfo = dinfo;
+    return chol_ws(ctx, n, true, cr.w);
+}
+
+int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr) {
+    const CholWs& w = cr.w;
+    const int n = cr.n;
     const long pad = (long)(w.N - n) * w.N + (long)n * (w.N - n), work = std::max<long>(pad, w.npf);
     hipLaunchKernelGGL(k_chol_reducing_prep, dim3((unsigned)std::max<long>(1, std::min<long>(1024, (work + 255) / 256))),
-                       dim3(256), 0, ctx->stream, w.P, w.ldp, w.T, n, w.bv, w.pf, w.npf, dinfo);
-    PNOL_CHECK(launch_check());
+                       dim3(256), 0, ctx->stream, w.P, w.ldp, w.T, n, w.bv, w.pf, w.npf, cr.dinfo);
+    return launch_check();
+}
+
+int launch_chol_reducing_run(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, const double* part, int sub,
+                             const int* cnt, int split, const double* jp, double lambda, double* rhs, double* sigma,
+                             const double* xbase, double* xnext) {
+    if (!part || !jp || !rhs || !sigma || sub < 1) return PNOL_ERR_ARG;
     RedArgs red;
     red.part = part;
+    red.cnt = cnt;
+    red.split = split;
     red.sub = sub;
-    red.n = n;
+    red.n = cr.n;
     red.lambda = lambda;
     red.jp = jp;
     red.rhs = rhs;
-    PNOL_CHECK(chol_persist_launch(ctx, w, dinfo, red));
-    return chol_bwd_launch(ctx, w, n, sigma, dinfo, xbase, xnext);
+    PNOL_CHECK(chol_persist_launch(ctx, st, cr.w, cr.dinfo, red));
+    return chol_bwd_launch(ctx, st, cr.w, cr.n, sigma, cr.dinfo, xbase, xnext);
 }
 
 }  // namespace pnol

@@ -74,6 +74,25 @@ struct pnol_ctx {
     hipStream_t comm_stream = nullptr;
     std::vector<hipEvent_t> phase_events;
     hipEvent_t comm_done = nullptr;
+    // the LM trip's wait-value gate (launch_fd_normal_solve): a signal word the J^T J's
+    // last-dispatched workgroup stores, and the value of the last launch
+    unsigned* tail_flag = nullptr;
+    unsigned tail_epoch = 0;
+};
+
+// The tile Cholesky's workspace for order n (chol.hip)
+struct CholWs {
+    int T = 0, N = 0;
+    long ldp = 0;
+    double *P = nullptr, *Lm = nullptr, *W = nullptr, *bv = nullptr, *zv = nullptr, *xw = nullptr;
+    int *rowflag = nullptr, *bwdflag = nullptr, *pf = nullptr;
+    int npf = 0;
+    bool gran = false;
+};
+struct CholRed {   // the LM trip's reducing Cholesky (launch_chol_reducing_*)
+    CholWs w;
+    int n = 0;
+    int* dinfo = nullptr;
 };
 
 struct pnol_dobj {
@@ -206,13 +225,18 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
                         int variant, const double* xbase = nullptr, double* xnext = nullptr);
 int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n, int method,
                  int* info);
-// The LM trip's damped solve from the J^T J split-K partials (chol.hip): the persistent tile
+// The LM trip's damped solve from the J^T J split-K partials (chol.hip): _prep takes the
+// workspace (before anything is queued: an allocation may free); _start queues the prep launch
+// (progress words, paddings, info) on the context stream; _run queues on `st` the persistent tile
 // Cholesky whose first tasks reduce the partials (part: k_syrk_tile's 128 x 128 layout, `sub`
-// chunks per m-slice) and the -J^T F slice partials jp into its padded matrix and b (rhs gets
-// -J^T F too), then the factorisation, the backward solve and xnext = xbase + sigma; bitwise the
-// reduce into A + launch_chol_solve
-int launch_chol_reducing(pnol_ctx* ctx, const double* part, int sub, const double* jp, int n, double lambda,
-                         double* rhs, double* sigma, int* dinfo, const double* xbase, double* xnext);
+// chunks per m-slice; tile t's once cnt[t] == split, nullptr: complete) and the -J^T F slice
+// partials jp into its padded matrix and b (rhs gets -J^T F too), then the factorisation, the
+// backward solve and xnext = xbase + sigma; bitwise the reduce into A + launch_chol_solve
+int launch_chol_reducing_prep(pnol_ctx* ctx, int n, int* dinfo, CholRed& cr);
+int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr);
+int launch_chol_reducing_run(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, const double* part, int sub,
+                             const int* cnt, int split, const double* jp, double lambda, double* rhs, double* sigma,
+                             const double* xbase, double* xnext);
 
 int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
 // rows [r0, r1) only (multiples of 64 but r1 = m; r1 < 0: all): a row-sharded LevMarqMPI rank
