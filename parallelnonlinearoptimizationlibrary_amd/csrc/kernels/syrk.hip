@@ -140,7 +140,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                                                       unsigned* __restrict__ tail_flag = nullptr,
                                                       unsigned tail_val = 0, int* __restrict__ tile_cnt = nullptr) {
     if constexpr (CNT)
-        if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+        if (tail_flag && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)   // (no gate: nullptr)
             __hip_atomic_store(tail_flag, tail_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     constexpr int NT = 64 * NW, WC = NW / 2;
     constexpr int WTM = TILE / 2, WTN = TILE / WC, NBM = WTM / 16, NBN = WTN / 16;
