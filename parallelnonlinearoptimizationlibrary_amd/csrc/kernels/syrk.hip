@@ -861,7 +861,7 @@ int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
     PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
     PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F0));
     PNOL_CHECK(launch_chol_reducing_start(ctx, cr));   // the prep launch (words, paddings, info)
-    PNOL_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)ntiles, ctx->stream));
+    if (gate) PNOL_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)ntiles, ctx->stream));
     hipStream_t cs = ctx->stream;
     if (gate) {
         PNOL_HIP(hipEventRecord(ctx->aux_events[0], ctx->stream));
@@ -869,18 +869,22 @@ int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
         PNOL_HIP(hipStreamWaitValue32(ctx->aux_stream, tf, tv, hipStreamWaitValueGte, 0xffffffffu));
         cs = ctx->aux_stream;
     }
-    {
+    if (gate) {   // write-through partials + tile counters: the Cholesky reads tiles in flight
         const dim3 grid(ntiles * split);
         LaunchTimer tm(ctx, "syrk");
         hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, 8, true>), grid, dim3(512), 0, ctx->stream, tm.start(), tm.stop(),
                               0, JT, (long)ldjt, n, m, split, sc.kfirst, sc.kchunk, sc.sub, 0, sc.mS, (long)sc.mS,
                               (double*)part, 0, tf, tv, (int*)cnt);
         PNOL_CHECK(launch_check());
+    } else {      // stream order: the plain SYRK (non-temporal partials, no counters)
+        syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
+                      syrk_t64(false));
+        PNOL_CHECK(launch_check());
     }
     {
         ScopedTimer tm(ctx, "solve", cs);
-        PNOL_CHECK(launch_chol_reducing_run(ctx, cs, cr, (const double*)part, sc.sub, (const int*)cnt, split,
-                                            (const double*)jp, lambda, rhs, sigma, x, xnext));
+        PNOL_CHECK(launch_chol_reducing_run(ctx, cs, cr, (const double*)part, sc.sub, gate ? (const int*)cnt : nullptr,
+                                            split, (const double*)jp, lambda, rhs, sigma, x, xnext));
     }
     if (gate) {
         PNOL_HIP(hipEventRecord(ctx->aux_events[1], ctx->aux_stream));
