@@ -191,6 +191,14 @@ int pnol_lm_eval_mpi_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, double* F
  * <= PNOL_LM_SLICES.  n > PNOL_SEQ_MAX or m > 4096. */
 int pnol_lm_normal_mpi_d(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F,
                          double* A, int lda, double* rhs, double* jtj_diag);
+/* pnol_lm_normal_mpi_d + pnol_solve_step_d without forming A (LevenbergMarquardtMPI.cpp:64-90):
+ * the allgathered J^T J tiles (one rank: its split-K partials) go straight into the persistent
+ * tile Cholesky's matrix; rhs = -(J^T F), sigma, xnext = x + sigma and *dinfo (device int) are
+ * bitwise those of the two calls.  *dinfo != 0: form A with pnol_lm_normal_unpack_mpi_d (same
+ * m, n, lambda) and solve with the LU. */
+int pnol_lm_normal_solve_mpi_d(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F,
+                               double* rhs, double* sigma, int* dinfo, const double* x, double* xnext);
+int pnol_lm_normal_unpack_mpi_d(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda);
 /* rhs = -(J^T F), LevenbergMarquardt.cpp:78-80 */
 int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
 /* sigma = A^{-1} rhs, replacing luSolve(A, rhs, sigma), LevenbergMarquardt.cpp:83.

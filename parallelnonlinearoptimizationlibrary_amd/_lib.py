@@ -88,6 +88,8 @@ _SIGS = {
     "pnol_lm_jacobian_mpi_d": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp]),
     "pnol_lm_eval_mpi_d": (_i, [_vp, _vp, _vp, _vp]),
     "pnol_lm_normal_mpi_d": (_i, [_vp, _vp, _i, _i, _d, _vp, _vp, _i, _vp, _vp]),
+    "pnol_lm_normal_solve_mpi_d": (_i, [_vp, _vp, _i, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "pnol_lm_normal_unpack_mpi_d": (_i, [_vp, _i, _i, _d, _vp, _i]),
     "pnol_lm_set_fd_mode": (_i, [_vp, _i]),
     "pnol_lm_fd_mode": (_i, [_vp, C.POINTER(C.c_int)]),
     "pnol_lm_rank_rows": (_i, [_i, _i, _i, C.POINTER(C.c_int), C.POINTER(C.c_int)]),

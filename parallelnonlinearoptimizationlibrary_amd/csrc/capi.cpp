@@ -297,6 +297,18 @@ int pnol_lm_normal_mpi_d(pnol_ctx* ctx, const double* JTs, int m, int n, double 
     return launch_lm_normal(ctx, JTs, m, n, lambda, F, A, lda, rhs, jtj_diag);
 }
 
+int pnol_lm_normal_solve_mpi_d(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F,
+                               double* rhs, double* sigma, int* dinfo, const double* x, double* xnext) {
+    PNOL_CHECK(set_device(ctx));
+    if (!JTs || !F || !rhs || !x || m <= 0) return PNOL_ERR_ARG;
+    return launch_lm_normal_solve(ctx, JTs, m, n, lambda, F, rhs, sigma, dinfo, x, xnext);
+}
+
+int pnol_lm_normal_unpack_mpi_d(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda) {
+    PNOL_CHECK(set_device(ctx));
+    return launch_lm_normal_unpack(ctx, m, n, lambda, A, lda);
+}
+
 int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs) {
     PNOL_CHECK(set_device(ctx));
     if (!JT || !F || !rhs || m <= 0 || n <= 0 || ldjt < m) return PNOL_ERR_ARG;

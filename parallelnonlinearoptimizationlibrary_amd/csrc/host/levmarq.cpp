@@ -201,7 +201,7 @@ class LMAsync {
         }
         // one trip without forming A (pnol_lm_trip_d; PNOL_LM_TRIP=0 keeps the two calls below;
         // read once per solve)
-        if (!sliced) {
+        {   // (LevMarqMPI: the normal equations and the solve in one call, A not formed either)
             const char* e = std::getenv("PNOL_LM_TRIP");
             trip_fused_ = !e || std::atoi(e) != 0;
         }
@@ -241,6 +241,14 @@ class LMAsync {
         if (sliced_) {
             check(pnol_lm_jacobian_mpi_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 3 : 1, JT_.get()),
                   "fd_jacobian");
+            if (trip_fused_) {
+                lambda_[s] = lambda;
+                check(pnol_lm_normal_solve_mpi_d(ctx_, JT_.get(), m_, n_, lambda, F(s), rhs_.get(), sig(s), info(s),
+                                                 x_[s].get(), x_[s ^ 1].get()),
+                      "normal equations + solve");
+                finish(s, false);
+                return;
+            }
             check(pnol_lm_normal_mpi_d(ctx_, JT_.get(), m_, n_, lambda, F(s), A_.get(), lda_, rhs_.get(),
                                        nullptr),
                   "normal equations");
@@ -278,7 +286,10 @@ class LMAsync {
     // the reference-order LU for a trip whose Cholesky reported a non-positive pivot (A intact)
     void redo_lu(int s) {
         check(pnol_ctx_synchronize(ctx_), "sync");
-        if (trip_fused_) check(pnol_lm_trip_normal_d(ctx_, m_, n_, lambda_[s], A_.get(), lda_), "normal equations");
+        if (trip_fused_ && sliced_)
+            check(pnol_lm_normal_unpack_mpi_d(ctx_, m_, n_, lambda_[s], A_.get(), lda_), "normal equations");
+        else if (trip_fused_)
+            check(pnol_lm_trip_normal_d(ctx_, m_, n_, lambda_[s], A_.get(), lda_), "normal equations");
         int info = 0;
         check(pnol_solve_d(ctx_, A_.get(), lda_, rhs_.get(), sig(s), n_, 2, &info), "solve");
         finish(s);

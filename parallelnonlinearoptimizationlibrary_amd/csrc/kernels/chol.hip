@@ -1311,6 +1311,12 @@ struct RedArgs {
     double lambda = 0.0;
     const double* jp = nullptr;     // the 8 -J^T F slice partials (jp[s n + e])
     double* rhs = nullptr;          // rhs = -J^T F, for the LU fallback
+    // LevMarqMPI: the J^T J tiles already summed (the allgathered packed tiles: tile t at
+    // packed + (t / tpr) slot + (t % tpr) 128^2) and rhs already formed (rhs_in)
+    const double* packed = nullptr;
+    long slot = 0;
+    int tpr = 1;
+    const double* rhs_in = nullptr;
 };
 
 // (the partials are read with sc1 loads: in the gated LM trip they were stored write-through by
@@ -1339,6 +1345,13 @@ __device__ __forceinline__ void red_pair(const double* __restrict__ p, long off,
 __device__ void red_task(int u, const RedArgs& red, double* __restrict__ P, long ldp, int T, double* __restrict__ bv,
                          const PersistWords& pw, int* __restrict__ info) {
     const int t = threadIdx.x;
+    if (u == 0 && red.rhs_in) {   // b = the rhs the caller formed
+        for (int e = t; e < red.n; e += 256) stg<true>(bv + e, red.rhs_in[e]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int i = t; i < T; i += 256) __hip_atomic_store(pw.bcnt + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     if (u == 0) {
         for (int e = t; e < red.n; e += 256) {
             double l[8];
@@ -1366,7 +1379,8 @@ __device__ void red_task(int u, const RedArgs& red, double* __restrict__ P, long
         __syncthreads();
         if (!ok_red) return;
     }
-    const double* p = red.part + tt * 8 * red.sub * (128L * 128L);
+    const double* p = red.part ? red.part + tt * 8 * red.sub * (128L * 128L) : nullptr;
+    const double* pk = red.packed ? red.packed + (tt / red.tpr) * red.slot + (tt % red.tpr) * (128L * 128L) : nullptr;
     const double scale = 1 + red.lambda;
     // two element pairs per step (the loads of both in flight; 2 x 8 x sub 16-byte loads)
     auto pairs = [&](auto SUBC) {
@@ -1376,7 +1390,14 @@ __device__ void red_task(int u, const RedArgs& red, double* __restrict__ P, long
 #pragma unroll
             for (int w = 0; w < 2; ++w) {
                 const int q = q0 + 256 * w, rr = q >> 5, c = 2 * (q & 31);
-                red_pair<S>(p, (long)(64 * (I & 1) + rr) * 128 + 64 * (J & 1) + c, red.sub, v[w][0], v[w][1]);
+                const long off = (long)(64 * (I & 1) + rr) * 128 + 64 * (J & 1) + c;
+                if (pk) {   // the summed tile (k_syrk_unpack's values)
+                    const double2 pv = *reinterpret_cast<const double2*>(pk + off);
+                    v[w][0] = pv.x;
+                    v[w][1] = pv.y;
+                } else {
+                    red_pair<S>(p, off, red.sub, v[w][0], v[w][1]);
+                }
             }
 #pragma unroll
             for (int w = 0; w < 2; ++w) {
@@ -1421,7 +1442,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
     if (blockIdx.x == 0) {   // ---------------- the diagonal chain
         const EarlyLds E{pfx, pll, pfc, ew};
         if (t < 4) ew[t] = 0;
-        const bool smode = red.part != nullptr;   // the reducing form: the chain also factors tile 0
+        const bool smode = red.part || red.packed;   // the reducing form: the chain also factors tile 0
         for (int d = smode ? 0 : 1; d < T; ++d) {
             const int k = d - 1;
 #ifdef PNOL_CHOL_TIMELINE
@@ -1475,7 +1496,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         return;
     }
 
-    const int nred = red.part ? 1 + T * (T + 1) / 2 : 0;   // the reducing form's first tasks
+    const int nred = (red.part || red.packed) ? 1 + T * (T + 1) / 2 : 0;   // the reducing form's first tasks
     for (;;) {   // ---------------- workers
         if (t == 0) task_sh = atomicAdd(pw.counter, 1);
         __syncthreads();
@@ -1509,7 +1530,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             if (!ok_sh) return;
             stage_tile<true>(X, P, ldp, i0, k0);
             if (t == 0) {   // W_k (tile 0 comes from the prep launch)
-                ok_sh = (k == 0 && !red.part) || spin_ge(pw.wdone + k, 1, info);
+                ok_sh = (k == 0 && !red.part && !red.packed) || spin_ge(pw.wdone + k, 1, info);
 #ifdef PNOL_CHOL_TIMELINE
                 if (i == k + 2) PNOL_CRIT(k, 2)
 #endif
@@ -1800,7 +1821,7 @@ static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, i
     const int lookahead = el ? std::max(0, std::atoi(el)) : 64;
     const int slots = std::max(ctx->num_cu, 1) - 1;
     const int want = ew ? std::atoi(ew) : slots;
-    const int nred = red.part ? 1 + T * (T + 1) / 2 : 0;
+    const int nred = (red.part || red.packed) ? 1 + T * (T + 1) / 2 : 0;
     const int workers = std::max(1, std::min(ntasks + nred, want));
     hipLaunchKernelGGL(k_chol_persist, dim3(1 + workers), dim3(256), 0, st, w.P, w.Lm, w.ldp, T, w.W, w.bv, w.zv, w.pf,
                        ntasks, dinfo, lookahead, red);
@@ -1853,8 +1874,10 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
 // P's padding (identity on the diagonal past n, as the copy of A gives), info = 0.
 __global__ __launch_bounds__(256) void k_chol_reducing_prep(double* __restrict__ P, long ldp, int T, int n,
                                                             double* __restrict__ bv, int* __restrict__ pflags,
-                                                            int npflags, int* __restrict__ info) {
+                                                            int npflags, int* __restrict__ info,
+                                                            int* __restrict__ zero, int nzero) {
     const int N = T * NB, tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+    for (int q = tid; q < nzero; q += nth) zero[q] = 0;   // the caller's words (the J^T J's tile counters)
     const int b0 = 2 * T, v1 = 3 * T + T * T;   // [bcnt | ver]
     for (int q = tid; q < npflags; q += nth) pflags[q] = (q >= b0 && q < v1) ? -1 : 0;
     for (int r = n + tid; r < N; r += nth) bv[r] = 0.0;
@@ -1883,12 +1906,12 @@ int launch_chol_reducing_prep(pnol_ctx* ctx, int n, int* dinfo, CholRed& cr) {
     return chol_ws(ctx, n, true, cr.w);
 }
 
-int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr) {
+int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr, int* zero, int nzero) {
     const CholWs& w = cr.w;
     const int n = cr.n;
-    const long pad = (long)(w.N - n) * w.N + (long)n * (w.N - n), work = std::max<long>(pad, w.npf);
+    const long pad = (long)(w.N - n) * w.N + (long)n * (w.N - n), work = std::max<long>({pad, (long)w.npf, (long)nzero});
     hipLaunchKernelGGL(k_chol_reducing_prep, dim3((unsigned)std::max<long>(1, std::min<long>(1024, (work + 255) / 256))),
-                       dim3(256), 0, ctx->stream, w.P, w.ldp, w.T, n, w.bv, w.pf, w.npf, cr.dinfo);
+                       dim3(256), 0, ctx->stream, w.P, w.ldp, w.T, n, w.bv, w.pf, w.npf, cr.dinfo, zero, nzero);
     return launch_check();
 }
 
@@ -1905,6 +1928,22 @@ int launch_chol_reducing_run(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, c
     red.lambda = lambda;
     red.jp = jp;
     red.rhs = rhs;
+    PNOL_CHECK(chol_persist_launch(ctx, st, cr.w, cr.dinfo, red));
+    return chol_bwd_launch(ctx, st, cr.w, cr.n, sigma, cr.dinfo, xbase, xnext);
+}
+
+// LevMarqMPI: the same from the allgathered, summed tiles (packed) and the formed rhs
+int launch_chol_reducing_run_packed(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, const double* packed, long slot,
+                                    int tpr, const double* rhs, double lambda, double* sigma, const double* xbase,
+                                    double* xnext) {
+    if (!packed || !rhs || !sigma || tpr < 1) return PNOL_ERR_ARG;
+    RedArgs red;
+    red.packed = packed;
+    red.slot = slot;
+    red.tpr = tpr;
+    red.rhs_in = rhs;
+    red.n = cr.n;
+    red.lambda = lambda;
     PNOL_CHECK(chol_persist_launch(ctx, st, cr.w, cr.dinfo, red));
     return chol_bwd_launch(ctx, st, cr.w, cr.n, sigma, cr.dinfo, xbase, xnext);
 }

@@ -860,8 +860,8 @@ int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
     }
     PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
     PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F0));
-    PNOL_CHECK(launch_chol_reducing_start(ctx, cr));   // the prep launch (words, paddings, info)
-    if (gate) PNOL_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)ntiles, ctx->stream));
+    // the prep launch (words, paddings, info; with the gate also the tile counters)
+    PNOL_CHECK(launch_chol_reducing_start(ctx, cr, gate ? (int*)cnt : nullptr, gate ? ntiles : 0));
     hipStream_t cs = ctx->stream;
     if (gate) {
         PNOL_HIP(hipEventRecord(ctx->aux_events[0], ctx->stream));
@@ -993,9 +993,20 @@ int launch_jtr(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const do
 //   3. the owner merges the nodes of its tiles; one allgather of (owned tiles + this rank's
 //      -J^T F nodes); every rank unpacks A and merges -J^T F.
 // Bitwise equal to launch_jtj + launch_jtr on the row-major J^T for every P <= kLmSlices.
-int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F, double* A,
-                     int lda, double* rhs, double* jtj_diag) {
-    if (!JTs || !F || !A || !rhs || m <= 0 || n <= 0 || lda < n) return PNOL_ERR_ARG;
+// where launch_lm_normal left the summed tiles when asked not to unpack them (A == nullptr)
+struct LmTiles {
+    bool partials = false;   // one rank: the split-K partials ("syrk_part") and -J^T F partials ("jtr_part")
+    const double* part = nullptr;
+    const double* jp = nullptr;
+    int sub = 0, split = 0;
+    const double* packed = nullptr;   // several ranks: the allgathered tiles
+    long slot = 0;
+    int tpr = 1;
+};
+
+static int lm_normal_core(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F, double* A,
+                          int lda, double* rhs, double* jtj_diag, LmTiles* out) {
+    if (!JTs || !F || !rhs || m <= 0 || n <= 0 || (A && lda < n) || (!A && !out)) return PNOL_ERR_ARG;
     if (n <= PNOL_SEQ_MAX && m <= 4096) return PNOL_ERR_UNSUPPORTED;   // reference-order kernels: row-major J^T
     const int P = comm_size(), me = comm_rank();
     if (P > kS) return PNOL_ERR_UNSUPPORTED;
@@ -1019,6 +1030,14 @@ int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lamb
         // the -J^T F tree rides in the reduce launch
         void* jp = nullptr;
         PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
+        if (!A) {   // the reducing Cholesky sums the partials itself
+            out->partials = true;
+            out->part = (const double*)part;
+            out->jp = (const double*)jp;
+            out->sub = sc.sub;
+            out->split = kS * sc.sub;
+            return PNOL_OK;
+        }
         {
             ScopedTimer tm(ctx, "syrk_reduce");
             launch_reduce(dim3(kTile / 32, ntiles + 1), dim3(256), 0, ctx->stream, (const double*)part, ntiles,
@@ -1089,9 +1108,15 @@ int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lamb
     PNOL_CHECK(comm_allgather_device(ctx, mine, (double*)packed, (size_t)slot));
     {
         ScopedTimer tm(ctx, "syrk_reduce");
-        hipLaunchKernelGGL(k_syrk_unpack, dim3(8, ntiles), dim3(256), 0, ctx->stream, (const double*)packed, ntiles, n,
-                           lambda, slot, tpr, A, (long)lda, jtj_diag);
-        PNOL_CHECK(launch_check());
+        if (A) {
+            hipLaunchKernelGGL(k_syrk_unpack, dim3(8, ntiles), dim3(256), 0, ctx->stream, (const double*)packed, ntiles,
+                               n, lambda, slot, tpr, A, (long)lda, jtj_diag);
+            PNOL_CHECK(launch_check());
+        } else {   // the reducing Cholesky reads the tiles itself
+            out->packed = (const double*)packed;
+            out->slot = slot;
+            out->tpr = tpr;
+        }
         TreeNodes tr{};
         for (int c = 0; c < NC; ++c) {
             const int lo = nodes[c].first;
@@ -1100,6 +1125,52 @@ int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lamb
         }
         hipLaunchKernelGGL(k_tree_combine, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, tr, (long)n, rhs);
     }
+    return launch_check();
+}
+
+int launch_lm_normal(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F, double* A,
+                     int lda, double* rhs, double* jtj_diag) {
+    if (!A) return PNOL_ERR_ARG;
+    return lm_normal_core(ctx, JTs, m, n, lambda, F, A, lda, rhs, jtj_diag, nullptr);
+}
+
+// LevMarqMPI's normal equations and damped solve without forming A: the tiles of
+// launch_lm_normal (summed by the slice tree over the ranks and allgathered; one rank: its
+// partials) go straight into the persistent Cholesky's matrix by its first tasks -- no unpack
+// into A, no copy of A -- then the factorisation, the backward solve and xnext = xbase + sigma.
+// rhs = -J^T F as launch_lm_normal's.  Bitwise launch_lm_normal + launch_chol_solve.
+int launch_lm_normal_solve(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F, double* rhs,
+                           double* sigma, int* dinfo, const double* xbase, double* xnext) {
+    if (!sigma || !dinfo || !xnext || n <= PNOL_SEQ_MAX) return PNOL_ERR_ARG;
+    CholRed cr;
+    PNOL_CHECK(launch_chol_reducing_prep(ctx, n, dinfo, cr));
+    LmTiles tl;
+    PNOL_CHECK(lm_normal_core(ctx, JTs, m, n, lambda, F, nullptr, 0, rhs, nullptr, &tl));
+    PNOL_CHECK(launch_chol_reducing_start(ctx, cr));
+    ScopedTimer tm(ctx, "solve");
+    if (tl.partials)
+        return launch_chol_reducing_run(ctx, ctx->stream, cr, tl.part, tl.sub, nullptr, tl.split, tl.jp, lambda, rhs,
+                                        sigma, xbase, xnext);
+    return launch_chol_reducing_run_packed(ctx, ctx->stream, cr, tl.packed, tl.slot, tl.tpr, rhs, lambda, sigma, xbase,
+                                           xnext);
+}
+
+// A from the tiles the last launch_lm_normal_solve left (the LU fallback; the same A as
+// launch_lm_normal's)
+int launch_lm_normal_unpack(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda) {
+    if (!A || m <= 0 || n <= PNOL_SEQ_MAX || lda < n) return PNOL_ERR_ARG;
+    const int P = comm_size();
+    if (P == 1) return launch_jtj_from_partials(ctx, m, n, lambda, A, lda);
+    const int nt = (n + kTile - 1) / kTile;
+    const int ntiles = nt * (nt + 1) / 2;
+    const long E = (long)kTile * kTile;
+    const int tpr = (ntiles + P - 1) / P;
+    constexpr int kMaxNodes = 4;
+    const long slot = (long)tpr * E + (long)kMaxNodes * n;
+    void* packed = nullptr;
+    PNOL_CHECK(ws_get(ctx, "lm_packed", sizeof(double) * (size_t)P * slot, &packed));
+    hipLaunchKernelGGL(k_syrk_unpack, dim3(8, ntiles), dim3(256), 0, ctx->stream, (const double*)packed, ntiles, n,
+                       lambda, slot, tpr, A, (long)lda, (double*)nullptr);
     return launch_check();
 }
 

@@ -233,10 +233,19 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
 // partials jp into its padded matrix and b (rhs gets -J^T F too), then the factorisation, the
 // backward solve and xnext = xbase + sigma; bitwise the reduce into A + launch_chol_solve
 int launch_chol_reducing_prep(pnol_ctx* ctx, int n, int* dinfo, CholRed& cr);
-int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr);
+int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr, int* zero = nullptr, int nzero = 0);
 int launch_chol_reducing_run(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, const double* part, int sub,
                              const int* cnt, int split, const double* jp, double lambda, double* rhs, double* sigma,
                              const double* xbase, double* xnext);
+int launch_chol_reducing_run_packed(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, const double* packed, long slot,
+                                    int tpr, const double* rhs, double lambda, double* sigma, const double* xbase,
+                                    double* xnext);
+// LevMarqMPI's normal equations + solve without forming A (syrk.hip): launch_lm_normal up to the
+// allgathered tiles and -J^T F, then the reducing Cholesky reading the tiles; A on request from
+// the last call's tiles (the LU fallback)
+int launch_lm_normal_solve(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F, double* rhs,
+                           double* sigma, int* dinfo, const double* xbase, double* xnext);
+int launch_lm_normal_unpack(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda);
 
 int launch_dobj_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* out);
 // rows [r0, r1) only (multiples of 64 but r1 = m; r1 < 0: all): a row-sharded LevMarqMPI rank

@@ -126,6 +126,22 @@ class Context:
                                              _ptr(rhs), _ptr(diag)), "pnol_lm_normal_mpi_d")
         return (A, rhs, diag) if want_diag else (A, rhs)
 
+    def lm_normal_solve_mpi(self, JTs, m, n, lam, F, x):
+        """pnol_lm_normal_solve_mpi_d: rhs, sigma, x + sigma and the solve status (read back)
+        without forming A; lm_normal_unpack_mpi forms A from the same tiles afterwards."""
+        rhs, sigma, xnext = self.empty(n), self.empty(n), self.empty(n)
+        info = self.torch.zeros(2, dtype=self.torch.int32, device=f"cuda:{self.device}")
+        L.check(L.lib().pnol_lm_normal_solve_mpi_d(self.h, _ptr(JTs), m, n, C.c_double(lam), _ptr(F), _ptr(rhs),
+                                                   _ptr(sigma), _ptr(info), _ptr(x), _ptr(xnext)),
+                "pnol_lm_normal_solve_mpi_d")
+        return rhs, sigma, xnext, int(info[0].item())
+
+    def lm_normal_unpack_mpi(self, m, n, lam, A=None):
+        A = self.empty(n, n) if A is None else A
+        L.check(L.lib().pnol_lm_normal_unpack_mpi_d(self.h, m, n, C.c_double(lam), _ptr(A), A.stride(0)),
+                "pnol_lm_normal_unpack_mpi_d")
+        return A
+
     def set_lm_fd_mode(self, mode):
         """LevMarqMPI's FD decomposition on this context: 0 columns (default), 1 rows, -1 env."""
         L.check(L.lib().pnol_lm_set_fd_mode(self.h, int(mode)), "pnol_lm_set_fd_mode")

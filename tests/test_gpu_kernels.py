@@ -640,6 +640,28 @@ def test_lm_sliced_jacobian_and_normal_bitwise(ctx, m, n, t64, monkeypatch):
     assert float((rb - rr).abs().max() / rr.abs().max()) < 1e-12
 
 
+@pytest.mark.parametrize("m,n", [(16384, 2048), (5000, 1000), (777, 129)])
+def test_lm_normal_solve_mpi_one_rank_bitwise(ctx, m, n):
+    """One rank of pnol_lm_normal_solve_mpi_d (the split-K partials of its slices summed by the
+    Cholesky's first tasks): rhs, sigma, x + sigma and the status bitwise pnol_lm_normal_mpi_d +
+    pnol_solve_step_d; pnol_lm_normal_unpack_mpi_d forms the same A."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    d = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+    x = ctx.tensor(np.linspace(-0.5, 0.5, n)); h = ctx.tensor(np.full(n, 1e-7))
+    F0, JTs = d.lm_jacobian_mpi(x, h)
+    for lam in (0.37, 1e-3):
+        Aa, ra = ctx.lm_normal_mpi(JTs, m, n, lam, F0)
+        sa, xa, ia = ctx.solve_step(Aa, ra, x)
+        rb, sb, xb, ib = ctx.lm_normal_solve_mpi(JTs, m, n, lam, F0, x)
+        ctx.synchronize()
+        assert ia == 0 and ib == 0
+        assert np.array_equal(_np(rb), _np(ra)) and np.array_equal(_np(sb), _np(sa)) and np.array_equal(_np(xb), _np(xa))
+        Ab = ctx.lm_normal_unpack_mpi(m, n, lam)
+        ctx.synchronize()
+        assert np.array_equal(_np(Ab), _np(Aa))
+
+
 @pytest.mark.parametrize("m,n,chunks", [(2000, 700, 4), (1500, 1000, 3), (513, 2048, 8), (300, 129, 2), (400, 300, 1)])
 def test_fd_jtj_pipelined_bitwise(ctx, m, n, chunks):
     """The pipelined FD Jacobian + J^T J (two streams, chunked) equals the two separate calls

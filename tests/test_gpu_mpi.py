@@ -107,6 +107,29 @@ def test_levmarq_mpi_fd_modes_bitwise(tmp_path, monkeypatch, mode, world, m, n):
         assert np.array_equal(z["F0"], F01) and np.array_equal(z["FO"], FO1), (mode, r)
 
 
+@pytest.mark.parametrize("trip,force", [("1", "0"), ("0", "0"), ("1", "1")])
+@pytest.mark.parametrize("world", [2, 4])
+def test_levmarq_mpi_trip_forms_bitwise(tmp_path, monkeypatch, trip, force, world):
+    """LevMarqMPI's normal equations + solve without forming A (pnol_lm_normal_solve_mpi_d: the
+    allgathered tiles go straight into the Cholesky's matrix; the default), the two calls
+    (PNOL_LM_TRIP=0), and the LU fallback forced on every trip (A formed from the same tiles,
+    pnol_lm_normal_unpack_mpi_d): X, F0 and FOpt on every rank bitwise the one-GPU LevMarq's
+    under the same settings."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_levmarq
+    m, n = 2000, 300
+    monkeypatch.setenv("PNOL_LM_TRIP", trip)
+    monkeypatch.setenv("PNOL_CHOL_FORCE_FALLBACK", force)
+    _run_workers(tmp_path, world, m, n, "lm")
+    ctx = Context(0)
+    obj = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+    X1, F01, FO1, _ = run_levmarq(obj, np.zeros(n), (0.001, 10.0, 1e-7, 5, 0.0, -1), which=0)
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        assert np.array_equal(z["X"], X1), (trip, force, r)
+        assert np.array_equal(z["F0"], F01) and np.array_equal(z["FO"], FO1), (trip, force, r)
+
+
 @pytest.mark.parametrize("mode", ["columns", "rows"])
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_levmarq_mpi_cfg4_full_size_bitwise(tmp_path, monkeypatch, mode, world):
