@@ -1305,8 +1305,6 @@ __device__ __forceinline__ void publish(int* w, int v) {
 // bitwise the one of A.
 struct RedArgs {
     const double* part = nullptr;   // nullptr: not the reducing form
-    const int* cnt = nullptr;       // tile t's partials are complete once cnt[t] == split (nullptr: all are)
-    int split = 0;
     int sub = 0, n = 0;
     double lambda = 0.0;
     const double* jp = nullptr;     // the 8 -J^T F slice partials (jp[s n + e])
@@ -1319,8 +1317,6 @@ struct RedArgs {
     const double* rhs_in = nullptr;
 };
 
-// (the partials are read with sc1 loads: in the gated LM trip they were stored write-through by
-// the J^T J running beside this launch, handed off by the tile counter)
 template <int SUB>
 __device__ __forceinline__ void red_pair(const double* __restrict__ p, long off, int sub, double& vx, double& vy) {
     constexpr long E = 128L * 128L;
@@ -1330,7 +1326,7 @@ __device__ __forceinline__ void red_pair(const double* __restrict__ p, long off,
         double ax = 0.0, ay = 0.0;
 #pragma unroll
         for (int u = 0; u < (SUB > 0 ? SUB : sub); ++u) {
-            const double2 w = ld16_sc1(p + (long)(s * sub + u) * E, (unsigned)(off * 8));
+            const double2 w = *reinterpret_cast<const double2*>(p + (long)(s * sub + u) * E + off);
             ax += w.x;
             ay += w.y;
         }
@@ -1373,12 +1369,6 @@ __device__ void red_task(int u, const RedArgs& red, double* __restrict__ P, long
     }
     const int I = J + r, ti = I >> 1, tj = J >> 1;
     const long tt = (long)ti * (ti + 1) / 2 + tj;
-    if (red.cnt) {   // the tile's partials: every split-K unit's counter add, after its stores drained
-        __shared__ int ok_red;
-        if (t == 0) ok_red = spin_ge(red.cnt + tt, red.split, info);
-        __syncthreads();
-        if (!ok_red) return;
-    }
     const double* p = red.part ? red.part + tt * 8 * red.sub * (128L * 128L) : nullptr;
     const double* pk = red.packed ? red.packed + (tt / red.tpr) * red.slot + (tt % red.tpr) * (128L * 128L) : nullptr;
     const double scale = 1 + red.lambda;
@@ -1874,10 +1864,8 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
 // P's padding (identity on the diagonal past n, as the copy of A gives), info = 0.
 __global__ __launch_bounds__(256) void k_chol_reducing_prep(double* __restrict__ P, long ldp, int T, int n,
                                                             double* __restrict__ bv, int* __restrict__ pflags,
-                                                            int npflags, int* __restrict__ info,
-                                                            int* __restrict__ zero, int nzero) {
+                                                            int npflags, int* __restrict__ info) {
     const int N = T * NB, tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
-    for (int q = tid; q < nzero; q += nth) zero[q] = 0;   // the caller's words (the J^T J's tile counters)
     const int b0 = 2 * T, v1 = 3 * T + T * T;   // [bcnt | ver]
     for (int q = tid; q < npflags; q += nth) pflags[q] = (q >= b0 && q < v1) ? -1 : 0;
     for (int r = n + tid; r < N; r += nth) bv[r] = 0.0;
@@ -1906,23 +1894,21 @@ int launch_chol_reducing_prep(pnol_ctx* ctx, int n, int* dinfo, CholRed& cr) {
     return chol_ws(ctx, n, true, cr.w);
 }
 
-int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr, int* zero, int nzero) {
+int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr) {
     const CholWs& w = cr.w;
     const int n = cr.n;
-    const long pad = (long)(w.N - n) * w.N + (long)n * (w.N - n), work = std::max<long>({pad, (long)w.npf, (long)nzero});
+    const long pad = (long)(w.N - n) * w.N + (long)n * (w.N - n), work = std::max<long>(pad, w.npf);
     hipLaunchKernelGGL(k_chol_reducing_prep, dim3((unsigned)std::max<long>(1, std::min<long>(1024, (work + 255) / 256))),
-                       dim3(256), 0, ctx->stream, w.P, w.ldp, w.T, n, w.bv, w.pf, w.npf, cr.dinfo, zero, nzero);
+                       dim3(256), 0, ctx->stream, w.P, w.ldp, w.T, n, w.bv, w.pf, w.npf, cr.dinfo);
     return launch_check();
 }
 
 int launch_chol_reducing_run(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, const double* part, int sub,
-                             const int* cnt, int split, const double* jp, double lambda, double* rhs, double* sigma,
-                             const double* xbase, double* xnext) {
+                             const double* jp, double lambda, double* rhs, double* sigma, const double* xbase,
+                             double* xnext) {
     if (!part || !jp || !rhs || !sigma || sub < 1) return PNOL_ERR_ARG;
     RedArgs red;
     red.part = part;
-    red.cnt = cnt;
-    red.split = split;
     red.sub = sub;
     red.n = cr.n;
     red.lambda = lambda;

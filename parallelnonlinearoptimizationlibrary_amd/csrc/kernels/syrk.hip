@@ -120,28 +120,10 @@ __device__ unsigned long long g_syrk_tl[3 * 65536];
 // TILE 128: waves 2 x 2 of 64 x 64 (4 x 4 MFMA blocks each); TILE 64: 2 x 2 of 32 x 32.
 // NW = 4: waves 2 x 2, each (TILE/2)^2; NW = 8: waves 2 x 4, each TILE/2 x TILE/4 (half the
 // accumulators per wave, so twice the waves per SIMD hide the stage boundaries).
-// A partial store: non-temporal, or (CNT: consumed in flight by the LM trip's Cholesky, after a
-// counter hand-off) write-through sc1 (MI355X_MICROARCH.md "Valid forms" row 1)
-template <bool CNT>
-__device__ __forceinline__ void part_st(double* p, double v) {
-    if constexpr (CNT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else __builtin_nontemporal_store(v, p);
-}
-
-// CNT (the LM trip, launch_fd_normal_solve): the last-dispatched workgroup stores tail_val into
-// *tail_flag when it starts (the Cholesky's stream waits for it: from then on no workgroup of
-// this launch waits for a CU, so a Cholesky that waits for this launch's tiles cannot starve
-// it), and every workgroup adds 1 to its tile's counter tile_cnt[t - tile0] once its partial
-// stores have drained.
-template <int MODE, int TILE, int NW = 4, bool CNT = false>
+template <int MODE, int TILE, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
                                                       int split_k, int kfirst, int kchunk, int sub, int slice0,
-                                                      int mS, long sstride, double* __restrict__ part, int tile0,
-                                                      unsigned* __restrict__ tail_flag = nullptr,
-                                                      unsigned tail_val = 0, int* __restrict__ tile_cnt = nullptr) {
-    if constexpr (CNT)
-        if (tail_flag && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)   // (no gate: nullptr)
-            __hip_atomic_store(tail_flag, tail_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                                                      int mS, long sstride, double* __restrict__ part, int tile0) {
     constexpr int NT = 64 * NW, WC = NW / 2;
     constexpr int WTM = TILE / 2, WTN = TILE / WC, NBM = WTM / 16, NBN = WTN / 16;
     __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
@@ -301,7 +283,8 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                 if (q < 4 || dcnt == 5)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        part_st<CNT>(out + (dbi[q] * 16 + orow + 4 * r) * ld + dbj[q] * 16 + ocol, acc[q >> 1][q & 1][r]);
+                        __builtin_nontemporal_store(acc[q >> 1][q & 1][r],
+                                                    out + (dbi[q] * 16 + orow + 4 * r) * ld + dbj[q] * 16 + ocol);
             // upper block u = bj (bj - 1) / 2 + bi (bi < bj): blocks wave, wave + 8, ... of the 28
             for (int u = __builtin_amdgcn_readfirstlane(wave); u < 28; u += NW) {
                 int bj = 1;
@@ -309,7 +292,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                 const int bi = u - bj * (bj - 1) / 2;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    part_st<CNT>(out + (bi * 16 + orow + 4 * r) * ld + bj * 16 + ocol, 0.0);
+                    __builtin_nontemporal_store(0.0, out + (bi * 16 + orow + 4 * r) * ld + bj * 16 + ocol);
             }
         } else {
 #pragma unroll
@@ -320,14 +303,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                     for (int r = 0; r < 4; ++r) {
                         int row = wr * WTM + mi * 16 + orow + 4 * r;
                         int col = wc * WTN + ni * 16 + ocol;
-                        part_st<CNT>(out + row * ld + col, acc[mi][ni][r]);
+                        __builtin_nontemporal_store(acc[mi][ni][r], out + row * ld + col);
                     }
         }
-    }
-    if constexpr (CNT) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();   // every wave's partial stores drained
-        if (threadIdx.x == 0) __hip_atomic_fetch_add(tile_cnt + (t - tile0), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #ifdef PNOL_SYRK_TIMELINE
     if (threadIdx.x == 0) {
@@ -652,13 +630,13 @@ static void syrk_partials(pnol_ctx* ctx, hipStream_t stream, bool rows_variant, 
         const int nt64 = (nr + 63) / 64;
         hipExtLaunchKernelGGL((k_syrk_tile<4, 64>), dim3(nt64 * (nt64 + 1) / 2 * split), dim3(256), 0, stream,
                               tm.start(), tm.stop(), 0, X, ldx, nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0,
-                              sc.mS, sstride, part, 0, (unsigned*)nullptr, 0u, (int*)nullptr);
+                              sc.mS, sstride, part, 0);
     } else if (rows_variant) {
         hipExtLaunchKernelGGL((k_syrk_tile<2, kTile, 8>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0, X, ldx,
-                              nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, tile0, (unsigned*)nullptr, 0u, (int*)nullptr);
+                              nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, tile0);
     } else {
         hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, 8>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0, X, ldx,
-                              nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, tile0, (unsigned*)nullptr, 0u, (int*)nullptr);
+                              nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, tile0);
     }
 }
 
@@ -786,50 +764,14 @@ int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h,
 // chain's first steps -- the backward solve and xnext = x + sigma.  JT, rhs, sigma, xnext and the
 // solve status are bitwise those of launch_fd_jtj (+ rhs) and launch_chol_solve; for the LU
 // fallback launch_jtj_from_partials forms A from the trip's partials.
-// The wait-value gate of the LM trip (launch_fd_normal_solve): one signal word per context,
-// a fresh value per launch.  Unsupported: the Cholesky follows the J^T J in stream order.
-static bool tail_gate_ok(pnol_ctx* ctx) {
-    static int supported = -1;
-    if (supported < 0) {
-        int v = 0;
-        supported = hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, ctx->device) == hipSuccess && v;
-    }
-    const char* e = std::getenv("PNOL_LM_TAIL");   // 0: stream order (read per call: A/B runs)
-    return supported && !(e && std::atoi(e) == 0);
-}
-
-static int tail_word(pnol_ctx* ctx, unsigned** flag, unsigned* val) {
-    if (!ctx->tail_flag) {
-        // one signal word (the command processor polls it); plain device memory where refused
-        if (hipExtMallocWithFlags((void**)&ctx->tail_flag, 8, hipMallocSignalMemory) != hipSuccess) {
-            (void)hipGetLastError();
-            ctx->tail_flag = nullptr;
-            PNOL_HIP(hipMalloc((void**)&ctx->tail_flag, 64));
-        }
-        PNOL_HIP(hipMemset(ctx->tail_flag, 0, 8));
-        ctx->tail_epoch = 0;
-    }
-    if (ctx->tail_epoch > (1u << 30)) {   // restart the values (the word is 0 again first)
-        PNOL_HIP(hipStreamSynchronize(ctx->stream));
-        PNOL_HIP(hipMemset(ctx->tail_flag, 0, 8));
-        ctx->tail_epoch = 0;
-    }
-    *flag = ctx->tail_flag;
-    *val = ++ctx->tail_epoch;
-    return PNOL_OK;
-}
-
 // One LM trip's linear algebra with A never formed (single process, n > PNOL_SEQ_MAX,
-// LevenbergMarquardt.cpp:55-90).  On the context stream: the FD Jacobian, the -J^T F slice
-// partials, the Cholesky's prep, then the J^T J split-K partials (k_syrk_tile, write-through,
-// one counter per tile).  On the aux stream, gated by the J^T J's last-dispatched workgroup
-// (hipStreamWaitValue32 on a word it stores when it starts): the persistent tile Cholesky, whose
-// first tasks sum each tile's partials into its own matrix once the tile's counter is full
-// (and b = -J^T F), then factors -- so its workgroups take the CUs the J^T J's last round frees
-// and the reduce and the chain's first steps run in the J^T J's tail; then the backward solve
-// and xnext = x + sigma.  The reduce launch and the copy of A are gone.  JT, rhs, sigma, xnext
-// and the solve status are bitwise those of launch_fd_jtj (+ rhs) and launch_chol_solve; for the
-// LU fallback launch_jtj_from_partials forms A from the trip's partials.
+// LevenbergMarquardt.cpp:55-90): the FD Jacobian, the -J^T F slice partials, the Cholesky's
+// prep launch, the J^T J split-K partials (k_syrk_tile), then the persistent tile Cholesky whose
+// first tasks sum the partials into its own matrix (and b = -J^T F) -- so the reduce's HBM
+// stream runs beside the chain's first steps -- then the backward solve and xnext = x + sigma.
+// The reduce launch and the copy of A are gone.  JT, rhs, sigma, xnext and the solve status are
+// bitwise those of launch_fd_jtj (+ rhs) and launch_chol_solve; for the LU fallback
+// launch_jtj_from_partials forms A from the trip's partials.
 int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
                            double* JT, int ldjt, double lambda, double* rhs, double* sigma, int* dinfo, double* xnext) {
     if (!o || !x || !h || !F0 || !JT || !rhs || !sigma || !dinfo || !xnext || ldjt < o->m) return PNOL_ERR_ARG;
@@ -840,57 +782,20 @@ int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
     const SliceCfg sc = slice_cfg(m, ntiles);
     const int split = kS * sc.sub;
     // every workspace first: a (re)allocation frees, and a free waits for the device
-    void *part = nullptr, *jp = nullptr, *cnt = nullptr;
+    void *part = nullptr, *jp = nullptr;
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * split * kTile * kTile, &part));
     PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
-    PNOL_CHECK(ws_get(ctx, "syrk_tile_cnt", sizeof(int) * (size_t)ntiles, &cnt));
     CholRed cr;
     PNOL_CHECK(launch_chol_reducing_prep(ctx, n, dinfo, cr));
-    const bool gate = tail_gate_ok(ctx);
-    unsigned* tf = nullptr;
-    unsigned tv = 0;
-    if (gate) {
-        PNOL_CHECK(tail_word(ctx, &tf, &tv));
-        if (!ctx->aux_stream) PNOL_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
-        while (ctx->aux_events.size() < 2) {
-            hipEvent_t e;
-            PNOL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            ctx->aux_events.push_back(e);
-        }
-    }
     PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
     PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F0));
-    // the prep launch (words, paddings, info; with the gate also the tile counters)
-    PNOL_CHECK(launch_chol_reducing_start(ctx, cr, gate ? (int*)cnt : nullptr, gate ? ntiles : 0));
-    hipStream_t cs = ctx->stream;
-    if (gate) {
-        PNOL_HIP(hipEventRecord(ctx->aux_events[0], ctx->stream));
-        PNOL_HIP(hipStreamWaitEvent(ctx->aux_stream, ctx->aux_events[0], 0));
-        PNOL_HIP(hipStreamWaitValue32(ctx->aux_stream, tf, tv, hipStreamWaitValueGte, 0xffffffffu));
-        cs = ctx->aux_stream;
-    }
-    if (gate) {   // write-through partials + tile counters: the Cholesky reads tiles in flight
-        const dim3 grid(ntiles * split);
-        LaunchTimer tm(ctx, "syrk");
-        hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, 8, true>), grid, dim3(512), 0, ctx->stream, tm.start(), tm.stop(),
-                              0, JT, (long)ldjt, n, m, split, sc.kfirst, sc.kchunk, sc.sub, 0, sc.mS, (long)sc.mS,
-                              (double*)part, 0, tf, tv, (int*)cnt);
-        PNOL_CHECK(launch_check());
-    } else {      // stream order: the plain SYRK (non-temporal partials, no counters)
-        syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
-                      syrk_t64(false));
-        PNOL_CHECK(launch_check());
-    }
-    {
-        ScopedTimer tm(ctx, "solve", cs);
-        PNOL_CHECK(launch_chol_reducing_run(ctx, cs, cr, (const double*)part, sc.sub, gate ? (const int*)cnt : nullptr,
-                                            split, (const double*)jp, lambda, rhs, sigma, x, xnext));
-    }
-    if (gate) {
-        PNOL_HIP(hipEventRecord(ctx->aux_events[1], ctx->aux_stream));
-        PNOL_HIP(hipStreamWaitEvent(ctx->stream, ctx->aux_events[1], 0));
-    }
-    return PNOL_OK;
+    PNOL_CHECK(launch_chol_reducing_start(ctx, cr));   // the prep launch (words, paddings, info)
+    syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
+                  syrk_t64(false));
+    PNOL_CHECK(launch_check());
+    ScopedTimer tm(ctx, "solve");
+    return launch_chol_reducing_run(ctx, ctx->stream, cr, (const double*)part, sc.sub, (const double*)jp, lambda, rhs,
+                                    sigma, x, xnext);
 }
 
 // A (lower triangle + mirror, the Marquardt diagonal) from the split-K partials of the last
@@ -1149,8 +1054,7 @@ int launch_lm_normal_solve(pnol_ctx* ctx, const double* JTs, int m, int n, doubl
     PNOL_CHECK(launch_chol_reducing_start(ctx, cr));
     ScopedTimer tm(ctx, "solve");
     if (tl.partials)
-        return launch_chol_reducing_run(ctx, ctx->stream, cr, tl.part, tl.sub, nullptr, tl.split, tl.jp, lambda, rhs,
-                                        sigma, xbase, xnext);
+        return launch_chol_reducing_run(ctx, ctx->stream, cr, tl.part, tl.sub, tl.jp, lambda, rhs, sigma, xbase, xnext);
     return launch_chol_reducing_run_packed(ctx, ctx->stream, cr, tl.packed, tl.slot, tl.tpr, rhs, lambda, sigma, xbase,
                                            xnext);
 }

@@ -74,10 +74,6 @@ struct pnol_ctx {
     hipStream_t comm_stream = nullptr;
     std::vector<hipEvent_t> phase_events;
     hipEvent_t comm_done = nullptr;
-    // the LM trip's wait-value gate (launch_fd_normal_solve): a signal word the J^T J's
-    // last-dispatched workgroup stores, and the value of the last launch
-    unsigned* tail_flag = nullptr;
-    unsigned tail_epoch = 0;
 };
 
 // The tile Cholesky's workspace for order n (chol.hip)
@@ -229,14 +225,14 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
 // workspace (before anything is queued: an allocation may free); _start queues the prep launch
 // (progress words, paddings, info) on the context stream; _run queues on `st` the persistent tile
 // Cholesky whose first tasks reduce the partials (part: k_syrk_tile's 128 x 128 layout, `sub`
-// chunks per m-slice; tile t's once cnt[t] == split, nullptr: complete) and the -J^T F slice
+// chunks per m-slice) and the -J^T F slice
 // partials jp into its padded matrix and b (rhs gets -J^T F too), then the factorisation, the
 // backward solve and xnext = xbase + sigma; bitwise the reduce into A + launch_chol_solve
 int launch_chol_reducing_prep(pnol_ctx* ctx, int n, int* dinfo, CholRed& cr);
-int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr, int* zero = nullptr, int nzero = 0);
+int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr);
 int launch_chol_reducing_run(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, const double* part, int sub,
-                             const int* cnt, int split, const double* jp, double lambda, double* rhs, double* sigma,
-                             const double* xbase, double* xnext);
+                             const double* jp, double lambda, double* rhs, double* sigma, const double* xbase,
+                             double* xnext);
 int launch_chol_reducing_run_packed(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, const double* packed, long slot,
                                     int tpr, const double* rhs, double lambda, double* sigma, const double* xbase,
                                     double* xnext);

@@ -491,7 +491,6 @@ int pnol_ctx_destroy(pnol_ctx* ctx) {
         (void)hipStreamDestroy(ctx->comm_stream);
     }
     for (hipEvent_t e : ctx->phase_events) (void)hipEventDestroy(e);
-    if (ctx->tail_flag) (void)hipFree(ctx->tail_flag);
     if (ctx->comm_done) (void)hipEventDestroy(ctx->comm_done);
     for (auto& kv : ctx->timers.pending)
         for (auto& ev : kv.second) {

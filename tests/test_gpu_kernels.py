@@ -705,16 +705,13 @@ def test_fd_normal_bitwise(ctx, m, n):
         assert np.array_equal(_np(rb), _np(ra)), rep
 
 
-@pytest.mark.parametrize("m,n,tail", [(16384, 2048, "1"), (16384, 2048, "0"), (5000, 1000, "1"), (777, 129, "1"),
-                                      (3000, 257, "0"), (2000, 700, "1")])
-def test_lm_trip_bitwise(ctx, m, n, tail, monkeypatch):
+@pytest.mark.parametrize("m,n", [(16384, 2048), (5000, 1000), (777, 129), (3000, 257), (2000, 700), (512, 96)])
+def test_lm_trip_bitwise(ctx, m, n):
     """The LM trip without A (pnol_lm_trip_d: the persistent Cholesky's first tasks sum the J^T J
     split-K partials and the -J^T F slice partials into its own matrix and b) gives JT, F0, rhs,
     sigma, x + sigma and the solve status bitwise those of pnol_fd_normal_d + pnol_solve_step_d,
     over repeated trips at new points and lambdas; the A the LU fallback forms from the trip's
-    partials (pnol_lm_trip_normal_d) is bitwise pnol_fd_normal_d's A.  tail = 1: the Cholesky
-    launched into the J^T J's tail (the default); 0: after it in stream order."""
-    monkeypatch.setenv("PNOL_LM_TAIL", tail)
+    partials (pnol_lm_trip_normal_d) is bitwise pnol_fd_normal_d's A."""
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
     d = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)

@@ -576,13 +576,11 @@ def test_lm_fused_trip_loop_equals_general_loop(ctx, oracle, m, n, force, monkey
     params = (0.001, 10, 1e-7, 8, 0.0, -1)
     monkeypatch.setenv("PNOL_CHOL_FORCE_FALLBACK", force)
     out = {}
-    for name, mode, trip, tail in (("fused", "1", "1", "1"), ("fused_stream_order", "1", "1", "0"),
-                                   ("two_call", "1", "0", "1"), ("general", "0", "0", "1")):
+    for name, mode, trip in (("fused", "1", "1"), ("two_call", "1", "0"), ("general", "0", "0")):
         monkeypatch.setenv("PNOL_LM_ASYNC", mode)
         monkeypatch.setenv("PNOL_LM_TRIP", trip)
-        monkeypatch.setenv("PNOL_LM_TAIL", tail)
         out[name] = run_levmarq(_obj(ctx, L.OBJ_LINRES, n, m, A, y), np.zeros(n), params)
-    for a, b in (("fused", "two_call"), ("fused_stream_order", "two_call"), ("two_call", "general")):
+    for a, b in (("fused", "two_call"), ("two_call", "general")):
         (Xa, F0a, FOa, ra), (Xs, F0s, FOs, rs) = out[a], out[b]
         assert np.array_equal(Xa, Xs), (a, b, rel(Xa, Xs))
         assert np.array_equal(F0a, F0s) and np.array_equal(FOa, FOs), (a, b)
