@@ -22,5 +22,5 @@ t0 = time.perf_counter()
 X, *_ = run_levmarq(d, np.zeros(n), params)
 t1 = time.perf_counter()
 Xo, *_ = O.lm_findmin(O.linres(m, n), np.zeros(n), params)
-print(f"m={m} n={n} trip={os.environ.get('PNOL_LM_TRIP', '1')} tail={os.environ.get('PNOL_LM_TAIL', '1')} "
+print(f"m={m} n={n} trip={os.environ.get('PNOL_LM_TRIP', '1')} "
       f"err={np.max(np.abs(X - Xo)) / np.max(np.abs(Xo)):.2e} s={t1 - t0:.3f}", flush=True)
