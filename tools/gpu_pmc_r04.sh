@@ -1,0 +1,16 @@
+# Round-4 PMC passes of the bench (one counter group per run, no trace domains):
+# FETCH_SIZE / WRITE_SIZE (bench + the sliced SYRK probe), the SYRK's MFMA busy, the FD's VALU busy.
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+B="bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-bfgs"
+run() { local name=$1; shift; timeout -s KILL 300 "$@" > gpurun_out/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; return $rc; }
+run pmc_fetch rocprofv3 --pmc FETCH_SIZE -d /tmp/pmc_fetch -o pmc --output-format csv -- python3 $B &&
+run pmc_write rocprofv3 --pmc WRITE_SIZE -d /tmp/pmc_write -o pmc --output-format csv -- python3 $B &&
+run pmc_fetch_sl rocprofv3 --pmc FETCH_SIZE -d /tmp/pmc_fetch -o probe --output-format csv -- python3 tools/syrk_sliced_probe.py 3 &&
+run pmc_write_sl rocprofv3 --pmc WRITE_SIZE -d /tmp/pmc_write -o probe --output-format csv -- python3 tools/syrk_sliced_probe.py 3 &&
+run pmc_mfma rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d /tmp/pmc_mfma -o pmc --output-format csv -- python3 $B --no-hg &&
+run pmc_valu rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -d /tmp/pmc_valu -o pmc --output-format csv -- python3 $B --no-hg || exit 1
+python3 tools/pmc_traffic.py /tmp/pmc_fetch /tmp/pmc_write gpurun_out/r04_pmc_traffic.json &&
+python3 tools/pmc_valu.py /tmp/pmc_mfma gpurun_out/r04_pmc_syrk_mfma.json k_syrk_tile &&
+python3 tools/pmc_valu.py /tmp/pmc_valu gpurun_out/r04_pmc_fd_valu.json k_linres_fdP k_linres_evalP
