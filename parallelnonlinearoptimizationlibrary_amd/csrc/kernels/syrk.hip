@@ -120,7 +120,15 @@ __device__ unsigned long long g_syrk_tl[3 * 65536];
 // TILE 128: waves 2 x 2 of 64 x 64 (4 x 4 MFMA blocks each); TILE 64: 2 x 2 of 32 x 32.
 // NW = 4: waves 2 x 2, each (TILE/2)^2; NW = 8: waves 2 x 4, each TILE/2 x TILE/4 (half the
 // accumulators per wave, so twice the waves per SIMD hide the stage boundaries).
-template <int MODE, int TILE, int NW = 4>
+// a partial store: non-temporal, or (NTS false) a plain store that may stay in the caches for the
+// reduce that reads it next
+template <bool NTS>
+__device__ __forceinline__ void part_store(double v, double* p) {
+    if constexpr (NTS) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <int MODE, int TILE, int NW = 4, bool NTS = true>
 __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
                                                       int split_k, int kfirst, int kchunk, int sub, int slice0,
                                                       int mS, long sstride, double* __restrict__ part, int tile0) {
@@ -283,8 +291,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                 if (q < 4 || dcnt == 5)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        __builtin_nontemporal_store(acc[q >> 1][q & 1][r],
-                                                    out + (dbi[q] * 16 + orow + 4 * r) * ld + dbj[q] * 16 + ocol);
+                        part_store<NTS>(acc[q >> 1][q & 1][r], out + (dbi[q] * 16 + orow + 4 * r) * ld + dbj[q] * 16 + ocol);
             // upper block u = bj (bj - 1) / 2 + bi (bi < bj): blocks wave, wave + 8, ... of the 28
             for (int u = __builtin_amdgcn_readfirstlane(wave); u < 28; u += NW) {
                 int bj = 1;
@@ -292,7 +299,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                 const int bi = u - bj * (bj - 1) / 2;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    __builtin_nontemporal_store(0.0, out + (bi * 16 + orow + 4 * r) * ld + bj * 16 + ocol);
+                    part_store<NTS>(0.0, out + (bi * 16 + orow + 4 * r) * ld + bj * 16 + ocol);
             }
         } else {
 #pragma unroll
@@ -303,7 +310,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                     for (int r = 0; r < 4; ++r) {
                         int row = wr * WTM + mi * 16 + orow + 4 * r;
                         int col = wc * WTN + ni * 16 + ocol;
-                        __builtin_nontemporal_store(acc[mi][ni][r], out + row * ld + col);
+                        part_store<NTS>(acc[mi][ni][r], out + row * ld + col);
                     }
         }
     }
@@ -635,8 +642,11 @@ static void syrk_partials(pnol_ctx* ctx, hipStream_t stream, bool rows_variant, 
         hipExtLaunchKernelGGL((k_syrk_tile<2, kTile, 8>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0, X, ldx,
                               nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, tile0);
     } else {
-        hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, 8>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0, X, ldx,
-                              nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, tile0);
+        // plain partial stores: the reduce (or the reducing Cholesky) that reads them next finds
+        // part of them in the caches -- solve 0.71 vs 0.73 ms, SYRK unchanged, in alternating
+        // same-box runs (non-temporal stores for J itself in the FD kernel measured slower)
+        hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, 8, false>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0,
+                              X, ldx, nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, tile0);
     }
 }
 
