@@ -2,6 +2,7 @@
 // Source/LevenbergMarquardtMPI.cpp).  Both share one device-resident loop; the MPI form
 // shards the FD Jacobian columns over the communicator (cost-balanced tiles) and shares the
 // rows of J^T between the ranks.
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -351,9 +352,18 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool s
     int iter = 0;
     double xdiff2Norm = P.xMinDiff * 2;
     bool ckpt = true;   // the checkpoints in the context are those of x_[s]
+    // PNOL_LM_HOSTPROF=1: the host's share of a trip (decision, enqueue) to stderr at the end
+    const bool hprof = std::getenv("PNOL_LM_HOSTPROF") != nullptr;
+    double h_dec = 0, h_enq = 0;
+    auto hnow = [] { return std::chrono::steady_clock::now(); };
+    auto t_dec = hnow();
     while (iter < P.maxIter) {
+        auto t0 = hnow();
+        if (hprof && iter > 0) h_dec += std::chrono::duration<double, std::micro>(t0 - t_dec).count();
         dev.enqueue(s, lambda, ckpt);
+        if (hprof) h_enq += std::chrono::duration<double, std::micro>(hnow() - t0).count();
         dev.wait(s);
+        if (hprof) t_dec = hnow();
         if (dev.info_h(s) != 0) {
             if (std::getenv("PNOL_LM_DEBUG"))   // which trips fell back (a timed-out chain: status <= -7)
                 std::cerr << "[pnol] LM trip " << iter << ": solve status " << dev.info_h(s) << ", LU redo" << std::endl;
@@ -395,6 +405,9 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool s
         }
         iter++;
     }
+    if (hprof && iter > 0)
+        std::cerr << "[pnol] LM host per trip: decision " << h_dec / iter << " us, enqueue " << h_enq / (iter + 1)
+                  << " us" << std::endl;
     FOpt.resize(m);
     check(pnol_memcpy_d2h(ctx, FOpt.data(), dev.F(s), sizeof(double) * m), "d2h");   // F(x_[s]) = F(X)
     if (P.verbose >= 0 && loud) {
