@@ -52,8 +52,13 @@ int main() {
     long long h[16];
     int hinfo = 0;
     hipMemcpy(h, out, sizeof(h), hipMemcpyDeviceToHost);
+    double w[NB * NB];
+    hipMemcpy(w, Wd, sizeof(w), hipMemcpyDeviceToHost);
+    unsigned long long fnv = 1469598103934665603ull;   // FNV-1a over W's bytes: bitwise comparisons across builds
+    const unsigned char* wb = reinterpret_cast<const unsigned char*>(w);
+    for (size_t i = 0; i < sizeof(w); ++i) fnv = (fnv ^ wb[i]) * 1099511628211ull;
     hipMemcpy(&hinfo, info, sizeof(int), hipMemcpyDeviceToHost);
-    std::printf("{\"info\": %d, \"stamps_cycles\": {", hinfo);
+    std::printf("{\"info\": %d, \"w_fnv\": \"%016llx\", \"stamps_cycles\": {", hinfo, fnv);
     const char* names[15] = {"p0_j0", "p0_j8", "p1_j0", "p1_j8", "p2_j0", "p2_j8", "p3_j0", "p3_j8", "w0_panels_done",
                              "w0_vx_done", "w1_inv1", "w1_inv2", "w1_inv3", "after_barrier", "total"};
     for (int i = 0; i < 15; ++i) std::printf("%s\"%s\": %lld", i ? ", " : "", names[i], h[i]);
