@@ -30,7 +30,9 @@ enum pnol_status {
     PNOL_ERR_NODEVICE = 4,   /* no MI355X (gfx950) visible: the product path has no CPU fallback */
     PNOL_ERR_SINGULAR = 5,   /* zero pivot in the damped solve */
     PNOL_ERR_COMM = 6,       /* collective failed / communicator not initialised */
-    PNOL_ERR_UNSUPPORTED = 7
+    PNOL_ERR_UNSUPPORTED = 7,
+    PNOL_ERR_TIMEOUT = 8     /* a device dependency wait of the tile Cholesky ran past its cap on
+                                every relaunch (a scheduling fault; never mapped to the LU) */
 };
 
 typedef struct pnol_ctx pnol_ctx;   /* one GPU: device, stream, workspace, communicator */
@@ -199,6 +201,15 @@ int pnol_lm_normal_mpi_d(pnol_ctx* ctx, const double* JTs, int m, int n, double 
 int pnol_lm_normal_solve_mpi_d(pnol_ctx* ctx, const double* JTs, int m, int n, double lambda, const double* F,
                                double* rhs, double* sigma, int* dinfo, const double* x, double* xnext);
 int pnol_lm_normal_unpack_mpi_d(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda);
+/* The trip's solve status agreed over the communicator's ranks, queued on the context stream:
+ * dinfo[0] (device int) is this rank's status from pnol_lm_trip_d / pnol_lm_normal_solve_mpi_d /
+ * pnol_solve_step_d; dinfo[1] becomes the max over all ranks of its code -- 0 none, 1 a wait of
+ * the tile Cholesky ran past its cap (relaunch the Cholesky: pnol_solve_d method 0 does), 2 a
+ * non-positive or NaN pivot (the reference-order LU, method 2).  The reference's replicas all run
+ * the same luSolve on the same A (LevenbergMarquardtMPI.cpp:88), so they never branch per rank;
+ * acting on dinfo[1] keeps every rank on the same branch and the same collectives.  One rank or
+ * no communicator: dinfo[1] = the code of dinfo[0]. */
+int pnol_lm_agree_status_d(pnol_ctx* ctx, int* dinfo);
 /* rhs = -(J^T F), LevenbergMarquardt.cpp:78-80 */
 int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs);
 /* sigma = A^{-1} rhs, replacing luSolve(A, rhs, sigma), LevenbergMarquardt.cpp:83.
@@ -208,9 +219,11 @@ int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const do
  * factorisation (bitwise) as one persistent launch: one workgroup runs the diagonal chain, the
  * others take the panel / update tiles from an ordered queue (the default of method 0;
  * PNOL_CHOL_PERSIST=0 makes method 0 use 4).  Methods 4 and 5 factor a padded copy and leave A
- * intact.  (Methods 1 and 3, the per-panel-launch and tile-DAG Cholesky forms, were removed:
- * PNOL_ERR_UNSUPPORTED.)  info (host, nullable) gets the method family used (1 = Cholesky,
- * 2 = LU) or -1 on a singular matrix. */
+ * intact.  A Cholesky whose dependency wait ran past its cap is relaunched (method 4 after the
+ * first, bitwise the same factorisation), never replaced by the LU; PNOL_ERR_TIMEOUT when the
+ * relaunches time out too.  (Methods 1 and 3, the per-panel-launch and tile-DAG Cholesky forms,
+ * were removed: PNOL_ERR_UNSUPPORTED.)  info (host, nullable) gets the method family used
+ * (1 = Cholesky, 2 = LU) or -1 on a singular matrix. */
 int pnol_solve_d(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n,
                  int method, int* info);
 /* The method-4 Cholesky solve queued without any host wait: *dinfo (a device int) ends 0 on

@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PNOL_AMD_LIB") or os.path.join(HERE, "libpnol_amd.so")
 
 PNOL_OK, PNOL_ERR_ARG, PNOL_ERR_HIP, PNOL_ERR_NOMEM, PNOL_ERR_NODEVICE = 0, 1, 2, 3, 4
-PNOL_ERR_SINGULAR, PNOL_ERR_COMM, PNOL_ERR_UNSUPPORTED = 5, 6, 7
+PNOL_ERR_SINGULAR, PNOL_ERR_COMM, PNOL_ERR_UNSUPPORTED, PNOL_ERR_TIMEOUT = 5, 6, 7, 8
 PNOL_SEQ_MAX = 64
 LM_SLICES = 8          # PNOL_LM_SLICES: m-slices of the LevMarqMPI J^T J / J^T F summation tree
 
@@ -90,6 +90,7 @@ _SIGS = {
     "pnol_lm_normal_mpi_d": (_i, [_vp, _vp, _i, _i, _d, _vp, _vp, _i, _vp, _vp]),
     "pnol_lm_normal_solve_mpi_d": (_i, [_vp, _vp, _i, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp]),
     "pnol_lm_normal_unpack_mpi_d": (_i, [_vp, _i, _i, _d, _vp, _i]),
+    "pnol_lm_agree_status_d": (_i, [_vp, _vp]),
     "pnol_lm_set_fd_mode": (_i, [_vp, _i]),
     "pnol_lm_fd_mode": (_i, [_vp, C.POINTER(C.c_int)]),
     "pnol_lm_rank_rows": (_i, [_i, _i, _i, C.POINTER(C.c_int), C.POINTER(C.c_int)]),

@@ -266,6 +266,7 @@ int pnol_lm_jacobian_mpi_d(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const
 int pnol_lm_set_fd_mode(pnol_ctx* ctx, int mode) {
     if (!ctx || mode < -1 || mode > 1) return PNOL_ERR_ARG;
     ctx->lm_fd_mode = mode < 0 ? lm_fd_mode_env() : mode;
+    ctx->lm_fd_mode_set = mode >= 0;
     return PNOL_OK;
 }
 
@@ -307,6 +308,12 @@ int pnol_lm_normal_solve_mpi_d(pnol_ctx* ctx, const double* JTs, int m, int n, d
 int pnol_lm_normal_unpack_mpi_d(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda) {
     PNOL_CHECK(set_device(ctx));
     return launch_lm_normal_unpack(ctx, m, n, lambda, A, lda);
+}
+
+int pnol_lm_agree_status_d(pnol_ctx* ctx, int* dinfo) {
+    PNOL_CHECK(set_device(ctx));
+    if (!dinfo) return PNOL_ERR_ARG;
+    return launch_status_agree(ctx, dinfo);
 }
 
 int pnol_jtr_d(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs) {

@@ -173,7 +173,8 @@ class LMDevice {
 // readback in between), x_{i+1} = x_i + sigma_i and F(x_{i+1}) with its checkpoints on the
 // device, then sigma_i, F(x_{i+1}) and the solve status into pinned memory behind one event.
 // The host then replays the reference's decision (LevenbergMarquardt.cpp:87-160).  A
-// non-positive Cholesky pivot is redone with the reference-order LU, as pnol_solve_d does.
+// non-positive Cholesky pivot is redone with the reference-order LU, as pnol_solve_d does; a
+// Cholesky wait that ran past its cap is redone with the same Cholesky (never the LU).
 // (Queueing trip i+1 before deciding step i was measured: a rejected step then costs a whole
 // wasted trip, and the post-convergence steps of the bench are mostly rejections.)
 //
@@ -192,9 +193,10 @@ class LMAsync {
         size_t jt = (size_t)n * ldjt_;
         if (sliced) {
             check(pnol_lm_sliced_layout(m, n, nullptr, &jt), "sliced layout");
-            // the FD decomposition, read once per solve (PNOL_LM_FD) and the same on every rank:
-            // the two modes pair different transfers, so ranks that disagreed would mismatch them
-            ctx->lm_fd_mode = lm_fd_mode_env();
+            // the FD decomposition, read once per solve (PNOL_LM_FD; a mode chosen through
+            // pnol_lm_set_fd_mode stands) and the same on every rank: the two modes pair
+            // different transfers, so ranks that disagreed would mismatch them
+            if (!ctx->lm_fd_mode_set) ctx->lm_fd_mode = lm_fd_mode_env();
             std::vector<int> all;
             check(comm_allgather_int(ctx, ctx->lm_fd_mode, all), "allgather(fd mode)");
             for (int v : all)
@@ -206,6 +208,9 @@ class LMAsync {
             const char* e = std::getenv("PNOL_LM_TRIP");
             trip_fused_ = !e || std::atoi(e) != 0;
         }
+        // several ranks: every trip's solve status is agreed over the ranks before the host acts
+        // on it (pnol_lm_agree_status_d), so all replicas take the same branch
+        agree_ = sliced && comm_size() > 1;
         JT_.reset(ctx, jt);
         A_.reset(ctx, (size_t)n * lda_);
         rhs_.reset(ctx, n);
@@ -247,6 +252,7 @@ class LMAsync {
                 check(pnol_lm_normal_solve_mpi_d(ctx_, JT_.get(), m_, n_, lambda, F(s), rhs_.get(), sig(s), info(s),
                                                  x_[s].get(), x_[s ^ 1].get()),
                       "normal equations + solve");
+                agree(s);
                 finish(s, false);
                 return;
             }
@@ -271,7 +277,19 @@ class LMAsync {
         // the solve's last launch also forms the trial point x_[s] + sigma
         check(pnol_solve_step_d(ctx_, A_.get(), lda_, rhs_.get(), sig(s), n_, info(s), x_[s].get(), x_[s ^ 1].get()),
               "solve");
+        agree(s);
         finish(s, false);
+    }
+    // LevMarqMPI on several ranks: info(s)[1] = the trip's solve status code agreed over the ranks
+    // (queued in stream order before the trial point, so it rides in the trip's one result copy)
+    void agree(int s) {
+        if (agree_) check(pnol_lm_agree_status_d(ctx_, info(s)), "agree(solve status)");
+    }
+    // what the host does about trip s's solve: 0 nothing, 1 relaunch the Cholesky (a wait ran past
+    // its cap), 2 the reference-order LU (a non-positive pivot) -- the same on every rank
+    int action_h(int s) const {
+        const int* w = reinterpret_cast<const int*>(static_cast<const double*>(pin_[s]) + np_ + mp_);
+        return agree_ ? w[1] : solve_status_code(w[0]);
     }
     // the rest of a trip once sigma_[s] is known: trial point (unless the solve formed it), its
     // residuals, copies back
@@ -284,15 +302,23 @@ class LMAsync {
         check(pnol_event_record(ctx_, ev_[s]), "event");
     }
     void wait(int s) { check(pnol_event_wait(ev_[s]), "event wait"); }
-    // the reference-order LU for a trip whose Cholesky reported a non-positive pivot (A intact)
-    void redo_lu(int s) {
+    // trip s's solve again, on every rank alike (action_h): A from the trip's tiles, then the
+    // reference-order LU after a non-positive pivot (action 2), or the same Cholesky relaunched
+    // after a timed-out wait (action 1; pnol_solve_d method 0 retries a timeout itself, and a
+    // pivot it finds non-positive goes to the LU there -- A is the same on every rank, so that
+    // outcome is too).  Then the trial point and its residuals again: in rows mode that is the
+    // same F exchange on every rank.
+    void redo(int s, int action) {
         check(pnol_ctx_synchronize(ctx_), "sync");
-        if (trip_fused_ && sliced_)
+        if (trip_fused_ && sliced_) {
             check(pnol_lm_normal_unpack_mpi_d(ctx_, m_, n_, lambda_[s], A_.get(), lda_), "normal equations");
-        else if (trip_fused_)
+        } else if (trip_fused_) {
             check(pnol_lm_trip_normal_d(ctx_, m_, n_, lambda_[s], A_.get(), lda_), "normal equations");
+            // -J^T F again (the reducing Cholesky's first task wrote it; bitwise pnol_jtr_d's)
+            check(pnol_jtr_d(ctx_, JT_.get(), ldjt_, m_, n_, F(s), rhs_.get()), "jtr");
+        }
         int info = 0;
-        check(pnol_solve_d(ctx_, A_.get(), lda_, rhs_.get(), sig(s), n_, 2, &info), "solve");
+        check(pnol_solve_d(ctx_, A_.get(), lda_, rhs_.get(), sig(s), n_, action == 2 ? 2 : 0, &info), "solve");
         finish(s);
         wait(s);
     }
@@ -303,6 +329,7 @@ class LMAsync {
     int n_, m_, ldjt_, lda_;
     bool sliced_;
     bool trip_fused_ = false;
+    bool agree_ = false;
     double lambda_[2] = {0, 0};   // trip s's lambda (the fused trip's LU fallback forms A)
     int np_ = 0, mp_ = 0;
     DevVec JT_, A_, rhs_, h_, x_[2], trip_[2];
@@ -364,10 +391,13 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool s
         if (hprof) h_enq += std::chrono::duration<double, std::micro>(hnow() - t0).count();
         dev.wait(s);
         if (hprof) t_dec = hnow();
-        if (dev.info_h(s) != 0) {
-            if (std::getenv("PNOL_LM_DEBUG"))   // which trips fell back (a timed-out chain: status <= -7)
-                std::cerr << "[pnol] LM trip " << iter << ": solve status " << dev.info_h(s) << ", LU redo" << std::endl;
-            dev.redo_lu(s);
+        if (const int action = dev.action_h(s)) {
+            // the same action on every rank (agreed in the trip); a timed-out wait is never mapped
+            // to the LU, and is always reported (PNOL_LM_DEBUG: the LU redos too)
+            if (action == 1 || std::getenv("PNOL_LM_DEBUG"))
+                std::cerr << "[pnol] LM trip " << iter << ": solve status " << dev.info_h(s) << " (agreed action "
+                      << action << "): " << (action == 2 ? "reference-order LU" : "Cholesky relaunched") << std::endl;
+            dev.redo(s, action);
         }
         obj->countEvals(own_cols + 1); // the trip's Jacobian
         obj->countEvals(1);            // its trial point

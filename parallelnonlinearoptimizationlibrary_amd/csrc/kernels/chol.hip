@@ -17,7 +17,9 @@
 // A final launch solves L^T x = z by block rows from the bottom up, chained by ready flags, each
 // diagonal block applied as the product W_w^T v.
 // A non-positive (or NaN) pivot sets *info; the host then solves with Gaussian elimination on
-// the untouched A (solve.hip).  Every wait is spin-capped, so a broken chain ends in a fallback.
+// the untouched A (solve.hip).  Every wait is spin-capped: a wait past the cap sets *info to
+// kCholTimeout and the host relaunches the same factorisation (bitwise the same result), never
+// the LU -- a timeout is a scheduling event, not a property of A.
 #include "../pnol_internal.hpp"
 
 #include <algorithm>
@@ -31,8 +33,10 @@ constexpr int NB = 64;
 constexpr int kPad = 18;             // LDS row stride of a 64 x 16 K-substage (doubles)
 constexpr int kSub = NB * kPad;      // doubles per substage
 constexpr int kStage = 4 * kSub;     // one 64 x 64 tile as four substages
-constexpr int kSpin = 1 << 24;       // ~1 s of polling
-constexpr int kInfoTimeout = -7;
+constexpr int kSpin = 1 << 24;       // polls (each >= one s_sleep(1) + one L2 round trip)
+// a wait that ran past kSpin: a scheduling event, never a numerical result -- the first failure
+// recorded sticks (atomicCAS), and the host relaunches the same factorisation (launch_solve)
+constexpr int kInfoTimeout = kCholTimeout;
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
@@ -205,7 +209,7 @@ __device__ __forceinline__ bool spin_ge(const int* f, int target, int* info) {
         if ((++it & 63) == 0) {
             if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
             if (it > kSpin) {
-                atomicExch(info, kInfoTimeout);
+                atomicCAS(info, 0, kInfoTimeout);
                 return false;
             }
         }
@@ -230,7 +234,7 @@ __device__ __forceinline__ bool spin_all(const int* const (&f)[N], const int (&t
         if ((++it & 63) == 0) {
             if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
             if (it > kSpin) {
-                atomicExch(info, kInfoTimeout);
+                atomicCAS(info, 0, kInfoTimeout);
                 return false;
             }
         }
@@ -1671,7 +1675,7 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm,
                 if ((++it & 63) == 0) {
                     if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
                     if (it > kSpin) {
-                        atomicExch(info, kInfoTimeout);
+                        atomicCAS(info, 0, kInfoTimeout);
                         return;   // every wave leaves (waves that ended no longer hold the barrier)
                     }
                 }
@@ -1820,7 +1824,7 @@ static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, i
 
 // the backward solve (+ the trial point)
 static int chol_bwd_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, int n, double* sigma, int* dinfo,
-                           const double* xbase, double* xnext) {
+                           const double* xbase, double* xnext, bool trip = false) {
     const int epoch = ++ctx->chol4_epoch;
     if (w.gran && ((uintptr_t)w.xw & 15) != 0) return PNOL_ERR_ARG;   // granules need 16-byte alignment
     if (w.gran)
@@ -1832,13 +1836,18 @@ static int chol_bwd_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, int n
                            (const double*)w.W, (const double*)w.bv, (const double*)w.zv, w.xw, sigma, w.bwdflag, epoch,
                            dinfo, xbase, xnext);
     PNOL_CHECK(launch_check());
-    // test hook (tests/test_gpu_solvers.py): report a non-positive pivot so the callers' LU
-    // fallback paths run on an SPD system (read per call: the tests flip it)
-    if (const char* e = std::getenv("PNOL_CHOL_FORCE_FALLBACK"))
-        if (std::atoi(e) != 0) {
-            hipLaunchKernelGGL(k_flag_info, dim3(1), dim3(1), 0, st, dinfo, 1);
+    // test hook (tests/test_gpu_solvers.py, tests/test_gpu_mpi.py; read per call: the tests flip
+    // it, per rank too): a value > 0 reports a non-positive pivot on every Cholesky solve, so the
+    // callers' LU paths run on an SPD system; kCholTimeout (-7) reports a timed-out wait on the LM
+    // trip's reducing solves only (`trip`), so the caller's relaunch -- which is not forced --
+    // runs
+    if (const char* e = std::getenv("PNOL_CHOL_FORCE_FALLBACK")) {
+        const int v = std::atoi(e);
+        if (v > 0 || (v == kCholTimeout && trip)) {
+            hipLaunchKernelGGL(k_flag_info, dim3(1), dim3(1), 0, st, dinfo, v);
             return launch_check();
         }
+    }
     return PNOL_OK;
 }
 
@@ -1915,7 +1924,7 @@ int launch_chol_reducing_run(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, c
     red.jp = jp;
     red.rhs = rhs;
     PNOL_CHECK(chol_persist_launch(ctx, st, cr.w, cr.dinfo, red));
-    return chol_bwd_launch(ctx, st, cr.w, cr.n, sigma, cr.dinfo, xbase, xnext);
+    return chol_bwd_launch(ctx, st, cr.w, cr.n, sigma, cr.dinfo, xbase, xnext, true);
 }
 
 // LevMarqMPI: the same from the allgathered, summed tiles (packed) and the formed rhs
@@ -1931,7 +1940,7 @@ int launch_chol_reducing_run_packed(pnol_ctx* ctx, hipStream_t st, const CholRed
     red.n = cr.n;
     red.lambda = lambda;
     PNOL_CHECK(chol_persist_launch(ctx, st, cr.w, cr.dinfo, red));
-    return chol_bwd_launch(ctx, st, cr.w, cr.n, sigma, cr.dinfo, xbase, xnext);
+    return chol_bwd_launch(ctx, st, cr.w, cr.n, sigma, cr.dinfo, xbase, xnext, true);
 }
 
 }  // namespace pnol

@@ -5,10 +5,11 @@
 //   k_lu_*     Gaussian elimination with partial pivoting in the reference's operation order:
 //              the method for n <= PNOL_SEQ_MAX (so the small ExampleObjectives problems are
 //              bitwise the CPU path's), and the fallback after a non-positive (or NaN) Cholesky
-//              pivot or a timed-out chain
+//              pivot (a timed-out wait relaunches the Cholesky instead)
 //   k_luinv_*  matrixInverse as one elimination of [B | I] plus per-column back substitution
 // (Round 4 removed the per-panel-launch Cholesky and the one-launch tile-DAG Cholesky, methods 1
 // and 3: both slower than the chol.hip forms and on no default path.)
+#include "../pnol_comm.hpp"
 #include "../pnol_internal.hpp"
 
 #include <cstring>
@@ -202,6 +203,19 @@ __global__ void k_copy_matrix(const double* __restrict__ A, long lda, double* __
 
 __global__ void k_set_int(int* p, int v) { *p = v; }
 
+// the solve status's code (solve_status_code) as a double for the allgather, or -- one rank --
+// straight into dinfo[1]
+__global__ void k_status_code(int* dinfo, double* out) {
+    const int c = solve_status_code(dinfo[0]);
+    if (out) *out = (double)c;
+    else dinfo[1] = c;
+}
+__global__ void k_status_max(const double* all, int P, int* dinfo) {
+    int c = 0;
+    for (int r = 0; r < P; ++r) c = max(c, (int)all[r]);
+    dinfo[1] = c;
+}
+
 }  // namespace
 
 static int lu_solve(pnol_ctx* ctx, const double* A, int lda, const double* rhs, double* sigma, int n, int* dinfo) {
@@ -260,6 +274,22 @@ int launch_matrix_inverse(pnol_ctx* ctx, const double* B, int ldb, int n, double
     return PNOL_OK;
 }
 
+int launch_status_agree(pnol_ctx* ctx, int* dinfo) {
+    const int P = comm_size();
+    if (P <= 1) {
+        hipLaunchKernelGGL(k_status_code, dim3(1), dim3(1), 0, ctx->stream, dinfo, (double*)nullptr);
+        return launch_check();
+    }
+    void* buf = nullptr;
+    PNOL_CHECK(ws_get(ctx, "status_agree", sizeof(double) * (size_t)(P + 1), &buf));
+    double* mine = (double*)buf;
+    hipLaunchKernelGGL(k_status_code, dim3(1), dim3(1), 0, ctx->stream, dinfo, mine);
+    PNOL_CHECK(launch_check());
+    PNOL_CHECK(comm_allgather_device(ctx, mine, mine + 1, 1));
+    hipLaunchKernelGGL(k_status_max, dim3(1), dim3(1), 0, ctx->stream, (const double*)(mine + 1), P, dinfo);
+    return launch_check();
+}
+
 int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* sigma, int n, int method,
                  int* info) {
     if (!A || !rhs || !sigma || n <= 0 || lda < n) return PNOL_ERR_ARG;
@@ -273,16 +303,27 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
         variant = 0;         // the default form (launch_chol_solve_v)
     }
     if (method == 4 || method == 5) {
-        // lookahead tile Cholesky with diagonal inverses (chol.hip); A itself is not modified
-        PNOL_CHECK(launch_chol_solve_v(ctx, A, lda, rhs, sigma, n, dinfo, variant));
-        int hinfo = 0;
-        PNOL_HIP(hipMemcpyAsync(&hinfo, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-        PNOL_HIP(hipStreamSynchronize(ctx->stream));
-        if (hinfo == 0) {
-            if (info) *info = 1;
-            return PNOL_OK;
+        // lookahead tile Cholesky with diagonal inverses (chol.hip); A itself is not modified.
+        // A wait past its spin cap (kCholTimeout) is a scheduling event, not a property of A:
+        // the same factorisation is relaunched -- per-step launches (method 4, bitwise the
+        // persistent form's result) after the first attempt -- so the solve's bits never depend
+        // on timing; after kRelaunch relaunches the status is an error, not an LU.
+        constexpr int kRelaunch = 2;
+        for (int attempt = 0;; ++attempt) {
+            PNOL_CHECK(launch_chol_solve_v(ctx, A, lda, rhs, sigma, n, dinfo, attempt == 0 ? variant : 4));
+            int hinfo = 0;
+            PNOL_HIP(hipMemcpyAsync(&hinfo, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+            PNOL_HIP(hipStreamSynchronize(ctx->stream));
+            if (hinfo == 0) {
+                if (info) *info = 1;
+                return PNOL_OK;
+            }
+            if (hinfo != kCholTimeout) break;   // a non-positive or NaN pivot: the LU below
+            std::fprintf(stderr, "[pnol_amd] tile Cholesky (n = %d): a dependency wait ran past its cap, relaunch %d\n",
+                         n, attempt + 1);
+            if (attempt >= kRelaunch) return PNOL_ERR_TIMEOUT;
         }
-        // non-positive pivot or a timed-out chain: reference-order LU on A
+        // non-positive pivot: reference-order LU on A
     }
     PNOL_CHECK(lu_solve(ctx, A, lda, rhs, sigma, n, dinfo));
     int hinfo = 0;

@@ -667,6 +667,7 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     const int ntiles = nt * (nt + 1) / 2;
     const SliceCfg sc = slice_cfg(m, ntiles);
     void* part = nullptr;
+    ctx->lm_trip_tiles.kind = 0;   // the trip's tiles are overwritten below
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * kS * sc.sub * kTile * kTile, &part));
     syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
                   syrk_t64(false));
@@ -698,6 +699,7 @@ int launch_jtj_rows(pnol_ctx* ctx, hipStream_t stream, const double* JT, int ldj
     const int t0 = row_begin * (row_begin + 1) / 2, t1 = row_end * (row_end + 1) / 2;
     const size_t per_tile = (size_t)kS * sc.sub * kTile * kTile;
     void* part = nullptr;
+    ctx->lm_trip_tiles.kind = 0;   // the trip's tiles are overwritten below
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * per_tile, &part));
     double* mypart = (double*)part + (size_t)t0 * per_tile;   // disjoint per row range
     syrk_partials(ctx, stream, true, JT, ldjt, sc.mS, n, m, sc, 0, kS, t0, t1 - t0, mypart);
@@ -767,14 +769,6 @@ int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h,
 }
 
 // One LM trip's linear algebra with A never formed (single process, n > PNOL_SEQ_MAX,
-// LevenbergMarquardt.cpp:55-90): the FD Jacobian, the J^T J split-K partials (k_syrk_tile) and
-// the -J^T F slice partials on the context stream, then the persistent tile Cholesky whose first
-// tasks sum both into its padded matrix and b (launch_chol_reducing) -- the reduce launch and the
-// copy of A into the Cholesky's matrix are gone, and the reduce's HBM stream runs beside the
-// chain's first steps -- the backward solve and xnext = x + sigma.  JT, rhs, sigma, xnext and the
-// solve status are bitwise those of launch_fd_jtj (+ rhs) and launch_chol_solve; for the LU
-// fallback launch_jtj_from_partials forms A from the trip's partials.
-// One LM trip's linear algebra with A never formed (single process, n > PNOL_SEQ_MAX,
 // LevenbergMarquardt.cpp:55-90): the FD Jacobian, the -J^T F slice partials, the Cholesky's
 // prep launch, the J^T J split-K partials (k_syrk_tile), then the persistent tile Cholesky whose
 // first tasks sum the partials into its own matrix (and b = -J^T F) -- so the reduce's HBM
@@ -793,6 +787,7 @@ int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
     const int split = kS * sc.sub;
     // every workspace first: a (re)allocation frees, and a free waits for the device
     void *part = nullptr, *jp = nullptr;
+    ctx->lm_trip_tiles.kind = 0;   // the trip's tiles are overwritten below
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * split * kTile * kTile, &part));
     PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
     CholRed cr;
@@ -804,14 +799,20 @@ int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
                   syrk_t64(false));
     PNOL_CHECK(launch_check());
     ScopedTimer tm(ctx, "solve");
-    return launch_chol_reducing_run(ctx, ctx->stream, cr, (const double*)part, sc.sub, (const double*)jp, lambda, rhs,
-                                    sigma, x, xnext);
+    PNOL_CHECK(launch_chol_reducing_run(ctx, ctx->stream, cr, (const double*)part, sc.sub, (const double*)jp, lambda,
+                                        rhs, sigma, x, xnext));
+    ctx->lm_trip_tiles = {1, m, n, 1};   // pnol_lm_trip_normal_d may form A from these partials
+    return PNOL_OK;
 }
 
 // A (lower triangle + mirror, the Marquardt diagonal) from the split-K partials of the last
 // launch_fd_normal_solve (the same reduce as launch_jtj, so the same A)
 int launch_jtj_from_partials(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda) {
     if (!A || m <= 0 || n <= PNOL_SEQ_MAX || lda < n) return PNOL_ERR_ARG;
+    // the partials must still be the last trip's, of this shape (any other J^T J call since
+    // overwrote them)
+    const auto& tt = ctx->lm_trip_tiles;
+    if (tt.kind != 1 || tt.m != m || tt.n != n || tt.nranks != 1) return PNOL_ERR_ARG;
     const int nt = (n + kTile - 1) / kTile;
     const int ntiles = nt * (nt + 1) / 2;
     const SliceCfg sc = slice_cfg(m, ntiles);
@@ -838,6 +839,7 @@ int launch_jtj_sharded(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, 
     const int t0 = std::min(ntiles, rank * tpr), cnt = std::min(ntiles, t0 + tpr) - t0;
     const size_t E = (size_t)kTile * kTile;
     void *part = nullptr, *packed = nullptr;
+    ctx->lm_trip_tiles.kind = 0;   // the trip's tiles are overwritten below
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)std::max(cnt, 1) * kS * sc.sub * E, &part));
     PNOL_CHECK(ws_get(ctx, "syrk_packed", sizeof(double) * (size_t)P * tpr * E, &packed));
     double* mine = (double*)packed + (size_t)rank * tpr * E;
@@ -934,6 +936,7 @@ static int lm_normal_core(pnol_ctx* ctx, const double* JTs, int m, int n, double
     lm_rank_slices(P, me, &s0, &s1);
     const int nsl = s1 - s0;
     void* part = nullptr;
+    ctx->lm_trip_tiles.kind = 0;   // the trip's tiles are overwritten below
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * std::max(nsl, 1) * sc.sub * E, &part));
     const bool t64 = syrk_t64(true);
     if (nsl > 0) {
@@ -1064,9 +1067,14 @@ int launch_lm_normal_solve(pnol_ctx* ctx, const double* JTs, int m, int n, doubl
     PNOL_CHECK(launch_chol_reducing_start(ctx, cr));
     ScopedTimer tm(ctx, "solve");
     if (tl.partials)
-        return launch_chol_reducing_run(ctx, ctx->stream, cr, tl.part, tl.sub, tl.jp, lambda, rhs, sigma, xbase, xnext);
-    return launch_chol_reducing_run_packed(ctx, ctx->stream, cr, tl.packed, tl.slot, tl.tpr, rhs, lambda, sigma, xbase,
-                                           xnext);
+        PNOL_CHECK(launch_chol_reducing_run(ctx, ctx->stream, cr, tl.part, tl.sub, tl.jp, lambda, rhs, sigma, xbase,
+                                            xnext));
+    else
+        PNOL_CHECK(launch_chol_reducing_run_packed(ctx, ctx->stream, cr, tl.packed, tl.slot, tl.tpr, rhs, lambda, sigma,
+                                                   xbase, xnext));
+    // pnol_lm_normal_unpack_mpi_d may form A from these tiles
+    ctx->lm_trip_tiles = {tl.partials ? 1 : 2, m, n, comm_size()};
+    return PNOL_OK;
 }
 
 // A from the tiles the last launch_lm_normal_solve left (the LU fallback; the same A as
@@ -1075,6 +1083,8 @@ int launch_lm_normal_unpack(pnol_ctx* ctx, int m, int n, double lambda, double* 
     if (!A || m <= 0 || n <= PNOL_SEQ_MAX || lda < n) return PNOL_ERR_ARG;
     const int P = comm_size();
     if (P == 1) return launch_jtj_from_partials(ctx, m, n, lambda, A, lda);
+    const auto& tt = ctx->lm_trip_tiles;   // the last trip's allgathered tiles, of this shape
+    if (tt.kind != 2 || tt.m != m || tt.n != n || tt.nranks != P) return PNOL_ERR_ARG;
     const int nt = (n + kTile - 1) / kTile;
     const int ntiles = nt * (nt + 1) / 2;
     const long E = (long)kTile * kTile;

@@ -69,6 +69,14 @@ struct pnol_ctx {
     // LevMarqMPI's FD decomposition (fd.hip): -1 = not chosen yet (PNOL_LM_FD at first use),
     // 0 = columns (the reference's: FD column tiles per rank + the m-slice exchange), 1 = rows
     int lm_fd_mode = -1;
+    bool lm_fd_mode_set = false;   // set by pnol_lm_set_fd_mode: the LevMarqMPI drop-in keeps it
+    // What the last LM trip without A (launch_fd_normal_solve / launch_lm_normal_solve) left for
+    // its A-forming entry points (pnol_lm_trip_normal_d, pnol_lm_normal_unpack_mpi_d): the
+    // split-K partials ("syrk_part", kind 1) or the allgathered tiles ("lm_packed", kind 2) of
+    // shape (m, n) over nranks ranks.  Every other writer of those buffers clears it.
+    struct {
+        int kind = 0, m = 0, n = 0, nranks = 0;
+    } lm_trip_tiles;
     // columns mode: the m-slice exchange of each FD tile runs on comm_stream, gated by the
     // event recorded behind that tile's FD launch on the context stream
     hipStream_t comm_stream = nullptr;
@@ -175,6 +183,17 @@ inline int launch_check() {
     }
     return PNOL_OK;
 }
+
+// The tile Cholesky's status for a wait that ran past its spin cap (chol.hip): not a numerical
+// result -- launch_solve relaunches the factorisation, the LM loop redoes the trip's solve
+constexpr int kCholTimeout = -7;
+// status codes a solve status maps to, ordered so that the max over ranks is the action every
+// rank takes: 0 none, 1 a timed-out wait (relaunch the Cholesky), 2 a non-positive / NaN pivot
+// (the reference-order LU)
+__host__ __device__ inline int solve_status_code(int info) { return info == 0 ? 0 : info == kCholTimeout ? 1 : 2; }
+// dinfo[1] = max over the communicator's ranks of solve_status_code(dinfo[0]) (device ints),
+// queued on the context stream (solve.hip)
+int launch_status_agree(pnol_ctx* ctx, int* dinfo);
 
 // ---- kernel launchers (defined in kernels/*.hip) ------------------------------------
 int launch_gemv_neg(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y);
@@ -302,8 +321,9 @@ int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
 // rank's rows to all ranks; columns mode: all rows on every rank (fd.hip)
 int launch_lm_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* F);
 // LevMarqMPI's decomposition on this context: rows mode (1) or columns mode (0); the first call
-// reads PNOL_LM_FD ("rows" -> 1, anything else -> 0), later calls keep it (lm_fd_mode_reset
-// re-reads it: once per LevMarqMPI solve, checked equal on every rank)
+// reads PNOL_LM_FD ("rows" -> 1, anything else -> 0), later calls keep it.  The LevMarqMPI
+// drop-in re-reads the environment once per solve unless pnol_lm_set_fd_mode chose the mode,
+// and checks it equal on every rank.
 bool lm_rows_mode(pnol_ctx* ctx);
 int lm_fd_mode_env();
 

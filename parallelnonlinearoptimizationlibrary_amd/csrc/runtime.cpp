@@ -436,6 +436,7 @@ const char* pnol_status_string(int s) {
         case PNOL_ERR_SINGULAR: return "singular system";
         case PNOL_ERR_COMM: return "communicator error";
         case PNOL_ERR_UNSUPPORTED: return "unsupported";
+        case PNOL_ERR_TIMEOUT: return "device wait timed out (the tile Cholesky, after its relaunches)";
         default: return "unknown status";
     }
 }

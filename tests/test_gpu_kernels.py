@@ -754,6 +754,43 @@ def test_lm_trip_reports_non_spd(ctx):
     assert np.array_equal(_np(sb), _np(sa))
 
 
+def test_lm_agree_status_codes_one_rank(ctx):
+    """pnol_lm_agree_status_d with one rank: dinfo[1] = the action code of dinfo[0] -- 0 none, 1 a
+    timed-out Cholesky wait (kCholTimeout = -7: relaunch the Cholesky), 2 any other nonzero status
+    (a non-positive / NaN pivot: the reference-order LU)."""
+    import ctypes as C
+    import torch
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    for v, code in ((0, 0), (-7, 1), (5, 2), (-1, 2), (2049, 2)):
+        t = torch.tensor([v, 99], dtype=torch.int32, device=f"cuda:{ctx.device}")
+        L.check(L.lib().pnol_lm_agree_status_d(ctx.h, C.c_void_p(t.data_ptr())), "agree")
+        ctx.synchronize()
+        assert t.cpu().tolist() == [v, code], (v, t.cpu().tolist())
+
+
+def test_lm_trip_normal_refuses_stale_partials(ctx):
+    """pnol_lm_trip_normal_d forms A only from the partials of the last pnol_lm_trip_d of the same
+    (m, n): after another J^T J call overwrote them, or for another shape, it refuses
+    (PNOL_ERR_ARG) instead of returning a wrong A."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    m, n = 1000, 300
+    d = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+    x, h = ctx.tensor(np.linspace(-0.5, 0.5, n)), ctx.tensor(np.full(n, 1e-7))
+    JT = ctx.empty(n, m)
+    d.lm_trip(x, h, 0.5, JT)
+    ctx.synchronize()
+    ctx.lm_trip_normal(m, n, 0.5)                          # the trip's own partials: fine
+    with pytest.raises(L.PnolError) as e:
+        ctx.lm_trip_normal(m + 64, n, 0.5)                 # another shape
+    assert e.value.status == L.PNOL_ERR_ARG
+    ctx.jtj(JT, 0.5)                                       # overwrites the partials
+    ctx.synchronize()
+    with pytest.raises(L.PnolError) as e:
+        ctx.lm_trip_normal(m, n, 0.5)
+    assert e.value.status == L.PNOL_ERR_ARG
+
+
 def test_synthetic_data_matches_oracle_stream(ctx, oracle):
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective

@@ -24,12 +24,13 @@ def _free_port():
     return p
 
 
-def _run_workers(tmp_path, world, m, n, *extra):
+def _run_workers(tmp_path, world, m, n, *extra, rank_env=None):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", PNOL_DEVICE="0",
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.update((rank_env or {}).get(r, {}))
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_mpi_worker.py"), str(tmp_path),
                                        str(m), str(n), *extra], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT))
@@ -128,6 +129,36 @@ def test_levmarq_mpi_trip_forms_bitwise(tmp_path, monkeypatch, trip, force, worl
         z = np.load(tmp_path / f"rank{r}.npz")
         assert np.array_equal(z["X"], X1), (trip, force, r)
         assert np.array_equal(z["F0"], F01) and np.array_equal(z["FO"], FO1), (trip, force, r)
+
+
+@pytest.mark.parametrize("status", ["1", "-7"])
+@pytest.mark.parametrize("mode", ["columns", "rows"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_levmarq_mpi_one_rank_solve_status(tmp_path, monkeypatch, status, mode, world):
+    """One rank's trip solve reports a status its peers do not see (PNOL_CHOL_FORCE_FALLBACK on
+    the last rank only, every trip): a non-positive pivot (1) or a timed-out wait (-7).  The
+    reference's replicas never branch per rank -- each runs the same luSolve on the same A
+    (LevenbergMarquardtMPI.cpp:88) -- so the status is agreed over the ranks inside the trip
+    (pnol_lm_agree_status_d) and every rank takes the same action: the reference-order LU for a
+    pivot, the same Cholesky relaunched for a timeout.  In both FD modes (rows mode exchanges the
+    trial residuals, so a rank-local redo would desync the collectives) X, F0 and FOpt on every
+    rank are bitwise the one-GPU LevMarq's with the LU on every trip (status 1) or unforced (-7)."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_levmarq
+    m, n = 1000, 700
+    _set_mode(monkeypatch, mode)
+    monkeypatch.delenv("PNOL_CHOL_FORCE_FALLBACK", raising=False)
+    _run_workers(tmp_path, world, m, n, "lmonly", rank_env={world - 1: {"PNOL_CHOL_FORCE_FALLBACK": status}})
+    monkeypatch.delenv("PNOL_LM_FD", raising=False)
+    if status == "1":
+        monkeypatch.setenv("PNOL_CHOL_FORCE_FALLBACK", "1")
+    ctx = Context(0)
+    obj = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+    X1, F01, FO1, _ = run_levmarq(obj, np.zeros(n), (0.001, 10.0, 1e-7, 5, 0.0, -1), which=0)
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        assert np.array_equal(z["X"], X1), (status, mode, r)
+        assert np.array_equal(z["F0"], F01) and np.array_equal(z["FO"], FO1), (status, mode, r)
 
 
 @pytest.mark.parametrize("mode", ["columns", "rows"])

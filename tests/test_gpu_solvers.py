@@ -588,6 +588,27 @@ def test_lm_fused_trip_loop_equals_general_loop(ctx, oracle, m, n, force, monkey
     assert rel(out["fused"][0], xs) <= 1e-8
 
 
+@pytest.mark.parametrize("m,n", [(3000, 257), (2000, 700)])
+def test_lm_timed_out_trip_relaunches_cholesky(ctx, oracle, m, n, monkeypatch, capfd):
+    """A trip whose Cholesky reports a dependency wait past its spin cap (forced on every trip's
+    reducing solve by PNOL_CHOL_FORCE_FALLBACK=-7) is a scheduling event, not a property of A: the
+    loop redoes the trip's solve with the same Cholesky (never the LU; the relaunch is not forced)
+    and reports it, so the trajectory -- X, F0, FOpt, evaluation count -- is bitwise the unforced
+    run's.  (The reference's luSolve, LevenbergMarquardt.cpp:83, has no timing-dependent branch.)"""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_levmarq
+    A, xs, y = oracle.linres_data(m, n)
+    params = (0.001, 10, 1e-7, 6, 0.0, -1)
+    monkeypatch.setenv("PNOL_CHOL_FORCE_FALLBACK", "-7")
+    Xt, F0t, FOt, rt = run_levmarq(_obj(ctx, L.OBJ_LINRES, n, m, A, y), np.zeros(n), params)
+    err = capfd.readouterr().err
+    assert err.count("Cholesky relaunched") == 6, err[-2000:]
+    monkeypatch.delenv("PNOL_CHOL_FORCE_FALLBACK")
+    X, F0, FO, r = run_levmarq(_obj(ctx, L.OBJ_LINRES, n, m, A, y), np.zeros(n), params)
+    assert np.array_equal(Xt, X) and np.array_equal(F0t, F0) and np.array_equal(FOt, FO)
+    assert rt.evals == r.evals
+
+
 @pytest.mark.parametrize("n", [1, 7, 100, 300])
 def test_matrix_inverse_bitwise(ctx, oracle, n):
     """pnol_matrix_inverse_d (one elimination of [B | I], per-column back substitution) equals
