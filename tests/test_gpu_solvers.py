@@ -441,7 +441,7 @@ def _quad_grad(d, b, x):
     return d * x - b + 0.25 * (np.r_[x[1:], 0.0] + np.r_[0.0, x[:-1]])
 
 
-@pytest.mark.parametrize("n", [200, 500, 1000])
+@pytest.mark.parametrize("n", [200, 500, 1000, 2048])
 def test_bfgs_bnd_fast_mode_cfg5_matches_oracle(ctx, oracle, n):
     """Serial BFGS_Bnd in fast mode (n > PNOL_SEQ_MAX: lazy rank-2 passes, the diagonal-D
     shortcuts, one borrowed device buffer for the whole active-set recursion) on the cfg-5
@@ -452,7 +452,8 @@ def test_bfgs_bnd_fast_mode_cfg5_matches_oracle(ctx, oracle, n):
     order, so the last reduced problem stops at a slightly different point inside the gradient
     tolerance (minGrad2Norm 1e-5 with FD steps of 1e-6): X is compared within 2e-6 (absolute,
     |X| <= 0.5; measured 4.3e-7 at n = 500), F within 1e-10 relative, the active set exactly,
-    the iteration and evaluation counts within 5% (the recursion path is the same)."""
+    the iteration and evaluation counts within 5% (the recursion path is the same).  n = 2048:
+    1385 recursion levels; the oracle's run takes ~1.5 min of one host core."""
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective, run_bfgs
     dd, bb = oracle.quadratic_data(n, bscale=4.0)
@@ -495,8 +496,10 @@ def test_bfgs_bnd_cfg5_full_size_properties(ctx):
     xs = _box_qp_solution(dd, bb, lb, ub)
     g = _quad_grad(dd, bb, X)
     free = (X > lb + 1e-5) & (X < ub - 1e-5)
-    assert np.max(np.abs(g[free])) <= 1e-3
-    assert np.max(np.abs(X - xs)) <= 1e-3, np.max(np.abs(X - xs))
+    # measured (profiles/r04_bench.json, bfgs_bnd_cfg5_solve): max |X - x*| = 9.99e-6; the bound is
+    # 2x that, and the free gradient 4 (the largest diagonal entry) times it plus the FD step
+    assert np.max(np.abs(g[free])) <= 1e-4, np.max(np.abs(g[free]))
+    assert np.max(np.abs(X - xs)) <= 2e-5, np.max(np.abs(X - xs))
     act = lambda x: (np.abs(x - lb) < 1e-5).astype(int) - (np.abs(x - ub) < 1e-5).astype(int)
     assert np.mean(act(X) != act(xs)) <= 1e-3
 
