@@ -350,8 +350,11 @@ def cpu_baseline(m, n, budget_s=20.0):
     t_lu = t_lu_s * (n / nl) ** 3
     t_trip1 = t_eval * (n + 2) + t_row * n + t_lu
     t_tripP_sampled = t_eval_par * (n + 2) + t_row_par * n + t_lu
+    # the whole trip timed twice (a one-shot timing of a multi-second threaded trip is exposed to
+    # noise; it sets the baseline): value from their median, both samples in the line
     with ThreadPoolExecutor(P) as ex:
-        t_trip_whole, _ = cpu_lm_trip(O, objs, np.zeros(n), np.full(n, 1e-7), ex, P)
+        s_trip = [cpu_lm_trip(O, objs, np.zeros(n), np.full(n, 1e-7), ex, P)[0] for _ in range(2)]
+    t_trip_whole = float(np.median(s_trip))
     t_tripP = t_trip_whole
     # cfg 1: the whole BFGS solve on the 2-D Rosenbrock (the reference's CPU example)
     g1 = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_survey.json")))["bfgs_rosenbrock2_m12_1"]
@@ -388,13 +391,15 @@ def cpu_baseline(m, n, budget_s=20.0):
         "value": 1.0 / t_tripP, "unit": "LM iters/sec", "cores": P, "kind": "port",
         "cpu_model": model, "host_logical_cpus": ncpu,
         "sample": (f"oracle (C restatement, gcc -O3 -march=x86-64-v3 -ffp-contract=off) at m={m}, n={n}: one whole LM "
-                   f"trip timed end to end on {P} threads ({t_trip_whole:.1f} s: F(x), the FD Jacobian's columns "
+                   f"trip timed end to end on {P} threads, median of 2 ({t_trip_whole:.1f} s: F(x), the FD Jacobian's columns "
                    f"round-robin over the threads, J^T J rows by the reference matrixMultiply split over the threads, "
                    f"-J^T F, luSolve, F(x + sigma)) on a {model}; the 1-thread trip extrapolated from medians of "
                    f"sampled legs: residual eval {t_eval*1e3:.1f} ms x{n + 2}, a J^T J row {t_row*1e3:.1f} ms x{n}, LU "
                    f"at n={nl} {t_lu_s:.2f} s scaled by (n/{nl})^3 = {t_trip1:.1f} s (the same legs on {P} threads: "
                    f"{t_tripP_sampled:.1f} s)"),
         "seconds_per_trip": t_tripP, "seconds_per_trip_whole_timed": t_trip_whole,
+        "seconds_per_trip_whole_samples": s_trip,
+        "whole_over_sampled_P_threads": t_trip_whole / t_tripP_sampled,
         "seconds_per_trip_sampled_P_threads": t_tripP_sampled,
         "seconds_per_trip_1_thread": t_trip1, "iters_per_s_1_thread": 1.0 / t_trip1,
         "threads": P,

@@ -202,11 +202,17 @@ class LMAsync {
             for (int v : all)
                 if (v != ctx->lm_fd_mode) throw std::runtime_error("LevMarqMPI: ranks disagree on PNOL_LM_FD");
         }
-        // one trip without forming A (pnol_lm_trip_d; PNOL_LM_TRIP=0 keeps the two calls below;
-        // read once per solve)
-        {   // (LevMarqMPI: the normal equations and the solve in one call, A not formed either)
+        // The trip without forming A (pnol_lm_trip_d / pnol_lm_normal_solve_mpi_d: the persistent
+        // Cholesky's first tasks reduce the J^T J tiles into its own matrix) or the two calls (A
+        // formed by the reduce launch, then the solve).  Default: the fused form only where the
+        // tiles arrive summed (LevMarqMPI on several ranks: the allgathered tiles, 33.5 MB); with
+        // one rank its reduce tasks stream the 285 MB of split-K partials in front of the chain's
+        // first steps, and the two calls measured faster in 5 of 5 alternating same-box pairs
+        // (324-328.5 vs 317-321 LM iters/s, profiles/r05_trip_ab.txt).  PNOL_LM_TRIP=1 / 0
+        // forces either (read once per solve).
+        {
             const char* e = std::getenv("PNOL_LM_TRIP");
-            trip_fused_ = !e || std::atoi(e) != 0;
+            trip_fused_ = e ? std::atoi(e) != 0 : (sliced && comm_size() > 1);
         }
         // several ranks: every trip's solve status is agreed over the ranks before the host acts
         // on it (pnol_lm_agree_status_d), so all replicas take the same branch

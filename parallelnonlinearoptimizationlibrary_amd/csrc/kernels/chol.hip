@@ -1839,8 +1839,8 @@ static int chol_bwd_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, int n
     // test hook (tests/test_gpu_solvers.py, tests/test_gpu_mpi.py; read per call: the tests flip
     // it, per rank too): a value > 0 reports a non-positive pivot on every Cholesky solve, so the
     // callers' LU paths run on an SPD system; kCholTimeout (-7) reports a timed-out wait on the LM
-    // trip's reducing solves only (`trip`), so the caller's relaunch -- which is not forced --
-    // runs
+    // trip's solves only (`trip`: the reducing form, pnol_solve_step_d), so the caller's relaunch
+    // -- pnol_solve_d, which is not forced -- runs
     if (const char* e = std::getenv("PNOL_CHOL_FORCE_FALLBACK")) {
         const int v = std::atoi(e);
         if (v > 0 || (v == kCholTimeout && trip)) {
@@ -1865,7 +1865,8 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
                            w.rowflag, epoch, dinfo, A, (long)lda, n, rhs, w.pf, persist ? w.npf : 0);
     }
     if (persist) PNOL_CHECK(chol_persist_launch(ctx, ctx->stream, w, dinfo, RedArgs{}));
-    return chol_bwd_launch(ctx, ctx->stream, w, n, sigma, dinfo, xbase, xnext);
+    // (xnext: the LM loop's trip solve -- pnol_solve_step_d -- which the timeout test hook may force)
+    return chol_bwd_launch(ctx, ctx->stream, w, n, sigma, dinfo, xbase, xnext, xnext != nullptr);
 }
 
 // The reducing form's prep: the persistent form's progress words -- the tile versions and b's

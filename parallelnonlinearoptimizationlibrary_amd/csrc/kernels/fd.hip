@@ -1090,6 +1090,29 @@ int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
         lm_phase_tiles(n, P, q, pst[q], pct[q]);
         nphase = std::max(nphase, (int)pst[q].size());
     }
+    // PNOL_LM_PHASED=0 (read per call, the same on every rank): one tile-list launch, then every
+    // tile's slices in one exchange on the context stream after it -- no second stream, no
+    // events; the same bits (the phased form's RCCL transport first runs on a multi-GPU node)
+    if (const char* e = std::getenv("PNOL_LM_PHASED"))
+        if (std::atoi(e) == 0) {
+            const int mine = (int)pst[me].size();
+            PNOL_CHECK(launch_fd_jacobian_tiles(ctx, o, x, h, pst[me].data(), pct[me].data(), mine, F0, compute_f0,
+                                                JTs, 0, mS, 1, mS, sstr));
+            ScopedTimer tm(ctx, "exchange_J");
+            return comm_exchange(ctx, JTs, JTs, [&](int q, int d, std::vector<XBlock>& bl) {
+                bl.clear();
+                int s0, s1;
+                lm_rank_slices(P, d, &s0, &s1);
+                for (size_t k = 0; k < pst[q].size(); ++k) {
+                    const size_t c0 = (size_t)pst[q][k], cc = (size_t)pct[q][k];
+                    for (int s = s0; s < s1; ++s) {
+                        if ((long)s * mS >= o->m) break;
+                        const size_t off = (size_t)s * sstr + c0 * mS;
+                        bl.push_back({off, off, cc * mS});
+                    }
+                }
+            });
+        }
     PNOL_CHECK(lm_comm_stream(ctx, nphase + 1));
     const int mine = (int)pst[me].size();
     // phase k is gated by the event behind this rank's k-th tile; phases past its last tile

@@ -131,6 +131,27 @@ def test_levmarq_mpi_trip_forms_bitwise(tmp_path, monkeypatch, trip, force, worl
         assert np.array_equal(z["F0"], F01) and np.array_equal(z["FO"], FO1), (trip, force, r)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_levmarq_mpi_columns_unphased_bitwise(tmp_path, monkeypatch, world):
+    """Columns mode with the Jacobian's slice exchange in one step after the FD launch
+    (PNOL_LM_PHASED=0: no second stream, no per-tile events) gives the same X, F0 and FOpt as
+    one GPU -- the same blocks reach the same ranks, only the overlap differs."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import Context, DeviceObjective, run_levmarq
+    m, n = 1000, 700
+    _set_mode(monkeypatch, "columns")
+    monkeypatch.setenv("PNOL_LM_PHASED", "0")
+    _run_workers(tmp_path, world, m, n, "lmonly")
+    monkeypatch.delenv("PNOL_LM_PHASED")
+    ctx = Context(0)
+    obj = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
+    X1, F01, FO1, _ = run_levmarq(obj, np.zeros(n), (0.001, 10.0, 1e-7, 5, 0.0, -1), which=0)
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        assert np.array_equal(z["X"], X1), r
+        assert np.array_equal(z["F0"], F01) and np.array_equal(z["FO"], FO1), r
+
+
 @pytest.mark.parametrize("status", ["1", "-7"])
 @pytest.mark.parametrize("mode", ["columns", "rows"])
 @pytest.mark.parametrize("world", [2, 3])

@@ -591,8 +591,8 @@ def test_lm_fused_trip_loop_equals_general_loop(ctx, oracle, m, n, force, monkey
     assert rel(out["fused"][0], xs) <= 1e-8
 
 
-@pytest.mark.parametrize("m,n", [(3000, 257), (2000, 700)])
-def test_lm_timed_out_trip_relaunches_cholesky(ctx, oracle, m, n, monkeypatch, capfd):
+@pytest.mark.parametrize("m,n,trip", [(3000, 257, "0"), (2000, 700, "0"), (2000, 700, "1")])
+def test_lm_timed_out_trip_relaunches_cholesky(ctx, oracle, m, n, trip, monkeypatch, capfd):
     """A trip whose Cholesky reports a dependency wait past its spin cap (forced on every trip's
     reducing solve by PNOL_CHOL_FORCE_FALLBACK=-7) is a scheduling event, not a property of A: the
     loop redoes the trip's solve with the same Cholesky (never the LU; the relaunch is not forced)
@@ -602,6 +602,7 @@ def test_lm_timed_out_trip_relaunches_cholesky(ctx, oracle, m, n, monkeypatch, c
     from parallelnonlinearoptimizationlibrary_amd.device import run_levmarq
     A, xs, y = oracle.linres_data(m, n)
     params = (0.001, 10, 1e-7, 6, 0.0, -1)
+    monkeypatch.setenv("PNOL_LM_TRIP", trip)   # the two calls (one-GPU default) or the fused trip
     monkeypatch.setenv("PNOL_CHOL_FORCE_FALLBACK", "-7")
     Xt, F0t, FOt, rt = run_levmarq(_obj(ctx, L.OBJ_LINRES, n, m, A, y), np.zeros(n), params)
     err = capfd.readouterr().err
