@@ -419,8 +419,8 @@ __device__ __forceinline__ void mp_def(double (&a)[kMW], double lp2, const ColBu
 // the scheduler issues the chain ops back to back (~280 cycles per pivot).
 template <int J, int P, bool STAMP>
 __device__ __forceinline__ void mp_step(double (&a)[kMW], double r, double lp1, const ColBuf16<J - 1>& cp1, double lp2,
-                                        const ColBuf16<J - 2>& cp2, double* __restrict__ Lp, double* __restrict__ disc,
-                                        double* __restrict__ rinv, int* cnt, int lane, bool& bad, long long* st) {
+                                        const ColBuf16<J - 2>& cp2, double* __restrict__ Lp, double* __restrict__ sb,
+                                        int ss, double* __restrict__ rinv, int* cnt, int lane, bool& bad, long long* st) {
     constexpr int c = kMW * P + J, LD = mp_ld(P);
     if constexpr (STAMP && (J & 7) == 0) st[2 * P + (J >> 3)] = __builtin_amdgcn_s_memtime();
     const double l = a[J] * r;
@@ -463,9 +463,9 @@ __device__ __forceinline__ void mp_step(double (&a)[kMW], double r, double lp1, 
         rn = fma(re, pp, r0);   // = rsqrt_nr(piv), the same operations
         PNOL_SB;
     }
-    // lanes above the micro-panel store into the discard row (a select, not a branch)
-    double* dst = (P == 0 || lane >= kMW * P) ? Lp + J * LD + (lane - kMW * P) : disc + lane;
-    *dst = l;
+    // this lane's value of column c: the panel's rows to the column copy, the V_P lanes to row J of
+    // W block (P, P), the rest to the discard block (per-lane base and stride: no select here)
+    sb[J * ss] = l;
     rinv[c] = r;   // every lane stores the same value: no divergent branch in the chain
     if constexpr ((J & 1) == 1) lds_signal(cnt, c + 1);
     ColBuf16<J> cv;
@@ -477,7 +477,7 @@ __device__ __forceinline__ void mp_step(double (&a)[kMW], double r, double lp1, 
     asm volatile("" ::: "memory");   // keep the next steps' LDS reads from being hoisted here
     PNOL_SB;
     if constexpr (J + 1 < kMW)
-        mp_step<J + 1, P, STAMP>(a, rn, l, cv, lp1, cp1, Lp, disc, rinv, cnt, lane, bad, st);
+        mp_step<J + 1, P, STAMP>(a, rn, l, cv, lp1, cp1, Lp, sb, ss, rinv, cnt, lane, bad, st);
 }
 
 template <int P, bool STAMP>
@@ -500,15 +500,27 @@ __device__ __forceinline__ void mp_panel(const MpLds& M, double* __restrict__ ri
 #pragma unroll
         for (int r = 0; r < 4; ++r) *mp_s(M, 48 + (lane >> 4) + 4 * r, 48 + (lane & 15)) = acc[r];
     }
+    // Lanes 0..15 of micro-panels 1..3 (rows already factored) compute V_P = L_PP^{-1} in the same
+    // instruction stream: lane j starts from the unit column e_j, and each pivot's l = a[J] r and
+    // rank-1 update a[k] -= l L_kJ are then exactly the forward substitution L_PP y = e_j
+    // (y_J = b_J r_J, b_k -= L_kJ y_J), with the column values L_kJ the panel's lanes use, so
+    // row J of V_P is these lanes' l of step J.  (Wave 1 forms V_0; it used to form every V_p one
+    // column pair behind the chain, which left V_3 ~1.9k cycles after the last pivot.)
     double a[kMW];
     const int row = max(lane, kMW * P);
+    const bool vlane = P > 0 && lane < kMW;
 #pragma unroll
-    for (int k = 0; k < kMW; ++k) a[k] = lane >= kMW * P ? *mp_s(M, row, kMW * P + k) : 0.0;
+    for (int k = 0; k < kMW; ++k)
+        a[k] = lane >= kMW * P ? *mp_s(M, row, kMW * P + k) : (vlane && k == lane ? 1.0 : 0.0);
     const double piv = readlane_d(a[0], kMW * P);
     bool bad = !(piv > 0.0);
     const ColBuf16<-1> n1{};
     const ColBuf16<-2> n2{};
-    mp_step<0, P, STAMP>(a, rsqrt_nr(piv), 0.0, n1, 0.0, n2, M.Lc + mp_base(P), M.disc, rinv, cnt, lane, bad, st);
+    double* const Lp = M.Lc + mp_base(P);
+    double* const sb = (P == 0 || lane >= kMW * P) ? Lp + (lane - kMW * P)
+                                                   : (vlane ? M.Wb + lblk(P, P) * kBlk + lane : M.disc + lane);
+    const int ss = (P == 0 || lane >= kMW * P) ? mp_ld(P) : (vlane ? kBP : 0);
+    mp_step<0, P, STAMP>(a, rsqrt_nr(piv), 0.0, n1, 0.0, n2, Lp, sb, ss, rinv, cnt, lane, bad, st);
     if (bad && lane == 0) atomicCAS(info, 0, d * NB + kMW * P + 1);
 }
 
@@ -628,6 +640,18 @@ __device__ __forceinline__ void mp_vx(const MpLds& M, const double* __restrict__
     blk_put(M.Wb + lblk(I, J) * kBlk, acc, lane);
 }
 
+// W_d's block row IB (rows 16 IB .. 16 IB + 15, final) to Wd: lane = column, zeros right of the
+// diagonal block; one coalesced 512-byte row per store
+template <bool SC1, int IB>
+__device__ __forceinline__ void mp_w_rows(const MpLds& M, double* __restrict__ Wd, int lane) {
+    const int jb = lane >> 4, c = lane & 15;
+    double v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = jb <= IB ? M.Wb[lblk(IB, jb <= IB ? jb : 0) * kBlk + q * kBP + c] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) stg<SC1>(Wd + (16 * IB + q) * NB + lane, v[q]);
+}
+
 template <bool STAMP = false, bool SC1 = false, class EARLY = NoEarly>
 __device__ __forceinline__ void factor_diag16(const DiagLds& L, double* __restrict__ rinv, int* cnt,
                                               double* __restrict__ Wd, int d, int* info, long long* st = nullptr,
@@ -645,18 +669,24 @@ __device__ __forceinline__ void factor_diag16(const DiagLds& L, double* __restri
         mp_vx<3, 1>(M, M.Xs + kBlk, lane);
         if constexpr (STAMP) st[9] = __builtin_amdgcn_s_memtime();
     } else if (wave == 1) {
+        // V_0 here; V_1 .. V_3 come from the chain wave's idle lanes (mp_panel), final once the
+        // column counter passes their micro-panel.  W's block rows 0..2 go to Wd as soon as they
+        // are final (rows 48..63 follow the barrier), so the publish after the last pivot drains
+        // a quarter of W's stores.
         const d4 z = {0.0, 0.0, 0.0, 0.0};
         mp_inverse<0>(M, rinv, cnt, lane);
         d4 x10 = mp_lw<1, 0, 0>(z, M, lane), x20 = mp_lw<2, 0, 0>(z, M, lane), x30 = mp_lw<3, 0, 0>(z, M, lane);
-        mp_inverse<1>(M, rinv, cnt, lane);
+        wait_lds_ge(cnt, 2 * kMW);   // V_1
         if constexpr (STAMP) st[10] = __builtin_amdgcn_s_memtime();
         blk_put(M.Xs, x10, lane);
         mp_vx<1, 0>(M, M.Xs, lane);
         lds_signal(cnt + 1, 1);   // W rows 0 .. 31 (blocks (0,0), (1,0), (1,1)) are final
+        mp_w_rows<SC1, 0>(M, Wd, lane);
+        mp_w_rows<SC1, 1>(M, Wd, lane);
         d4 x21 = mp_lw<2, 1, 1>(z, M, lane), x31 = mp_lw<3, 1, 1>(z, M, lane);
         x20 = mp_lw<2, 1, 0>(x20, M, lane);
         x30 = mp_lw<3, 1, 0>(x30, M, lane);
-        mp_inverse<2>(M, rinv, cnt, lane);
+        wait_lds_ge(cnt, 3 * kMW);   // V_2
         if constexpr (STAMP) st[11] = __builtin_amdgcn_s_memtime();
         blk_put(M.Xs, x20, lane);
         blk_put(M.Xs + kBlk, x21, lane);
@@ -668,8 +698,9 @@ __device__ __forceinline__ void factor_diag16(const DiagLds& L, double* __restri
         blk_put(M.Xs, x30, lane);   // after mp_vx<2, *>'s reads of Xs (one wave's LDS ops are ordered)
         blk_put(M.Xs + kBlk, x31, lane);
         blk_put(M.Xs + 2 * kBlk, x32, lane);
-        mp_inverse<3>(M, rinv, cnt, lane);
         lds_signal(cnt + 4, 1);
+        mp_w_rows<SC1, 2>(M, Wd, lane);
+        wait_lds_ge(cnt, 4 * kMW);   // V_3
         if constexpr (STAMP) st[12] = __builtin_amdgcn_s_memtime();
         mp_vx<3, 2>(M, M.Xs + 2 * kBlk, lane);
     } else {
@@ -680,11 +711,11 @@ __device__ __forceinline__ void factor_diag16(const DiagLds& L, double* __restri
     }
     __syncthreads();
     if constexpr (STAMP) if (wave == 0) st[13] = __builtin_amdgcn_s_memtime();
-    // W_d to HBM: wave w writes rows 16 w .. 16 w + 15, lane = column (each store one coalesced
-    // 512-byte row; zeros above the diagonal blocks); with Wst, the same values also go to LDS in
-    // the substage layout (the next tile's L = A W^T operand: late_prepare reads rows 32..63,
-    // diag_prepare all of it).  Wst overlaps the column and W areas: every value is read before
-    // the barrier.
+    // W_d to HBM: rows 48..63 (wave 3; wave 1 stored rows 0..47 as they became final), lane =
+    // column (each store one coalesced 512-byte row; zeros above the diagonal blocks); with Wst,
+    // every wave's 16 rows also go to LDS in the substage layout (the next tile's L = A W^T
+    // operand: late_prepare reads rows 32..63, diag_prepare all of it).  Wst overlaps the column
+    // and W areas: every value is read before the barrier.
     {
         const int jb = lane >> 4, c = lane & 15;
         double v[16];
@@ -693,8 +724,9 @@ __device__ __forceinline__ void factor_diag16(const DiagLds& L, double* __restri
             const int ib = wave;
             v[q] = jb <= ib ? M.Wb[lblk(ib, jb <= ib ? jb : 0) * kBlk + q * kBP + c] : 0.0;
         }
+        if (wave == 3)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) stg<SC1>(Wd + (16 * wave + q) * NB + lane, v[q]);
+            for (int q = 0; q < 16; ++q) stg<SC1>(Wd + (16 * wave + q) * NB + lane, v[q]);
         if (Wst) {
             __syncthreads();
 #pragma unroll
