@@ -202,17 +202,16 @@ class LMAsync {
             for (int v : all)
                 if (v != ctx->lm_fd_mode) throw std::runtime_error("LevMarqMPI: ranks disagree on PNOL_LM_FD");
         }
-        // The trip without forming A (pnol_lm_trip_d / pnol_lm_normal_solve_mpi_d: the persistent
-        // Cholesky's first tasks reduce the J^T J tiles into its own matrix) or the two calls (A
-        // formed by the reduce launch, then the solve).  Default: the fused form only where the
-        // tiles arrive summed (LevMarqMPI on several ranks: the allgathered tiles, 33.5 MB); with
-        // one rank its reduce tasks stream the 285 MB of split-K partials in front of the chain's
-        // first steps, and the two calls measured faster in 5 of 5 alternating same-box pairs
-        // (324-328.5 vs 317-321 LM iters/s, profiles/r05_trip_ab.txt).  PNOL_LM_TRIP=1 / 0
-        // forces either (read once per solve).
+        // The trip without forming A (default; PNOL_LM_TRIP=0 keeps the two calls, read once per
+        // solve): one GPU, pnol_lm_trip_d -- the reduce launch writes A straight into the
+        // Cholesky's padded matrix; LevMarqMPI, pnol_lm_normal_solve_mpi_d -- the persistent
+        // Cholesky's first tasks sum the allgathered tiles (33.5 MB) into it.  (With one rank the
+        // reduce tasks would stream the 285 MB of split-K partials in front of the chain's first
+        // steps: 5 of 5 alternating same-box pairs slower than the two calls, 317-321 vs
+        // 324-328.5 LM iters/s, profiles/r05_trip_ab.txt; PNOL_LM_REDUCE=tasks keeps that form.)
         {
             const char* e = std::getenv("PNOL_LM_TRIP");
-            trip_fused_ = e ? std::atoi(e) != 0 : (sliced && comm_size() > 1);
+            trip_fused_ = !e || std::atoi(e) != 0;
         }
         // several ranks: every trip's solve status is agreed over the ranks before the host acts
         // on it (pnol_lm_agree_status_d), so all replicas take the same branch

@@ -1343,7 +1343,7 @@ struct RedArgs {
     const double* part = nullptr;   // nullptr: not the reducing form
     int sub = 0, n = 0;
     double lambda = 0.0;
-    const double* jp = nullptr;     // the 8 -J^T F slice partials (jp[s n + e])
+    const double* jp = nullptr;     // the -J^T F units jp[(s sub + u) n + e] (k_syrk_tile)
     double* rhs = nullptr;          // rhs = -J^T F, for the LU fallback
     // LevMarqMPI: the J^T J tiles already summed (the allgathered packed tiles: tile t at
     // packed + (t / tpr) slot + (t % tpr) 128^2) and rhs already formed (rhs_in)
@@ -1351,6 +1351,9 @@ struct RedArgs {
     long slot = 0;
     int tpr = 1;
     const double* rhs_in = nullptr;
+    // the matrix and b already in P / bv (a reduce launch wrote them; every version and b word
+    // starts at 0): no reduce tasks, the chain factors tile 0 itself
+    bool preloaded = false;
 };
 
 template <int SUB>
@@ -1388,7 +1391,11 @@ __device__ void red_task(int u, const RedArgs& red, double* __restrict__ P, long
         for (int e = t; e < red.n; e += 256) {
             double l[8];
 #pragma unroll
-            for (int s = 0; s < 8; ++s) l[s] = 0.0 + red.jp[(long)s * red.n + e];
+            for (int s = 0; s < 8; ++s) {   // leaf = 0.0 + the unit sub-chunks in order (k_syrk_reduce)
+                double a = 0.0;
+                for (int q = 0; q < red.sub; ++q) a += red.jp[(long)(s * red.sub + q) * red.n + e];
+                l[s] = a;
+            }
             const double v = ((l[0] + l[1]) + (l[2] + l[3])) + ((l[4] + l[5]) + (l[6] + l[7]));
             red.rhs[e] = v;
             stg<true>(bv + e, v);
@@ -1468,7 +1475,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
     if (blockIdx.x == 0) {   // ---------------- the diagonal chain
         const EarlyLds E{pfx, pll, pfc, ew};
         if (t < 4) ew[t] = 0;
-        const bool smode = red.part || red.packed;   // the reducing form: the chain also factors tile 0
+        const bool smode = red.part || red.packed || red.preloaded;   // the chain also factors tile 0
         for (int d = smode ? 0 : 1; d < T; ++d) {
             const int k = d - 1;
 #ifdef PNOL_CHOL_TIMELINE
@@ -1556,7 +1563,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             if (!ok_sh) return;
             stage_tile<true>(X, P, ldp, i0, k0);
             if (t == 0) {   // W_k (tile 0 comes from the prep launch)
-                ok_sh = (k == 0 && !red.part && !red.packed) || spin_ge(pw.wdone + k, 1, info);
+                ok_sh = (k == 0 && !red.part && !red.packed && !red.preloaded) || spin_ge(pw.wdone + k, 1, info);
 #ifdef PNOL_CHOL_TIMELINE
                 if (i == k + 2) PNOL_CRIT(k, 2)
 #endif
@@ -1906,10 +1913,10 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
 // P's padding (identity on the diagonal past n, as the copy of A gives), info = 0.
 __global__ __launch_bounds__(256) void k_chol_reducing_prep(double* __restrict__ P, long ldp, int T, int n,
                                                             double* __restrict__ bv, int* __restrict__ pflags,
-                                                            int npflags, int* __restrict__ info) {
+                                                            int npflags, int* __restrict__ info, int vinit) {
     const int N = T * NB, tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
     const int b0 = 2 * T, v1 = 3 * T + T * T;   // [bcnt | ver]
-    for (int q = tid; q < npflags; q += nth) pflags[q] = (q >= b0 && q < v1) ? -1 : 0;
+    for (int q = tid; q < npflags; q += nth) pflags[q] = (q >= b0 && q < v1) ? vinit : 0;
     for (int r = n + tid; r < N; r += nth) bv[r] = 0.0;
     if (n < N) {
         const long pad = (long)(N - n) * N + (long)n * (N - n);   // rows >= n, then columns >= n of rows < n
@@ -1936,13 +1943,25 @@ int launch_chol_reducing_prep(pnol_ctx* ctx, int n, int* dinfo, CholRed& cr) {
     return chol_ws(ctx, n, true, cr.w);
 }
 
-int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr) {
+int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr, bool preloaded) {
     const CholWs& w = cr.w;
     const int n = cr.n;
     const long pad = (long)(w.N - n) * w.N + (long)n * (w.N - n), work = std::max<long>(pad, w.npf);
     hipLaunchKernelGGL(k_chol_reducing_prep, dim3((unsigned)std::max<long>(1, std::min<long>(1024, (work + 255) / 256))),
-                       dim3(256), 0, ctx->stream, w.P, w.ldp, w.T, n, w.bv, w.pf, w.npf, cr.dinfo);
+                       dim3(256), 0, ctx->stream, w.P, w.ldp, w.T, n, w.bv, w.pf, w.npf, cr.dinfo, preloaded ? 0 : -1);
     return launch_check();
+}
+
+// the persistent factorisation of the matrix a reduce launch left in P (and b in bv), then the
+// backward solve and xnext = xbase + sigma (launch_chol_reducing_start(preloaded) first)
+int launch_chol_preloaded_run(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, double* sigma, const double* xbase,
+                              double* xnext) {
+    if (!sigma) return PNOL_ERR_ARG;
+    RedArgs red;
+    red.n = cr.n;
+    red.preloaded = true;
+    PNOL_CHECK(chol_persist_launch(ctx, st, cr.w, cr.dinfo, red));
+    return chol_bwd_launch(ctx, st, cr.w, cr.n, sigma, cr.dinfo, xbase, xnext, true);
 }
 
 int launch_chol_reducing_run(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, const double* part, int sub,

@@ -198,10 +198,6 @@ int launch_status_agree(pnol_ctx* ctx, int* dinfo);
 // ---- kernel launchers (defined in kernels/*.hip) ------------------------------------
 int launch_gemv_neg(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y);
 int launch_gemv_neg_seq(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y);
-// y[(s - s0) * rows + j] = -sum_{k in m-slice s} A_s[j][k] x[s mS + k], s in [s0, s0 + nsl)
-// stream: nullptr = the context stream
-int launch_gemv_neg_slices(pnol_ctx* ctx, const double* A, int lda, long sstride, int rows, int m, int mS, int s0,
-                           int nsl, const double* x, double* y, hipStream_t stream = nullptr);
 int launch_bfgs_update_exact(pnol_ctx* ctx, double* D, int ldd, const double* y, const double* s, int n);
 int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p, const double* a_p,
                      const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,
@@ -248,7 +244,11 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
 // partials jp into its padded matrix and b (rhs gets -J^T F too), then the factorisation, the
 // backward solve and xnext = xbase + sigma; bitwise the reduce into A + launch_chol_solve
 int launch_chol_reducing_prep(pnol_ctx* ctx, int n, int* dinfo, CholRed& cr);
-int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr);
+// preloaded: the matrix and b will be in P / bv before the persistent launch (every version and
+// b word starts at 0; launch_chol_preloaded_run), else the reduce tasks store them (words at -1)
+int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr, bool preloaded = false);
+int launch_chol_preloaded_run(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, double* sigma, const double* xbase,
+                              double* xnext);
 int launch_chol_reducing_run(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, const double* part, int sub,
                              const double* jp, double lambda, double* rhs, double* sigma, const double* xbase,
                              double* xnext);

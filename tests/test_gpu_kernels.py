@@ -705,15 +705,18 @@ def test_fd_normal_bitwise(ctx, m, n):
         assert np.array_equal(_np(rb), _np(ra)), rep
 
 
+@pytest.mark.parametrize("reduce", ["launch", "tasks"])
 @pytest.mark.parametrize("m,n", [(16384, 2048), (5000, 1000), (777, 129), (3000, 257), (2000, 700), (512, 96)])
-def test_lm_trip_bitwise(ctx, m, n):
-    """The LM trip without A (pnol_lm_trip_d: the persistent Cholesky's first tasks sum the J^T J
-    split-K partials and the -J^T F slice partials into its own matrix and b) gives JT, F0, rhs,
-    sigma, x + sigma and the solve status bitwise those of pnol_fd_normal_d + pnol_solve_step_d,
-    over repeated trips at new points and lambdas; the A the LU fallback forms from the trip's
-    partials (pnol_lm_trip_normal_d) is bitwise pnol_fd_normal_d's A."""
+def test_lm_trip_bitwise(ctx, monkeypatch, m, n, reduce):
+    """The LM trip without A (pnol_lm_trip_d: the reduce launch writes the J^T J split-K partials'
+    sums straight into the persistent Cholesky's padded matrix and -J^T F into b -- or, reduce =
+    tasks, the persistent launch's first tasks do that reduce) gives JT, F0, rhs, sigma, x + sigma
+    and the solve status bitwise those of pnol_fd_normal_d + pnol_solve_step_d, over repeated trips
+    at new points and lambdas; the A the LU fallback forms from the trip's partials
+    (pnol_lm_trip_normal_d) is bitwise pnol_fd_normal_d's A."""
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
+    monkeypatch.setenv("PNOL_LM_REDUCE", reduce)
     d = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
     h = ctx.tensor(np.full(n, 1e-7))
     JTa, Aa, ra, JTb = ctx.empty(n, m), ctx.empty(n, n), ctx.empty(n), ctx.empty(n, m)
@@ -752,6 +755,26 @@ def test_lm_trip_reports_non_spd(ctx):
     *_, sb, _, ib = d2.lm_trip(x, h, 0.5, ctx.empty(n, 1000))
     assert ia == 0 and ib == 0
     assert np.array_equal(_np(sb), _np(sa))
+
+
+@pytest.mark.parametrize("n", [300, 4096, 8192])
+def test_bfgs_pass_prefetch_depth_bitwise(ctx, monkeypatch, n):
+    """The fused BFGS pass with two row groups of D in flight (PNOL_PASS_PF=2) instead of one:
+    the same arithmetic in the same row order, so u, w, v and the written-back D are bitwise the
+    one-group-ahead pass's (BFGS_with_linesearch.cpp:389-432 as the rank-2 fold)."""
+    rng = np.random.default_rng(n)
+    D0 = rng.standard_normal((n, n))
+    y, g = ctx.tensor(rng.standard_normal(n)), ctx.tensor(rng.standard_normal(n))
+    pend = tuple(ctx.tensor(1e-3 * rng.standard_normal(n)) for _ in range(3))
+    out = {}
+    for pf in ("1", "2"):
+        monkeypatch.setenv("PNOL_PASS_PF", pf)
+        D = ctx.tensor(D0)
+        u, w, v = ctx.bfgs_pass(D, y, g, pend, True)
+        ctx.synchronize()
+        out[pf] = [_np(t) for t in (u, w, v, D)]
+    for a, b in zip(out["1"], out["2"]):
+        assert np.array_equal(a, b)
 
 
 def test_lm_agree_status_codes_one_rank(ctx):

@@ -567,9 +567,12 @@ def test_lm_one_wait_loop_lu_fallback_equals_general_loop(ctx, oracle, m, n, mon
     assert rel(Xa, Xo) <= 1e-10
 
 
-@pytest.mark.parametrize("m,n,force", [(3000, 257, "0"), (2000, 700, "0"), (3000, 257, "1")])
-def test_lm_fused_trip_loop_equals_general_loop(ctx, oracle, m, n, force, monkeypatch):
-    """The one-wait LM loop with the fused trip (pnol_lm_trip_d, the default) replays the
+@pytest.mark.parametrize("m,n,force,reduce", [(3000, 257, "0", "launch"), (2000, 700, "0", "launch"),
+                                              (3000, 257, "1", "launch"), (2000, 700, "0", "tasks"),
+                                              (3000, 257, "1", "tasks")])
+def test_lm_fused_trip_loop_equals_general_loop(ctx, oracle, m, n, force, reduce, monkeypatch):
+    """The one-wait LM loop with the fused trip (pnol_lm_trip_d, the default; its reduce as a
+    launch into the Cholesky's matrix, or as the persistent launch's first tasks) replays the
     one-wait loop with the two calls (PNOL_LM_TRIP=0) and the general loop (PNOL_LM_ASYNC=0)
     bitwise -- X, F0, FOpt, evaluation count -- also with the LU fallback forced on every trip
     (force = 1: A formed from the trip's partials, pnol_lm_trip_normal_d)."""
@@ -578,6 +581,7 @@ def test_lm_fused_trip_loop_equals_general_loop(ctx, oracle, m, n, force, monkey
     A, xs, y = oracle.linres_data(m, n)
     params = (0.001, 10, 1e-7, 8, 0.0, -1)
     monkeypatch.setenv("PNOL_CHOL_FORCE_FALLBACK", force)
+    monkeypatch.setenv("PNOL_LM_REDUCE", reduce)
     out = {}
     for name, mode, trip in (("fused", "1", "1"), ("two_call", "1", "0"), ("general", "0", "0")):
         monkeypatch.setenv("PNOL_LM_ASYNC", mode)
@@ -591,7 +595,7 @@ def test_lm_fused_trip_loop_equals_general_loop(ctx, oracle, m, n, force, monkey
     assert rel(out["fused"][0], xs) <= 1e-8
 
 
-@pytest.mark.parametrize("m,n,trip", [(3000, 257, "0"), (2000, 700, "0"), (2000, 700, "1")])
+@pytest.mark.parametrize("m,n,trip", [(3000, 257, "1"), (2000, 700, "1"), (2000, 700, "0")])
 def test_lm_timed_out_trip_relaunches_cholesky(ctx, oracle, m, n, trip, monkeypatch, capfd):
     """A trip whose Cholesky reports a dependency wait past its spin cap (forced on every trip's
     reducing solve by PNOL_CHOL_FORCE_FALLBACK=-7) is a scheduling event, not a property of A: the
@@ -602,7 +606,7 @@ def test_lm_timed_out_trip_relaunches_cholesky(ctx, oracle, m, n, trip, monkeypa
     from parallelnonlinearoptimizationlibrary_amd.device import run_levmarq
     A, xs, y = oracle.linres_data(m, n)
     params = (0.001, 10, 1e-7, 6, 0.0, -1)
-    monkeypatch.setenv("PNOL_LM_TRIP", trip)   # the two calls (one-GPU default) or the fused trip
+    monkeypatch.setenv("PNOL_LM_TRIP", trip)   # the fused trip (the default) or the two calls
     monkeypatch.setenv("PNOL_CHOL_FORCE_FALLBACK", "-7")
     Xt, F0t, FOt, rt = run_levmarq(_obj(ctx, L.OBJ_LINRES, n, m, A, y), np.zeros(n), params)
     err = capfd.readouterr().err
