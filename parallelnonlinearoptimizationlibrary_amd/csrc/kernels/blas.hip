@@ -228,6 +228,18 @@ __global__ __launch_bounds__(256) void k_gemv_neg_wg(const double* __restrict__ 
     gemv_neg_wg_body<R, NT>(A, lda, rows, cols, x, y);
 }
 
+// -J^T F per m-slice (LevMarq / LevMarqMPI, syrk.hip): blockIdx.y = slice s0 + y of J^T (at
+// A + s * sstride, row stride lda) against F[s mS, (s + 1) mS) -> y[blockIdx.y * rows + j].
+template <int R, bool VEC>
+__global__ __launch_bounds__(256) void k_gemv_neg_slices(const double* __restrict__ A, long lda, long sstride, int rows,
+                                                         int m, int mS, int s0, const double* __restrict__ x,
+                                                         double* __restrict__ y) {
+    const int s = s0 + blockIdx.y;
+    const int cols = max(0, min(mS, m - s * mS));
+    gemv_neg_wg_body<R, true, VEC>(A + (long)s * sstride, lda, rows, cols, x + (long)s * mS,
+                                   y + (long)blockIdx.y * rows);
+}
+
 // any lda / alignment: one wave per row, 8-byte loads, 4 in flight per lane
 __global__ __launch_bounds__(256) void k_gemv_neg_scalar(const double* __restrict__ A, long lda, int rows, int cols,
                                                          const double* __restrict__ x, double* __restrict__ y) {
@@ -311,7 +323,6 @@ __global__ void k_bfgs_exact_2(const double* __restrict__ T, double* __restrict_
 // ------------------------------------------------------------------------------------
 constexpr int kPassCols = 512;
 constexpr int kGroup = 8;
-constexpr int kPassPF = 1;   // default row groups in flight ahead (PNOL_PASS_PF)
 
 // reduce-scatter 16 values across the wave; the lanes with (lane & 3) == 0 end up with the
 // full 64-lane sum of value index ((lane>>5)&1)*8 + ((lane>>4)&1)*4 + ((lane>>3)&1)*2 + ((lane>>2)&1)
@@ -393,10 +404,7 @@ __device__ __forceinline__ void pass_ident(double2 (&d)[kGroup], const double* _
 // Row shard form (BFGS D row-sharded over the ranks): D holds rows [rb, re) of the n x n
 // matrix (rb a multiple of the row-tile height); row tiles, partial indices and outputs use global rows,
 // so every partial is the one the whole-matrix pass (rb = 0, re = n) would produce.
-// PF: row groups in flight ahead of the one being reduced (1: the next group; 2: the next two --
-// 24 16-byte loads per lane outstanding instead of 16).  The arithmetic and the row order are the
-// same, so every output is bitwise the PF = 1 pass's.
-template <bool PEND, bool WB, bool VEC, bool IDS = false, int PF = 1>
+template <bool PEND, bool WB, bool VEC, bool IDS = false>
 __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ Dsh, long ldd, int n, int rb, int re, int prows,
                                                    const double* __restrict__ sp, const double* __restrict__ ap,
                                                    const double* __restrict__ bp, const double* __restrict__ y,
@@ -429,21 +437,16 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ Dsh, lon
     const int r_end = min(re, r_begin + prows);
     const int ngroups = (r_end - r_begin + kGroup - 1) / kGroup;
     int grp = rt % ngroups;
-    auto fetch = [&](double2 (&dst)[kGroup], int gi) {
-        if (IDS) pass_ident(dst, id_scale, r_begin + gi * kGroup, col, r_end - 1);
-        else pass_load<VEC>(dst, D, ldd, n, r_begin + gi * kGroup, colc, r_end - 1);
-    };
-    double2 cur[kGroup], nxt[kGroup];
-    fetch(cur, grp);
-    if (PF == 2 && ngroups > 1) fetch(nxt, grp + 1 == ngroups ? 0 : grp + 1);
+    double2 cur[kGroup];
+    if (IDS) pass_ident(cur, id_scale, r_begin + grp * kGroup, col, r_end - 1);
+    else pass_load<VEC>(cur, D, ldd, n, r_begin + grp * kGroup, colc, r_end - 1);
     for (int t = 0; t < ngroups; ++t) {
         const int r0 = r_begin + grp * kGroup;
         const int gnext = (grp + 1 == ngroups) ? 0 : grp + 1;
-        double2 nn[kGroup];
-        if (PF == 1) {
-            if (t + 1 < ngroups) fetch(nxt, gnext);
-        } else if (t + 2 < ngroups) {
-            fetch(nn, gnext + 1 == ngroups ? 0 : gnext + 1);
+        double2 nxt[kGroup];
+        if (t + 1 < ngroups) {
+            if (IDS) pass_ident(nxt, id_scale, r_begin + gnext * kGroup, col, r_end - 1);
+            else pass_load<VEC>(nxt, D, ldd, n, r_begin + gnext * kGroup, colc, r_end - 1);
         }
         double yr[kGroup], sr[kGroup], br[kGroup];
 #pragma unroll
@@ -489,10 +492,7 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ Dsh, lon
             }
         }
 #pragma unroll
-        for (int q = 0; q < kGroup; ++q) {
-            cur[q] = nxt[q];
-            if (PF == 2) nxt[q] = nn[q];
-        }
+        for (int q = 0; q < kGroup; ++q) cur[q] = nxt[q];
         grp = gnext;
     }
     if (c0ok) part_w[(long)rt * n + col] = w0;
@@ -615,6 +615,30 @@ int launch_gemv_neg(pnol_ctx* ctx, const double* A, int lda, int rows, int cols,
     return launch_check();
 }
 
+int launch_gemv_neg_slices(pnol_ctx* ctx, const double* A, int lda, long sstride, int rows, int m, int mS, int s0,
+                           int nsl, const double* x, double* y, hipStream_t stream) {
+    if (!stream) stream = ctx->stream;
+    if (!A || !x || !y || rows <= 0 || nsl <= 0 || (mS & 1) || !aligned16(x)) return PNOL_ERR_ARG;
+    // rows per workgroup (PNOL_JTR_ROWS = 1, 2 or 4; tuning -- each row's sum is the same for all)
+    static const int R = [] {
+        const char* e = std::getenv("PNOL_JTR_ROWS");
+        const int v = e ? std::atoi(e) : 2;
+        return (v == 1 || v == 4) ? v : 2;
+    }();
+    // 16-byte row loads when every row start is 16-byte aligned; the same sums otherwise
+    const bool vec = !((lda & 1) || (sstride & 1) || !aligned16(A));
+    const dim3 grid((rows + R - 1) / R, nsl);
+#define PNOL_SLICES(RR, V) \
+    hipLaunchKernelGGL((k_gemv_neg_slices<RR, V>), grid, dim3(256), 0, stream, A, (long)lda, sstride, rows, m, mS, s0, x, y)
+    if (vec) {
+        if (R == 1) PNOL_SLICES(1, true); else if (R == 4) PNOL_SLICES(4, true); else PNOL_SLICES(2, true);
+    } else {
+        if (R == 1) PNOL_SLICES(1, false); else if (R == 4) PNOL_SLICES(4, false); else PNOL_SLICES(2, false);
+    }
+#undef PNOL_SLICES
+    return launch_check();
+}
+
 int launch_gemv_neg_seq(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y) {
     if (!A || !x || !y || rows <= 0 || cols <= 0 || lda < cols) return PNOL_ERR_ARG;
     int blocks = (rows + 63) / 64;
@@ -677,18 +701,9 @@ int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p
     if (myrowt > 0) {
         dim3 grd(myrowt * ncolt), blk(256);
         const bool vec = (ldd % 2 == 0) && aligned16(D);
-        // PNOL_PASS_PF = 1 / 2 (tuning, read per call): row groups of D in flight ahead (bitwise equal)
-        const char* epf = std::getenv("PNOL_PASS_PF");
-        const int pf = epf ? std::atoi(epf) : kPassPF;
 #define PNOL_PASS(PE, W, V)                                                                                        \
-    do {                                                                                                       \
-        if (pf == 2)                                                                                           \
-            hipLaunchKernelGGL((k_bfgs_pass<PE, W, V, false, 2>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb, re, \
-                               prows, s_p, a_p, b_p, y, g, P0, P1, P2);                                        \
-        else                                                                                                   \
-            hipLaunchKernelGGL((k_bfgs_pass<PE, W, V, false, 1>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb, re, \
-                               prows, s_p, a_p, b_p, y, g, P0, P1, P2);                                        \
-    } while (0)
+    hipLaunchKernelGGL((k_bfgs_pass<PE, W, V>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb, re, prows, s_p, a_p, b_p, y, \
+                       g, P0, P1, P2)
         if (ident_src) {
             if (vec)
                 hipLaunchKernelGGL((k_bfgs_pass<true, true, true, true>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb,

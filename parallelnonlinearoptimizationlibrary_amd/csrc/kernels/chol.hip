@@ -1343,7 +1343,7 @@ struct RedArgs {
     const double* part = nullptr;   // nullptr: not the reducing form
     int sub = 0, n = 0;
     double lambda = 0.0;
-    const double* jp = nullptr;     // the -J^T F units jp[(s sub + u) n + e] (k_syrk_tile)
+    const double* jp = nullptr;     // the 8 -J^T F slice partials (jp[s n + e])
     double* rhs = nullptr;          // rhs = -J^T F, for the LU fallback
     // LevMarqMPI: the J^T J tiles already summed (the allgathered packed tiles: tile t at
     // packed + (t / tpr) slot + (t % tpr) 128^2) and rhs already formed (rhs_in)
@@ -1354,6 +1354,9 @@ struct RedArgs {
     // the matrix and b already in P / bv (a reduce launch wrote them; every version and b word
     // starts at 0): no reduce tasks, the chain factors tile 0 itself
     bool preloaded = false;
+    // the diagonal chain's wave 0 at issue priority 3 (s_setprio; PNOL_CHOL_PRIO, tuning): the
+    // CU's shared arbiters favour the pivot chain over the look-ahead's polling and staging
+    int prio = 0;
 };
 
 template <int SUB>
@@ -1391,11 +1394,7 @@ __device__ void red_task(int u, const RedArgs& red, double* __restrict__ P, long
         for (int e = t; e < red.n; e += 256) {
             double l[8];
 #pragma unroll
-            for (int s = 0; s < 8; ++s) {   // leaf = 0.0 + the unit sub-chunks in order (k_syrk_reduce)
-                double a = 0.0;
-                for (int q = 0; q < red.sub; ++q) a += red.jp[(long)(s * red.sub + q) * red.n + e];
-                l[s] = a;
-            }
+            for (int s = 0; s < 8; ++s) l[s] = 0.0 + red.jp[(long)s * red.n + e];
             const double v = ((l[0] + l[1]) + (l[2] + l[3])) + ((l[4] + l[5]) + (l[6] + l[7]));
             red.rhs[e] = v;
             stg<true>(bv + e, v);
@@ -1473,6 +1472,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
     double* Y = smem + kStage;
 
     if (blockIdx.x == 0) {   // ---------------- the diagonal chain
+        if (red.prio && wave == 0) __builtin_amdgcn_s_setprio(3);
         const EarlyLds E{pfx, pll, pfc, ew};
         if (t < 4) ew[t] = 0;
         const bool smode = red.part || red.packed || red.preloaded;   // the chain also factors tile 0
@@ -1852,12 +1852,14 @@ static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, i
     // update task (~6 us each after W_{d-1}), so waiting for them inside the factor costs more
     // than the prepare it saves.
     const int lookahead = el ? std::max(0, std::atoi(el)) : 64;
+    RedArgs rp = red;
+    if (const char* ep = std::getenv("PNOL_CHOL_PRIO")) rp.prio = std::atoi(ep) != 0;
     const int slots = std::max(ctx->num_cu, 1) - 1;
     const int want = ew ? std::atoi(ew) : slots;
     const int nred = (red.part || red.packed) ? 1 + T * (T + 1) / 2 : 0;
     const int workers = std::max(1, std::min(ntasks + nred, want));
     hipLaunchKernelGGL(k_chol_persist, dim3(1 + workers), dim3(256), 0, st, w.P, w.Lm, w.ldp, T, w.W, w.bv, w.zv, w.pf,
-                       ntasks, dinfo, lookahead, red);
+                       ntasks, dinfo, lookahead, rp);
     return launch_check();
 }
 

@@ -129,24 +129,13 @@ __device__ __forceinline__ void part_store(double v, double* p) {
     else *p = v;
 }
 
-// -J^T F rides in the diagonal tiles (Fv / jp non-null; the 128-row balanced path and the 64-row
-// tiles): the operand rows of a diagonal tile are the FD columns [128 ti, +128) (or 64 ti) and its
-// K range is one (m-slice, sub-chunk) unit, so one lane per row runs the sequential chain
-// c = fma(JT_rk, F_k, c) from 0.0 over the unit's k ascending -- the k of the staged LDS rows, F
-// staged beside them -- and stores -c at jp[(slice * sub + u) * njp + r].  The units are then summed
-// exactly as the J^T J partials: leaf = 0.0 + the sub-chunks in order, then the slice tree
-// (k_syrk_reduce's extra row, the reducing Cholesky's task 0, k_tree_nodes).  k_jtr_units forms
-// the same unit values from J^T alone (pnol_jtr_d), so every -J^T F is the same sum.
 template <int MODE, int TILE, int NW = 4, bool NTS = true>
 __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
                                                       int split_k, int kfirst, int kchunk, int sub, int slice0,
-                                                      int mS, long sstride, double* __restrict__ part, int tile0,
-                                                      const double* __restrict__ Fv, double* __restrict__ jp,
-                                                      int njp) {
+                                                      int mS, long sstride, double* __restrict__ part, int tile0) {
     constexpr int NT = 64 * NW, WC = NW / 2;
     constexpr int WTM = TILE / 2, WTN = TILE / WC, NBM = WTM / 16, NBN = WTN / 16;
     __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
-    __shared__ __attribute__((aligned(16))) double fst[2][kTK];              // F of the stage (rhs chains)
 #ifdef PNOL_SYRK_TIMELINE
     const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -201,43 +190,15 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
         }
     }
     const int drow0 = dbi[0], drow1 = dsplit >= 4 ? dbi[4] : dsplit == 3 ? dbi[3] : dsplit == 2 ? dbi[2] : dbi[1];
-    // the -J^T F chain: which operand row this thread runs (-1: none).  128-row tiles: waves 4, 5
-    // (the lighter waves of the balanced diagonal layout); 64-row tiles: wave 0.
-    const bool rhs_on = jp != nullptr && diag && (kBal || TILE == 64);
-    const int rrow = !rhs_on ? -1 : (kBal ? ((int)threadIdx.x >= 256 && (int)threadIdx.x < 256 + TILE ? (int)threadIdx.x - 256 : -1)
-                                          : ((int)threadIdx.x < TILE ? (int)threadIdx.x : -1));
-    double racc = 0.0;
-    // F of the stage starting at k0 (zero past kend): 8 lanes, one pair each
-    auto load_f = [&](double2& fv, int k0) {
-        const int k = k0 + 2 * (int)threadIdx.x;
-        fv.x = k < kend ? Fv[k] : 0.0;
-        fv.y = k + 1 < kend ? Fv[k + 1] : 0.0;
-    };
-    auto rhs_chain = [&](const double* __restrict__ Pst, const double* __restrict__ fs) {
-        const double* pr = Pst + rrow * kPad;
-#pragma unroll
-        for (int q = 0; q < kTK / 2; ++q) {
-            const double2 pv = *reinterpret_cast<const double2*>(pr + 2 * q);
-            const double2 fv = *reinterpret_cast<const double2*>(fs + 2 * q);
-            racc = fma(pv.x, fv.x, racc);
-            racc = fma(pv.y, fv.y, racc);
-        }
-    };
 
     // the stage loop, instantiated once per path (diagonal-balanced or 2 x 4 waves) so each copy
     // holds only its own fragments live
     auto stage_loop = [&](auto BAL) {
-        // the rhs chain's code exists only in the balanced diagonal instantiation and in the
-        // 64-row kernel (the 128-row general loop stays at its register budget)
-        constexpr bool RHS = decltype(BAL)::value || TILE == 64;
         StageRegs<TILE, NT> ps, qs;
-        double2 fv = make_double2(0.0, 0.0);
-        const bool fload = RHS && rhs_on && threadIdx.x < kTK / 2;
         if (nstages > 0) {
             bool full = ldx_even && (kbeg + kTK <= kend);
             load_stage<TILE, NT>(ps, X, ldx, nr, prow0, kbeg, kend, full);
             if (!diag) load_stage<TILE, NT>(qs, X, ldx, nr, qrow0, kbeg, kend, full);
-            if (fload) load_f(fv, kbeg);
         }
         const int frow = lane & 15;
         const int fk = lane >> 4;
@@ -247,17 +208,13 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
             double* Q = diag ? lds[buf][0] : lds[buf][1];
             store_stage<TILE, NT>(ps, P);
             if (!diag) store_stage<TILE, NT>(qs, Q);
-            if (fload) *reinterpret_cast<double2*>(&fst[buf][2 * threadIdx.x]) = fv;
             __syncthreads();
             if (st + 1 < nstages) {
                 const int k0 = kbeg + (st + 1) * kTK;
                 bool full = ldx_even && (k0 + kTK <= kend);
                 load_stage<TILE, NT>(ps, X, ldx, nr, prow0, k0, kend, full);
                 if (!diag) load_stage<TILE, NT>(qs, X, ldx, nr, qrow0, k0, kend, full);
-                if (fload) load_f(fv, k0);
             }
-            if constexpr (RHS)
-                if (rrow >= 0) rhs_chain(P, fst[buf]);
             // one 16-byte fragment read per operand block covers two MFMA K-groups: lane l holds
             // k = 8 kk + 2 (l >> 4) + {0, 1}; the first MFMA takes the even k of the 8-block, the
             // second the odd ones (half the ds_read instructions; the 144-byte row stride keeps the
@@ -311,8 +268,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
     if (kBal && bal) stage_loop(std::true_type{});
     else stage_loop(std::false_type{});
 
-    if (rrow >= 0 && prow0 + rrow < nr)
-        jp[(long)(slice * sub + u) * njp + prow0 + rrow] = -racc;
     // f64 MFMA C/D layout: lane l, register r -> row (l >> 4) + 4 r, column l & 15
     const int ocol = lane & 15;
     const int orow = lane >> 4;
@@ -502,8 +457,8 @@ __global__ void k_syrk_unpack(const double* __restrict__ packed, int ntiles, int
 // SUB > 0: the sub-chunk count at compile time (all kS * SUB loads of an element in flight at
 // once); SUB = 0: runtime `sub`.
 // jp / rhs (nullable): one more row of blocks (blockIdx.y == ntiles) forms rhs = the slice
-// tree of the -J^T F units jp[(s * sub + u) * n + e], exactly as k_tree_nodes over all slices
-// does (leaf = 0.0 + the sub-chunks in order, then tree8): the tree rides in this launch.
+// tree of the 8 -J^T F slice partials jp[s * n + e], exactly as k_tree_nodes over all slices does
+// (leaf = 0.0 + partial, then tree8): the tree rides in this launch instead of its own.
 template <int SUB, int SR = 32>
 __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ part, int ntiles, int sub_rt, int n,
                                                      double lambda, double* __restrict__ A, long lda,
@@ -511,22 +466,18 @@ __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ 
                                                      const double* __restrict__ jp = nullptr,
                                                      double* __restrict__ rhs = nullptr,
                                                      double* __restrict__ rhs2 = nullptr) {
-    const int sub = SUB > 0 ? SUB : sub_rt;                // SR: strip rows
     if (jp && (int)blockIdx.y == ntiles) {
         for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
             double l[kS];
 #pragma unroll
-            for (int s = 0; s < kS; ++s) {
-                double a = 0.0;
-                for (int u = 0; u < sub; ++u) a += jp[(long)(s * sub + u) * n + e];
-                l[s] = a;
-            }
+            for (int s = 0; s < kS; ++s) l[s] = 0.0 + jp[(long)s * n + e];
             const double v = tree8(l);
             rhs[e] = v;
             if (rhs2) rhs2[e] = v;   // (the Cholesky's b when the reduce writes its matrix)
         }
         return;
     }
+    const int sub = SUB > 0 ? SUB : sub_rt;                // SR: strip rows
     __shared__ double st[SR][kTile + 1];
     const int t = tile0 + blockIdx.y;                      // part holds this launch's tiles from tile0 on
     int ti, tj;
@@ -680,35 +631,41 @@ static bool syrk_t64(bool sliced) {
 // Partial tiles [tile0, tile0 + ntl) x slices [slice0, slice0 + nsl) x sub-chunks of
 // X (nr rows, K columns; slice s at X + s * sstride, row stride ldx) into
 // part[((t - tile0) * nsl * sub + (s - slice0) * sub + u) * 128^2].
-// F / jp (non-null, all tiles): the diagonal tiles also form the -J^T F units of these slices into
-// jp[(s * sub + u) * nr + r] (jtr_part's layout; see k_syrk_tile)
 static void syrk_partials(pnol_ctx* ctx, hipStream_t stream, bool rows_variant, const double* X, long ldx,
                           long sstride, int nr, int K, const SliceCfg& sc, int slice0, int nsl, int tile0, int ntl,
-                          double* part, bool t64 = false, const double* F = nullptr, double* jp = nullptr) {
+                          double* part, bool t64 = false) {
     const int split = nsl * sc.sub;
     const dim3 grid(ntl * split);
-    if (!F) jp = nullptr;
     LaunchTimer tm(ctx, rows_variant ? "syrk_rows" : "syrk");
     if (t64) {   // all tiles (tile0 = 0): ntl counts the 64 x 64 lower tiles
         const int nt64 = (nr + 63) / 64;
         hipExtLaunchKernelGGL((k_syrk_tile<4, 64>), dim3(nt64 * (nt64 + 1) / 2 * split), dim3(256), 0, stream,
                               tm.start(), tm.stop(), 0, X, ldx, nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0,
-                              sc.mS, sstride, part, 0, F, jp, nr);
+                              sc.mS, sstride, part, 0);
     } else if (rows_variant) {
         hipExtLaunchKernelGGL((k_syrk_tile<2, kTile, 8>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0, X, ldx,
-                              nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, tile0,
-                              (const double*)nullptr, (double*)nullptr, 0);
+                              nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, tile0);
     } else {
         // plain partial stores: the reduce (or the reducing Cholesky) that reads them next finds
         // part of them in the caches -- solve 0.71 vs 0.73 ms, SYRK unchanged, in alternating
-        // same-box runs (non-temporal stores for J itself in the FD kernel measured slower)
-        hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, 8, false>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0,
-                              X, ldx, nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, tile0,
-                              F, jp, nr);
+        // same-box runs (non-temporal stores for J itself in the FD kernel measured slower).
+        // PNOL_SYRK_NTS=1 (tuning, read per call): non-temporal partial stores (kept out of the
+        // L2s that hold the operand panels)
+        const char* e = std::getenv("PNOL_SYRK_NTS");
+        if (e && std::atoi(e) != 0)
+            hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, 8, true>), grid, dim3(512), 0, stream, tm.start(), tm.stop(),
+                                  0, X, ldx, nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part,
+                                  tile0);
+        else
+            hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, 8, false>), grid, dim3(512), 0, stream, tm.start(), tm.stop(),
+                                  0, X, ldx, nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part,
+                                  tile0);
     }
 }
 
-static int jtr_tree(pnol_ctx* ctx, int n, int sub, int s0, int nsl, double* out);
+static int jtr_gemv(pnol_ctx* ctx, const double* JT, int ldjt, long sstride, int m, int n, int mS, int s0, int nsl,
+                    const double* F, hipStream_t stream = nullptr);
+static int jtr_tree(pnol_ctx* ctx, int n, int s0, int nsl, double* out);
 
 int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                double* jtj_diag, const double* F, double* rhs) {
@@ -722,16 +679,20 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
     const int nt = (n + kTile - 1) / kTile;
     const int ntiles = nt * (nt + 1) / 2;
     const SliceCfg sc = slice_cfg(m, ntiles);
-    void *part = nullptr, *jp = nullptr;
-    const bool fold = rhs != nullptr;
+    void* part = nullptr;
     ctx->lm_trip_tiles.kind = 0;   // the trip's tiles are overwritten below
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * kS * sc.sub * kTile * kTile, &part));
-    if (fold) PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * sc.sub * n, &jp));
-    // -J^T F: its units in the SYRK's diagonal tiles, its slice tree in the reduce launch (an extra
-    // row of blocks) -- no pass of its own over J^T
     syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
-                  syrk_t64(false), fold ? F : nullptr, (double*)jp);
+                  syrk_t64(false));
     PNOL_CHECK(launch_check());
+    if (rhs) PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F));
+    // -J^T F's slice tree rides in the reduce launch (an extra row of blocks).  (The GEMV on a
+    // second stream released by the SYRK's last-dispatched workgroup -- hipStreamWaitValue32 on a
+    // tail word -- measured slower, 305-311 vs 314-317 LM iters/s: its HBM stream slowed the
+    // SYRK's last workgroups more than it hid; removed.)
+    const bool fold = rhs != nullptr;
+    void* jp = nullptr;
+    if (fold) PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
     {
         ScopedTimer tm(ctx, "syrk_reduce");
         launch_reduce(dim3(kTile / 32, ntiles + (fold ? 1 : 0)), dim3(256), 0, ctx->stream, (const double*)part,
@@ -821,15 +782,16 @@ int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h,
 }
 
 // One LM trip's linear algebra with A never formed (single process, n > PNOL_SEQ_MAX,
-// LevenbergMarquardt.cpp:55-90): the FD Jacobian, the Cholesky's prep launch (its words and
-// paddings), the J^T J split-K partials with the -J^T F units (k_syrk_tile), the reduce launch
-// writing A (the Marquardt diagonal) straight into the Cholesky's padded matrix and -J^T F into
-// rhs and b, then the persistent tile Cholesky (its chain factors tile 0 itself), the backward
-// solve and xnext = x + sigma: no A, no copy of A into the workspace.  (PNOL_LM_REDUCE=tasks:
-// the persistent launch's first tasks do the reduce themselves, beside the chain's first steps --
-// measured slower, its 285 MB partial stream in front of the chain.)  JT, rhs, sigma, xnext and
-// the solve status are bitwise those of launch_fd_jtj (+ rhs) and launch_chol_solve; for the LU
-// fallback launch_jtj_from_partials forms A from the trip's partials.
+// LevenbergMarquardt.cpp:55-90): the FD Jacobian, the -J^T F slice partials, the Cholesky's
+// prep launch (its words and paddings), the J^T J split-K partials (k_syrk_tile), the reduce
+// launch writing A (the Marquardt diagonal) straight into the Cholesky's padded matrix and
+// -J^T F into rhs and b, then the persistent tile Cholesky (its chain factors tile 0 itself), the
+// backward solve and xnext = x + sigma: no A, no copy of A into the workspace.
+// (PNOL_LM_REDUCE=tasks: the persistent launch's first tasks do the reduce themselves, beside the
+// chain's first steps -- measured slower, 5/5 same-box trip A/Bs, its 285 MB partial stream in
+// front of the chain.)  JT, rhs, sigma, xnext and the solve status are bitwise those of
+// launch_fd_jtj (+ rhs) and launch_chol_solve; for the LU fallback launch_jtj_from_partials forms
+// A from the trip's partials.
 int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
                            double* JT, int ldjt, double lambda, double* rhs, double* sigma, int* dinfo, double* xnext) {
     if (!o || !x || !h || !F0 || !JT || !rhs || !sigma || !dinfo || !xnext || ldjt < o->m) return PNOL_ERR_ARG;
@@ -840,21 +802,22 @@ int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
     const SliceCfg sc = slice_cfg(m, ntiles);
     const int split = kS * sc.sub;
     // the reduce: a launch of its own over the whole chip writing the Cholesky's padded matrix
-    // and b directly (default), or the persistent launch's first tasks (PNOL_LM_REDUCE=tasks, the
-    // round-4 form; read per call)
+    // and b directly (default), or the persistent launch's first tasks (PNOL_LM_REDUCE=tasks;
+    // read per call)
     const char* er = std::getenv("PNOL_LM_REDUCE");
     const bool tasks = er && std::strcmp(er, "tasks") == 0;
     // every workspace first: a (re)allocation frees, and a free waits for the device
     void *part = nullptr, *jp = nullptr;
     ctx->lm_trip_tiles.kind = 0;   // the trip's tiles are overwritten below
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * split * kTile * kTile, &part));
-    PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * sc.sub * n, &jp));
+    PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
     CholRed cr;
     PNOL_CHECK(launch_chol_reducing_prep(ctx, n, dinfo, cr));
     PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
+    PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F0));
     PNOL_CHECK(launch_chol_reducing_start(ctx, cr, !tasks));   // the prep launch (words, paddings, info)
     syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
-                  syrk_t64(false), F0, (double*)jp);
+                  syrk_t64(false));
     PNOL_CHECK(launch_check());
     if (!tasks) {
         {   // A (Marquardt diagonal, mirror) straight into the padded matrix, rhs into rhs and b
@@ -938,66 +901,36 @@ static void dyadic_nodes(int a, int b, std::vector<std::pair<int, int>>& out) {
     }
 }
 
-// The -J^T F units from J^T alone (pnol_jtr_d; the LM loops' fallback and general paths): thread
-// (row r, unit) runs the chain of k_syrk_tile's diagonal tiles -- c = fma(JT_rk, F_k, c) from 0.0
-// over the unit's k ascending (the unit = sub-chunk u of m-slice s, the same bounds) -- and stores
-// -c at jp[(s * sub + u) * n + r].  JT slice s at JT + s * sstride, row stride ldx (row-major J^T:
-// sstride == mS).
-__global__ __launch_bounds__(256) void k_jtr_units(const double* __restrict__ X, long ldx, long sstride, int n, int K,
-                                                   int mS, int sub, int kfirst, int kchunk, int s0, int nunits,
-                                                   const double* __restrict__ F, double* __restrict__ jp) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x, un = blockIdx.y;
-    if (r >= n || un >= nunits) return;
-    const int slice = s0 + un / sub, u = un % sub;
-    const int kbeg = slice * mS + (u == 0 ? 0 : kfirst + (u - 1) * kchunk);
-    const int kend = min(K, min((slice + 1) * mS, u == 0 ? slice * mS + kfirst : kbeg + kchunk));
-    const double* row = X + (long)slice * (sstride - mS) + (long)r * ldx;
-    double c = 0.0;
-    int k = kbeg;
-    for (; k + 8 <= kend; k += 8) {   // eight loads in flight, the chain in order
-        double a[8], f[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            a[q] = row[k + q];
-            f[q] = F[k + q];
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) c = fma(a[q], f[q], c);
-    }
-    for (; k < kend; ++k) c = fma(row[k], F[k], c);
-    jp[(long)(slice * sub + u) * n + r] = -c;
-}
-
-// the -J^T F units of slices [s0, s0 + nsl) into "jtr_part" (k_jtr_units)
-static int jtr_units(pnol_ctx* ctx, const double* JT, long ldx, long sstride, int m, int n, const SliceCfg& sc, int s0,
-                     int nsl, const double* F) {
+// -J^T F on the m-slices [s0, s0 + nsl): jp[(s - s0) * n + j] = -sum_{k in slice s} JT_jk F_k
+// (JT slice s at JT + s * sstride, row stride ldjt), then the slice nodes of that range into
+// out[c * n + j] (one node = -J^T F itself when the range is all kLmSlices slices).
+static int jtr_gemv(pnol_ctx* ctx, const double* JT, int ldjt, long sstride, int m, int n, int mS, int s0, int nsl,
+                    const double* F, hipStream_t stream) {
     if (!F) return PNOL_ERR_ARG;
     void* jp = nullptr;
-    PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * sc.sub * n, &jp));
-    if (nsl <= 0) return PNOL_OK;
-    hipLaunchKernelGGL(k_jtr_units, dim3((n + 255) / 256, nsl * sc.sub), dim3(256), 0, ctx->stream, JT, ldx, sstride, n,
-                       m, sc.mS, sc.sub, sc.kfirst, sc.kchunk, s0, nsl * sc.sub, F, (double*)jp);
+    PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
+    return launch_gemv_neg_slices(ctx, JT, ldjt, sstride, n, m, mS, s0, nsl, F, (double*)jp, stream);
+}
+
+static int jtr_tree(pnol_ctx* ctx, int n, int s0, int nsl, double* out) {
+    void* jp = nullptr;
+    PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
+    hipLaunchKernelGGL(k_tree_nodes, dim3((n + 255) / 256, 1), dim3(256), 0, ctx->stream, (const double*)jp, 0L,
+                       (long)n, 1, s0, s0 + nsl, n, out, (long)n, 0L);
     return launch_check();
 }
 
-// the slice nodes of [s0, s0 + nsl) from the units in "jtr_part" (leaf = 0.0 + the sub-chunks in
-// order) into out[c * n + j] (one node = -J^T F itself when the range is all kLmSlices slices)
-static int jtr_tree(pnol_ctx* ctx, int n, int sub, int s0, int nsl, double* out) {
-    void* jp = nullptr;
-    PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * sub * n, &jp));
-    hipLaunchKernelGGL(k_tree_nodes, dim3((n + 255) / 256, 1), dim3(256), 0, ctx->stream,
-                       (const double*)jp + (long)s0 * sub * n, 0L, (long)n, sub, s0, s0 + nsl, n, out, (long)n, 0L);
-    return launch_check();
+static int jtr_slices(pnol_ctx* ctx, const double* JT, int ldjt, long sstride, int m, int n, int mS, int s0, int nsl,
+                      const double* F, double* out) {
+    PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sstride, m, n, mS, s0, nsl, F));
+    return jtr_tree(ctx, n, s0, nsl, out);
 }
 
 int launch_jtr(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, const double* F, double* rhs) {
     if (n <= PNOL_SEQ_MAX && m <= 4096) return launch_gemv_neg_seq(ctx, JT, ldjt, n, m, F, rhs);
     if (!JT || !F || !rhs || m <= 0 || n <= 0 || ldjt < m) return PNOL_ERR_ARG;
-    const int nt = (n + kTile - 1) / kTile;
-    const SliceCfg sc = slice_cfg(m, nt * (nt + 1) / 2);
-    ScopedTimer tm(ctx, "jtr");
-    PNOL_CHECK(jtr_units(ctx, JT, ldjt, sc.mS, m, n, sc, 0, kS, F));
-    return jtr_tree(ctx, n, sc.sub, 0, kS, rhs);
+    const int mS = lm_slice_rows(m);
+    return jtr_slices(ctx, JT, ldjt, mS, m, n, mS, 0, kS, F, rhs);
 }
 
 // LevMarqMPI normal equations on the m-sliced Jacobian (layout of pnol_lm_sliced_layout):
@@ -1038,15 +971,15 @@ static int lm_normal_core(pnol_ctx* ctx, const double* JTs, int m, int n, double
     ctx->lm_trip_tiles.kind = 0;   // the trip's tiles are overwritten below
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * std::max(nsl, 1) * sc.sub * E, &part));
     const bool t64 = syrk_t64(true);
-    void* jp = nullptr;
-    PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * sc.sub * n, &jp));
-    if (nsl > 0) {   // the J^T J partials and, in their diagonal tiles, the -J^T F units of my slices
-        syrk_partials(ctx, ctx->stream, false, JTs, sc.mS, sstr, n, m, sc, s0, nsl, 0, ntiles, (double*)part, t64, F,
-                      (double*)jp);
+    if (nsl > 0) {
+        syrk_partials(ctx, ctx->stream, false, JTs, sc.mS, sstr, n, m, sc, s0, nsl, 0, ntiles, (double*)part, t64);
         PNOL_CHECK(launch_check());
+        PNOL_CHECK(jtr_gemv(ctx, JTs, sc.mS, sstr, m, n, sc.mS, s0, nsl, F));
     }
     if (P == 1) {
         // the -J^T F tree rides in the reduce launch
+        void* jp = nullptr;
+        PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
         if (!A) {   // the reducing Cholesky sums the partials itself
             out->partials = true;
             out->part = (const double*)part;
@@ -1096,7 +1029,7 @@ static int lm_normal_core(pnol_ctx* ctx, const double* JTs, int m, int n, double
     }
     PNOL_CHECK(launch_check());
     // -J^T F nodes of my slices into the tail of my allgather slot
-    if (nsl > 0) PNOL_CHECK(jtr_tree(ctx, n, sc.sub, s0, nsl, mine + (long)tpr * E));
+    if (nsl > 0) PNOL_CHECK(jtr_tree(ctx, n, s0, nsl, mine + (long)tpr * E));
     // reduce-scatter in tree order: rank q's nodes of owner d's tiles -> d
     {
         ScopedTimer tm(ctx, "exchange_A");

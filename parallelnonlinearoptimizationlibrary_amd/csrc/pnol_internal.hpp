@@ -198,6 +198,10 @@ int launch_status_agree(pnol_ctx* ctx, int* dinfo);
 // ---- kernel launchers (defined in kernels/*.hip) ------------------------------------
 int launch_gemv_neg(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y);
 int launch_gemv_neg_seq(pnol_ctx* ctx, const double* A, int lda, int rows, int cols, const double* x, double* y);
+// y[(s - s0) * rows + j] = -sum_{k in m-slice s} A_s[j][k] x[s mS + k], s in [s0, s0 + nsl)
+// stream: nullptr = the context stream
+int launch_gemv_neg_slices(pnol_ctx* ctx, const double* A, int lda, long sstride, int rows, int m, int mS, int s0,
+                           int nsl, const double* x, double* y, hipStream_t stream = nullptr);
 int launch_bfgs_update_exact(pnol_ctx* ctx, double* D, int ldd, const double* y, const double* s, int n);
 int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p, const double* a_p,
                      const double* b_p, int write_back, const double* y, const double* g, double* u, double* w,

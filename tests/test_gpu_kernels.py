@@ -757,26 +757,6 @@ def test_lm_trip_reports_non_spd(ctx):
     assert np.array_equal(_np(sb), _np(sa))
 
 
-@pytest.mark.parametrize("n", [300, 4096, 8192])
-def test_bfgs_pass_prefetch_depth_bitwise(ctx, monkeypatch, n):
-    """The fused BFGS pass with two row groups of D in flight (PNOL_PASS_PF=2) instead of one:
-    the same arithmetic in the same row order, so u, w, v and the written-back D are bitwise the
-    one-group-ahead pass's (BFGS_with_linesearch.cpp:389-432 as the rank-2 fold)."""
-    rng = np.random.default_rng(n)
-    D0 = rng.standard_normal((n, n))
-    y, g = ctx.tensor(rng.standard_normal(n)), ctx.tensor(rng.standard_normal(n))
-    pend = tuple(ctx.tensor(1e-3 * rng.standard_normal(n)) for _ in range(3))
-    out = {}
-    for pf in ("1", "2"):
-        monkeypatch.setenv("PNOL_PASS_PF", pf)
-        D = ctx.tensor(D0)
-        u, w, v = ctx.bfgs_pass(D, y, g, pend, True)
-        ctx.synchronize()
-        out[pf] = [_np(t) for t in (u, w, v, D)]
-    for a, b in zip(out["1"], out["2"]):
-        assert np.array_equal(a, b)
-
-
 def test_lm_agree_status_codes_one_rank(ctx):
     """pnol_lm_agree_status_d with one rank: dinfo[1] = the action code of dinfo[0] -- 0 none, 1 a
     timed-out Cholesky wait (kCholTimeout = -7: relaunch the Cholesky), 2 any other nonzero status
