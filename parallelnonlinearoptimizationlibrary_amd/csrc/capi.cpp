@@ -423,6 +423,7 @@ int pnol_dobj_destroy(pnol_dobj* o) {
     if (o->p1) (void)hipFree(o->p1);
     if (o->p2) (void)hipFree(o->p2);
     if (o->at) (void)hipFree(o->at);
+    (void)hipGetLastError();   // a failed clean-up call must not surface at the next launch check
     delete o;
     return PNOL_OK;
 }

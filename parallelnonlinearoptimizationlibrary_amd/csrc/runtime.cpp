@@ -500,6 +500,7 @@ int pnol_ctx_destroy(pnol_ctx* ctx) {
         }
     for (hipEvent_t e : ctx->timers.free_events) (void)hipEventDestroy(e);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    (void)hipGetLastError();   // a failed clean-up call must not surface at the next launch check
     if (ctx == g_default) g_default = nullptr;
     delete ctx;
     return PNOL_OK;
@@ -654,6 +655,7 @@ int pnol_event_destroy(pnol_event* ev) {
     if (!ev) return PNOL_ERR_ARG;
     (void)hipSetDevice(ev->device);
     (void)hipEventDestroy(ev->e);
+    (void)hipGetLastError();
     delete ev;
     return PNOL_OK;
 }
