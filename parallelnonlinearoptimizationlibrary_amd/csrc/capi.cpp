@@ -351,7 +351,7 @@ int pnol_dobj_create(pnol_ctx* ctx, int kind, int n, int m, const double* host_p
             return PNOL_ERR_UNSUPPORTED;
     }
     auto* o = new pnol_dobj();
-    o->kind = kind; o->n = n; o->m = m; o->power = power; o->ctx = ctx;
+    o->kind = kind; o->n = n; o->m = m; o->power = power; o->ctx = ctx; o->device = ctx->device;
     o->len0 = len0; o->len1 = len1;
     auto upload = [&](const double* src, size_t len, double** dst) -> int {
         if (!src || !len) return PNOL_OK;
@@ -382,7 +382,7 @@ int pnol_dobj_create_synthetic(pnol_ctx* ctx, int kind, int n, int m, unsigned l
     if (!out || n <= 0) return PNOL_ERR_ARG;
     *out = nullptr;
     auto* o = new pnol_dobj();
-    o->kind = kind; o->n = n; o->m = m; o->ctx = ctx;
+    o->kind = kind; o->n = n; o->m = m; o->ctx = ctx; o->device = ctx->device;
     int st = PNOL_OK;
     if (kind == PNOL_OBJ_QUADRATIC) {
         if (hipMalloc(&o->p0, sizeof(double) * n) != hipSuccess || hipMalloc(&o->p1, sizeof(double) * n) != hipSuccess)
@@ -418,7 +418,7 @@ int pnol_dobj_create_synthetic(pnol_ctx* ctx, int kind, int n, int m, unsigned l
 
 int pnol_dobj_destroy(pnol_dobj* o) {
     if (!o) return PNOL_ERR_ARG;
-    if (o->ctx) (void)hipSetDevice(o->ctx->device);
+    (void)hipSetDevice(o->device);
     if (o->p0) (void)hipFree(o->p0);
     if (o->p1) (void)hipFree(o->p1);
     if (o->p2) (void)hipFree(o->p2);

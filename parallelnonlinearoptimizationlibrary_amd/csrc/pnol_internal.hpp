@@ -110,6 +110,7 @@ struct pnol_dobj {
     double* at = nullptr;     // LINRES: A in 64-row k-major panels (fd.hip), built on first FD use
     size_t len0 = 0, len1 = 0;
     pnol_ctx* ctx = nullptr;
+    int device = 0;           // ctx's device, kept so destroy never reads a context freed before it
     unsigned long long id = pnol_dobj_next_id();   // unique per creation (checkpoint slot tags)
   private:
     static unsigned long long pnol_dobj_next_id() {
