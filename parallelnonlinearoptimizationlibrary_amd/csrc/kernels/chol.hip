@@ -1354,9 +1354,10 @@ struct RedArgs {
     // the matrix and b already in P / bv (a reduce launch wrote them; every version and b word
     // starts at 0): no reduce tasks, the chain factors tile 0 itself
     bool preloaded = false;
-    // the diagonal chain's wave 0 at issue priority 3 (s_setprio; PNOL_CHOL_PRIO, tuning): the
-    // CU's shared arbiters favour the pivot chain over the look-ahead's polling and staging
-    int prio = 0;
+    // the worker claim order: each step's critical tasks (panels (k+1, k), (k+2, k), updates
+    // (k+2, k+1), (k+2, k+2)) claimed one step early, ahead of the previous step's bulk
+    // (crit_order; PNOL_CHOL_CRITFIRST=0 keeps the plain step order)
+    int crit_first = 0;
 };
 
 template <int SUB>
@@ -1451,6 +1452,46 @@ __device__ void red_task(int u, const RedArgs& red, double* __restrict__ P, long
 }
 
 
+// The worker claim order with each step's critical tasks one step early.  Step k (R = T-1-k
+// panel rows) holds S_k = R + R (R + 1) / 2 - 1 tasks, local index g: panels g < R, then the
+// updates with its two critical ones first (g = R: (k+2, k+1), g = R+1: (k+2, k+2)).  Its
+// critical set C_k is g in {0, 1, R, R+1} (R >= 2; {0} for R = 1): the chain's next tiles come
+// from these.  Claim order: C_0, C_1, rest_0, C_2, rest_1, ..., C_{T-2}, rest_{T-3}, rest_{T-2}.
+// A task of C_{k+1} may wait on a task of rest_k claimed after it, so up to |C| = 4 workers can
+// wait on unclaimed tasks: the order is used only with more than 8 workers (every other task
+// waits only on tasks claimed before it).  Maps the claim index g to (k, R, local g).
+__device__ __forceinline__ void crit_order(int& g, int T, int& k, int& R) {
+    auto csz = [&](int kk) { return T - 1 - kk >= 2 ? 4 : 1; };
+    auto cmap = [&](int x, int RR) { return x < 2 ? x : RR + x - 2; };
+    if (g < csz(0)) {
+        k = 0;
+        R = T - 1;
+        g = cmap(g, R);
+        return;
+    }
+    g -= csz(0);
+    for (int kk = 0;; ++kk) {
+        if (kk + 1 <= T - 2) {
+            const int c1 = csz(kk + 1);
+            if (g < c1) {
+                k = kk + 1;
+                R = T - 1 - k;
+                g = cmap(g, R);
+                return;
+            }
+            g -= c1;
+        }
+        const int RR = T - 1 - kk, S = RR + RR * (RR + 1) / 2 - 1, rest = S - csz(kk);
+        if (g < rest) {
+            k = kk;
+            R = RR;
+            g = g < RR - 2 ? g + 2 : g + 4;
+            return;
+        }
+        g -= rest;
+    }
+}
+
 __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P, double* __restrict__ Lm, long ldp,
                                                       int T, double* __restrict__ W, double* __restrict__ bv,
                                                       double* __restrict__ zv, int* __restrict__ flags, int ntasks,
@@ -1472,7 +1513,6 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
     double* Y = smem + kStage;
 
     if (blockIdx.x == 0) {   // ---------------- the diagonal chain
-        if (red.prio && wave == 0) __builtin_amdgcn_s_setprio(3);
         const EarlyLds E{pfx, pll, pfc, ew};
         if (t < 4) ew[t] = 0;
         const bool smode = red.part || red.packed || red.preloaded;   // the chain also factors tile 0
@@ -1542,12 +1582,16 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         }
         g -= nred;
         int k = 0, R = T - 1;
-        for (;;) {   // step k holds R panel rows and R (R + 1) / 2 - 1 update tiles
-            const int S = R + R * (R + 1) / 2 - 1;
-            if (g < S) break;
-            g -= S;
-            ++k;
-            --R;
+        if (red.crit_first && gridDim.x > 8) {
+            crit_order(g, T, k, R);
+        } else {
+            for (;;) {   // step k holds R panel rows and R (R + 1) / 2 - 1 update tiles
+                const int S = R + R * (R + 1) / 2 - 1;
+                if (g < S) break;
+                g -= S;
+                ++k;
+                --R;
+            }
         }
         const int k0 = k * NB;
         if (g < R) {   // ---- panel row i: L_ik = A_ik W_k^T, then b_i -= L_ik (W_k b_k)
@@ -1853,7 +1897,10 @@ static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, i
     // than the prepare it saves.
     const int lookahead = el ? std::max(0, std::atoi(el)) : 64;
     RedArgs rp = red;
-    if (const char* ep = std::getenv("PNOL_CHOL_PRIO")) rp.prio = std::atoi(ep) != 0;
+    {
+        const char* ec = std::getenv("PNOL_CHOL_CRITFIRST");
+        rp.crit_first = !ec || std::atoi(ec) != 0;
+    }
     const int slots = std::max(ctx->num_cu, 1) - 1;
     const int want = ew ? std::atoi(ew) : slots;
     const int nred = (red.part || red.packed) ? 1 + T * (T + 1) / 2 : 0;
