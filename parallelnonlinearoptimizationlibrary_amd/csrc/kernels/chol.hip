@@ -1354,10 +1354,9 @@ struct RedArgs {
     // the matrix and b already in P / bv (a reduce launch wrote them; every version and b word
     // starts at 0): no reduce tasks, the chain factors tile 0 itself
     bool preloaded = false;
-    // the worker claim order: each step's critical tasks (panels (k+1, k), (k+2, k), updates
-    // (k+2, k+1), (k+2, k+2)) claimed one step early, ahead of the previous step's bulk
-    // (crit_order; PNOL_CHOL_CRITFIRST=0 keeps the plain step order)
-    int crit_first = 0;
+    // the worker claim order (task_of): 0 by step, 1 each step's critical tasks one step early,
+    // 2 by tile column (PNOL_CHOL_ORDER)
+    int order = 0;
 };
 
 template <int SUB>
@@ -1452,44 +1451,78 @@ __device__ void red_task(int u, const RedArgs& red, double* __restrict__ P, long
 }
 
 
-// The worker claim order with each step's critical tasks one step early.  Step k (R = T-1-k
-// panel rows) holds S_k = R + R (R + 1) / 2 - 1 tasks, local index g: panels g < R, then the
-// updates with its two critical ones first (g = R: (k+2, k+1), g = R+1: (k+2, k+2)).  Its
-// critical set C_k is g in {0, 1, R, R+1} (R >= 2; {0} for R = 1): the chain's next tiles come
-// from these.  Claim order: C_0, C_1, rest_0, C_2, rest_1, ..., C_{T-2}, rest_{T-3}, rest_{T-2}.
-// A task of C_{k+1} may wait on a task of rest_k claimed after it, so up to |C| = 4 workers can
-// wait on unclaimed tasks: the order is used only with more than 8 workers (every other task
-// waits only on tasks claimed before it).  Maps the claim index g to (k, R, local g).
-__device__ __forceinline__ void crit_order(int& g, int T, int& k, int& R) {
-    auto csz = [&](int kk) { return T - 1 - kk >= 2 ? 4 : 1; };
-    auto cmap = [&](int x, int RR) { return x < 2 ? x : RR + x - 2; };
-    if (g < csz(0)) {
-        k = 0;
-        R = T - 1;
-        g = cmap(g, R);
-        return;
+// The workers' claim order: claim index g -> step k and task -- a panel row i (L_ik, b_i), or
+// an update tile (i, j) -= L_ik L_jk^T.  Step k (R = T-1-k panel rows) holds
+// S_k = R + R (R + 1) / 2 - 1 tasks, local index l: panels l < R, then the update tiles in
+// column order with the two the chain needs next first (l = R: (k+2, k+1), l = R+1: (k+2, k+2)).
+//   order 0: step by step (every task waits only on tasks claimed before it).
+//   order 1: each step's critical set C_k (l in {0, 1, R, R+1}; {0} for R = 1) one step early:
+//            C_0, C_1, rest_0, C_2, rest_1, ..., C_{T-2}, rest_{T-3}, rest_{T-2}.  A task of C_{k+1}
+//            may wait on a task of rest_k claimed after it: up to 4 workers can wait on unclaimed
+//            tasks, so this order needs more than 4 workers.
+//   order 2: by tile column s = 1 .. T-1 (left-looking): the panels (i, s-1), i >= s, then every
+//            update of column s's tiles, by step k = 0 .. s-1 and row i (the chain's own (s, s) at
+//            k = s-1 excluded).  Every dependency (the tile's earlier update, the panels (., k), b's
+//            earlier panels, W_k) comes earlier in this order, so any worker count is safe; the
+//            tiles near the diagonal -- the chain's next ones -- get their updates without
+//            queueing behind far columns.
+struct Task {
+    int k, i, j;   // j < 0: panel row i of step k
+};
+__device__ __forceinline__ Task task_local(int k, int l, int T) {
+    const int R = T - 1 - k;
+    if (l < R) return {k, k + 1 + l, -1};
+    const int q = l - R;
+    // full column order f: column k+1 holds f = 0 .. R-1 (f = 0 is the chain's), column k+2
+    // starts at f = R, ...
+    int u = q == 0 ? 1 : (q == 1 ? R : (q < R ? q : q + 1));
+    int j = k + 1;
+    while (u >= T - j) {
+        u -= T - j;
+        ++j;
     }
-    g -= csz(0);
-    for (int kk = 0;; ++kk) {
-        if (kk + 1 <= T - 2) {
-            const int c1 = csz(kk + 1);
-            if (g < c1) {
-                k = kk + 1;
-                R = T - 1 - k;
-                g = cmap(g, R);
-                return;
+    return {k, j + u, j};
+}
+__device__ __forceinline__ Task task_of(int g, int T, int order) {
+    if (order == 2) {
+        for (int s = 1;; ++s) {
+            const int c = T - s, sz = (s + 1) * c - 1;
+            if (g < sz || s == T - 1) {
+                if (g < c) return {s - 1, s + g, -1};
+                int y = g - c;
+                const int k = y / c;
+                int i = s + y % c;
+                if (k == s - 1) i = s + 1 + (y - (s - 1) * c);   // skip the chain's (s, s)
+                return {k, i, s};
             }
-            g -= c1;
+            g -= sz;
         }
-        const int RR = T - 1 - kk, S = RR + RR * (RR + 1) / 2 - 1, rest = S - csz(kk);
-        if (g < rest) {
-            k = kk;
-            R = RR;
-            g = g < RR - 2 ? g + 2 : g + 4;
-            return;
-        }
-        g -= rest;
     }
+    if (order == 1) {
+        auto csz = [&](int kk) { return T - 1 - kk >= 2 ? 4 : 1; };
+        auto cmap = [&](int x, int RR) { return x < 2 ? x : RR + x - 2; };
+        if (g < csz(0)) return task_local(0, cmap(g, T - 1), T);
+        g -= csz(0);
+        for (int kk = 0;; ++kk) {
+            if (kk + 1 <= T - 2) {
+                const int c1 = csz(kk + 1);
+                if (g < c1) return task_local(kk + 1, cmap(g, T - 2 - kk), T);
+                g -= c1;
+            }
+            const int RR = T - 1 - kk, S = RR + RR * (RR + 1) / 2 - 1, rest = S - csz(kk);
+            if (g < rest || kk >= T - 2) return task_local(kk, g < RR - 2 ? g + 2 : g + 4, T);
+            g -= rest;
+        }
+    }
+    int k = 0, R = T - 1;
+    for (;;) {
+        const int S = R + R * (R + 1) / 2 - 1;
+        if (g < S || R <= 1) break;
+        g -= S;
+        ++k;
+        --R;
+    }
+    return task_local(k, g, T);
 }
 
 __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P, double* __restrict__ Lm, long ldp,
@@ -1581,21 +1614,11 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             continue;
         }
         g -= nred;
-        int k = 0, R = T - 1;
-        if (red.crit_first && gridDim.x > 8) {
-            crit_order(g, T, k, R);
-        } else {
-            for (;;) {   // step k holds R panel rows and R (R + 1) / 2 - 1 update tiles
-                const int S = R + R * (R + 1) / 2 - 1;
-                if (g < S) break;
-                g -= S;
-                ++k;
-                --R;
-            }
-        }
+        const Task tk = task_of(g, T, red.order == 1 && gridDim.x <= 5 ? 0 : red.order);
+        const int k = tk.k;
         const int k0 = k * NB;
-        if (g < R) {   // ---- panel row i: L_ik = A_ik W_k^T, then b_i -= L_ik (W_k b_k)
-            const int i = k + 1 + g, i0 = i * NB;
+        if (tk.j < 0) {   // ---- panel row i: L_ik = A_ik W_k^T, then b_i -= L_ik (W_k b_k)
+            const int i = tk.i, i0 = i * NB;
 #ifdef PNOL_CHOL_TIMELINE
             const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
             if (i == k + 2) PNOL_CRIT(k, 1)
@@ -1645,18 +1668,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
 #endif
             continue;
         }
-        // ---- update tile (i, j) -= L_ik L_jk^T.  Full column order f: column k+1 holds
-        // f = 0 .. R-1 (tile (k+1+f, k+1); f = 0 is the diagonal chain's), column k+2 starts with
-        // (k+2, k+2) at f = R, and so on.  Step k's first two tasks are the tiles the chain needs
-        // next, f = 1 = (k+2, k+1) and f = R = (k+2, k+2); the rest follow in column order.
-        const int q = g - R;
-        int u = q == 0 ? 1 : (q == 1 ? R : (q < R ? q : q + 1));
-        int j = k + 1;
-        while (u >= T - j) {
-            u -= T - j;
-            ++j;
-        }
-        const int i = j + u;
+        // ---- update tile (i, j) -= L_ik L_jk^T (task_of's order)
+        const int i = tk.i, j = tk.j;
 #ifdef PNOL_CHOL_TIMELINE
         const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
         const bool crit = i == k + 2 && j == k + 1;
@@ -1898,8 +1911,8 @@ static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, i
     const int lookahead = el ? std::max(0, std::atoi(el)) : 64;
     RedArgs rp = red;
     {
-        const char* ec = std::getenv("PNOL_CHOL_CRITFIRST");
-        rp.crit_first = !ec || std::atoi(ec) != 0;
+        const char* eo = std::getenv("PNOL_CHOL_ORDER");
+        rp.order = eo ? std::max(0, std::min(2, std::atoi(eo))) : 0;
     }
     const int slots = std::max(ctx->num_cu, 1) - 1;
     const int want = ew ? std::atoi(ew) : slots;
