@@ -1331,6 +1331,23 @@ __device__ __forceinline__ void publish(int* w, int v) {
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// a worker task's last publish: lane 0 also claims the worker's next task, so the claim's
+// round trip overlaps the store drain the publish waits for anyway (the claim order is unchanged)
+__device__ __forceinline__ void publish_claim(int* w, int v, int* counter, int& pre) {
+    if (threadIdx.x == 0) pre = atomicAdd(counter, 1);
+    publish(w, v);
+}
+// every *f[q] >= tg[q] in one round of loads (no waiting)
+template <int N>
+__device__ __forceinline__ bool ready_all(const int* const (&f)[N], const int (&tg)[N]) {
+    int v[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] = __hip_atomic_load(f[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool ok = true;
+#pragma unroll
+    for (int q = 0; q < N; ++q) ok = ok && v[q] >= tg[q];
+    return ok;
+}
 
 // The reducing form (launch_chol_reducing, the LM trip): A is not formed -- the persistent
 // launch's first tasks sum the J^T J split-K partials of k_syrk_tile into the padded matrix P
@@ -1589,8 +1606,12 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
     }
 
     const int nred = (red.part || red.packed) ? 1 + T * (T + 1) / 2 : 0;   // the reducing form's first tasks
+    int pre = -1;   // lane 0: the next task, claimed during the last one's publish (publish_claim)
     for (;;) {   // ---------------- workers
-        if (t == 0) task_sh = atomicAdd(pw.counter, 1);
+        if (t == 0) {
+            task_sh = pre >= 0 ? pre : atomicAdd(pw.counter, 1);
+            pre = -1;
+        }
         __syncthreads();
         int g = task_sh;
         __syncthreads();   // task_sh is rewritten by the next claim
@@ -1648,7 +1669,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
                 stg<true>(bv + i0 + t, ldg<true>(bv + i0 + t) - s);
                 if (i == k + 1) stg<true>(zv + k0 + t, zsh[t]);
             }
-            publish(pw.bcnt + i, k + 1);
+            publish_claim(pw.bcnt + i, k + 1, pw.counter, pre);
 #ifdef PNOL_CHOL_TIMELINE
             chol_tl_mark(k, 1, tl0);
 #endif
@@ -1662,26 +1683,38 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         if (crit) PNOL_CRIT(k, 4)
 #endif
         // the tile's earlier updates first: its loads stay in flight while the workgroup waits
-        // for the two panels
-        if (t == 0) ok_sh = spin_ge(pw.ver + i * T + j, k, info);
-        __syncthreads();
-        if (!ok_sh) return;
-        d4 acc[2][2];
-        acc_load<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
+        // for the two panels; when all three words are already there (one round of loads), the
+        // tile and both panels are loaded together
         if (t == 0) {
-            ok_sh = spin_all<2>({pw.lcnt + i, pw.lcnt + j}, {k + 1, k + 1}, info);
-#ifdef PNOL_CHOL_TIMELINE
-            if (crit) PNOL_CRIT(k, 5)
-#endif
+            ok_sh = ready_all<3>({pw.ver + i * T + j, pw.lcnt + i, pw.lcnt + j}, {k, k + 1, k + 1})
+                        ? 2
+                        : spin_ge(pw.ver + i * T + j, k, info);
         }
         __syncthreads();
-        if (!ok_sh) return;
+        const int st0 = ok_sh;
+        if (!st0) return;
+        d4 acc[2][2];
+        acc_load<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
+        if (st0 != 2) {
+            __syncthreads();   // every read of ok_sh above is done
+            if (t == 0) {
+                ok_sh = spin_all<2>({pw.lcnt + i, pw.lcnt + j}, {k + 1, k + 1}, info);
+#ifdef PNOL_CHOL_TIMELINE
+                if (crit) PNOL_CRIT(k, 5)
+#endif
+            }
+            __syncthreads();
+            if (!ok_sh) return;
+        }
+#ifdef PNOL_CHOL_TIMELINE
+        else if (crit) PNOL_CRIT(k, 5)
+#endif
         stage_tile<true>(X, Lm, ldp, i * NB, k0);
         if (i != j) stage_tile<true>(Y, Lm, ldp, j * NB, k0);
         __syncthreads();
         mfma_xyt<true>(acc, X, i != j ? Y : X, wr, wc, lane);
         acc_store<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
-        publish(pw.ver + i * T + j, k + 1);
+        publish_claim(pw.ver + i * T + j, k + 1, pw.counter, pre);
 #ifdef PNOL_CHOL_TIMELINE
         if (crit) PNOL_CRIT(k, 6)
         chol_tl_mark(k, 2, tl0);
