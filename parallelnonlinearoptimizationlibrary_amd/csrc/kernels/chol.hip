@@ -1922,12 +1922,14 @@ static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, i
     const char* ew = std::getenv("PNOL_CHOL5_WORKERS");
     const char* el = std::getenv("PNOL_CHOL_LOOKAHEAD");
     // > 0: the look-ahead gives up once wave 0 has finished that many columns of the tile
-    // (0 off; above 64: the factor waits for the next tiles).  Measured at n = 2048
-    // (tools/microbench/chol_timeline.hip): 0: 0.645 ms, 52: 0.625, 64: 0.621 (default; half
-    // the steps find their tiles ready), 1000: 0.705 -- the next tiles wait on a panel and an
-    // update task (~6 us each after W_{d-1}), so waiting for them inside the factor costs more
-    // than the prepare it saves.
-    const int lookahead = el ? std::max(0, std::atoi(el)) : 64;
+    // (0 off; above 64: the factor waits for the next tiles).  The next tiles wait on a panel and
+    // an update task (~6 us each after W_{d-1}), so a look-ahead that starts late runs past the
+    // factor (its staging and MFMAs take ~9k cycles) and costs more than the prepare it saves.
+    // Measured at n = 2048 with the micro-panel factor (tools/microbench/chol_timeline.hip, two
+    // rounds, profiles/r05_lookahead_sweep.txt): 0: 0.585-0.587 ms, 32: 0.582-0.587, 40: 0.579-
+    // 0.585, 48: 0.571-0.578 (default), 56: 0.588-0.597, 64: 0.596-0.601; LM bench 52 vs 64: 3
+    // of 3 same-box pairs faster (327-328 vs 324-328 LM iters/s).  (Round 2's factor: 64 best.)
+    const int lookahead = el ? std::max(0, std::atoi(el)) : 48;
     RedArgs rp = red;
     {
         const char* eo = std::getenv("PNOL_CHOL_ORDER");
