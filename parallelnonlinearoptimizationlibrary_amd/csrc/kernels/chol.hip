@@ -530,15 +530,20 @@ __device__ __forceinline__ void blk_put(double* __restrict__ B, const d4& acc, i
     for (int r = 0; r < 4; ++r) B[((lane >> 4) + 4 * r) * kBP + (lane & 15)] = acc[r];
 }
 
-__host__ __device__ constexpr int own_i(int ow, int b) { return ow == 2 ? (b == 0 ? 1 : (b == 2 ? 2 : 3)) : (b == 0 ? 2 : 3); }
-__host__ __device__ constexpr int own_q(int ow, int b) { return ow == 2 ? (b < 2 ? 1 : b) : b + 1; }
+__host__ __device__ constexpr int own_i(int ow, int b) { return ow == 2 ? (b == 0 ? 1 : 3) : (b == 1 ? 3 : 2); }
+__host__ __device__ constexpr int own_q(int ow, int b) { return ow == 2 ? (b < 2 ? 1 : 3) : (b == 0 ? 1 : 2); }
 // The trailing update by micro-panels 0 and 1, owned by wave OW (2 or 3): blocks (ib, q),
-// 1 <= q <= ib <= 3, with (ib - q) & 1 == OW - 2.  Wave 2: (1,1) (3,1) (2,2) (3,3); wave 3:
-// (2,1) (3,2).  Block (3,3) goes to LDS with the blocks of micro-panel 2; wave 0 applies
-// micro-panel 2's update to it (mp_panel<3>).
+// 1 <= q <= ib <= 3, three each.  Wave 2: (1,1) (3,1) (3,3); wave 3: (2,1) (3,2) (2,2).  Block
+// (3,3) goes to LDS with the blocks of micro-panel 2; wave 0 applies micro-panel 2's update to
+// it (mp_panel<3>).
+// Lsrc / kb0 (the persistent chain, Lsrc non-null): the prepare left these blocks without their
+// K blocks kb0 .. 3 of -L L^T (deferred, so the chain's first micro-panel starts after only the
+// block column 0 products); the owner applies them first, from L in the substage layout at Lsrc
+// -- the same MFMAs in the same order as diag_prepare / late_prepare, so the blocks and W are
+// bitwise unchanged.  kb0 = 4: nothing deferred.
 template <int OW>
-__device__ __forceinline__ void mp_owner(const MpLds& M, int* cnt, int lane) {
-    constexpr int NBk = OW == 2 ? 4 : 2;
+__device__ __forceinline__ void mp_owner(const MpLds& M, int* cnt, int lane, const double* __restrict__ Lsrc, int kb0) {
+    constexpr int NBk = 3;
     const int frow = lane & 15, fk = lane >> 4;
     d4 acc[NBk];
 #pragma unroll
@@ -546,6 +551,27 @@ __device__ __forceinline__ void mp_owner(const MpLds& M, int* cnt, int lane) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             acc[b][r] = *mp_s(M, 16 * own_i(OW, b) + (lane >> 4) + 4 * r, 16 * own_q(OW, b) + (lane & 15));
+    if (Lsrc && kb0 < 4) {
+#pragma unroll
+        for (int b = 0; b < NBk; ++b) {
+            const int ib = own_i(OW, b), q = own_q(OW, b);
+            double fa[4][4], fb[4][4];
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+                if (kb >= kb0)
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) {
+                        fa[kb][kk] = -Lsrc[kb * kSub + (ib * 16 + frow) * kPad + kk * 4 + fk];
+                        fb[kb][kk] = Lsrc[kb * kSub + (q * 16 + frow) * kPad + kk * 4 + fk];
+                    }
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+                if (kb >= kb0)
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk)
+                        acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[kb][kk], fb[kb][kk], acc[b], 0, 0, 0);
+        }
+    }
     auto panel = [&](auto pc) {
         constexpr int P = decltype(pc)::value, LD = mp_ld(P);
         const double* Lp = M.Lc + mp_base(P);
@@ -655,7 +681,8 @@ __device__ __forceinline__ void mp_w_rows(const MpLds& M, double* __restrict__ W
 template <bool STAMP = false, bool SC1 = false, class EARLY = NoEarly>
 __device__ __forceinline__ void factor_diag16(const DiagLds& L, double* __restrict__ rinv, int* cnt,
                                               double* __restrict__ Wd, int d, int* info, long long* st = nullptr,
-                                              const EARLY& early = EARLY(), double* __restrict__ Wst = nullptr) {
+                                              const EARLY& early = EARLY(), double* __restrict__ Wst = nullptr,
+                                              const double* __restrict__ Lsrc = nullptr, int kb0 = 4) {
     const int t = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
     const MpLds M = mp_lds(L);
     if (wave == 0) {
@@ -704,8 +731,8 @@ __device__ __forceinline__ void factor_diag16(const DiagLds& L, double* __restri
         if constexpr (STAMP) st[12] = __builtin_amdgcn_s_memtime();
         mp_vx<3, 2>(M, M.Xs + 2 * kBlk, lane);
     } else {
-        if (wave == 2) mp_owner<2>(M, cnt, lane);
-        else mp_owner<3>(M, cnt, lane);
+        if (wave == 2) mp_owner<2>(M, cnt, lane, Lsrc, kb0);
+        else mp_owner<3>(M, cnt, lane, Lsrc, kb0);
         wait_lds_ge(cnt + 1, 1);   // EarlyNext reads W rows 0..31
         early(wave, lane);
     }
@@ -738,8 +765,9 @@ __device__ __forceinline__ void factor_diag16(const DiagLds& L, double* __restri
 template <bool STAMP = false, bool SC1 = false, class EARLY = NoEarly>
 __device__ __forceinline__ void factor_diag(const DiagLds& L, double* __restrict__ rinv, int* cnt,
                                             double* __restrict__ Wd, int d, int* info, long long* st = nullptr,
-                                            const EARLY& early = EARLY(), double* __restrict__ Wst = nullptr) {
-    factor_diag16<STAMP, SC1, EARLY>(L, rinv, cnt, Wd, d, info, st, early, Wst);
+                                            const EARLY& early = EARLY(), double* __restrict__ Wst = nullptr,
+                                            const double* __restrict__ Lsrc = nullptr, int kb0 = 4) {
+    factor_diag16<STAMP, SC1, EARLY>(L, rinv, cnt, Wd, d, info, st, early, Wst, Lsrc, kb0);
 }
 
 // ---- the diagonal workgroup's two products, balanced over its 4 waves --------------------
@@ -807,6 +835,14 @@ __device__ __forceinline__ int diag_blk(int w, int s) {   // (ib << 2) | jb, or 
                                {(2 << 2) | 0, (2 << 2) | 1, -1}, {(2 << 2) | 2, (1 << 2) | 1, -1}};
     return tab[w][s];
 }
+// the deferred form (the persistent chain): only the block column jb = 0 gets -L L^T here, one
+// block per wave (listed first); the other blocks are stored as they are and their owners in
+// factor_diag16 (mp_owner) apply the products during the first micro-panel
+__device__ __forceinline__ int diag_blk_def(int w, int s) {
+    constexpr int tab[4][3] = {{0, (3 << 2) | 1, (1 << 2) | 1}, {(1 << 2) | 0, (3 << 2) | 2, (3 << 2) | 3},
+                               {(2 << 2) | 0, (2 << 2) | 1, -1}, {(3 << 2) | 0, (2 << 2) | 2, -1}};
+    return tab[w][s];
+}
 
 #ifdef PNOL_CHOL_TIMELINE
 // tools/microbench/chol_timeline.hip only: per launch k + 1 and workgroup class (0 diagonal,
@@ -844,18 +880,21 @@ __device__ __forceinline__ void chol_tl_mark(int k, int cls, unsigned long long 
 // copy L.  X / Y: the two staging areas (smem, smem + kStage).
 // w_in_lds: Y already holds W_k in the substage layout (the previous factor_diag16 of the chain
 // left it there), so only A_{d,k} is staged.
+// Ldef (the persistent chain): L goes to Ldef (substage layout) and only block column 0 gets
+// -L L^T here (diag_blk_def); factor_diag16's owners apply the rest (mp_owner, kb0 = 0).
 template <bool SC1 = false>
 __device__ __forceinline__ void diag_prepare(const double* __restrict__ P, long ldp, const double* __restrict__ W,
                                              int k, double* __restrict__ X, double* __restrict__ Y, const DiagLds& L,
-                                             int wave, int lane, bool w_in_lds = false) {
+                                             int wave, int lane, bool w_in_lds = false, double* __restrict__ Ldef = nullptr) {
     const int d0 = (k + 1) * NB;
     const int k0 = k * NB;
+    const bool def = Ldef != nullptr;
     stage_tile<SC1>(X, P, ldp, d0, k0);
     if (!w_in_lds) stage_tile<SC1>(Y, W + (long)k * NB * NB, NB, 0, 0);
     d4 cdd[3];   // this wave's lower blocks of A_dd, in flight during the first product
 #pragma unroll
     for (int sb = 0; sb < 3; ++sb) {
-        const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
+        const int bl = def ? diag_blk_def(wave, sb) : diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             cdd[sb][r] = bl < 0 ? 0.0
@@ -867,20 +906,21 @@ __device__ __forceinline__ void diag_prepare(const double* __restrict__ P, long 
     diag_l_strip(lst, X, Y, wave, lane);        // L_{d,k} = A_{d,k} W_k^T, strip `wave`
     __syncthreads();
     PNOL_CHOL_STAMP(k, 2)
-    diag_strip_to_stage(lst, X, wave, lane);
+    double* const Ls = def ? Ldef : X;
+    diag_strip_to_stage(lst, Ls, wave, lane);
     __syncthreads();
     const int frow = lane & 15, fk = lane >> 4;
 #pragma unroll
     for (int sb = 0; sb < 3; ++sb) {           // A_dd - L L^T, lower blocks
-        const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
-        if (bl < 0) continue;                   // wave-uniform
+        const int bl = def ? diag_blk_def(wave, sb) : diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
+        if (bl < 0 || (def && jb != 0)) continue;   // wave-uniform
         double fa[4][4], fb[4][4];              // the block's operands, read before its MFMAs
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
-                fa[kb][kk] = -X[kb * kSub + (ib * 16 + frow) * kPad + kk * 4 + fk];
-                fb[kb][kk] = X[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
+                fa[kb][kk] = -Ls[kb * kSub + (ib * 16 + frow) * kPad + kk * 4 + fk];
+                fb[kb][kk] = Ls[kb * kSub + (jb * 16 + frow) * kPad + kk * 4 + fk];
             }
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb)
@@ -890,7 +930,7 @@ __device__ __forceinline__ void diag_prepare(const double* __restrict__ P, long 
     __syncthreads();                            // X / Y are rewritten below
 #pragma unroll
     for (int sb = 0; sb < 3; ++sb) {
-        const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
+        const int bl = def ? diag_blk_def(wave, sb) : diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
         if (bl < 0) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -1070,8 +1110,10 @@ struct EarlyNext {
 // The rest of diag_prepare after a look-ahead: L's right half (block columns 2, 3) from the staged
 // A_{d,k} (E.pfx) and W_k's rows 32..63 (Wst), then K blocks 2, 3 of A_dd - L L^T on the partial
 // blocks in E.pfc, into the split LDS copy L.
+// def: only block column 0 gets K blocks 2, 3 here (diag_blk_def); factor_diag16's owners apply
+// the rest from E.pfx (mp_owner, kb0 = 2)
 __device__ __forceinline__ void late_prepare(const EarlyLds& E, const double* __restrict__ Wst, const DiagLds& L,
-                                             int wave, int lane) {
+                                             int wave, int lane, bool def = false) {
     const int frow = lane & 15, fk = lane >> 4;
     // each phase's MFMA operands are read from LDS before its first MFMA (as in EarlyNext)
     {
@@ -1105,7 +1147,8 @@ __device__ __forceinline__ void late_prepare(const EarlyLds& E, const double* __
     d4 c[3];
 #pragma unroll
     for (int sb = 0; sb < 3; ++sb) {
-        const int bl = diag_blk(wave, sb), ib = bl < 0 ? 0 : bl >> 2, jb = bl < 0 ? 0 : bl & 3;
+        const int b0 = def ? diag_blk_def(wave, sb) : diag_blk(wave, sb);
+        const int bl = b0, ib = bl < 0 ? 0 : bl >> 2, jb = bl < 0 ? 0 : bl & 3;
         const int b = ib * (ib + 1) / 2 + jb;
 #pragma unroll
         for (int r = 0; r < 4; ++r) c[sb][r] = E.pfc[b * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15)];
@@ -1119,13 +1162,14 @@ __device__ __forceinline__ void late_prepare(const EarlyLds& E, const double* __
     }
 #pragma unroll
     for (int sb = 0; sb < 3; ++sb) {
-        const int bl = diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
+        const int bl = def ? diag_blk_def(wave, sb) : diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
         if (bl < 0) continue;   // wave-uniform
+        if (!def || jb == 0)
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
+            for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-                c[sb] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[sb][kb][kk], fb[sb][kb][kk], c[sb], 0, 0, 0);
+                for (int kk = 0; kk < 4; ++kk)
+                    c[sb] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[sb][kb][kk], fb[sb][kb][kk], c[sb], 0, 0, 0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) diag_put(L, ib * 16 + (lane >> 4) + 4 * r, jb * 16 + (lane & 15), c[sb][r]);
     }
@@ -1580,19 +1624,23 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
 #pragma unroll
                 for (int q = 0; q < 16; ++q) diag_put(L, row, c0 + q, v[q]);
             } else if (pre) {
-                late_prepare(E, Y, L, wave, lane);
+                late_prepare(E, Y, L, wave, lane, true);
             } else {   // W_{d-1} stays in Y after the chain's own factor
-                diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane, d > 1 || smode);
+                diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane, d > 1 || smode, pfx);
             }
             if (t < 6) cnt[t] = 0;   // every read of cnt / ew above is behind a barrier inside
             if (t < 4) ew[t] = 0;    // either prepare
             __syncthreads();
             PNOL_CHOL_STAMP(k, 3)
+            // the owners' deferred -L L^T: K blocks 0..3 after diag_prepare, 2..3 after late_prepare,
+            // none for tile 0 (stored whole)
+            const int kb0 = d == 0 ? 4 : (pre ? 2 : 0);
             if (lookahead)
                 factor_diag<false, true, EarlyNext>(L, rinv, cnt, W + (long)d * NB * NB, d, info, nullptr,
-                                                    EarlyNext{P, ldp, T, d, pw.ver, diag_w11(L), cnt, lookahead, E}, Y);
+                                                    EarlyNext{P, ldp, T, d, pw.ver, diag_w11(L), cnt, lookahead, E}, Y,
+                                                    pfx, kb0);
             else   // micro-panel factor: W_d also stays in Y for the next diag_prepare
-                factor_diag<false, true>(L, rinv, cnt, W + (long)d * NB * NB, d, info, nullptr, NoEarly(), Y);
+                factor_diag<false, true>(L, rinv, cnt, W + (long)d * NB * NB, d, info, nullptr, NoEarly(), Y, pfx, kb0);
             PNOL_CHOL_STAMP(k, 4)
             publish(pw.wdone + d, 1);   // its barrier also ends every read of this step's LDS
             PNOL_CRIT(d, 0)
