@@ -530,31 +530,26 @@ __device__ __forceinline__ void blk_put(double* __restrict__ B, const d4& acc, i
     for (int r = 0; r < 4; ++r) B[((lane >> 4) + 4 * r) * kBP + (lane & 15)] = acc[r];
 }
 
-__host__ __device__ constexpr int own_i(int ow, int b) { return ow == 2 ? (b == 0 ? 1 : 3) : (b == 1 ? 3 : 2); }
-__host__ __device__ constexpr int own_q(int ow, int b) { return ow == 2 ? (b < 2 ? 1 : 3) : (b == 0 ? 1 : 2); }
-// The trailing update by micro-panels 0 and 1, owned by wave OW (2 or 3): blocks (ib, q),
-// 1 <= q <= ib <= 3, three each.  Wave 2: (1,1) (3,1) (3,3); wave 3: (2,1) (3,2) (2,2).  Block
-// (3,3) goes to LDS with the blocks of micro-panel 2; wave 0 applies micro-panel 2's update to
-// it (mp_panel<3>).
+// The trailing update by micro-panels 0 and 1, owned by wave OW (2 or 3), in two phases:
+//   A  the block column 1 -- wave 2: (1,1) (3,1); wave 3: (2,1) -- micro-panel 0 applied four
+//      columns at a time as wave 0 publishes them, then stored to LDS (cnt[OW] = 1: micro-panel
+//      1 may start);
+//   B  (3,3) (wave 2), (3,2) (2,2) (wave 3): micro-panel 0 (final by then), then micro-panel 1
+//      as it is published, stored (cnt[OW] = 2); block (3,3)'s micro-panel 2 update is wave 0's
+//      (mp_panel<3>).
 // Lsrc / kb0 (the persistent chain, Lsrc non-null): the prepare left these blocks without their
 // K blocks kb0 .. 3 of -L L^T (deferred, so the chain's first micro-panel starts after only the
-// block column 0 products); the owner applies them first, from L in the substage layout at Lsrc
+// block column 0 products); each block takes them first, from L in the substage layout at Lsrc
 // -- the same MFMAs in the same order as diag_prepare / late_prepare, so the blocks and W are
 // bitwise unchanged.  kb0 = 4: nothing deferred.
 template <int OW>
 __device__ __forceinline__ void mp_owner(const MpLds& M, int* cnt, int lane, const double* __restrict__ Lsrc, int kb0) {
-    constexpr int NBk = 3;
     const int frow = lane & 15, fk = lane >> 4;
-    d4 acc[NBk];
+    // block (ib, q): its LDS value, then the deferred K blocks of -L L^T
+    auto lld = [&](d4& acc, int ib, int q) {
 #pragma unroll
-    for (int b = 0; b < NBk; ++b)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            acc[b][r] = *mp_s(M, 16 * own_i(OW, b) + (lane >> 4) + 4 * r, 16 * own_q(OW, b) + (lane & 15));
-    if (Lsrc && kb0 < 4) {
-#pragma unroll
-        for (int b = 0; b < NBk; ++b) {
-            const int ib = own_i(OW, b), q = own_q(OW, b);
+        for (int r = 0; r < 4; ++r) acc[r] = *mp_s(M, 16 * ib + (lane >> 4) + 4 * r, 16 * q + (lane & 15));
+        if (Lsrc && kb0 < 4) {
             double fa[4][4], fb[4][4];
 #pragma unroll
             for (int kb = 0; kb < 4; ++kb)
@@ -569,34 +564,53 @@ __device__ __forceinline__ void mp_owner(const MpLds& M, int* cnt, int lane, con
                 if (kb >= kb0)
 #pragma unroll
                     for (int kk = 0; kk < 4; ++kk)
-                        acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[kb][kk], fb[kb][kk], acc[b], 0, 0, 0);
+                        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[kb][kk], fb[kb][kk], acc, 0, 0, 0);
         }
-    }
-    auto panel = [&](auto pc) {
+    };
+    // group g (columns 4g .. 4g+3) of micro-panel P applied to block (ib, q)
+    auto upd = [&](d4& acc, int ib, int q, auto pc, int g) {
         constexpr int P = decltype(pc)::value, LD = mp_ld(P);
         const double* Lp = M.Lc + mp_base(P);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            wait_lds_ge(cnt, kMW * P + 4 * g + 4);
-#pragma unroll
-            for (int b = 0; b < NBk; ++b) {
-                const int ib = own_i(OW, b), q = own_q(OW, b);
-                if (q <= P) continue;   // compile-time after unrolling
-                const double x = -Lp[(4 * g + fk) * LD + 16 * ib - kMW * P + frow];
-                const double y = Lp[(4 * g + fk) * LD + 16 * q - kMW * P + frow];
-                acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc[b], 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int b = 0; b < NBk; ++b)
-            if (own_q(OW, b) == P + 1 || (P == 1 && own_q(OW, b) == 3))
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    *mp_s(M, 16 * own_i(OW, b) + (lane >> 4) + 4 * r, 16 * own_q(OW, b) + (lane & 15)) = acc[b][r];
-        lds_signal(cnt + OW, P + 1);   // in order after the block stores (one wave's LDS ops are ordered)
+        const double x = -Lp[(4 * g + fk) * LD + 16 * ib - kMW * P + frow];
+        const double y = Lp[(4 * g + fk) * LD + 16 * q - kMW * P + frow];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
     };
-    panel(std::integral_constant<int, 0>());
-    panel(std::integral_constant<int, 1>());
+    auto put = [&](const d4& acc, int ib, int q) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) *mp_s(M, 16 * ib + (lane >> 4) + 4 * r, 16 * q + (lane & 15)) = acc[r];
+    };
+    constexpr int NA = OW == 2 ? 2 : 1;
+    const int ia[2] = {OW == 2 ? 1 : 2, 3};
+    d4 a[NA];
+#pragma unroll
+    for (int b = 0; b < NA; ++b) lld(a[b], ia[b], 1);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        wait_lds_ge(cnt, 4 * g + 4);
+#pragma unroll
+        for (int b = 0; b < NA; ++b) upd(a[b], ia[b], 1, std::integral_constant<int, 0>(), g);
+    }
+#pragma unroll
+    for (int b = 0; b < NA; ++b) put(a[b], ia[b], 1);
+    lds_signal(cnt + OW, 1);   // in order after the block stores (one wave's LDS ops are ordered)
+    constexpr int NB2 = OW == 2 ? 1 : 2;
+    const int ibb[2] = {3, OW == 2 ? 3 : 2}, qb[2] = {OW == 2 ? 3 : 2, 2};
+    d4 c[NB2];
+#pragma unroll
+    for (int b = 0; b < NB2; ++b) lld(c[b], ibb[b], qb[b]);
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int b = 0; b < NB2; ++b) upd(c[b], ibb[b], qb[b], std::integral_constant<int, 0>(), g);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        wait_lds_ge(cnt, kMW + 4 * g + 4);
+#pragma unroll
+        for (int b = 0; b < NB2; ++b) upd(c[b], ibb[b], qb[b], std::integral_constant<int, 1>(), g);
+    }
+#pragma unroll
+    for (int b = 0; b < NB2; ++b) put(c[b], ibb[b], qb[b]);
+    lds_signal(cnt + OW, 2);
 }
 
 // V_P = L_PP^{-1} (wave 1, lane j = column j; lanes >= 16 compute zeros) into W block (P, P)
