@@ -2058,10 +2058,12 @@ int launch_chol_solve_v(pnol_ctx* ctx, const double* A, int lda, const double* r
 // P's padding (identity on the diagonal past n, as the copy of A gives), info = 0.
 __global__ __launch_bounds__(256) void k_chol_reducing_prep(double* __restrict__ P, long ldp, int T, int n,
                                                             double* __restrict__ bv, int* __restrict__ pflags,
-                                                            int npflags, int* __restrict__ info, int vinit) {
+                                                            int npflags, int* __restrict__ info, int vinit,
+                                                            int* __restrict__ zc, int nz) {
     const int N = T * NB, tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
     const int b0 = 2 * T, v1 = 3 * T + T * T;   // [bcnt | ver]
     for (int q = tid; q < npflags; q += nth) pflags[q] = (q >= b0 && q < v1) ? vinit : 0;
+    for (int q = tid; q < nz; q += nth) zc[q] = 0;   // the caller's counters (k_syrk_red's tile counts)
     for (int r = n + tid; r < N; r += nth) bv[r] = 0.0;
     if (n < N) {
         const long pad = (long)(N - n) * N + (long)n * (N - n);   // rows >= n, then columns >= n of rows < n
@@ -2088,12 +2090,13 @@ int launch_chol_reducing_prep(pnol_ctx* ctx, int n, int* dinfo, CholRed& cr) {
     return chol_ws(ctx, n, true, cr.w);
 }
 
-int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr, bool preloaded) {
+int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr, bool preloaded, int* zc, int nz) {
     const CholWs& w = cr.w;
     const int n = cr.n;
     const long pad = (long)(w.N - n) * w.N + (long)n * (w.N - n), work = std::max<long>(pad, w.npf);
     hipLaunchKernelGGL(k_chol_reducing_prep, dim3((unsigned)std::max<long>(1, std::min<long>(1024, (work + 255) / 256))),
-                       dim3(256), 0, ctx->stream, w.P, w.ldp, w.T, n, w.bv, w.pf, w.npf, cr.dinfo, preloaded ? 0 : -1);
+                       dim3(256), 0, ctx->stream, w.P, w.ldp, w.T, n, w.bv, w.pf, w.npf, cr.dinfo, preloaded ? 0 : -1,
+                       zc, zc ? nz : 0);
     return launch_check();
 }
 

@@ -123,19 +123,23 @@ __device__ unsigned long long g_syrk_tl[3 * 65536];
 // accumulators per wave, so twice the waves per SIMD hide the stage boundaries).
 // a partial store: non-temporal, or (NTS false) a plain store that may stay in the caches for the
 // reduce that reads it next
-template <bool NTS>
+template <bool NTS, bool SC1 = false>
 __device__ __forceinline__ void part_store(double v, double* p) {
-    if constexpr (NTS) __builtin_nontemporal_store(v, p);
+    if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // write-through
+    else if constexpr (NTS) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 
-template <int MODE, int TILE, int NW = 4, bool NTS = true>
-__global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
-                                                      int split_k, int kfirst, int kchunk, int sub, int slice0,
-                                                      int mS, long sstride, double* __restrict__ part, int tile0) {
+// The tile body (k_syrk_tile, and k_syrk_red's SYRK workgroups): workgroup bid of nblk, its
+// LDS (lds[buf][P/Q]) passed in; returns the lower-triangle tile index it formed a partial of.
+// SC1: the partial stores write through (k_syrk_red's reduce workgroups read them in-launch).
+template <int MODE, int TILE, int NW = 4, bool NTS = true, bool SC1 = false>
+__device__ __forceinline__ int syrk_tile_body(const double* __restrict__ X, long ldx, int nr, int K, int split_k,
+                                              int kfirst, int kchunk, int sub, int slice0, int mS, long sstride,
+                                              double* __restrict__ part, int tile0, int bid, int nblk,
+                                              double (&lds)[2][2][TILE * kPad]) {
     constexpr int NT = 64 * NW, WC = NW / 2;
     constexpr int WTM = TILE / 2, WTN = TILE / WC, NBM = WTM / 16, NBN = WTN / 16;
-    __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
 #ifdef PNOL_SYRK_TIMELINE
     const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -143,8 +147,8 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
     // chunks fill the last dispatch round instead of leaving it part-empty
     int blk, t, sidx;
     {
-        const int ntl = gridDim.x / split_k, nsl = split_k / sub;
-        const int u0 = blockIdx.x / (ntl * nsl), rest = blockIdx.x % (ntl * nsl);
+        const int ntl = nblk / split_k, nsl = split_k / sub;
+        const int u0 = bid / (ntl * nsl), rest = bid % (ntl * nsl);
         const int tl = rest / nsl;
         sidx = (rest % nsl) * sub + u0;
         blk = tl * split_k + sidx;           // partial slot (local to this launch)
@@ -292,7 +296,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                 if (q < 4 || dcnt == 5)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        part_store<NTS>(acc[q >> 1][q & 1][r], out + (dbi[q] * 16 + orow + 4 * r) * ld + dbj[q] * 16 + ocol);
+                        part_store<NTS, SC1>(acc[q >> 1][q & 1][r], out + (dbi[q] * 16 + orow + 4 * r) * ld + dbj[q] * 16 + ocol);
             // upper block u = bj (bj - 1) / 2 + bi (bi < bj): blocks wave, wave + 8, ... of the 28
             for (int u = __builtin_amdgcn_readfirstlane(wave); u < 28; u += NW) {
                 int bj = 1;
@@ -300,7 +304,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                 const int bi = u - bj * (bj - 1) / 2;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    part_store<NTS>(0.0, out + (bi * 16 + orow + 4 * r) * ld + bj * 16 + ocol);
+                    part_store<NTS, SC1>(0.0, out + (bi * 16 + orow + 4 * r) * ld + bj * 16 + ocol);
             }
         } else {
 #pragma unroll
@@ -311,7 +315,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
                     for (int r = 0; r < 4; ++r) {
                         int row = wr * WTM + mi * 16 + orow + 4 * r;
                         int col = wc * WTN + ni * 16 + ocol;
-                        part_store<NTS>(acc[mi][ni][r], out + row * ld + col);
+                        part_store<NTS, SC1>(acc[mi][ni][r], out + row * ld + col);
                     }
         }
     }
@@ -320,11 +324,21 @@ __global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restri
         const unsigned long long tl1 = __builtin_amdgcn_s_memrealtime();
         const unsigned hw = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));     // HW_ID
         const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11));    // XCC_ID
-        g_syrk_tl[3 * blockIdx.x] = tl0;
-        g_syrk_tl[3 * blockIdx.x + 1] = tl1;
-        g_syrk_tl[3 * blockIdx.x + 2] = ((unsigned long long)xcc << 32) | hw;
+        g_syrk_tl[3 * bid] = tl0;
+        g_syrk_tl[3 * bid + 1] = tl1;
+        g_syrk_tl[3 * bid + 2] = ((unsigned long long)xcc << 32) | hw;
     }
 #endif
+    return t;
+}
+
+template <int MODE, int TILE, int NW = 4, bool NTS = true>
+__global__ __launch_bounds__(64 * NW, 2) void k_syrk_tile(const double* __restrict__ X, long ldx, int nr, int K,
+                                                      int split_k, int kfirst, int kchunk, int sub, int slice0,
+                                                      int mS, long sstride, double* __restrict__ part, int tile0) {
+    __shared__ __attribute__((aligned(16))) double lds[2][2][TILE * kPad];   // [buf][P/Q]
+    (void)syrk_tile_body<MODE, TILE, NW, NTS>(X, ldx, nr, K, split_k, kfirst, kchunk, sub, slice0, mS, sstride, part,
+                                              tile0, blockIdx.x, gridDim.x, lds);
 }
 
 // ---- the m-slice summation tree ------------------------------------------------------------
@@ -459,15 +473,16 @@ __global__ void k_syrk_unpack(const double* __restrict__ packed, int ntiles, int
 // jp / rhs (nullable): one more row of blocks (blockIdx.y == ntiles) forms rhs = the slice
 // tree of the 8 -J^T F slice partials jp[s * n + e], exactly as k_tree_nodes over all slices does
 // (leaf = 0.0 + partial, then tree8): the tree rides in this launch instead of its own.
-template <int SUB, int SR = 32>
-__global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ part, int ntiles, int sub_rt, int n,
-                                                     double lambda, double* __restrict__ A, long lda,
-                                                     double* __restrict__ diag_out, int tile0,
-                                                     const double* __restrict__ jp = nullptr,
-                                                     double* __restrict__ rhs = nullptr,
-                                                     double* __restrict__ rhs2 = nullptr) {
-    if (jp && (int)blockIdx.y == ntiles) {
-        for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+// (the body: workgroup (bx, by) of nbx x .., NT threads, the strip staging st[SR][kTile + 1]
+// passed in -- k_syrk_reduce, and k_syrk_red's reduce workgroups)
+template <int SUB, int SR, int NT>
+__device__ __forceinline__ void syrk_reduce_body(const double* __restrict__ part, int ntiles, int sub_rt, int n,
+                                                 double lambda, double* __restrict__ A, long lda,
+                                                 double* __restrict__ diag_out, int tile0, const double* __restrict__ jp,
+                                                 double* __restrict__ rhs, double* __restrict__ rhs2, int bx, int by,
+                                                 int nbx, double (*st)[kTile + 1]) {
+    if (jp && by == ntiles) {
+        for (int e = bx * NT + (int)threadIdx.x; e < n; e += nbx * NT) {
             double l[kS];
 #pragma unroll
             for (int s = 0; s < kS; ++s) l[s] = 0.0 + jp[(long)s * n + e];
@@ -478,17 +493,16 @@ __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ 
         return;
     }
     const int sub = SUB > 0 ? SUB : sub_rt;                // SR: strip rows
-    __shared__ double st[SR][kTile + 1];
-    const int t = tile0 + blockIdx.y;                      // part holds this launch's tiles from tile0 on
+    const int t = tile0 + by;                              // part holds this launch's tiles from tile0 on
     int ti, tj;
     tile_of(t, ti, tj);
     const double scale = 1 + lambda;
-    const int r0 = blockIdx.x * SR;
+    const int r0 = bx * SR;
     const long E = kTile * kTile;
     const double* p = part + ((long)(t - tile0) * kS * sub) * E + (long)r0 * kTile;
     // 32 x 128 doubles = 2048 double2; 256 threads x 8
 #pragma unroll 2
-    for (int q = threadIdx.x; q < SR * kTile / 2; q += 256) {
+    for (int q = threadIdx.x; q < SR * kTile / 2; q += NT) {
         const int r = (2 * q) / kTile, c = (2 * q) % kTile;
         double lx[kS], ly[kS];
 #pragma unroll
@@ -521,12 +535,88 @@ __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ 
     }
     __syncthreads();
     // mirror: A[j][i] = tile[i][j] for j > i; row j of A gets 32 consecutive columns i
-    for (int q = threadIdx.x; q < SR * kTile; q += 256) {
+    for (int q = threadIdx.x; q < SR * kTile; q += NT) {
         const int c = q / SR, r = q % SR;                  // consecutive threads: consecutive i
         const int i = ti * kTile + r0 + r, j = tj * kTile + c;
         if (i < n && j < n && j < i) A[(long)j * lda + i] = st[r][c];
     }
 }
+
+template <int SUB, int SR = 32>
+__global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ part, int ntiles, int sub_rt, int n,
+                                                     double lambda, double* __restrict__ A, long lda,
+                                                     double* __restrict__ diag_out, int tile0,
+                                                     const double* __restrict__ jp = nullptr,
+                                                     double* __restrict__ rhs = nullptr,
+                                                     double* __restrict__ rhs2 = nullptr) {
+    __shared__ double st[SR][kTile + 1];
+    syrk_reduce_body<SUB, SR, 256>(part, ntiles, sub_rt, n, lambda, A, lda, diag_out, tile0, jp, rhs, rhs2, blockIdx.x,
+                                   blockIdx.y, gridDim.x, st);
+}
+
+// The one-GPU LM trip's J^T J split-K partials AND their reduce in one launch (k_syrk_red):
+// workgroups [0, nsyrk) are k_syrk_tile<0, 128, 8>'s; each, after its partial, publishes it by
+// the in-launch split-K hand-off (MI355X guide, cdna_hip_programming.md "In-launch split-K
+// reduction": plain stores, every wave's vmcnt(0), the barrier, lane 0's agent release and
+// vmcnt(0), then a relaxed agent add to its tile's counter -- or, SC1, write-through partial
+// stores and no release).  Workgroups [nsyrk, ..) are k_syrk_reduce's (32-row strips, the extra
+// row of blocks forming -J^T F): lane 0 polls its tile's counter (relaxed) until all split_k
+// partials are in, then one agent acquire, vmcnt(0) and the barrier, then plain loads.  The
+// reduce workgroups come after every SYRK workgroup in the grid, so they take the slots of the
+// SYRK's last dispatch round as it drains (nothing a SYRK workgroup does waits on them); a poll
+// past its cap sets info = kCholTimeout and gives up (the trip then redoes the solve from A formed
+// from the partials).  Every value is the sum k_syrk_reduce forms: bitwise the two launches.
+constexpr int kRedSR = 32, kRedSpin = 1 << 22;
+template <int SUB, bool SC1>
+__global__ __launch_bounds__(512, 2) void k_syrk_red(const double* __restrict__ X, long ldx, int nr, int K,
+                                                     int split_k, int kfirst, int kchunk, int sub, int mS, long sstride,
+                                                     double* __restrict__ part, int nsyrk, int* __restrict__ tcnt,
+                                                     int ntiles, int n, double lambda, double* __restrict__ A, long lda,
+                                                     const double* __restrict__ jp, double* __restrict__ rhs,
+                                                     double* __restrict__ rhs2, int* __restrict__ info) {
+    __shared__ __attribute__((aligned(16))) double lds[2][2][kTile * kPad];
+    __shared__ int ok_sh;
+    const int b = blockIdx.x;
+    if (b < nsyrk) {
+        const int t = syrk_tile_body<0, kTile, 8, false, SC1>(X, ldx, nr, K, split_k, kfirst, kchunk, sub, 0, mS, sstride,
+                                                             part, 0, b, nsyrk, lds);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if constexpr (!SC1) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __hip_atomic_fetch_add(tcnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    constexpr int NBX = kTile / kRedSR;
+    const int r = b - nsyrk, bx = r % NBX, by = r / NBX;
+    if (by < ntiles) {
+        if (threadIdx.x == 0) {
+            int it = 0, ok = 1;
+            while (__hip_atomic_load(tcnt + by, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < split_k) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++it > kRedSpin) {
+                    ok = 0;
+                    atomicCAS(info, 0, kCholTimeout);
+                    break;
+                }
+            }
+            if (ok) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            ok_sh = ok;
+        }
+        __syncthreads();
+        if (!ok_sh) return;
+    }
+    double(*st)[kTile + 1] = reinterpret_cast<double(*)[kTile + 1]>(&lds[0][0][0]);
+    syrk_reduce_body<SUB, kRedSR, 512>(part, ntiles, sub, n, lambda, A, lda, nullptr, 0, jp, rhs, rhs2, bx, by, NBX, st);
+}
+static_assert(kRedSR * (kTile + 1) <= 2 * 2 * kTile * kPad, "the reduce strip fits the SYRK's LDS");
 
 // reference order: JTJ_ij = sum_k JT_ik * JT_jk (k ascending, from 0.0); A_ii = (1+lambda) JTJ_ii
 __global__ void k_jtj_seq(const double* __restrict__ JT, long ldjt, int m, int n, double lambda,
@@ -806,6 +896,10 @@ int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
     // read per call)
     const char* er = std::getenv("PNOL_LM_REDUCE");
     const bool tasks = er && std::strcmp(er, "tasks") == 0;
+    // PNOL_LM_REDUCE=tail: the reduce workgroups in the SYRK's own launch (k_syrk_red), taking
+    // the slots of its last dispatch round; PNOL_SYRK_RED_SC1=1: write-through partials, no
+    // release fence (read per call)
+    const bool tail = er && std::strcmp(er, "tail") == 0 && !syrk_t64(false);
     // every workspace first: a (re)allocation frees, and a free waits for the device
     void *part = nullptr, *jp = nullptr;
     ctx->lm_trip_tiles.kind = 0;   // the trip's tiles are overwritten below
@@ -815,7 +909,34 @@ int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
     PNOL_CHECK(launch_chol_reducing_prep(ctx, n, dinfo, cr));
     PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
     PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F0));
-    PNOL_CHECK(launch_chol_reducing_start(ctx, cr, !tasks));   // the prep launch (words, paddings, info)
+    void* tcnt = nullptr;
+    if (tail) PNOL_CHECK(ws_get(ctx, "syrk_tcnt", sizeof(int) * (size_t)ntiles, &tcnt));
+    // the prep launch (words, paddings, info; the tile counters)
+    PNOL_CHECK(launch_chol_reducing_start(ctx, cr, !tasks, (int*)tcnt, ntiles));
+    if (tail) {
+        const int nsyrk = ntiles * split, nred = (kTile / kRedSR) * (ntiles + 1);
+        const char* es = std::getenv("PNOL_SYRK_RED_SC1");
+        const bool sc1 = es && std::atoi(es) != 0;
+        {
+            LaunchTimer tm(ctx, "syrk");
+#define PNOL_RED(SB, SC)                                                                                              \
+    hipExtLaunchKernelGGL((k_syrk_red<SB, SC>), dim3(nsyrk + nred), dim3(512), 0, ctx->stream, tm.start(), tm.stop(), 0, \
+                          JT, (long)ldjt, n, m, split, sc.kfirst, sc.kchunk, sc.sub, sc.mS, (long)sc.mS, (double*)part,   \
+                          nsyrk, (int*)tcnt, ntiles, n, lambda, cr.w.P, cr.w.ldp, (const double*)jp, rhs, cr.w.bv,       \
+                          cr.dinfo)
+            if (sc.sub == 2) {
+                if (sc1) PNOL_RED(2, true); else PNOL_RED(2, false);
+            } else {
+                if (sc1) PNOL_RED(0, true); else PNOL_RED(0, false);
+            }
+#undef PNOL_RED
+        }
+        PNOL_CHECK(launch_check());
+        ScopedTimer tm(ctx, "solve");
+        PNOL_CHECK(launch_chol_preloaded_run(ctx, ctx->stream, cr, sigma, x, xnext));
+        ctx->lm_trip_tiles = {1, m, n, 1};
+        return PNOL_OK;
+    }
     syrk_partials(ctx, ctx->stream, false, JT, ldjt, sc.mS, n, m, sc, 0, kS, 0, ntiles, (double*)part,
                   syrk_t64(false));
     PNOL_CHECK(launch_check());

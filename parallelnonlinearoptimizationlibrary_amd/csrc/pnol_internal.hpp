@@ -251,7 +251,8 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
 int launch_chol_reducing_prep(pnol_ctx* ctx, int n, int* dinfo, CholRed& cr);
 // preloaded: the matrix and b will be in P / bv before the persistent launch (every version and
 // b word starts at 0; launch_chol_preloaded_run), else the reduce tasks store them (words at -1)
-int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr, bool preloaded = false);
+// zc / nz: int counters the prep launch also zeroes (k_syrk_red's per-tile partial counts)
+int launch_chol_reducing_start(pnol_ctx* ctx, const CholRed& cr, bool preloaded = false, int* zc = nullptr, int nz = 0);
 int launch_chol_preloaded_run(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, double* sigma, const double* xbase,
                               double* xnext);
 int launch_chol_reducing_run(pnol_ctx* ctx, hipStream_t st, const CholRed& cr, const double* part, int sub,

@@ -705,18 +705,21 @@ def test_fd_normal_bitwise(ctx, m, n):
         assert np.array_equal(_np(rb), _np(ra)), rep
 
 
-@pytest.mark.parametrize("reduce", ["launch", "tasks"])
+@pytest.mark.parametrize("reduce", ["launch", "tasks", "tail", "tail_sc1"])
 @pytest.mark.parametrize("m,n", [(16384, 2048), (5000, 1000), (777, 129), (3000, 257), (2000, 700), (512, 96)])
 def test_lm_trip_bitwise(ctx, monkeypatch, m, n, reduce):
     """The LM trip without A (pnol_lm_trip_d: the reduce launch writes the J^T J split-K partials'
     sums straight into the persistent Cholesky's padded matrix and -J^T F into b -- or, reduce =
-    tasks, the persistent launch's first tasks do that reduce) gives JT, F0, rhs, sigma, x + sigma
+    tasks, the persistent launch's first tasks do that reduce; tail, the reduce workgroups ride in
+    the SYRK's own launch behind an in-launch split-K hand-off, _sc1 with write-through partials)
+    gives JT, F0, rhs, sigma, x + sigma
     and the solve status bitwise those of pnol_fd_normal_d + pnol_solve_step_d, over repeated trips
     at new points and lambdas; the A the LU fallback forms from the trip's partials
     (pnol_lm_trip_normal_d) is bitwise pnol_fd_normal_d's A."""
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
-    monkeypatch.setenv("PNOL_LM_REDUCE", reduce)
+    monkeypatch.setenv("PNOL_LM_REDUCE", reduce.replace("_sc1", ""))
+    monkeypatch.setenv("PNOL_SYRK_RED_SC1", "1" if reduce.endswith("_sc1") else "0")
     d = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
     h = ctx.tensor(np.full(n, 1e-7))
     JTa, Aa, ra, JTb = ctx.empty(n, m), ctx.empty(n, n), ctx.empty(n), ctx.empty(n, m)

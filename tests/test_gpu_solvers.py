@@ -569,7 +569,8 @@ def test_lm_one_wait_loop_lu_fallback_equals_general_loop(ctx, oracle, m, n, mon
 
 @pytest.mark.parametrize("m,n,force,reduce", [(3000, 257, "0", "launch"), (2000, 700, "0", "launch"),
                                               (3000, 257, "1", "launch"), (2000, 700, "0", "tasks"),
-                                              (3000, 257, "1", "tasks")])
+                                              (3000, 257, "1", "tasks"), (2000, 700, "0", "tail"),
+                                              (3000, 257, "1", "tail")])
 def test_lm_fused_trip_loop_equals_general_loop(ctx, oracle, m, n, force, reduce, monkeypatch):
     """The one-wait LM loop with the fused trip (pnol_lm_trip_d, the default; its reduce as a
     launch into the Cholesky's matrix, or as the persistent launch's first tasks) replays the
