@@ -682,7 +682,10 @@ def main():
         pmc = pmc_traffic()
         one_gpu = world == 1
         roofline = {
-            "kernel": ("k_syrk_tile<0,128,8 waves> (J^T J, fp64 MFMA v_mfma_f64_16x16x4_f64)" if one_gpu else
+            "kernel": (("k_syrk_red<2> (J^T J split-K partials on fp64 MFMA v_mfma_f64_16x16x4_f64, 8 waves per "
+                        "128 x 128 tile, with their reduce into the Cholesky's matrix in the same launch)"
+                        if os.environ.get("PNOL_LM_REDUCE", "tail") == "tail" else
+                        "k_syrk_tile<0,128,8 waves> (J^T J, fp64 MFMA v_mfma_f64_16x16x4_f64)") if one_gpu else
                        "k_syrk_tile<4,64> on this rank's m-slices (J^T J share, fp64 MFMA v_mfma_f64_16x16x4_f64)"),
             "bound": "mfma", "achieved": jtj_flop / (syrk_ms * 1e-3) / 1e12 if syrk_ms else None,
             "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -690,12 +693,13 @@ def main():
             # one GPU: the PMC passes of this bench; N > 1: the PMC passes of the sliced kernel over
             # all 8 m-slices in one process (tools/syrk_sliced_probe.py, the metric's m and n), times
             # this rank's rows / m; other sizes have no committed pass (null)
-            "traffic": (pmc.get("k_syrk_tile<0, 128>", {}).get("traffic_bytes_per_launch") if one_gpu else
+            "traffic": ((pmc.get("k_syrk_red", {}) or pmc.get("k_syrk_tile<0, 128>", {})).get("traffic_bytes_per_launch")
+                        if one_gpu else
                         (pmc["k_syrk_tile<4, 64>"]["traffic_bytes_per_launch"] * jtj_rows / m
                          if (m, n) == (M_RES, N_PAR) and "traffic_bytes_per_launch" in pmc.get("k_syrk_tile<4, 64>", {})
                          else None)),
             "mfma_busy_pmc": next((v.get("mfma_busy_frac") for k, v in pmc_valu("syrk_mfma").items()
-                                   if "k_syrk_tile" in k), None) if one_gpu else None,
+                                   if "k_syrk_red" in k or "k_syrk_tile" in k), None) if one_gpu else None,
         }
         roofline["frac"] = roofline["achieved"] / FP64_PEAK_TFLOPS if roofline["achieved"] else None
         fd_ms = per["fd_jacobian"]

@@ -891,15 +891,15 @@ int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
     const int ntiles = nt * (nt + 1) / 2;
     const SliceCfg sc = slice_cfg(m, ntiles);
     const int split = kS * sc.sub;
-    // the reduce: a launch of its own over the whole chip writing the Cholesky's padded matrix
-    // and b directly (default), or the persistent launch's first tasks (PNOL_LM_REDUCE=tasks;
-    // read per call)
+    // the reduce (PNOL_LM_REDUCE, read per call): "tail" (default) its workgroups in the SYRK's
+    // own launch (k_syrk_red), taking the slots of the SYRK's last dispatch round -- 3 of 3
+    // same-box bench pairs faster than "launch", a reduce launch of its own writing the
+    // Cholesky's padded matrix and b (1.18-1.20 ms for both against 1.14-1.16 + 0.07); "tasks":
+    // the persistent launch's first tasks (round 4).  PNOL_SYRK_RED_SC1=1: write-through partials
+    // and no release fence in the tail form (the same speed).
     const char* er = std::getenv("PNOL_LM_REDUCE");
     const bool tasks = er && std::strcmp(er, "tasks") == 0;
-    // PNOL_LM_REDUCE=tail: the reduce workgroups in the SYRK's own launch (k_syrk_red), taking
-    // the slots of its last dispatch round; PNOL_SYRK_RED_SC1=1: write-through partials, no
-    // release fence (read per call)
-    const bool tail = er && std::strcmp(er, "tail") == 0 && !syrk_t64(false);
+    const bool tail = (!er || std::strcmp(er, "tail") == 0) && !syrk_t64(false);
     // every workspace first: a (re)allocation frees, and a free waits for the device
     void *part = nullptr, *jp = nullptr;
     ctx->lm_trip_tiles.kind = 0;   // the trip's tiles are overwritten below

@@ -15,7 +15,7 @@ run pmc_valu rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -
 run pmc_csq rocprofv3 --pmc $SQ -d /tmp/c_sq_t -o pmc --output-format csv -- python3 $B --no-hg &&
 run pmc_cmf rocprofv3 --pmc $MF -d /tmp/c_mf_t -o pmc --output-format csv -- python3 $B --no-hg || exit 1
 python3 tools/pmc_traffic.py /tmp/pmc_fetch /tmp/pmc_write gpurun_out/r05_pmc_traffic.json &&
-python3 tools/pmc_valu.py /tmp/pmc_mfma gpurun_out/r05_pmc_syrk_mfma.json k_syrk_tile &&
+python3 tools/pmc_valu.py /tmp/pmc_mfma gpurun_out/r05_pmc_syrk_mfma.json k_syrk_red k_syrk_tile &&
 python3 tools/pmc_valu.py /tmp/pmc_valu gpurun_out/r05_pmc_fd_valu.json k_linres_fdP k_linres_evalP &&
 python3 tools/pmc_valu.py /tmp/c_sq_t gpurun_out/r05_pmc_chol_trip_sq.json k_chol_persist k_chol_bwd &&
 python3 tools/pmc_valu.py /tmp/c_mf_t gpurun_out/r05_pmc_chol_trip_mfma.json k_chol_persist k_chol_bwd

@@ -29,7 +29,7 @@ def load(dirname, counter):
 
 
 def short(name):
-    for key in ("k_syrk_tile<0, 128", "k_syrk_tile<1, 64", "k_syrk_tile<4, 64", "k_linres_fdP", "k_linres_evalP", "k_linres_fd2",
+    for key in ("k_syrk_red", "k_syrk_tile<0, 128", "k_syrk_tile<1, 64", "k_syrk_tile<4, 64", "k_linres_fdP", "k_linres_evalP", "k_linres_fd2",
                 "k_linres_fd", "k_linres_eval",
                 "k_gemv_neg_wg<2, true>", "k_gemv_neg<2>", "k_gemv_neg<1>", "k_bfgs_pass<", "k_trsv_fwd", "k_trsv_bwd",
                 "k_potrf_diag", "k_trsm_panel", "k_syrk_reduce", "k_chol_dag", "k_chol_persist", "k_chol_bwd",
