@@ -367,13 +367,41 @@ def test_cholesky_lookahead_equals_plain_chain(ctx, monkeypatch, n):
     s_off, i_off = ctx.solve(At, bt, method=5)
     monkeypatch.setenv("PNOL_CHOL_LOOKAHEAD", "52")   # gives up when late: mixed steps
     s_mix, i_mix = ctx.solve(At, bt, method=5)
-    monkeypatch.delenv("PNOL_CHOL_LOOKAHEAD")           # default: every step
+    monkeypatch.setenv("PNOL_CHOL_LOOKAHEAD", "1000")   # waits for the tiles: every step
     s_on, i_on = ctx.solve(At, bt, method=5)
+    monkeypatch.delenv("PNOL_CHOL_LOOKAHEAD")           # default (48)
+    s_def, i_def = ctx.solve(At, bt, method=5)
     s4, i4 = ctx.solve(At, bt, method=4)
-    assert i_off == i_mix == i_on == i4 == 1
+    assert i_off == i_mix == i_on == i_def == i4 == 1
     assert np.array_equal(_np(s_on), _np(s_off))
     assert np.array_equal(_np(s_mix), _np(s_off))
+    assert np.array_equal(_np(s_def), _np(s_off))
     assert np.array_equal(_np(s_on), _np(s4))
+
+
+@pytest.mark.parametrize("n", [100, 130, 700, 2048, 2111])
+def test_cholesky_bwd_pairs_equal_single_rows(ctx, monkeypatch, n):
+    """The backward solve with two block rows per workgroup (k_chol_bwd2: x_w1's hand-off to w0 in
+    LDS) is the same arithmetic in the same order as one block row per workgroup
+    (PNOL_BWD_PAIRS=0): sigma and the trial point bitwise equal, for even and odd tile counts."""
+    rng = np.random.default_rng(n + 11)
+    J = rng.standard_normal((n + 64, n))
+    A = J.T @ J + 0.25 * np.eye(n)
+    At, bt, xt = ctx.tensor(A), ctx.tensor(rng.standard_normal(n)), ctx.tensor(rng.standard_normal(n))
+    out = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("PNOL_BWD_PAIRS", v)
+        for meth in (4, 5):
+            s, i = ctx.solve(At, bt, method=meth)
+            assert i == 1
+            out[(v, meth)] = _np(s)
+        sg, xn, info = ctx.solve_step(At, bt, xt)
+        assert info == 0
+        out[(v, "step")] = (_np(sg), _np(xn))
+    for k in (4, 5):
+        assert np.array_equal(out[("0", k)], out[("1", k)])
+    assert np.array_equal(out[("0", "step")][0], out[("1", "step")][0])
+    assert np.array_equal(out[("0", "step")][1], out[("1", "step")][1])
 
 
 def test_cholesky_bwd_granules_equal_flag_form(ctx, monkeypatch):
