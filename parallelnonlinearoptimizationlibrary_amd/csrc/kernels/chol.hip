@@ -1902,132 +1902,6 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm,
     }
 }
 
-// The granule form with two block rows per workgroup (the default): workgroup b owns blocks
-// w1 = T-1-2b and w0 = w1-1 (w0 < 0: w1 alone).  Both accumulate L_cw^T x_c as each x_c
-// arrives; x_w1 is formed and published, then w0 takes its last term (c = w1) from x_w1 in LDS
-// instead of a memory hop: half the hops of k_chol_bwd on the chain.  Every x_w is the same
-// arithmetic in the same order as k_chol_bwd's (the c = w1 term last, the same 16-term fma
-// chains and partial sums), so sigma is bitwise unchanged.
-__global__ __launch_bounds__(256) void k_chol_bwd2(const double* __restrict__ Lm, long ldp, int T, int n,
-                                                   const double* __restrict__ W, const double* __restrict__ bv,
-                                                   const double* __restrict__ zv, double* xw, double* __restrict__ x,
-                                                   int epoch, int* info, const double* __restrict__ xbase,
-                                                   double* __restrict__ xnext) {
-    __shared__ double part[4][NB];
-    __shared__ double vsh[NB];
-    __shared__ double xl[NB];
-    if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
-    const int t = threadIdx.x, j = t & 63, q = t >> 6;
-    const int w1 = T - 1 - 2 * (int)blockIdx.x, w0 = w1 - 1;
-    const bool two = w0 >= 0;
-    double z1 = 0.0, z0 = 0.0;
-    if (t < NB) {
-        if (w1 == T - 1) {
-            const double* Wl = W + (long)w1 * NB * NB;
-            double s = 0.0;
-#pragma unroll 16
-            for (int c = 0; c < NB; ++c) s = fma(Wl[t * NB + c], bv[w1 * NB + c], s);
-            z1 = s;
-        } else {
-            z1 = zv[w1 * NB + t];
-        }
-        if (two) z0 = zv[w0 * NB + t];
-    }
-    auto load_blk = [&](double (&dst)[16], int c, int w) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dst[r] = Lm[(long)(c * NB + q * 16 + r) * ldp + w * NB + j];
-    };
-    double L1[16], L1n[16], L0[16], L0n[16], Lw[16];
-    if (w1 + 1 < T) {
-        load_blk(L1, T - 1, w1);
-        if (two) load_blk(L0, T - 1, w0);
-    }
-    if (two) load_blk(Lw, w1, w0);   // w0's last term, L_{w1, w0}
-    double wr1[16], wr0[16];          // the W columns j, rows q*16 .. +16
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        wr1[r] = W[(long)w1 * NB * NB + (q * 16 + r) * NB + j];
-        wr0[r] = two ? W[(long)w0 * NB * NB + (q * 16 + r) * NB + j] : 0.0;
-    }
-    const double ep = (double)epoch;
-    double acc1 = 0.0, acc0 = 0.0;
-    for (int c = T - 1; c > w1; --c) {
-        if (c - 1 > w1) {
-            load_blk(L1n, c - 1, w1);
-            if (two) load_blk(L0n, c - 1, w0);
-        }
-        // lanes 0..15 of wave q poll the granules of x_c[q*16 .. q*16+15]
-        double* g = xw + 2 * ((long)c * NB + q * 16);   // wave-uniform
-        double v = 0.0;
-        int it = 0;
-        for (;;) {
-            const double2 gv = j < 16 ? ld16_sc1(g, (unsigned)(j * 16)) : make_double2(0.0, ep);
-            if (__all(gv.y == ep)) {
-                v = gv.x;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            if ((++it & 63) == 0) {
-                if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
-                if (it > kSpin) {
-                    atomicCAS(info, 0, kInfoTimeout);
-                    return;
-                }
-            }
-        }
-        double xr[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) xr[r] = readlane_d(v, r);
-        double s1 = 0.0;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s1 = fma(L1[r], xr[r], s1);
-        acc1 += s1;
-        if (two) {
-            double s0 = 0.0;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) s0 = fma(L0[r], xr[r], s0);
-            acc0 += s0;
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            L1[r] = L1n[r];
-            L0[r] = L0n[r];
-        }
-    }
-    // x_w = W_w^T (z_w - acc): the four waves' partial sums in the fixed order
-    auto finish = [&](double acc, double zj, const double (&wr)[16], int w) -> double {
-        part[q][j] = acc;
-        __syncthreads();
-        if (t < NB) vsh[t] = zj - ((part[0][t] + part[1][t]) + (part[2][t] + part[3][t]));
-        __syncthreads();
-        double s = 0.0;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s = fma(wr[r], vsh[q * 16 + r], s);
-        part[q][j] = s;
-        __syncthreads();
-        double xv = 0.0;
-        if (t < NB) {   // wave 0 alone stores x_w
-            xv = (part[0][t] + part[1][t]) + (part[2][t] + part[3][t]);
-            st16_sc1(xw + 2 * (long)w * NB, (unsigned)(t * 16), make_double2(xv, ep));
-            if (w * NB + t < n) {
-                x[w * NB + t] = xv;
-                // the LM trial point X + sigma (LevenbergMarquardt.cpp:87-90), the add of pnol_add_d
-                if (xnext) xnext[w * NB + t] = xbase[w * NB + t] + xv;
-            }
-        }
-        return xv;
-    };
-    const double xv1 = finish(acc1, z1, wr1, w1);
-    if (!two) return;
-    if (t < NB) xl[t] = xv1;
-    __syncthreads();   // x_w1 in LDS; every read of part / vsh above is done
-    double s0 = 0.0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s0 = fma(Lw[r], xl[q * 16 + r], s0);
-    acc0 += s0;
-    (void)finish(acc0, z0, wr0, w0);
-}
-
 __global__ void k_flag_info(int* info, int v) { *info = v; }
 
 }  // namespace
@@ -2137,13 +2011,7 @@ static int chol_bwd_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, int n
                            const double* xbase, double* xnext, bool trip = false) {
     const int epoch = ++ctx->chol4_epoch;
     if (w.gran && ((uintptr_t)w.xw & 15) != 0) return PNOL_ERR_ARG;   // granules need 16-byte alignment
-    // PNOL_BWD_PAIRS=0 (read per call): one block row per workgroup (k_chol_bwd)
-    const char* ep = std::getenv("PNOL_BWD_PAIRS");
-    if (w.gran && !(ep && std::atoi(ep) == 0))
-        hipLaunchKernelGGL(k_chol_bwd2, dim3((w.T + 1) / 2), dim3(256), 0, st, (const double*)w.Lm, w.ldp, w.T, n,
-                           (const double*)w.W, (const double*)w.bv, (const double*)w.zv, w.xw, sigma, epoch, dinfo,
-                           xbase, xnext);
-    else if (w.gran)
+    if (w.gran)
         hipLaunchKernelGGL(k_chol_bwd<true>, dim3(w.T), dim3(256), 0, st, (const double*)w.Lm, w.ldp, w.T, n,
                            (const double*)w.W, (const double*)w.bv, (const double*)w.zv, w.xw, sigma, w.bwdflag, epoch,
                            dinfo, xbase, xnext);

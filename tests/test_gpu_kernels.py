@@ -379,31 +379,6 @@ def test_cholesky_lookahead_equals_plain_chain(ctx, monkeypatch, n):
     assert np.array_equal(_np(s_on), _np(s4))
 
 
-@pytest.mark.parametrize("n", [100, 130, 700, 2048, 2111])
-def test_cholesky_bwd_pairs_equal_single_rows(ctx, monkeypatch, n):
-    """The backward solve with two block rows per workgroup (k_chol_bwd2: x_w1's hand-off to w0 in
-    LDS) is the same arithmetic in the same order as one block row per workgroup
-    (PNOL_BWD_PAIRS=0): sigma and the trial point bitwise equal, for even and odd tile counts."""
-    rng = np.random.default_rng(n + 11)
-    J = rng.standard_normal((n + 64, n))
-    A = J.T @ J + 0.25 * np.eye(n)
-    At, bt, xt = ctx.tensor(A), ctx.tensor(rng.standard_normal(n)), ctx.tensor(rng.standard_normal(n))
-    out = {}
-    for v in ("0", "1"):
-        monkeypatch.setenv("PNOL_BWD_PAIRS", v)
-        for meth in (4, 5):
-            s, i = ctx.solve(At, bt, method=meth)
-            assert i == 1
-            out[(v, meth)] = _np(s)
-        sg, xn, info = ctx.solve_step(At, bt, xt)
-        assert info == 0
-        out[(v, "step")] = (_np(sg), _np(xn))
-    for k in (4, 5):
-        assert np.array_equal(out[("0", k)], out[("1", k)])
-    assert np.array_equal(out[("0", "step")][0], out[("1", "step")][0])
-    assert np.array_equal(out[("0", "step")][1], out[("1", "step")][1])
-
-
 def test_cholesky_bwd_granules_equal_flag_form(ctx, monkeypatch):
     """The backward solve's granule hand-off (x_w[t] with its epoch in one 16-byte sc1 store,
     polled by the consumers) assumes an aligned 16-byte store is seen whole.  A torn read (new
