@@ -1,4 +1,4 @@
-"""Fused BFGS pass / H.g timing at n = 4096 and 8192, cold Infinity Cache, one child process per
+"""Fused BFGS pass / H.g timing at n = 4096 and 8192 (PASS_SIZES=a,b,..), cold Infinity Cache, one child process per
 setting (the tuning variables are read once per process): arguments VAR=value, e.g.
     python tools/pass_sweep.py PNOL_PASS_ROWS=128 PNOL_PASS_ROWS=256 PNOL_GEMV_ROWS=1"""
 import json
@@ -13,8 +13,8 @@ sys.path.insert(0, %r)
 import bench
 from parallelnonlinearoptimizationlibrary_amd.device import Context
 ctx = Context(0)
-print(json.dumps({n: bench.bench_hg(ctx, n) for n in (4096, 8192)}))
-""" % ROOT
+print(json.dumps({n: bench.bench_hg(ctx, n) for n in %r}))
+""" % (ROOT, tuple(int(v) for v in os.environ.get("PASS_SIZES", "4096,8192").split(",")))
 
 if __name__ == "__main__":
     for v in sys.argv[1:] or ["PNOL_PASS_ROWS=128", "PNOL_PASS_ROWS=256"]:
