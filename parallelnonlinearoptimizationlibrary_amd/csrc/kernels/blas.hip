@@ -665,10 +665,14 @@ int bfgs_pass_rows(int n) {
     static const int forced = [] {
         const char* e = std::getenv("PNOL_PASS_ROWS");
         const int v = e ? std::atoi(e) : 0;
-        return (v == 64 || v == 128 || v == 256) ? v : 0;
+        return (v == 32 || v == 64 || v == 128 || v == 256) ? v : 0;
     }();
     if (forced) return forced;
-    return n >= 8192 ? 256 : 128;
+    // measured (tools/pass_sweep.py, cold Infinity Cache, two rounds; profiles/r05_pass_rows_sweep.txt):
+    // n = 4096: 128 rows 0.605 of HBM (256: 0.43, 32: 0.55); 8192: 256 rows 0.67 (32: 0.66, 64:
+    // 0.61); 16384: 32 rows 0.655 (64: 0.63, 256: 0.59) -- the short tiles of the largest D
+    // stream at a better rate despite 8x the w = D^T y partials
+    return n >= 12288 ? 32 : (n >= 8192 ? 256 : 128);
 }
 
 int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p, const double* a_p,
