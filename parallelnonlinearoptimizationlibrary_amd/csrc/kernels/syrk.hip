@@ -905,12 +905,12 @@ int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
     ctx->lm_trip_tiles.kind = 0;   // the trip's tiles are overwritten below
     PNOL_CHECK(ws_get(ctx, "syrk_part", sizeof(double) * (size_t)ntiles * split * kTile * kTile, &part));
     PNOL_CHECK(ws_get(ctx, "jtr_part", sizeof(double) * (size_t)kS * n, &jp));
+    void* tcnt = nullptr;
+    if (tail) PNOL_CHECK(ws_get(ctx, "syrk_tcnt", sizeof(int) * (size_t)ntiles, &tcnt));
     CholRed cr;
     PNOL_CHECK(launch_chol_reducing_prep(ctx, n, dinfo, cr));
     PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
     PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F0));
-    void* tcnt = nullptr;
-    if (tail) PNOL_CHECK(ws_get(ctx, "syrk_tcnt", sizeof(int) * (size_t)ntiles, &tcnt));
     // the prep launch (words, paddings, info; the tile counters)
     PNOL_CHECK(launch_chol_reducing_start(ctx, cr, !tasks, (int*)tcnt, ntiles));
     if (tail) {
