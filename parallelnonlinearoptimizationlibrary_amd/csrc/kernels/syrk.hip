@@ -738,18 +738,10 @@ static void syrk_partials(pnol_ctx* ctx, hipStream_t stream, bool rows_variant, 
     } else {
         // plain partial stores: the reduce (or the reducing Cholesky) that reads them next finds
         // part of them in the caches -- solve 0.71 vs 0.73 ms, SYRK unchanged, in alternating
-        // same-box runs (non-temporal stores for J itself in the FD kernel measured slower).
-        // PNOL_SYRK_NTS=1 (tuning, read per call): non-temporal partial stores (kept out of the
-        // L2s that hold the operand panels)
-        const char* e = std::getenv("PNOL_SYRK_NTS");
-        if (e && std::atoi(e) != 0)
-            hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, 8, true>), grid, dim3(512), 0, stream, tm.start(), tm.stop(),
-                                  0, X, ldx, nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part,
-                                  tile0);
-        else
-            hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, 8, false>), grid, dim3(512), 0, stream, tm.start(), tm.stop(),
-                                  0, X, ldx, nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part,
-                                  tile0);
+        // same-box runs (non-temporal stores for J itself in the FD kernel measured slower; so did
+        // non-temporal partials again in round 5: SYRK +10-30 us)
+        hipExtLaunchKernelGGL((k_syrk_tile<0, kTile, 8, false>), grid, dim3(512), 0, stream, tm.start(), tm.stop(), 0,
+                              X, ldx, nr, K, split, sc.kfirst, sc.kchunk, sc.sub, slice0, sc.mS, sstride, part, tile0);
     }
 }
 
