@@ -950,10 +950,6 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
             hipExtLaunchKernelGGL((k_linres_fdP<16>), grid, dim3(64 * (kFdTile / 16)), 0, ctx->stream, ea, eb, 0,
                                   (const double*)o->at, (const double*)o->p1, x, h, o->m, o->n, tl, (const double*)F0,
                                   Cc, JT, (long)ldjt, mS, sstride, mt0, nmt);
-        else if (force_pw == 64)
-            hipExtLaunchKernelGGL((k_linres_fdP<64>), grid, dim3(64 * (kFdTile / 64)), 0, ctx->stream, ea, eb, 0,
-                                  (const double*)o->at, (const double*)o->p1, x, h, o->m, o->n, tl, (const double*)F0,
-                                  Cc, JT, (long)ldjt, mS, sstride, mt0, nmt);
         else
             hipExtLaunchKernelGGL((k_linres_fdP<kPW>), grid, dim3(64 * (kFdTile / kPW)), 0, ctx->stream, ea, eb, 0,
                                   (const double*)o->at, (const double*)o->p1, x, h, o->m, o->n, tl, (const double*)F0,
