@@ -133,7 +133,7 @@ __device__ __forceinline__ void part_store(double v, double* p) {
 // The tile body (k_syrk_tile, and k_syrk_red's SYRK workgroups): workgroup bid of nblk, its
 // LDS (lds[buf][P/Q]) passed in; returns the lower-triangle tile index it formed a partial of.
 // SC1: the partial stores write through (k_syrk_red's reduce workgroups read them in-launch).
-template <int MODE, int TILE, int NW = 4, bool NTS = true, bool SC1 = false>
+template <int MODE, int TILE, int NW = 4, bool NTS = true, bool SC1 = false, bool DLAST = false>
 __device__ __forceinline__ int syrk_tile_body(const double* __restrict__ X, long ldx, int nr, int K, int split_k,
                                               int kfirst, int kchunk, int sub, int slice0, int mS, long sstride,
                                               double* __restrict__ part, int tile0, int bid, int nblk,
@@ -149,7 +149,24 @@ __device__ __forceinline__ int syrk_tile_body(const double* __restrict__ X, long
     {
         const int ntl = nblk / split_k, nsl = split_k / sub;
         const int u0 = bid / (ntl * nsl), rest = bid % (ntl * nsl);
-        const int tl = rest / nsl;
+        int tl = rest / nsl;
+        // DLAST (the whole lower triangle of 128-row tiles): the off-diagonal tiles first, in
+        // row order, then the diagonal ones -- the co-resident workgroups of an XCD then do equal
+        // work on neighbouring panels in step (the diagonal tiles, 36 of 64 blocks, used to run
+        // ahead of the tiles sharing their panels), and the cheap diagonal tiles fill the tail
+        if (DLAST) {
+            const int nt = (int)((sqrt(8.0 * ntl + 1.0) - 1.0) * 0.5 + 0.5);
+            const int noff = ntl - nt;
+            if (tl < noff) {
+                int r = (int)((sqrt(8.0 * tl + 1.0) + 1.0) * 0.5);   // row r >= 1: r (r - 1) / 2 <= tl
+                while (r * (r - 1) / 2 > tl) --r;
+                while ((r + 1) * r / 2 <= tl) ++r;
+                tl = r * (r + 1) / 2 + (tl - r * (r - 1) / 2);
+            } else {
+                const int d = tl - noff;
+                tl = d * (d + 1) / 2 + d;
+            }
+        }
         sidx = (rest % nsl) * sub + u0;
         blk = tl * split_k + sidx;           // partial slot (local to this launch)
         t = tile0 + tl;                      // lower-triangle tile index
@@ -567,7 +584,7 @@ __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ 
 // past its cap sets info = kCholTimeout and gives up (the trip then redoes the solve from A formed
 // from the partials).  Every value is the sum k_syrk_reduce forms: bitwise the two launches.
 constexpr int kRedSR = 32, kRedSpin = 1 << 22;
-template <int SUB, bool SC1>
+template <int SUB, bool SC1, bool DLAST = false>
 __global__ __launch_bounds__(512, 2) void k_syrk_red(const double* __restrict__ X, long ldx, int nr, int K,
                                                      int split_k, int kfirst, int kchunk, int sub, int mS, long sstride,
                                                      double* __restrict__ part, int nsyrk, int* __restrict__ tcnt,
@@ -578,8 +595,8 @@ __global__ __launch_bounds__(512, 2) void k_syrk_red(const double* __restrict__ 
     __shared__ int ok_sh;
     const int b = blockIdx.x;
     if (b < nsyrk) {
-        const int t = syrk_tile_body<0, kTile, 8, false, SC1>(X, ldx, nr, K, split_k, kfirst, kchunk, sub, 0, mS, sstride,
-                                                             part, 0, b, nsyrk, lds);
+        const int t = syrk_tile_body<0, kTile, 8, false, SC1, DLAST>(X, ldx, nr, K, split_k, kfirst, kchunk, sub, 0, mS,
+                                                                    sstride, part, 0, b, nsyrk, lds);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -909,17 +926,21 @@ int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
         const int nsyrk = ntiles * split, nred = (kTile / kRedSR) * (ntiles + 1);
         const char* es = std::getenv("PNOL_SYRK_RED_SC1");
         const bool sc1 = es && std::atoi(es) != 0;
+        const char* ed = std::getenv("PNOL_SYRK_DLAST");   // tile order (read per call)
+        const bool dlast = ed && std::atoi(ed) != 0;
         {
             LaunchTimer tm(ctx, "syrk");
-#define PNOL_RED(SB, SC)                                                                                              \
-    hipExtLaunchKernelGGL((k_syrk_red<SB, SC>), dim3(nsyrk + nred), dim3(512), 0, ctx->stream, tm.start(), tm.stop(), 0, \
+#define PNOL_RED(SB, SC, DL)                                                                                          \
+    hipExtLaunchKernelGGL((k_syrk_red<SB, SC, DL>), dim3(nsyrk + nred), dim3(512), 0, ctx->stream, tm.start(), tm.stop(), 0, \
                           JT, (long)ldjt, n, m, split, sc.kfirst, sc.kchunk, sc.sub, sc.mS, (long)sc.mS, (double*)part,   \
                           nsyrk, (int*)tcnt, ntiles, n, lambda, cr.w.P, cr.w.ldp, (const double*)jp, rhs, cr.w.bv,       \
                           cr.dinfo)
             if (sc.sub == 2) {
-                if (sc1) PNOL_RED(2, true); else PNOL_RED(2, false);
+                if (dlast) PNOL_RED(2, false, true);
+                else if (sc1) PNOL_RED(2, true, false);
+                else PNOL_RED(2, false, false);
             } else {
-                if (sc1) PNOL_RED(0, true); else PNOL_RED(0, false);
+                if (sc1) PNOL_RED(0, true, false); else PNOL_RED(0, false, false);
             }
 #undef PNOL_RED
         }
