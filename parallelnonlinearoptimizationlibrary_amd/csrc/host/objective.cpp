@@ -98,11 +98,6 @@ void host_points_recur(Objective* o, const std::vector<double>& X, const std::ve
 struct RecurCache {
     unsigned long long oid = 0;   // pnol_dobj::id (never reused)
     std::vector<double> Xf, hf, gf, pts, fv;
-    // a coordinate's step from the last call in which it was free (1.0 before that): a frozen
-    // coordinate's perturbed value is evaluated with it instead of a dummy step, so when the
-    // coordinate is freed again at the same full point (the recursion unwinding, with its step
-    // restored) its value is already cached; the reuse check still compares every free step
-    std::vector<double> hlast;
     std::vector<double> p0h, p1h;   // host copies of the objective's data (oid's)
     std::vector<int> redo;
     double F = 0.0;
@@ -238,20 +233,13 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
         gf.resize(nf);
         gr.resize(nf + 1);
         const size_t last = N > 0 ? (size_t)N - 1 : 0;
-        RecurCache& rc = recur_cache();
-        if (rc.hlast.size() != nf || rc.oid != d->id) {
-            rc.hlast.assign(nf, 1.0);
-        }
         size_t ir = 0;
         for (size_t i = 0; i < nf; ++i) {
             const bool c = constantIndicator[i];
             const size_t k = ir < last ? ir : last;
             const double xr = N > 0 ? X[k] : 0.0, hr = N > 0 ? dX[k] : 1.0;
             Xf[i] = c ? constantX[i] : xr;
-            // frozen: the step it had when last free (1.0 if never free); free: its own step
-            const double hl = rc.hlast[i];
-            hf[i] = c ? hl : hr;
-            rc.hlast[i] = c ? hl : hr;
+            hf[i] = c ? 1.0 : hr;
             ir += !c;
         }
         // Same-point reuse: the bounded solvers' recursion unwinds through one level per frozen
@@ -267,6 +255,7 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
         // Only kinds whose host formula is bitwise the device's (host_bitwise_kind: PowerObject
         // with power != 2 calls pow, which may not be); the evaluation count is the reference's
         // N + 1.
+        RecurCache& rc = recur_cache();
         const bool pure = host_bitwise_kind(d->kind, d->power);
         std::vector<int>& redo = rc.redo;
         redo.clear();
