@@ -708,7 +708,7 @@ def test_fd_normal_bitwise(ctx, m, n):
         assert np.array_equal(_np(rb), _np(ra)), rep
 
 
-@pytest.mark.parametrize("reduce", ["launch", "tasks", "tail", "tail_sc1", "tail_dlast"])
+@pytest.mark.parametrize("reduce", ["launch", "tasks", "tail", "tail_sc1", "tail_rowsorder"])
 @pytest.mark.parametrize("m,n", [(16384, 2048), (5000, 1000), (777, 129), (3000, 257), (2000, 700), (512, 96)])
 def test_lm_trip_bitwise(ctx, monkeypatch, m, n, reduce):
     """The LM trip without A (pnol_lm_trip_d: the reduce launch writes the J^T J split-K partials'
@@ -723,7 +723,7 @@ def test_lm_trip_bitwise(ctx, monkeypatch, m, n, reduce):
     from parallelnonlinearoptimizationlibrary_amd.device import DeviceObjective
     monkeypatch.setenv("PNOL_LM_REDUCE", reduce.split("_")[0])
     monkeypatch.setenv("PNOL_SYRK_RED_SC1", "1" if reduce.endswith("_sc1") else "0")
-    monkeypatch.setenv("PNOL_SYRK_DLAST", "1" if reduce.endswith("_dlast") else "0")
+    monkeypatch.setenv("PNOL_SYRK_DLAST", "0" if reduce.endswith("_rowsorder") else "1")
     d = DeviceObjective.synthetic(ctx, L.OBJ_LINRES, n, m)
     h = ctx.tensor(np.full(n, 1e-7))
     JTa, Aa, ra, JTb = ctx.empty(n, m), ctx.empty(n, n), ctx.empty(n), ctx.empty(n, m)
