@@ -938,9 +938,11 @@ int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
                           nsyrk, (int*)tcnt, ntiles, n, lambda, cr.w.P, cr.w.ldp, (const double*)jp, rhs, cr.w.bv,       \
                           cr.dinfo)
             if (sc.sub == 2) {
-                if (dlast) PNOL_RED(2, false, true);
-                else if (sc1) PNOL_RED(2, true, false);
-                else PNOL_RED(2, false, false);
+                if (dlast) {
+                    if (sc1) PNOL_RED(2, true, true); else PNOL_RED(2, false, true);
+                } else {
+                    if (sc1) PNOL_RED(2, true, false); else PNOL_RED(2, false, false);
+                }
             } else {
                 if (sc1) PNOL_RED(0, true, false); else PNOL_RED(0, false, false);
             }
