@@ -896,14 +896,19 @@ __device__ __forceinline__ void chol_tl_mark(int k, int cls, unsigned long long 
 // left it there), so only A_{d,k} is staged.
 // Ldef (the persistent chain): L goes to Ldef (substage layout) and only block column 0 gets
 // -L L^T here (diag_blk_def); factor_diag16's owners apply the rest (mp_owner, kb0 = 0).
+// Astg / Cstg (the persistent chain after a staged-only look-ahead): A_{d,k} already in Astg
+// (the substage layout) and A_dd's lower blocks in Cstg (16 x 16 row-major each, lower-block
+// order) -- nothing is loaded from memory but W_k when it is not in LDS.
 template <bool SC1 = false>
 __device__ __forceinline__ void diag_prepare(const double* __restrict__ P, long ldp, const double* __restrict__ W,
                                              int k, double* __restrict__ X, double* __restrict__ Y, const DiagLds& L,
-                                             int wave, int lane, bool w_in_lds = false, double* __restrict__ Ldef = nullptr) {
+                                             int wave, int lane, bool w_in_lds = false, double* __restrict__ Ldef = nullptr,
+                                             const double* __restrict__ Astg = nullptr,
+                                             const double* __restrict__ Cstg = nullptr) {
     const int d0 = (k + 1) * NB;
     const int k0 = k * NB;
     const bool def = Ldef != nullptr;
-    stage_tile<SC1>(X, P, ldp, d0, k0);
+    if (!Astg) stage_tile<SC1>(X, P, ldp, d0, k0);
     if (!w_in_lds) stage_tile<SC1>(Y, W + (long)k * NB * NB, NB, 0, 0);
     d4 cdd[3];   // this wave's lower blocks of A_dd, in flight during the first product
 #pragma unroll
@@ -911,13 +916,14 @@ __device__ __forceinline__ void diag_prepare(const double* __restrict__ P, long 
         const int bl = def ? diag_blk_def(wave, sb) : diag_blk(wave, sb), ib = bl >> 2, jb = bl & 3;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            cdd[sb][r] = bl < 0 ? 0.0
+            cdd[sb][r] = bl < 0  ? 0.0
+                         : Cstg ? Cstg[(ib * (ib + 1) / 2 + jb) * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15)]
                                 : ldg<SC1>(P + (long)(d0 + ib * 16 + (lane >> 4) + 4 * r) * ldp + d0 + jb * 16 + (lane & 15));
     }
     __syncthreads();
     PNOL_CHOL_STAMP(k, 1)
     d4 lst[4];
-    diag_l_strip(lst, X, Y, wave, lane);        // L_{d,k} = A_{d,k} W_k^T, strip `wave`
+    diag_l_strip(lst, Astg ? Astg : X, Y, wave, lane);   // L_{d,k} = A_{d,k} W_k^T, strip `wave`
     __syncthreads();
     PNOL_CHOL_STAMP(k, 2)
     double* const Ls = def ? Ldef : X;
@@ -998,20 +1004,30 @@ struct EarlyNext {
         if (dn >= T) return;
         if (wave == 2) {
             PNOL_LA_STAMP(d, 0)
-            int ready = 0;
+            // 1: the tiles came before `cutoff` columns of this factor were final -- stage them and
+            // start their products; 3: they came later, before the factor's last column -- stage
+            // them only (the next step's diag_prepare takes them from LDS instead of memory);
+            // 2: not in time
+            int ready = 0, late = 0;
             for (int it = 0;; ++it) {
                 ready = __hip_atomic_load(ver + dn * T + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= d &&
                         __hip_atomic_load(ver + dn * T + dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= d;
                 ready = __builtin_amdgcn_readfirstlane(ready);
-                if (ready || it > 4096 || lds_peek(cnt) >= cutoff) break;
+                const int c = __builtin_amdgcn_readfirstlane(lds_peek(cnt));
+                if (ready) {
+                    late = c >= cutoff;
+                    break;
+                }
+                if (it > 4096 || (cutoff <= NB && c >= NB)) break;
                 __builtin_amdgcn_s_sleep(1);
             }
             PNOL_LA_STAMP(d, 1)
-            lds_signal(E.w, ready ? 1 : 2);
+            lds_signal(E.w, ready ? (late ? 3 : 1) : 2);
         } else {
             wait_lds_ge(E.w, 1);
         }
-        if (__builtin_amdgcn_readfirstlane(lds_peek(E.w)) != 1) return;
+        const int mode = __builtin_amdgcn_readfirstlane(lds_peek(E.w));
+        if (mode != 1 && mode != 3) return;
         const int h = wave - 2;   // wave 2: rows 0..31 and blocks 0..4; wave 3: rows 32..63, blocks 5..9
         {
             // an opaque copy of the lane id: keeps the (loop-invariant) load offsets from being
@@ -1046,6 +1062,7 @@ struct EarlyNext {
             }
         }
         PNOL_LA_STAMP(d, 2)
+        if (mode == 3) return;   // staged only
         const int frow = lane & 15, fk = lane >> 4;
         // Every MFMA operand of a phase is read from LDS before its first MFMA (one wait, not one
         // LDS round trip per K step); each accumulator takes the same MFMAs in the same order.
@@ -1627,8 +1644,9 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             const DiagLds L = diag_lds(smem);
             // the previous factor's waves 2 / 3 staged this tile and did half of its products
             const bool pre = lookahead && ew[0] == 1;
+            const bool staged = lookahead && ew[0] == 3;   // the tiles only, in pfx / pfc
 #ifdef PNOL_CHOL_TIMELINE
-            if (t == 0 && k + 1 < 64) g_chol_clk[8 * (k + 1) + 6] = pre ? 1 : 0;
+            if (t == 0 && k + 1 < 64) g_chol_clk[8 * (k + 1) + 6] = pre ? 1 : (staged ? 2 : 0);
 #endif
             if (d == 0) {   // tile 0 as the reduce tasks stored it (sc1 loads)
                 const int row = t >> 2, c0 = (t & 3) * 16;
@@ -1640,7 +1658,8 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             } else if (pre) {
                 late_prepare(E, Y, L, wave, lane, true);
             } else {   // W_{d-1} stays in Y after the chain's own factor
-                diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane, d > 1 || smode, pfx);
+                diag_prepare<true>(P, ldp, W, k, X, Y, L, wave, lane, d > 1 || smode, pfx, staged ? pfx : nullptr,
+                                   staged ? pfc : nullptr);
             }
             if (t < 6) cnt[t] = 0;   // every read of cnt / ew above is behind a barrier inside
             if (t < 4) ew[t] = 0;    // either prepare
@@ -1991,6 +2010,10 @@ static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, i
     // rounds, profiles/r05_lookahead_sweep.txt): 0: 0.585-0.587 ms, 32: 0.582-0.587, 40: 0.579-
     // 0.585, 48: 0.571-0.578 (default), 56: 0.588-0.597, 64: 0.596-0.601; LM bench 52 vs 64: 3
     // of 3 same-box pairs faster (327-328 vs 324-328 LM iters/s).  (Round 2's factor: 64 best.)
+    // Tiles that come after the cutoff but before the factor's last column are still staged
+    // (EarlyNext mode 3): their step's prepare skips the loads, ~4.5k of its ~10.5k cycles, and
+    // the solve goes 0.559-0.561 -> 0.553-0.556 ms; with it every cutoff from 1 to 48 measures
+    // the same (56: 0.562-0.566), profiles/r05_lookahead_sweep.txt.
     const int lookahead = el ? std::max(0, std::atoi(el)) : 48;
     RedArgs rp = red;
     {

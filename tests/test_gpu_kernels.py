@@ -357,7 +357,8 @@ def test_cholesky_lookahead_equals_plain_chain(ctx, monkeypatch, n):
     """Method 5's diagonal chain starts the next tile's products inside the current factor
     (waves 2 / 3: the left half of L and K blocks 0, 1 of A_dd - L L^T), the rest after it.
     Every accumulator takes the same MFMAs in the same order: sigma is bitwise the chain without
-    the look-ahead (PNOL_CHOL_LOOKAHEAD=0) and method 4's."""
+    the look-ahead (PNOL_CHOL_LOOKAHEAD=0) and method 4's; so is a step whose tiles came too
+    late for the products and were only staged (the next prepare reads them from LDS)."""
     rng = np.random.default_rng(n + 7)
     J = rng.standard_normal((n + 64, n))
     A = J.T @ J + 0.25 * np.eye(n)
@@ -369,11 +370,14 @@ def test_cholesky_lookahead_equals_plain_chain(ctx, monkeypatch, n):
     s_mix, i_mix = ctx.solve(At, bt, method=5)
     monkeypatch.setenv("PNOL_CHOL_LOOKAHEAD", "1000")   # waits for the tiles: every step
     s_on, i_on = ctx.solve(At, bt, method=5)
+    monkeypatch.setenv("PNOL_CHOL_LOOKAHEAD", "1")   # late tiles staged only, prepared from LDS
+    s_stg, i_stg = ctx.solve(At, bt, method=5)
     monkeypatch.delenv("PNOL_CHOL_LOOKAHEAD")           # default (48)
     s_def, i_def = ctx.solve(At, bt, method=5)
     s4, i4 = ctx.solve(At, bt, method=4)
-    assert i_off == i_mix == i_on == i_def == i4 == 1
+    assert i_off == i_mix == i_on == i_stg == i_def == i4 == 1
     assert np.array_equal(_np(s_on), _np(s_off))
+    assert np.array_equal(_np(s_stg), _np(s_off))
     assert np.array_equal(_np(s_mix), _np(s_off))
     assert np.array_equal(_np(s_def), _np(s_off))
     assert np.array_equal(_np(s_on), _np(s4))
