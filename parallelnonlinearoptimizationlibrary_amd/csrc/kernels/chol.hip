@@ -417,9 +417,11 @@ __device__ __forceinline__ void mp_def(double (&a)[kMW], double lp2, const ColBu
 // cycles of latency each, tools/microbench/piv_chain.hip: 124 cycles per pivot for the bare
 // chain) is followed by a group of independent updates that fill its latency; left to itself
 // the scheduler issues the chain ops back to back (~280 cycles per pivot).
+// Lp and sb alias (a panel lane's sb points into Lp, and the read-back of column J follows its
+// store), so neither is __restrict__.
 template <int J, int P, bool STAMP>
 __device__ __forceinline__ void mp_step(double (&a)[kMW], double r, double lp1, const ColBuf16<J - 1>& cp1, double lp2,
-                                        const ColBuf16<J - 2>& cp2, double* __restrict__ Lp, double* __restrict__ sb,
+                                        const ColBuf16<J - 2>& cp2, double* Lp, double* sb,
                                         int ss, double* __restrict__ rinv, int* cnt, int lane, bool& bad, long long* st) {
     constexpr int c = kMW * P + J, LD = mp_ld(P);
     if constexpr (STAMP && (J & 7) == 0) st[2 * P + (J >> 3)] = __builtin_amdgcn_s_memtime();
