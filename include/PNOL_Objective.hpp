@@ -33,6 +33,15 @@
 
 #include "pnol_amd.h"
 
+// A program compiled with <mpi.h> on its include path (every reference program: the reference
+// header includes it, PNOL_Objective.hpp:20) gets the *_MPI classes bound to MPI_COMM_WORLD
+// with no code change (pnol_mpi_bind.hpp).  The library's own sources never include it.
+#if !defined(PNOL_AMD_BUILDING_LIBRARY) && !defined(PNOL_AMD_NO_MPI_BIND) && defined(__has_include)
+#if __has_include(<mpi.h>)
+#include "pnol_mpi_bind.hpp"
+#endif
+#endif
+
 using namespace std;  // the reference header exports namespace std to its users
 
 class Objective {

@@ -119,6 +119,10 @@ int pnol_set_identity_d(pnol_ctx* ctx, double* D, int ldd, int n, const double* 
  * same as the one-GPU pnol_hg_d / pnol_bfgs_pass_d on the whole D (same per-row order, the
  * column partials of w summed in the same fixed tile order). */
 int pnol_bfgs_rows(int n, int nranks, int rank, int* begin, int* count);
+/* Row tiles of w = D^T y partials the fused pass's workspace holds for n and nranks ranks:
+ * max(the whole-matrix tile count, nranks * the tiles of one pnol_bfgs_rows shard) -- the
+ * allgathered layout puts rank r's tiles at r * (tiles per shard).  Shape math only. */
+int pnol_bfgs_pass_part_tiles(int n, int nranks);
 int pnol_set_identity_rows_d(pnol_ctx* ctx, double* Dsh, int ldd, int n, const double* scale);
 int pnol_hg_mpi_d(pnol_ctx* ctx, const double* Dsh, int ldd, const double* g, double* p, int n);
 int pnol_bfgs_pass_mpi_d(pnol_ctx* ctx, double* Dsh, int ldd, int n, const double* s_p, const double* a_p,
@@ -332,6 +336,29 @@ typedef int (*pnol_host_allgather_fn)(const void* send, void* recv, size_t bytes
 int pnol_comm_init_host(int nranks, int rank, pnol_host_allgather_fn fn, void* user);
 int pnol_comm_finalize(void);
 int pnol_comm_size(int* nranks, int* rank);
+/* MPI launcher binding (the reference's *_MPI classes take P and the rank from MPI_COMM_WORLD:
+ * LevenbergMarquardtMPI.cpp:16-17, PNOL_Objective.cpp:102-103, BFGS_with_linesearch_MPI.cpp:231-235).
+ * The library itself links no MPI.  A program that includes the drop-in headers with <mpi.h>
+ * on its include path (the reference header includes it, PNOL_Objective.hpp:20) registers a
+ * hook compiled against the program's own MPI (include/pnol_mpi_bind.hpp); the first *_MPI
+ * call runs it: P and the rank from MPI_COMM_WORLD, the GPU by node-local rank, and RCCL
+ * bootstrapped with the unique id broadcast over MPI (the host backend over MPI_Allgather
+ * when node-local ranks outnumber the GPUs).  Hook return: 0 bound (or nothing to bind,
+ * P = 1), 1 MPI not initialised yet (asked again on the next *_MPI call), < 0 failure. */
+typedef int (*pnol_launcher_hook_fn)(void);
+int pnol_comm_set_launcher_hook(pnol_launcher_hook_fn fn);
+/* Run the hook if no communicator is bound (what every *_MPI entry point does first).
+ * PNOL_ERR_COMM when an MPI launcher's environment (PMI_SIZE, OMPI_COMM_WORLD_SIZE,
+ * MV2_COMM_WORLD_SIZE) says the job has more than one rank and still no communicator is
+ * bound: a *_MPI class never runs such a job silently as one rank. */
+int pnol_comm_bind_launcher(void);
+/* The job size an MPI launcher's environment announces (1 without one). */
+int pnol_launcher_world_size(void);
+/* GPU of the process's default context, when chosen before its first use (the launcher hook
+ * picks the node-local rank's GPU); otherwise PNOL_DEVICE, then LOCAL_RANK / MPI_LOCALRANKID /
+ * OMPI_COMM_WORLD_LOCAL_RANK modulo the device count, then 0.  PNOL_ERR_ARG once the default
+ * context exists on another device. */
+int pnol_set_default_device(int device);
 /* recv[r * count + i] = send_r[i]  (device buffers on the RCCL backend) */
 int pnol_comm_allgather_d(pnol_ctx* ctx, const double* send, double* recv, size_t count);
 /* contiguous column block owned by `rank` of `nranks` over `ncols` columns (also the host split) */

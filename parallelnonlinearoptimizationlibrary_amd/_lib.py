@@ -77,6 +77,7 @@ _SIGS = {
     "pnol_bfgs_pass_ident_d": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "pnol_bfgs_pass_ident_mpi_d": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "pnol_bfgs_rows": (_i, [_i, _i, _i, C.POINTER(_i), C.POINTER(_i)]),
+    "pnol_bfgs_pass_part_tiles": (_i, [_i, _i]),
     "pnol_set_identity_rows_d": (_i, [_vp, _vp, _i, _i, _vp]),
     "pnol_hg_mpi_d": (_i, [_vp, _vp, _i, _vp, _vp, _i]),
     "pnol_bfgs_pass_mpi_d": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
@@ -120,6 +121,10 @@ _SIGS = {
     "pnol_comm_init_host": (_i, [_i, _i, ALLGATHER_FN, _vp]),
     "pnol_comm_finalize": (_i, []),
     "pnol_comm_size": (_i, [C.POINTER(_i), C.POINTER(_i)]),
+    "pnol_comm_set_launcher_hook": (_i, [_vp]),
+    "pnol_comm_bind_launcher": (_i, []),
+    "pnol_launcher_world_size": (_i, []),
+    "pnol_set_default_device": (_i, [_i]),
     "pnol_comm_allgather_d": (_i, [_vp, _vp, _vp, _sz]),
     "pnol_block_range": (None, [_i, _i, _i, C.POINTER(_i), C.POINTER(_i)]),
     "pnol_fd_tiles": (_i, [_i, _i, _i, C.POINTER(_i), C.POINTER(_i), _i]),

@@ -116,6 +116,14 @@ extern "C" int pnol_bfgs_rows(int n, int nranks, int rank, int* begin, int* coun
     return PNOL_OK;
 }
 
+extern "C" int pnol_bfgs_pass_part_tiles(int n, int nranks) {
+    if (n <= 0 || nranks <= 0) return 0;
+    const int prows = bfgs_pass_rows(n);
+    const int whole = (n + prows - 1) / prows;
+    const int gathered = nranks * (bfgs_rows_per(n, nranks) / prows);
+    return std::max(whole, gathered);
+}
+
 namespace {
 
 // part_w of the fused pass: every rank's row tiles, in place (rank r's tiles at r * tiles_per)

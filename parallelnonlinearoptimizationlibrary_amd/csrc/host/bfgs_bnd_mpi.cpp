@@ -296,6 +296,7 @@ void BFGSBnd_MPI::mainBFGSLoop(double& F, vector<double>& X, vector<double>& dFd
 void BFGSBnd_MPI::findMinBnd(vector<double>& X, vector<double>& Xlb, vector<double>& Xub, double& f0,
                              double& fOpt) {
     // :14-81
+    require_comm("BFGSBnd_MPI::findMinBnd");
     const int n = (int)X.size();
     std::vector<double> cX(n, 0.0), dX(n, dXGrad), dFdX(n, 0.0);
     std::vector<bool> cI(n, false);

@@ -377,7 +377,9 @@ void BFGS_Bnd_MPI_SW::mainBFGSLoop(double& F, vector<double>& X, vector<double>&
 
 void BFGS_Bnd_MPI_SW::findMinBnd(vector<double>& X, vector<double>& Xlb, vector<double>& Xub, double& f0,
                                  double& fOpt) {
-    // the active-set recursion is one level per frozen coordinate (deep_stack.hpp)
+    // the communicator is bound on the calling thread; the active-set recursion is one level
+    // per frozen coordinate (deep_stack.hpp)
+    require_comm("BFGS_Bnd_MPI_SW::findMinBnd");
     run_deep([&] { findMinBndBody(X, Xlb, Xub, f0, fOpt); });
 }
 

@@ -142,6 +142,7 @@ void BFGS_MPI::secantLineSearch(vector<double>& X, double FX, vector<double>& dF
 
 void BFGS_MPI::findMin(vector<double>& X, double& f0, double& fOpt) {
     // BFGS_with_linesearch_MPI.cpp:12-142
+    require_comm("BFGS_MPI::findMin");   // Npool = Nprocs of MPI_COMM_WORLD (:231-235)
     const int n = (int)X.size();
     const int rank = comm_rank();
     pnol_ctx* ctx = require_ctx();

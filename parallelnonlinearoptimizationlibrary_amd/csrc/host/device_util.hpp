@@ -18,6 +18,15 @@ inline void check(int status, const char* what) {
         throw std::runtime_error(std::string("pnol_amd: ") + what + ": " + pnol_status_string(status));
 }
 
+// Every *_MPI entry point: the communicator of the MPI launch (pnol_comm_bind_launcher), or an
+// error rather than a silent single-rank run of a multi-rank job.
+inline void require_comm(const char* who) {
+    if (comm_bind_launcher() != PNOL_OK)
+        throw std::runtime_error(std::string("pnol_amd: ") + who +
+                                 ": started by an MPI launcher with several ranks but no communicator is bound "
+                                 "(MPI_Init + <mpi.h> on the include path, or pnol_comm_init_rccl)");
+}
+
 inline pnol_ctx* require_ctx() {
     pnol_ctx* c = default_ctx_or_null();
     if (!c) throw std::runtime_error("pnol_amd: no gfx950 (MI355X) device visible; the HIP path has no CPU fallback");

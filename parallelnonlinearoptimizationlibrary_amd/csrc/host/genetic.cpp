@@ -240,6 +240,7 @@ void GeneticAlgorithm::findMinBnd(std::vector<double>& X, std::vector<double>& X
 
 void GeneticAlgorithmMPI::findMinBnd(std::vector<double>& X, std::vector<double>& Xlb, std::vector<double>& Xub,
                                      double& f0, double& fOpt) {
+    require_comm("GeneticAlgorithmMPI::findMinBnd");   // GeneticAlgorithmMPI.cpp:17-18
     runGA(X, Xlb, Xub, f0, fOpt, comm_rank() == 0);
 }
 

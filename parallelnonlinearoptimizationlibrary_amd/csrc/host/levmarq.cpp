@@ -201,6 +201,12 @@ class LMAsync {
             check(comm_allgather_int(ctx, ctx->lm_fd_mode, all), "allgather(fd mode)");
             for (int v : all)
                 if (v != ctx->lm_fd_mode) throw std::runtime_error("LevMarqMPI: ranks disagree on PNOL_LM_FD");
+            // the columns mode's phasing likewise: a phased rank posts one exchange per tile phase
+            // on a second stream, an unphased one a single exchange
+            ctx->lm_phased = lm_phased_env();
+            check(comm_allgather_int(ctx, ctx->lm_phased, all), "allgather(phased)");
+            for (int v : all)
+                if (v != ctx->lm_phased) throw std::runtime_error("LevMarqMPI: ranks disagree on PNOL_LM_PHASED");
         }
         // The trip without forming A (default; PNOL_LM_TRIP=0 keeps the two calls, read once per
         // solve): one GPU, pnol_lm_trip_d -- the reduce launch writes A straight into the
@@ -323,7 +329,16 @@ class LMAsync {
             check(pnol_jtr_d(ctx_, JT_.get(), ldjt_, m_, n_, F(s), rhs_.get()), "jtr");
         }
         int info = 0;
-        check(pnol_solve_d(ctx_, A_.get(), lda_, rhs_.get(), sig(s), n_, action == 2 ? 2 : 0, &info), "solve");
+        const int st = pnol_solve_d(ctx_, A_.get(), lda_, rhs_.get(), sig(s), n_, action == 2 ? 2 : 0, &info);
+        if (agree_) {
+            // a relaunch budget exhausted on one rank only must fail every rank alike: its peers
+            // would otherwise go on into the next trip's collectives and wait for it forever
+            std::vector<int> all;
+            check(comm_allgather_int(ctx_, st, all), "allgather(redo status)");
+            for (int v : all)
+                if (v != PNOL_OK) check(st != PNOL_OK ? st : v, "solve (redo, agreed over the ranks)");
+        }
+        check(st, "solve");
         finish(s);
         wait(s);
     }
@@ -538,6 +553,7 @@ void LevMarq::findMin(vector<double>& X, vector<double>& F0, vector<double>& FOp
 }
 
 void LevMarqMPI::findMin(vector<double>& X, vector<double>& F0, vector<double>& FOpt) {
+    require_comm("LevMarqMPI::findMin");   // LevenbergMarquardtMPI.cpp:16-17
     stepCounts[0] = stepCounts[1] = 0;
     LMParams P{lambda0, lambdaFactor, dXGrad, xMinDiff, maxIter, verbose, stepCounts};
     lm_solve(mObjPtr, P, true, X, F0, FOpt);

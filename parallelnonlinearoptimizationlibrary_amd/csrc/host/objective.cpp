@@ -186,6 +186,7 @@ void Objective::hessianApproximation(vector<double>& X, vector<double>& dX, vect
 }
 
 void Objective::gradientApproximationMPI(vector<double>& X, vector<double>& dX, vector<double>& dFdX) {
+    require_comm("Objective::gradientApproximationMPI");   // PNOL_Objective.cpp:102-103
     const int N = (int)X.size();
     const int P = comm_size(), r = comm_rank();
     int b = 0, cnt = 0;
@@ -329,6 +330,7 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
 void Objective::gradientApproximationMPIRecur(vector<double>& X, vector<double>& dX, vector<double>& dFdX,
                                               vector<double>& constantX, vector<bool>& constantIndicator) {
     // PNOL_Objective.cpp:366-459: same values as the serial Recur gradient, points sharded
+    require_comm("Objective::gradientApproximationMPIRecur");
     const int N = (int)X.size();
     const int P = comm_size(), r = comm_rank();
     int b = 0, cnt = 0;
@@ -442,6 +444,7 @@ void MultiObjective::gradientApproximation(vector<double>& X, vector<double>& dX
 }
 
 void MultiObjective::gradientApproximationMPI(vector<double>& X, vector<double>& dX, vector<vector<double>>& J) {
+    require_comm("MultiObjective::gradientApproximationMPI");   // PNOL_Objective.cpp:227-228
     const int n = (int)X.size();
     const int m = (int)J.size();
     std::vector<double> JT((size_t)n * m);

@@ -13,6 +13,7 @@
 //
 // All device code is compiled with -ffp-contract=off: every fma here is explicit.
 #include "../pnol_internal.hpp"
+#include "../pnol_comm.hpp"
 
 #include <cstdlib>
 
@@ -693,8 +694,11 @@ int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p
     void *pu = nullptr, *pv = nullptr, *pw = nullptr, *zeros = nullptr;
     PNOL_CHECK(ws_get(ctx, "pass_part_u", sizeof(double) * (size_t)nstrips * n, &pu));
     PNOL_CHECK(ws_get(ctx, "pass_part_v", sizeof(double) * (size_t)nstrips * n, &pv));
-    // room for the allgather's padded layout: nranks * (tiles per rank) >= nrowt tiles
-    PNOL_CHECK(ws_get(ctx, "pass_part_w", sizeof(double) * (size_t)(nrowt + 64) * n, &pw));
+    // room for the allgather's padded layout (rank r's tiles at r * tiles per shard): up to
+    // nranks * tiles per shard, which exceeds nrowt for short row tiles and many ranks
+    const int wtiles = pw_gather ? pnol_bfgs_pass_part_tiles(n, comm_size()) : nrowt;
+    if (wtiles < nrowt) return PNOL_ERR_ARG;
+    PNOL_CHECK(ws_get(ctx, "pass_part_w", sizeof(double) * (size_t)wtiles * n, &pw));
     if (!y || !g) {
         PNOL_CHECK(ws_get(ctx, "pass_zeros", sizeof(double) * (size_t)n, &zeros));
         PNOL_CHECK(launch_fill(ctx, (double*)zeros, (size_t)n, 0.0));

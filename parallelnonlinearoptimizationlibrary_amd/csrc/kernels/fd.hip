@@ -1011,6 +1011,11 @@ int launch_synthetic_linres(pnol_ctx* ctx, unsigned long long seed, int m, int n
     return launch_check();
 }
 
+int lm_phased_env() {
+    const char* e = std::getenv("PNOL_LM_PHASED");
+    return (e && std::atoi(e) == 0) ? 0 : 1;
+}
+
 int lm_fd_mode_env() {
     const char* e = std::getenv("PNOL_LM_FD");
     return (e && std::strcmp(e, "rows") == 0) ? 1 : 0;
@@ -1090,11 +1095,12 @@ int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
         lm_phase_tiles(n, P, q, pst[q], pct[q]);
         nphase = std::max(nphase, (int)pst[q].size());
     }
-    // PNOL_LM_PHASED=0 (read per call, the same on every rank): one tile-list launch, then every
-    // tile's slices in one exchange on the context stream after it -- no second stream, no
-    // events; the same bits (the phased form's RCCL transport first runs on a multi-GPU node)
-    if (const char* e = std::getenv("PNOL_LM_PHASED"))
-        if (std::atoi(e) == 0) {
+    // PNOL_LM_PHASED=0 (read once per LevMarqMPI solve and agreed over the ranks, ctx->lm_phased):
+    // one tile-list launch, then every tile's slices in one exchange on the context stream after
+    // it -- no second stream, no events; the same bits (the phased form's RCCL transport first
+    // runs on a multi-GPU node)
+    if (ctx->lm_phased < 0) ctx->lm_phased = lm_phased_env();
+    if (ctx->lm_phased == 0) {
             const int mine = (int)pst[me].size();
             PNOL_CHECK(launch_fd_jacobian_tiles(ctx, o, x, h, pst[me].data(), pct[me].data(), mine, F0, compute_f0,
                                                 JTs, 0, mS, 1, mS, sstr));

@@ -11,6 +11,10 @@ namespace pnol {
 
 int comm_size();
 int comm_rank();
+// bind the MPI launcher's communicator if none is bound (every *_MPI entry point calls this
+// first); PNOL_ERR_COMM when a multi-rank launch has no communicator
+int comm_bind_launcher();
+int launcher_world_size();
 // contiguous ceil-sized column block of `rank`
 void block_range(int ncols, int nranks, int rank, int* begin, int* count);
 // cost-balanced FD column tiles (PNOL_FD_TILE columns each, dealt in snake order)

@@ -69,6 +69,9 @@ struct pnol_ctx {
     // LevMarqMPI's FD decomposition (fd.hip): -1 = not chosen yet (PNOL_LM_FD at first use),
     // 0 = columns (the reference's: FD column tiles per rank + the m-slice exchange), 1 = rows
     int lm_fd_mode = -1;
+    // PNOL_LM_PHASED (columns mode's phased slice exchange; 1 default, 0 one exchange after one
+    // FD launch): read once per LevMarqMPI solve and agreed over the ranks (-1: read at first use)
+    int lm_phased = -1;
     bool lm_fd_mode_set = false;   // set by pnol_lm_set_fd_mode: the LevMarqMPI drop-in keeps it
     // What the last LM trip without A (launch_fd_normal_solve / launch_lm_normal_solve) left for
     // its A-forming entry points (pnol_lm_trip_normal_d, pnol_lm_normal_unpack_mpi_d): the
@@ -332,6 +335,7 @@ int launch_lm_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* F);
 // and checks it equal on every rank.
 bool lm_rows_mode(pnol_ctx* ctx);
 int lm_fd_mode_env();
+int lm_phased_env();   // PNOL_LM_PHASED (0 or 1)
 
 // Timer events that do not bracket one stream: timer_event records an event on `stream` when
 // the timer `name` is on (nullptr otherwise); timer_pair books (a, b) under `name` -- elapsed

@@ -69,6 +69,53 @@ static CommState g_comm;
 int comm_size() { return g_comm.nranks; }
 int comm_rank() { return g_comm.rank; }
 
+// MPI launcher binding: the hook is compiled into the user's program against its own MPI
+// (include/pnol_mpi_bind.hpp); the library only calls it.
+static pnol_launcher_hook_fn g_launch_hook = nullptr;
+static bool g_launch_bound = false;
+static std::mutex g_launch_mu;
+
+static int env_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    if (!e || !*e) return dflt;
+    char* end = nullptr;
+    const long v = std::strtol(e, &end, 10);
+    return (end && *end == 0) ? (int)v : dflt;
+}
+
+int launcher_world_size() {
+    for (const char* k : {"PMI_SIZE", "OMPI_COMM_WORLD_SIZE", "MV2_COMM_WORLD_SIZE"}) {
+        const int v = env_int(k, 0);
+        if (v > 0) return v;
+    }
+    return 1;
+}
+
+int comm_bind_launcher() {
+    std::lock_guard<std::mutex> lk(g_launch_mu);
+    if (g_comm.kind != 0) return PNOL_OK;
+    if (g_launch_hook && !g_launch_bound) {
+        const int st = g_launch_hook();
+        if (st == 0) g_launch_bound = true;
+        if (st < 0) {
+            std::fprintf(stderr, "pnol_amd: the MPI launcher binding failed (status %d)\n", st);
+            return PNOL_ERR_COMM;
+        }
+    }
+    const int ws = launcher_world_size();
+    if (g_comm.kind == 0 && ws > 1) {
+        std::fprintf(stderr,
+                     "pnol_amd: this process was started by an MPI launcher with %d ranks, but no communicator is "
+                     "bound.  Call MPI_Init before the first *_MPI call and compile with <mpi.h> on the include "
+                     "path (the drop-in headers then bind MPI_COMM_WORLD), or bootstrap one with "
+                     "pnol_comm_init_rccl / pnol_comm_init_host.  A *_MPI class does not run a %d-rank job as one "
+                     "rank.\n",
+                     ws, ws);
+        return PNOL_ERR_COMM;
+    }
+    return PNOL_OK;
+}
+
 void block_range(int ncols, int nranks, int rank, int* begin, int* count) {
     // ceil-sized contiguous blocks: the padded allgather buffer is then the row-major JT itself
     int per = (ncols + nranks - 1) / nranks;
@@ -384,6 +431,7 @@ static void resolve_timers(pnol_ctx* ctx) {
 // ---------------------------------------------------------------------------------------
 static pnol_ctx* g_default = nullptr;
 static std::mutex g_default_mu;
+static int g_default_dev = -1;   // pnol_set_default_device
 
 pnol_ctx* default_ctx_or_null() {
     std::lock_guard<std::mutex> lk(g_default_mu);
@@ -391,8 +439,18 @@ pnol_ctx* default_ctx_or_null() {
     int count = 0;
     if (pnol_device_count(&count) != PNOL_OK || count == 0) return nullptr;
     int dev = 0;
-    if (const char* e = std::getenv("PNOL_DEVICE")) dev = std::atoi(e);
-    else if (const char* l = std::getenv("LOCAL_RANK")) dev = std::atoi(l) % count;
+    if (g_default_dev >= 0) dev = g_default_dev;
+    else if (const char* e = std::getenv("PNOL_DEVICE")) dev = std::atoi(e);
+    else {
+        // node-local rank of torchrun, MPICH / Intel MPI (hydra) or Open MPI
+        for (const char* k : {"LOCAL_RANK", "MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK"}) {
+            const int l = env_int(k, -1);
+            if (l >= 0) {
+                dev = l % count;
+                break;
+            }
+        }
+    }
     pnol_ctx* c = nullptr;
     if (pnol_ctx_create(dev, &c) != PNOL_OK) return nullptr;
     g_default = c;
@@ -699,6 +757,25 @@ int pnol_comm_init_host(int nranks, int rank, pnol_host_allgather_fn fn, void* u
 int pnol_comm_finalize(void) {
     if (g_comm.kind == 1 && g_comm.nccl) ncclCommDestroy(g_comm.nccl);
     g_comm = CommState();
+    return PNOL_OK;
+}
+
+int pnol_comm_set_launcher_hook(pnol_launcher_hook_fn fn) {
+    std::lock_guard<std::mutex> lk(g_launch_mu);
+    g_launch_hook = fn;
+    g_launch_bound = false;
+    return PNOL_OK;
+}
+
+int pnol_comm_bind_launcher(void) { return comm_bind_launcher(); }
+
+int pnol_launcher_world_size(void) { return launcher_world_size(); }
+
+int pnol_set_default_device(int device) {
+    if (device < 0) return PNOL_ERR_ARG;
+    std::lock_guard<std::mutex> lk(g_default_mu);
+    if (g_default) return g_default->device == device ? PNOL_OK : PNOL_ERR_ARG;
+    g_default_dev = device;
     return PNOL_OK;
 }
 
