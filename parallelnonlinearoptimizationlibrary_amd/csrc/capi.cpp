@@ -410,12 +410,12 @@ int pnol_dobj_create_synthetic(pnol_ctx* ctx, int kind, int n, int m, unsigned l
             if (hipMemcpyAsync(xstar_out, xs, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
                 st = PNOL_ERR_HIP;
         }
-        if (hipStreamSynchronize(ctx->stream) != hipSuccess) st = PNOL_ERR_HIP;
+        if (const int w = stream_wait(ctx->stream)) st = w;
         if (xs) (void)hipFree(xs);
     } else {
         st = PNOL_ERR_UNSUPPORTED;
     }
-    if (st == PNOL_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) st = PNOL_ERR_HIP;
+    if (st == PNOL_OK) st = stream_wait(ctx->stream);
     if (st != PNOL_OK) {
         pnol_dobj_destroy(o);
         return st;
@@ -489,7 +489,7 @@ int pnol_fd_gradient(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const doubl
         }
         if (cnt > 0) PNOL_HIP(hipMemcpyAsync(g, dg, sizeof(double) * cnt, hipMemcpyDeviceToHost, ctx->stream));
         PNOL_HIP(hipMemcpyAsync(f0, df, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-        PNOL_HIP(hipStreamSynchronize(ctx->stream));
+        PNOL_CHECK(stream_wait(ctx->stream));
         return PNOL_OK;
     }
     std::memcpy(st, x, sizeof(double) * n);
@@ -520,7 +520,7 @@ int pnol_fd_gradient(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const doubl
         PNOL_CHECK(launch_fd_gradient(ctx, obj, dx, dh, i0, cnt, df, dg));
     }
     PNOL_HIP(hipMemcpyAsync(st + 2 * n, dg, sizeof(double) * ((size_t)cnt + 1), hipMemcpyDeviceToHost, ctx->stream));
-    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    PNOL_CHECK(stream_wait(ctx->stream));
     if (cnt > 0) std::memcpy(g, st + 2 * n, sizeof(double) * cnt);
     *f0 = st[2 * n + cnt];
     return PNOL_OK;
@@ -544,7 +544,7 @@ int pnol_dobj_eval_batch(pnol_ctx* ctx, pnol_dobj* obj, const double* Xs, int np
     }
     PNOL_CHECK(launch_eval_batch(ctx, obj, dX, npts, dF));
     PNOL_HIP(hipMemcpyAsync(st ? st : out, dF, sizeof(double) * nout, hipMemcpyDeviceToHost, ctx->stream));
-    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    PNOL_CHECK(stream_wait(ctx->stream));
     if (st) std::memcpy(out, st, sizeof(double) * nout);
     return PNOL_OK;
 }

@@ -1013,7 +1013,10 @@ int launch_synthetic_linres(pnol_ctx* ctx, unsigned long long seed, int m, int n
 
 int lm_phased_env() {
     const char* e = std::getenv("PNOL_LM_PHASED");
-    return (e && std::atoi(e) == 0) ? 0 : 1;
+    if (e && std::atoi(e) == 0) return 0;
+    const char* s = std::getenv("PNOL_LM_SUBPHASES");   // column groups of each rank's last tile
+    const int v = s ? std::atoi(s) : kLmSubphases;
+    return std::min(8, std::max(1, v));
 }
 
 int lm_fd_mode_env() {
@@ -1037,11 +1040,23 @@ static void lm_my_rows(int m, int* r0, int* r1) {
 
 // Rank q's FD tiles in phase order: cheapest first (the latest first column: the shortest
 // prefix-shared chains), so the exchange of the early tiles runs while the expensive ones compute
-// and only the last tile's exchange is left after the FD.
-static void lm_phase_tiles(int n, int P, int q, std::vector<int>& st, std::vector<int>& ct) {
+// and only the last phase's exchange is left after the FD.  sub >= 2 cuts the last tile into
+// `sub` column groups (multiples of 16 columns, the prefix checkpoints' stride), each its own
+// launch and exchange phase: only the last group's slices are then exposed, 1/sub of a tile's
+// (the same columns, the same bits).
+static void lm_phase_tiles(int n, int P, int q, std::vector<int>& st, std::vector<int>& ct, int sub = 1) {
     fd_tiles_of(n, P, q, st, ct);   // ascending first column
     std::reverse(st.begin(), st.end());
     std::reverse(ct.begin(), ct.end());
+    if (sub < 2 || st.empty()) return;
+    const int s0 = st.back(), c = ct.back();
+    const int w = std::max(16, (c / sub + 15) / 16 * 16);
+    st.pop_back();
+    ct.pop_back();
+    for (int a = 0; a < c; a += w) {
+        st.push_back(s0 + a);
+        ct.push_back(std::min(w, c - a));
+    }
 }
 
 static int lm_comm_stream(pnol_ctx* ctx, int nphase) {
@@ -1089,17 +1104,17 @@ int launch_lm_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
         return launch_fd_jacobian_tiles(ctx, o, x, h, st.data(), ct.data(), (int)st.size(), F0, compute_f0, JTs, 0,
                                         mS, 1, mS, sstr);
     }
+    // ctx->lm_phased (read once per LevMarqMPI solve and agreed over the ranks): 0 (PNOL_LM_PHASED=0)
+    // one tile-list launch, then every tile's slices in one exchange on the context stream after
+    // it -- no second stream, no events; S >= 1 one launch and exchange phase per tile, the last
+    // tile cut into S column groups (PNOL_LM_SUBPHASES); the same bits either way
+    if (ctx->lm_phased < 0) ctx->lm_phased = lm_phased_env();
     std::vector<std::vector<int>> pst(P), pct(P);
     int nphase = 0;
     for (int q = 0; q < P; ++q) {
-        lm_phase_tiles(n, P, q, pst[q], pct[q]);
+        lm_phase_tiles(n, P, q, pst[q], pct[q], ctx->lm_phased);
         nphase = std::max(nphase, (int)pst[q].size());
     }
-    // PNOL_LM_PHASED=0 (read once per LevMarqMPI solve and agreed over the ranks, ctx->lm_phased):
-    // one tile-list launch, then every tile's slices in one exchange on the context stream after
-    // it -- no second stream, no events; the same bits (the phased form's RCCL transport first
-    // runs on a multi-GPU node)
-    if (ctx->lm_phased < 0) ctx->lm_phased = lm_phased_env();
     if (ctx->lm_phased == 0) {
             const int mine = (int)pst[me].size();
             PNOL_CHECK(launch_fd_jacobian_tiles(ctx, o, x, h, pst[me].data(), pct[me].data(), mine, F0, compute_f0,

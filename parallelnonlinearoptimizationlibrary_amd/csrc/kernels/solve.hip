@@ -269,7 +269,7 @@ int launch_matrix_inverse(pnol_ctx* ctx, const double* B, int ldb, int n, double
     PNOL_CHECK(launch_check());
     int h = 0;
     PNOL_HIP(hipMemcpyAsync(&h, di, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    PNOL_CHECK(stream_wait(ctx->stream));
     if (info_host) *info_host = h;
     return PNOL_OK;
 }
@@ -313,7 +313,7 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
             PNOL_CHECK(launch_chol_solve_v(ctx, A, lda, rhs, sigma, n, dinfo, attempt == 0 ? variant : 4));
             int hinfo = 0;
             PNOL_HIP(hipMemcpyAsync(&hinfo, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-            PNOL_HIP(hipStreamSynchronize(ctx->stream));
+            PNOL_CHECK(stream_wait(ctx->stream));
             if (hinfo == 0) {
                 if (info) *info = 1;
                 return PNOL_OK;
@@ -328,7 +328,7 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
     PNOL_CHECK(lu_solve(ctx, A, lda, rhs, sigma, n, dinfo));
     int hinfo = 0;
     PNOL_HIP(hipMemcpyAsync(&hinfo, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    PNOL_CHECK(stream_wait(ctx->stream));
     if (info) *info = hinfo;
     return PNOL_OK;
 }

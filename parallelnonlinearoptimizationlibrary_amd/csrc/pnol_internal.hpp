@@ -69,8 +69,9 @@ struct pnol_ctx {
     // LevMarqMPI's FD decomposition (fd.hip): -1 = not chosen yet (PNOL_LM_FD at first use),
     // 0 = columns (the reference's: FD column tiles per rank + the m-slice exchange), 1 = rows
     int lm_fd_mode = -1;
-    // PNOL_LM_PHASED (columns mode's phased slice exchange; 1 default, 0 one exchange after one
-    // FD launch): read once per LevMarqMPI solve and agreed over the ranks (-1: read at first use)
+    // columns mode's slice exchange (lm_phased_env: 0 one exchange after one FD launch
+    // (PNOL_LM_PHASED=0), S >= 1 a phase per tile with the last tile in S column groups
+    // (PNOL_LM_SUBPHASES)): read once per LevMarqMPI solve and agreed over the ranks (-1: at first use)
     int lm_phased = -1;
     bool lm_fd_mode_set = false;   // set by pnol_lm_set_fd_mode: the LevMarqMPI drop-in keeps it
     // What the last LM trip without A (launch_fd_normal_solve / launch_lm_normal_solve) left for
@@ -310,6 +311,9 @@ int launch_fill(pnol_ctx* ctx, double* p, size_t count, double value);
 // kLmSlices ranks with bitwise the one-GPU A.  Sliced J^T layout: slice s is an n x mS
 // row-major block at JTs + s * n * mS (FD column j, rows [s mS, (s + 1) mS) of J).
 constexpr int kLmSlices = 8;
+// columns mode: each rank's last FD tile is launched and exchanged as this many column groups
+// (PNOL_LM_SUBPHASES overrides), so only the last group's m-slices are exposed after the FD
+constexpr int kLmSubphases = 2;
 inline int lm_slice_rows(int m) { return (((m + kLmSlices - 1) / kLmSlices) + 63) / 64 * 64; }
 // rank r of P (<= kLmSlices) holds slices [floor(r 8 / P), floor((r + 1) 8 / P))
 inline void lm_rank_slices(int P, int r, int* s0, int* s1) {
@@ -335,7 +339,11 @@ int launch_lm_eval(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* F);
 // and checks it equal on every rank.
 bool lm_rows_mode(pnol_ctx* ctx);
 int lm_fd_mode_env();
-int lm_phased_env();   // PNOL_LM_PHASED (0 or 1)
+// host waits bounded while an RCCL communicator is bound (runtime.cpp): PNOL_ERR_COMM after
+// ncclCommAbort when an exchange fails or stalls past PNOL_COMM_TIMEOUT_S
+int stream_wait(hipStream_t st);
+int event_wait(hipEvent_t ev);
+int lm_phased_env();   // PNOL_LM_PHASED / PNOL_LM_SUBPHASES (0 unphased, else the last tile's groups)
 
 // Timer events that do not bracket one stream: timer_event records an event on `stream` when
 // the timer `name` is on (nullptr otherwise); timer_pair books (a, b) under `name` -- elapsed

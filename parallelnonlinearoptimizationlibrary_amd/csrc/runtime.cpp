@@ -5,6 +5,7 @@
 // RCCL (one process per GPU, xGMI) or a caller-supplied host allgather (tests / host objectives).
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 
@@ -22,7 +23,7 @@ int ws_get(pnol_ctx* ctx, const char* key, size_t bytes, void** out, bool* fresh
     if (slot.second < bytes) {
         if (fresh) *fresh = true;   // new contents, even when the allocator hands back the old address
         if (slot.first) {
-            PNOL_HIP(hipStreamSynchronize(ctx->stream));
+            PNOL_CHECK(stream_wait(ctx->stream));
             PNOL_HIP(hipFree(slot.first));
             slot.first = nullptr;
             slot.second = 0;
@@ -60,6 +61,7 @@ struct CommState {
     int kind = 0;   // 0 none (single process), 1 rccl, 2 host callback
     int nranks = 1, rank = 0;
     ncclComm_t nccl = nullptr;
+    bool dead = false;   // aborted after a stuck or failed exchange: every later collective fails
     pnol_ctx* ctx = nullptr;
     pnol_host_allgather_fn fn = nullptr;
     void* user = nullptr;
@@ -116,6 +118,67 @@ int comm_bind_launcher() {
     return PNOL_OK;
 }
 
+// Bounded host waits.  With an RCCL communicator bound, a stuck exchange (a peer that died or
+// never posted its side) would hang the blocking HIP wait forever: every host wait of the
+// library then polls the stream / event, checks ncclCommGetAsyncError every millisecond, and
+// past PNOL_COMM_TIMEOUT_S seconds (default 300) aborts the communicator (ncclCommAbort) and
+// returns PNOL_ERR_COMM, so the job fails with an error instead of hanging.  Without RCCL the
+// waits are the plain HIP ones.
+static double comm_timeout_s() {   // read per wait (cheap beside a wait; tests change it)
+    const char* e = std::getenv("PNOL_COMM_TIMEOUT_S");
+    const double v = e ? std::atof(e) : 0.0;
+    return v > 0.0 ? v : 300.0;
+}
+
+static int comm_abort(const char* why) {
+    std::fprintf(stderr, "[pnol_amd] rank %d of %d: %s; aborting the RCCL communicator\n", g_comm.rank, g_comm.nranks,
+                 why);
+    if (g_comm.nccl) (void)ncclCommAbort(g_comm.nccl);
+    g_comm.nccl = nullptr;
+    g_comm.dead = true;
+    return PNOL_ERR_COMM;
+}
+
+template <class Q>
+static int bounded_poll(Q query) {
+    const double limit = comm_timeout_s();
+    const auto t0 = std::chrono::steady_clock::now();
+    auto last = t0;
+    for (;;) {
+        const hipError_t q = query();
+        if (q == hipSuccess) return PNOL_OK;
+        if (q != hipErrorNotReady) return PNOL_ERR_HIP;
+        const auto now = std::chrono::steady_clock::now();
+        if (now - last >= std::chrono::milliseconds(1)) {
+            last = now;
+            ncclResult_t ae = ncclSuccess;
+            if (g_comm.nccl && ncclCommGetAsyncError(g_comm.nccl, &ae) == ncclSuccess && ae != ncclSuccess &&
+                ae != ncclInProgress)
+                return comm_abort(ncclGetErrorString(ae));
+            if (std::chrono::duration<double>(now - t0).count() > limit)
+                return comm_abort("a device wait with RCCL operations in flight passed PNOL_COMM_TIMEOUT_S");
+        }
+    }
+}
+
+int stream_wait(hipStream_t st) {
+    if (g_comm.kind != 1 || !g_comm.nccl) return hipStreamSynchronize(st) == hipSuccess ? PNOL_OK : PNOL_ERR_HIP;
+    return bounded_poll([st] { return hipStreamQuery(st); });
+}
+
+int event_wait(hipEvent_t ev) {
+    if (g_comm.kind != 1 || !g_comm.nccl) {
+        for (;;) {   // busy-poll (a blocking wait returns tens of microseconds late)
+            const hipError_t q = hipEventQuery(ev);
+            if (q == hipSuccess) return PNOL_OK;
+            if (q != hipErrorNotReady) return PNOL_ERR_HIP;
+        }
+    }
+    return bounded_poll([ev] { return hipEventQuery(ev); });
+}
+
+bool comm_dead() { return g_comm.kind == 1 && g_comm.dead; }
+
 void block_range(int ncols, int nranks, int rank, int* begin, int* count) {
     // ceil-sized contiguous blocks: the padded allgather buffer is then the row-major JT itself
     int per = (ncols + nranks - 1) / nranks;
@@ -156,6 +219,7 @@ int comm_share_rows(pnol_ctx* ctx, double* buf, size_t ld, int ncols) {
     if (g_comm.kind == 0 || P == 1) return PNOL_OK;
     const int nt = (ncols + kFdTileCols - 1) / kFdTileCols;
     if (g_comm.kind == 1) {
+        if (!g_comm.nccl) return PNOL_ERR_COMM;
         ScopedTimer tm(ctx, "allgather");
         if (ncclGroupStart() != ncclSuccess) return PNOL_ERR_COMM;
         for (int t = 0; t < nt; ++t) {
@@ -206,6 +270,7 @@ int comm_exchange(pnol_ctx* ctx, const double* sbase, double* rbase,
     const hipStream_t st = stream_ ? (hipStream_t)stream_ : ctx->stream;
     std::vector<XBlock> bl;
     if (g_comm.kind == 1) {
+        if (!g_comm.nccl) return PNOL_ERR_COMM;
         if (ncclGroupStart() != ncclSuccess) return PNOL_ERR_COMM;
         bool ok = true;
         for (int d = 0; d < P && ok; ++d) {
@@ -229,7 +294,7 @@ int comm_exchange(pnol_ctx* ctx, const double* sbase, double* rbase,
     // slot of the largest rank's size; one allgather; receivers pick their blocks out.  The
     // host waits for `st` anyway (the allgather below): first for its earlier copies, so a
     // scratch regrow cannot free a buffer they still read.
-    PNOL_HIP(hipStreamSynchronize(st));
+    PNOL_CHECK(stream_wait(st));
     auto out_size = [&](int q) {
         size_t t = 0;
         for (int d = 0; d < P; ++d) {
@@ -300,7 +365,7 @@ int comm_allgather_host(pnol_ctx* ctx, const double* send, double* recv, size_t 
     PNOL_HIP(hipMemcpyAsync(ds, send, sizeof(double) * count, hipMemcpyHostToDevice, ctx->stream));
     PNOL_CHECK(comm_allgather_device(ctx, (const double*)ds, (double*)dr, count));
     PNOL_HIP(hipMemcpyAsync(recv, dr, sizeof(double) * count * g_comm.nranks, hipMemcpyDeviceToHost, ctx->stream));
-    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    PNOL_CHECK(stream_wait(ctx->stream));
     return PNOL_OK;
 }
 
@@ -311,6 +376,7 @@ int comm_allgather_device(pnol_ctx* ctx, const double* send, double* recv, size_
         return PNOL_OK;
     }
     if (g_comm.kind == 1) {
+        if (!g_comm.nccl) return PNOL_ERR_COMM;
         ScopedTimer tm(ctx, "allgather", st);
         if (ncclAllGather(send, recv, count, ncclDouble, g_comm.nccl, st) != ncclSuccess) return PNOL_ERR_COMM;
         return PNOL_OK;
@@ -318,10 +384,10 @@ int comm_allgather_device(pnol_ctx* ctx, const double* send, double* recv, size_
     // host backend with device buffers: bounce through host memory
     std::vector<double> hs(count), hr(count * (size_t)g_comm.nranks);
     PNOL_HIP(hipMemcpyAsync(hs.data(), send, sizeof(double) * count, hipMemcpyDeviceToHost, st));
-    PNOL_HIP(hipStreamSynchronize(st));
+    PNOL_CHECK(stream_wait(st));
     if (g_comm.fn(hs.data(), hr.data(), sizeof(double) * count, g_comm.user) != 0) return PNOL_ERR_COMM;
     PNOL_HIP(hipMemcpyAsync(recv, hr.data(), sizeof(double) * hr.size(), hipMemcpyHostToDevice, st));
-    PNOL_HIP(hipStreamSynchronize(st));
+    PNOL_CHECK(stream_wait(st));
     return PNOL_OK;
 }
 
@@ -566,7 +632,7 @@ int pnol_ctx_destroy(pnol_ctx* ctx) {
 
 int pnol_ctx_synchronize(pnol_ctx* ctx) {
     if (!ctx) return PNOL_ERR_ARG;
-    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    PNOL_CHECK(stream_wait(ctx->stream));
     return PNOL_OK;
 }
 
@@ -638,7 +704,7 @@ int pnol_memcpy_h2d(pnol_ctx* ctx, void* dst, const void* src, size_t bytes) {
     } else {
         PNOL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
     }
-    PNOL_HIP(hipStreamSynchronize(ctx->stream));
+    PNOL_CHECK(stream_wait(ctx->stream));
     return PNOL_OK;
 }
 
@@ -647,11 +713,11 @@ int pnol_memcpy_d2h(pnol_ctx* ctx, void* dst, const void* src, size_t bytes) {
     if (!bytes) return PNOL_OK;
     if (void* st = pinned_stage(ctx, bytes)) {
         PNOL_HIP(hipMemcpyAsync(st, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
-        PNOL_HIP(hipStreamSynchronize(ctx->stream));
+        PNOL_CHECK(stream_wait(ctx->stream));
         std::memcpy(dst, st, bytes);
     } else {
         PNOL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
-        PNOL_HIP(hipStreamSynchronize(ctx->stream));
+        PNOL_CHECK(stream_wait(ctx->stream));
     }
     return PNOL_OK;
 }
@@ -702,11 +768,7 @@ int pnol_event_record(pnol_ctx* ctx, pnol_event* ev) {
 // tens of microseconds late, which the LM loop pays on every trip).
 int pnol_event_wait(pnol_event* ev) {
     if (!ev) return PNOL_ERR_ARG;
-    for (;;) {
-        const hipError_t q = hipEventQuery(ev->e);
-        if (q == hipSuccess) return PNOL_OK;
-        if (q != hipErrorNotReady) return PNOL_ERR_HIP;
-    }
+    return event_wait(ev->e);
 }
 
 int pnol_event_destroy(pnol_event* ev) {

@@ -388,3 +388,15 @@ def test_rccl_selfcheck_world1():
     assert r.returncode == 0, out[-3000:]
     assert "RCCL self-check ok=True" in out
     assert "host-communicator fallback ok=True" in out
+
+
+def test_rccl_stuck_wait_is_bounded():
+    """A device wait with an RCCL communicator bound is bounded: a stream blocked past
+    PNOL_COMM_TIMEOUT_S returns PNOL_ERR_COMM after ncclCommAbort, and later collectives fail
+    with PNOL_ERR_COMM -- a stuck exchange on a multi-GPU node ends in an error, not a hang
+    (tools/rccl_timeout_probe.py, one rank on the box's GPU)."""
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(HERE), "tools", "rccl_timeout_probe.py")],
+                       capture_output=True, timeout=180)
+    out = r.stdout.decode(errors="replace") + r.stderr.decode(errors="replace")
+    assert r.returncode == 0, out[-3000:]
+    assert "RCCL bounded wait ok=True" in out
