@@ -29,11 +29,19 @@ L.check(lib.pnol_ctx_get_stream(ctx, C.byref(stream)), "get_stream")
 hip.hipStreamWaitValue32.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint, C.c_uint32]
 rc_wait = hip.hipStreamWaitValue32(stream, word, 1, 0, 0xFFFFFFFF)   # 0 = hipStreamWaitValueGte
 assert rc_wait == 0, f"hipStreamWaitValue32 -> {rc_wait}"
+# The stream-wait packet stands in for an RCCL kernel waiting on a peer that never comes.  A real
+# one exits when ncclCommAbort raises the communicator's abort flag; a wait packet does not, and
+# the abort's own device synchronisation waits for the stream -- so a timer thread releases the
+# word 3 s in (after the 1 s deadline has fired), which lets the abort complete.
+import threading  # noqa: E402
+rel = threading.Timer(3.0, lambda: flag.__setitem__(0, 1))
+rel.start()
 try:
     t0 = time.time()
     st = lib.pnol_ctx_synchronize(ctx)
     dt = time.time() - t0
 finally:
+    rel.join()
     flag[0] = 1   # release the stream whatever happened
 rc_after = lib.pnol_ctx_synchronize(ctx)
 dev = C.c_void_p()
