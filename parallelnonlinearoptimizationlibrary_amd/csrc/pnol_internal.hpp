@@ -313,7 +313,7 @@ int launch_fill(pnol_ctx* ctx, double* p, size_t count, double value);
 constexpr int kLmSlices = 8;
 // columns mode: each rank's last FD tile is launched and exchanged as this many column groups
 // (PNOL_LM_SUBPHASES overrides), so only the last group's m-slices are exposed after the FD
-constexpr int kLmSubphases = 2;
+constexpr int kLmSubphases = 1;
 inline int lm_slice_rows(int m) { return (((m + kLmSlices - 1) / kLmSlices) + 63) / 64 * 64; }
 // rank r of P (<= kLmSlices) holds slices [floor(r 8 / P), floor((r + 1) 8 / P))
 inline void lm_rank_slices(int P, int r, int* s0, int* s1) {
