@@ -495,21 +495,10 @@ int pnol_fd_gradient(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const doubl
     std::memcpy(st, x, sizeof(double) * n);
     // the step vector rarely changes between calls (a solver's dX): it is staged and sent only
     // when its content differs from the copy on the device (compared while it is staged)
-    bool same = ctx->fdg_h_dev == dh && ctx->fdg_h_host.size() == n;
-    {
-        double* sh = st + n;
-        const double* prev = ctx->fdg_h_host.data();
-        if (same) {
-            bool diff = false;
-            for (size_t i = 0; i < n; ++i) {
-                sh[i] = h[i];
-                diff |= std::memcmp(&h[i], &prev[i], sizeof(double)) != 0;
-            }
-            same = !diff;
-        } else {
-            std::memcpy(sh, h, sizeof(double) * n);
-        }
-    }
+    // (one memcmp of the whole vector: a solver's steps are the same call after call)
+    bool same = ctx->fdg_h_dev == dh && ctx->fdg_h_host.size() == n &&
+                std::memcmp(h, ctx->fdg_h_host.data(), sizeof(double) * n) == 0;
+    if (!same) std::memcpy(st + n, h, sizeof(double) * n);
     PNOL_HIP(hipMemcpyAsync(dx, st, sizeof(double) * (same ? n : 2 * n), hipMemcpyHostToDevice, ctx->stream));
     if (!same) {
         ctx->fdg_h_host.assign(h, h + n);

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <chrono>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -98,6 +99,19 @@ class PhaseClock {
     double* acc_;
     std::chrono::steady_clock::time_point t0_;
 };
+
+// PNOL_BND_DETAIL=1: where the host time of the device Recur FD gradient goes (diagnostics):
+// the full point / step build, the same-point check, the device call (copies + kernels), the
+// host re-evaluations of a reuse, and the gather / cache bookkeeping
+enum RecurDetail { kRdBuild = 0, kRdCheck, kRdDevice, kRdRedo, kRdGather, kRdCount };
+inline double* recur_detail(int k) {
+    static const bool on = [] {
+        const char* e = std::getenv("PNOL_BND_DETAIL");
+        return e && std::atoi(e) != 0;
+    }();
+    thread_local double slots[kRdCount];
+    return on ? &slots[k] : nullptr;
+}
 
 // slots of a solve profile (8 doubles)
 enum ProfileSlot { kProfIters = 0, kProfTotal, kProfGrad, kProfLineSearch, kProfUpdate, kProfPoints, kProfGradCalls,

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "PNOL_Objective.hpp"
+#include "recur_simd.hpp"
 
 namespace pnol {
 
@@ -40,21 +41,9 @@ inline void eval_line_points_recur(Objective* o, const std::vector<double>& X, c
     const int nf = (int)cX.size();
     thread_local std::vector<double> pts;   // kept across calls (two per bounded BFGS iteration)
     pts.resize((size_t)na * nf);
-    // branch-free (the frozen pattern follows the active set: unpredictable); the free index
-    // advances by !frozen and is clamped, so the unused operand of a frozen entry stays in bounds
-    const size_t nr = X.size(), last = nr > 0 ? nr - 1 : 0;
-    for (int k = 0; k < na; ++k) {
-        double* row = pts.data() + (size_t)k * nf;
-        const double a = alphas[k];
-        size_t r = 0;
-        for (int i = 0; i < nf; ++i) {
-            const bool c = cI[i];
-            const size_t q = r < last ? r : last;
-            const double v = nr > 0 ? X[q] + a * p[q] : 0.0;
-            row[i] = c ? cX[i] : v;
-            r += !c;
-        }
-    }
+    // recur::scatter: AVX-512 expand where the host has it, else the branch-free walk (the
+    // frozen pattern follows the active set: unpredictable) with the clamped free index
+    for (int k = 0; k < na; ++k) recur::scatter(pts.data() + (size_t)k * nf, X, p.data(), alphas[k], cX, cI);
     o->objEvalBatch(pts.data(), na, nf, f);
 }
 

@@ -16,6 +16,7 @@
 #include "../pnol_comm.hpp"
 #include "../pnol_internal.hpp"
 #include "PNOL_Objective.hpp"
+#include "recur_simd.hpp"
 #include "device_util.hpp"
 #include "scalar_host.hpp"
 
@@ -65,6 +66,10 @@ void device_gradient(pnol_dobj* d, const std::vector<double>& X, const std::vect
 std::vector<double> scatter_full(const std::vector<double>& Xr, const std::vector<double>& cX,
                                  const std::vector<bool>& cI) {
     std::vector<double> X(cX.size());
+    if (recur::free_count(cI) == Xr.size() && !Xr.empty()) {
+        recur::scatter(X.data(), Xr, nullptr, 0.0, cX, cI);
+        return X;
+    }
     size_t ir = 0;
     for (size_t i = 0; i < cX.size(); ++i) X[i] = cI[i] ? cX[i] : Xr[ir++];
     return X;
@@ -223,26 +228,17 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
         // perturbed point equals the reference's scatter(X + dX_i e_i) bit for bit.  One pass
         // builds both (frozen coordinates: their constant and a dummy step 1.0), in buffers kept
         // across calls (the bounded solvers call this twice per iteration at full length).
-        // Branch-free: which coordinates are frozen follows the active set, which looks random
-        // to a branch predictor (a mispredicted branch per few coordinates was ~30 us per pass
-        // at n = 16384); the reduced index advances by !frozen (X, dX read one past their end
-        // at most through the clamp, never used).
+        // recur_simd.hpp: eight entries per AVX-512 expand (the frozen pattern follows the active
+        // set, which looks random to a branch predictor; the scalar fallback is branch-free).
         const size_t nf = constantX.size();
+        PhaseClock t_build(recur_detail(kRdBuild));
         thread_local std::vector<double> Xf, hf, gf, gr;
         Xf.resize(nf);
         hf.resize(nf);
         gf.resize(nf);
         gr.resize(nf + 1);
-        const size_t last = N > 0 ? (size_t)N - 1 : 0;
-        size_t ir = 0;
-        for (size_t i = 0; i < nf; ++i) {
-            const bool c = constantIndicator[i];
-            const size_t k = ir < last ? ir : last;
-            const double xr = N > 0 ? X[k] : 0.0, hr = N > 0 ? dX[k] : 1.0;
-            Xf[i] = c ? constantX[i] : xr;
-            hf[i] = c ? 1.0 : hr;
-            ir += !c;
-        }
+        recur::scatter(Xf.data(), X, nullptr, 0.0, constantX, constantIndicator);
+        recur::scatter_steps(hf.data(), dX, constantIndicator);
         // Same-point reuse: the bounded solvers' recursion unwinds through one level per frozen
         // coordinate, and every level asks for the gradient at the SAME full point (its free
         // coordinates are a superset of the level below's; BFGS_bnd_linesearch.cpp:620-650).
@@ -256,6 +252,8 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
         // Only kinds whose host formula is bitwise the device's (host_bitwise_kind: PowerObject
         // with power != 2 calls pow, which may not be); the evaluation count is the reference's
         // N + 1.
+        t_build.stop();
+        PhaseClock t_check(recur_detail(kRdCheck));
         RecurCache& rc = recur_cache();
         const bool pure = host_bitwise_kind(d->kind, d->power);
         std::vector<int>& redo = rc.redo;
@@ -263,12 +261,13 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
         bool reuse = pure && rc.oid == d->id && rc.Xf.size() == nf &&
                      std::memcmp(rc.Xf.data(), Xf.data(), sizeof(double) * nf) == 0;
         if (reuse) {
-            for (size_t i = 0; i < nf && redo.size() <= kRecurRedoMax; ++i)
-                if (!constantIndicator[i] && std::memcmp(&rc.hf[i], &hf[i], sizeof(double)) != 0) redo.push_back((int)i);
+            recur::free_diffs(rc.hf.data(), hf.data(), constantIndicator, kRecurRedoMax, redo);
             reuse = redo.size() <= kRecurRedoMax;
         }
+        t_check.stop();
         const double* gsrc = gf.data();   // this call's per-coordinate values
         if (reuse) {
+            PhaseClock t_redo(recur_detail(kRdRedo));
             gsrc = rc.gf.data();
             const int k = (int)redo.size();
             if (k > 0) {
@@ -291,8 +290,11 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
             }
             countEvals(N + 1);
         } else {
+            PhaseClock t_dev(recur_detail(kRdDevice));
             double F = 0;
             device_gradient(d, Xf, hf, 0, (int)nf, &F, gf.data());
+            t_dev.stop();
+            PhaseClock t_keep(recur_detail(kRdGather));
             countEvals(N + 1);
             if (pure) {
                 if (rc.oid != d->id) {   // the objective's data, once per objective
@@ -314,12 +316,17 @@ void Objective::gradientApproximationRecur(vector<double>& X, vector<double>& dX
                 if (d->kind == PNOL_OBJ_QUADRATIC && (rc.p0h.size() < nf || rc.p1h.size() < nf)) rc.oid = 0;
             }
         }
-        ir = 0;
-        for (size_t i = 0; i < nf; ++i) {
-            gr[ir] = gsrc[i];
-            ir += !constantIndicator[i];
+        PhaseClock t_gather(recur_detail(kRdGather));
+        if (recur::free_count(constantIndicator) == (size_t)N) {
+            recur::gather(dFdX.data(), gsrc, constantIndicator);
+        } else {   // a fallback walk's mismatched lengths: the scalar gather, slot for slot
+            size_t ir = 0;
+            for (size_t i = 0; i < nf; ++i) {
+                gr[ir] = gsrc[i];
+                ir += !constantIndicator[i];
+            }
+            std::copy(gr.begin(), gr.begin() + N, dFdX.begin());
         }
-        std::copy(gr.begin(), gr.begin() + N, dFdX.begin());
         return;
     }
     std::vector<double> v(N + 1);

@@ -2,6 +2,7 @@
 gradientApproximationMPI with a C callback objective): no GPU needed, bitwise vs the oracle
 (PNOL_Objective.cpp:165-299)."""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -117,3 +118,25 @@ def test_host_ga_plateau_terminates(tmp_path, which):
     r = subprocess.run([sys.executable, str(s), root, str(which)], capture_output=True, timeout=120)
     assert r.returncode == 0, r.stderr.decode(errors="replace")[-2000:]
     assert b"generations" in r.stdout
+
+
+def test_recur_simd_matches_scalar_walks(tmp_path):
+    """csrc/host/recur_simd.hpp (the bounded solvers' frozen-coordinate scatter / gather, AVX-512
+    expand / compress where the host has it) is bitwise the scalar walks it replaces: random
+    indicator patterns, tail blocks, all-frozen / all-free words, mismatched reduced lengths."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "recur_simd_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I",
+                    os.path.join(root, "parallelnonlinearoptimizationlibrary_amd", "csrc", "host"),
+                    os.path.join(root, "tests", "cpp", "recur_simd_check.cpp"), "-o", exe], check=True, timeout=120)
+    for scalar in ("0", "1"):   # the AVX-512 paths (where the host has them), then the scalar walks
+        env = dict(os.environ)
+        env.pop("PNOL_NO_AVX512", None)
+        if scalar == "1":
+            env["PNOL_NO_AVX512"] = "1"
+        r = subprocess.run([exe], capture_output=True, timeout=120, env=env)
+        assert r.returncode == 0, (r.stdout + r.stderr).decode()[-2000:]
+        assert "fails=0" in r.stdout.decode()
+        if scalar == "1":
+            assert "avx512=0" in r.stdout.decode()
