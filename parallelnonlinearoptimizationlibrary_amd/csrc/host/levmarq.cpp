@@ -329,6 +329,7 @@ class LMAsync {
             check(pnol_jtr_d(ctx_, JT_.get(), ldjt_, m_, n_, F(s), rhs_.get()), "jtr");
         }
         int info = 0;
+        if (action == 1) ctx_->chol_order0 = true;   // a timed-out wait: step-order claims from now on
         const int st = pnol_solve_d(ctx_, A_.get(), lda_, rhs_.get(), sig(s), n_, action == 2 ? 2 : 0, &info);
         if (agree_) {
             // a relaunch budget exhausted on one rank only must fail every rank alike: its peers

@@ -21,6 +21,7 @@
 // kCholTimeout and the host relaunches the same factorisation (bitwise the same result), never
 // the LU -- a timeout is a scheduling event, not a property of A.
 #include "../pnol_internal.hpp"
+#include "../pnol_comm.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -2019,8 +2020,13 @@ static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, i
     const int lookahead = el ? std::max(0, std::atoi(el)) : 48;
     RedArgs rp = red;
     {
+        // order 1 (each step's critical tasks a step early) lets up to four workers wait on tasks
+        // nobody has claimed yet, so it needs more than four workers resident.  A GPU shared by
+        // several processes may hold fewer (a 4-process run at cfg 3 stalled one trip until the
+        // spin cap, profiles/r06_chol_contention_4p_cfg3.json): ranks sharing the GPU over the
+        // host backend, and a context that has seen a timed-out wait, claim in step order.
         const char* eo = std::getenv("PNOL_CHOL_ORDER");
-        rp.order = eo ? (std::atoi(eo) != 0 ? 1 : 0) : 1;
+        rp.order = eo ? (std::atoi(eo) != 0 ? 1 : 0) : ((ctx->chol_order0 || comm_shares_device()) ? 0 : 1);
     }
     const int slots = std::max(ctx->num_cu, 1) - 1;
     const int want = ew ? std::atoi(ew) : slots;

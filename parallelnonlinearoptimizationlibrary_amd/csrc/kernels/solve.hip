@@ -319,6 +319,7 @@ int launch_solve(pnol_ctx* ctx, double* A, int lda, const double* rhs, double* s
                 return PNOL_OK;
             }
             if (hinfo != kCholTimeout) break;   // a non-positive or NaN pivot: the LU below
+            ctx->chol_order0 = true;            // the persistent launches claim in step order from now on
             std::fprintf(stderr, "[pnol_amd] tile Cholesky (n = %d): a dependency wait ran past its cap, relaunch %d\n",
                          n, attempt + 1);
             if (attempt >= kRelaunch) return PNOL_ERR_TIMEOUT;

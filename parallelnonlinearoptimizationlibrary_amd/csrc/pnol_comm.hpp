@@ -15,6 +15,8 @@ int comm_rank();
 // first); PNOL_ERR_COMM when a multi-rank launch has no communicator
 int comm_bind_launcher();
 int launcher_world_size();
+// ranks sharing one GPU (the host backend with several ranks)
+bool comm_shares_device();
 // contiguous ceil-sized column block of `rank`
 void block_range(int ncols, int nranks, int rank, int* begin, int* count);
 // cost-balanced FD column tiles (PNOL_FD_TILE columns each, dealt in snake order)

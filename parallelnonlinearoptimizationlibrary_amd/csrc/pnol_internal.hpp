@@ -63,6 +63,10 @@ struct pnol_ctx {
     int chol_tasks_T = 0;
     int* chol4_flags = nullptr;     // method-4 Cholesky: per-row panel flags + backward-solve flags
     int chol4_cap = 0;              // tile rows the flag buffer holds (2 * cap ints)
+    // a persistent Cholesky's dependency wait ran past its cap on this context (the GPU is shared
+    // with other processes, so fewer workers are resident than launched): from then on its
+    // workers claim in step order (order 0, which drains with any co-residency)
+    bool chol_order0 = false;
     int chol4_epoch = 0;            // last flag value handed out (monotonic; flags reset on regrow)
     hipStream_t aux_stream = nullptr;   // second stream (J^T J rows beside the FD chunks), lazily created
     std::vector<hipEvent_t> aux_events; // chunk-done events between the two streams

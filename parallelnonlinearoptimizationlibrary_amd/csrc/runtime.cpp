@@ -179,6 +179,9 @@ int event_wait(hipEvent_t ev) {
 
 bool comm_dead() { return g_comm.kind == 1 && g_comm.dead; }
 
+// several ranks over the host backend: the tests' and a one-GPU MPI launch's ranks share a GPU
+bool comm_shares_device() { return g_comm.kind == 2 && g_comm.nranks > 1; }
+
 void block_range(int ncols, int nranks, int rank, int* begin, int* count) {
     // ceil-sized contiguous blocks: the padded allgather buffer is then the row-major JT itself
     int per = (ncols + nranks - 1) / nranks;
