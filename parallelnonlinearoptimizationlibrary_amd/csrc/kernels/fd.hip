@@ -247,11 +247,19 @@ __device__ __forceinline__ double chain_sum(double f, const double* __restrict__
     return f;
 }
 
-template <int KIND>
+// FUSED (the default): one launch instead of three -- each workgroup forms the base terms of
+// its LDS chunks itself (scalar_term, the k_scalar_terms values; T unused), and the last workgroup
+// to finish forms g_p = (vals_p - F) / h_{i0 + p} and f0 = F as k_scalar_fd_finish does (the
+// guide's in-launch hand-off: every wave's vmcnt(0), the barrier, lane 0's agent release and
+// vmcnt(0), a relaxed agent add on `done`; the last arriver's agent acquire; it zeroes `done`
+// again).  Same values, two launches and their gaps fewer per gradient.
+template <int KIND, bool FUSED = false>
 __global__ __launch_bounds__(256) void k_scalar_fd_chain(const double* __restrict__ x, const double* __restrict__ h,
                                                          int n, int i0, int cnt, const double* __restrict__ p0,
                                                          const double* __restrict__ p1, double power,
-                                                         const double* __restrict__ T, double* __restrict__ vals) {
+                                                         const double* __restrict__ T, double* __restrict__ vals,
+                                                         int* __restrict__ done = nullptr, double* __restrict__ f0 = nullptr,
+                                                         double* __restrict__ g = nullptr) {
     __shared__ __attribute__((aligned(16))) double Ts[2][kTermChunk];
     constexpr int kPer = kTermChunk / 2 / 256;   // double2 loads per thread per chunk
     const int lane = threadIdx.x & 63;
@@ -280,7 +288,17 @@ __global__ __launch_bounds__(256) void k_scalar_fd_chain(const double* __restric
 #pragma unroll
         for (int r = 0; r < kPer; ++r) {
             const int e = c0 + 2 * (threadIdx.x + 256 * r);
-            pre[r] = make_double2(e < nt ? T[e] : 0.0, e + 1 < nt ? T[e + 1] : 0.0);
+            if (FUSED) {
+                double t0 = 0.0, t1 = 0.0;
+                if (e < nt) {
+                    const double xe = x[e], xe1 = e + 1 < n ? x[e + 1] : 0.0;
+                    t0 = scalar_term<KIND>(e, n, xe, xe1, p0, p1, power);
+                    if (e + 1 < nt) t1 = scalar_term<KIND>(e + 1, n, xe1, e + 2 < n ? x[e + 2] : 0.0, p0, p1, power);
+                }
+                pre[r] = make_double2(t0, t1);
+            } else {
+                pre[r] = make_double2(e < nt ? T[e] : 0.0, e + 1 < nt ? T[e + 1] : 0.0);
+            }
         }
     };
     auto stash = [&](double* dst) {
@@ -310,6 +328,28 @@ __global__ __launch_bounds__(256) void k_scalar_fd_chain(const double* __restric
         __syncthreads();
     }
     if (active) vals[q] = f;
+    if constexpr (FUSED) {
+        int* last = reinterpret_cast<int*>(&Ts[0][0]);   // the chunks are done with (barrier above)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int prev = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int is_last = prev == (int)gridDim.x - 1;
+            if (is_last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            *last = is_last;
+        }
+        __syncthreads();
+        if (!*last) return;
+        const double F = vals[cnt];
+        if (threadIdx.x == 0 && f0) *f0 = F;
+        for (int p = threadIdx.x; p < cnt; p += 256) g[p] = (vals[p] - F) / h[i0 + p];
+        if (threadIdx.x == 0) __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 __global__ void k_scalar_fd_finish(const double* __restrict__ vals, const double* __restrict__ h, int i0, int cnt,
@@ -801,14 +841,29 @@ int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* 
 
 template <int KIND>
 static int launch_fd_chain(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt, double* T,
-                           double* V) {
+                           double* V, double* f0, double* g) {
+    const int waves = (cnt + 1 + 63) / 64;
+    // PNOL_FD_FUSED=0 keeps the three launches (terms, chain, finish); read once
+    static const bool fused = [] {
+        const char* e = std::getenv("PNOL_FD_FUSED");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (fused) {
+        void* dn = nullptr;
+        PNOL_CHECK(ws_get_zeroed(ctx, "fd_chain_done", sizeof(int) * 64, &dn));
+        hipLaunchKernelGGL((k_scalar_fd_chain<KIND, true>), dim3((waves + 3) / 4), dim3(256), 0, ctx->stream, x, h, o->n,
+                           i0, cnt, o->p0, o->p1, o->power, (const double*)nullptr, V, (int*)dn, f0, g);
+        return launch_check();
+    }
     const int nt = std::max(o->n - (KIND == PNOL_OBJ_ROSENBROCK ? 1 : 0), 1);
     hipLaunchKernelGGL((k_scalar_terms<KIND>), dim3(std::min((nt + 255) / 256, 1024)), dim3(256), 0, ctx->stream, x, o->n,
                        o->p0, o->p1, o->power, T);
     PNOL_CHECK(launch_check());
-    const int waves = (cnt + 1 + 63) / 64;
     hipLaunchKernelGGL((k_scalar_fd_chain<KIND>), dim3((waves + 3) / 4), dim3(256), 0, ctx->stream, x, h, o->n, i0, cnt,
                        o->p0, o->p1, o->power, (const double*)T, V);
+    PNOL_CHECK(launch_check());
+    hipLaunchKernelGGL(k_scalar_fd_finish, dim3((cnt + 255) / 256 + 1), dim3(256), 0, ctx->stream, (const double*)V, h, i0,
+                       cnt, f0, g);
     return launch_check();
 }
 
@@ -826,9 +881,9 @@ int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
         return !e || std::atoi(e) != 0;
     }();
     if (chain) {
-        if (o->kind == PNOL_OBJ_ROSENBROCK) PNOL_CHECK(launch_fd_chain<PNOL_OBJ_ROSENBROCK>(ctx, o, x, h, i0, cnt, T, V));
-        else if (o->kind == PNOL_OBJ_POWER) PNOL_CHECK(launch_fd_chain<PNOL_OBJ_POWER>(ctx, o, x, h, i0, cnt, T, V));
-        else PNOL_CHECK(launch_fd_chain<PNOL_OBJ_QUADRATIC>(ctx, o, x, h, i0, cnt, T, V));
+        if (o->kind == PNOL_OBJ_ROSENBROCK) return launch_fd_chain<PNOL_OBJ_ROSENBROCK>(ctx, o, x, h, i0, cnt, T, V, f0, g);
+        if (o->kind == PNOL_OBJ_POWER) return launch_fd_chain<PNOL_OBJ_POWER>(ctx, o, x, h, i0, cnt, T, V, f0, g);
+        return launch_fd_chain<PNOL_OBJ_QUADRATIC>(ctx, o, x, h, i0, cnt, T, V, f0, g);
     } else {
         const int blocks = (cnt + 1 + 255) / 256;
         if (o->kind == PNOL_OBJ_ROSENBROCK)
