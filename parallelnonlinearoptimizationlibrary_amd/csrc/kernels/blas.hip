@@ -574,22 +574,27 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ Dsh, lon
             const int idx = ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
             const int row = r0 + (idx & 7);
             if (row < r_end) {
-                if (idx < 8) part_u[(long)strip * n + row] = red;
-                else part_v[(long)strip * n + row] = red;
+                double* dst = (idx < 8 ? part_u : part_v) + (long)strip * n + row;
+                if (FIN) __hip_atomic_store(dst, red, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // write-through
+                else *dst = red;
             }
         }
 #pragma unroll
         for (int q = 0; q < kGroup; ++q) cur[q] = nxt[q];
         grp = gnext;
     }
-    if (c0ok) part_w[(long)rt * n + col] = w0;
-    if (c1ok) part_w[(long)rt * n + col + 1] = w1;
+    if constexpr (!FIN) {
+        if (c0ok) part_w[(long)rt * n + col] = w0;
+        if (c1ok) part_w[(long)rt * n + col + 1] = w1;
+    }
     if constexpr (FIN) {
+        // the partials are stored write-through (sc1): drained, they are visible to every XCD
+        // without a release fence (one per workgroup -- an L2 write-back each -- doubled the pass)
+        if (c0ok) __hip_atomic_store(part_w + (long)rt * n + col, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c1ok) __hip_atomic_store(part_w + (long)rt * n + col + 1, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const int nrowt = (n + prows - 1) / prows;
             __hip_atomic_fetch_add(fin.cnt + rt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add(fin.cnt + nrowt + ct, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -282,28 +282,57 @@ __global__ __launch_bounds__(256) void k_scalar_fd_chain(const double* __restric
         w0 = max(0, min(KIND == PNOL_OBJ_POWER ? jlo : jlo - 1, nt));
         w1 = max(w0, min(jhi + 1, nt));
     }
-    // chunk c of T into registers (zero past nt; only [c0, c1) is ever read)
+    // chunk c of T into registers (zero past nt; only [c0, c1) is ever read).  FUSED: the raw
+    // operands of the chunk's terms are loaded by fetch (in flight during the chain) and the terms
+    // formed by stash, after the chain -- forming them in fetch would wait for the loads there
     double2 pre[kPer];
+    struct Raw {
+        double x0, x1, x2, a0, a1, b0, b1;
+    };
+    Raw raw[FUSED ? kPer : 1];
+    int cfetch = 0;
     auto fetch = [&](int c0) {
+        cfetch = c0;
 #pragma unroll
         for (int r = 0; r < kPer; ++r) {
             const int e = c0 + 2 * (threadIdx.x + 256 * r);
-            if (FUSED) {
-                double t0 = 0.0, t1 = 0.0;
-                if (e < nt) {
-                    const double xe = x[e], xe1 = e + 1 < n ? x[e + 1] : 0.0;
-                    t0 = scalar_term<KIND>(e, n, xe, xe1, p0, p1, power);
-                    if (e + 1 < nt) t1 = scalar_term<KIND>(e + 1, n, xe1, e + 2 < n ? x[e + 2] : 0.0, p0, p1, power);
+            if constexpr (FUSED) {
+                Raw& w = raw[r];
+                w.x0 = e < n ? x[e] : 0.0;
+                w.x1 = e + 1 < n ? x[e + 1] : 0.0;
+                w.x2 = (KIND != PNOL_OBJ_POWER && e + 2 < n) ? x[e + 2] : 0.0;
+                w.a0 = w.a1 = w.b0 = w.b1 = 0.0;
+                if (KIND == PNOL_OBJ_QUADRATIC) {
+                    if (e < nt) { w.a0 = p0[e]; w.b0 = p1[e]; }
+                    if (e + 1 < nt) { w.a1 = p0[e + 1]; w.b1 = p1[e + 1]; }
                 }
-                pre[r] = make_double2(t0, t1);
             } else {
                 pre[r] = make_double2(e < nt ? T[e] : 0.0, e + 1 < nt ? T[e + 1] : 0.0);
             }
         }
     };
+    // scalar_term's expressions on the loaded operands (QUADRATIC reads p0 / p1 at the term's own
+    // index, as the copies a0 / b0, a1 / b1 hold)
+    auto form = [&](int k, double xk, double xk1, double a, double b) {
+        if (KIND == PNOL_OBJ_QUADRATIC) {
+            double t = (0.5 * a * xk) * xk - b * xk;
+            if (k + 1 < n) t = t + (0.25 * xk) * xk1;
+            return t;
+        }
+        return scalar_term<KIND>(k, n, xk, xk1, p0, p1, power);
+    };
     auto stash = [&](double* dst) {
 #pragma unroll
-        for (int r = 0; r < kPer; ++r) reinterpret_cast<double2*>(dst)[threadIdx.x + 256 * r] = pre[r];
+        for (int r = 0; r < kPer; ++r) {
+            if constexpr (FUSED) {
+                const int e = cfetch + 2 * (threadIdx.x + 256 * r);
+                const Raw& w = raw[r];
+                const double t0 = e < nt ? form(e, w.x0, w.x1, w.a0, w.b0) : 0.0;
+                const double t1 = e + 1 < nt ? form(e + 1, w.x1, w.x2, w.a1, w.b1) : 0.0;
+                pre[r] = make_double2(t0, t1);
+            }
+            reinterpret_cast<double2*>(dst)[threadIdx.x + 256 * r] = pre[r];
+        }
     };
     double f = 0.0;
     fetch(0);
@@ -327,14 +356,15 @@ __global__ __launch_bounds__(256) void k_scalar_fd_chain(const double* __restric
         if (more) stash(Ts[cb ^ 1]);
         __syncthreads();
     }
-    if (active) vals[q] = f;
-    if constexpr (FUSED) {
+    if constexpr (!FUSED) {
+        if (active) vals[q] = f;
+    } else {
+        // vals written through (sc1): drained, visible to every XCD without a release fence
+        if (active) __hip_atomic_store(vals + q, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int* last = reinterpret_cast<int*>(&Ts[0][0]);   // the chunks are done with (barrier above)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const int prev = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int is_last = prev == (int)gridDim.x - 1;
             if (is_last) {
