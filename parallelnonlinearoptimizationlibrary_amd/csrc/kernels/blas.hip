@@ -16,7 +16,6 @@
 #include "../pnol_comm.hpp"
 
 #include <cstdlib>
-#include <type_traits>
 
 namespace pnol {
 namespace {
@@ -406,102 +405,17 @@ __device__ __forceinline__ void pass_ident(double2 (&d)[kGroup], const double* _
 // Row shard form (BFGS D row-sharded over the ranks): D holds rows [rb, re) of the n x n
 // matrix (rb a multiple of the row-tile height); row tiles, partial indices and outputs use global rows,
 // so every partial is the one the whole-matrix pass (rb = 0, re = n) would produce.
-// Sum the pass partials in a fixed order.  Workgroup = 64 outputs x 4 quarters: quarter q sums
-// strips s == q (mod 4) (and row tiles t == q (mod 4)) ascending, then the four quarter sums
-// are added (0+1)+(2+3) -- 4x the loads in flight of a thread per output.
-__device__ __forceinline__ void pass_finish_body(int bx, int n, int nstrips, int nrowt, const double* __restrict__ part_u,
-                                                 const double* __restrict__ part_v, const double* __restrict__ part_w,
-                                                 double* __restrict__ u, double* __restrict__ v, double* __restrict__ w,
-                                                 int ub, int ue, double (&red)[3][4][64]) {
-    const int il = threadIdx.x & 63, q = threadIdx.x >> 6;
-    const int i = bx * 64 + il;
-    const int ic = min(i, n - 1);
-    double su = 0.0, sv = 0.0, sw = 0.0;
-#pragma unroll 4
-    for (int s = q; s < nstrips; s += 4) {
-        su += part_u[(long)s * n + ic];
-        sv += part_v[(long)s * n + ic];
-    }
-#pragma unroll 4
-    for (int t = q; t < nrowt; t += 4) sw += part_w[(long)t * n + ic];
-    red[0][q][il] = su;
-    red[1][q][il] = sv;
-    red[2][q][il] = sw;
-    __syncthreads();
-    if (q == 0 && i < n) {
-        const bool mine = i >= ub && i < ue;   // u, v: this shard's rows only
-        if (u && mine) u[i] = (red[0][0][il] + red[0][1][il]) + (red[0][2][il] + red[0][3][il]);
-        if (v && mine) v[i] = (red[1][0][il] + red[1][1][il]) + (red[1][2][il] + red[1][3][il]);
-        if (w) w[i] = (red[2][0][il] + red[2][1][il]) + (red[2][2][il] + red[2][3][il]);
-    }
-}
-
-// FIN (the whole matrix, one GPU): the finish runs in the same launch.  The grid's first
-// workgroups are the pass's; after its partials each signals its row tile's and its column tile's
-// counter (every wave's vmcnt(0), the barrier, lane 0's agent release, vmcnt(0), relaxed agent
-// adds).  The last workgroups (one per 64 outputs, dispatched after every pass workgroup) poll
-// the counters of the row tiles and the column tile their outputs need (relaxed, then one agent
-// acquire) and sum exactly as k_bfgs_pass_finish: the same bits, one launch and its gap fewer.
-// Counters count up across launches (target epoch x contributors), so nothing resets them.
-struct PassFin {
-    int npass = 0;          // pass workgroups (the grid's first)
-    int* cnt = nullptr;     // [nrowt] row-tile counters, then [ncolt] column-tile counters
-    int epoch = 0;
-    double *u = nullptr, *v = nullptr, *w = nullptr;
-};
-constexpr int kPassSpin = 1 << 24;
-
-template <bool PEND, bool WB, bool VEC, bool IDS = false, bool FIN = false>
+template <bool PEND, bool WB, bool VEC, bool IDS = false>
 __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ Dsh, long ldd, int n, int rb, int re, int prows,
                                                    const double* __restrict__ sp, const double* __restrict__ ap,
                                                    const double* __restrict__ bp, const double* __restrict__ y,
                                                    const double* __restrict__ g, double* __restrict__ part_u,
                                                    double* __restrict__ part_v, double* __restrict__ part_w,
-                                                   const double* __restrict__ id_scale = nullptr, PassFin fin = {}) {
+                                                   const double* __restrict__ id_scale = nullptr) {
     double* __restrict__ D = Dsh - (long)rb * ldd;   // global-row view (only rows [rb, re) touched)
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int ncolt = (n + kPassCols - 1) / kPassCols;
-    if constexpr (FIN) {
-        if ((int)blockIdx.x >= fin.npass) {   // ---- a finish workgroup: outputs [64 b, 64 b + 64)
-            __shared__ double red[3][4][64];
-            __shared__ int ok_sh;
-            const int b = blockIdx.x - fin.npass, nrowt = (n + prows - 1) / prows;
-            if (threadIdx.x == 0) {
-                const int r0 = (64 * b) / prows, r1 = min(nrowt - 1, (64 * b + 63) / prows), ct = (64 * b) / kPassCols;
-                int ok = 1;
-                for (int it = 0;; ++it) {
-                    bool ready = __hip_atomic_load(fin.cnt + nrowt + ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                                 fin.epoch * nrowt;
-                    for (int r = r0; r <= r1 && ready; ++r)
-                        ready = __hip_atomic_load(fin.cnt + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                                fin.epoch * ncolt;
-                    if (ready) break;
-                    if (it > kPassSpin) {
-                        ok = 0;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                ok_sh = ok;
-            }
-            __syncthreads();
-            if (!ok_sh) {   // never expected (every pass workgroup was dispatched first): fail loudly
-                const int i = 64 * b + (threadIdx.x & 63);
-                if (threadIdx.x < 64 && i < n) {
-                    const double nan = __builtin_nan("");
-                    if (fin.u) fin.u[i] = nan;
-                    if (fin.v) fin.v[i] = nan;
-                    if (fin.w) fin.w[i] = nan;
-                }
-                return;
-            }
-            pass_finish_body(b, n, ncolt * 4, nrowt, part_u, part_v, part_w, fin.u, fin.v, fin.w, 0, n, red);
-            return;
-        }
-    }
     const int rt = rb / prows + blockIdx.x / ncolt;   // global row tile (prows = bfgs_pass_rows(n))
     const int ct = blockIdx.x % ncolt;            // column tile
     const int strip = ct * 4 + wave;              // 128-column strip index
@@ -574,41 +488,48 @@ __global__ __launch_bounds__(256) void k_bfgs_pass(double* __restrict__ Dsh, lon
             const int idx = ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
             const int row = r0 + (idx & 7);
             if (row < r_end) {
-                double* dst = (idx < 8 ? part_u : part_v) + (long)strip * n + row;
-                if (FIN) __hip_atomic_store(dst, red, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // write-through
-                else *dst = red;
+                if (idx < 8) part_u[(long)strip * n + row] = red;
+                else part_v[(long)strip * n + row] = red;
             }
         }
 #pragma unroll
         for (int q = 0; q < kGroup; ++q) cur[q] = nxt[q];
         grp = gnext;
     }
-    if constexpr (!FIN) {
-        if (c0ok) part_w[(long)rt * n + col] = w0;
-        if (c1ok) part_w[(long)rt * n + col + 1] = w1;
-    }
-    if constexpr (FIN) {
-        // the partials are stored write-through (sc1): drained, they are visible to every XCD
-        // without a release fence (one per workgroup -- an L2 write-back each -- doubled the pass)
-        if (c0ok) __hip_atomic_store(part_w + (long)rt * n + col, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (c1ok) __hip_atomic_store(part_w + (long)rt * n + col + 1, w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const int nrowt = (n + prows - 1) / prows;
-            __hip_atomic_fetch_add(fin.cnt + rt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(fin.cnt + nrowt + ct, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    if (c0ok) part_w[(long)rt * n + col] = w0;
+    if (c1ok) part_w[(long)rt * n + col + 1] = w1;
 }
 
+// Sum the pass partials in a fixed order.  Workgroup = 64 outputs x 4 quarters: quarter q sums
+// strips s == q (mod 4) (and row tiles t == q (mod 4)) ascending, then the four quarter sums
+// are added (0+1)+(2+3) -- 4x the loads in flight of a thread per output.
 __global__ __launch_bounds__(256) void k_bfgs_pass_finish(int n, int nstrips, int nrowt, const double* __restrict__ part_u,
                                                           const double* __restrict__ part_v,
                                                           const double* __restrict__ part_w, double* __restrict__ u,
                                                           double* __restrict__ v, double* __restrict__ w, int ub,
                                                           int ue) {
     __shared__ double red[3][4][64];
-    pass_finish_body(blockIdx.x, n, nstrips, nrowt, part_u, part_v, part_w, u, v, w, ub, ue, red);
+    const int il = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + il;
+    const int ic = min(i, n - 1);
+    double su = 0.0, sv = 0.0, sw = 0.0;
+#pragma unroll 4
+    for (int s = q; s < nstrips; s += 4) {
+        su += part_u[(long)s * n + ic];
+        sv += part_v[(long)s * n + ic];
+    }
+#pragma unroll 4
+    for (int t = q; t < nrowt; t += 4) sw += part_w[(long)t * n + ic];
+    red[0][q][il] = su;
+    red[1][q][il] = sv;
+    red[2][q][il] = sw;
+    __syncthreads();
+    if (q == 0 && i < n) {
+        const bool mine = i >= ub && i < ue;   // u, v: this shard's rows only
+        if (u && mine) u[i] = (red[0][0][il] + red[0][1][il]) + (red[0][2][il] + red[0][3][il]);
+        if (v && mine) v[i] = (red[1][0][il] + red[1][1][il]) + (red[1][2][il] + red[1][3][il]);
+        if (w) w[i] = (red[2][0][il] + red[2][1][il]) + (red[2][2][il] + red[2][3][il]);
+    }
 }
 
 // rows [rb, rb + nrows) of the identity (or diag(scale)), stored from D
@@ -785,63 +706,32 @@ int launch_bfgs_pass(pnol_ctx* ctx, double* D, int ldd, int n, const double* s_p
         if (!g) g = (const double*)zeros;
     }
     auto* P0 = (double*)pu; auto* P1 = (double*)pv; auto* P2 = (double*)pw;
-    // the finish inside the pass launch (k_bfgs_pass<..., FIN>) for the whole matrix on one GPU;
-    // the row-sharded pass keeps the two launches (its w partials are allgathered in between).
-    // PNOL_PASS_FIN=0 keeps them everywhere (read once)
-    static const bool fin_on = [] {
-        const char* e = std::getenv("PNOL_PASS_FIN");
-        return !e || std::atoi(e) != 0;
-    }();
-    const bool fin = fin_on && !pw_gather && rb == 0 && re == n && myrowt > 0;
-    PassFin pf;
-    if (fin) {
-        void* cv = nullptr;
-        bool fresh = false;
-        const size_t cbytes = sizeof(int) * (size_t)(nrowt + ncolt);
-        PNOL_CHECK(ws_get(ctx, "pass_fin_cnt", cbytes, &cv, &fresh));
-        if (fresh || ctx->pass_fin_n != n || ctx->pass_fin_epoch >= (1 << 20)) {
-            PNOL_HIP(hipMemsetAsync(cv, 0, cbytes, ctx->stream));
-            ctx->pass_fin_epoch = 0;
-            ctx->pass_fin_n = n;
-        }
-        pf.npass = myrowt * ncolt;
-        pf.cnt = (int*)cv;
-        pf.epoch = ++ctx->pass_fin_epoch;
-        pf.u = u;
-        pf.v = v;
-        pf.w = w;
-    }
     if (myrowt > 0) {
-        dim3 grd(myrowt * ncolt + (fin ? (n + 63) / 64 : 0)), blk(256);
+        dim3 grd(myrowt * ncolt), blk(256);
         const bool vec = (ldd % 2 == 0) && aligned16(D);
-        auto go = [&](auto PE, auto W, auto V, auto IDS) {
-            constexpr bool pe = decltype(PE)::value, wb = decltype(W)::value, ve = decltype(V)::value,
-                           ids = decltype(IDS)::value;
-            if (fin)
-                hipLaunchKernelGGL((k_bfgs_pass<pe, wb, ve, ids, true>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb, re,
-                                   prows, s_p, a_p, b_p, y, g, P0, P1, P2, id_scale, pf);
-            else
-                hipLaunchKernelGGL((k_bfgs_pass<pe, wb, ve, ids, false>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb,
-                                   re, prows, s_p, a_p, b_p, y, g, P0, P1, P2, id_scale, pf);
-        };
-        using T_ = std::true_type;
-        using F_ = std::false_type;
+#define PNOL_PASS(PE, W, V)                                                                                        \
+    hipLaunchKernelGGL((k_bfgs_pass<PE, W, V>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb, re, prows, s_p, a_p, b_p, y, \
+                       g, P0, P1, P2)
         if (ident_src) {
-            if (vec) go(T_{}, T_{}, T_{}, T_{});
-            else go(T_{}, T_{}, F_{}, T_{});
+            if (vec)
+                hipLaunchKernelGGL((k_bfgs_pass<true, true, true, true>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb,
+                                   re, prows, s_p, a_p, b_p, y, g, P0, P1, P2, id_scale);
+            else
+                hipLaunchKernelGGL((k_bfgs_pass<true, true, false, true>), grd, blk, 0, ctx->stream, D, (long)ldd, n, rb,
+                                   re, prows, s_p, a_p, b_p, y, g, P0, P1, P2, id_scale);
         } else if (vec) {
-            if (pend && write_back) go(T_{}, T_{}, T_{}, F_{});
-            else if (pend) go(T_{}, F_{}, T_{}, F_{});
-            else if (write_back) go(F_{}, T_{}, T_{}, F_{});
-            else go(F_{}, F_{}, T_{}, F_{});
+            if (pend && write_back) PNOL_PASS(true, true, true);
+            else if (pend) PNOL_PASS(true, false, true);
+            else if (write_back) PNOL_PASS(false, true, true);
+            else PNOL_PASS(false, false, true);
         } else {
-            if (pend && write_back) go(T_{}, T_{}, F_{}, F_{});
-            else if (pend) go(T_{}, F_{}, F_{}, F_{});
-            else if (write_back) go(F_{}, T_{}, F_{}, F_{});
-            else go(F_{}, F_{}, F_{}, F_{});
+            if (pend && write_back) PNOL_PASS(true, true, false);
+            else if (pend) PNOL_PASS(true, false, false);
+            else if (write_back) PNOL_PASS(false, true, false);
+            else PNOL_PASS(false, false, false);
         }
+#undef PNOL_PASS
         PNOL_CHECK(launch_check());
-        if (fin) return PNOL_OK;
     }
     if (pw_gather) PNOL_CHECK(pw_gather(ctx, P2, n, nrowt));
     hipLaunchKernelGGL(k_bfgs_pass_finish, dim3((n + 63) / 64), dim3(256), 0, ctx->stream, n, nstrips, nrowt,

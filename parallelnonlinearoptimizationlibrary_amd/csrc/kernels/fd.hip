@@ -247,19 +247,15 @@ __device__ __forceinline__ double chain_sum(double f, const double* __restrict__
     return f;
 }
 
-// FUSED (the default): one launch instead of three -- each workgroup forms the base terms of
-// its LDS chunks itself (scalar_term, the k_scalar_terms values; T unused), and the last workgroup
-// to finish forms g_p = (vals_p - F) / h_{i0 + p} and f0 = F as k_scalar_fd_finish does (the
-// guide's in-launch hand-off: every wave's vmcnt(0), the barrier, lane 0's agent release and
-// vmcnt(0), a relaxed agent add on `done`; the last arriver's agent acquire; it zeroes `done`
-// again).  Same values, two launches and their gaps fewer per gradient.
+// FUSED (the default): each workgroup forms the base terms of its LDS chunks itself
+// (scalar_term's values, so T is unused) -- the k_scalar_terms launch and its gap go.  (The finish
+// by the last workgroup to arrive was built and measured slower than the finish launch: one
+// workgroup's 16384 dependent-load iterations take longer than 65 workgroups and a launch.)
 template <int KIND, bool FUSED = false>
 __global__ __launch_bounds__(256) void k_scalar_fd_chain(const double* __restrict__ x, const double* __restrict__ h,
                                                          int n, int i0, int cnt, const double* __restrict__ p0,
                                                          const double* __restrict__ p1, double power,
-                                                         const double* __restrict__ T, double* __restrict__ vals,
-                                                         int* __restrict__ done = nullptr, double* __restrict__ f0 = nullptr,
-                                                         double* __restrict__ g = nullptr) {
+                                                         const double* __restrict__ T, double* __restrict__ vals) {
     __shared__ __attribute__((aligned(16))) double Ts[2][kTermChunk];
     constexpr int kPer = kTermChunk / 2 / 256;   // double2 loads per thread per chunk
     const int lane = threadIdx.x & 63;
@@ -356,30 +352,7 @@ __global__ __launch_bounds__(256) void k_scalar_fd_chain(const double* __restric
         if (more) stash(Ts[cb ^ 1]);
         __syncthreads();
     }
-    if constexpr (!FUSED) {
-        if (active) vals[q] = f;
-    } else {
-        // vals written through (sc1): drained, visible to every XCD without a release fence
-        if (active) __hip_atomic_store(vals + q, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int* last = reinterpret_cast<int*>(&Ts[0][0]);   // the chunks are done with (barrier above)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const int prev = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int is_last = prev == (int)gridDim.x - 1;
-            if (is_last) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            *last = is_last;
-        }
-        __syncthreads();
-        if (!*last) return;
-        const double F = vals[cnt];
-        if (threadIdx.x == 0 && f0) *f0 = F;
-        for (int p = threadIdx.x; p < cnt; p += 256) g[p] = (vals[p] - F) / h[i0 + p];
-        if (threadIdx.x == 0) __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (active) vals[q] = f;
 }
 
 __global__ void k_scalar_fd_finish(const double* __restrict__ vals, const double* __restrict__ h, int i0, int cnt,
@@ -873,24 +846,22 @@ template <int KIND>
 static int launch_fd_chain(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt, double* T,
                            double* V, double* f0, double* g) {
     const int waves = (cnt + 1 + 63) / 64;
-    // PNOL_FD_FUSED=0 keeps the three launches (terms, chain, finish); read once
+    // PNOL_FD_FUSED=0 keeps the terms launch (read once)
     static const bool fused = [] {
         const char* e = std::getenv("PNOL_FD_FUSED");
         return !e || std::atoi(e) != 0;
     }();
     if (fused) {
-        void* dn = nullptr;
-        PNOL_CHECK(ws_get_zeroed(ctx, "fd_chain_done", sizeof(int) * 64, &dn));
         hipLaunchKernelGGL((k_scalar_fd_chain<KIND, true>), dim3((waves + 3) / 4), dim3(256), 0, ctx->stream, x, h, o->n,
-                           i0, cnt, o->p0, o->p1, o->power, (const double*)nullptr, V, (int*)dn, f0, g);
-        return launch_check();
+                           i0, cnt, o->p0, o->p1, o->power, (const double*)nullptr, V);
+    } else {
+        const int nt = std::max(o->n - (KIND == PNOL_OBJ_ROSENBROCK ? 1 : 0), 1);
+        hipLaunchKernelGGL((k_scalar_terms<KIND>), dim3(std::min((nt + 255) / 256, 1024)), dim3(256), 0, ctx->stream, x,
+                           o->n, o->p0, o->p1, o->power, T);
+        PNOL_CHECK(launch_check());
+        hipLaunchKernelGGL((k_scalar_fd_chain<KIND>), dim3((waves + 3) / 4), dim3(256), 0, ctx->stream, x, h, o->n, i0,
+                           cnt, o->p0, o->p1, o->power, (const double*)T, V);
     }
-    const int nt = std::max(o->n - (KIND == PNOL_OBJ_ROSENBROCK ? 1 : 0), 1);
-    hipLaunchKernelGGL((k_scalar_terms<KIND>), dim3(std::min((nt + 255) / 256, 1024)), dim3(256), 0, ctx->stream, x, o->n,
-                       o->p0, o->p1, o->power, T);
-    PNOL_CHECK(launch_check());
-    hipLaunchKernelGGL((k_scalar_fd_chain<KIND>), dim3((waves + 3) / 4), dim3(256), 0, ctx->stream, x, h, o->n, i0, cnt,
-                       o->p0, o->p1, o->power, (const double*)T, V);
     PNOL_CHECK(launch_check());
     hipLaunchKernelGGL(k_scalar_fd_finish, dim3((cnt + 255) / 256 + 1), dim3(256), 0, ctx->stream, (const double*)V, h, i0,
                        cnt, f0, g);

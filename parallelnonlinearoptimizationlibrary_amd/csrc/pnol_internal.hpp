@@ -67,9 +67,6 @@ struct pnol_ctx {
     // with other processes, so fewer workers are resident than launched): from then on its
     // workers claim in step order (order 0, which drains with any co-residency)
     bool chol_order0 = false;
-    // the fused BFGS pass's in-launch finish: its counters count up by epoch (blas.hip PassFin)
-    int pass_fin_epoch = 0;
-    int pass_fin_n = -1;
     int chol4_epoch = 0;            // last flag value handed out (monotonic; flags reset on regrow)
     hipStream_t aux_stream = nullptr;   // second stream (J^T J rows beside the FD chunks), lazily created
     std::vector<hipEvent_t> aux_events; // chunk-done events between the two streams
