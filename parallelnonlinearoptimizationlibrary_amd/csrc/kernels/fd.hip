@@ -247,11 +247,7 @@ __device__ __forceinline__ double chain_sum(double f, const double* __restrict__
     return f;
 }
 
-// FUSED (the default): each workgroup forms the base terms of its LDS chunks itself
-// (scalar_term's values, so T is unused) -- the k_scalar_terms launch and its gap go.  (The finish
-// by the last workgroup to arrive was built and measured slower than the finish launch: one
-// workgroup's 16384 dependent-load iterations take longer than 65 workgroups and a launch.)
-template <int KIND, bool FUSED = false>
+template <int KIND>
 __global__ __launch_bounds__(256) void k_scalar_fd_chain(const double* __restrict__ x, const double* __restrict__ h,
                                                          int n, int i0, int cnt, const double* __restrict__ p0,
                                                          const double* __restrict__ p1, double power,
@@ -278,57 +274,18 @@ __global__ __launch_bounds__(256) void k_scalar_fd_chain(const double* __restric
         w0 = max(0, min(KIND == PNOL_OBJ_POWER ? jlo : jlo - 1, nt));
         w1 = max(w0, min(jhi + 1, nt));
     }
-    // chunk c of T into registers (zero past nt; only [c0, c1) is ever read).  FUSED: the raw
-    // operands of the chunk's terms are loaded by fetch (in flight during the chain) and the terms
-    // formed by stash, after the chain -- forming them in fetch would wait for the loads there
+    // chunk c of T into registers (zero past nt; only [c0, c1) is ever read)
     double2 pre[kPer];
-    struct Raw {
-        double x0, x1, x2, a0, a1, b0, b1;
-    };
-    Raw raw[FUSED ? kPer : 1];
-    int cfetch = 0;
     auto fetch = [&](int c0) {
-        cfetch = c0;
 #pragma unroll
         for (int r = 0; r < kPer; ++r) {
             const int e = c0 + 2 * (threadIdx.x + 256 * r);
-            if constexpr (FUSED) {
-                Raw& w = raw[r];
-                w.x0 = e < n ? x[e] : 0.0;
-                w.x1 = e + 1 < n ? x[e + 1] : 0.0;
-                w.x2 = (KIND != PNOL_OBJ_POWER && e + 2 < n) ? x[e + 2] : 0.0;
-                w.a0 = w.a1 = w.b0 = w.b1 = 0.0;
-                if (KIND == PNOL_OBJ_QUADRATIC) {
-                    if (e < nt) { w.a0 = p0[e]; w.b0 = p1[e]; }
-                    if (e + 1 < nt) { w.a1 = p0[e + 1]; w.b1 = p1[e + 1]; }
-                }
-            } else {
-                pre[r] = make_double2(e < nt ? T[e] : 0.0, e + 1 < nt ? T[e + 1] : 0.0);
-            }
+            pre[r] = make_double2(e < nt ? T[e] : 0.0, e + 1 < nt ? T[e + 1] : 0.0);
         }
-    };
-    // scalar_term's expressions on the loaded operands (QUADRATIC reads p0 / p1 at the term's own
-    // index, as the copies a0 / b0, a1 / b1 hold)
-    auto form = [&](int k, double xk, double xk1, double a, double b) {
-        if (KIND == PNOL_OBJ_QUADRATIC) {
-            double t = (0.5 * a * xk) * xk - b * xk;
-            if (k + 1 < n) t = t + (0.25 * xk) * xk1;
-            return t;
-        }
-        return scalar_term<KIND>(k, n, xk, xk1, p0, p1, power);
     };
     auto stash = [&](double* dst) {
 #pragma unroll
-        for (int r = 0; r < kPer; ++r) {
-            if constexpr (FUSED) {
-                const int e = cfetch + 2 * (threadIdx.x + 256 * r);
-                const Raw& w = raw[r];
-                const double t0 = e < nt ? form(e, w.x0, w.x1, w.a0, w.b0) : 0.0;
-                const double t1 = e + 1 < nt ? form(e + 1, w.x1, w.x2, w.a1, w.b1) : 0.0;
-                pre[r] = make_double2(t0, t1);
-            }
-            reinterpret_cast<double2*>(dst)[threadIdx.x + 256 * r] = pre[r];
-        }
+        for (int r = 0; r < kPer; ++r) reinterpret_cast<double2*>(dst)[threadIdx.x + 256 * r] = pre[r];
     };
     double f = 0.0;
     fetch(0);
@@ -844,27 +801,14 @@ int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* 
 
 template <int KIND>
 static int launch_fd_chain(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt, double* T,
-                           double* V, double* f0, double* g) {
-    const int waves = (cnt + 1 + 63) / 64;
-    // PNOL_FD_FUSED=0 keeps the terms launch (read once)
-    static const bool fused = [] {
-        const char* e = std::getenv("PNOL_FD_FUSED");
-        return !e || std::atoi(e) != 0;
-    }();
-    if (fused) {
-        hipLaunchKernelGGL((k_scalar_fd_chain<KIND, true>), dim3((waves + 3) / 4), dim3(256), 0, ctx->stream, x, h, o->n,
-                           i0, cnt, o->p0, o->p1, o->power, (const double*)nullptr, V);
-    } else {
-        const int nt = std::max(o->n - (KIND == PNOL_OBJ_ROSENBROCK ? 1 : 0), 1);
-        hipLaunchKernelGGL((k_scalar_terms<KIND>), dim3(std::min((nt + 255) / 256, 1024)), dim3(256), 0, ctx->stream, x,
-                           o->n, o->p0, o->p1, o->power, T);
-        PNOL_CHECK(launch_check());
-        hipLaunchKernelGGL((k_scalar_fd_chain<KIND>), dim3((waves + 3) / 4), dim3(256), 0, ctx->stream, x, h, o->n, i0,
-                           cnt, o->p0, o->p1, o->power, (const double*)T, V);
-    }
+                           double* V) {
+    const int nt = std::max(o->n - (KIND == PNOL_OBJ_ROSENBROCK ? 1 : 0), 1);
+    hipLaunchKernelGGL((k_scalar_terms<KIND>), dim3(std::min((nt + 255) / 256, 1024)), dim3(256), 0, ctx->stream, x, o->n,
+                       o->p0, o->p1, o->power, T);
     PNOL_CHECK(launch_check());
-    hipLaunchKernelGGL(k_scalar_fd_finish, dim3((cnt + 255) / 256 + 1), dim3(256), 0, ctx->stream, (const double*)V, h, i0,
-                       cnt, f0, g);
+    const int waves = (cnt + 1 + 63) / 64;
+    hipLaunchKernelGGL((k_scalar_fd_chain<KIND>), dim3((waves + 3) / 4), dim3(256), 0, ctx->stream, x, h, o->n, i0, cnt,
+                       o->p0, o->p1, o->power, (const double*)T, V);
     return launch_check();
 }
 
@@ -882,9 +826,9 @@ int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
         return !e || std::atoi(e) != 0;
     }();
     if (chain) {
-        if (o->kind == PNOL_OBJ_ROSENBROCK) return launch_fd_chain<PNOL_OBJ_ROSENBROCK>(ctx, o, x, h, i0, cnt, T, V, f0, g);
-        if (o->kind == PNOL_OBJ_POWER) return launch_fd_chain<PNOL_OBJ_POWER>(ctx, o, x, h, i0, cnt, T, V, f0, g);
-        return launch_fd_chain<PNOL_OBJ_QUADRATIC>(ctx, o, x, h, i0, cnt, T, V, f0, g);
+        if (o->kind == PNOL_OBJ_ROSENBROCK) PNOL_CHECK(launch_fd_chain<PNOL_OBJ_ROSENBROCK>(ctx, o, x, h, i0, cnt, T, V));
+        else if (o->kind == PNOL_OBJ_POWER) PNOL_CHECK(launch_fd_chain<PNOL_OBJ_POWER>(ctx, o, x, h, i0, cnt, T, V));
+        else PNOL_CHECK(launch_fd_chain<PNOL_OBJ_QUADRATIC>(ctx, o, x, h, i0, cnt, T, V));
     } else {
         const int blocks = (cnt + 1 + 255) / 256;
         if (o->kind == PNOL_OBJ_ROSENBROCK)
