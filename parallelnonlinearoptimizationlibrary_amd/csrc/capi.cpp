@@ -467,9 +467,9 @@ int pnol_fd_gradient(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const doubl
                      double* g) {
     PNOL_CHECK(set_device(ctx));
     if (!obj || !x || !h || !f0 || (cnt > 0 && !g) || cnt < 0 || i0 < 0 || i0 + cnt > obj->n) return PNOL_ERR_ARG;
-    // device block [x | h | g | f0] and its pinned image: x (and h, when it changed) go up in ONE
-    // copy, g and f0 come down in one
-    // sized by n alone (cnt <= n), so a span that changes between calls does not regrow it
+    // device block [x | h | g | f0] and its pinned image [x | h | g | f0]: the kernels read x from
+    // the pinned image and write g and f0 into it (zero-copy); h goes up only when it changed.
+    // Sized by n alone (cnt <= n), so a span that changes between calls does not regrow it
     const size_t n = (size_t)obj->n, io = 3 * n + 1;
     void* dv = nullptr;
     bool fresh = false;
@@ -494,21 +494,21 @@ int pnol_fd_gradient(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const doubl
     }
     std::memcpy(st, x, sizeof(double) * n);
     // the step vector rarely changes between calls (a solver's dX): it is staged and sent only
-    // when its content differs from the copy on the device (compared while it is staged)
-    // (one memcmp of the whole vector: a solver's steps are the same call after call)
+    // when its content differs from the device's copy (one memcmp of the whole vector)
     bool same = ctx->fdg_h_dev == dh && ctx->fdg_h_host.size() == n &&
                 std::memcmp(h, ctx->fdg_h_host.data(), sizeof(double) * n) == 0;
     if (!same) std::memcpy(st + n, h, sizeof(double) * n);
-    PNOL_HIP(hipMemcpyAsync(dx, st, sizeof(double) * (same ? n : 2 * n), hipMemcpyHostToDevice, ctx->stream));
-    if (!same) {
+    if (!same) {   // the steps changed: up they go (x travels with the first kernel below)
+        PNOL_HIP(hipMemcpyAsync(dh, st + n, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
         ctx->fdg_h_host.assign(h, h + n);
         ctx->fdg_h_dev = dh;
     }
     {
+        // zero-copy: the terms kernel reads x from the pinned block (and copies it to dx for the
+        // chain), the finish writes g and f0 straight into it -- no copy commands, no copy gaps
         ScopedTimer tm(ctx, "fd_gradient");
-        PNOL_CHECK(launch_fd_gradient(ctx, obj, dx, dh, i0, cnt, df, dg));
+        PNOL_CHECK(launch_fd_gradient(ctx, obj, st, dh, i0, cnt, st + 2 * n + cnt, st + 2 * n, dx));
     }
-    PNOL_HIP(hipMemcpyAsync(st + 2 * n, dg, sizeof(double) * ((size_t)cnt + 1), hipMemcpyDeviceToHost, ctx->stream));
     PNOL_CHECK(stream_wait(ctx->stream));
     if (cnt > 0) std::memcpy(g, st + 2 * n, sizeof(double) * cnt);
     *f0 = st[2 * n + cnt];

@@ -173,13 +173,25 @@ __device__ __forceinline__ double scalar_term(int k, int n, double xk, double xk
     }
 }
 
+// xcopy (the host-pointer gradient): x is the caller's pinned host block, read once here over
+// PCIe and copied to device memory for the chain kernel -- no separate host-to-device copy
 template <int KIND>
 __global__ __launch_bounds__(256) void k_scalar_terms(const double* __restrict__ x, int n, const double* __restrict__ p0,
                                                       const double* __restrict__ p1, double power,
-                                                      double* __restrict__ T) {
+                                                      double* __restrict__ T, double* __restrict__ xcopy = nullptr) {
     const int nt = scalar_nterms<KIND>(n);
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nt; k += gridDim.x * blockDim.x)
-        T[k] = scalar_term<KIND>(k, n, x[k], k + 1 < n ? x[k + 1] : 0.0, p0, p1, power);
+    const int lane = threadIdx.x & 63;
+    const int stride = gridDim.x * blockDim.x;
+    for (int k0 = blockIdx.x * blockDim.x; k0 < n; k0 += stride) {   // whole waves (uniform trip count)
+        const int k = k0 + threadIdx.x;
+        const double xk = k < n ? x[k] : 0.0;
+        // x[k + 1] from the next lane (one read of host memory per element); lane 63 reads its own
+        double xk1 = __shfl_down(xk, 1, 64);
+        if (lane == 63) xk1 = k + 1 < n ? x[k + 1] : 0.0;
+        if (k + 1 >= n) xk1 = 0.0;
+        if (xcopy && k < n) xcopy[k] = xk;
+        if (k < nt) T[k] = scalar_term<KIND>(k, n, xk, xk1, p0, p1, power);
+    }
 }
 
 // Points q in [0, cnt] (q == cnt: the base point): vals[q] = f(x + h_j e_j), j = i0 + q.
@@ -801,19 +813,19 @@ int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* 
 
 template <int KIND>
 static int launch_fd_chain(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt, double* T,
-                           double* V) {
-    const int nt = std::max(o->n - (KIND == PNOL_OBJ_ROSENBROCK ? 1 : 0), 1);
+                           double* V, double* xdev) {
+    const int nt = std::max(o->n, 1);
     hipLaunchKernelGGL((k_scalar_terms<KIND>), dim3(std::min((nt + 255) / 256, 1024)), dim3(256), 0, ctx->stream, x, o->n,
-                       o->p0, o->p1, o->power, T);
+                       o->p0, o->p1, o->power, T, xdev);
     PNOL_CHECK(launch_check());
     const int waves = (cnt + 1 + 63) / 64;
-    hipLaunchKernelGGL((k_scalar_fd_chain<KIND>), dim3((waves + 3) / 4), dim3(256), 0, ctx->stream, x, h, o->n, i0, cnt,
-                       o->p0, o->p1, o->power, (const double*)T, V);
+    hipLaunchKernelGGL((k_scalar_fd_chain<KIND>), dim3((waves + 3) / 4), dim3(256), 0, ctx->stream,
+                       xdev ? (const double*)xdev : x, h, o->n, i0, cnt, o->p0, o->p1, o->power, (const double*)T, V);
     return launch_check();
 }
 
 int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt, double* f0,
-                       double* g) {
+                       double* g, double* xdev) {
     if (!o || !x || !h || !is_scalar_kind(o->kind)) return PNOL_ERR_ARG;
     if (i0 < 0 || cnt < 0 || i0 + cnt > o->n) return PNOL_ERR_ARG;
     void *vals = nullptr, *terms = nullptr;
@@ -825,10 +837,14 @@ int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
         const char* e = std::getenv("PNOL_FD_SCALAR");
         return !e || std::atoi(e) != 0;
     }();
+    if (xdev && !chain) {   // the point-per-thread form reads x throughout: bring it to the device
+        PNOL_HIP(hipMemcpyAsync(xdev, x, sizeof(double) * (size_t)o->n, hipMemcpyHostToDevice, ctx->stream));
+        x = xdev;
+    }
     if (chain) {
-        if (o->kind == PNOL_OBJ_ROSENBROCK) PNOL_CHECK(launch_fd_chain<PNOL_OBJ_ROSENBROCK>(ctx, o, x, h, i0, cnt, T, V));
-        else if (o->kind == PNOL_OBJ_POWER) PNOL_CHECK(launch_fd_chain<PNOL_OBJ_POWER>(ctx, o, x, h, i0, cnt, T, V));
-        else PNOL_CHECK(launch_fd_chain<PNOL_OBJ_QUADRATIC>(ctx, o, x, h, i0, cnt, T, V));
+        if (o->kind == PNOL_OBJ_ROSENBROCK) PNOL_CHECK(launch_fd_chain<PNOL_OBJ_ROSENBROCK>(ctx, o, x, h, i0, cnt, T, V, xdev));
+        else if (o->kind == PNOL_OBJ_POWER) PNOL_CHECK(launch_fd_chain<PNOL_OBJ_POWER>(ctx, o, x, h, i0, cnt, T, V, xdev));
+        else PNOL_CHECK(launch_fd_chain<PNOL_OBJ_QUADRATIC>(ctx, o, x, h, i0, cnt, T, V, xdev));
     } else {
         const int blocks = (cnt + 1 + 255) / 256;
         if (o->kind == PNOL_OBJ_ROSENBROCK)
