@@ -1454,6 +1454,9 @@ struct RedArgs {
     // the worker claim order (task_of): 1 (default) each step's critical tasks one step early,
     // 0 by step (PNOL_CHOL_ORDER=0)
     int order = 1;
+    // the two critical update tasks of each step form their L panels themselves
+    // (PNOL_CHOL_SELFL=0: they wait for the panel tasks' stored L)
+    bool selfl = true;
 };
 
 template <int SUB>
@@ -1766,6 +1769,47 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         const bool crit = i == k + 2 && j == k + 1;
         if (crit) PNOL_CRIT(k, 4)
 #endif
+        if (red.selfl && i == k + 2 && j >= k + 1) {
+            // The two tiles the chain needs next, (k+2, k+1) and (k+2, k+2): this task forms the L
+            // panels it needs itself -- L_ik = A_ik W_k^T (and L_jk), diag_l_strip exactly as the
+            // panel tasks form them, so the same bits -- instead of waiting for the panel tasks to
+            // store them: the tiles are ready one store / flag / poll / staging round trip earlier
+            // (the panel tasks still store L for every other update and run the forward
+            // substitution).  A_ik, A_jk and the tile are final through column k - 1 long before
+            // W_k, so they are staged while the workgroup waits for the chain.
+            double* Z = pfx;   // the chain's look-ahead area (unused by workers) holds A_jk / L_jk
+            if (t == 0)
+                ok_sh = spin_all<3>({pw.ver + i * T + j, pw.ver + i * T + k, pw.ver + j * T + k}, {k, k, k}, info);
+            __syncthreads();
+            if (!ok_sh) return;
+            d4 acc[2][2];
+            acc_load<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
+            stage_tile<true>(X, P, ldp, i * NB, k0);
+            if (i != j) stage_tile<true>(Z, P, ldp, j * NB, k0);
+            if (t == 0) ok_sh = (k == 0 && !red.part && !red.packed && !red.preloaded) || spin_ge(pw.wdone + k, 1, info);
+            __syncthreads();
+            if (!ok_sh) return;
+#ifdef PNOL_CHOL_TIMELINE
+            if (crit) PNOL_CRIT(k, 5)
+#endif
+            stage_tile<true>(Y, W + (long)k * NB * NB, NB, 0, 0);
+            __syncthreads();
+            d4 li[4], lj[4];
+            diag_l_strip(li, X, Y, wave, lane);
+            if (i != j) diag_l_strip(lj, Z, Y, wave, lane);
+            __syncthreads();   // every read of the A staging areas is done
+            diag_strip_to_stage(li, X, wave, lane);
+            if (i != j) diag_strip_to_stage(lj, Z, wave, lane);
+            __syncthreads();
+            mfma_xyt<true>(acc, X, i != j ? Z : X, wr, wc, lane);
+            acc_store<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
+            publish_claim(pw.ver + i * T + j, k + 1, pw.counter, pre);
+#ifdef PNOL_CHOL_TIMELINE
+            if (crit) PNOL_CRIT(k, 6)
+            chol_tl_mark(k, 2, tl0);
+#endif
+            continue;
+        }
         // the tile's earlier updates first: its loads stay in flight while the workgroup waits
         // for the two panels; when all three words are already there (one round of loads), the
         // tile and both panels are loaded together
@@ -2027,6 +2071,8 @@ static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, i
         // host backend, and a context that has seen a timed-out wait, claim in step order.
         const char* eo = std::getenv("PNOL_CHOL_ORDER");
         rp.order = eo ? (std::atoi(eo) != 0 ? 1 : 0) : ((ctx->chol_order0 || comm_shares_device()) ? 0 : 1);
+        const char* es = std::getenv("PNOL_CHOL_SELFL");   // read per call (A/B, tests)
+        rp.selfl = !es || std::atoi(es) != 0;
     }
     const int slots = std::max(ctx->num_cu, 1) - 1;
     const int want = ew ? std::atoi(ew) : slots;
