@@ -630,8 +630,18 @@ __global__ __launch_bounds__(512, 2) void k_syrk_red(const double* __restrict__ 
         __syncthreads();
         if (!ok_sh) return;
     }
+#ifdef PNOL_SYRK_TIMELINE
+    const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     double(*st)[kTile + 1] = reinterpret_cast<double(*)[kTile + 1]>(&lds[0][0][0]);
     syrk_reduce_body<SUB, kRedSR, 512>(part, ntiles, sub, n, lambda, A, lda, nullptr, 0, jp, rhs, rhs2, bx, by, NBX, st);
+#ifdef PNOL_SYRK_TIMELINE
+    if (threadIdx.x == 0) {   // the reduce workgroups' entries follow the SYRK ones (start = poll done)
+        g_syrk_tl[3 * b] = rt0;
+        g_syrk_tl[3 * b + 1] = __builtin_amdgcn_s_memrealtime();
+        g_syrk_tl[3 * b + 2] = (unsigned long long)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) << 32;
+    }
+#endif
 }
 static_assert(kRedSR * (kTile + 1) <= 2 * 2 * kTile * kPad, "the reduce strip fits the SYRK's LDS");
 
