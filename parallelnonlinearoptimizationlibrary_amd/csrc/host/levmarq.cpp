@@ -218,6 +218,8 @@ class LMAsync {
         {
             const char* e = std::getenv("PNOL_LM_TRIP");
             trip_fused_ = !e || std::atoi(e) != 0;
+            const char* z = std::getenv("PNOL_LM_ZEROCOPY");
+            zero_copy_ = trip_fused_ && !sliced && (!z || std::atoi(z) != 0);
         }
         // several ranks: every trip's solve status is agreed over the ranks before the host acts
         // on it (pnol_lm_agree_status_d), so all replicas take the same branch
@@ -249,6 +251,7 @@ class LMAsync {
     double* sig(int s) { return trip_[s].get(); }
     int* info(int s) { return reinterpret_cast<int*>(trip_[s].get() + np_ + mp_); }
     const double* sigma_h(int s) const { return static_cast<const double*>(pin_[s]); }
+    double* pin_sigma(int s) { return static_cast<double*>(pin_[s]); }
     const double* Fnext_h(int s) const { return static_cast<const double*>(pin_[s]) + np_; }
     int info_h(int s) const { return *reinterpret_cast<const int*>(static_cast<const double*>(pin_[s]) + np_ + mp_); }
     void uploadH(const std::vector<double>& dX) { h_.upload(dX); }
@@ -272,12 +275,16 @@ class LMAsync {
                   "normal equations");
         } else if (trip_fused_) {
             // FD Jacobian, the J^T J / -J^T F partials, the Cholesky that reduces them itself,
-            // the backward solve forming the trial point
+            // the backward solve forming the trial point; the backward solve and the trial point's
+            // evaluation also write sigma, F(x + sigma) and the status straight into the pinned
+            // block (pnol_ctx::TripMirror), so no copy follows the trip (PNOL_LM_ZEROCOPY=0: the copy)
             lambda_[s] = lambda;
-            check(pnol_lm_trip_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 3 : 1, JT_.get(), ldjt_, lambda,
-                                 rhs_.get(), sig(s), info(s), x_[s ^ 1].get()),
-                  "lm trip");
-            finish(s, false);
+            if (zero_copy_) ctx_->trip_mirror.sigma = pin_sigma(s);
+            const int st = pnol_lm_trip_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 3 : 1, JT_.get(), ldjt_,
+                                          lambda, rhs_.get(), sig(s), info(s), x_[s ^ 1].get());
+            ctx_->trip_mirror = {};
+            check(st, "lm trip");
+            finish(s, false, zero_copy_);
             return;
         } else {
             // FD Jacobian, A and -J^T F in one queue (the GEMV in the J^T J's tail)
@@ -304,12 +311,27 @@ class LMAsync {
     }
     // the rest of a trip once sigma_[s] is known: trial point (unless the solve formed it), its
     // residuals, copies back
-    void finish(int s, bool add = true) {
+    // zero_copy: the evaluation writes F(x + sigma) and the status word into the pinned block
+    // itself (the backward solve wrote sigma there), instead of the copy of the three
+    void finish(int s, bool add = true, bool zero_copy = false) {
         if (add) check(pnol_add_d(ctx_, x_[s].get(), sig(s), x_[s ^ 1].get(), n_), "add");
         // LevMarqMPI: each rank's rows, then all rows everywhere (rows mode)
-        if (sliced_) check(pnol_lm_eval_mpi_d(ctx_, d_, x_[s ^ 1].get(), F(s ^ 1)), "objective eval");
-        else check(pnol_dobj_eval_ckpt_d(ctx_, d_, x_[s ^ 1].get(), F(s ^ 1)), "objective eval");
-        check(pnol_memcpy_d2h_async(ctx_, pin_[s], trip_[s].get(), sizeof(double) * ((size_t)np_ + mp_ + 1)), "d2h");
+        if (sliced_) {
+            check(pnol_lm_eval_mpi_d(ctx_, d_, x_[s ^ 1].get(), F(s ^ 1)), "objective eval");
+        } else {
+            if (zero_copy) {
+                double* pin = static_cast<double*>(pin_[s]);
+                ctx_->trip_mirror.F = pin + np_;
+                ctx_->trip_mirror.info_d = info(s);
+                ctx_->trip_mirror.info_h = reinterpret_cast<int*>(pin + np_ + mp_);
+            }
+            const int st = pnol_dobj_eval_ckpt_d(ctx_, d_, x_[s ^ 1].get(), F(s ^ 1));
+            ctx_->trip_mirror = {};
+            check(st, "objective eval");
+        }
+        if (!zero_copy)
+            check(pnol_memcpy_d2h_async(ctx_, pin_[s], trip_[s].get(), sizeof(double) * ((size_t)np_ + mp_ + 1)),
+                  "d2h");
         check(pnol_event_record(ctx_, ev_[s]), "event");
     }
     void wait(int s) { check(pnol_event_wait(ev_[s]), "event wait"); }
@@ -350,6 +372,7 @@ class LMAsync {
     int n_, m_, ldjt_, lda_;
     bool sliced_;
     bool trip_fused_ = false;
+    bool zero_copy_ = false;   // the one-GPU fused trip's results written into pin_ by its kernels
     bool agree_ = false;
     double lambda_[2] = {0, 0};   // trip s's lambda (the fused trip's LU fallback forms A)
     int np_ = 0, mp_ = 0;

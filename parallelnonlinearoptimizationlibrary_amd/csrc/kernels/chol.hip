@@ -1870,7 +1870,8 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm,
                                                   const double* __restrict__ zv, double* xw, double* __restrict__ x,
                                                   int* flags, int epoch, int* info,
                                                   const double* __restrict__ xbase = nullptr,
-                                                  double* __restrict__ xnext = nullptr) {
+                                                  double* __restrict__ xnext = nullptr,
+                                                  double* __restrict__ x_host = nullptr) {
     __shared__ double part[4][NB];
     __shared__ double vsh[NB];
     __shared__ int ok_sh;
@@ -1958,6 +1959,7 @@ __global__ __launch_bounds__(256) void k_chol_bwd(const double* __restrict__ Lm,
         }
         if (w0 + t < n) {
             x[w0 + t] = xv;
+            if (x_host) x_host[w0 + t] = xv;   // the LM trip's pinned result block (TripMirror)
             // the LM trial point X + sigma (LevenbergMarquardt.cpp:87-90), the add of pnol_add_d
             if (xnext) xnext[w0 + t] = xbase[w0 + t] + xv;
         }
@@ -2091,11 +2093,11 @@ static int chol_bwd_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, int n
     if (w.gran)
         hipLaunchKernelGGL(k_chol_bwd<true>, dim3(w.T), dim3(256), 0, st, (const double*)w.Lm, w.ldp, w.T, n,
                            (const double*)w.W, (const double*)w.bv, (const double*)w.zv, w.xw, sigma, w.bwdflag, epoch,
-                           dinfo, xbase, xnext);
+                           dinfo, xbase, xnext, ctx->trip_mirror.sigma);
     else
         hipLaunchKernelGGL(k_chol_bwd<false>, dim3(w.T), dim3(256), 0, st, (const double*)w.Lm, w.ldp, w.T, n,
                            (const double*)w.W, (const double*)w.bv, (const double*)w.zv, w.xw, sigma, w.bwdflag, epoch,
-                           dinfo, xbase, xnext);
+                           dinfo, xbase, xnext, ctx->trip_mirror.sigma);
     PNOL_CHECK(launch_check());
     // test hook (tests/test_gpu_solvers.py, tests/test_gpu_mpi.py; read per call: the tests flip
     // it, per rank too): a value > 0 reports a non-positive pivot on every Cholesky solve, so the

@@ -496,7 +496,10 @@ __global__ __launch_bounds__(64) void k_linres_evalP(const double* __restrict__ 
                                                      const double* __restrict__ y, int m, int n,
                                                      double* __restrict__ F, double* __restrict__ C,
                                                      double* __restrict__ xsave = nullptr,
-                                                     const double* __restrict__ xcheck = nullptr, int rb0 = 0) {
+                                                     const double* __restrict__ xcheck = nullptr, int rb0 = 0,
+                                                     double* __restrict__ Fh = nullptr,
+                                                     const int* __restrict__ info_d = nullptr,
+                                                     int* __restrict__ info_h = nullptr) {
     // rb0: the first row panel of this launch (a row-sharded LevMarqMPI rank evaluates its
     // m-slices only; the grid covers its panels)
     const int rb = rb0 + blockIdx.x, row = rb * kPanel + threadIdx.x;
@@ -509,6 +512,9 @@ __global__ __launch_bounds__(64) void k_linres_evalP(const double* __restrict__ 
     }
     if (xsave && blockIdx.x == 0)
         for (int k = threadIdx.x; k < n; k += 64) xsave[k] = x[k];
+    // the LM trip's pinned result block (TripMirror): the solve status word, final by now (every
+    // kernel that writes it ran before this one)
+    if (info_h && blockIdx.x == 0 && threadIdx.x == 0) info_h[0] = info_d[0];
     const double* a = panel_col(AP, n, rb, 0) + threadIdx.x;
     constexpr int U = kCkpt;
     double acc = 0.0;
@@ -542,7 +548,11 @@ __global__ __launch_bounds__(64) void k_linres_evalP(const double* __restrict__ 
     int k = nb * U;
     if (CKPT && k > 0 && k < n && row < m) C[(long)(k / kCkpt) * m + row] = acc;
     for (; k < n; ++k) acc = fma(a[(size_t)k * kPanel], x[k], acc);
-    if (row < m && F) F[row] = y ? acc - y[row] : acc;
+    if (row < m && F) {
+        const double v = y ? acc - y[row] : acc;
+        F[row] = v;
+        if (Fh) Fh[row] = v;
+    }
 }
 
 // FD GEMM from AP.  Workgroup = 4 waves on the same 64-row panel (one row per lane), wave w
@@ -804,8 +814,10 @@ int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* 
     const int nb = (r1 - r0 + kPanel - 1) / kPanel;
     if (nb > 0) {
         ScopedTimer tm(ctx, "linres_eval");
+        const auto& tm_ = ctx->trip_mirror;
         hipLaunchKernelGGL((k_linres_evalP<true>), dim3(nb), dim3(64), 0, ctx->stream, (const double*)o->at, x, o->p1,
-                           o->m, o->n, out, (double*)C, (double*)xc, (const double*)nullptr, r0 / kPanel);
+                           o->m, o->n, out, (double*)C, (double*)xc, (const double*)nullptr, r0 / kPanel, tm_.F,
+                           tm_.info_d, tm_.info_h);
     }
     return launch_check();
 }
@@ -929,7 +941,8 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
         LaunchTimer tm(ctx, "fd_ckpt");
         hipExtLaunchKernelGGL((k_linres_evalP<true>), dim3(nmt), dim3(64), 0, ctx->stream, tm.start(), tm.stop(), 0,
                               (const double*)o->at, x, (const double*)o->p1, o->m, o->n, f0_out, (double*)C,
-                              xcheck ? (double*)nullptr : (double*)xc, xcheck, mt0);
+                              xcheck ? (double*)nullptr : (double*)xc, xcheck, mt0, (double*)nullptr,
+                              (const int*)nullptr, (int*)nullptr);
         PNOL_CHECK(launch_check());
     }
     if (nmt == 0) return PNOL_OK;   // a rank without rows

@@ -67,6 +67,16 @@ struct pnol_ctx {
     // with other processes, so fewer workers are resident than launched): from then on its
     // workers claim in step order (order 0, which drains with any co-residency)
     bool chol_order0 = false;
+    // The one-GPU LM trip's results written straight into the host's pinned block by the kernels
+    // that form them (set by the LM loop around its launches, null otherwise): sigma by the
+    // backward solve, F(x + sigma) and the solve status word by the trial point's evaluation --
+    // no copy command behind the trip, whose launch left a ~12 us gap after the evaluation.
+    struct TripMirror {
+        double* sigma = nullptr;
+        double* F = nullptr;
+        const int* info_d = nullptr;
+        int* info_h = nullptr;
+    } trip_mirror;
     int chol4_epoch = 0;            // last flag value handed out (monotonic; flags reset on regrow)
     hipStream_t aux_stream = nullptr;   // second stream (J^T J rows beside the FD chunks), lazily created
     std::vector<hipEvent_t> aux_events; // chunk-done events between the two streams

@@ -666,6 +666,17 @@ int pnol_default_ctx(pnol_ctx** out) {
 int pnol_ctx_enable_timers(pnol_ctx* ctx, int on) {
     if (!ctx) return PNOL_ERR_ARG;
     ctx->timers.on = on == 2 ? 2 : (on != 0 ? 1 : 0);
+    // events for the timers made up front: a hipEventCreate between a trip's launches sat on the
+    // host's path to the next FD launch (events return to the pool when the timers are read)
+    if (ctx->timers.on) {
+        PNOL_HIP(hipSetDevice(ctx->device));
+        auto& pool = ctx->timers.free_events;
+        while (pool.size() < 512) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) break;
+            pool.push_back(e);
+        }
+    }
     return PNOL_OK;
 }
 
