@@ -16,8 +16,15 @@ the exchange steps at a stated xGMI rate (the 8-GPU run itself is the driver's).
   solve        the persistent tile Cholesky + backward solve at n (replicated on every rank)
   eval         F(x + sigma) (columns mode: all rows on every rank)
   exchanges    + the J^T J node reduce-scatter and the tile allgather (~8 n^2 bytes over the ranks)
+  device-initiated (a design, NOT built): the FD kernel's epilogue stores each m-slice row block of
+               its tiles straight into the slice owner's buffer over xGMI (IPC-mapped peer memory)
+               and bumps a completion word there, so the transfer runs under the FD launch itself:
+               max_r FD_r(P) (one tile-list launch) + max(0, per-link bytes / LINK_GBPS - FD_r(P))
+               + FLAG_LATENCY_US -- assuming the remote stores do not slow the VALU-bound FD
 
     python tools/rank_model.py [--out profiles/r06_rank_model.json]
+    python tools/rank_model.py --derive profiles/r06_rank_model.json   (recompute the modelled fields
+                                                                       of a measured file, no GPU)
 """
 import argparse
 import json
@@ -29,6 +36,20 @@ sys.path.insert(0, ROOT)
 
 LINK_GBPS = 64.0          # assumed effective one-direction rate of one xGMI peer link (GB/s)
 PHASE_LATENCY_US = 10.0   # assumed fixed cost of one grouped RCCL send/recv phase (launch + handshake)
+FLAG_LATENCY_US = 5.0     # assumed cost of the device-initiated design's cross-GPU completion word
+
+
+def device_initiated(d, P, m, n, t1):
+    """the device-initiated exchange design's prediction from a rank's measured one-launch FD"""
+    fd = d["fd_ms_max_one_launch"]
+    cols = -(-n // P)                       # a rank's FD columns (cost-balanced tiles, ~n / P)
+    rows_out = m - -(-m // P)               # the rows of its columns that other ranks hold
+    per_link = cols * rows_out * 8.0 / (P - 1)
+    link_ms = per_link / (LINK_GBPS * 1e9) * 1e3
+    total = fd + max(0.0, link_ms - fd) + FLAG_LATENCY_US / 1e3
+    return {"fd_ms_max_one_launch": fd, "bytes_per_link": per_link, "link_ms": link_ms,
+            "flag_latency_us_assumed": FLAG_LATENCY_US, "fd_jacobian_ms_max_over_ranks": total,
+            "speedup_vs_one_gpu": t1 / total, "built": False}
 
 
 def phase_tiles(tiles, sub):
@@ -49,7 +70,19 @@ def main():
     ap.add_argument("--n", type=int, default=2048)
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--out", default="")
+    ap.add_argument("--derive", default="", help="recompute the modelled fields of a measured file")
     args = ap.parse_args()
+    if args.derive:
+        out = json.load(open(args.derive))
+        for P, d in out["per_P"].items():
+            if int(P) > 1:
+                d["fd_jacobian_model_device_initiated"] = device_initiated(d, int(P), out["m"], out["n"],
+                                                                           out["fd_ms_one_gpu"])
+        out["flag_latency_us_assumed"] = FLAG_LATENCY_US
+        with open(args.derive, "w") as f:
+            json.dump(out, f, indent=1)
+        print(json.dumps({P: d.get("fd_jacobian_model_device_initiated") for P, d in out["per_P"].items()}, indent=1))
+        return
     import numpy as np
     import torch
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
@@ -96,7 +129,7 @@ def main():
         return ts[len(ts) // 2]
 
     out = {"m": m, "n": n, "link_GBps_assumed": LINK_GBPS, "phase_latency_us_assumed": PHASE_LATENCY_US,
-           "reps": args.reps, "per_P": {}}
+           "flag_latency_us_assumed": FLAG_LATENCY_US, "reps": args.reps, "per_P": {}}
     full = L.fd_tiles(n, 1, 0)
     t1 = fd_span([full])
     out["fd_ms_one_gpu"] = t1
@@ -123,6 +156,7 @@ def main():
                                "speedup_vs_one_gpu": t1 / (fmax + exposed),
                                "launch_overhead_vs_one_launch": fmax / d["fd_ms_max_one_launch"] - 1.0}
             d["fd_jacobian_model"] = fdj
+            d["fd_jacobian_model_device_initiated"] = device_initiated(d, P, m, n, t1)
         mp = m // P
         JTs = torch.randn(n, mp, dtype=torch.float64, device=f"cuda:{ctx.device}")
         d["syrk_reduce_ms"] = timed(lambda: ctx.jtj(JTs, 0.01))
