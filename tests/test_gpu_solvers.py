@@ -576,7 +576,9 @@ def test_lm_fused_trip_loop_equals_general_loop(ctx, oracle, m, n, force, reduce
     launch into the Cholesky's matrix, or as the persistent launch's first tasks) replays the
     one-wait loop with the two calls (PNOL_LM_TRIP=0) and the general loop (PNOL_LM_ASYNC=0)
     bitwise -- X, F0, FOpt, evaluation count -- also with the LU fallback forced on every trip
-    (force = 1: A formed from the trip's partials, pnol_lm_trip_normal_d)."""
+    (force = 1: A formed from the trip's partials, pnol_lm_trip_normal_d); the fused trip's results
+    reach the host alike written into the pinned block by its kernels (the default) or copied
+    (PNOL_LM_ZEROCOPY=0)."""
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import run_levmarq
     A, xs, y = oracle.linres_data(m, n)
@@ -584,11 +586,13 @@ def test_lm_fused_trip_loop_equals_general_loop(ctx, oracle, m, n, force, reduce
     monkeypatch.setenv("PNOL_CHOL_FORCE_FALLBACK", force)
     monkeypatch.setenv("PNOL_LM_REDUCE", reduce)
     out = {}
-    for name, mode, trip in (("fused", "1", "1"), ("two_call", "1", "0"), ("general", "0", "0")):
+    for name, mode, trip, zc in (("fused", "1", "1", "1"), ("fused_copy", "1", "1", "0"), ("two_call", "1", "0", "1"),
+                                 ("general", "0", "0", "1")):
         monkeypatch.setenv("PNOL_LM_ASYNC", mode)
         monkeypatch.setenv("PNOL_LM_TRIP", trip)
+        monkeypatch.setenv("PNOL_LM_ZEROCOPY", zc)
         out[name] = run_levmarq(_obj(ctx, L.OBJ_LINRES, n, m, A, y), np.zeros(n), params)
-    for a, b in (("fused", "two_call"), ("two_call", "general")):
+    for a, b in (("fused", "fused_copy"), ("fused", "two_call"), ("two_call", "general")):
         (Xa, F0a, FOa, ra), (Xs, F0s, FOs, rs) = out[a], out[b]
         assert np.array_equal(Xa, Xs), (a, b, rel(Xa, Xs))
         assert np.array_equal(F0a, F0s) and np.array_equal(FOa, FOs), (a, b)
