@@ -497,17 +497,19 @@ int pnol_fd_gradient(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const doubl
     // when its content differs from the device's copy (one memcmp of the whole vector)
     bool same = ctx->fdg_h_dev == dh && ctx->fdg_h_host.size() == n &&
                 std::memcmp(h, ctx->fdg_h_host.data(), sizeof(double) * n) == 0;
-    if (!same) std::memcpy(st + n, h, sizeof(double) * n);
-    if (!same) {   // the steps changed: up they go (x travels with the first kernel below)
-        PNOL_HIP(hipMemcpyAsync(dh, st + n, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
+    if (!same) {   // the steps changed: the terms kernel brings them up with x (no copy command)
+        std::memcpy(st + n, h, sizeof(double) * n);
         ctx->fdg_h_host.assign(h, h + n);
         ctx->fdg_h_dev = dh;
     }
     {
-        // zero-copy: the terms kernel reads x from the pinned block (and copies it to dx for the
-        // chain), the finish writes g and f0 straight into it -- no copy commands, no copy gaps
+        // zero-copy: the terms kernel reads x (and a changed h) from the pinned block and copies
+        // them to dx / dh for the chain, the finish writes g and f0 straight into it -- no copy
+        // commands, no copy gaps (the bounded solvers' step vector changes with the active set,
+        // i.e. on nearly every cfg-5 iteration)
         ScopedTimer tm(ctx, "fd_gradient");
-        PNOL_CHECK(launch_fd_gradient(ctx, obj, st, dh, i0, cnt, st + 2 * n + cnt, st + 2 * n, dx));
+        PNOL_CHECK(launch_fd_gradient(ctx, obj, st, dh, i0, cnt, st + 2 * n + cnt, st + 2 * n, dx,
+                                      same ? nullptr : st + n));
     }
     PNOL_CHECK(stream_wait(ctx->stream));
     if (cnt > 0) std::memcpy(g, st + 2 * n, sizeof(double) * cnt);

@@ -174,11 +174,14 @@ __device__ __forceinline__ double scalar_term(int k, int n, double xk, double xk
 }
 
 // xcopy (the host-pointer gradient): x is the caller's pinned host block, read once here over
-// PCIe and copied to device memory for the chain kernel -- no separate host-to-device copy
+// PCIe and copied to device memory for the chain kernel -- no separate host-to-device copy;
+// likewise hsrc -> hdst, the step vector when it changed since the last call
 template <int KIND>
 __global__ __launch_bounds__(256) void k_scalar_terms(const double* __restrict__ x, int n, const double* __restrict__ p0,
                                                       const double* __restrict__ p1, double power,
-                                                      double* __restrict__ T, double* __restrict__ xcopy = nullptr) {
+                                                      double* __restrict__ T, double* __restrict__ xcopy = nullptr,
+                                                      const double* __restrict__ hsrc = nullptr,
+                                                      double* __restrict__ hdst = nullptr) {
     const int nt = scalar_nterms<KIND>(n);
     const int lane = threadIdx.x & 63;
     const int stride = gridDim.x * blockDim.x;
@@ -190,6 +193,7 @@ __global__ __launch_bounds__(256) void k_scalar_terms(const double* __restrict__
         if (lane == 63) xk1 = k + 1 < n ? x[k + 1] : 0.0;
         if (k + 1 >= n) xk1 = 0.0;
         if (xcopy && k < n) xcopy[k] = xk;
+        if (hsrc && k < n) hdst[k] = hsrc[k];
         if (k < nt) T[k] = scalar_term<KIND>(k, n, xk, xk1, p0, p1, power);
     }
 }
@@ -825,10 +829,10 @@ int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* 
 
 template <int KIND>
 static int launch_fd_chain(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt, double* T,
-                           double* V, double* xdev) {
+                           double* V, double* xdev, const double* hsrc) {
     const int nt = std::max(o->n, 1);
     hipLaunchKernelGGL((k_scalar_terms<KIND>), dim3(std::min((nt + 255) / 256, 1024)), dim3(256), 0, ctx->stream, x, o->n,
-                       o->p0, o->p1, o->power, T, xdev);
+                       o->p0, o->p1, o->power, T, xdev, hsrc, hsrc ? const_cast<double*>(h) : (double*)nullptr);
     PNOL_CHECK(launch_check());
     const int waves = (cnt + 1 + 63) / 64;
     hipLaunchKernelGGL((k_scalar_fd_chain<KIND>), dim3((waves + 3) / 4), dim3(256), 0, ctx->stream,
@@ -837,7 +841,7 @@ static int launch_fd_chain(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
 }
 
 int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt, double* f0,
-                       double* g, double* xdev) {
+                       double* g, double* xdev, const double* hsrc) {
     if (!o || !x || !h || !is_scalar_kind(o->kind)) return PNOL_ERR_ARG;
     if (i0 < 0 || cnt < 0 || i0 + cnt > o->n) return PNOL_ERR_ARG;
     void *vals = nullptr, *terms = nullptr;
@@ -853,10 +857,17 @@ int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
         PNOL_HIP(hipMemcpyAsync(xdev, x, sizeof(double) * (size_t)o->n, hipMemcpyHostToDevice, ctx->stream));
         x = xdev;
     }
+    if (hsrc && !chain) {
+        PNOL_HIP(hipMemcpyAsync(const_cast<double*>(h), hsrc, sizeof(double) * (size_t)o->n, hipMemcpyHostToDevice,
+                                ctx->stream));
+        hsrc = nullptr;
+    }
     if (chain) {
-        if (o->kind == PNOL_OBJ_ROSENBROCK) PNOL_CHECK(launch_fd_chain<PNOL_OBJ_ROSENBROCK>(ctx, o, x, h, i0, cnt, T, V, xdev));
-        else if (o->kind == PNOL_OBJ_POWER) PNOL_CHECK(launch_fd_chain<PNOL_OBJ_POWER>(ctx, o, x, h, i0, cnt, T, V, xdev));
-        else PNOL_CHECK(launch_fd_chain<PNOL_OBJ_QUADRATIC>(ctx, o, x, h, i0, cnt, T, V, xdev));
+        if (o->kind == PNOL_OBJ_ROSENBROCK)
+            PNOL_CHECK(launch_fd_chain<PNOL_OBJ_ROSENBROCK>(ctx, o, x, h, i0, cnt, T, V, xdev, hsrc));
+        else if (o->kind == PNOL_OBJ_POWER)
+            PNOL_CHECK(launch_fd_chain<PNOL_OBJ_POWER>(ctx, o, x, h, i0, cnt, T, V, xdev, hsrc));
+        else PNOL_CHECK(launch_fd_chain<PNOL_OBJ_QUADRATIC>(ctx, o, x, h, i0, cnt, T, V, xdev, hsrc));
     } else {
         const int blocks = (cnt + 1 + 255) / 256;
         if (o->kind == PNOL_OBJ_ROSENBROCK)

@@ -292,9 +292,10 @@ int launch_dobj_eval_ckpt(pnol_ctx* ctx, pnol_dobj* o, const double* x, double* 
 // out[k] = f(Xs row k) (scalar kinds) or out rows = F(Xs row k) (residual kinds), k < npts
 int launch_eval_batch(pnol_ctx* ctx, pnol_dobj* o, const double* Xs, int npts, double* out);
 // xdev != nullptr: x is a pinned host block, read once by the first kernel and copied to xdev
-// (device memory, n doubles) for the rest; f0 / g may be pinned host memory too
+// (device memory, n doubles) for the rest; f0 / g may be pinned host memory too.  hsrc != nullptr:
+// the step vector's new content in pinned host memory, copied to h (device) by the first kernel
 int launch_fd_gradient(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, int i0, int cnt,
-                       double* f0, double* g, double* xdev = nullptr);
+                       double* f0, double* g, double* xdev = nullptr, const double* hsrc = nullptr);
 // ckpt: 1 = run the base-chain pass (F0 when compute_f0, prefix checkpoints), 0 = reuse the
 // checkpoints of the previous call at the same x (chunked launches of one Jacobian)
 // mS > 0: the sliced J^T layout (row r of J in slice r / mS at JT + (r / mS) * sstride, row
