@@ -827,6 +827,45 @@ __device__ __forceinline__ void diag_strip_to_stage(const d4 (&acc)[4], double* 
         for (int r = 0; r < 4; ++r) X[jb * kSub + (w * 16 + (lane >> 4) + 4 * r) * kPad + (lane & 15)] = acc[jb][r];
 }
 
+// Two blocks (strip s, column blocks j0 and j1) of diag_l_strip's product -- each block's MFMA
+// chain exactly as diag_l_strip forms it (K blocks kb <= jb ascending, kk ascending), so the
+// same bits; a half critical update task forms its half of L_ik this way, two blocks per wave.
+__device__ __forceinline__ void diag_l_blocks(d4 (&acc)[2], const double* __restrict__ X, const double* __restrict__ Y,
+                                              int s, int j0, int j1, int lane) {
+    const int frow = lane & 15, fk = lane >> 4;
+    acc[0] = acc[1] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const double a = X[kb * kSub + (s * 16 + frow) * kPad + kk * 4 + fk];
+            if (kb <= j0)
+                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Y[kb * kSub + (j0 * 16 + frow) * kPad + kk * 4 + fk],
+                                                              acc[0], 0, 0, 0);
+            if (kb <= j1)
+                acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Y[kb * kSub + (j1 * 16 + frow) * kPad + kk * 4 + fk],
+                                                              acc[1], 0, 0, 0);
+        }
+}
+
+// acc[mi] (output block row 2 h + mi, column block w) -= X Y^T over the 64-wide K: the per-block
+// MFMA chain of mfma_xyt<true> (the same operands in the same order), for a half tile
+__device__ __forceinline__ void mfma_xyt_half(d4 (&acc)[2], const double* __restrict__ X, const double* __restrict__ Y,
+                                              int h, int w, int lane) {
+    const int frow = lane & 15, fk = lane >> 4;
+#pragma unroll
+    for (int sub = 0; sub < 4; ++sub)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const double b = Y[sub * kSub + (w * 16 + frow) * kPad + kk * 4 + fk];
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi) {
+                const double a = -X[sub * kSub + ((2 * h + mi) * 16 + frow) * kPad + kk * 4 + fk];
+                acc[mi] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[mi], 0, 0, 0);
+            }
+        }
+}
+
 // a panel's L strip (this wave's 16 rows of L_ik, from diag_l_strip) to the factor matrix, and
 // into LDS row-major 64 x 65 (the forward substitution's copy)
 template <bool SC1 = false>
@@ -1397,10 +1436,11 @@ __global__ __launch_bounds__(256, 2) void k_chol_step(double* __restrict__ P, do
 // row 1; one workgroup per CU: __launch_bounds__(256, 1) and the register count).  Every tile, panel and b update is the same arithmetic in the same order as in
 // the per-step launches, so the result is bitwise method 4's.
 struct PersistWords {
-    int *wdone, *lcnt, *bcnt, *ver, *counter;
+    int *wdone, *lcnt, *bcnt, *ver, *counter, *half;
 };
+// half: per tile, the halves of a split critical update stored (0, 1, 2)
 __device__ __forceinline__ PersistWords persist_words(int* f, int T) {
-    return {f, f + T, f + 2 * T, f + 3 * T, f + 3 * T + T * T};
+    return {f, f + T, f + 2 * T, f + 3 * T, f + 3 * T + T * T, f + 3 * T + T * T + 1};
 }
 
 // publish `v` into *w after every wave's (sc1) stores of this workgroup have completed
@@ -1414,6 +1454,15 @@ __device__ __forceinline__ void publish(int* w, int v) {
 __device__ __forceinline__ void publish_claim(int* w, int v, int* counter, int& pre) {
     if (threadIdx.x == 0) pre = atomicAdd(counter, 1);
     publish(w, v);
+}
+// a half critical update's publish: the second half to finish publishes the tile's version (each
+// half's sc1 stores have completed before its arrival count, so both halves are in L2 by then)
+__device__ __forceinline__ void publish_half_claim(int* hc, int* w, int v, int* counter, int& pre) {
+    if (threadIdx.x == 0) pre = atomicAdd(counter, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && __hip_atomic_fetch_add(hc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1)
+        __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // every *f[q] >= tg[q] in one round of loads (no waiting)
 template <int N>
@@ -1457,6 +1506,8 @@ struct RedArgs {
     // the two critical update tasks of each step form their L panels themselves
     // (PNOL_CHOL_SELFL=0: they wait for the panel tasks' stored L)
     bool selfl = true;
+    // ... and run as two tasks each, one per 32-row half of the tile (selfl only; PNOL_CHOL_SPLIT)
+    bool split = true;
 };
 
 template <int SUB>
@@ -1566,11 +1617,18 @@ __device__ void red_task(int u, const RedArgs& red, double* __restrict__ P, long
 // Order 1 against order 0: 6 of 6 same-box bench pairs faster, +0.5-1% LM iters/s.
 struct Task {
     int k, i, j;   // j < 0: panel row i of step k
+    int h;         // >= 0: the 32-row half h of a split critical update
 };
-__device__ __forceinline__ Task task_local(int k, int l, int T) {
+// split: the two critical updates (l = R, R + 1) are four half tasks (l = R .. R + 3), the other
+// updates one index later by two
+__device__ __forceinline__ Task task_local(int k, int l, int T, bool split) {
     const int R = T - 1 - k;
-    if (l < R) return {k, k + 1 + l, -1};
-    const int q = l - R;
+    if (l < R) return {k, k + 1 + l, -1, -1};
+    int q = l - R;
+    if (split && R >= 2) {
+        if (q < 4) return {k, k + 2, q < 2 ? k + 1 : k + 2, q & 1};
+        q -= 2;
+    }
     // full column order f: column k+1 holds f = 0 .. R-1 (f = 0 is the chain's), column k+2
     // starts at f = R, ...
     int u = q == 0 ? 1 : (q == 1 ? R : (q < R ? q : q + 1));
@@ -1579,34 +1637,40 @@ __device__ __forceinline__ Task task_local(int k, int l, int T) {
         u -= T - j;
         ++j;
     }
-    return {k, j + u, j};
+    return {k, j + u, j, -1};
 }
-__device__ __forceinline__ Task task_of(int g, int T, int order) {
+// tasks of step k (R = T - 1 - k panel rows), with the split critical updates
+__host__ __device__ __forceinline__ int step_tasks(int R, bool split) {
+    return R + R * (R + 1) / 2 - 1 + (split && R >= 2 ? 2 : 0);
+}
+__device__ __forceinline__ Task task_of(int g, int T, int order, bool split) {
     if (order == 1) {
-        auto csz = [&](int kk) { return T - 1 - kk >= 2 ? 4 : 1; };
+        const int nc = split ? 6 : 4;   // the critical set: panels k+1, k+2 and the updates (halves)
+        auto csz = [&](int kk) { return T - 1 - kk >= 2 ? nc : 1; };
         auto cmap = [&](int x, int RR) { return x < 2 ? x : RR + x - 2; };
-        if (g < csz(0)) return task_local(0, cmap(g, T - 1), T);
+        if (g < csz(0)) return task_local(0, cmap(g, T - 1), T, split);
         g -= csz(0);
         for (int kk = 0;; ++kk) {
             if (kk + 1 <= T - 2) {
                 const int c1 = csz(kk + 1);
-                if (g < c1) return task_local(kk + 1, cmap(g, T - 2 - kk), T);
+                if (g < c1) return task_local(kk + 1, cmap(g, T - 2 - kk), T, split);
                 g -= c1;
             }
-            const int RR = T - 1 - kk, S = RR + RR * (RR + 1) / 2 - 1, rest = S - csz(kk);
-            if (g < rest || kk >= T - 2) return task_local(kk, g < RR - 2 ? g + 2 : g + 4, T);
+            const int RR = T - 1 - kk, S = step_tasks(RR, split), rest = S - csz(kk);
+            if (g < rest || kk >= T - 2)
+                return task_local(kk, g < RR - 2 ? g + 2 : g + (split && RR >= 2 ? 6 : 4), T, split);
             g -= rest;
         }
     }
     int k = 0, R = T - 1;
     for (;;) {
-        const int S = R + R * (R + 1) / 2 - 1;
+        const int S = step_tasks(R, split);
         if (g < S || R <= 1) break;
         g -= S;
         ++k;
         --R;
     }
-    return task_local(k, g, T);
+    return task_local(k, g, T, split);
 }
 
 __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P, double* __restrict__ Lm, long ldp,
@@ -1708,7 +1772,10 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             continue;
         }
         g -= nred;
-        const Task tk = task_of(g, T, red.order == 1 && gridDim.x <= 5 ? 0 : red.order);
+        const bool split = red.selfl && red.split;
+        // order 1 lets each critical set's tasks (4, or 6 split) wait on unclaimed ones: more
+        // workers than that, or step order
+        const Task tk = task_of(g, T, red.order == 1 && gridDim.x <= (split ? 7 : 5) ? 0 : red.order, split);
         const int k = tk.k;
         const int k0 = k * NB;
         if (tk.j < 0) {   // ---- panel row i: L_ik = A_ik W_k^T, then b_i -= L_ik (W_k b_k)
@@ -1769,6 +1836,70 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         const bool crit = i == k + 2 && j == k + 1;
         if (crit) PNOL_CRIT(k, 4)
 #endif
+        if (tk.h >= 0) {
+            // Half h (rows 32 h .. 32 h + 31) of a critical update tile (k+2, k+1) or (k+2, k+2):
+            // as the whole-tile task below (L_ik and L_jk formed here from A and W_k), on half the
+            // output rows -- L_ik's half only (two blocks per wave, diag_l_blocks) for (k+2, k+1),
+            // L_jk whole (the output's columns); the diagonal tile needs L_ik whole on both sides.
+            // Every output block's MFMA chain is the whole-tile task's (mfma_xyt_half), so the tile
+            // is bitwise the same; the second half to finish publishes its version.
+            const int h = tk.h, w = wave;
+            double* Z = pfx;
+            if (t == 0)
+                ok_sh = spin_all<3>({pw.ver + i * T + j, pw.ver + i * T + k, pw.ver + j * T + k}, {k, k, k}, info);
+            __syncthreads();
+            if (!ok_sh) return;
+            d4 acc[2];
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    acc[mi][r] = ldg<true>(P + (long)(i * NB + (2 * h + mi) * 16 + (lane >> 4) + 4 * r) * ldp + j * NB +
+                                           w * 16 + (lane & 15));
+            stage_tile<true>(X, P, ldp, i * NB, k0);
+            if (i != j) stage_tile<true>(Z, P, ldp, j * NB, k0);
+            if (t == 0) ok_sh = (k == 0 && !red.part && !red.packed && !red.preloaded) || spin_ge(pw.wdone + k, 1, info);
+            __syncthreads();
+            if (!ok_sh) return;
+#ifdef PNOL_CHOL_TIMELINE
+            if (crit && h == 0) PNOL_CRIT(k, 5)
+#endif
+            stage_tile<true>(Y, W + (long)k * NB * NB, NB, 0, 0);
+            __syncthreads();
+            if (i != j) {
+                const int s = 2 * h + (w >> 1), j0 = (w & 1) ? 1 : 0, j1 = (w & 1) ? 2 : 3;
+                d4 lh[2], lj[4];
+                diag_l_blocks(lh, X, Y, s, j0, j1, lane);
+                diag_l_strip(lj, Z, Y, w, lane);
+                __syncthreads();   // every read of the A staging areas is done
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    X[j0 * kSub + (s * 16 + (lane >> 4) + 4 * r) * kPad + (lane & 15)] = lh[0][r];
+                    X[j1 * kSub + (s * 16 + (lane >> 4) + 4 * r) * kPad + (lane & 15)] = lh[1][r];
+                }
+                diag_strip_to_stage(lj, Z, w, lane);
+            } else {
+                d4 li[4];
+                diag_l_strip(li, X, Y, w, lane);
+                __syncthreads();
+                diag_strip_to_stage(li, X, w, lane);
+            }
+            __syncthreads();
+            mfma_xyt_half(acc, X, i != j ? Z : X, h, w, lane);
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    stg<true>(P + (long)(i * NB + (2 * h + mi) * 16 + (lane >> 4) + 4 * r) * ldp + j * NB + w * 16 +
+                                  (lane & 15),
+                              acc[mi][r]);
+            publish_half_claim(pw.half + i * T + j, pw.ver + i * T + j, k + 1, pw.counter, pre);
+#ifdef PNOL_CHOL_TIMELINE
+            if (crit) PNOL_CRIT(k, 6)
+            chol_tl_mark(k, 2, tl0);
+#endif
+            continue;
+        }
         if (red.selfl && i == k + 2 && j >= k + 1) {
             // The two tiles the chain needs next, (k+2, k+1) and (k+2, k+2): this task forms the L
             // panels it needs itself -- L_ik = A_ik W_k^T (and L_jk), diag_l_strip exactly as the
@@ -2034,7 +2165,7 @@ static int chol_ws(pnol_ctx* ctx, int n, bool persist, CholWs& w) {
     }
     w.rowflag = ctx->chol4_flags;
     w.bwdflag = ctx->chol4_flags + ctx->chol4_cap;
-    w.npf = 3 * T + T * T + 1;
+    w.npf = 3 * T + 2 * T * T + 1;   // [wdone | lcnt | bcnt | ver | claim counter | half counts]
     if (persist) PNOL_CHECK(ws_get(ctx, "chol5_words", sizeof(int) * (size_t)w.npf, &pf));
     w.P = (double*)P; w.Lm = (double*)Lm; w.W = (double*)W; w.bv = (double*)bv; w.zv = (double*)zv;
     w.xw = (double*)xw; w.pf = (int*)pf;
@@ -2044,8 +2175,15 @@ static int chol_ws(pnol_ctx* ctx, int n, bool persist, CholWs& w) {
 // k_chol_persist: steps 0 .. T-2 (the reducing form: the reduce tasks first, and tile 0 too)
 static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, int* dinfo, const RedArgs& red) {
     const int T = w.T;
+    RedArgs rp = red;
+    {
+        const char* es = std::getenv("PNOL_CHOL_SELFL");   // read per call (A/B, tests)
+        rp.selfl = !es || std::atoi(es) != 0;
+        const char* eh = std::getenv("PNOL_CHOL_SPLIT");
+        rp.split = !eh || std::atoi(eh) != 0;
+    }
     int ntasks = 0;
-    for (int R = T - 1; R >= 1; --R) ntasks += R + R * (R + 1) / 2 - 1;
+    for (int R = T - 1; R >= 1; --R) ntasks += step_tasks(R, rp.selfl && rp.split);
     // tuning knob (read per call): PNOL_CHOL5_WORKERS = worker workgroups; one per CU
     // (the look-ahead areas already hold the static LDS to one workgroup per CU).
     // PNOL_CHOL_LOOKAHEAD = 0 turns the diagonal chain's look-ahead off (read per call).
@@ -2064,7 +2202,6 @@ static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, i
     // the solve goes 0.559-0.561 -> 0.553-0.556 ms; with it every cutoff from 1 to 48 measures
     // the same (56: 0.562-0.566), profiles/r05_lookahead_sweep.txt.
     const int lookahead = el ? std::max(0, std::atoi(el)) : 48;
-    RedArgs rp = red;
     {
         // order 1 (each step's critical tasks a step early) lets up to four workers wait on tasks
         // nobody has claimed yet, so it needs more than four workers resident.  A GPU shared by
@@ -2073,8 +2210,6 @@ static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, i
         // host backend, and a context that has seen a timed-out wait, claim in step order.
         const char* eo = std::getenv("PNOL_CHOL_ORDER");
         rp.order = eo ? (std::atoi(eo) != 0 ? 1 : 0) : ((ctx->chol_order0 || comm_shares_device()) ? 0 : 1);
-        const char* es = std::getenv("PNOL_CHOL_SELFL");   // read per call (A/B, tests)
-        rp.selfl = !es || std::atoi(es) != 0;
     }
     const int slots = std::max(ctx->num_cu, 1) - 1;
     const int want = ew ? std::atoi(ew) : slots;

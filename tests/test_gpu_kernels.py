@@ -356,22 +356,24 @@ def test_cholesky_persistent_equals_per_step_launches(ctx, n):
 def test_cholesky_step_order_claims_bitwise(ctx, monkeypatch, n):
     """The persistent Cholesky's workers in step order (order 0: what a shared GPU and a context
     that saw a timed-out wait use) perform the same tile operations as the default order 1, with
-    the critical update tasks forming their own L panels (PNOL_CHOL_SELFL=1, default) or waiting
-    for the panel tasks' (0): sigma bitwise equal in all four, and equal to method 4's."""
+    the critical update tasks forming their own L panels (PNOL_CHOL_SELFL=1, default) as one task
+    per tile or as two half-tile tasks (PNOL_CHOL_SPLIT=1, default), or waiting for the panel
+    tasks' (SELFL 0): sigma bitwise equal in all six, and equal to method 4's."""
     rng = np.random.default_rng(n + 7)
     J = rng.standard_normal((n + 40, n))
     A = J.T @ J + 0.5 * np.eye(n)
     b = rng.standard_normal(n)
     At, bt = ctx.tensor(A), ctx.tensor(b)
     s4, _ = ctx.solve(At, bt, method=4)
-    for selfl in ("1", "0"):   # the critical updates forming their own L panels, or waiting for them
+    for selfl, split in (("1", "1"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("PNOL_CHOL_SELFL", selfl)
+        monkeypatch.setenv("PNOL_CHOL_SPLIT", split)
         monkeypatch.setenv("PNOL_CHOL_ORDER", "0")
         s_0, i_0 = ctx.solve(At, bt, method=5)
         monkeypatch.setenv("PNOL_CHOL_ORDER", "1")
         s_1, i_1 = ctx.solve(At, bt, method=5)
         assert i_0 == i_1 == 1
-        assert np.array_equal(_np(s_0), _np(s4)) and np.array_equal(_np(s_1), _np(s4)), selfl
+        assert np.array_equal(_np(s_0), _np(s4)) and np.array_equal(_np(s_1), _np(s4)), (selfl, split)
 
 
 @pytest.mark.parametrize("n", [130, 700, 2048, 2111])
