@@ -499,8 +499,7 @@ int pnol_fd_gradient(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const doubl
                 std::memcmp(h, ctx->fdg_h_host.data(), sizeof(double) * n) == 0;
     if (!same) {   // the steps changed: the terms kernel brings them up with x (no copy command)
         std::memcpy(st + n, h, sizeof(double) * n);
-        ctx->fdg_h_host.assign(h, h + n);
-        ctx->fdg_h_dev = dh;
+        ctx->fdg_h_dev = nullptr;   // until the launch below has been queued
     }
     {
         // zero-copy: the terms kernel reads x (and a changed h) from the pinned block and copies
@@ -510,6 +509,10 @@ int pnol_fd_gradient(pnol_ctx* ctx, pnol_dobj* obj, const double* x, const doubl
         ScopedTimer tm(ctx, "fd_gradient");
         PNOL_CHECK(launch_fd_gradient(ctx, obj, st, dh, i0, cnt, st + 2 * n + cnt, st + 2 * n, dx,
                                       same ? nullptr : st + n));
+    }
+    if (!same) {
+        ctx->fdg_h_host.assign(h, h + n);
+        ctx->fdg_h_dev = dh;
     }
     PNOL_CHECK(stream_wait(ctx->stream));
     if (cnt > 0) std::memcpy(g, st + 2 * n, sizeof(double) * cnt);
