@@ -930,6 +930,24 @@ __device__ __forceinline__ void chol_tl_mark(int k, int cls, unsigned long long 
 #define PNOL_CRIT(k, i)
 #define PNOL_LA_STAMP(d, i)
 #endif
+#ifdef PNOL_CHOL_TASKTRACE
+// tools/microbench/chol_tasktrace.hip: per worker task (claim index g) the claim, the end of its
+// dependency waits and its publish (100 MHz realtime), its step and kind
+__device__ unsigned long long g_chol_tasks[16384 * 4];
+#define PNOL_TASK_T0(g) const unsigned long long tt0_ = __builtin_amdgcn_s_memrealtime(); const int tg_ = (g);
+#define PNOL_TASK_READY() const unsigned long long tt1_ = __builtin_amdgcn_s_memrealtime();
+#define PNOL_TASK_END(k, kind)                                                                         \
+    if (threadIdx.x == 0 && tg_ < 16384) {                                                              \
+        g_chol_tasks[4 * tg_] = tt0_;                                                                  \
+        g_chol_tasks[4 * tg_ + 1] = tt1_;                                                              \
+        g_chol_tasks[4 * tg_ + 2] = __builtin_amdgcn_s_memrealtime();                                  \
+        g_chol_tasks[4 * tg_ + 3] = ((unsigned long long)(k) << 8) | (unsigned long long)(kind);       \
+    }
+#else
+#define PNOL_TASK_T0(g)
+#define PNOL_TASK_READY()
+#define PNOL_TASK_END(k, kind)
+#endif
 
 // The diagonal tile d = k + 1 (k >= 0) ready for factor_diag: L = A_{d,k} W_k^T (recomputed
 // here rather than waited for), A_dd - L L^T on its 10 lower 16 x 16 blocks, into the split LDS
@@ -1508,6 +1526,8 @@ struct RedArgs {
     bool selfl = true;
     // ... and run as two tasks each, one per 32-row half of the tile (selfl only; PNOL_CHOL_SPLIT)
     bool split = true;
+    // each step's other updates claimed by tile row (task_local; PNOL_CHOL_ROWMAJOR)
+    bool rowmajor = true;
 };
 
 template <int SUB>
@@ -1620,14 +1640,24 @@ struct Task {
     int h;         // >= 0: the 32-row half h of a split critical update
 };
 // split: the two critical updates (l = R, R + 1) are four half tasks (l = R .. R + 3), the other
-// updates one index later by two
-__device__ __forceinline__ Task task_local(int k, int l, int T, bool split) {
+// updates one index later by two.  rowmajor: the updates after the critical two by tile row
+// (rows k+3, k+4, ..., each from column k+1 to the diagonal) instead of by tile column: the chain
+// needs row d's tiles at step d - 1, so the rows near the diagonal come first.
+__device__ __forceinline__ Task task_local(int k, int l, int T, bool split, bool rowmajor = false) {
     const int R = T - 1 - k;
     if (l < R) return {k, k + 1 + l, -1, -1};
     int q = l - R;
     if (split && R >= 2) {
         if (q < 4) return {k, k + 2, q < 2 ? k + 1 : k + 2, q & 1};
         q -= 2;
+    }
+    if (rowmajor && q >= 2) {
+        int r = q - 2, i = k + 3;   // row i holds the tiles (i, k+1) .. (i, i): i - k of them
+        while (r >= i - k) {
+            r -= i - k;
+            ++i;
+        }
+        return {k, i, k + 1 + r, -1};
     }
     // full column order f: column k+1 holds f = 0 .. R-1 (f = 0 is the chain's), column k+2
     // starts at f = R, ...
@@ -1643,22 +1673,22 @@ __device__ __forceinline__ Task task_local(int k, int l, int T, bool split) {
 __host__ __device__ __forceinline__ int step_tasks(int R, bool split) {
     return R + R * (R + 1) / 2 - 1 + (split && R >= 2 ? 2 : 0);
 }
-__device__ __forceinline__ Task task_of(int g, int T, int order, bool split) {
+__device__ __forceinline__ Task task_of(int g, int T, int order, bool split, bool rowmajor = false) {
     if (order == 1) {
         const int nc = split ? 6 : 4;   // the critical set: panels k+1, k+2 and the updates (halves)
         auto csz = [&](int kk) { return T - 1 - kk >= 2 ? nc : 1; };
         auto cmap = [&](int x, int RR) { return x < 2 ? x : RR + x - 2; };
-        if (g < csz(0)) return task_local(0, cmap(g, T - 1), T, split);
+        if (g < csz(0)) return task_local(0, cmap(g, T - 1), T, split, rowmajor);
         g -= csz(0);
         for (int kk = 0;; ++kk) {
             if (kk + 1 <= T - 2) {
                 const int c1 = csz(kk + 1);
-                if (g < c1) return task_local(kk + 1, cmap(g, T - 2 - kk), T, split);
+                if (g < c1) return task_local(kk + 1, cmap(g, T - 2 - kk), T, split, rowmajor);
                 g -= c1;
             }
             const int RR = T - 1 - kk, S = step_tasks(RR, split), rest = S - csz(kk);
             if (g < rest || kk >= T - 2)
-                return task_local(kk, g < RR - 2 ? g + 2 : g + (split && RR >= 2 ? 6 : 4), T, split);
+                return task_local(kk, g < RR - 2 ? g + 2 : g + (split && RR >= 2 ? 6 : 4), T, split, rowmajor);
             g -= rest;
         }
     }
@@ -1670,7 +1700,7 @@ __device__ __forceinline__ Task task_of(int g, int T, int order, bool split) {
         ++k;
         --R;
     }
-    return task_local(k, g, T, split);
+    return task_local(k, g, T, split, rowmajor);
 }
 
 __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P, double* __restrict__ Lm, long ldp,
@@ -1772,10 +1802,11 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             continue;
         }
         g -= nred;
+        PNOL_TASK_T0(g)
         const bool split = red.selfl && red.split;
         // order 1 lets each critical set's tasks (4, or 6 split) wait on unclaimed ones: more
         // workers than that, or step order
-        const Task tk = task_of(g, T, red.order == 1 && gridDim.x <= (split ? 7 : 5) ? 0 : red.order, split);
+        const Task tk = task_of(g, T, red.order == 1 && gridDim.x <= (split ? 7 : 5) ? 0 : red.order, split, red.rowmajor);
         const int k = tk.k;
         const int k0 = k * NB;
         if (tk.j < 0) {   // ---- panel row i: L_ik = A_ik W_k^T, then b_i -= L_ik (W_k b_k)
@@ -1800,6 +1831,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             if (!ok_sh) return;
             stage_tile<true>(Y, W + (long)k * NB * NB, NB, 0, 0);
             __syncthreads();
+            PNOL_TASK_READY()
             d4 acc[4];   // this wave's 16-row strip of L_ik (nonzero K blocks of W_k^T only)
             diag_l_strip(acc, X, Y, wave, lane);
             strip_store<true>(acc, Lm, ldp, i0, k0, wave, lane);
@@ -1824,6 +1856,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
                 if (i == k + 1) stg<true>(zv + k0 + t, zsh[t]);
             }
             publish_claim(pw.bcnt + i, k + 1, pw.counter, pre);
+            PNOL_TASK_END(k, 0)
 #ifdef PNOL_CHOL_TIMELINE
             chol_tl_mark(k, 1, tl0);
 #endif
@@ -1866,6 +1899,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
 #endif
             stage_tile<true>(Y, W + (long)k * NB * NB, NB, 0, 0);
             __syncthreads();
+            PNOL_TASK_READY()
             if (i != j) {
                 const int s = 2 * h + (w >> 1), j0 = (w & 1) ? 1 : 0, j1 = (w & 1) ? 2 : 3;
                 d4 lh[2], lj[4];
@@ -1894,6 +1928,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
                                   (lane & 15),
                               acc[mi][r]);
             publish_half_claim(pw.half + i * T + j, pw.ver + i * T + j, k + 1, pw.counter, pre);
+            PNOL_TASK_END(k, 2)
 #ifdef PNOL_CHOL_TIMELINE
             if (crit) PNOL_CRIT(k, 6)
             chol_tl_mark(k, 2, tl0);
@@ -1925,6 +1960,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
 #endif
             stage_tile<true>(Y, W + (long)k * NB * NB, NB, 0, 0);
             __syncthreads();
+            PNOL_TASK_READY()
             d4 li[4], lj[4];
             diag_l_strip(li, X, Y, wave, lane);
             if (i != j) diag_l_strip(lj, Z, Y, wave, lane);
@@ -1935,6 +1971,7 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
             mfma_xyt<true>(acc, X, i != j ? Z : X, wr, wc, lane);
             acc_store<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
             publish_claim(pw.ver + i * T + j, k + 1, pw.counter, pre);
+            PNOL_TASK_END(k, 3)
 #ifdef PNOL_CHOL_TIMELINE
             if (crit) PNOL_CRIT(k, 6)
             chol_tl_mark(k, 2, tl0);
@@ -1971,9 +2008,11 @@ __global__ __launch_bounds__(256, 1) void k_chol_persist(double* __restrict__ P,
         stage_tile<true>(X, Lm, ldp, i * NB, k0);
         if (i != j) stage_tile<true>(Y, Lm, ldp, j * NB, k0);
         __syncthreads();
+        PNOL_TASK_READY()
         mfma_xyt<true>(acc, X, i != j ? Y : X, wr, wc, lane);
         acc_store<true>(acc, P, ldp, i * NB, j * NB, wr, wc, lane);
         publish_claim(pw.ver + i * T + j, k + 1, pw.counter, pre);
+        PNOL_TASK_END(k, 1)
 #ifdef PNOL_CHOL_TIMELINE
         if (crit) PNOL_CRIT(k, 6)
         chol_tl_mark(k, 2, tl0);
@@ -2181,6 +2220,8 @@ static int chol_persist_launch(pnol_ctx* ctx, hipStream_t st, const CholWs& w, i
         rp.selfl = !es || std::atoi(es) != 0;
         const char* eh = std::getenv("PNOL_CHOL_SPLIT");
         rp.split = !eh || std::atoi(eh) != 0;
+        const char* er = std::getenv("PNOL_CHOL_ROWMAJOR");
+        rp.rowmajor = !er || std::atoi(er) != 0;
     }
     int ntasks = 0;
     for (int R = T - 1; R >= 1; --R) ntasks += step_tasks(R, rp.selfl && rp.split);

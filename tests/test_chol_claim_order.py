@@ -12,7 +12,7 @@ def step_tasks(R, split):
     return R + R * (R + 1) // 2 - 1 + (2 if split and R >= 2 else 0)
 
 
-def task_local(k, l, T, split):
+def task_local(k, l, T, split, rowmajor=False):
     R = T - 1 - k
     if l < R:
         return (k, k + 1 + l, -1, -1)
@@ -21,6 +21,12 @@ def task_local(k, l, T, split):
         if q < 4:
             return (k, k + 2, k + 1 if q < 2 else k + 2, q & 1)
         q -= 2
+    if rowmajor and q >= 2:
+        r, i = q - 2, k + 3
+        while r >= i - k:
+            r -= i - k
+            i += 1
+        return (k, i, k + 1 + r, -1)
     u = 1 if q == 0 else (R if q == 1 else (q if q < R else q + 1))
     j = k + 1
     while u >= T - j:
@@ -29,26 +35,26 @@ def task_local(k, l, T, split):
     return (k, j + u, j, -1)
 
 
-def task_of(g, T, order, split):
+def task_of(g, T, order, split, rowmajor=False):
     if order == 1:
         nc = 6 if split else 4
         csz = lambda kk: nc if T - 1 - kk >= 2 else 1
         cmap = lambda x, RR: x if x < 2 else RR + x - 2
         if g < csz(0):
-            return task_local(0, cmap(g, T - 1), T, split)
+            return task_local(0, cmap(g, T - 1), T, split, rowmajor)
         g -= csz(0)
         kk = 0
         while True:
             if kk + 1 <= T - 2:
                 c1 = csz(kk + 1)
                 if g < c1:
-                    return task_local(kk + 1, cmap(g, T - 2 - kk), T, split)
+                    return task_local(kk + 1, cmap(g, T - 2 - kk), T, split, rowmajor)
                 g -= c1
             RR = T - 1 - kk
             S = step_tasks(RR, split)
             rest = S - csz(kk)
             if g < rest or kk >= T - 2:
-                return task_local(kk, g + 2 if g < RR - 2 else g + (6 if split and RR >= 2 else 4), T, split)
+                return task_local(kk, g + 2 if g < RR - 2 else g + (6 if split and RR >= 2 else 4), T, split, rowmajor)
             g -= rest
             kk += 1
     k, R = 0, T - 1
@@ -59,14 +65,14 @@ def task_of(g, T, order, split):
         g -= S
         k += 1
         R -= 1
-    return task_local(k, g, T, split)
+    return task_local(k, g, T, split, rowmajor)
 
 
 def all_tasks(T, split):
     return [(k, *task_local(k, l, T, split)[1:]) for k in range(T - 1) for l in range(step_tasks(T - 1 - k, split))]
 
 
-def simulate(T, workers, order, split, selfl=True):
+def simulate(T, workers, order, split, selfl=True, rowmajor=False):
     """True when every task and chain step completes (no state in which every worker waits on a
     task nobody can run)."""
     ntasks = sum(step_tasks(R, split) for R in range(T - 1, 0, -1))
@@ -112,7 +118,7 @@ def simulate(T, workers, order, split, selfl=True):
             progress = True
         for w in range(workers):
             if held[w] is None and nxt < ntasks:
-                held[w] = task_of(nxt, T, order, split)
+                held[w] = task_of(nxt, T, order, split, rowmajor)
                 nxt += 1
                 progress = True
             if held[w] is not None and ready(held[w]):
@@ -125,23 +131,23 @@ def simulate(T, workers, order, split, selfl=True):
     return True
 
 
-@pytest.mark.parametrize("split", [False, True])
-def test_claim_order_is_a_permutation(split):
+@pytest.mark.parametrize("split,rowmajor", [(False, False), (True, False), (True, True), (False, True)])
+def test_claim_order_is_a_permutation(split, rowmajor):
     for T in range(2, 36):
         nt = sum(step_tasks(R, split) for R in range(T - 1, 0, -1))
         for order in (0, 1):
-            got = sorted(task_of(g, T, order, split) for g in range(nt))
+            got = sorted(task_of(g, T, order, split, rowmajor) for g in range(nt))
             assert got == sorted(all_tasks(T, split)), (T, order)
 
 
-@pytest.mark.parametrize("split", [False, True])
-def test_claim_orders_drain(split):
+@pytest.mark.parametrize("split,rowmajor", [(False, False), (True, False), (True, True), (False, True)])
+def test_claim_orders_drain(split, rowmajor):
     need = 7 if split else 5   # order 1 needs more workers than one critical set holds
     for T in (2, 3, 4, 5, 8, 17, 33):
         for workers in (1, 2, 3, need - 1, need, need + 1, 16, 64):
-            assert simulate(T, workers, 0, split), ("step order", T, workers)
+            assert simulate(T, workers, 0, split, rowmajor=rowmajor), ("step order", T, workers)
             if workers >= need:
-                assert simulate(T, workers, 1, split), ("order 1", T, workers)
+                assert simulate(T, workers, 1, split, rowmajor=rowmajor), ("order 1", T, workers)
 
 
 def test_order1_needs_the_worker_guard():

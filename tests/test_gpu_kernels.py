@@ -358,22 +358,24 @@ def test_cholesky_step_order_claims_bitwise(ctx, monkeypatch, n):
     that saw a timed-out wait use) perform the same tile operations as the default order 1, with
     the critical update tasks forming their own L panels (PNOL_CHOL_SELFL=1, default) as one task
     per tile or as two half-tile tasks (PNOL_CHOL_SPLIT=1, default), or waiting for the panel
-    tasks' (SELFL 0): sigma bitwise equal in all six, and equal to method 4's."""
+    tasks' (SELFL 0), each step's other updates claimed by tile row (PNOL_CHOL_ROWMAJOR=1,
+    default) or by column: sigma bitwise equal in all of them, and equal to method 4's."""
     rng = np.random.default_rng(n + 7)
     J = rng.standard_normal((n + 40, n))
     A = J.T @ J + 0.5 * np.eye(n)
     b = rng.standard_normal(n)
     At, bt = ctx.tensor(A), ctx.tensor(b)
     s4, _ = ctx.solve(At, bt, method=4)
-    for selfl, split in (("1", "1"), ("1", "0"), ("0", "1")):
+    for selfl, split, rowmajor in (("1", "1", "1"), ("1", "1", "0"), ("1", "0", "1"), ("0", "1", "1")):
         monkeypatch.setenv("PNOL_CHOL_SELFL", selfl)
         monkeypatch.setenv("PNOL_CHOL_SPLIT", split)
+        monkeypatch.setenv("PNOL_CHOL_ROWMAJOR", rowmajor)
         monkeypatch.setenv("PNOL_CHOL_ORDER", "0")
         s_0, i_0 = ctx.solve(At, bt, method=5)
         monkeypatch.setenv("PNOL_CHOL_ORDER", "1")
         s_1, i_1 = ctx.solve(At, bt, method=5)
         assert i_0 == i_1 == 1
-        assert np.array_equal(_np(s_0), _np(s4)) and np.array_equal(_np(s_1), _np(s4)), (selfl, split)
+        assert np.array_equal(_np(s_0), _np(s4)) and np.array_equal(_np(s_1), _np(s4)), (selfl, split, rowmajor)
 
 
 @pytest.mark.parametrize("n", [130, 700, 2048, 2111])
