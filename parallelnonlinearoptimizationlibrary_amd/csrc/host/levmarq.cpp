@@ -220,6 +220,14 @@ class LMAsync {
             trip_fused_ = !e || std::atoi(e) != 0;
             const char* z = std::getenv("PNOL_LM_ZEROCOPY");
             zero_copy_ = trip_fused_ && !sliced && (!z || std::atoi(z) != 0);
+            // the next trip's Jacobian queued behind a gate while the host decides (PNOL_LM_GATE=0:
+            // queued after the decision, as the rest of the trip)
+            const char* g = std::getenv("PNOL_LM_GATE");
+            gate_ok_ = zero_copy_ && (!g || std::atoi(g) != 0);
+            // how long a gate waits for the decision (ticks of 100 MHz; default 1 s; a test sets 0
+            // to exercise the repeat of a trip whose gate gave up)
+            const char* c = std::getenv("PNOL_LM_GATE_CAP");
+            gate_cap_ = c ? std::strtoull(c, nullptr, 10) : 100000000ull;
         }
         // several ranks: every trip's solve status is agreed over the ranks before the host acts
         // on it (pnol_lm_agree_status_d), so all replicas take the same branch
@@ -238,9 +246,18 @@ class LMAsync {
             check(pnol_host_alloc(&pin_[s], sizeof(double) * ((size_t)np_ + mp_ + 2)), "host_alloc");
             check(pnol_event_create(ctx, &ev_[s]), "event_create");
         }
+        if (gate_ok_) {
+            void* g = nullptr;
+            check(pnol_host_alloc(&g, sizeof(int) * 4), "host_alloc");
+            gate_h_ = static_cast<int*>(g);
+            gate_h_[0] = gate_h_[1] = gate_h_[2] = gate_h_[3] = 0;
+            gsel_.reset(ctx, 1);
+        }
     }
     ~LMAsync() {
+        if (gate_pending_) release(-1);   // a queued Jacobian returns at once
         (void)pnol_ctx_synchronize(ctx_);
+        if (gate_h_) (void)pnol_host_free(gate_h_);
         for (int s = 0; s < 2; ++s) {
             (void)pnol_host_free(pin_[s]);
             (void)pnol_event_destroy(ev_[s]);
@@ -256,8 +273,39 @@ class LMAsync {
     int info_h(int s) const { return *reinterpret_cast<const int*>(static_cast<const double*>(pin_[s]) + np_ + mp_); }
     void uploadH(const std::vector<double>& dX) { h_.upload(dX); }
 
+    // The next trip's FD Jacobian queued now, behind a gate the host opens with its decision
+    // (release): at x_[s] if trip s's step is rejected, at x_[s^1] if accepted.  Between the
+    // trial point's evaluation and the next Jacobian the GPU then waits only for the host's
+    // decision, not for it to queue the launch as well.  False: nothing queued.
+    bool prequeue(int s) {
+        if (!gate_ok_) return false;
+        ++gate_seq_;
+        const int st = lm_prequeue_fd(ctx_, d_, x_[s].get(), F(s), x_[s ^ 1].get(), F(s ^ 1), h_.get(), JT_.get(),
+                                      ldjt_, gate_h_, gate_seq_, reinterpret_cast<int*>(gsel_.get()),
+                                      gate_h_ + 2, gate_cap_);
+        if (st == PNOL_ERR_UNSUPPORTED) return false;
+        check(st, "fd_jacobian (queued)");
+        gate_pending_ = true;
+        return true;
+    }
+    // the decision for the queued Jacobian: 0 at x_[s], 1 at x_[s^1], -1 none (it returns at once)
+    void release(int choice) {
+        __atomic_store_n(&gate_h_[1], choice, __ATOMIC_RELAXED);
+        __atomic_store_n(&gate_h_[0], gate_seq_, __ATOMIC_RELEASE);
+        gate_pending_ = false;
+        rel_seq_ = gate_seq_;
+        rel_choice_ = choice;
+    }
+    // after the trip that used the queued Jacobian: its gate passed the released choice on (a gate
+    // that timed out -- the host answered after its cap -- made the Jacobian launch return)
+    bool gate_passed() const {
+        return __atomic_load_n(&gate_h_[3], __ATOMIC_ACQUIRE) == rel_seq_ &&
+               __atomic_load_n(&gate_h_[2], __ATOMIC_RELAXED) == rel_choice_;
+    }
+
     // trip at x_[s] (F_[s] = F(x_[s]); ckpt: its checkpoints are current) -> sigma, x_[s^1], F_[s^1]
-    void enqueue(int s, double lambda, bool ckpt) {
+    // queued: its FD Jacobian is queued already (prequeue, released)
+    void enqueue(int s, double lambda, bool ckpt, bool queued = false) {
         if (sliced_) {
             check(pnol_lm_jacobian_mpi_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 3 : 1, JT_.get()),
                   "fd_jacobian");
@@ -280,8 +328,10 @@ class LMAsync {
             // block (pnol_ctx::TripMirror), so no copy follows the trip (PNOL_LM_ZEROCOPY=0: the copy)
             lambda_[s] = lambda;
             if (zero_copy_) ctx_->trip_mirror.sigma = pin_sigma(s);
-            const int st = pnol_lm_trip_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 3 : 1, JT_.get(), ldjt_,
-                                          lambda, rhs_.get(), sig(s), info(s), x_[s ^ 1].get());
+            const int st = queued ? launch_fd_normal_solve(ctx_, d_, x_[s].get(), h_.get(), F(s), 3, JT_.get(), ldjt_,
+                                                           lambda, rhs_.get(), sig(s), info(s), x_[s ^ 1].get(), true)
+                                  : pnol_lm_trip_d(ctx_, d_, x_[s].get(), h_.get(), F(s), ckpt ? 3 : 1, JT_.get(),
+                                                   ldjt_, lambda, rhs_.get(), sig(s), info(s), x_[s ^ 1].get());
             ctx_->trip_mirror = {};
             check(st, "lm trip");
             finish(s, false, zero_copy_);
@@ -373,6 +423,13 @@ class LMAsync {
     bool sliced_;
     bool trip_fused_ = false;
     bool zero_copy_ = false;   // the one-GPU fused trip's results written into pin_ by its kernels
+    bool gate_ok_ = false;     // prequeue in use (one GPU, zero-copy trip)
+    bool gate_pending_ = false;
+    unsigned long long gate_cap_ = 0;
+    int gate_seq_ = 0;                 // the last gate queued
+    int rel_seq_ = 0, rel_choice_ = 0; // the last gate released and its choice
+    int* gate_h_ = nullptr;    // pinned {seq, choice} (host -> gate), {choice, seq} (gate -> host)
+    DevVec gsel_;
     bool agree_ = false;
     double lambda_[2] = {0, 0};   // trip s's lambda (the fused trip's LU fallback forms A)
     int np_ = 0, mp_ = 0;
@@ -428,14 +485,31 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool s
     double h_dec = 0, h_enq = 0;
     auto hnow = [] { return std::chrono::steady_clock::now(); };
     auto t_dec = hnow();
+    bool queued = false;   // trip s's Jacobian was queued behind the last trip (prequeue) and released
     while (iter < P.maxIter) {
         auto t0 = hnow();
         if (hprof && iter > 0) h_dec += std::chrono::duration<double, std::micro>(t0 - t_dec).count();
-        dev.enqueue(s, lambda, ckpt);
+        dev.enqueue(s, lambda, ckpt, queued);
+        // the next trip's Jacobian, behind a gate that the decision below opens (not after the
+        // last trip; PNOL_LM_GATE=0: never)
+        bool pre = iter + 1 < P.maxIter && dev.prequeue(s);
         if (hprof) h_enq += std::chrono::duration<double, std::micro>(hnow() - t0).count();
         dev.wait(s);
         if (hprof) t_dec = hnow();
+        if (queued && !dev.gate_passed()) {
+            // the gate gave up before the host answered (its 1 s cap): trip s ran without its
+            // Jacobian -- run it again whole
+            std::cerr << "[pnol] LM trip " << iter << ": queued Jacobian gate timed out; trip repeated" << std::endl;
+            if (pre) dev.release(-1);
+            dev.enqueue(s, lambda, ckpt, false);
+            pre = iter + 1 < P.maxIter && dev.prequeue(s);
+            dev.wait(s);
+        }
+        queued = false;
         if (const int action = dev.action_h(s)) {
+            // the redo queues behind the gate: open it with no Jacobian first
+            if (pre) dev.release(-1);
+            pre = false;
             // the same action on every rank (agreed in the trip); a timed-out wait is never mapped
             // to the LU, and is always reported (PNOL_LM_DEBUG: the LU redos too)
             if (action == 1 || std::getenv("PNOL_LM_DEBUG"))
@@ -463,15 +537,19 @@ void lm_solve_async(MultiObjective* obj, pnol_dobj* d, const LMParams& P, bool s
             if (P.steps) P.steps[1]++;
             ckpt = true;               // x_[s], F_[s] stand, and so do x_[s]'s checkpoints (the
                                        // trial point's went to the other slot)
+            if (pre) dev.release(0);   // the queued Jacobian at x_[s]
         } else {
             lambda = lambda / P.lambdaFactor;
             if (P.steps) P.steps[0]++;
+            xdiff2Norm = std::sqrt(seq_dot(sig_h, sig_h, (size_t)n));
+            const bool done = xdiff2Norm < P.xMinDiff;
+            if (pre) dev.release(done ? -1 : 1);   // the queued Jacobian at x_[s^1], or none
             for (int i = 0; i < n; ++i) X[i] = X[i] + sig_h[i];   // == x_[s^1] (same IEEE add)
             s ^= 1;
             ckpt = true;
-            xdiff2Norm = std::sqrt(seq_dot(sig_h, sig_h, (size_t)n));
-            if (xdiff2Norm < P.xMinDiff) break;
+            if (done) break;
         }
+        queued = pre;
         if ((sharded ? (P.verbose >= 1 && loud) : (P.verbose > 0)) && iter % 10 == 0) {
             std::cout << "At iter = " << iter << " the xdiff 2Norm = " << xdiff2Norm << ", chi^2 = " << chiSq
                       << ", and params: ";

@@ -576,7 +576,19 @@ template <int PW = kPW>
 __global__ __launch_bounds__(64 * (PNOL_FD_TILE / PW)) void k_linres_fdP(
     const double* __restrict__ AP, const double* __restrict__ y, const double* __restrict__ x,
     const double* __restrict__ h, int m, int n, const FdTiles tl, const double* __restrict__ F0,
-    const double* __restrict__ C, double* __restrict__ JT, long ldjt, int mS, long sstride, int mt0, int nmt) {
+    const double* __restrict__ C, double* __restrict__ JT, long ldjt, int mS, long sstride, int mt0, int nmt,
+    const int* __restrict__ sel, const double* __restrict__ x1, const double* __restrict__ F01,
+    const double* __restrict__ C1) {
+    // sel (the LM loop's pre-queued Jacobian, pnol_ctx::FdGate): the point k_trip_gate passed on
+    if (sel) {
+        const int v = __builtin_amdgcn_readfirstlane(*sel);
+        if (v < 0) return;
+        if (v == 1) {
+            x = x1;
+            F0 = F01;
+            C = C1;
+        }
+    }
     // Longest work first: the host sorts the tiles by first column (the chains of tile t run
     // k = ks_t .. n-1), and blockIdx walks all panels of tile 0, then of tile 1, ..., so the
     // short tiles fill the tail.  Panel mt lands on XCD mt % 8 for every tile (L2 reuse).
@@ -680,6 +692,30 @@ __global__ __launch_bounds__(64 * (PNOL_FD_TILE / PW)) void k_linres_fdP(
                 __builtin_nontemporal_store(((acc[j] - yr) - f0) / h[col], out + (long)(col - tl.jbase) * ldjt);
             }
     }
+}
+
+// The LM loop's pre-queued Jacobian (pnol_ctx::FdGate): one lane polls the host's word
+// {seq, choice} (system-scope loads of pinned memory) until it carries this gate's seq, then
+// hands the choice to the FD launch queued behind it (sel) and reports it to the host (res).  A
+// host that never answers is given up on after cap ticks of the 100 MHz clock (choice -2: the FD
+// launch returns, and the host's check of res sees it).  (The same poll inside the FD launch --
+// workgroup 0 polling the host, the others a device word -- measured slower: the FD launch 20-40
+// us longer with its resident workgroups spinning, profiles/r06_lm_gate_ab.txt.)
+__global__ void k_trip_gate(const int* hw, int seq, int* sel, int* res, unsigned long long cap) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    int v = -2;
+    for (;;) {
+        if (__hip_atomic_load(hw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == seq) {
+            v = __hip_atomic_load(hw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > cap) break;
+        __builtin_amdgcn_s_sleep(4);
+    }
+    sel[0] = v;
+    res[0] = v;
+    res[1] = seq;
 }
 
 // ---- synthetic data, splitmix64 counter stream ---------------------------
@@ -936,6 +972,18 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
     double* f0_out = (compute_f0 == 1 || compute_f0 == 2) ? F0 : nullptr;
     const double* xcheck = nullptr;
     const int have = compute_f0 >= 2 ? ckpt_find(ctx, o, x, r0, r1) : -1;
+    // the pre-queued form (lm_prequeue_fd): both points' checkpoints in place, one batched launch
+    const pnol_ctx::FdGate gate = ctx->fd_gate;
+    void* C1 = nullptr;
+    if (gate.hw) {
+        const int have1 = ckpt_find(ctx, o, gate.x1, r0, r1);
+        if (have < 0 || have1 < 0 || have1 == have || compute_f0 != 3 || after_tile || sliced || !rows_all ||
+            ntiles > kFdMaxTiles)
+            return PNOL_ERR_UNSUPPORTED;
+        const int ncp = (o->n + kCkpt - 1) / kCkpt;
+        PNOL_CHECK(ws_get(ctx, have1 ? "linres_ckpt1" : "linres_ckpt0", sizeof(double) * (size_t)o->m * (ncp > 1 ? ncp : 1),
+                          &C1));
+    }
     if (have >= 0) {
         ctx->ckpt_last = have;
         PNOL_CHECK(ckpt_buf(ctx, o, have, &C, &xc));
@@ -972,6 +1020,11 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
         const char* e = std::getenv("PNOL_FD_PW");
         return e ? std::atoi(e) : 0;
     }();
+    if (gate.hw) {
+        hipLaunchKernelGGL(k_trip_gate, dim3(1), dim3(64), 0, ctx->stream, gate.hw, gate.seq, gate.sel, gate.res,
+                           gate.cap);
+        PNOL_CHECK(launch_check());
+    }
     LaunchTimer lt(ctx, "fd_jacobian");
     for (int t0 = 0; t0 < ntiles; t0 += per_launch) {
         FdTiles tl;
@@ -989,11 +1042,13 @@ int launch_fd_jacobian_tiles(pnol_ctx* ctx, pnol_dobj* o, const double* x, const
         if (pw16)
             hipExtLaunchKernelGGL((k_linres_fdP<16>), grid, dim3(64 * (kFdTile / 16)), 0, ctx->stream, ea, eb, 0,
                                   (const double*)o->at, (const double*)o->p1, x, h, o->m, o->n, tl, (const double*)F0,
-                                  Cc, JT, (long)ldjt, mS, sstride, mt0, nmt);
+                                  Cc, JT, (long)ldjt, mS, sstride, mt0, nmt, (const int*)gate.sel, gate.x1,
+                                  gate.F01, (const double*)C1);
         else
             hipExtLaunchKernelGGL((k_linres_fdP<kPW>), grid, dim3(64 * (kFdTile / kPW)), 0, ctx->stream, ea, eb, 0,
                                   (const double*)o->at, (const double*)o->p1, x, h, o->m, o->n, tl, (const double*)F0,
-                                  Cc, JT, (long)ldjt, mS, sstride, mt0, nmt);
+                                  Cc, JT, (long)ldjt, mS, sstride, mt0, nmt, (const int*)gate.sel, gate.x1,
+                                  gate.F01, (const double*)C1);
         PNOL_CHECK(launch_check());
         if (after_tile) PNOL_CHECK((*after_tile)(ord[t0]));
     }
@@ -1029,6 +1084,24 @@ int launch_fd_jacobian(pnol_ctx* ctx, pnol_dobj* o, const double* x, const doubl
         default:
             return PNOL_ERR_UNSUPPORTED;
     }
+}
+
+int lm_prequeue_fd(pnol_ctx* ctx, pnol_dobj* o, const double* x0, double* F00, const double* x1, double* F01,
+                   const double* h, double* JT, int ldjt, const int* hw, int seq, int* sel, int* res,
+                   unsigned long long cap) {
+    if (!o || o->kind != PNOL_OBJ_LINRES || !x0 || !F00 || !x1 || !F01 || !hw || !sel || !res) return PNOL_ERR_ARG;
+    ctx->fd_gate = {hw, seq, sel, res, x1, F01, cap};
+    const int st = launch_fd_jacobian(ctx, o, x0, h, 0, o->n, F00, 3, JT, ldjt);
+    ctx->fd_gate = {};
+    return st;
+}
+
+int lm_fd_commit(pnol_ctx* ctx, pnol_dobj* o, const double* x) {
+    const int have = ckpt_find(ctx, o, x, 0, o->m);
+    if (have < 0) return PNOL_ERR_ARG;
+    ctx->ckpt_last = have;
+    void *C = nullptr, *xc = nullptr;
+    return ckpt_buf(ctx, o, have, &C, &xc);
 }
 
 int launch_synthetic_quadratic(pnol_ctx* ctx, unsigned long long seed, int n, double bscale, double* d, double* b) {

@@ -902,7 +902,8 @@ int launch_fd_jtj(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h,
 // launch_fd_jtj (+ rhs) and launch_chol_solve; for the LU fallback launch_jtj_from_partials forms
 // A from the trip's partials.
 int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
-                           double* JT, int ldjt, double lambda, double* rhs, double* sigma, int* dinfo, double* xnext) {
+                           double* JT, int ldjt, double lambda, double* rhs, double* sigma, int* dinfo, double* xnext,
+                           bool fd_queued) {
     if (!o || !x || !h || !F0 || !JT || !rhs || !sigma || !dinfo || !xnext || ldjt < o->m) return PNOL_ERR_ARG;
     const int n = o->n, m = o->m;
     if (n <= PNOL_SEQ_MAX) return PNOL_ERR_ARG;
@@ -928,7 +929,8 @@ int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const d
     if (tail) PNOL_CHECK(ws_get(ctx, "syrk_tcnt", sizeof(int) * (size_t)ntiles, &tcnt));
     CholRed cr;
     PNOL_CHECK(launch_chol_reducing_prep(ctx, n, dinfo, cr));
-    PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
+    if (fd_queued) PNOL_CHECK(lm_fd_commit(ctx, o, x));   // the Jacobian at x is queued already
+    else PNOL_CHECK(launch_fd_jacobian(ctx, o, x, h, 0, n, F0, compute_f0, JT, ldjt));
     PNOL_CHECK(jtr_gemv(ctx, JT, ldjt, sc.mS, m, n, sc.mS, 0, kS, F0));
     // the prep launch (words, paddings, info; the tile counters)
     PNOL_CHECK(launch_chol_reducing_start(ctx, cr, !tasks, (int*)tcnt, ntiles));

@@ -77,6 +77,21 @@ struct pnol_ctx {
         const int* info_d = nullptr;
         int* info_h = nullptr;
     } trip_mirror;
+    // The LM loop's next Jacobian queued behind a gate before the host decides the step (set by
+    // lm_prequeue_fd around its launch, null otherwise): k_trip_gate polls the host word hw
+    // ({seq, choice}) and passes the choice on in sel (device); the FD launch then takes x0 / F0 /
+    // its checkpoints (choice 0: the step rejected), x1 / F01 / the checkpoints of x1 (choice 1:
+    // accepted), or returns at once (choice < 0: no further trip).  res: the choice the gate
+    // passed on and its seq, for the host's check (pinned).
+    struct FdGate {
+        const int* hw = nullptr;
+        int seq = 0;
+        int* sel = nullptr;
+        int* res = nullptr;
+        const double* x1 = nullptr;
+        const double* F01 = nullptr;
+        unsigned long long cap = 0;   // ticks of the 100 MHz clock the gate waits at most
+    } fd_gate;
     int chol4_epoch = 0;            // last flag value handed out (monotonic; flags reset on regrow)
     hipStream_t aux_stream = nullptr;   // second stream (J^T J rows beside the FD chunks), lazily created
     std::vector<hipEvent_t> aux_events; // chunk-done events between the two streams
@@ -240,8 +255,20 @@ int launch_jtj(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double l
 // One LM trip's linear algebra without forming A (syrk.hip): FD Jacobian, J^T J split-K
 // partials, -J^T F slice partials, then launch_chol_reducing; A only on request from the
 // partials of the last trip (the LU fallback)
+// fd_queued: the Jacobian at x is already queued (lm_prequeue_fd, released with the decision)
 int launch_fd_normal_solve(pnol_ctx* ctx, pnol_dobj* o, const double* x, const double* h, double* F0, int compute_f0,
-                           double* JT, int ldjt, double lambda, double* rhs, double* sigma, int* dinfo, double* xnext);
+                           double* JT, int ldjt, double lambda, double* rhs, double* sigma, int* dinfo, double* xnext,
+                           bool fd_queued = false);
+// The one-GPU LM loop's next FD Jacobian (fd.hip), queued before the host has decided the step:
+// k_trip_gate then the FD launch, at x0 (F00 = F(x0)) or x1 (F01) as the host's word hw picks
+// ({seq, choice}: 0 -> x0, 1 -> x1, < 0 -> no launch work).  Both points' prefix checkpoints must
+// be in the context's slots (PNOL_ERR_UNSUPPORTED otherwise: nothing queued).  sel: a device int;
+// res: pinned {choice passed on, seq}.  lm_fd_commit: the checkpoint bookkeeping of the chosen
+// point, as its own FD launch would have left it.
+int lm_prequeue_fd(pnol_ctx* ctx, pnol_dobj* o, const double* x0, double* F00, const double* x1, double* F01,
+                   const double* h, double* JT, int ldjt, const int* hw, int seq, int* sel, int* res,
+                   unsigned long long cap);
+int lm_fd_commit(pnol_ctx* ctx, pnol_dobj* o, const double* x);
 int launch_jtj_from_partials(pnol_ctx* ctx, int m, int n, double lambda, double* A, int lda);
 int launch_jtj_sharded(pnol_ctx* ctx, const double* JT, int ldjt, int m, int n, double lambda, double* A, int lda,
                        double* jtj_diag);

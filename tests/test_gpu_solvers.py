@@ -578,7 +578,8 @@ def test_lm_fused_trip_loop_equals_general_loop(ctx, oracle, m, n, force, reduce
     bitwise -- X, F0, FOpt, evaluation count -- also with the LU fallback forced on every trip
     (force = 1: A formed from the trip's partials, pnol_lm_trip_normal_d); the fused trip's results
     reach the host alike written into the pinned block by its kernels (the default) or copied
-    (PNOL_LM_ZEROCOPY=0)."""
+    (PNOL_LM_ZEROCOPY=0), and with each next Jacobian queued behind a gate before the host's
+    decision (the default) or after it (PNOL_LM_GATE=0)."""
     from parallelnonlinearoptimizationlibrary_amd import _lib as L
     from parallelnonlinearoptimizationlibrary_amd.device import run_levmarq
     A, xs, y = oracle.linres_data(m, n)
@@ -586,18 +587,44 @@ def test_lm_fused_trip_loop_equals_general_loop(ctx, oracle, m, n, force, reduce
     monkeypatch.setenv("PNOL_CHOL_FORCE_FALLBACK", force)
     monkeypatch.setenv("PNOL_LM_REDUCE", reduce)
     out = {}
-    for name, mode, trip, zc in (("fused", "1", "1", "1"), ("fused_copy", "1", "1", "0"), ("two_call", "1", "0", "1"),
-                                 ("general", "0", "0", "1")):
+    for name, mode, trip, zc, gate in (("fused", "1", "1", "1", "1"), ("fused_nogate", "1", "1", "1", "0"),
+                                       ("fused_copy", "1", "1", "0", "1"), ("two_call", "1", "0", "1", "1"),
+                                       ("general", "0", "0", "1", "1")):
         monkeypatch.setenv("PNOL_LM_ASYNC", mode)
         monkeypatch.setenv("PNOL_LM_TRIP", trip)
         monkeypatch.setenv("PNOL_LM_ZEROCOPY", zc)
+        monkeypatch.setenv("PNOL_LM_GATE", gate)
         out[name] = run_levmarq(_obj(ctx, L.OBJ_LINRES, n, m, A, y), np.zeros(n), params)
-    for a, b in (("fused", "fused_copy"), ("fused", "two_call"), ("two_call", "general")):
+    for a, b in (("fused", "fused_nogate"), ("fused", "fused_copy"), ("fused", "two_call"), ("two_call", "general")):
         (Xa, F0a, FOa, ra), (Xs, F0s, FOs, rs) = out[a], out[b]
         assert np.array_equal(Xa, Xs), (a, b, rel(Xa, Xs))
         assert np.array_equal(F0a, F0s) and np.array_equal(FOa, FOs), (a, b)
         assert ra.evals == rs.evals, (a, b)
     assert rel(out["fused"][0], xs) <= 1e-8
+
+
+def test_lm_gate_timeout_repeats_the_trip(ctx, oracle, monkeypatch, capfd):
+    """A queued Jacobian's gate that gives up before the host decides (PNOL_LM_GATE_CAP=0: at
+    once) makes that Jacobian launch return; the host sees it in the gate's report and runs the
+    trip again whole -- the same X, F and evaluation count as without the gate."""
+    from parallelnonlinearoptimizationlibrary_amd import _lib as L
+    from parallelnonlinearoptimizationlibrary_amd.device import run_levmarq
+    m, n = 3000, 257
+    A, xs, y = oracle.linres_data(m, n)
+    params = (0.001, 10, 1e-7, 6, 0.0, -1)
+    out = {}
+    for name, gate, cap in (("nogate", "0", None), ("gave_up", "1", "0")):
+        monkeypatch.setenv("PNOL_LM_GATE", gate)
+        if cap is None:
+            monkeypatch.delenv("PNOL_LM_GATE_CAP", raising=False)
+        else:
+            monkeypatch.setenv("PNOL_LM_GATE_CAP", cap)
+        out[name] = run_levmarq(_obj(ctx, L.OBJ_LINRES, n, m, A, y), np.zeros(n), params)
+    err = capfd.readouterr().err
+    assert "gate timed out" in err
+    (Xa, F0a, FOa, ra), (Xb, F0b, FOb, rb) = out["nogate"], out["gave_up"]
+    assert np.array_equal(Xa, Xb) and np.array_equal(F0a, F0b) and np.array_equal(FOa, FOb)
+    assert ra.evals == rb.evals
 
 
 @pytest.mark.parametrize("m,n,trip", [(3000, 257, "1"), (2000, 700, "1"), (2000, 700, "0")])
