@@ -176,7 +176,9 @@ class LMDevice {
 // non-positive Cholesky pivot is redone with the reference-order LU, as pnol_solve_d does; a
 // Cholesky wait that ran past its cap is redone with the same Cholesky (never the LU).
 // (Queueing trip i+1 before deciding step i was measured: a rejected step then costs a whole
-// wasted trip, and the post-convergence steps of the bench are mostly rejections.)
+// wasted trip, and the post-convergence steps of the bench are mostly rejections.  What is queued
+// early instead is trip i+1's FD Jacobian alone, behind a gate kernel that the decision opens at
+// the point it picks -- prequeue / release, PNOL_LM_GATE.)
 //
 // LevMarqMPI (sliced = true) runs the same loop with the Jacobian split over the ranks
 // (pnol_lm_jacobian_mpi_d): each rank evaluates its FD column tiles for all rows, every m-slice
